@@ -1,0 +1,358 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures from the REFERENCE code (build container only).
+
+Runs the reference's own Python (imported read-only from /root/reference via
+sys.path, PYTHONDONTWRITEBYTECODE=1) and writes small .npz fixtures into
+tests/golden/.  Nothing here ships: the GPU box never sees /root/reference; the
+tests only read the committed .npz files.
+
+Reference pieces executed:
+  * kymatio Scattering1D (ref/kymatio/kymatio/scattering1d/*)
+  * KymatioPhaseScattering1D (ref/hdf5_dataset/kymatio_phase_scattering.py)
+  * SeqVaeTeb + block classes (ref/model/vae_teb_model.py)
+  * normalize_tensor_data (ref/hdf5_dataset/hdf5_dataset.py:18-137) and the
+    stats formula (ref/hdf5_dataset/calculate_dataset_stats.py:134-273): their
+    modules import h5py (absent here), so the function *definitions* are
+    extracted with `ast` from the reference file and executed unchanged.
+The kymatio known-answer file test_data_1d.npz is copied verbatim (data).
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only NAME]
+"""
+import argparse
+import ast
+import os
+import shutil
+import sys
+import time
+import types
+import typing
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, os.path.join(REF, "kymatio"))
+sys.path.insert(0, os.path.join(REF, "hdf5_dataset"))
+sys.path.insert(0, os.path.join(REF, "model"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
+
+from golden_util import det_fill_  # noqa: E402
+from vaeteb import synthetic  # noqa: E402  (data generator only)
+
+torch.set_num_threads(8)
+
+
+def save(name, **arrs):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
+    print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+def extract_functions(path, names, extra_globals):
+    """Execute selected top-level function / method definitions of a
+    reference file without importing the module (its imports need h5py)."""
+    src = open(path).read()
+    tree = ast.parse(src)
+    g = dict(extra_globals)
+    found = {}
+    for node in ast.walk(tree):
+        if isinstance(node, ast.FunctionDef) and node.name in names and node.name not in found:
+            mod = ast.Module(body=[node], type_ignores=[])
+            exec(compile(mod, path, "exec"), g)
+            found[node.name] = g[node.name]
+    missing = set(names) - set(found)
+    if missing:
+        raise RuntimeError(f"not found in {path}: {missing}")
+    return found
+
+
+# ---------------------------------------------------------------------------
+def gen_kymatio_kat():
+    src = os.path.join(REF, "kymatio/tests/scattering1d/test_data_1d.npz")
+    shutil.copyfile(src, os.path.join(OUT, "kymatio_test_data_1d.npz"))
+    print("copied kymatio_test_data_1d.npz")
+
+
+def gen_filters():
+    from kymatio.scattering1d.filter_bank import scattering_filter_factory
+    from kymatio_phase_scattering import KymatioPhaseScattering1D
+    for (J, Q, T, N, order) in [(11, 4, 16, 4096, 1), (6, 1, 16, 4096, 1), (8, 12, 256, 16384, 2)]:
+        m = KymatioPhaseScattering1D(J=J, Q=Q, T=T, shape=N, device=torch.device("cpu"), max_order=order)
+        phi_f, psi1_f, psi2_f, tmax = scattering_filter_factory(m.J_pad, J, Q, T)
+        sel = m.get_optimal_coefficients_for_fhr(J, Q, T)
+        d = dict(J=J, Q=Q, T=T, N=N, J_pad=m.J_pad, pad_left=m.pad_left, pad_right=m.pad_right,
+                 t_max_phi=tmax,
+                 ind_start=np.array([m.ind_start[k] for k in range(J + 1)]),
+                 ind_end=np.array([m.ind_end[k] for k in range(J + 1)]),
+                 xi1=np.array([p["xi"] for p in psi1_f]), sigma1=np.array([p["sigma"] for p in psi1_f]),
+                 j1=np.array([p["j"] for p in psi1_f]),
+                 xi2=np.array([p["xi"] for p in psi2_f]), sigma2=np.array([p["sigma"] for p in psi2_f]),
+                 j2=np.array([p["j"] for p in psi2_f]),
+                 n_psi2_levels=np.array([len(p["levels"]) for p in psi2_f]),
+                 n_phi_levels=len(phi_f["levels"]), sigma_low=phi_f["sigma"],
+                 i_idx=m.i_idx.numpy(), j_idx=m.j_idx.numpy(), powers=m.powers.numpy(),
+                 autoc_idx=m.autoc_idx.numpy(),
+                 phase_mask=sel["recommendations"]["use_phase_mask"].numpy(),
+                 cross_mask=sel["recommendations"]["use_cross_mask"].numpy(),
+                 center_freqs=m.center_freqs.numpy())
+        # tables: full precision for the small configs, checksums for c5
+        psi1 = np.stack([p["levels"][0] for p in psi1_f])
+        d["psi1_sum"] = psi1.sum(1)
+        d["psi1_l2"] = np.sqrt((psi1 ** 2).sum(1))
+        d["phi_levels_sum"] = np.array([lv.sum() for lv in phi_f["levels"]])
+        d["phi0"] = phi_f["levels"][0]
+        if N <= 4096:
+            d["psi1"] = psi1
+        else:
+            d["psi1_rows"] = psi1[[0, len(psi1) // 2, len(psi1) - 1]]
+            d["psi2_l2"] = np.array([np.sqrt((p["levels"][0] ** 2).sum()) for p in psi2_f])
+        save(f"filters_j{J}q{Q}t{T}_n{N}.npz", **d)
+
+
+def gen_scattering():
+    from kymatio.torch import Scattering1D
+    cases = [(6, 1, 16, 4096, 1, 2), (6, 1, 16, 4096, 2, 2), (11, 4, 16, 4096, 1, 2),
+             (8, 12, 256, 16384, 2, 1)]
+    for (J, Q, T, N, order, B) in cases:
+        x = np.ascontiguousarray(synthetic.batch(1000, B, N)[:, 0, :])
+        sc = Scattering1D(J=J, shape=N, Q=Q, max_order=order, T=T)
+        t = time.time()
+        S, _ = sc(torch.from_numpy(x))
+        print(f"scattering J{J} Q{Q} T{T} N{N} o{order}: {tuple(S.shape)} {time.time() - t:.2f}s")
+        sc64 = Scattering1D(J=J, shape=N, Q=Q, max_order=order, T=T).double()
+        S64, _ = sc64(torch.from_numpy(x).double())
+        save(f"scattering_j{J}q{Q}t{T}_n{N}_o{order}.npz", x=x, S=S.numpy(), S64=S64.numpy(),
+             pad_left=sc.pad_left, pad_right=sc.pad_right, J_pad=sc.J_pad)
+
+
+def _frontend_double(m):
+    m.double()
+    m.psi1_filters = m.psi1_filters.to(torch.complex128)
+    m.phi_filter = m.phi_filter.to(torch.complex128)
+    return m
+
+
+def gen_frontend():
+    from kymatio_phase_scattering import KymatioPhaseScattering1D
+    for (J, Q, T, N, B) in [(11, 4, 16, 4096, 2), (6, 1, 16, 4096, 2)]:
+        x = synthetic.batch(2000, B, N)
+        outs = {}
+        for tag, prec in (("", torch.float32), ("64", torch.float64)):
+            m = KymatioPhaseScattering1D(J=J, Q=Q, T=T, shape=N, device=torch.device("cpu"), max_order=1)
+            sel = m.get_optimal_coefficients_for_fhr(J, Q, T)
+            pm = sel["recommendations"]["use_phase_mask"]
+            cm = sel["recommendations"]["use_cross_mask"]
+            if prec == torch.float64:
+                _frontend_double(m)
+            xt = torch.from_numpy(x).to(prec)
+            t = time.time()
+            # invocation contract: ref/hdf5_dataset/create_hdf5_dataset.py:418-441
+            rp = m(x=xt, compute_phase=True, compute_cross_phase=False, scattering_channel=0, phase_channels=[0])
+            rc = m(x=xt, compute_phase=False, compute_cross_phase=True, scattering_channel=0, phase_channels=[0, 1])
+            print(f"frontend J{J} {tag or '32'}: {time.time() - t:.2f}s")
+            outs["fhr_st" + tag] = rp["scattering"].numpy()
+            if prec == torch.float32:
+                outs["phase_full"] = rp["phase_corr"].numpy()
+            outs["fhr_ph" + tag] = rp["phase_corr"][:, pm, :].numpy()
+            outs["fhr_up_ph" + tag] = rc["cross_phase_corr"][:, cm, :].numpy()
+            # analytic signals of a few filters (stage pin, a5)
+            if prec == torch.float32:
+                a = m._apply_filters(xt[:, [0, 1], :])
+                outs["analytic_ch0_f0"] = a[:, 0, 0].numpy()
+                outs["analytic_ch1_flast"] = a[:, 1, -1].numpy()
+                outs["analytic_ch0_fmid"] = a[:, 0, a.shape[2] // 2].numpy()
+        save(f"frontend_j{J}q{Q}t{T}_n{N}.npz", x=x, phase_mask=pm.numpy(), cross_mask=cm.numpy(), **outs)
+
+
+def gen_stats_and_norm():
+    """Frozen normalisation statistics for the synthetic windows (computed
+    with the reference front-end + the reference stats formula), and a
+    normalisation known-answer case through the reference function."""
+    from kymatio_phase_scattering import KymatioPhaseScattering1D
+    norm = extract_functions(os.path.join(REF, "hdf5_dataset/hdf5_dataset.py"), ["normalize_tensor_data"],
+                             {"torch": torch, "np": np, **vars(typing)})
+    statf = extract_functions(os.path.join(REF, "hdf5_dataset/calculate_dataset_stats.py"),
+                              ["_update_single_channel_stats", "_update_multi_channel_stats", "_finalize_stats"],
+                              {"torch": torch, "np": np, "warnings": __import__("warnings"), **vars(typing)})
+    for (J, Q, T, N, nwin) in [(11, 4, 16, 4096, 96), (6, 1, 16, 4096, 96)]:
+        m = KymatioPhaseScattering1D(J=J, Q=Q, T=T, shape=N, device=torch.device("cpu"), max_order=1)
+        sel = m.get_optimal_coefficients_for_fhr(J, Q, T)
+        pm = sel["recommendations"]["use_phase_mask"]
+        cm = sel["recommendations"]["use_cross_mask"]
+        fields = {"fhr": [], "up": [], "fhr_st": [], "fhr_ph": [], "fhr_up_ph": []}
+        t = time.time()
+        for s in range(0, nwin, 16):
+            x = torch.from_numpy(synthetic.batch(s, 16, N))
+            rp = m(x=x, compute_phase=True, compute_cross_phase=False, scattering_channel=0, phase_channels=[0])
+            rc = m(x=x, compute_phase=False, compute_cross_phase=True, scattering_channel=0, phase_channels=[0, 1])
+            fields["fhr"].append(x[:, 0].numpy()); fields["up"].append(x[:, 1].numpy())
+            fields["fhr_st"].append(rp["scattering"].numpy())
+            fields["fhr_ph"].append(rp["phase_corr"][:, pm].numpy())
+            fields["fhr_up_ph"].append(rc["cross_phase_corr"][:, cm].numpy())
+        print(f"stats front-end J{J}: {time.time() - t:.1f}s")
+        data = {k: np.concatenate(v) for k, v in fields.items()}
+        self_ = types.SimpleNamespace(device="cpu")
+        stats = {}
+        for k, v in data.items():
+            if k in ("fhr", "up"):
+                st = {"count": 0, "sum": torch.tensor(0.0, dtype=torch.float64),
+                      "sum_squares": torch.tensor(0.0, dtype=torch.float64)}
+                statf["_update_single_channel_stats"](self_, st, v)
+            else:
+                C = v.shape[1]
+                logc = [c for c in range(C) if c != 0] if k == "fhr_st" else []
+                asc = list(range(C)) if k != "fhr_st" else []
+                st = {"n_channels": C, "regular_channels": [c for c in range(C) if c not in logc and c not in asc],
+                      "log_channels": logc, "asinh_channels": asc, "log_epsilon": 1e-6,
+                      "sum": torch.zeros(C, dtype=torch.float64), "sum_squares": torch.zeros(C, dtype=torch.float64)}
+                statf["_update_multi_channel_stats"](self_, st, v)
+            stats[k] = st
+        statf["_finalize_stats"](self_, stats)
+        flat = {}
+        for k, st in stats.items():
+            flat[f"{k}_mean"] = np.asarray(st["mean"], np.float64)
+            flat[f"{k}_variance"] = np.asarray(st["variance"], np.float64)
+        # product data: the frozen stats file (like the reference's stats.hdf5)
+        pkg_data = os.path.join(ROOT, "vae-teb_amd", "vaeteb", "data")
+        os.makedirs(pkg_data, exist_ok=True)
+        np.savez(os.path.join(pkg_data, f"stats_j{J}q{Q}t{T}_n{N}.npz"), n_windows=nwin, **flat)
+        # known-answer normalisation on the first 4 windows through the reference function
+        nstats = {k: {"mean": (float(st["mean"]) if k in ("fhr", "up") else st["mean"]),
+                      "variance": (float(st["variance"]) if k in ("fhr", "up") else st["variance"])}
+                  for k, st in stats.items()}
+        kat = {}
+        for k in data:
+            inp = torch.from_numpy(data[k][:4].copy())
+            out = norm["normalize_tensor_data"](inp, k, nstats, {"fhr_st": "all_except_0"},
+                                                {"fhr_ph": "all", "fhr_up_ph": "all"}, 1e-6)
+            kat[f"in_{k}"] = data[k][:4]
+            kat[f"out_{k}"] = out.numpy()
+        save(f"normalize_j{J}q{Q}t{T}_n{N}.npz", **kat, **flat)
+
+
+# ---------------------------------------------------------------------------
+def build_ref_model(S):
+    import torch.nn as nn
+    import vae_teb_model as V
+    model = V.SeqVaeTeb(input_channels=76, sequence_length=S, decimation_factor=16, warmup_period=30)
+    if S != 300:
+        R = 16 * S
+        model.decoder.output_mu = V.ResidualMLP(R, (R, R), final_activation=False,
+                                                use_skip_connection=False, activation=nn.ReLU)
+        model.decoder.output_logvar = V.ResidualMLP(R, (R, R), final_activation=False,
+                                                    use_skip_connection=False, activation=nn.ReLU)
+    det_fill_(model)
+    return model
+
+
+def run_ref_step(model, y_st, y_ph, x_ph, y_raw, eps, beta, lr=1e-3, clip=1.0):
+    model.train()
+    model.reparameterize = lambda mu, lv: mu + torch.from_numpy(eps) * torch.exp(0.5 * lv)
+    fw = model(torch.from_numpy(y_st), torch.from_numpy(y_ph), torch.from_numpy(x_ph))
+    losses = model.compute_loss(fw, torch.from_numpy(y_st), torch.from_numpy(y_ph), torch.from_numpy(y_raw),
+                                compute_kld_loss=True, beta=beta)
+    losses["total_loss"].backward()
+    grads = {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+    gnorm = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=clip)
+    # AdamW as configured in ref/model/graph_model.py:654-660
+    opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=1e-4, eps=1e-8, betas=(0.9, 0.98))
+    opt.step()
+    return fw, losses, grads, gnorm
+
+
+def gen_model():
+    for (S, B, full) in [(16, 4, True), (4, 3, True), (256, 2, False)]:
+        rng = np.random.Generator(np.random.PCG64(7 + S))
+        y_st = rng.standard_normal((B, S, 43)).astype(np.float32)
+        y_ph = rng.standard_normal((B, S, 44)).astype(np.float32)
+        x_ph = rng.standard_normal((B, S, 130)).astype(np.float32)
+        y_raw = rng.standard_normal((B, 16 * S)).astype(np.float32)
+        eps = rng.standard_normal((B, S, 32)).astype(np.float32)
+        beta = 1e-5
+        model = build_ref_model(S)
+        t = time.time()
+        fw, losses, grads, gnorm = run_ref_step(model, y_st, y_ph, x_ph, y_raw, eps, beta)
+        print(f"model S={S} B={B}: {time.time() - t:.2f}s total={losses['total_loss'].item():.6f}")
+        d = dict(S=S, B=B, beta=beta, y_st=y_st, y_ph=y_ph, x_ph=x_ph, y_raw=y_raw, eps=eps,
+                 grad_norm_total=gnorm.item())
+        for k in ("mse_loss", "nll_loss", "kld_loss", "total_loss", "reconstruction_loss"):
+            d["loss_" + k] = losses[k].item()
+        for k, v in fw.items():
+            d["fw_" + k] = v.detach().numpy()
+        names = list(grads.keys())
+        d["param_names"] = np.array(names)
+        d["grad_l2"] = np.array([grads[k].norm().item() for k in names])
+        d["grad_sum"] = np.array([grads[k].sum().item() for k in names])
+        sd = model.state_dict()
+        bn_keys = [k for k in sd if k.endswith("running_mean") or k.endswith("running_var")]
+        d["bn_names"] = np.array(bn_keys)
+        if full:
+            for i, k in enumerate(names):
+                d[f"grad_{i}"] = grads[k].numpy()
+                d[f"after_{i}"] = sd[k].numpy()
+            for i, k in enumerate(bn_keys):
+                d[f"bn_{i}"] = sd[k].numpy()
+        else:
+            d["after_l2"] = np.array([sd[k].norm().item() for k in names])
+            d["bn_sum"] = np.array([sd[k].sum().item() for k in bn_keys])
+            d["fw_mu_pr"] = fw["mu_pr"].detach().numpy()
+            for k in list(d):
+                if k.startswith("fw_") and k not in ("fw_mu_pr", "fw_logvar_pr"):
+                    d[k] = np.asarray(d[k])[:, :8]  # keep fixtures small
+        save(f"model_s{S}_b{B}.npz", **d)
+
+
+def gen_tiny():
+    """Config 1: TinyVaeTeb built only from reference blocks."""
+    import torch.nn as nn
+    import vae_teb_model as V
+
+    class TinyRef(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.enc = nn.Sequential(V.CausalMultiChannelConvBlock(1, 16, filter_size=3),
+                                     V.CausalMultiChannelConvBlock(16, 16, filter_size=5))
+            self.mu = V.ResidualMLP(16, (8,), final_activation=False)
+            self.logvar = V.ResidualMLP(16, (8,), final_activation=False)
+            self.dec = nn.Sequential(V.MultiChannelConvBlock(8, 16, filter_size=3),
+                                     V.MultiChannelConvBlock(16, 2, filter_size=3, tanh=True))
+
+    x = synthetic.tiny_batch(8, 256, seed=0)
+    rng = np.random.Generator(np.random.PCG64(11))
+    eps = rng.standard_normal((8, 256, 8)).astype(np.float32)
+    m = TinyRef()
+    det_fill_(m)
+    m.train()
+    xt = torch.from_numpy(x)
+    h = m.enc(xt).transpose(1, 2)
+    mu, lv = m.mu(h), m.logvar(h)
+    z = mu + torch.from_numpy(eps) * torch.exp(0.5 * lv)
+    out = m.dec(z.transpose(1, 2))
+    mu_r, lv_r = out[:, 0], out[:, 1]
+    zero = torch.zeros_like(mu)
+    kld = V.SeqVaeTeb._kld_loss(None, zero, zero, mu, lv)
+    nll = V.Decoder.compute_loss(torch.zeros(1), mu_r, lv_r, torch.zeros(1), torch.zeros(1), xt[:, 0])["nll_loss"]
+    total = nll + kld
+    total.backward()
+    d = dict(x=x, eps=eps, mu=mu.detach().numpy(), logvar=lv.detach().numpy(), mu_r=mu_r.detach().numpy(),
+             lv_r=lv_r.detach().numpy(), kld=kld.item(), nll=nll.item(), total=total.item())
+    names = [k for k, _ in m.named_parameters()]
+    d["param_names"] = np.array(names)
+    for i, (k, p) in enumerate(m.named_parameters()):
+        d[f"grad_{i}"] = p.grad.numpy()
+    save("tiny_c1.npz", **d)
+
+
+GENS = dict(kat=gen_kymatio_kat, filters=gen_filters, scattering=gen_scattering, frontend=gen_frontend,
+            stats=gen_stats_and_norm, model=gen_model, tiny=gen_tiny)
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=list(GENS))
+    a = ap.parse_args()
+    os.makedirs(OUT, exist_ok=True)
+    for name in a.only:
+        GENS[name]()
