@@ -1,0 +1,143 @@
+/*
+ * vaeteb.h — C ABI of the MI355X (gfx950) VAE-TEB training-step library
+ * (libvaeteb.so, built from vae-teb_amd/csrc/).
+ *
+ * Conventions
+ *  - Plain C: pointers, int / int64_t sizes, `void* stream` (a hipStream_t;
+ *    NULL = default stream).  No torch or C++ types cross the boundary.
+ *  - The caller owns every buffer (device memory) and every table; nothing
+ *    here allocates or frees caller memory.  Workspaces are passed in.
+ *  - Complex data is interleaved float2 {re, im} — the layout of a torch
+ *    complex64 tensor and of kymatio's "trailing dim 2" convention
+ *    (ref/kymatio/kymatio/backend/torch_backend.py:129-135).
+ *  - Every call is stream-ordered, asynchronous, re-entrant and host-sync free
+ *    (capturable in a hipGraph).  Return 0 (VT_OK) or a negative code; the
+ *    message of the last failure on the calling thread is vt_last_error().
+ *
+ * Each entry point names the reference interface it replaces (file:line,
+ * paths relative to the reference repository root).
+ */
+#ifndef VAETEB_H
+#define VAETEB_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VT_OK 0
+#define VT_ERR_ARG (-1)    /* bad argument / shape  -> Python ValueError     */
+#define VT_ERR_LAYOUT (-2) /* non-contiguous input  -> RuntimeError        */
+#define VT_ERR_HIP (-3)    /* HIP runtime error     -> RuntimeError        */
+
+#define VT_FFT_MAX_LDS 8192 /* longest FFT held in one workgroup's LDS     */
+
+const char* vt_last_error(void);
+int vt_abi_version(void);
+
+/* ------------------------------------------------------------------ front-end
+ * Twiddle tables `tw`: float2[n], tw[k] = exp(-2*pi*i*k/n) computed in fp64 on
+ * the host; an FFT of length n/stride reads it with that stride.            */
+
+/* Reflect-pad (to n_pad, pad_left on the left) + forward FFT of each row.
+ * replaces: kymatio pad+rfft  ref/kymatio/kymatio/scattering1d/core/scattering1d.py:288-290,
+ *           _pad_signal + fft ref/hdf5_dataset/kymatio_phase_scattering.py:222-223   */
+int vt_fe_spectrum(const float* x, int64_t rows, int N, int n_pad, int pad_left, const void* tw, void* xhat,
+                   void* stream);
+
+/* S0: phi-lowpass + 2^log2T decimation of the padded signal, as a short
+ * correlation with h0 = ifft(phi_0) (even, radius taps each side).
+ * out[row*out_row_stride + m] = sum_d x_pad[step*(m+start)-d] * h0[|d|], m < S.
+ * replaces: scattering1d.py:295-303 (S_0 = unpad(irfft(subsample(U_0_hat*phi))))      */
+int vt_fe_lowpass(const float* x, int64_t rows, int64_t x_row_stride, int N, int n_pad, int pad_left,
+                  const float* h0, int radius, int step, int start, int S, float* out, int64_t out_row_stride,
+                  void* stream);
+
+/* One workgroup per (sample b, item): xhat[b,chan] * psi[filter] -> inverse FFT
+ * in LDS -> analytic[b, slot, 0:N] = result[pad_left:pad_left+N] (if slot>=0)
+ * and s1[b, s1_channel, :] = lowpass(|result[::2^k1]|) (if s1_channel>=0).
+ * items: int[n_items][5] = {chan, filter, slot, s1_channel, k1}.
+ * replaces: first-order loop scattering1d.py:306-333 and
+ *           _apply_filters kymatio_phase_scattering.py:220-231                           */
+int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* psi, int n_items, const int* items,
+                  const void* tw, int N, int pad_left, void* analytic, int n_slots, const float* h0, int radius,
+                  int step, int start, int S, float* s1, int s1_channels, void* stream);
+
+/* One workgroup per (sample b, pair p): c = |a_i| e^{i power*arg(a_i)} conj(a_j),
+ * reflect-pad to n_pad, FFT, multiply bins [0, n_pad/dec) by phi0 (real),
+ * inverse FFT of length n_pad/dec, out[b,p,m] = Re(.)[start+m], m < S.
+ * replaces: _compute_phase_correlation        kymatio_phase_scattering.py:275-301,
+ *           _compute_cross_channel_phase_correlation :303-360, _apply_phi_filter :233-273 */
+int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
+                const int* slot_i, const int* slot_j, const float* power, const void* tw, const float* phi0, int dec,
+                int start, int S, float* out, void* stream);
+
+/* Per-channel transform (kind 0 none, 1 log(max(x,0)+log_eps), 2 asinh) and
+ * z-score (x-mean)/(std+1e-8); in[b, c, s] (batch stride in_C*S) -> out[b, s, out_off + c]
+ * (row width out_C).
+ * replaces: normalize_tensor_data ref/hdf5_dataset/hdf5_dataset.py:18-137 + the
+ *           (C,S)->(S,C) transpose :758-759                                              */
+int vt_fe_normalize(const float* in, int64_t B, int C, int in_C, int S, const int* kind, const float* mean, const float* stdv,
+                    float log_eps, float* out, int out_C, int out_off, void* stream);
+/* fhr / up: (x-mean)/(std+1e-8)  (hdf5_dataset.py:78-80)                                */
+int vt_normalize_raw(const float* x, int64_t rows, int64_t row_stride, int N, float mean, float stdv, float* out,
+                     void* stream);
+
+/* kymatio backend-plugin primitives (TorchBackend1D, ref/kymatio/kymatio/scattering1d/
+ * backend/torch_backend.py:17-174 and ref/kymatio/kymatio/backend/torch_backend.py:99-219) */
+int vt_fft(const void* in, void* out, int64_t rows, int n, int inverse, const void* tw, int tw_stride,
+           void* stream);                                                   /* fft / ifft (1/n)   */
+int vt_cdgmm(const void* A, const void* B, int b_is_real, void* C, int64_t rows, int n, void* stream);
+int vt_modulus(const void* in, float* out, int64_t count, void* stream);
+int vt_modulus_bwd(const void* in, const float* mod, const float* grad, void* grad_in, int64_t count, void* stream);
+int vt_subsample_fourier(const void* in, void* out, int64_t rows, int n, int k, void* stream);
+int vt_pad_reflect(const float* in, float* out, int64_t rows, int N, int pad_left, int pad_right, void* stream);
+
+
+/* ---------------------------------------------------------------------- ELBO
+ * Workspace `ws`: float[vt_elbo_workspace_floats()], device.  Scalars (kl,
+ * nll, mse, g_kl) are single device floats, so no host sync is needed.       */
+int vt_elbo_workspace_floats(void);
+
+/* mu_post = mu_c + mu_y; z = mu_post + eps*exp(0.5*lv_q);
+ * kl = mean_rows sum_D 0.5*(lv_p - lv_q - 1 + (exp(lv_q) + (mu_post-mu_y)^2)/exp(lv_p)).
+ * replaces: SeqVaeTeb.reparameterize ref/model/vae_teb_model.py:1046-1050,
+ *           _kld_loss :1052-1082 and the residual mu_post += mu_y :1115          */
+int vt_elbo_latent_fwd(const float* mu_c, const float* lv_q, const float* mu_y, const float* lv_p, const float* eps,
+                       int64_t rows, int D, float* z, float* mu_post, float* kl, float* ws, void* stream);
+/* Gradients of the above given dL/dz (nullable), dL/dmu_post (nullable) and the
+ * device scalar dL/dkl (nullable).                                               */
+int vt_elbo_latent_bwd(const float* mu_c, const float* lv_q, const float* mu_y, const float* lv_p, const float* eps,
+                       int64_t rows, int D, const float* g_z, const float* g_mu_post, const float* g_kl,
+                       float* g_mu_c, float* g_lv_q, float* g_mu_y, float* g_lv_p, void* stream);
+/* nll = mean 0.5*(lv + (y-mu)^2/exp(lv)) over n_nll; mse = mean (lin - [t_st|t_ph])^2
+ * over rows x (c_st+c_ph) (skipped when lin == NULL); writes the unit-upstream
+ * gradients g_mu, g_lv, g_lin.
+ * replaces: Decoder.compute_loss ref/model/vae_teb_model.py:932-979              */
+int vt_elbo_output_fwd(const float* mu, const float* lv, const float* y, int64_t n_nll, const float* lin,
+                       const float* t_st, const float* t_ph, int64_t rows, int c_st, int c_ph, float* g_mu,
+                       float* g_lv, float* g_lin, float* nll, float* mse, float* ws, void* stream);
+/* x *= s[0] (s a device scalar): applies an upstream loss gradient.             */
+int vt_scale_by_device_scalar(float* x, int64_t n, const float* s, void* stream);
+
+/* ----------------------------------------------------------------- optimiser
+ * Flat fp32 buffers: every parameter / gradient / moment is a view of one
+ * contiguous allocation.                                                        */
+int vt_grad_norm_workspace_floats(void);
+/* out2[0] = ||pre_scale*g||_2; out2[1] = pre_scale * min(max_norm/(out2[0]+1e-6), 1)
+ * (max_norm <= 0: no clipping).  replaces: clip_grad_norm_ ref/model/graph_model.py:724 */
+int vt_grad_norm_clip(const float* g, int64_t n, float pre_scale, float max_norm, float* out2, float* ws,
+                      void* stream);
+/* torch.optim.AdamW (decoupled decay) with g <- g*gscale[0] (nullable).
+ * replaces: torch.optim.AdamW configured at ref/model/graph_model.py:654-660,
+ *           ref/model/pytorch_lightning_modules.py:540-546                       */
+int vt_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                  float eps, float weight_decay, int step, const float* gscale, void* stream);
+/* bf16 (RNE) shadow copy of fp32 data, for MFMA operands.                         */
+int vt_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAETEB_H */

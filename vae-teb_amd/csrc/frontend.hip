@@ -1,0 +1,374 @@
+// Scattering1D + phase-harmonic front-end on gfx950.
+//
+// Data path for one training batch (x: B x 2 x N, ch0 = fhr, ch1 = up):
+//   vt_fe_spectrum  reflect-pad + forward FFT (n_pad) per (sample, channel)
+//                   -> xhat (B, 2, n_pad) complex64, L2/HBM resident
+//   vt_fe_lowpass   S0 = phi-lowpass of the padded signal, decimated by 2^log2T
+//   vt_fe_wavelet   one workgroup per (sample, wavelet item): xhat * psi_f ->
+//                   inverse FFT in LDS -> (a) the analytic signal slice the
+//                   phase path needs, (b) |U1| -> phi-lowpass -> S1 row
+//   vt_fe_pairs     one workgroup per (sample, selected pair): accelerated
+//                   product, reflect-pad, FFT, x phi, crop, 512-pt iFFT, real
+//   vt_fe_normalize log/asinh + per-channel z-score, (B,C,S) -> (B,S,C)
+// Reference: ref/kymatio/kymatio/scattering1d/core/scattering1d.py:197-399,
+// ref/hdf5_dataset/kymatio_phase_scattering.py:211-301 (+ :303-360 cross),
+// ref/hdf5_dataset/hdf5_dataset.py:18-137 (normalisation).
+//
+// Lowpass identity used for S0/S1 (exact up to an l1 tail < 1e-9 of the
+// Gaussian h0 = ifft(phi_0)): kymatio's
+//   unpad(irfft(periodize_K(fft_M(U) * phi_k)))  with phi_k = periodize_2^k(phi_0)
+// equals the circular correlation of U with h0 sampled on the 2^k grid,
+// evaluated every 2^log2T full-rate samples; h0 is even and decays like a
+// Gaussian (sigma ~ 25 samples at T = 16), so each output is a short dot
+// product read straight from the inverse-FFT result already in LDS.  The phase
+// path's crop-to-n_pad/dec low-pass is NOT Gaussian in time (one-sided
+// spectrum -> slowly decaying imaginary tail), so it stays in the FFT domain.
+#include <math.h>
+
+#include "common.h"
+#include "fft.h"
+
+namespace vt {
+
+static constexpr int FE_THREADS = 512;
+
+// ---------------------------------------------------------------- spectrum
+__global__ __launch_bounds__(FE_THREADS) void k_fe_spectrum(const float* __restrict__ x, int N, int n_pad,
+                                                            int pad_left, const float2* __restrict__ tw,
+                                                            float2* __restrict__ xhat) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2* X = sm;
+    float2* Y = sm + n_pad;
+    const int64_t row = blockIdx.x;
+    const float* xr = x + row * N;
+    for (int n = threadIdx.x; n < n_pad; n += blockDim.x) X[n] = make_float2(xr[reflect_idx(n - pad_left, N)], 0.f);
+    __syncthreads();
+    float2* R = fft_lds<false>(X, Y, n_pad, tw, 1);
+    float2* o = xhat + row * n_pad;
+    for (int n = threadIdx.x; n < n_pad; n += blockDim.x) o[n] = R[n];
+}
+
+// ---------------------------------------------------------------- S0 lowpass
+__global__ void k_fe_lowpass(const float* __restrict__ x, int64_t x_row_stride, int N, int n_pad, int pad_left,
+                             const float* __restrict__ h0, int radius, int step, int start, int S,
+                             float* __restrict__ out, int64_t out_row_stride) {
+    const int64_t row = blockIdx.y;
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= S) return;
+    const float* xr = x + row * x_row_stride;
+    const int c = step * (m + start);
+    float acc = 0.f;
+    for (int d = -radius; d <= radius; ++d) {
+        int n = c - d;
+        n %= n_pad;
+        if (n < 0) n += n_pad;
+        acc += xr[reflect_idx(n - pad_left, N)] * h0[d < 0 ? -d : d];
+    }
+    out[row * out_row_stride + m] = acc;
+}
+
+// ---------------------------------------------------------------- wavelets
+// items: n_items x 5 ints {chan, filter, analytic_slot|-1, s1_channel|-1, k1}
+__global__ __launch_bounds__(FE_THREADS) void k_fe_wavelet(
+    const float2* __restrict__ xhat, int C, int n_pad, const float* __restrict__ psi, int n_items,
+    const int* __restrict__ items, const float2* __restrict__ tw, int N, int pad_left, float2* __restrict__ analytic,
+    int n_slots, const float* __restrict__ h0, int radius, int step, int start, int S, float* __restrict__ s1,
+    int s1_channels) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2* X = sm;
+    float2* Y = sm + n_pad;
+    const int item = blockIdx.x;
+    const int64_t b = blockIdx.y;
+    const int chan = items[item * 5 + 0], filt = items[item * 5 + 1], slot = items[item * 5 + 2];
+    const int s1ch = items[item * 5 + 3], k1 = items[item * 5 + 4];
+    const float2* xh = xhat + (b * C + chan) * n_pad;
+    const float* ps = psi + (int64_t)filt * n_pad;
+    for (int n = threadIdx.x; n < n_pad; n += blockDim.x) X[n] = cscale(xh[n], ps[n]);
+    __syncthreads();
+    float2* R = fft_lds<true>(X, Y, n_pad, tw, 1);
+    const float inv_n = 1.0f / (float)n_pad;
+    if (slot >= 0) {
+        float2* a = analytic + (b * n_slots + slot) * (int64_t)N;
+        for (int i = threadIdx.x; i < N; i += blockDim.x) a[i] = cscale(R[pad_left + i], inv_n);
+    }
+    if (s1ch >= 0) {
+        float* U = reinterpret_cast<float*>(R == X ? Y : X);
+        const int M = n_pad >> k1;
+        for (int n = threadIdx.x; n < M; n += blockDim.x) {
+            const float2 v = cscale(R[n << k1], inv_n);
+            U[n] = sqrtf(v.x * v.x + v.y * v.y);
+        }
+        __syncthreads();
+        for (int m = threadIdx.x; m < S; m += blockDim.x) {
+            const int c = step * (m + start);
+            // n' such that |c - (n' << k1)| <= radius
+            const int lo = (c - radius + (1 << k1) - 1) >> k1;  // c - radius >= 0 assumed by host check
+            const int hi = (c + radius) >> k1;
+            float acc = 0.f;
+            for (int n = lo; n <= hi; ++n) {
+                int d = c - (n << k1);
+                d = d < 0 ? -d : d;
+                int nn = n % M;
+                if (nn < 0) nn += M;
+                acc += U[nn] * h0[d];
+            }
+            s1[(b * s1_channels + s1ch) * S + m] = acc;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- phase pairs
+__global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
+    const float2* __restrict__ analytic, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
+    const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
+    const float2* __restrict__ tw, const float* __restrict__ phi0, int dec, int start, int S,
+    float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2* X = sm;
+    float2* Y = sm + n_pad;
+    const int pair = blockIdx.x;
+    const int64_t b = blockIdx.y;
+    const float2* ai = analytic + (b * n_slots + slot_i[pair]) * (int64_t)N;
+    const float2* aj = analytic + (b * n_slots + slot_j[pair]) * (int64_t)N;
+    const float pw = power[pair];
+    // accelerated product (kymatio_phase_scattering.py:211-218, :282-283)
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const float2 u = ai[i], v = aj[i];
+        const float mag = sqrtf(u.x * u.x + u.y * u.y);
+        const float ph = atan2f(u.y, u.x) * pw;
+        float sn, cs;
+        sincosf(ph, &sn, &cs);
+        const float2 acc = make_float2(mag * cs, mag * sn);
+        Y[i] = cmul(acc, cconj(v));
+    }
+    __syncthreads();
+    for (int n = threadIdx.x; n < n_pad; n += blockDim.x) X[n] = Y[reflect_idx(n - pad_left, N)];
+    __syncthreads();
+    float2* R = fft_lds<false>(X, Y, n_pad, tw, 1);
+    float2* Z = (R == X) ? Y : X;
+    const int nb = n_pad / dec;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) Z[k] = cscale(R[k], phi0[k]);
+    __syncthreads();
+    float2* Rs = fft_lds<true>(Z, R, nb, tw, dec);
+    const float inv = 1.0f / (float)nb;
+    float* o = out + (b * n_pairs + pair) * (int64_t)S;
+    for (int m = threadIdx.x; m < S; m += blockDim.x) o[m] = Rs[start + m].x * inv;
+}
+
+// ---------------------------------------------------------------- normalise
+// in (B, C, S) raw -> out[b, s, off + c] with row width out_C.
+// kind: 0 = z-score only, 1 = log(max(x,0)+eps) then z, 2 = asinh then z.
+__global__ void k_fe_normalize(const float* __restrict__ in, int C, int in_C, int S, const int* __restrict__ kind,
+                               const float* __restrict__ mean, const float* __restrict__ stdv, float log_eps,
+                               float* __restrict__ out, int out_C, int out_off) {
+    const int64_t b = blockIdx.y;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= C * S) return;
+    const int c = idx % C, s = idx / C;  // consecutive threads -> consecutive output channels
+    float v = in[(b * in_C + c) * S + s];
+    const int k = kind[c];
+    if (k == 1) v = logf(fmaxf(v, 0.f) + log_eps);
+    else if (k == 2) v = asinhf(v);
+    out[(b * S + s) * out_C + out_off + c] = (v - mean[c]) / (stdv[c] + 1e-8f);
+}
+
+__global__ void k_normalize_raw(const float* __restrict__ x, int64_t row_stride, int N, float mean, float stdv,
+                                float* __restrict__ out) {
+    const int64_t r = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) out[r * N + i] = (x[r * row_stride + i] - mean) / (stdv + 1e-8f);
+}
+
+// ---------------------------------------------------------------- backend plugin ops
+__global__ __launch_bounds__(FE_THREADS) void k_fft_rows(const float2* __restrict__ in, float2* __restrict__ out,
+                                                         int n, const float2* __restrict__ tw, int tw_stride,
+                                                         int inverse) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2* X = sm;
+    float2* Y = sm + n;
+    const int64_t r = blockIdx.x;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) X[i] = in[r * n + i];
+    __syncthreads();
+    float2* R = inverse ? fft_lds<true>(X, Y, n, tw, tw_stride) : fft_lds<false>(X, Y, n, tw, tw_stride);
+    const float sc = inverse ? 1.0f / (float)n : 1.0f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) out[r * n + i] = cscale(R[i], sc);
+}
+
+__global__ void k_cdgmm(const float2* __restrict__ A, const float* __restrict__ Bf, int b_real,
+                        float2* __restrict__ C, int64_t total, int n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int k = (int)(i % n);
+    const float2 a = A[i];
+    C[i] = b_real ? cscale(a, Bf[k]) : cmul(a, reinterpret_cast<const float2*>(Bf)[k]);
+}
+
+__global__ void k_modulus(const float2* __restrict__ in, float* __restrict__ out, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < total) {
+        const float2 v = in[i];
+        out[i] = sqrtf(v.x * v.x + v.y * v.y);
+    }
+}
+
+// ModulusStable backward (ref/kymatio/kymatio/backend/torch_backend.py:63-96)
+__global__ void k_modulus_bwd(const float2* __restrict__ in, const float* __restrict__ mod,
+                              const float* __restrict__ g, float2* __restrict__ gin, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < total) {
+        const float m = mod[i];
+        gin[i] = m == 0.f ? make_float2(0.f, 0.f) : cscale(in[i], g[i] / m);
+    }
+}
+
+// mean over k chunks (ref/kymatio/kymatio/scattering1d/backend/torch_backend.py:18-48)
+__global__ void k_subsample_fourier(const float2* __restrict__ in, float2* __restrict__ out, int64_t rows, int n,
+                                    int k) {
+    const int m = n / k;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * m) return;
+    const int64_t r = i / m;
+    const int j = (int)(i % m);
+    float2 acc = make_float2(0.f, 0.f);
+    for (int c = 0; c < k; ++c) acc = cadd(acc, in[r * n + c * m + j]);
+    out[i] = cscale(acc, 1.0f / (float)k);
+}
+
+__global__ void k_pad_reflect(const float* __restrict__ in, float* __restrict__ out, int64_t rows, int N,
+                              int pad_left, int n_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * n_out) return;
+    const int64_t r = i / n_out;
+    const int j = (int)(i % n_out);
+    out[i] = in[r * N + reflect_idx(j - pad_left, N)];
+}
+
+static inline bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+static inline size_t fft_lds_bytes(int n) { return (size_t)2 * n * sizeof(float2); }
+
+}  // namespace vt
+
+using namespace vt;
+
+extern "C" {
+
+int vt_fe_spectrum(const float* x, int64_t rows, int N, int n_pad, int pad_left, const void* tw, void* xhat,
+                   void* stream) {
+    VT_CHECK_ARG(pow2(n_pad) && n_pad <= VT_FFT_MAX_LDS && n_pad >= N, "vt_fe_spectrum: n_pad=%d", n_pad);
+    VT_CHECK_ARG(rows > 0 && N > 1, "vt_fe_spectrum: rows/N");
+    hipLaunchKernelGGL(k_fe_spectrum, dim3((unsigned)rows), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream), x, N,
+                       n_pad, pad_left, (const float2*)tw, (float2*)xhat);
+    VT_LAUNCH_CHECK("vt_fe_spectrum");
+    return VT_OK;
+}
+
+int vt_fe_lowpass(const float* x, int64_t rows, int64_t x_row_stride, int N, int n_pad, int pad_left,
+                  const float* h0, int radius, int step, int start, int S_out, float* out, int64_t out_row_stride,
+                  void* stream) {
+    VT_CHECK_ARG(rows > 0 && S_out > 0 && radius >= 0, "vt_fe_lowpass: shape");
+    dim3 grid((S_out + 255) / 256, (unsigned)rows);
+    hipLaunchKernelGGL(k_fe_lowpass, grid, dim3(256), 0, S(stream), x, x_row_stride, N, n_pad, pad_left, h0, radius,
+                       step, start, S_out, out, out_row_stride);
+    VT_LAUNCH_CHECK("vt_fe_lowpass");
+    return VT_OK;
+}
+
+int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* psi, int n_items, const int* items,
+                  const void* tw, int N, int pad_left, void* analytic, int n_slots, const float* h0, int radius,
+                  int step, int start, int S_out, float* s1, int s1_channels, void* stream) {
+    VT_CHECK_ARG(pow2(n_pad) && n_pad <= VT_FFT_MAX_LDS, "vt_fe_wavelet: n_pad=%d", n_pad);
+    VT_CHECK_ARG(B > 0 && n_items > 0, "vt_fe_wavelet: empty");
+    VT_CHECK_ARG(step * start - radius >= 0, "vt_fe_wavelet: lowpass window leaves the padded support");
+    hipLaunchKernelGGL(k_fe_wavelet, dim3(n_items, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
+                       (const float2*)xhat, C, n_pad, psi, n_items, items, (const float2*)tw, N, pad_left,
+                       (float2*)analytic, n_slots, h0, radius, step, start, S_out, s1, s1_channels);
+    VT_LAUNCH_CHECK("vt_fe_wavelet");
+    return VT_OK;
+}
+
+int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
+                const int* slot_i, const int* slot_j, const float* power, const void* tw, const float* phi0, int dec,
+                int start, int S_out, float* out, void* stream) {
+    VT_CHECK_ARG(pow2(n_pad) && n_pad <= VT_FFT_MAX_LDS, "vt_fe_pairs: n_pad=%d", n_pad);
+    VT_CHECK_ARG(dec >= 1 && pow2(dec) && n_pad / dec >= start + S_out, "vt_fe_pairs: dec/start");
+    VT_CHECK_ARG(B > 0 && n_pairs > 0, "vt_fe_pairs: empty");
+    hipLaunchKernelGGL(k_fe_pairs, dim3(n_pairs, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
+                       (const float2*)analytic, n_slots, N, n_pad, pad_left, n_pairs, slot_i, slot_j, power,
+                       (const float2*)tw, phi0, dec, start, S_out, out);
+    VT_LAUNCH_CHECK("vt_fe_pairs");
+    return VT_OK;
+}
+
+int vt_fe_normalize(const float* in, int64_t B, int C, int in_C, int S_len, const int* kind, const float* mean,
+                    const float* stdv, float log_eps, float* out, int out_C, int out_off, void* stream) {
+    VT_CHECK_ARG(B > 0 && C > 0 && S_len > 0 && out_off + C <= out_C && in_C >= C, "vt_fe_normalize: shape");
+    dim3 grid((C * S_len + 255) / 256, (unsigned)B);
+    hipLaunchKernelGGL(k_fe_normalize, grid, dim3(256), 0, S(stream), in, C, in_C, S_len, kind, mean, stdv, log_eps, out,
+                       out_C, out_off);
+    VT_LAUNCH_CHECK("vt_fe_normalize");
+    return VT_OK;
+}
+
+int vt_normalize_raw(const float* x, int64_t rows, int64_t row_stride, int N, float mean, float stdv, float* out,
+                     void* stream) {
+    VT_CHECK_ARG(rows > 0 && N > 0, "vt_normalize_raw: shape");
+    dim3 grid((N + 255) / 256, (unsigned)rows);
+    hipLaunchKernelGGL(k_normalize_raw, grid, dim3(256), 0, S(stream), x, row_stride, N, mean, stdv, out);
+    VT_LAUNCH_CHECK("vt_normalize_raw");
+    return VT_OK;
+}
+
+int vt_fft(const void* in, void* out, int64_t rows, int n, int inverse, const void* tw, int tw_stride,
+           void* stream) {
+    VT_CHECK_ARG(pow2(n) && n <= VT_FFT_MAX_LDS && rows > 0, "vt_fft: n=%d rows=%lld", n, (long long)rows);
+    hipLaunchKernelGGL(k_fft_rows, dim3((unsigned)rows), dim3(FE_THREADS), fft_lds_bytes(n), S(stream),
+                       (const float2*)in, (float2*)out, n, (const float2*)tw, tw_stride, inverse);
+    VT_LAUNCH_CHECK("vt_fft");
+    return VT_OK;
+}
+
+int vt_cdgmm(const void* A, const void* Bf, int b_is_real, void* Cout, int64_t rows, int n, void* stream) {
+    VT_CHECK_ARG(rows > 0 && n > 0, "vt_cdgmm: shape");
+    const int64_t total = rows * n;
+    hipLaunchKernelGGL(k_cdgmm, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream), (const float2*)A,
+                       (const float*)Bf, b_is_real, (float2*)Cout, total, n);
+    VT_LAUNCH_CHECK("vt_cdgmm");
+    return VT_OK;
+}
+
+int vt_modulus(const void* in, float* out, int64_t count, void* stream) {
+    VT_CHECK_ARG(count > 0, "vt_modulus: empty");
+    hipLaunchKernelGGL(k_modulus, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, S(stream), (const float2*)in,
+                       out, count);
+    VT_LAUNCH_CHECK("vt_modulus");
+    return VT_OK;
+}
+
+int vt_modulus_bwd(const void* in, const float* mod, const float* grad, void* grad_in, int64_t count, void* stream) {
+    VT_CHECK_ARG(count > 0, "vt_modulus_bwd: empty");
+    hipLaunchKernelGGL(k_modulus_bwd, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, S(stream),
+                       (const float2*)in, mod, grad, (float2*)grad_in, count);
+    VT_LAUNCH_CHECK("vt_modulus_bwd");
+    return VT_OK;
+}
+
+int vt_subsample_fourier(const void* in, void* out, int64_t rows, int n, int k, void* stream) {
+    VT_CHECK_ARG(rows > 0 && k >= 1 && n % k == 0, "vt_subsample_fourier: n=%d k=%d", n, k);
+    const int64_t total = rows * (n / k);
+    hipLaunchKernelGGL(k_subsample_fourier, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream),
+                       (const float2*)in, (float2*)out, rows, n, k);
+    VT_LAUNCH_CHECK("vt_subsample_fourier");
+    return VT_OK;
+}
+
+int vt_pad_reflect(const float* in, float* out, int64_t rows, int N, int pad_left, int pad_right, void* stream) {
+    VT_CHECK_ARG(rows > 0 && N > 1 && pad_left >= 0 && pad_right >= 0, "vt_pad_reflect: shape");
+    const int n_out = N + pad_left + pad_right;
+    const int64_t total = rows * n_out;
+    hipLaunchKernelGGL(k_pad_reflect, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream), in, out, rows, N,
+                       pad_left, n_out);
+    VT_LAUNCH_CHECK("vt_pad_reflect");
+    return VT_OK;
+}
+
+}  // extern "C"

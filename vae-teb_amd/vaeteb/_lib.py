@@ -1,0 +1,105 @@
+"""ctypes binding of libvaeteb.so (the C ABI declared in include/vaeteb.h).
+
+Signatures are read from the header itself, so the Python side can never drift
+from the C side.  There is deliberately NO fallback: if the shared library is
+missing or was built for another architecture, importing any op raises, and the
+training step does not silently run on PyTorch kernels instead.
+"""
+import ctypes
+import os
+import re
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(os.path.dirname(_HERE))
+LIB_PATH = os.environ.get("VAETEB_LIB", os.path.join(_HERE, "_lib", "libvaeteb.so"))
+HEADER = os.path.join(_ROOT, "include", "vaeteb.h")
+
+VT_ERR_ARG, VT_ERR_LAYOUT, VT_ERR_HIP = -1, -2, -3
+
+_CT = {
+    "int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "double": ctypes.c_double,
+    "void*": ctypes.c_void_p, "float*": ctypes.c_void_p, "int*": ctypes.c_void_p, "int64_t*": ctypes.c_void_p,
+    "char*": ctypes.c_char_p,
+}
+
+
+def parse_header(path=HEADER):
+    """Return {name: (restype_str, [arg_type_str, ...])} for every `vt_*` prototype."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"\b(const\s+char\s*\*|int|void)\s+(vt_\w+)\s*\(([^)]*)\)\s*;", src):
+        ret, name, args = m.group(1).replace(" ", ""), m.group(2), m.group(3).strip()
+        types = []
+        if args and args != "void":
+            for a in args.split(","):
+                a = a.replace("const", " ").strip()
+                a = re.sub(r"\s*\*\s*", "* ", a)
+                a = re.sub(r"\b\w+$", "", a.strip()).strip()  # drop the parameter name
+                a = a.replace(" ", "")
+                if a.endswith("**") or a.endswith("*const*"):
+                    a = "void*"
+                types.append(a)
+        protos[name] = (ret, types)
+    return protos
+
+
+class VtError(RuntimeError):
+    pass
+
+
+class _Lib:
+    def __init__(self):
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libvaeteb.so not found at {LIB_PATH}. Build it first: "
+                f"`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C vae-teb_amd/csrc`).")
+        self.dll = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        self.protos = parse_header()
+        self.fns = {}
+        for name, (ret, args) in self.protos.items():
+            f = getattr(self.dll, name)
+            f.restype = ctypes.c_char_p if ret == "constchar*" else ctypes.c_int
+            f.argtypes = [_CT[a] for a in args]
+            self.fns[name] = f
+
+    def last_error(self):
+        return self.fns["vt_last_error"]().decode()
+
+    def call(self, name, *args):
+        rc = self.fns[name](*args)
+        if rc != 0:
+            msg = f"{name}: {self.last_error()}"
+            if rc == VT_ERR_ARG:
+                raise ValueError(msg)
+            raise VtError(msg)
+        return rc
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _Lib()
+    return _lib
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL).  Tensors must be contiguous."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise RuntimeError("Tensors must be contiguous.")
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name, *args):
+    return lib().call(name, *args)

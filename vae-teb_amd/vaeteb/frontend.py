@@ -1,0 +1,228 @@
+"""MI355X front-end: Scattering1D + phase harmonics + normalisation, fused.
+
+`FrontEndPlan` is built once on the host (filter bank, padding, pair and
+slot tables, twiddles) and uploaded; `FrontEnd.__call__` then turns a batch of
+raw windows x (B, 2, N) [ch0 = fhr, ch1 = up] into the model inputs of the
+reference's data contract (ref/hdf5_dataset/hdf5_dataset.py:706-779,
+ref/model/pytorch_lightning_modules.py:480-483):
+    fhr_st (B, S, 43), fhr_ph (B, S, 44), fhr_up_ph (B, S, 130), fhr (B, N)
+normalised with the dataset statistics, all in one stream of HIP launches.
+
+Reference semantics reproduced:
+  * the two front-end calls of ref/hdf5_dataset/create_hdf5_dataset.py:418-441
+    (phase on ch0; cross-phase ch0 x ch1) with the selection masks of
+    get_optimal_coefficients_for_fhr (kymatio_phase_scattering.py:635-760);
+  * only the selected pairs are computed (the reference computes all 903 per
+    call and masks afterwards; pairs are independent, so the result is equal);
+  * each analytic signal a_{c,f} is computed once and shared by every pair
+    that uses it and by the first-order scattering of ch0.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .filter_bank import build_bank, lowpass_taps, padding, twiddles
+
+FIELDS = ("fhr_st", "fhr_ph", "fhr_up_ph")
+
+
+def _i32(a, dev):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.int32), device=dev)
+
+
+def _f32(a, dev):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=dev)
+
+
+class FrontEndPlan:
+    """Host-built, device-resident tables for one (J, Q, T, N) configuration."""
+
+    def __init__(self, J=11, Q=4, T=16, N=4096, device="cuda", tail_tol=1e-9):
+        self.J, self.Q, self.T, self.N = J, Q, T, N
+        self.device = torch.device(device)
+        pd = padding(N, J, Q, T)
+        self.pad = pd
+        self.n_pad, self.pad_left, self.pad_right = pd.n_pad, pd.pad_left, pd.pad_right
+        if self.n_pad > 8192:
+            raise NotImplementedError(f"fused front-end holds one FFT in LDS (n_pad <= 8192), got {self.n_pad}")
+        bank = build_bank(pd.J_pad, J, Q, T)
+        self.bank = bank
+        self.log2T = int(math.floor(math.log2(T)))
+        self.step = 2 ** self.log2T
+        self.start = pd.ind_start[self.log2T]
+        self.S = pd.ind_end[self.log2T] - pd.ind_start[self.log2T]
+        self.n_filters = len(bank.xi1)
+        self.k1 = np.maximum(np.minimum(bank.j1, self.log2T), 0)
+
+        # pair tables (kymatio_phase_scattering.py:134-160): float32 powers as
+        # the reference computes them (xi stored float32, divided in float32)
+        xi = bank.xi1.astype(np.float32)
+        ii, jj, pw = [], [], []
+        for i in range(len(xi)):
+            for j in range(len(xi)):
+                if xi[j] >= xi[i]:
+                    ii.append(i); jj.append(j)
+                    pw.append(np.float32(xi[j]) / np.float32(xi[i]) if xi[i] > 1e-8 else np.float32(1.0))
+        self.i_idx, self.j_idx = np.array(ii), np.array(jj)
+        self.powers = np.array(pw, dtype=np.float32)
+        self.autoc_idx = np.array([k for k in range(len(ii)) if ii[k] == jj[k]])
+        self.center_freqs = xi
+        self.phase_mask, self.cross_mask = self.fhr_masks()
+
+        # phase-path low-pass decimation (kymatio_phase_scattering.py:287-292, :255-268)
+        self.dec = max(1, min(N, N // self.S)) if N > self.S else 1
+        self.nb = self.n_pad // self.dec
+        self.pair_start = self.pad_left // self.dec
+        self.pair_len = min(N // self.dec, self.nb - self.pair_start)
+        h0, radius = lowpass_taps(bank.phi_levels[0], tail_tol)
+        self.radius = radius
+
+        dev = self.device
+        self.t_psi = _f32(bank.psi1, dev)
+        self.t_h0 = _f32(h0, dev)
+        self.t_phi_crop = _f32(bank.phi_levels[0][: self.nb], dev)
+        self.t_tw = _f32(twiddles(self.n_pad), dev)
+
+    # ------------------------------------------------------------------ masks
+    def fhr_masks(self):
+        """get_optimal_coefficients_for_fhr (kymatio_phase_scattering.py:635-760)."""
+        xi, pw, ii, jj = self.center_freqs, self.powers, self.i_idx, self.j_idx
+        fmin = np.float32(0.006 if self.J >= 11 else 0.003)
+        band = xi >= fmin
+        auto = np.zeros(len(ii), bool)
+        auto[self.autoc_idx] = True
+        phase = band[ii] & band[jj] & auto
+        for r in (2, 3):
+            phase |= band[ii] & band[jj] & (np.abs(pw - np.float32(r)) < np.float32(0.1)) & (pw <= 8)
+        up = xi < np.float32(0.02)
+        fh = (xi >= np.float32(0.04)) & (xi <= np.float32(0.5))
+        cross = up[ii] & fh[jj] & (pw >= 1) & (pw <= 32)
+        return phase, cross
+
+    # ------------------------------------------------------------- work tables
+    def tables(self, phase_pairs, cross_pairs, scattering=True):
+        """Wavelet items, analytic slots and pair tables for the given pair index
+        lists (indices into the 903-pair enumeration)."""
+        need = set()
+        for k in phase_pairs:
+            need.add((0, int(self.i_idx[k]))); need.add((0, int(self.j_idx[k])))
+        for k in cross_pairs:
+            need.add((0, int(self.i_idx[k]))); need.add((1, int(self.j_idx[k])))
+        slots = {cf: s for s, cf in enumerate(sorted(need))}
+        items = []
+        for f in range(self.n_filters):
+            s1 = 1 + f if scattering else -1
+            slot = slots.get((0, f), -1)
+            if s1 >= 0 or slot >= 0:
+                items.append((0, f, slot, s1, int(self.k1[f])))
+        for f in range(self.n_filters):
+            if (1, f) in slots:
+                items.append((1, f, slots[(1, f)], -1, 0))
+        pi = [slots[(0, int(self.i_idx[k]))] for k in phase_pairs] + \
+             [slots[(0, int(self.i_idx[k]))] for k in cross_pairs]
+        pj = [slots[(0, int(self.j_idx[k]))] for k in phase_pairs] + \
+             [slots[(1, int(self.j_idx[k]))] for k in cross_pairs]
+        pw = [self.powers[k] for k in phase_pairs] + [self.powers[k] for k in cross_pairs]
+        dev = self.device
+        return dict(n_slots=len(slots), items=_i32(np.array(items).reshape(-1, 5), dev), n_items=len(items),
+                    slot_i=_i32(pi, dev), slot_j=_i32(pj, dev), power=_f32(pw, dev), n_pairs=len(pi))
+
+
+class FrontEnd:
+    """Fused training-step front-end: raw windows -> normalised model inputs."""
+
+    def __init__(self, plan: FrontEndPlan, stats=None):
+        self.plan = p = plan
+        self.phase_pairs = np.nonzero(p.phase_mask)[0]
+        self.cross_pairs = np.nonzero(p.cross_mask)[0]
+        self.tab = p.tables(self.phase_pairs, self.cross_pairs, scattering=True)
+        self.C_st = 1 + p.n_filters
+        self.C_ph, self.C_x = len(self.phase_pairs), len(self.cross_pairs)
+        self.stats = None
+        if stats is not None:
+            self.set_stats(stats)
+        self._bufs = {}
+
+    def set_stats(self, stats):
+        """stats: mapping with '<field>_mean' / '<field>_variance' arrays (the
+        layout of vaeteb/data/stats_*.npz, cf. calculate_dataset_stats.py:364-444)."""
+        dev = self.plan.device
+        s = {}
+        for f, n, kind in (("fhr_st", self.C_st, None), ("fhr_ph", self.C_ph, 2), ("fhr_up_ph", self.C_x, 2)):
+            m = np.asarray(stats[f + "_mean"], np.float32).reshape(-1)
+            v = np.asarray(stats[f + "_variance"], np.float32).reshape(-1)
+            assert m.shape[0] == n, (f, m.shape, n)
+            k = np.full(n, 2, np.int32) if kind == 2 else np.array([0] + [1] * (n - 1), np.int32)
+            s[f] = (_i32(k, dev), _f32(m, dev), _f32(np.sqrt(v), dev))
+        s["fhr"] = (float(np.asarray(stats["fhr_mean"])), float(np.sqrt(np.asarray(stats["fhr_variance"]))))
+        self.stats = s
+
+    def _buf(self, name, shape, dtype=torch.float32):
+        b = self._bufs.get(name)
+        if b is None or tuple(b.shape) != tuple(shape):
+            b = torch.empty(shape, dtype=dtype, device=self.plan.device)
+            self._bufs[name] = b
+        return b
+
+    def raw(self, x):
+        """x (B, 2, N) float32 on device -> raw (un-normalised) features
+        {'fhr_st': (B,43,S), 'pairs': (B, 44+130, S)} as the reference stores them."""
+        p, t = self.plan, self.tab
+        if x.dim() != 3 or x.shape[1] != 2 or x.shape[2] != p.N:
+            raise ValueError(f"expected (B, 2, {p.N}) windows, got {tuple(x.shape)}")
+        x = x.contiguous()
+        B = x.shape[0]
+        st = _lib.stream()
+        xhat = self._buf("xhat", (B, 2, p.n_pad, 2))
+        _lib.call("vt_fe_spectrum", _lib.ptr(x), B * 2, p.N, p.n_pad, p.pad_left, _lib.ptr(p.t_tw), _lib.ptr(xhat), st)
+        s_raw = self._buf("s_raw", (B, self.C_st, p.S))
+        _lib.call("vt_fe_lowpass", _lib.ptr(x), B, 2 * p.N, p.N, p.n_pad, p.pad_left, _lib.ptr(p.t_h0), p.radius,
+                  p.step, p.start, p.S, _lib.ptr(s_raw), self.C_st * p.S, st)
+        an = self._buf("analytic", (B, t["n_slots"], p.N, 2))
+        _lib.call("vt_fe_wavelet", _lib.ptr(xhat), B, 2, p.n_pad, _lib.ptr(p.t_psi), t["n_items"], _lib.ptr(t["items"]),
+                  _lib.ptr(p.t_tw), p.N, p.pad_left, _lib.ptr(an), t["n_slots"], _lib.ptr(p.t_h0), p.radius, p.step,
+                  p.start, p.S, _lib.ptr(s_raw), self.C_st, st)
+        pr = self._buf("pairs", (B, t["n_pairs"], p.pair_len))
+        _lib.call("vt_fe_pairs", _lib.ptr(an), B, t["n_slots"], p.N, p.n_pad, p.pad_left, t["n_pairs"],
+                  _lib.ptr(t["slot_i"]), _lib.ptr(t["slot_j"]), _lib.ptr(t["power"]), _lib.ptr(p.t_tw),
+                  _lib.ptr(p.t_phi_crop), p.dec, p.pair_start, p.pair_len, _lib.ptr(pr), st)
+        return {"fhr_st": s_raw, "pairs": pr}
+
+    def __call__(self, x, out=None):
+        """Normalised model inputs (AttributeDict fields of the reference batch)."""
+        if self.stats is None:
+            raise RuntimeError("FrontEnd needs normalisation statistics (set_stats)")
+        p = self.plan
+        r = self.raw(x)
+        B, S = x.shape[0], p.S
+        st = _lib.stream()
+        out = {} if out is None else out
+        get = lambda k, shape: out[k] if k in out else torch.empty(shape, device=p.device)
+        y_st = get("fhr_st", (B, S, self.C_st))
+        y_ph = get("fhr_ph", (B, S, self.C_ph))
+        x_ph = get("fhr_up_ph", (B, S, self.C_x))
+        y_raw = get("fhr", (B, p.N))
+        k, m, s = self.stats["fhr_st"]
+        _lib.call("vt_fe_normalize", _lib.ptr(r["fhr_st"]), B, self.C_st, self.C_st, S, _lib.ptr(k), _lib.ptr(m),
+                  _lib.ptr(s),
+                  1e-6, _lib.ptr(y_st), self.C_st, 0, st)
+        pairs = r["pairs"]
+        if self.C_ph:
+            k, m, s = self.stats["fhr_ph"]
+            _lib.call("vt_fe_normalize", pairs.data_ptr(), B, self.C_ph, pairs.shape[1], S, _lib.ptr(k),
+                      _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(y_ph), self.C_ph, 0, st)
+        if self.C_x:
+            k, m, s = self.stats["fhr_up_ph"]
+            _lib.call("vt_fe_normalize", pairs[:, self.C_ph:].data_ptr(), B, self.C_x, pairs.shape[1], S,
+                      _lib.ptr(k), _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(x_ph), self.C_x, 0, st)
+        fm, fs = self.stats["fhr"]
+        _lib.call("vt_normalize_raw", _lib.ptr(x), B, 2 * p.N, p.N, fm, fs, _lib.ptr(y_raw), st)
+        return {"fhr_st": y_st, "fhr_ph": y_ph, "fhr_up_ph": x_ph, "fhr": y_raw}
+
+
+def load_stats(J=11, Q=4, T=16, N=4096):
+    import os
+    path = os.path.join(os.path.dirname(__file__), "data", f"stats_j{J}q{Q}t{T}_n{N}.npz")
+    return dict(np.load(path, allow_pickle=False))
