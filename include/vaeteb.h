@@ -137,6 +137,72 @@ int vt_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float
 /* bf16 (RNE) shadow copy of fp32 data, for MFMA operands.                         */
 int vt_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
 
+/* --------------------------------------------------------------- dense layers
+ * fp32 tiled GEMM engine (gemm.hip).  Activations are row-major (rows, C);
+ * rows = B*S.  `ws` is caller scratch for split-K partials (ws_floats floats). */
+int vt_gemm_splits_hint(int64_t M, int N, int64_t K);
+/* Y[R,N] = X[R,K] W[N,K]^T + b   — nn.Linear inside ResidualMLP
+ * (ref/model/vae_teb_model.py:336-403) and the LSTM input projections.        */
+int vt_linear_fwd(const float* X, int64_t R, int K, const float* W, int N, const float* bias, float* Y, void* stream);
+/* dX (+)= dY W                                                                   */
+int vt_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K, float* dX, int accumulate,
+                       void* stream);
+/* dW (+)= dY^T X  (split-K over R)                                              */
+int vt_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, int accumulate,
+                         float* ws, int64_t ws_floats, void* stream);
+/* out[N] (+)= column sums of X[R,N]                                             */
+int vt_colsum(const float* X, int64_t R, int N, float* out, int accumulate, float* ws, int64_t ws_floats,
+              void* stream);
+
+/* ------------------------------------------------------------------ 1-D conv
+ * Conv1d(bias=False) over (B, L, C) activations as an implicit GEMM whose
+ * operand load performs the padding / upsampling.
+ * mode 0: CausalMultiChannelConvBlock  (ref/model/vae_teb_model.py:128-212)
+ * mode 1: MultiChannelConvBlock, reflect pad (K-1)/2, replicate if L <= pad,
+ *         up = 1: F.interpolate(x2, linear, align_corners=False) first (:214-253) */
+int vt_conv1d_out_len(int L_in, int K, int mode, int up);
+int vt_conv1d_fwd(const float* X, int B, int L_in, int Cin, const float* W, int Cout, int K, int mode, int up,
+                  float* Y, void* stream);
+/* gpad: scratch of B*(L_out+K-1)*Cin floats                                       */
+int vt_conv1d_bwd_data(const float* dY, int B, int L_in, int Cin, const float* W, int Cout, int K, int mode, int up,
+                       float* dX, int accumulate, float* gpad, void* stream);
+int vt_conv1d_bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode, int up,
+                         float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);
+
+/* -------------------------------------------------------- norms / activations
+ * act: 0 none, 1 ReLU, 2 GELU (erf), 3 tanh.                                    */
+/* y = act(LayerNorm(x)*gamma + beta); saves xhat (nullable) and rstd (nullable).
+ * replaces: nn.LayerNorm (+ the following activation) in ResidualMLP and the
+ *           encoders' fused/lstm norms (ref/model/vae_teb_model.py:342-403, :460-464) */
+int vt_layernorm_fwd(const float* x, int64_t R, int C, const float* gamma, const float* beta, int act, float eps,
+                     float* y, float* xhat, float* rstd, void* stream);
+int vt_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, int64_t R, int C, const float* gamma,
+                     const float* beta, int act, float* dx, float* dgamma, float* dbeta, int accumulate_params,
+                     float* ws, int64_t ws_floats, void* stream);
+/* Train-mode BatchNorm1d (batch stats over M = B*L rows, momentum semantics of
+ * torch, running stats updated in place) + activation.
+ * replaces: nn.BatchNorm1d(C, momentum=0.9) + ReLU/tanh (vae_teb_model.py:175, :230) */
+int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const float* beta, int act, float eps,
+                     float momentum, float* y, float* mean, float* rstd, float* run_mean, float* run_var, float* ws,
+                     int64_t ws_floats, void* stream);
+int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, int act, float* dx, float* dgamma, float* dbeta,
+                     int accumulate_params, float* ws, int64_t ws_floats, void* stream);
+int vt_act_fwd(const float* x, int64_t n, int act, float* y, void* stream);
+int vt_act_bwd(const float* dy, const float* x, int64_t n, int act, float* dx, void* stream);
+
+/* ----------------------------------------------------------------------- LSTM
+ * One layer's recurrence (hidden 64).  gin = X W_ih^T + b_ih for all t (from
+ * vt_linear_fwd); b_hh is added here.  Outputs h, h_{t-1}, c and the
+ * post-activation gates (saved for the backward).
+ * replaces: nn.LSTM(in, 64, num_layers=4, batch_first=True)
+ *           (ref/model/vae_teb_model.py:474-480, :647-653)                          */
+int vt_lstm_layer_fwd(const float* gin, const float* w_hh, const float* b_hh, int B, int S, int hidden, float* out_h,
+                      float* out_hprev, float* out_c, float* gates, void* stream);
+/* dgates = d(loss)/d(gate pre-activations) given d(loss)/d(h_t) of this layer.     */
+int vt_lstm_layer_bwd(const float* dh_out, const float* gates, const float* cst, const float* w_hh, int B, int S,
+                      int hidden, float* dgates, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -125,6 +125,27 @@ def _sub(xf, k):                                          # torch_backend.py:18-
     return xf.reshape(xf.shape[:-1] + (k, xf.shape[-1] // k)).mean(axis=-2)
 
 
+# FFT engine: numpy (pocketfft) by default.  FFT_ENGINE = "torch" runs the
+# transforms through torch.fft on the CPU — the engine the reference itself
+# uses (torch_backend.py:7-9, kymatio_phase_scattering.py:223,236,252) — which
+# the tests use to measure the reference's own fp32 rounding level.
+FFT_ENGINE = "numpy"
+
+
+def _fft(x, axis=-1):
+    if FFT_ENGINE == "torch":
+        import torch
+        return torch.fft.fft(torch.from_numpy(np.ascontiguousarray(x)), dim=axis).numpy()
+    return np.fft.fft(x, axis=axis)
+
+
+def _ifft(x, axis=-1):
+    if FFT_ENGINE == "torch":
+        import torch
+        return torch.fft.ifft(torch.from_numpy(np.ascontiguousarray(x)), dim=axis).numpy()
+    return np.fft.ifft(x, axis=axis)
+
+
 def scattering1d(x, J, Q, T, max_order=1, dtype=np.float32):
     """Averaged, vectorised Scattering1D (oversampling=0), returns (B, C, S)."""
     x = np.asarray(x)
@@ -135,25 +156,25 @@ def scattering1d(x, J, Q, T, max_order=1, dtype=np.float32):
     cast = lambda a: np.asarray(a, rd)
     x = x.astype(rd).reshape(-1, N)
     U0 = np.pad(x, ((0, 0), (pl, pr)), mode="reflect")    # torch reflect == numpy reflect
-    U0h = np.fft.fft(U0.astype(cd), axis=-1).astype(cd)
+    U0h = _fft(U0.astype(cd), axis=-1).astype(cd)
     lt = int(math.floor(math.log2(T)))
-    out = [np.fft.ifft(_sub(U0h * cast(phi["levels"][0]), 2 ** lt)).real[:, i0[lt]:i1[lt]]]
+    out = [_ifft(_sub(U0h * cast(phi["levels"][0]), 2 ** lt)).real[:, i0[lt]:i1[lt]]]
     s2 = []
     for p1 in psi1:
         k1 = max(min(p1["j"], lt), 0)
-        U1c = np.fft.ifft(_sub(U0h * cast(p1["levels"][0]), 2 ** k1)).astype(cd)
+        U1c = _ifft(_sub(U0h * cast(p1["levels"][0]), 2 ** k1)).astype(cd)
         U1 = np.abs(U1c).astype(rd)
-        U1h = np.fft.fft(U1.astype(cd)).astype(cd)
+        U1h = _fft(U1.astype(cd)).astype(cd)
         kJ = max(lt - k1, 0)
-        out.append(np.fft.ifft(_sub(U1h * cast(phi["levels"][k1]), 2 ** kJ)).real[:, i0[kJ + k1]:i1[kJ + k1]])
+        out.append(_ifft(_sub(U1h * cast(phi["levels"][k1]), 2 ** kJ)).real[:, i0[kJ + k1]:i1[kJ + k1]])
         if max_order == 2:
             for p2 in psi2:
                 if p2["j"] > p1["j"]:
                     k2 = max(min(p2["j"] - k1, lt - k1), 0)
-                    U2 = np.abs(np.fft.ifft(_sub(U1h * cast(p2["levels"][k1]), 2 ** k2)).astype(cd)).astype(rd)
-                    U2h = np.fft.fft(U2.astype(cd)).astype(cd)
+                    U2 = np.abs(_ifft(_sub(U1h * cast(p2["levels"][k1]), 2 ** k2)).astype(cd)).astype(rd)
+                    U2h = _fft(U2.astype(cd)).astype(cd)
                     k2J = max(lt - k2 - k1, 0)
-                    s2.append(np.fft.ifft(_sub(U2h * cast(phi["levels"][k1 + k2]), 2 ** k2J)).real
+                    s2.append(_ifft(_sub(U2h * cast(phi["levels"][k1 + k2]), 2 ** k2J)).real
                               [:, i0[k1 + k2 + k2J]:i1[k1 + k2 + k2J]])
     return np.stack(out + s2, axis=1).astype(rd)
 
@@ -204,8 +225,8 @@ class PhaseFrontEnd:
         return x
 
     def analytic(self, x):                                                           # :220-231
-        xf = np.fft.fft(self._reflect(x.astype(self.dtype)).astype(self.cdtype), axis=-1).astype(self.cdtype)
-        a = np.fft.ifft(xf[..., None, :] * self.psi1, axis=-1).astype(self.cdtype)
+        xf = _fft(self._reflect(x.astype(self.dtype)).astype(self.cdtype), axis=-1).astype(self.cdtype)
+        a = _ifft(xf[..., None, :] * self.psi1, axis=-1).astype(self.cdtype)
         return a[..., self.i0[0]:self.i1[0]]
 
     def _accelerate(self, a, p):                                                     # :211-218
@@ -215,14 +236,14 @@ class PhaseFrontEnd:
 
     def _lowpass(self, c, target):                                                   # :233-273
         dec = max(1, min(c.shape[-1], c.shape[-1] // target)) if (target > 0 and c.shape[-1] > target) else 1
-        cf = np.fft.fft(self._reflect(c), axis=-1).astype(self.cdtype) * self.phi
+        cf = _fft(self._reflect(c), axis=-1).astype(self.cdtype) * self.phi
         if dec > 1:
             cf = cf[..., :max(cf.shape[-1] // dec, 1)]
-            sm = np.fft.ifft(cf, axis=-1).astype(self.cdtype)
+            sm = _ifft(cf, axis=-1).astype(self.cdtype)
             s0 = self.pl // dec
             sm = sm[..., s0:min(s0 + self.N // dec, sm.shape[-1])]
         else:
-            sm = np.fft.ifft(cf, axis=-1)[..., self.i0[0]:self.i1[0]]
+            sm = _ifft(cf, axis=-1)[..., self.i0[0]:self.i1[0]]
         return sm.real.astype(self.dtype)
 
     def pairs(self, a_i, a_j, powers, target):

@@ -1,8 +1,11 @@
 """HIP front-end vs the oracle and the reference's golden outputs (MI355X).
 
 Tolerances (DESIGN.md "Parity tolerances"):
-  * FFT / spectra / analytic signals / scattering: relative L2 per row or
-    channel <= 1e-5 against the fp64 oracle (fp32 arithmetic, log2(n) stages).
+  * FFT rows: relative L2 <= 2e-6 vs numpy fp64.
+  * analytic signals / scattering: relative L2 per row vs the fp64 oracle,
+    bounded (max and median over rows) by 2x the error of the oracle run in
+    fp32 with torch.fft — the reference's own FFT engine and precision
+    (oracle.frontend_ref.FFT_ENGINE = "torch") — plus a 1e-6 floor.
   * phase-harmonic pairs: errors normalised by the cancellation-free scale
     ||lowpass(|a_i||a_j|)||; the max and median over channels must stay
     within 2x the reference's (or the fp32 oracle's) own fp32-vs-fp64 error
@@ -25,7 +28,22 @@ def _dev():
 
 
 def rel_rows(a, b):
-    return np.sqrt(((a - b) ** 2).sum(-1) / np.maximum((b ** 2).sum(-1), 1e-30))
+    return np.sqrt((np.abs(a - b) ** 2).sum(-1) / np.maximum((np.abs(b) ** 2).sum(-1), 1e-30))
+
+
+def torch_engine(fn, *a, **k):
+    """Run an oracle call with the reference's FFT engine (torch.fft, CPU fp32)."""
+    old = F.FFT_ENGINE
+    F.FFT_ENGINE = "torch"
+    try:
+        return fn(*a, **k)
+    finally:
+        F.FFT_ENGINE = old
+
+
+def assert_ref_precision(err, ref_err, floor_max=1e-6, floor_med=1e-7, what=""):
+    assert err.max() <= 2 * ref_err.max() + floor_max, (what, err.max(), ref_err.max())
+    assert np.median(err) <= 2 * np.median(ref_err) + floor_med, (what, np.median(err), np.median(ref_err))
 
 
 @pytest.fixture(scope="module")
@@ -77,8 +95,9 @@ def test_scattering_vs_oracle(request, cfg):
     r = fe.raw(torch.from_numpy(x).cuda())
     S = r["fhr_st"].cpu().numpy()
     S64 = F.scattering1d(x[:, 0], p.J, p.Q, p.T, 1, dtype=np.float64)
+    S32 = torch_engine(F.scattering1d, x[:, 0], p.J, p.Q, p.T, 1)
     assert S.shape == S64.shape
-    assert rel_rows(S, S64).max() < 1e-5
+    assert_ref_precision(rel_rows(S, S64), rel_rows(S32, S64), what="scattering")
 
 
 @pytest.mark.parametrize("J,Q", [(11, 4), (6, 1)])
@@ -88,7 +107,8 @@ def test_frontend_vs_reference_golden(golden, request, J, Q):
     g = _golden_x(golden, J, Q)
     x = g["x"]
     r = fe.raw(torch.from_numpy(x).cuda())
-    assert rel_rows(r["fhr_st"].cpu().numpy(), g["fhr_st64"]).max() < 1e-5
+    assert_ref_precision(rel_rows(r["fhr_st"].cpu().numpy(), g["fhr_st64"]), rel_rows(g["fhr_st"], g["fhr_st64"]),
+                         what="fhr_st")
     pairs = r["pairs"].cpu().numpy()
     nph = fe.C_ph
     fe64 = F.PhaseFrontEnd(J, Q, 16, 4096, dtype=np.float64)
@@ -111,11 +131,15 @@ def test_analytic_signals(fe11):
     fe11.raw(torch.from_numpy(x).cuda())
     an = torch.view_as_complex(fe11._bufs["analytic"]).cpu().numpy()
     a64 = F.PhaseFrontEnd(11, 4, 16, 4096, dtype=np.float64).analytic(x[:, [0, 1]])
+    a32 = torch_engine(F.PhaseFrontEnd(11, 4, 16, 4096).analytic, x[:, [0, 1]])
     items = t["items"].cpu().numpy()
+    errs, ref_errs = [], []
     for chan, filt, slot, _, _ in items:
         if slot < 0:
             continue
-        assert rel_rows(an[:, slot], a64[:, chan, filt]).max() < 1e-5, (chan, filt)
+        errs.append(rel_rows(an[:, slot], a64[:, chan, filt]))
+        ref_errs.append(rel_rows(a32[:, chan, filt], a64[:, chan, filt]))
+    assert_ref_precision(np.array(errs), np.array(ref_errs), what="analytic")
 
 
 def test_pairs_random_inputs_vs_oracle(fe11):
@@ -126,14 +150,12 @@ def test_pairs_random_inputs_vs_oracle(fe11):
     r = fe11.raw(torch.from_numpy(x).cuda())
     pairs = r["pairs"].cpu().numpy()
     p = fe11.plan
-    for dt in (np.float64, np.float32):
-        pass
     o32 = F.PhaseFrontEnd(11, 4, 16, 4096)
     o64 = F.PhaseFrontEnd(11, 4, 16, 4096, dtype=np.float64)
     a64 = o64.analytic(x[:, [0, 1]])
     nph = fe11.C_ph
     for key, sel, cross in (("ph", p.phase_mask, False), ("x", p.cross_mask, True)):
-        r32 = o32.forward(x, compute_phase=not cross, compute_cross_phase=cross, pair_subset=sel)
+        r32 = torch_engine(o32.forward, x, compute_phase=not cross, compute_cross_phase=cross, pair_subset=sel)
         r64 = o64.forward(x, compute_phase=not cross, compute_cross_phase=cross, pair_subset=sel)
         k = "cross_phase_corr" if cross else "phase_corr"
         out = pairs[:, nph:] if cross else pairs[:, :nph]

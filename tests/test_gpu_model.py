@@ -1,0 +1,185 @@
+"""HIP model ops and the full SeqVaeTeb step vs torch references (MI355X).
+
+Op tests compare each HIP kernel with the plain-PyTorch fp64 CPU version of
+the same op (tolerance rel-L2 <= 1e-5 unless stated).  The model tests load the
+deterministic weights (tests/golden_util.py) and compare forward outputs, the
+loss parts and every gradient with the REFERENCE's own values in
+tests/golden/model_s*.npz (fp32 CPU reference vs fp32 HIP: different
+summation orders through a 4-layer LSTM and 17 train-mode BatchNorms, so
+per-tensor rel-L2 <= 2e-4 for gradients and 1e-5 for the losses).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vaeteb import ops as o
+    return o
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _leaf(t, dev="cuda"):
+    return t.detach().to(dev, torch.float32).requires_grad_(True)
+
+
+@pytest.mark.parametrize("R,K,N", [(1000, 130, 103), (65, 32, 32), (300, 64, 256), (17, 4096, 4096)])
+def test_linear(ops, R, K, N):
+    torch.manual_seed(R)
+    x, w, b = torch.randn(R, K, dtype=torch.float64), torch.randn(N, K, dtype=torch.float64) / K ** 0.5, \
+        torch.randn(N, dtype=torch.float64)
+    gy = torch.randn(R, N, dtype=torch.float64)
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    (F.linear(xr, wr, br) * gy).sum().backward()
+    xd, wd, bd = _leaf(x), _leaf(w), _leaf(b)
+    y = ops.linear(xd, wd, bd)
+    (y * gy.float().cuda()).sum().backward()
+    assert rel(y, F.linear(x, w, b)) < 1e-5
+    assert rel(xd.grad, xr.grad) < 1e-5 and rel(wd.grad, wr.grad) < 1e-5 and rel(bd.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("C", [16, 44, 130, 4096])
+@pytest.mark.parametrize("act", ["none", "relu", "gelu"])
+def test_layernorm_act(ops, C, act):
+    torch.manual_seed(C)
+    R = 512 if C < 4096 else 8
+    x = torch.randn(R, C, dtype=torch.float64) * 3 + 1
+    g, b = 1 + 0.1 * torch.randn(C, dtype=torch.float64), 0.1 * torch.randn(C, dtype=torch.float64)
+    gy = torch.randn(R, C, dtype=torch.float64)
+    xr, gr, br = x.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
+    fn = {"none": lambda t: t, "relu": F.relu, "gelu": F.gelu}[act]
+    yr = fn(F.layer_norm(xr, (C,), gr, br, 1e-5))
+    (yr * gy).sum().backward()
+    xd, gd, bd = _leaf(x), _leaf(g), _leaf(b)
+    y = ops.layer_norm_act(xd, gd, bd, act)
+    (y * gy.float().cuda()).sum().backward()
+    assert rel(y, yr) < 1e-5
+    for a, e in ((xd.grad, xr.grad), (gd.grad, gr.grad), (bd.grad, br.grad)):
+        assert rel(a, e) < 2e-5
+
+
+def _ref_conv_block(x_blc, w, g, b, rm, rv, causal, up, tanh):
+    """Plain-torch version of the reference block on (B, L, C) input."""
+    x = x_blc.transpose(1, 2)
+    K = w.shape[-1]
+    if causal:
+        x = F.pad(x, (K - 1, 0))
+    else:
+        if up:
+            x = F.interpolate(x, scale_factor=2, mode="linear", align_corners=False)
+        p = (K - 1) // 2
+        if p > 0:
+            if x.shape[-1] <= p:
+                x = F.pad(x, (p, p), mode="replicate")
+            else:
+                x = torch.cat([x[..., 1:p + 1].flip(-1), x, x[..., -p - 1:-1].flip(-1)], -1)
+    y = F.batch_norm(F.conv1d(x, w), rm, rv, g, b, True, 0.9, 1e-5)
+    y = torch.tanh(y) if tanh else F.relu(y)
+    return y.transpose(1, 2)
+
+
+@pytest.mark.parametrize("B,L,Cin,Cout,K,causal,up,tanh", [
+    (8, 64, 16, 16, 7, True, False, False),
+    (4, 40, 32, 32, 3, True, False, False),
+    (4, 16, 87, 77, 11, False, False, False),
+    (4, 32, 77, 66, 9, False, True, False),
+    (3, 4, 87, 77, 11, False, False, False),     # L <= pad: replicate fallback
+    (2, 3, 8, 6, 5, False, True, False),         # upsample then replicate
+    (4, 256, 11, 1, 3, False, False, False),
+    (8, 256, 16, 2, 3, False, False, True),
+])
+def test_conv_bn_act(ops, B, L, Cin, Cout, K, causal, up, tanh):
+    torch.manual_seed(B * 1000 + L)
+    x = torch.randn(B, L, Cin, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, K, dtype=torch.float64) / (Cin * K) ** 0.5
+    g, b = 1 + 0.1 * torch.randn(Cout, dtype=torch.float64), 0.1 * torch.randn(Cout, dtype=torch.float64)
+    rm, rv = torch.randn(Cout, dtype=torch.float64) * 0.1, torch.rand(Cout, dtype=torch.float64) + 0.5
+    xr, wr, gr, br = [t.clone().requires_grad_() for t in (x, w, g, b)]
+    rmr, rvr = rm.clone(), rv.clone()
+    yr = _ref_conv_block(xr, wr, gr, br, rmr, rvr, causal, up, tanh)
+    gy = torch.randn_like(yr)
+    (yr * gy).sum().backward()
+    xd, wd, gd, bd = [_leaf(t) for t in (x, w, g, b)]
+    rmd, rvd = rm.float().cuda(), rv.float().cuda()
+    y = ops.conv_bn_act(xd, wd, gd, bd, rmd, rvd, mode=0 if causal else 1, up=up, act="tanh" if tanh else "relu")
+    (y * gy.float().cuda()).sum().backward()
+    assert y.shape == yr.shape
+    assert rel(y, yr) < 1e-5
+    assert rel(rmd, rmr) < 1e-6 and rel(rvd, rvr) < 1e-6
+    for a, e, n in ((xd.grad, xr.grad, "x"), (wd.grad, wr.grad, "w"), (gd.grad, gr.grad, "g"), (bd.grad, br.grad, "b")):
+        assert rel(a, e) < 5e-5, n
+
+
+@pytest.mark.parametrize("In,B,S", [(20, 4, 33), (32, 3, 16)])
+def test_lstm(ops, In, B, S):
+    torch.manual_seed(In)
+    ref = torch.nn.LSTM(In, 64, 4, batch_first=True).double()
+    x = torch.randn(B, S, In, dtype=torch.float64)
+    gy = torch.randn(B, S, 64, dtype=torch.float64)
+    xr = x.clone().requires_grad_()
+    yr, _ = ref(xr)
+    (yr * gy).sum().backward()
+    params = [_leaf(p) for p in ref.parameters()]   # order: w_ih, w_hh, b_ih, b_hh per layer
+    xd = _leaf(x)
+    y = ops.lstm(xd, params)
+    (y * gy.float().cuda()).sum().backward()
+    assert rel(y, yr) < 1e-5
+    assert rel(xd.grad, xr.grad) < 2e-5
+    for p, pr in zip(params, ref.parameters()):
+        assert rel(p.grad, pr.grad) < 2e-5
+
+
+def _load_model(S):
+    from golden_util import det_fill_
+    from vaeteb.model import SeqVaeTeb
+    return det_fill_(SeqVaeTeb(sequence_length=S)).cuda()
+
+
+@pytest.mark.parametrize("name", ["model_s16_b4", "model_s4_b3"])
+def test_model_step_vs_reference_golden(golden, name):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = golden(name)
+    S = int(g["S"])
+    m = _load_model(S)
+    m.train()
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    fw = m(T("y_st"), T("y_ph"), T("x_ph"), eps=T("eps"))
+    L = m.compute_loss(fw, T("y_st"), T("y_ph"), T("y_raw"), compute_kld_loss=True, beta=float(g["beta"]))
+    for k in ("mse_loss", "nll_loss", "kld_loss", "total_loss"):
+        exp = float(g["loss_" + k])
+        assert abs(L[k].item() - exp) <= 1e-5 * abs(exp) + 1e-7, (k, L[k].item(), exp)
+    for k in ("z", "mu_pr", "logvar_pr", "mu_post", "logvar_post", "mu_prior", "logvar_prior", "linear_output"):
+        assert rel(fw[k], torch.from_numpy(g["fw_" + k])) < 2e-5, k
+    L["total_loss"].backward()
+    names = list(g["param_names"])
+    params = dict(m.named_parameters())
+    worst = max((rel(params[k].grad, torch.from_numpy(g[f"grad_{i}"])), k) for i, k in enumerate(names))
+    assert worst[0] < 2e-4, worst
+    sd = m.state_dict()
+    for i, k in enumerate(list(g["bn_names"])):
+        assert rel(sd[k], torch.from_numpy(g[f"bn_{i}"])) < 1e-5, k
+
+
+def test_tiny_c1_vs_reference_golden(golden):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb.model import TinyVaeTeb
+    g = golden("tiny_c1")
+    m = det_fill_(TinyVaeTeb()).cuda().train()
+    r = m(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["eps"]).cuda())
+    assert abs(r["total"].item() - float(g["total"])) <= 1e-5 * abs(float(g["total"]))
+    r["total"].backward()
+    for i, (k, p) in enumerate(m.named_parameters()):
+        assert rel(p.grad, torch.from_numpy(g[f"grad_{i}"])) < 1e-4, k

@@ -1,0 +1,420 @@
+// Normalisation + activation kernels on (rows, C) row-major activations.
+//
+// LayerNorm (+ activation) fused: every ResidualMLP layer is Linear -> LN ->
+// act (ref/model/vae_teb_model.py:336-403), the encoders' fused/lstm norms and
+// the decoder heads' LN(4096) (:882-896).  One wave per row, two-pass mean /
+// variance in registers, affine + activation in the same pass; the backward
+// recomputes z = xhat*gamma + beta for the activation derivative and keeps
+// the gamma/beta column sums in registers per wave (no atomics, fixed order).
+//
+// BatchNorm1d in training mode (batch statistics over B*L per channel,
+// momentum 0.9, eps 1e-5) + ReLU/tanh for the conv blocks
+// (ref/model/vae_teb_model.py:175, :206-210, :230, :252-253).
+#include <math.h>
+
+#include "common.h"
+
+namespace vt {
+
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3 };
+
+__device__ __forceinline__ float act_f(float z, int act) {
+    switch (act) {
+        case ACT_RELU: return z > 0.f ? z : 0.f;
+        case ACT_GELU: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+        case ACT_TANH: return tanhf(z);
+        default: return z;
+    }
+}
+// d act / dz
+__device__ __forceinline__ float act_d(float z, int act) {
+    switch (act) {
+        case ACT_RELU: return z > 0.f ? 1.f : 0.f;
+        case ACT_GELU: {
+            const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+            const float pdf = 0.39894228040143268f * expf(-0.5f * z * z);
+            return cdf + z * pdf;
+        }
+        case ACT_TANH: {
+            const float t = tanhf(z);
+            return 1.f - t * t;
+        }
+        default: return 1.f;
+    }
+}
+
+static constexpr int NT = 256;  // 4 waves
+
+// ------------------------------------------------------------- LayerNorm fwd
+__global__ __launch_bounds__(NT) void k_ln_fwd(const float* __restrict__ x, int64_t R, int C,
+                                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                                               int act, float eps, float* __restrict__ y, float* __restrict__ xhat,
+                                               float* __restrict__ rstd_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+    if (row >= R) return;
+    const float* xr = x + row * C;
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += xr[c];
+    const float mean = wave_sum(s) / (float)C;
+    float v = 0.f;
+    for (int c = lane; c < C; c += 64) {
+        const float d = xr[c] - mean;
+        v += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(v) / (float)C + eps);
+    float* yr = y + row * C;
+    float* hr = xhat ? xhat + row * C : nullptr;
+    for (int c = lane; c < C; c += 64) {
+        const float h = (xr[c] - mean) * rstd;
+        if (hr) hr[c] = h;
+        yr[c] = act_f(h * gamma[c] + beta[c], act);
+    }
+    if (lane == 0 && rstd_out) rstd_out[row] = rstd;
+}
+
+// ------------------------------------------------------------- LayerNorm bwd
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * act'(z) * gamma.
+// gamma/beta column partials per block: part[block][0:C] = sum dz*xhat,
+// part[block][C:2C] = sum dz.  Small-C path (C <= 512): per-lane registers.
+template <int CPL>  // columns per lane (C <= 64*CPL)
+__global__ __launch_bounds__(NT) void k_ln_bwd(const float* __restrict__ dy, const float* __restrict__ xhat,
+                                               const float* __restrict__ rstd, int64_t R, int C,
+                                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                                               int act, int64_t rows_per_block, float* __restrict__ dx,
+                                               float* __restrict__ part) {
+    __shared__ float red[NT / 64][2][64 * CPL];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float dg[CPL], db[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) dg[j] = db[j] = 0.f;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < R ? r0 + rows_per_block : R;
+    for (int64_t row = r0 + w; row < r1; row += NT / 64) {
+        const float* dyr = dy + row * C;
+        const float* hr = xhat + row * C;
+        float gv[CPL], hv[CPL];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+            const int c = lane + 64 * j;
+            gv[j] = 0.f;
+            hv[j] = 0.f;
+            if (c < C) {
+                const float h = hr[c];
+                const float dz = dyr[c] * act_d(h * gamma[c] + beta[c], act);
+                dg[j] += dz * h;
+                db[j] += dz;
+                gv[j] = dz * gamma[c];
+                hv[j] = h;
+                s1 += gv[j];
+                s2 += gv[j] * h;
+            }
+        }
+        const float m1 = wave_sum(s1) / (float)C, m2 = wave_sum(s2) / (float)C;
+        const float rs = rstd[row];
+        float* dxr = dx + row * C;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+            const int c = lane + 64 * j;
+            if (c < C) dxr[c] = rs * (gv[j] - m1 - hv[j] * m2);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+        red[w][0][lane + 64 * j] = dg[j];
+        red[w][1][lane + 64 * j] = db[j];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += NT) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int i = 0; i < NT / 64; ++i) {
+            a += red[i][0][c];
+            b += red[i][1][c];
+        }
+        part[(int64_t)blockIdx.x * 2 * C + c] = a;
+        part[(int64_t)blockIdx.x * 2 * C + C + c] = b;
+    }
+}
+
+// Large-C path (C > 512, few rows, e.g. the LN(4096) of the decoder heads):
+// one block per row; per-row (dz*xhat, dz) written to scratch and reduced by
+// k_rows_to_cols afterwards.
+__global__ __launch_bounds__(NT) void k_ln_bwd_wide(const float* __restrict__ dy, const float* __restrict__ xhat,
+                                                    const float* __restrict__ rstd, int C,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    int act, float* __restrict__ dx, float* __restrict__ rowpart) {
+    __shared__ float red[16];
+    const int64_t row = blockIdx.x;
+    const float* dyr = dy + row * C;
+    const float* hr = xhat + row * C;
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = threadIdx.x; c < C; c += NT) {
+        const float h = hr[c];
+        const float dz = dyr[c] * act_d(h * gamma[c] + beta[c], act);
+        const float g = dz * gamma[c];
+        s1 += g;
+        s2 += g * h;
+        rowpart[row * 2 * C + c] = dz * h;
+        rowpart[row * 2 * C + C + c] = dz;
+    }
+    const float m1 = block_sum(s1, red) / (float)C;
+    const float m2 = block_sum(s2, red) / (float)C;
+    const float rs = rstd[row];
+    for (int c = threadIdx.x; c < C; c += NT) {
+        const float h = hr[c];
+        const float dz = dyr[c] * act_d(h * gamma[c] + beta[c], act);
+        dx[row * C + c] = rs * (dz * gamma[c] - m1 - h * m2);
+    }
+}
+
+// out[c] (+)= sum_b part[b][c] for c < n (fixed order).
+__global__ void k_reduce_parts(const float* __restrict__ part, int blocks, int n, float* __restrict__ out0,
+                               float* __restrict__ out1, int split, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    float a = 0.f;
+    for (int b = 0; b < blocks; ++b) a += part[(int64_t)b * n + c];
+    float* o = c < split ? out0 + c : out1 + (c - split);
+    *o = accumulate ? *o + a : a;
+}
+
+// ------------------------------------------------------------- BatchNorm
+// column partial sums over (M, C) row-major data; value per element chosen by `kind`:
+//   0: x         1: (x - mean)^2         2: (dz, dz*xhat) [two outputs]
+__global__ __launch_bounds__(NT) void k_col_partial(const float* __restrict__ x, const float* __restrict__ dy,
+                                                    int64_t M, int C, int64_t rows_per_block, int kind,
+                                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    int act, float* __restrict__ part) {
+    __shared__ float red0[NT], red1[NT];
+    const int rpi = C <= NT ? NT / C : 1;  // rows per iteration
+    const int c = threadIdx.x % C;
+    const int ro = threadIdx.x / C;
+    const bool active = C <= NT ? ro < rpi : true;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
+    float a0 = 0.f, a1 = 0.f;
+    if (active && C <= NT) {
+        const float mu = mean ? mean[c] : 0.f;
+        const float rs = rstd ? rstd[c] : 0.f;
+        for (int64_t r = r0 + ro; r < r1; r += rpi) {
+            const float v = x[r * C + c];
+            if (kind == 0) {
+                a0 += v;
+            } else if (kind == 1) {
+                const float d = v - mu;
+                a0 += d * d;
+            } else {
+                const float h = (v - mu) * rs;
+                const float dz = dy[r * C + c] * act_d(h * gamma[c] + beta[c], act);
+                a0 += dz;
+                a1 += dz * h;
+            }
+        }
+    }
+    red0[threadIdx.x] = a0;
+    red1[threadIdx.x] = a1;
+    __syncthreads();
+    if (C <= NT) {
+        for (int cc = threadIdx.x; cc < C; cc += NT) {
+            float s0 = 0.f, s1 = 0.f;
+            for (int i = 0; i < rpi; ++i) {
+                s0 += red0[i * C + cc];
+                s1 += red1[i * C + cc];
+            }
+            part[(int64_t)blockIdx.x * 2 * C + cc] = s0;
+            part[(int64_t)blockIdx.x * 2 * C + C + cc] = s1;
+        }
+    }
+}
+
+// mode 0: mean[c] = S/M.  mode 1: var = S/M -> rstd, running stats update.
+// mode 2: dbeta = S0, dgamma = S1.
+__global__ void k_bn_finalize(const float* __restrict__ part, int blocks, int C, int64_t M, int mode, float eps,
+                              float momentum, float* __restrict__ mean, float* __restrict__ rstd,
+                              float* __restrict__ run_mean, float* __restrict__ run_var, float* __restrict__ dgamma,
+                              float* __restrict__ dbeta, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s0 = 0.0, s1 = 0.0;
+    for (int b = 0; b < blocks; ++b) {
+        s0 += (double)part[(int64_t)b * 2 * C + c];
+        s1 += (double)part[(int64_t)b * 2 * C + C + c];
+    }
+    if (mode == 0) {
+        mean[c] = (float)(s0 / (double)M);
+    } else if (mode == 1) {
+        const double var = s0 / (double)M;
+        rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+        if (run_mean) {
+            const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+            run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean[c]);
+            run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+        }
+    } else {
+        dbeta[c] = accumulate ? dbeta[c] + (float)s0 : (float)s0;
+        dgamma[c] = accumulate ? dgamma[c] + (float)s1 : (float)s1;
+    }
+}
+
+__global__ void k_bn_apply(const float* __restrict__ x, int64_t M, int C, const float* __restrict__ mean,
+                           const float* __restrict__ rstd, const float* __restrict__ gamma,
+                           const float* __restrict__ beta, int act, float* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M * C) return;
+    const int c = (int)(i % C);
+    y[i] = act_f((x[i] - mean[c]) * rstd[c] * gamma[c] + beta[c], act);
+}
+
+// dx = gamma*rstd*(dz - dbeta/M - xhat*dgamma/M)
+__global__ void k_bn_dx(const float* __restrict__ dy, const float* __restrict__ x, int64_t M, int C,
+                        const float* __restrict__ mean, const float* __restrict__ rstd,
+                        const float* __restrict__ gamma, const float* __restrict__ beta, int act,
+                        const float* __restrict__ dgamma, const float* __restrict__ dbeta, float* __restrict__ dx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M * C) return;
+    const int c = (int)(i % C);
+    const float h = (x[i] - mean[c]) * rstd[c];
+    const float dz = dy[i] * act_d(h * gamma[c] + beta[c], act);
+    const float inv = 1.f / (float)M;
+    dx[i] = gamma[c] * rstd[c] * (dz - dbeta[c] * inv - h * dgamma[c] * inv);
+}
+
+__global__ void k_act_fwd(const float* __restrict__ x, int64_t n, int act, float* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = act_f(x[i], act);
+}
+__global__ void k_act_bwd(const float* __restrict__ dy, const float* __restrict__ x, int64_t n, int act,
+                          float* __restrict__ dx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dx[i] = dy[i] * act_d(x[i], act);
+}
+
+static inline unsigned blocks_for(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace vt
+
+using namespace vt;
+
+extern "C" {
+
+int vt_layernorm_fwd(const float* x, int64_t R, int C, const float* gamma, const float* beta, int act, float eps,
+                     float* y, float* xhat, float* rstd, void* stream) {
+    VT_CHECK_ARG(R > 0 && C > 0 && act >= 0 && act <= 3, "vt_layernorm_fwd: shape/act");
+    hipLaunchKernelGGL(k_ln_fwd, dim3(blocks_for(R, NT / 64)), dim3(NT), 0, S(stream), x, R, C, gamma, beta, act, eps,
+                       y, xhat, rstd);
+    VT_LAUNCH_CHECK("vt_layernorm_fwd");
+    return VT_OK;
+}
+
+// workspace: small C (<=512): 2*C*min(1024, ceil(R/64)) floats; wide C: 2*R*C floats.
+int vt_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, int64_t R, int C, const float* gamma,
+                     const float* beta, int act, float* dx, float* dgamma, float* dbeta, int accumulate_params,
+                     float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(R > 0 && C > 0, "vt_layernorm_bwd: shape");
+    hipStream_t st = S(stream);
+    if (C <= 512) {
+        int64_t blocks = (R + 63) / 64;
+        if (blocks > 1024) blocks = 1024;
+        if (blocks * 2 * C > ws_floats) blocks = ws_floats / (2 * C);
+        VT_CHECK_ARG(blocks >= 1, "vt_layernorm_bwd: workspace too small");
+        const int64_t rpb = (R + blocks - 1) / blocks;
+        blocks = (R + rpb - 1) / rpb;
+        if (C <= 64)
+            hipLaunchKernelGGL(k_ln_bwd<1>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
+                               act, rpb, dx, ws);
+        else if (C <= 128)
+            hipLaunchKernelGGL(k_ln_bwd<2>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
+                               act, rpb, dx, ws);
+        else if (C <= 256)
+            hipLaunchKernelGGL(k_ln_bwd<4>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
+                               act, rpb, dx, ws);
+        else
+            hipLaunchKernelGGL(k_ln_bwd<8>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
+                               act, rpb, dx, ws);
+        hipLaunchKernelGGL(k_reduce_parts, dim3(blocks_for(2 * C)), dim3(256), 0, st, ws, (int)blocks, 2 * C, dgamma,
+                           dbeta, C, accumulate_params);
+    } else {
+        VT_CHECK_ARG(ws_floats >= 2 * R * C, "vt_layernorm_bwd: workspace too small (wide)");
+        hipLaunchKernelGGL(k_ln_bwd_wide, dim3((unsigned)R), dim3(NT), 0, st, dy, xhat, rstd, C, gamma, beta, act, dx,
+                           ws);
+        hipLaunchKernelGGL(k_reduce_parts, dim3(blocks_for(2 * C)), dim3(256), 0, st, ws, (int)R, 2 * C, dgamma, dbeta,
+                           C, accumulate_params);
+    }
+    VT_LAUNCH_CHECK("vt_layernorm_bwd");
+    return VT_OK;
+}
+
+static int bn_blocks(int64_t M, int64_t ws_floats, int C, int64_t* rpb) {
+    int64_t blocks = (M + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks * 2 * C > ws_floats) blocks = ws_floats / (2 * C);
+    if (blocks < 1) return 0;
+    *rpb = (M + blocks - 1) / blocks;
+    return (int)((M + *rpb - 1) / *rpb);
+}
+
+// Train-mode BatchNorm1d over x (M = B*L rows, C channels) + activation.
+// Writes y, the batch mean / rstd (saved for backward) and updates the
+// running statistics in place (nullable) with PyTorch's momentum semantics.
+int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const float* beta, int act, float eps,
+                     float momentum, float* y, float* mean, float* rstd, float* run_mean, float* run_var, float* ws,
+                     int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0 && C <= 256, "vt_batchnorm_fwd: shape (C <= 256)");
+    int64_t rpb;
+    const int blocks = bn_blocks(M, ws_floats, C, &rpb);
+    VT_CHECK_ARG(blocks >= 1, "vt_batchnorm_fwd: workspace too small");
+    hipStream_t st = S(stream);
+    hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, nullptr, M, C, rpb, 0, nullptr, nullptr,
+                       nullptr, nullptr, 0, ws);
+    hipLaunchKernelGGL(k_bn_finalize, dim3(blocks_for(C)), dim3(256), 0, st, ws, blocks, C, M, 0, eps, momentum, mean,
+                       rstd, nullptr, nullptr, nullptr, nullptr, 0);
+    hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, nullptr, M, C, rpb, 1, mean, nullptr, nullptr,
+                       nullptr, 0, ws);
+    hipLaunchKernelGGL(k_bn_finalize, dim3(blocks_for(C)), dim3(256), 0, st, ws, blocks, C, M, 1, eps, momentum, mean,
+                       rstd, run_mean, run_var, nullptr, nullptr, 0);
+    hipLaunchKernelGGL(k_bn_apply, dim3(blocks_for(M * C)), dim3(256), 0, st, x, M, C, mean, rstd, gamma, beta, act, y);
+    VT_LAUNCH_CHECK("vt_batchnorm_fwd");
+    return VT_OK;
+}
+
+int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, int act, float* dx, float* dgamma, float* dbeta,
+                     int accumulate_params, float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0 && C <= 256, "vt_batchnorm_bwd: shape");
+    int64_t rpb;
+    const int blocks = bn_blocks(M, ws_floats - 2 * C, C, &rpb);
+    VT_CHECK_ARG(blocks >= 1, "vt_batchnorm_bwd: workspace too small");
+    hipStream_t st = S(stream);
+    // fresh sums for the dx formula live at the end of ws; params may accumulate
+    float* dg_now = ws + (ws_floats - 2 * C);
+    float* db_now = dg_now + C;
+    hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, 2, mean, rstd, gamma, beta, act,
+                       ws);
+    hipLaunchKernelGGL(k_bn_finalize, dim3(blocks_for(C)), dim3(256), 0, st, ws, blocks, C, M, 2, 0.f, 0.f, nullptr,
+                       nullptr, nullptr, nullptr, dg_now, db_now, 0);
+    hipLaunchKernelGGL(k_bn_dx, dim3(blocks_for(M * C)), dim3(256), 0, st, dy, x, M, C, mean, rstd, gamma, beta, act,
+                       dg_now, db_now, dx);
+    hipLaunchKernelGGL(k_reduce_parts, dim3(blocks_for(2 * C)), dim3(256), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
+                       accumulate_params);
+    VT_LAUNCH_CHECK("vt_batchnorm_bwd");
+    return VT_OK;
+}
+
+int vt_act_fwd(const float* x, int64_t n, int act, float* y, void* stream) {
+    VT_CHECK_ARG(n > 0, "vt_act_fwd: n");
+    hipLaunchKernelGGL(k_act_fwd, dim3(blocks_for(n)), dim3(256), 0, S(stream), x, n, act, y);
+    VT_LAUNCH_CHECK("vt_act_fwd");
+    return VT_OK;
+}
+
+int vt_act_bwd(const float* dy, const float* x, int64_t n, int act, float* dx, void* stream) {
+    VT_CHECK_ARG(n > 0, "vt_act_bwd: n");
+    hipLaunchKernelGGL(k_act_bwd, dim3(blocks_for(n)), dim3(256), 0, S(stream), dy, x, n, act, dx);
+    VT_LAUNCH_CHECK("vt_act_bwd");
+    return VT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,343 @@
+"""SeqVaeTeb on MI355X: same constructor / forward / compute_loss contract and
+the same state_dict key names as the reference (ref/model/vae_teb_model.py:982-1192),
+so checkpoints interchange (ref/model/graph_model.py:338-342,381-390), with
+every op routed to the HIP kernels in libvaeteb.so (vaeteb.ops).
+
+Activations stay (B, S, C) / (B, L, C) row-major end to end; the conv stacks
+read that layout directly (their kernels fuse the reference's transposes,
+padding and upsampling).  Widths follow the reference exactly (geometric
+schedules, SURVEY.md §8(a) "Exact ResidualMLP widths"); the encoder input
+widths and the decoder head size R = 16*S are constructor parameters so the
+J=6/Q=1 front-end variant and other sequence lengths work unchanged.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+def geometric_schedule(input_size, output_size, n_hidden, round_fn=round):
+    """ref/model/vae_teb_model.py:11-44 (repeated-multiplication ratio, as there)."""
+    r = (output_size / input_size) ** (1 / (n_hidden + 1))
+    sizes, cur = [], r
+    for _ in range(n_hidden):
+        sizes.append(int(round_fn(input_size * cur)))
+        cur *= r
+    return tuple(sizes + [output_size])
+
+
+# ------------------------------------------------------------- parameter holders
+class Linear(nn.Module):
+    def __init__(self, din, dout):
+        super().__init__()
+        self.in_features, self.out_features = din, dout
+        self.weight = nn.Parameter(torch.empty(dout, din))
+        self.bias = nn.Parameter(torch.zeros(dout))
+        nn.init.xavier_uniform_(self.weight)          # initialization(), vae_teb_model.py:55-59
+
+    def forward(self, x):
+        return ops.linear(x, self.weight, self.bias)
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, c, eps=1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(c))
+        self.bias = nn.Parameter(torch.zeros(c))
+
+    def forward(self, x, act="none"):
+        return ops.layer_norm_act(x, self.weight, self.bias, act, self.eps)
+
+
+class Activation(nn.Module):
+    """Parameter-free marker keeping the reference's Sequential indices."""
+
+    def __init__(self, kind):
+        super().__init__()
+        self.kind = kind
+
+
+class ResidualMLP(nn.Module):
+    """LN(in) -> [Linear -> LN -> act]* -> Linear (-> LN -> act) (+ skip);
+    ref/model/vae_teb_model.py:336-403."""
+
+    def __init__(self, input_dim, hidden_dims, final_activation=True, activation="relu", use_skip_connection=True):
+        super().__init__()
+        self.input_norm = LayerNorm(input_dim)
+        self.final_activation = final_activation
+        self.act = activation
+        mods, self._plan, d = [], [], input_dim
+        for i, h in enumerate(hidden_dims):
+            last = i == len(hidden_dims) - 1
+            lin = Linear(d, h)
+            idx = len(mods)
+            mods.append(lin)
+            ln = None
+            if not (last and not final_activation):
+                ln = LayerNorm(h)
+                mods.append(ln)
+            if not last:
+                mods.append(Activation(activation))
+            # fused: Linear, then LN + (act for hidden layers; final act for the last with final_activation)
+            act = activation if (not last or final_activation) else "none"
+            self._plan.append((idx, ln is not None, act))
+            d = h
+        self.body = nn.Sequential(*mods)
+        self.use_skip_connection = use_skip_connection
+        if use_skip_connection:
+            self.skip_proj = Linear(input_dim, hidden_dims[-1]) if input_dim != hidden_dims[-1] else nn.Identity()
+        else:
+            self.skip_proj = None
+
+    def forward(self, x):
+        x0 = self.input_norm(x)
+        h = x0
+        for (idx, has_ln, act) in self._plan:
+            h = self.body[idx](h)
+            if has_ln:
+                h = self.body[idx + 1](h, act)
+        if self.use_skip_connection:
+            s = x0 if isinstance(self.skip_proj, nn.Identity) else self.skip_proj(x0)
+            h = h + s
+        return h
+
+
+class _ConvWeight(nn.Module):
+    def __init__(self, cin, cout, k):
+        super().__init__()
+        self.in_channels, self.out_channels, self.kernel_size = cin, cout, k
+        self.weight = nn.Parameter(torch.empty(cout, cin, k))
+        nn.init.xavier_uniform_(self.weight)
+
+
+class _BatchNorm(nn.Module):
+    def __init__(self, c, momentum=0.9, eps=1e-5):
+        super().__init__()
+        self.momentum, self.eps = momentum, eps
+        self.weight = nn.Parameter(torch.ones(c))
+        self.bias = nn.Parameter(torch.zeros(c))
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+
+class ConvBlock(nn.Module):
+    """Conv1d(bias=False) -> BatchNorm1d(momentum 0.9) -> ReLU/tanh on (B, L, C).
+    causal=True: CausalMultiChannelConvBlock (ref/model/vae_teb_model.py:128-212);
+    causal=False: MultiChannelConvBlock with reflect/replicate padding and the
+    optional x2 linear upsample (:214-253)."""
+
+    def __init__(self, cin, cout, k, causal, up=False, tanh=False):
+        super().__init__()
+        self.causal, self.up, self.tanh = causal, up, tanh
+        self.conv = _ConvWeight(cin, cout, k)
+        self.bn_layer = _BatchNorm(cout)
+
+    def forward(self, x):
+        bn = self.bn_layer
+        if not self.training:
+            raise NotImplementedError("eval-mode BatchNorm is not on the training path yet")
+        y = ops.conv_bn_act(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                            mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
+                            momentum=bn.momentum, eps=bn.eps)
+        bn.num_batches_tracked.add_(1)
+        return y
+
+
+class LSTM(nn.Module):
+    """nn.LSTM(input_size, hidden, num_layers, batch_first=True) parameters
+    (same names), run by the HIP recurrence kernels."""
+
+    def __init__(self, input_size, hidden_size=64, num_layers=4):
+        super().__init__()
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        for l in range(num_layers):
+            din = input_size if l == 0 else hidden_size
+            w_ih = nn.Parameter(torch.empty(4 * hidden_size, din))
+            w_hh = nn.Parameter(torch.empty(4 * hidden_size, hidden_size))
+            nn.init.orthogonal_(w_ih)
+            nn.init.orthogonal_(w_hh)                      # initialization(), vae_teb_model.py:60-70
+            b_ih = nn.Parameter(torch.zeros(4 * hidden_size))
+            b_hh = nn.Parameter(torch.zeros(4 * hidden_size))
+            with torch.no_grad():
+                b_hh[hidden_size:2 * hidden_size].fill_(1.0)
+            setattr(self, f"weight_ih_l{l}", w_ih)
+            setattr(self, f"weight_hh_l{l}", w_hh)
+            setattr(self, f"bias_ih_l{l}", b_ih)
+            setattr(self, f"bias_hh_l{l}", b_hh)
+
+    def flat(self):
+        out = []
+        for l in range(self.num_layers):
+            out += [getattr(self, f"weight_ih_l{l}"), getattr(self, f"weight_hh_l{l}"),
+                    getattr(self, f"bias_ih_l{l}"), getattr(self, f"bias_hh_l{l}")]
+        return out
+
+    def forward(self, x):
+        return ops.lstm(x, self.flat())
+
+
+def _seq1(m):
+    s = nn.Sequential()
+    s.add_module("0", m)
+    return s
+
+
+# ---------------------------------------------------------------- encoders
+class SourceEncoder(nn.Module):
+    """ref/model/vae_teb_model.py:589-721."""
+
+    def __init__(self, input_channels=130):
+        super().__init__()
+        self.mlp = ResidualMLP(input_channels, geometric_schedule(130, 32, 5), final_activation=False)
+        self.conv = nn.Sequential(*[ConvBlock(32, 32, k, causal=True) for k in (3, 5, 7)])
+        self.fused_norm = LayerNorm(32)
+        self.lstm_norm = LayerNorm(64)
+        self.lstm = LSTM(32, 64, 4)
+        self.pre_output = ResidualMLP(64, geometric_schedule(64, 32, 4), final_activation=True)
+        self.mu_layer = ResidualMLP(32, geometric_schedule(32, 32, 4), final_activation=False)
+
+    def forward(self, x):
+        h = self.conv(self.mlp(x))
+        h = self.lstm(self.fused_norm(h))
+        return self.mu_layer(self.pre_output(self.lstm_norm(h)))
+
+
+class TargetEncoder(nn.Module):
+    """ref/model/vae_teb_model.py:406-575."""
+
+    def __init__(self, scattering_channels=43, phase_channels=44):
+        super().__init__()
+        self.mlp_scattering = _seq1(ResidualMLP(scattering_channels, geometric_schedule(43, 16, 4),
+                                                final_activation=False, activation="gelu"))
+        self.mlp_phase = ResidualMLP(phase_channels, geometric_schedule(44, 16, 4), final_activation=False)
+        self.conv_scattering = nn.Sequential(*[ConvBlock(16, 16, k, causal=True) for k in (3, 5, 7)])
+        self.conv_phase = nn.Sequential(*[ConvBlock(16, 16, k, causal=True) for k in (3, 5, 7)])
+        self.scatter_fused_norm = LayerNorm(16)
+        self.phase_fused_norm = LayerNorm(16)
+        self.lstm_norm = LayerNorm(64)
+        self.cross_modal_fusion = ResidualMLP(32, geometric_schedule(32, 20, 5), final_activation=False)
+        self.lstm = LSTM(20, 64, 4)
+        self.pre_output = ResidualMLP(64, geometric_schedule(64, 32, 5), final_activation=True)
+        self.mu_layer = ResidualMLP(32, geometric_schedule(32, 32, 32), final_activation=False)
+        self.logvar_layer = ResidualMLP(32, geometric_schedule(32, 64, 4), final_activation=False)
+
+    def forward(self, y_st, y_ph):
+        a = self.scatter_fused_norm(self.conv_scattering(self.mlp_scattering(y_st)))
+        b = self.phase_fused_norm(self.conv_phase(self.mlp_phase(y_ph)))
+        h = self.lstm(self.cross_modal_fusion(torch.cat([a, b], dim=-1)))
+        h = self.pre_output(self.lstm_norm(h))
+        return self.mu_layer(h), torch.clamp(self.logvar_layer(h), -10, 10)
+
+
+class ConditionalEncoder(nn.Module):
+    """ref/model/vae_teb_model.py:743-820."""
+
+    def __init__(self, dim_hx=32, dim_hy=32):
+        super().__init__()
+        hd = geometric_schedule(dim_hx + dim_hy, 32, 8)
+        self.mlp = ResidualMLP(dim_hx + dim_hy, hd[0:5], final_activation=True)
+        self.fc_mu = ResidualMLP(hd[4], hd[5:], final_activation=False, use_skip_connection=False)
+        self.fc_logvar = ResidualMLP(hd[4], hd[5:], final_activation=False, use_skip_connection=False)
+
+    def forward(self, h_x, h_y):
+        h = self.mlp(torch.cat([h_x, h_y], dim=-1))
+        return self.fc_mu(h), self.fc_logvar(h)
+
+
+class Decoder(nn.Module):
+    """ref/model/vae_teb_model.py:823-929 with the head width R = 16*S."""
+
+    SPEC = [(87, 77, 11, False), (77, 66, 9, True), (66, 55, 7, True), (55, 44, 5, False),
+            (44, 33, 5, True), (33, 22, 3, True), (22, 11, 3, False), (11, 1, 3, False)]
+
+    def __init__(self, latent_dim=32, sequence_length=300):
+        super().__init__()
+        self.sequence_length = sequence_length
+        R = 16 * sequence_length
+        self.linear = nn.Sequential(ResidualMLP(latent_dim, geometric_schedule(latent_dim, 50, 5)),
+                                    ResidualMLP(50, geometric_schedule(50, 87, 5)))
+        self.conv = nn.Sequential(*[ConvBlock(a, b, k, causal=False, up=u) for a, b, k, u in self.SPEC])
+        self.output_mu = ResidualMLP(R, (R, R), final_activation=False, use_skip_connection=False)
+        self.output_logvar = ResidualMLP(R, (R, R), final_activation=False, use_skip_connection=False)
+
+    def forward(self, z):
+        lin = self.linear(z)                       # (B, S, 87)
+        x = self.conv(lin)                         # (B, 16S, 1)
+        x = x.reshape(x.shape[0], -1)              # flatten (B, 16S)
+        return lin, self.output_mu(x), self.output_logvar(x)
+
+
+class SeqVaeTeb(nn.Module):
+    """Drop-in for ref/model/vae_teb_model.py:982-1192 (training path)."""
+
+    def __init__(self, input_channels=76, sequence_length=300, latent_dim_source=32, latent_dim_target=32,
+                 latent_dim_z=32, decimation_factor=16, warmup_period=30, scattering_channels=43,
+                 phase_channels=44, cross_phase_channels=130):
+        super().__init__()
+        self.latent_dim_source, self.latent_dim_target, self.latent_dim_z = latent_dim_source, latent_dim_target, \
+            latent_dim_z
+        self.decimation_factor, self.warmup_period = decimation_factor, warmup_period
+        self.source_encoder = SourceEncoder(cross_phase_channels)
+        self.target_encoder = TargetEncoder(scattering_channels, phase_channels)
+        self.conditional_encoder = ConditionalEncoder(latent_dim_source, latent_dim_target)
+        self.decoder = Decoder(latent_dim_z, sequence_length)
+
+    def forward(self, y_st, y_ph, x_ph, eps=None):
+        mu_x = self.source_encoder(x_ph)
+        mu_y, logvar_y_full = self.target_encoder(y_st, y_ph)
+        logvar_y_prior, c_logvar = torch.split(logvar_y_full, self.latent_dim_target, dim=-1)
+        mu_c, logvar_post = self.conditional_encoder(mu_x, c_logvar)
+        if eps is None:
+            eps = torch.randn_like(mu_c)            # reparameterize, vae_teb_model.py:1046-1050
+        lvp = logvar_y_prior.contiguous()
+        z, mu_post, kld = ops.latent(mu_c, logvar_post, mu_y, lvp, eps)
+        linear_output, mu_pr, logvar_pr = self.decoder(z)
+        return {"z": z, "linear_output": linear_output, "mu_pr": mu_pr, "logvar_pr": logvar_pr,
+                "mu_prior": mu_y, "logvar_prior": lvp, "mu_post": mu_post, "logvar_post": logvar_post,
+                "_kld": kld}
+
+    def compute_loss(self, forward_outputs, y_st, y_ph, y_raw, compute_kld_loss=True, beta=1.0):
+        """ref/model/vae_teb_model.py:1133-1192 (same keys)."""
+        if y_raw.dim() == 3 and y_raw.size(-1) == 1:
+            y_raw = y_raw.squeeze(-1)
+        nll, mse = ops.output_losses(forward_outputs["mu_pr"], forward_outputs["logvar_pr"], y_raw,
+                                     forward_outputs["linear_output"], y_st, y_ph)
+        kld = forward_outputs["_kld"] if compute_kld_loss else torch.zeros((), device=y_raw.device)
+        rec = mse + nll
+        return {"reconstruction_loss": rec, "mse_loss": mse, "nll_loss": nll, "kld_loss": kld,
+                "total_loss": rec + beta * kld, "classification_loss": None}
+
+    @staticmethod
+    def kld_elementwise(mu_prior, logvar_prior, mu_post, logvar_post):
+        """_kld_loss(reduce_mean=False), ref/model/vae_teb_model.py:1071-1082."""
+        return 0.5 * (logvar_prior - logvar_post - 1 + (logvar_post.exp() + (mu_post - mu_prior) ** 2)
+                      / logvar_prior.exp())
+
+
+class TinyVaeTeb(nn.Module):
+    """Config 1 (BASELINE.json configs[0]): 2-layer causal conv
+    encoder, latent 8, 2-layer reflect conv decoder on 256-pt windows."""
+
+    def __init__(self):
+        super().__init__()
+        self.enc = nn.Sequential(ConvBlock(1, 16, 3, causal=True), ConvBlock(16, 16, 5, causal=True))
+        self.mu = ResidualMLP(16, (8,), final_activation=False)
+        self.logvar = ResidualMLP(16, (8,), final_activation=False)
+        self.dec = nn.Sequential(ConvBlock(8, 16, 3, causal=False), ConvBlock(16, 2, 3, causal=False, tanh=True))
+
+    def forward(self, x, eps):
+        """x (B, 1, L) (reference layout) -> losses dict (NLL + KL with a
+        standard-normal prior)."""
+        xb = x.transpose(1, 2).contiguous()         # (B, L, 1)
+        h = self.enc(xb)
+        mu, lv = self.mu(h), self.logvar(h)
+        zero = torch.zeros_like(mu)
+        z, _, kld = ops.latent(mu, lv, zero, zero, eps)
+        out = self.dec(z)                           # (B, L, 2)
+        mu_r, lv_r = out[..., 0].contiguous(), out[..., 1].contiguous()
+        nll, _ = ops.output_losses(mu_r, lv_r, x[:, 0].contiguous())
+        return {"mu": mu, "logvar": lv, "mu_r": mu_r, "lv_r": lv_r, "kld": kld, "nll": nll, "total": nll + kld}

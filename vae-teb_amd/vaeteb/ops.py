@@ -1,0 +1,319 @@
+"""Autograd wrappers of the HIP kernels (every compute op of the training step).
+
+Each Function calls into libvaeteb.so through the C ABI (vaeteb._lib); the
+tensors are only device buffers here.  Activations are (rows, C) row-major
+with rows = B*S (or B*L for the conv stacks), the layout the kernels assume,
+so no transposes are needed between the MLP, conv and LSTM stages (the
+reference transposes to (B, C, L) for torch's conv1d at
+ref/model/vae_teb_model.py:539,545,693,917).
+"""
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
+
+
+# --------------------------------------------------------------- workspace
+class _Workspace:
+    """Grow-only scratch per device; ops are stream-ordered on the current
+    stream, so consecutive ops may reuse it."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, nfloats, device, slot=0):
+        key = (str(device), slot)
+        b = self.buf.get(key)
+        if b is None or b.numel() < nfloats:
+            b = torch.empty(max(int(nfloats), 1 << 20), dtype=torch.float32, device=device)
+            self.buf[key] = b
+        return b
+
+
+WS = _Workspace()
+WS_LINEAR = 1 << 24  # 64 MiB of split-K partials
+
+
+def _st():
+    return _lib.stream()
+
+
+def _check(*ts):
+    for t in ts:
+        if t is not None and (t.dtype != torch.float32 or not t.is_cuda):
+            raise TypeError(f"expected a CUDA float32 tensor, got {t.dtype} on {t.device}")
+
+
+# ------------------------------------------------------------------ Linear
+class LinearF(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        _check(x, w, b)
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = x.reshape(-1, K).contiguous()
+        R = x2.shape[0]
+        y = torch.empty((R, N), device=x.device)
+        call("vt_linear_fwd", ptr(x2), R, K, ptr(w), N, ptr(b), ptr(y), _st())
+        ctx.save_for_backward(x2, w)
+        ctx.shape = x.shape
+        ctx.has_bias = b is not None
+        return y.reshape(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        N, K = w.shape
+        R = x2.shape[0]
+        gy2 = gy.reshape(R, N).contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x2)
+            call("vt_linear_bwd_data", ptr(gy2), R, N, ptr(w), K, ptr(gx), 0, _st())
+            gx = gx.reshape(ctx.shape)
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty_like(w)
+            ws = WS.get(WS_LINEAR, w.device, 1)
+            call("vt_linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw), 0, ptr(ws), ws.numel(), _st())
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = torch.empty(N, device=w.device)
+            ws = WS.get(2048 * N, w.device, 2)
+            call("vt_colsum", ptr(gy2), R, N, ptr(gb), 0, ptr(ws), ws.numel(), _st())
+        return gx, gw, gb
+
+
+# -------------------------------------------------------- LayerNorm + act
+class LayerNormActF(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, act, eps):
+        _check(x, g, b)
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C).contiguous()
+        R = x2.shape[0]
+        y = torch.empty_like(x2)
+        xhat = torch.empty_like(x2)
+        rstd = torch.empty(R, device=x.device)
+        call("vt_layernorm_fwd", ptr(x2), R, C, ptr(g), ptr(b), ACT[act], eps, ptr(y), ptr(xhat), ptr(rstd), _st())
+        ctx.save_for_backward(xhat, rstd, g, b)
+        ctx.act, ctx.shape = act, x.shape
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xhat, rstd, g, b = ctx.saved_tensors
+        R, C = xhat.shape
+        gy2 = gy.reshape(R, C).contiguous()
+        gx = torch.empty_like(xhat)
+        gg, gbeta = torch.empty_like(g), torch.empty_like(b)
+        need = 2 * C * max(1024, R if C > 512 else 0)
+        ws = WS.get(need, xhat.device, 2)
+        call("vt_layernorm_bwd", ptr(gy2), ptr(xhat), ptr(rstd), R, C, ptr(g), ptr(b), ACT[ctx.act], ptr(gx),
+             ptr(gg), ptr(gbeta), 0, ptr(ws), ws.numel(), _st())
+        return gx.reshape(ctx.shape), gg, gbeta, None, None
+
+
+# ------------------------------------------------- Conv1d + BatchNorm + act
+class ConvBNActF(torch.autograd.Function):
+    """(B, L, Cin) -> (B, L_out, Cout): conv (implicit GEMM with fused
+    padding/upsampling) -> train-mode BatchNorm (running stats updated) -> act."""
+
+    @staticmethod
+    def forward(ctx, x, w, g, b, run_mean, run_var, mode, up, act, momentum, eps):
+        _check(x, w, g, b)
+        B, L, Cin = x.shape
+        Cout, _, K = w.shape
+        x = x.contiguous()
+        Lo = _lib.lib().fns["vt_conv1d_out_len"](L, K, mode, up)
+        conv = torch.empty((B, Lo, Cout), device=x.device)
+        call("vt_conv1d_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(conv), _st())
+        y = torch.empty_like(conv)
+        mean = torch.empty(Cout, device=x.device)
+        rstd = torch.empty(Cout, device=x.device)
+        ws = WS.get(4096 * Cout + 2 * Cout, x.device, 2)
+        call("vt_batchnorm_fwd", ptr(conv), B * Lo, Cout, ptr(g), ptr(b), ACT[act], eps, momentum, ptr(y), ptr(mean),
+             ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws), ws.numel(), _st())
+        ctx.save_for_backward(x, w, g, b, conv, mean, rstd)
+        ctx.cfg = (mode, up, act)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, g, b, conv, mean, rstd = ctx.saved_tensors
+        mode, up, act = ctx.cfg
+        B, L, Cin = x.shape
+        Cout, _, K = w.shape
+        Lo = conv.shape[1]
+        gy = gy.contiguous()
+        gconv = torch.empty_like(conv)
+        gg, gb = torch.empty_like(g), torch.empty_like(b)
+        ws = WS.get(4096 * Cout + 2 * Cout, x.device, 2)
+        call("vt_batchnorm_bwd", ptr(gy), ptr(conv), B * Lo, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT[act],
+             ptr(gconv), ptr(gg), ptr(gb), 0, ptr(ws), ws.numel(), _st())
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            gpad = WS.get(B * (Lo + K - 1) * Cin, x.device, 3)
+            call("vt_conv1d_bwd_data", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gx), 0, ptr(gpad), _st())
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty_like(w)
+            ws1 = WS.get(WS_LINEAR, x.device, 1)
+            call("vt_conv1d_bwd_weight", ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(gw), 0, ptr(ws1),
+                 ws1.numel(), _st())
+        return gx, gw, gg, gb, None, None, None, None, None, None, None
+
+
+# ---------------------------------------------------------------------- LSTM
+class LSTMF(torch.autograd.Function):
+    """Multi-layer unidirectional LSTM, batch_first, zero initial state.
+    params: flat list [w_ih_l0, w_hh_l0, b_ih_l0, b_hh_l0, w_ih_l1, ...]."""
+
+    @staticmethod
+    def forward(ctx, x, *params):
+        _check(x, *params)
+        B, S, _ = x.shape
+        nl = len(params) // 4
+        H = params[1].shape[1]
+        saved = []
+        inp = x.contiguous()
+        for l in range(nl):
+            w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
+            In = inp.shape[-1]
+            gin = torch.empty((B, S, 4 * H), device=x.device)
+            call("vt_linear_fwd", ptr(inp), B * S, In, ptr(w_ih), 4 * H, ptr(b_ih), ptr(gin), _st())
+            h = torch.empty((B, S, H), device=x.device)
+            hp = torch.empty_like(h)
+            c = torch.empty_like(h)
+            gates = gin  # overwritten in place by the post-activation gates
+            call("vt_lstm_layer_fwd", ptr(gin), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h), ptr(hp), ptr(c), ptr(gates),
+                 _st())
+            saved += [inp, hp, c, gates]
+            inp = h
+        ctx.save_for_backward(*saved, *params)
+        ctx.nl = nl
+        return inp
+
+    @staticmethod
+    def backward(ctx, gy):
+        t = ctx.saved_tensors
+        nl = ctx.nl
+        saved, params = t[: 4 * nl], t[4 * nl:]
+        gy = gy.contiguous()
+        B, S, H = gy.shape
+        grads = [None] * len(params)
+        dh = gy
+        ws = WS.get(WS_LINEAR, gy.device, 1)
+        wsb = WS.get(2048 * 4 * H, gy.device, 2)
+        gx = None
+        for l in reversed(range(nl)):
+            inp, hp, c, gates = saved[4 * l: 4 * l + 4]
+            w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
+            In = inp.shape[-1]
+            dg = torch.empty((B, S, 4 * H), device=gy.device)
+            call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
+            gw_ih, gw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
+            gb = torch.empty_like(b_ih)
+            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(gw_ih), 0, ptr(ws), ws.numel(), _st())
+            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(gw_hh), 0, ptr(ws), ws.numel(), _st())
+            call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), 0, ptr(wsb), wsb.numel(), _st())
+            grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, gb, gb.clone()]
+            if l > 0 or ctx.needs_input_grad[0]:
+                gin = torch.empty((B, S, In), device=gy.device)
+                call("vt_linear_bwd_data", ptr(dg), B * S, 4 * H, ptr(w_ih), In, ptr(gin), 0, _st())
+                dh = gin
+                gx = gin
+        return (gx, *grads)
+
+
+# ---------------------------------------------------------------------- ELBO
+class LatentF(torch.autograd.Function):
+    """(mu_c, lv_q, mu_y, lv_p, eps) -> (z, mu_post, kl): fused reparameterisation
+    + KL (vt_elbo_latent_*)."""
+
+    @staticmethod
+    def forward(ctx, mu_c, lv_q, mu_y, lv_p, eps):
+        _check(mu_c, lv_q, mu_y, lv_p, eps)
+        ins = [t.contiguous() for t in (mu_c, lv_q, mu_y, lv_p, eps)]
+        D = mu_c.shape[-1]
+        rows = mu_c.numel() // D
+        z, mp = torch.empty_like(ins[0]), torch.empty_like(ins[0])
+        kl = torch.empty((), device=mu_c.device)
+        ws = WS.get(_lib.lib().fns["vt_elbo_workspace_floats"](), mu_c.device, 4)
+        call("vt_elbo_latent_fwd", *[ptr(t) for t in ins], rows, D, ptr(z), ptr(mp), ptr(kl), ptr(ws), _st())
+        ctx.save_for_backward(*ins)
+        ctx.dims = (rows, D)
+        return z, mp, kl
+
+    @staticmethod
+    def backward(ctx, gz, gmp, gkl):
+        ins = ctx.saved_tensors
+        rows, D = ctx.dims
+        outs = [torch.empty_like(ins[0]) for _ in range(4)]
+        gz = gz.contiguous() if gz is not None else None
+        gmp = gmp.contiguous() if gmp is not None else None
+        gkl = gkl.reshape(1).contiguous() if gkl is not None else None
+        call("vt_elbo_latent_bwd", *[ptr(t) for t in ins], rows, D, ptr(gz), ptr(gmp), ptr(gkl), *[ptr(t) for t in outs],
+             _st())
+        return outs[0], outs[1], outs[2], outs[3], None
+
+
+class OutputLossF(torch.autograd.Function):
+    """(mu_pr, lv_pr, y_raw, lin, y_st, y_ph) -> (nll, mse) with gradients
+    computed in the forward (vt_elbo_output_fwd) and scaled in the backward."""
+
+    @staticmethod
+    def forward(ctx, mu, lv, y, lin, y_st, y_ph):
+        _check(mu, lv, y)
+        mu, lv, y = mu.contiguous(), lv.contiguous(), y.contiguous()
+        use_mse = lin is not None and lin.shape[-1] == 87 and y_st.shape[-1] == 43 and y_ph.shape[-1] == 44
+        out = torch.zeros(2, device=mu.device)
+        g_mu, g_lv = torch.empty_like(mu), torch.empty_like(lv)
+        ws = WS.get(_lib.lib().fns["vt_elbo_workspace_floats"](), mu.device, 4)
+        if use_mse:
+            lin, y_st, y_ph = lin.contiguous(), y_st.contiguous(), y_ph.contiguous()
+            g_lin = torch.empty_like(lin)
+            rows = lin.numel() // 87
+            call("vt_elbo_output_fwd", ptr(mu), ptr(lv), ptr(y), mu.numel(), ptr(lin), ptr(y_st), ptr(y_ph), rows, 43,
+                 44, ptr(g_mu), ptr(g_lv), ptr(g_lin), out.data_ptr(), out.data_ptr() + 4, ptr(ws), _st())
+        else:
+            g_lin = torch.zeros_like(lin) if lin is not None else None
+            call("vt_elbo_output_fwd", ptr(mu), ptr(lv), ptr(y), mu.numel(), None, None, None, 0, 0, 0, ptr(g_mu),
+                 ptr(g_lv), None, out.data_ptr(), out.data_ptr() + 4, ptr(ws), _st())
+        ctx.save_for_backward(g_mu, g_lv, g_lin if g_lin is not None else torch.empty(0, device=mu.device))
+        ctx.has_lin = lin is not None
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, gnll, gmse):
+        g_mu, g_lv, g_lin = ctx.saved_tensors
+        # scale the unit-upstream gradients by the incoming device scalars (no host sync)
+        for t, s in ((g_mu, gnll), (g_lv, gnll), (g_lin, gmse)):
+            if t.numel() and s is not None:
+                call("vt_scale_by_device_scalar", ptr(t), t.numel(), ptr(s.reshape(1).contiguous()), _st())
+        return g_mu, g_lv, None, (g_lin if ctx.has_lin else None), None, None
+
+
+# ------------------------------------------------------------- functional API
+def linear(x, w, b=None):
+    return LinearF.apply(x, w, b)
+
+
+def layer_norm_act(x, g, b, act="none", eps=1e-5):
+    return LayerNormActF.apply(x, g, b, act, eps)
+
+
+def conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momentum=0.9, eps=1e-5):
+    return ConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps)
+
+
+def lstm(x, params):
+    return LSTMF.apply(x, *params)
+
+
+def latent(mu_c, lv_q, mu_y, lv_p, eps):
+    return LatentF.apply(mu_c, lv_q, mu_y, lv_p, eps)
+
+
+def output_losses(mu, lv, y, lin=None, y_st=None, y_ph=None):
+    return OutputLossF.apply(mu, lv, y, lin, y_st, y_ph)
