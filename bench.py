@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""VAE-TEB training-step benchmark (BASELINE.json metric: train samples/sec + ELBO,
+4096-pt windows, batch 256 per GPU, 1/2/4/8 MI355X).
+
+A step = one pass of the north-star hot path over one batch resident in HBM:
+raw windows x (B, 2, 4096) -> HIP front-end (Scattering1D + phase harmonics +
+normalisation) -> SeqVaeTeb forward -> ELBO -> backward -> RCCL bucketed
+gradient all-reduce (N > 1) -> grad-norm clip -> AdamW.  Data are synthetic
+fetal-monitoring windows (vaeteb.synthetic; the clinical HDF5 records are not
+available), weights are the reference architecture's random init.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--frontend j11|j6] [--batch B]
+  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel, timed
+live with HIP events on its own stream inside the timed region; `cpu_baseline`
+is the oracle (faithful CPU restatement) on a bounded sample, rank 0 / N = 1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from vaeteb import _lib, synthetic  # noqa: E402
+from vaeteb.frontend import FrontEnd, FrontEndPlan, load_stats  # noqa: E402
+from vaeteb.model import SeqVaeTeb  # noqa: E402
+from vaeteb.train import Trainer, init_distributed  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+FRONTENDS = {"j11": (11, 4, 16), "j6": (6, 1, 16)}
+
+
+class KernelTimer:
+    """HIP events around every launch of one named C-ABI entry point, recorded
+    on the stream the kernel is launched on (the current stream)."""
+
+    def __init__(self, name):
+        self.name, self.pairs, self.enabled = name, [], False
+        lib = _lib.lib()
+        self._orig = lib.call
+
+        def call(fname, *args):
+            if self.enabled and fname == self.name:
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                rc = self._orig(fname, *args)
+                e.record()
+                self.pairs.append((s, e))
+                return rc
+            return self._orig(fname, *args)
+        lib.call = call
+
+    def mean_ms(self):
+        ts = [s.elapsed_time(e) for s, e in self.pairs]
+        return sum(ts) / len(ts) if ts else float("nan"), len(ts)
+
+
+def pair_kernel_bytes(fe, B):
+    """Algorithmic HBM bytes of one vt_fe_pairs launch: read a_i and a_j
+    (N complex64 each) per (sample, pair), write S float32 outputs."""
+    p = fe.plan
+    n_pairs = fe.tab["n_pairs"]
+    return B * n_pairs * (2 * p.N * 8 + p.pair_len * 4)
+
+
+def cpu_baseline(frontend_cfg, batch=8, threads=None):
+    """Faithful CPU restatement (oracle): front-end called twice per window with
+    all 903 pairs then masked (create_hdf5_dataset.py:418-441), torch.fft as in
+    the reference, + SeqVaeTeb(S=256) fwd/bwd/clip/AdamW on torch-CPU fp32."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import frontend_ref as F
+    from oracle import model_ref as M
+    threads = threads or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    J, Q, T = frontend_cfg
+    F.FFT_ENGINE = "torch"
+    fe = F.PhaseFrontEnd(J, Q, T, 4096)
+    pm, cm = fe.masks()
+    x = synthetic.batch(10_000_000, batch, 4096)
+    model = M.SeqVaeTebRef(256)
+    t0 = time.perf_counter()
+    rp = fe.forward(x, compute_phase=True)
+    rc = fe.forward(x, compute_phase=False, compute_cross_phase=True)
+    st = load_stats(J, Q, T)
+    y_st = F.normalize(rp["scattering"], "fhr_st", st["fhr_st_mean"], st["fhr_st_variance"])
+    y_ph = F.normalize(rp["phase_corr"][:, pm], "fhr_ph", st["fhr_ph_mean"], st["fhr_ph_variance"])
+    x_ph = F.normalize(rc["cross_phase_corr"][:, cm], "fhr_up_ph", st["fhr_up_ph_mean"], st["fhr_up_ph_variance"])
+    y_raw = F.normalize(x[:, 0], "fhr", st["fhr_mean"], st["fhr_variance"])
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a.transpose(0, 2, 1)))
+    b = dict(y_st=tt(y_st), y_ph=tt(y_ph), x_ph=tt(x_ph), y_raw=torch.from_numpy(y_raw))
+    M.train_step(model, b, torch.randn(batch, 256, 32), 1e-5)
+    dt = time.perf_counter() - t0
+    F.FFT_ENGINE = "numpy"
+    return {"value": round(batch / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"1 faithful CPU step at batch {batch}: front-end x2 calls with all 903 pairs + "
+                      f"SeqVaeTeb(S=256) fwd/bwd/clip/AdamW, torch threads={threads}, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--frontend", choices=list(FRONTENDS), default="j11")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=8)
+    args = ap.parse_args()
+
+    rank, world, local, dev = init_distributed()
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    torch.cuda.set_device(dev)
+    J, Q, T = FRONTENDS[args.frontend]
+    N, B = 4096, args.batch
+    plan = FrontEndPlan(J, Q, T, N, device=dev)
+    fe = FrontEnd(plan, load_stats(J, Q, T, N))
+    S = plan.S
+    torch.manual_seed(1234)  # same initial weights on every rank (DDP semantics)
+    model = SeqVaeTeb(sequence_length=S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,
+                      cross_phase_channels=fe.C_x).to(dev)
+    trainer = Trainer(model, lr=1e-3, frontend=fe, world_size=world)
+
+    # synthetic windows resident in HBM before timing; global sample index ->
+    # rank sharding as DistributedSampler (each rank its own B windows per step)
+    pool = [torch.from_numpy(synthetic.batch((rank + world * i) * B, B, N)).to(dev) for i in range(2)]
+    torch.cuda.synchronize()
+
+    timer = KernelTimer("vt_fe_pairs")
+    for i in range(args.warmup):
+        trainer.step({"x": pool[i % 2]})
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    last = None
+    for i in range(args.steps):
+        last = trainer.step({"x": pool[i % 2]})
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    elbo = {k: round(float(last[k].item()), 6) for k in ("total_loss", "nll_loss", "mse_loss", "kld_loss")}
+    samples = args.steps * B * world
+    value = samples / dt
+    k_ms, k_n = timer.mean_ms()
+    k_bytes = pair_kernel_bytes(fe, B)
+    achieved = k_bytes / (k_ms * 1e-3) / 1e9
+    out = {
+        "metric": "train samples/sec + ELBO, 4096-pt windows, batch 256, 1/2/4/8 MI355X",
+        "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": f"c2: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTeb(R={16 * S}) "
+                               f"train step, batch {B}/GPU", "global_batch": B * world, "seq_len": N,
+                   "parallelism": f"dp{world}"},
+        "elbo": elbo,
+        "roofline": {"bound": "hbm", "kernel": "vt_fe_pairs", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "avg_launch_ms": round(k_ms, 4), "launches": k_n, "algorithmic_bytes": k_bytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline((J, Q, T), batch=args.cpu_batch)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+"""Thin training-step module: the MI355X replacement for the reference's
+PyTorch-Lightning / hand-written DDP loops (ref/model/graph_model.py:404-908,
+ref/model/pytorch_lightning_modules.py:401-564).
+
+One process per GPU (torchrun), RCCL (torch backend "nccl") over xGMI.
+Per step (ref/model/graph_model.py:700-726 order, no host synchronisation):
+  zero grads -> [front-end] -> forward -> loss -> backward
+  (bucketed gradient all-reduce launched from post-accumulate hooks, overlapped
+  with the rest of the backward) -> grad-norm clip -> AdamW
+All parameters, gradients and Adam moments are views into four flat fp32
+buffers, so zeroing, clipping and the optimiser are single launches over
+contiguous memory and the all-reduce buckets are plain slices.
+"""
+import math
+import os
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+
+class FlatState:
+    """Flat parameter / gradient / moment storage for a module's parameters.
+    Layout is reverse registration order (≈ the order gradients become ready
+    in backward), so the all-reduce buckets fill front to back."""
+
+    def __init__(self, module):
+        params = [p for p in module.parameters() if p.requires_grad]
+        self.params = list(reversed(params))
+        dev = self.params[0].device
+        self.numel = sum(p.numel() for p in self.params)
+        self.p = torch.empty(self.numel, device=dev)
+        self.g = torch.zeros(self.numel, device=dev)
+        self.m = torch.zeros(self.numel, device=dev)
+        self.v = torch.zeros(self.numel, device=dev)
+        self.offsets = []
+        o = 0
+        with torch.no_grad():
+            for p in self.params:
+                n = p.numel()
+                self.p[o:o + n].copy_(p.reshape(-1))
+                p.data = self.p[o:o + n].view_as(p)
+                p.grad = self.g[o:o + n].view_as(p)
+                self.offsets.append((o, n))
+                o += n
+
+    def zero_grad(self):
+        self.g.zero_()
+        for p, (o, n) in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.g[o:o + n].data_ptr():
+                p.grad = self.g[o:o + n].view_as(p)
+
+
+class GradBuckets:
+    """Bucketed all-reduce (SUM) of the flat gradient buffer, launched from
+    post-accumulate-grad hooks as soon as every parameter of a bucket has its
+    gradient, on RCCL's stream (overlaps the remaining backward).  Buckets are
+    >= bucket_mb of contiguous gradient memory (xGMI rings are per-link bound:
+    fewer, larger collectives)."""
+
+    def __init__(self, state: FlatState, group=None, bucket_mb=64.0):
+        self.state, self.group = state, group
+        limit = int(bucket_mb * (1 << 20) / 4)
+        self.buckets = []  # (start, end, n_params)
+        self.param_bucket = {}
+        start, count, cur = 0, 0, 0
+        for i, (p, (o, n)) in enumerate(zip(state.params, state.offsets)):
+            self.param_bucket[id(p)] = len(self.buckets)
+            count += 1
+            cur = o + n
+            if cur - start >= limit or i == len(state.params) - 1:
+                self.buckets.append((start, cur, count))
+                start, count = cur, 0
+        self.pending = [0] * len(self.buckets)
+        self.works = []
+        self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in state.params]
+
+    def reset(self):
+        self.pending = [b[2] for b in self.buckets]
+        self.works = []
+
+    def _hook(self, p):
+        b = self.param_bucket[id(p)]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            s, e, _ = self.buckets[b]
+            self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True))
+
+    def finish(self):
+        # parameters that received no gradient this step still have to be reduced
+        for b, left in enumerate(self.pending):
+            if left > 0:
+                s, e, _ = self.buckets[b]
+                self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
+                                                  async_op=True))
+                self.pending[b] = 0
+        for w in self.works:
+            w.wait()  # orders the compute stream after the collective; no host wait for RCCL
+        self.works = []
+
+
+class Trainer:
+    """AdamW(lr, weight_decay=1e-4, eps=1e-8, betas) + clip_grad_norm_(max_norm)
+    over flat buffers (ref/model/graph_model.py:654-660, :724)."""
+
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=1e-4, max_norm=1.0, beta_kld=1e-5,
+                 frontend=None, world_size=1, group=None, bucket_mb=64.0):
+        self.model = model
+        self.frontend = frontend
+        self.state = FlatState(model)
+        self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_norm
+        self.beta_kld = beta_kld
+        self.world = world_size
+        self.steps = 0
+        dev = self.state.p.device
+        self.norm_out = torch.zeros(2, device=dev)
+        self.norm_ws = torch.empty(_lib.lib().fns["vt_grad_norm_workspace_floats"](), device=dev)
+        self.buckets = GradBuckets(self.state, group, bucket_mb) if world_size > 1 else None
+
+    def loss(self, batch, eps=None):
+        """Forward + loss for an AttributeDict-like batch with fields fhr_st,
+        fhr_ph, fhr_up_ph (B,S,C) and fhr (B,R) (the reference batch contract,
+        ref/model/graph_model.py:702-705), or raw windows under key 'x'."""
+        if "x" in batch:
+            batch = self.frontend(batch["x"])
+        fw = self.model(batch["fhr_st"], batch["fhr_ph"], batch["fhr_up_ph"], eps=eps)
+        return self.model.compute_loss(fw, batch["fhr_st"], batch["fhr_ph"], batch["fhr"], compute_kld_loss=True,
+                                       beta=self.beta_kld)
+
+    def step(self, batch, eps=None):
+        """One optimisation step; returns the loss dict (device scalars, no sync)."""
+        self.model.train()
+        self.state.zero_grad()
+        if self.buckets:
+            self.buckets.reset()
+        losses = self.loss(batch, eps)
+        losses["total_loss"].backward()
+        if self.buckets:
+            self.buckets.finish()
+        self.steps += 1
+        st = _lib.stream()
+        s = self.state
+        _lib.call("vt_grad_norm_clip", s.g.data_ptr(), s.numel, 1.0 / self.world, float(self.max_norm),
+                  self.norm_out.data_ptr(), self.norm_ws.data_ptr(), st)
+        _lib.call("vt_adamw_step", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(), s.numel,
+                  float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
+                  self.steps, self.norm_out.data_ptr() + 4, st)
+        losses["grad_norm"] = self.norm_out[0]
+        return losses
+
+
+def init_distributed():
+    """torchrun environment -> (rank, world, local_rank, device); RCCL on GPUs,
+    gloo on CPU-only hosts (the multi-process CPU tests)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    dev = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device("cpu")
+    return rank, world, local, dev
+
+
+def smoke_step():
+    """One small HIP training step checked against the oracle (used by
+    __graft_entry__.smoke())."""
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from golden_util import det_fill_
+    from oracle import model_ref as M
+    from .model import SeqVaeTeb
+    S, B = 16, 2
+    rng = np.random.default_rng(0)
+    batch = {k: rng.standard_normal(s).astype(np.float32) for k, s in
+             (("fhr_st", (B, S, 43)), ("fhr_ph", (B, S, 44)), ("fhr_up_ph", (B, S, 130)), ("fhr", (B, 16 * S)))}
+    eps = rng.standard_normal((B, S, 32)).astype(np.float32)
+    ref = det_fill_(M.SeqVaeTebRef(S))
+    T = {k: torch.from_numpy(v) for k, v in batch.items()}
+    _, Lr, _, _ = M.train_step(ref, dict(y_st=T["fhr_st"], y_ph=T["fhr_ph"], x_ph=T["fhr_up_ph"], y_raw=T["fhr"]),
+                               torch.from_numpy(eps), 1e-5)
+    m = det_fill_(SeqVaeTeb(sequence_length=S)).cuda()
+    tr = Trainer(m, lr=1e-3)
+    L = tr.step({k: v.cuda() for k, v in T.items()}, eps=torch.from_numpy(eps).cuda())
+    got, exp = L["total_loss"].item(), Lr["total_loss"].item()
+    assert abs(got - exp) <= 1e-5 * abs(exp), (got, exp)
+    sd = m.state_dict()
+    worst = max(((sd[k].cpu() - v).norm() / v.norm().clamp_min(1e-12)).item() for k, v in ref.state_dict().items()
+                if v.dtype == torch.float32)
+    assert worst < 1e-3, worst
+    print(f"smoke: training step ok (loss {got:.6f} vs oracle {exp:.6f}, worst param rel err {worst:.2e})")
