@@ -113,7 +113,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--frontend", choices=list(FRONTENDS), default="j11")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-batch", type=int, default=32)
     args = ap.parse_args()
 
     rank, world, local, dev = init_distributed()

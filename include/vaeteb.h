@@ -147,9 +147,10 @@ int vt_linear_fwd(const float* X, int64_t R, int K, const float* W, int N, const
 /* dX (+)= dY W                                                                   */
 int vt_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K, float* dX, int accumulate,
                        void* stream);
-/* dW (+)= dY^T X  (split-K over R)                                              */
-int vt_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, int accumulate,
-                         float* ws, int64_t ws_floats, void* stream);
+/* dW (+)= dY^T X and, if db != NULL, db (+)= column sums of dY (fused as a
+ * ones-column of X); split-K over R with a fixed-order reduction.              */
+int vt_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
+                         int accumulate, float* ws, int64_t ws_floats, void* stream);
 /* out[N] (+)= column sums of X[R,N]                                             */
 int vt_colsum(const float* X, int64_t R, int N, float* out, int accumulate, float* ws, int64_t ws_floats,
               void* stream);
@@ -168,6 +169,17 @@ int vt_conv1d_bwd_data(const float* dY, int B, int L_in, int Cin, const float* W
                        float* dX, int accumulate, float* gpad, void* stream);
 int vt_conv1d_bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode, int up,
                          float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);
+/* Direct (LDS-windowed) conv kernels used on the training path (conv.hip), K <= 11:
+ * forward; bwd-data as a full correlation into gpad (B, L_out+K-1, Cin) + fold;
+ * bwd-weight with fixed-order split reduction.                                   */
+int vt_conv1d_direct_fwd(const float* X, int B, int L_in, int Cin, const float* W, int Cout, int K, int mode, int up,
+                         float* Y, void* stream);
+int vt_conv1d_direct_bwd_gpad(const float* dY, int B, int L_in, int Cin, const float* W, int Cout, int K, int mode,
+                              int up, float* gpad, void* stream);
+int vt_conv1d_fold(const float* gpad, int B, int L_in, int Cin, int Cout, int K, int mode, int up, float* dX,
+                   int accumulate, void* stream);
+int vt_conv1d_direct_bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode,
+                                int up, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);
 
 /* -------------------------------------------------------- norms / activations
  * act: 0 none, 1 ReLU, 2 GELU (erf), 3 tanh.                                    */

@@ -124,21 +124,38 @@ __global__ __launch_bounds__(GT) void k_gemm(LA la, LB lb, int64_t M, int N, int
     const int64_t kb = (int64_t)blockIdx.z * k_chunk;
     const int64_t ke = kb + k_chunk < K ? kb + k_chunk : K;
     float acc[4][4] = {};
-    for (int64_t k0 = kb; k0 < ke; k0 += TK) {
+    // register prefetch: the global loads of tile k0+TK are issued before the
+    // FMAs of tile k0, so their latency hides under the compute
+    float ra[4], rb[4];
+    auto fetch = [&](int64_t k0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int idx = tid + GT * i;
             int mm, kk;
             if (A_M_FAST) { kk = idx >> 6; mm = idx & 63; } else { mm = idx >> 4; kk = idx & 15; }
             const int64_t gm = m0 + mm, gk = k0 + kk;
-            As[kk][mm] = (gm < M && gk < ke) ? la.at(gm, gk) : 0.f;
+            ra[i] = (gm < M && gk < ke) ? la.at(gm, gk) : 0.f;
             int nn, kb2;
             if (B_N_FAST) { kb2 = idx >> 6; nn = idx & 63; } else { nn = idx >> 4; kb2 = idx & 15; }
             const int gn = n0 + nn;
             const int64_t gk2 = k0 + kb2;
-            Bs[kb2][nn] = (gn < N && gk2 < ke) ? lb.at(gk2, gn) : 0.f;
+            rb[i] = (gn < N && gk2 < ke) ? lb.at(gk2, gn) : 0.f;
+        }
+    };
+    if (kb < ke) fetch(kb);
+    for (int64_t k0 = kb; k0 < ke; k0 += TK) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int idx = tid + GT * i;
+            int mm, kk;
+            if (A_M_FAST) { kk = idx >> 6; mm = idx & 63; } else { mm = idx >> 4; kk = idx & 15; }
+            As[kk][mm] = ra[i];
+            int nn, kb2;
+            if (B_N_FAST) { kb2 = idx >> 6; nn = idx & 63; } else { nn = idx >> 4; kb2 = idx & 15; }
+            Bs[kb2][nn] = rb[i];
         }
         __syncthreads();
+        if (k0 + TK < ke) fetch(k0 + TK);
 #pragma unroll
         for (int kk = 0; kk < TK; ++kk) {
             const float4 a = *reinterpret_cast<const float4*>(&As[kk][ty * 4]);
@@ -171,47 +188,78 @@ __global__ __launch_bounds__(GT) void k_gemm(LA la, LB lb, int64_t M, int N, int
 }
 
 // out[m, n] (+)= sum_z ws[z, m, n] + bias; layout 0 row-major (ldc), 1 conv
-// weight (m = co, n = k*Cin + ci -> C[(co*Cin + ci)*K + k]).
+// weight (m = co, n = k*Cin + ci -> C[(co*Cin + ci)*K + k]), 2 row-major with
+// the last column (the fused ones-column = bias gradient) written to col_out[m].
 __global__ void k_splitk_reduce(const float* __restrict__ ws, int splits, int64_t M, int N, float* __restrict__ C,
                                 int64_t ldc, const float* __restrict__ bias, int accumulate, int layout, int Cin,
-                                int Kw) {
+                                int Kw, float* __restrict__ col_out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= M * N) return;
     const int64_t m = i / N;
     const int n = (int)(i - m * N);
     float v = 0.f;
+#pragma unroll 8
     for (int z = 0; z < splits; ++z) v += ws[(int64_t)z * M * N + i];
     if (bias) v += bias[n];
-    int64_t o;
-    if (layout == 0) {
-        o = m * ldc + n;
-    } else {
+    float* o;
+    if (layout == 1) {
         const int k = n / Cin, ci = n - k * Cin;
-        o = (m * Cin + ci) * Kw + k;
+        o = C + (m * Cin + ci) * Kw + k;
+    } else if (layout == 2 && n == N - 1) {
+        o = col_out + m;
+    } else {
+        o = C + m * ldc + n;
     }
-    if (accumulate) v += C[o];
-    C[o] = v;
+    if (accumulate) v += *o;
+    *o = v;
 }
+
+struct RowMajorOnes {        // X[r * ld + c] for c < K, 1 for c == K (fused bias-gradient column)
+    const float* p;
+    int64_t ld;
+    int K;
+    __device__ float at(int64_t r, int64_t c) const { return c < K ? p[r * ld + c] : 1.f; }
+};
 
 // column sums: out[n] (+)= sum_m X[m, n] over a row-major (M, N) matrix.
 // Two-stage, fixed order: partial[block][n] then reduction.
-__global__ void k_colsum_partial(const float* __restrict__ X, int64_t M, int N, int64_t rows_per_block,
-                                 float* __restrict__ partial) {
+// 256 threads cover rpi = 256/N rows x N columns per iteration (coalesced rows);
+// columns wider than 256 loop.  Partials combined per column in LDS.
+__global__ __launch_bounds__(256) void k_colsum_partial(const float* __restrict__ X, int64_t M, int N,
+                                                        int64_t rows_per_block, float* __restrict__ partial) {
+    __shared__ float red[256];
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
-    for (int n = threadIdx.x; n < N; n += blockDim.x) {
+    if (N <= 256) {
+        const int rpi = 256 / N;
+        const int c = threadIdx.x % N, ro = threadIdx.x / N;
         float a = 0.f;
-        for (int64_t r = r0; r < r1; ++r) a += X[r * N + n];
-        partial[(int64_t)blockIdx.x * N + n] = a;
+        if (ro < rpi)
+            for (int64_t r = r0 + ro; r < r1; r += rpi) a += X[r * N + c];
+        red[threadIdx.x] = a;
+        __syncthreads();
+        if (threadIdx.x < N) {
+            float s = 0.f;
+            for (int i = 0; i < rpi; ++i) s += red[i * N + threadIdx.x];
+            partial[(int64_t)blockIdx.x * N + threadIdx.x] = s;
+        }
+    } else {
+        for (int n = threadIdx.x; n < N; n += 256) {
+            float a = 0.f;
+            for (int64_t r = r0; r < r1; ++r) a += X[r * N + n];
+            partial[(int64_t)blockIdx.x * N + n] = a;
+        }
     }
 }
-__global__ void k_colsum_final(const float* __restrict__ partial, int blocks, int N, float* __restrict__ out,
-                               int accumulate) {
-    const int n = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= N) return;
+// one workgroup per column
+__global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ partial, int blocks, int N,
+                                                      float* __restrict__ out, int accumulate) {
+    __shared__ float red[16];
+    const int n = blockIdx.x;
     float a = 0.f;
-    for (int b = 0; b < blocks; ++b) a += partial[(int64_t)b * N + n];
-    out[n] = accumulate ? out[n] + a : a;
+    for (int b = threadIdx.x; b < blocks; b += 256) a += partial[(int64_t)b * N + n];
+    a = block_sum(a, red);
+    if (threadIdx.x == 0) out[n] = accumulate ? out[n] + a : a;
 }
 
 // conv bwd-data fold: gradient of the padded / upsampled input (B, Lp, Cin)
@@ -273,7 +321,7 @@ static inline dim3 gemm_grid(int64_t M, int N, int splits) {
 template <class LA, class LB, bool AM, bool BN>
 static int launch(const char* name, LA la, LB lb, int64_t M, int N, int64_t K, float* C, int64_t ldc,
                   const float* bias, int accumulate, float* ws, int64_t ws_floats, int splits_wanted, int layout,
-                  int Cin, int Kw, hipStream_t st) {
+                  int Cin, int Kw, hipStream_t st, float* col_out = nullptr) {
     int splits = 1;
     if (splits_wanted > 1 && ws) {
         int64_t cap = ws_floats / (M * (int64_t)N);
@@ -296,7 +344,7 @@ static int launch(const char* name, LA la, LB lb, int64_t M, int N, int64_t K, f
                            C, ldc, bias, accumulate, ws);
         const int64_t tot = M * (int64_t)N;
         hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ws, splits, M, N, C,
-                           ldc, bias, accumulate, layout, Cin, Kw);
+                           ldc, bias, accumulate, layout, Cin, Kw, col_out);
     }
     VT_LAUNCH_CHECK(name);
     return VT_OK;
@@ -319,8 +367,11 @@ extern "C" {
 
 int vt_gemm_splits_hint(int64_t M, int N, int64_t K) {
     const int64_t tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+    // ~4 workgroups per CU (latency hiding), >= 256 reduction rows per split,
+    // <= 256 splits so the fixed-order split reduction stays short
     int64_t s = 1024 / (tiles > 0 ? tiles : 1);
-    const int64_t maxs = (K + 255) / 256;
+    int64_t maxs = (K + 255) / 256;
+    if (maxs > 256) maxs = 256;
     if (s > maxs) s = maxs;
     return (int)(s < 1 ? 1 : s);
 }
@@ -342,12 +393,31 @@ int vt_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K,
 }
 
 // dW[N,K] (+)= dY[R,N]^T X[R,K]  (split-K over R through `ws`)
-int vt_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, int accumulate,
-                         float* ws, int64_t ws_floats, void* stream) {
+int vt_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
+                         int accumulate, float* ws, int64_t ws_floats, void* stream) {
     VT_CHECK_ARG(R > 0 && K > 0 && N > 0, "vt_linear_bwd_weight: shape");
+    if (db) {  // bias gradient fused as an extra ones-column of X
+        const int K1 = K + 1;
+        int splits = vt_gemm_splits_hint(N, K1, R);
+        return launch<ColMajor, RowMajorOnes, true, true>("vt_linear_bwd_weight", ColMajor{dY, N},
+                                                          RowMajorOnes{X, K, K}, N, K1, R, dW, K, nullptr, accumulate,
+                                                          ws, ws_floats, splits, 2, 0, 0, S(stream), db);
+    }
     return launch<ColMajor, RowMajor, true, true>("vt_linear_bwd_weight", ColMajor{dY, N}, RowMajor{X, K}, N, K, R, dW,
                                                   K, nullptr, accumulate, ws, ws_floats, vt_gemm_splits_hint(N, K, R),
                                                   0, 0, 0, S(stream));
+}
+
+// fold of a padded / upsampled input gradient gpad (B, L_out+K-1, Cin) onto dX (B, L_in, Cin)
+int vt_conv1d_fold(const float* gpad, int B, int L_in, int Cin, int Cout, int K, int mode, int up, float* dX,
+                   int accumulate, void* stream) {
+    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0, "vt_conv1d_fold: shape");
+    ConvGeom g = make_geom(B, L_in, Cin, Cout, K, mode, up);
+    const int64_t total = (int64_t)B * L_in * Cin;
+    hipLaunchKernelGGL(k_conv_fold, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream), gpad, g, dX,
+                       accumulate);
+    VT_LAUNCH_CHECK("vt_conv1d_fold");
+    return VT_OK;
 }
 
 // out[N] (+)= column sums of X[R,N]  (bias / BN-beta gradients)
@@ -360,9 +430,9 @@ int vt_colsum(const float* X, int64_t R, int N, float* out, int accumulate, floa
     VT_CHECK_ARG(blocks >= 1, "vt_colsum: workspace too small");
     const int64_t rpb = (R + blocks - 1) / blocks;
     blocks = (R + rpb - 1) / rpb;
-    hipLaunchKernelGGL(k_colsum_partial, dim3((unsigned)blocks), dim3(N < 256 ? ((N + 63) / 64) * 64 : 256), 0,
+    hipLaunchKernelGGL(k_colsum_partial, dim3((unsigned)blocks), dim3(256), 0,
                        S(stream), X, R, N, rpb, ws);
-    hipLaunchKernelGGL(k_colsum_final, dim3((N + 255) / 256), dim3(256), 0, S(stream), ws, (int)blocks, N, out,
+    hipLaunchKernelGGL(k_colsum_final, dim3(N), dim3(256), 0, S(stream), ws, (int)blocks, N, out,
                        accumulate);
     VT_LAUNCH_CHECK("vt_colsum");
     return VT_OK;

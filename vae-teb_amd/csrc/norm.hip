@@ -169,15 +169,20 @@ __global__ __launch_bounds__(NT) void k_ln_bwd_wide(const float* __restrict__ dy
     }
 }
 
-// out[c] (+)= sum_b part[b][c] for c < n (fixed order).
-__global__ void k_reduce_parts(const float* __restrict__ part, int blocks, int n, float* __restrict__ out0,
-                               float* __restrict__ out1, int split, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
+// out[c] (+)= sum_b part[b][c] for c < n: one workgroup per column, threads
+// stride over the partials, fixed-order tree -> deterministic.
+__global__ __launch_bounds__(NT) void k_reduce_parts(const float* __restrict__ part, int blocks, int n,
+                                                     float* __restrict__ out0, float* __restrict__ out1, int split,
+                                                     int accumulate) {
+    __shared__ float red[16];
+    const int c = blockIdx.x;
     float a = 0.f;
-    for (int b = 0; b < blocks; ++b) a += part[(int64_t)b * n + c];
-    float* o = c < split ? out0 + c : out1 + (c - split);
-    *o = accumulate ? *o + a : a;
+    for (int b = threadIdx.x; b < blocks; b += NT) a += part[(int64_t)b * n + c];
+    a = block_sum(a, red);
+    if (threadIdx.x == 0) {
+        float* o = c < split ? out0 + c : out1 + (c - split);
+        *o = accumulate ? *o + a : a;
+    }
 }
 
 // ------------------------------------------------------------- BatchNorm
@@ -232,17 +237,31 @@ __global__ __launch_bounds__(NT) void k_col_partial(const float* __restrict__ x,
 
 // mode 0: mean[c] = S/M.  mode 1: var = S/M -> rstd, running stats update.
 // mode 2: dbeta = S0, dgamma = S1.
-__global__ void k_bn_finalize(const float* __restrict__ part, int blocks, int C, int64_t M, int mode, float eps,
-                              float momentum, float* __restrict__ mean, float* __restrict__ rstd,
-                              float* __restrict__ run_mean, float* __restrict__ run_var, float* __restrict__ dgamma,
-                              float* __restrict__ dbeta, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s0 = 0.0, s1 = 0.0;
-    for (int b = 0; b < blocks; ++b) {
-        s0 += (double)part[(int64_t)b * 2 * C + c];
-        s1 += (double)part[(int64_t)b * 2 * C + C + c];
+// one workgroup per channel; double accumulation, fixed-order tree
+__global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ part, int blocks, int C, int64_t M,
+                                                    int mode, float eps, float momentum, float* __restrict__ mean,
+                                                    float* __restrict__ rstd, float* __restrict__ run_mean,
+                                                    float* __restrict__ run_var, float* __restrict__ dgamma,
+                                                    float* __restrict__ dbeta, int accumulate) {
+    __shared__ double r0[NT], r1[NT];
+    const int c = blockIdx.x;
+    double a0 = 0.0, a1 = 0.0;
+    for (int b = threadIdx.x; b < blocks; b += NT) {
+        a0 += (double)part[(int64_t)b * 2 * C + c];
+        a1 += (double)part[(int64_t)b * 2 * C + C + c];
     }
+    r0[threadIdx.x] = a0;
+    r1[threadIdx.x] = a1;
+    __syncthreads();
+    for (int o = NT / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            r0[threadIdx.x] += r0[threadIdx.x + o];
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const double s0 = r0[0], s1 = r1[0];
     if (mode == 0) {
         mean[c] = (float)(s0 / (double)M);
     } else if (mode == 1) {
@@ -334,13 +353,13 @@ int vt_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, int6
         else
             hipLaunchKernelGGL(k_ln_bwd<8>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
                                act, rpb, dx, ws);
-        hipLaunchKernelGGL(k_reduce_parts, dim3(blocks_for(2 * C)), dim3(256), 0, st, ws, (int)blocks, 2 * C, dgamma,
+        hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, ws, (int)blocks, 2 * C, dgamma,
                            dbeta, C, accumulate_params);
     } else {
         VT_CHECK_ARG(ws_floats >= 2 * R * C, "vt_layernorm_bwd: workspace too small (wide)");
         hipLaunchKernelGGL(k_ln_bwd_wide, dim3((unsigned)R), dim3(NT), 0, st, dy, xhat, rstd, C, gamma, beta, act, dx,
                            ws);
-        hipLaunchKernelGGL(k_reduce_parts, dim3(blocks_for(2 * C)), dim3(256), 0, st, ws, (int)R, 2 * C, dgamma, dbeta,
+        hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, ws, (int)R, 2 * C, dgamma, dbeta,
                            C, accumulate_params);
     }
     VT_LAUNCH_CHECK("vt_layernorm_bwd");
@@ -369,11 +388,11 @@ int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const
     hipStream_t st = S(stream);
     hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, nullptr, M, C, rpb, 0, nullptr, nullptr,
                        nullptr, nullptr, 0, ws);
-    hipLaunchKernelGGL(k_bn_finalize, dim3(blocks_for(C)), dim3(256), 0, st, ws, blocks, C, M, 0, eps, momentum, mean,
+    hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 0, eps, momentum, mean,
                        rstd, nullptr, nullptr, nullptr, nullptr, 0);
     hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, nullptr, M, C, rpb, 1, mean, nullptr, nullptr,
                        nullptr, 0, ws);
-    hipLaunchKernelGGL(k_bn_finalize, dim3(blocks_for(C)), dim3(256), 0, st, ws, blocks, C, M, 1, eps, momentum, mean,
+    hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 1, eps, momentum, mean,
                        rstd, run_mean, run_var, nullptr, nullptr, 0);
     hipLaunchKernelGGL(k_bn_apply, dim3(blocks_for(M * C)), dim3(256), 0, st, x, M, C, mean, rstd, gamma, beta, act, y);
     VT_LAUNCH_CHECK("vt_batchnorm_fwd");
@@ -393,11 +412,11 @@ int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const fl
     float* db_now = dg_now + C;
     hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, 2, mean, rstd, gamma, beta, act,
                        ws);
-    hipLaunchKernelGGL(k_bn_finalize, dim3(blocks_for(C)), dim3(256), 0, st, ws, blocks, C, M, 2, 0.f, 0.f, nullptr,
+    hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 2, 0.f, 0.f, nullptr,
                        nullptr, nullptr, nullptr, dg_now, db_now, 0);
     hipLaunchKernelGGL(k_bn_dx, dim3(blocks_for(M * C)), dim3(256), 0, st, dy, x, M, C, mean, rstd, gamma, beta, act,
                        dg_now, db_now, dx);
-    hipLaunchKernelGGL(k_reduce_parts, dim3(blocks_for(2 * C)), dim3(256), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
+    hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
                        accumulate_params);
     VT_LAUNCH_CHECK("vt_batchnorm_bwd");
     return VT_OK;

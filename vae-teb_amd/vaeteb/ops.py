@@ -33,7 +33,7 @@ class _Workspace:
 
 
 WS = _Workspace()
-WS_LINEAR = 1 << 24  # 64 MiB of split-K partials
+WS_LINEAR = 1 << 25  # 128 MiB of split-K partials (a 4096x4097 head gradient fits unsplit)
 
 
 def _st():
@@ -73,11 +73,13 @@ class LinearF(torch.autograd.Function):
             gx = torch.empty_like(x2)
             call("vt_linear_bwd_data", ptr(gy2), R, N, ptr(w), K, ptr(gx), 0, _st())
             gx = gx.reshape(ctx.shape)
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             gw = torch.empty_like(w)
+            gb = torch.empty(N, device=w.device) if want_b else None
             ws = WS.get(WS_LINEAR, w.device, 1)
-            call("vt_linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw), 0, ptr(ws), ws.numel(), _st())
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+            call("vt_linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw), ptr(gb), 0, ptr(ws), ws.numel(), _st())
+        elif want_b:
             gb = torch.empty(N, device=w.device)
             ws = WS.get(2048 * N, w.device, 2)
             call("vt_colsum", ptr(gy2), R, N, ptr(gb), 0, ptr(ws), ws.numel(), _st())
@@ -127,7 +129,7 @@ class ConvBNActF(torch.autograd.Function):
         x = x.contiguous()
         Lo = _lib.lib().fns["vt_conv1d_out_len"](L, K, mode, up)
         conv = torch.empty((B, Lo, Cout), device=x.device)
-        call("vt_conv1d_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(conv), _st())
+        call("vt_conv1d_direct_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(conv), _st())
         y = torch.empty_like(conv)
         mean = torch.empty(Cout, device=x.device)
         rstd = torch.empty(Cout, device=x.device)
@@ -155,12 +157,13 @@ class ConvBNActF(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             gpad = WS.get(B * (Lo + K - 1) * Cin, x.device, 3)
-            call("vt_conv1d_bwd_data", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gx), 0, ptr(gpad), _st())
+            call("vt_conv1d_direct_bwd_gpad", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gpad), _st())
+            call("vt_conv1d_fold", ptr(gpad), B, L, Cin, Cout, K, mode, up, ptr(gx), 0, _st())
         if ctx.needs_input_grad[1]:
             gw = torch.empty_like(w)
             ws1 = WS.get(WS_LINEAR, x.device, 1)
-            call("vt_conv1d_bwd_weight", ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(gw), 0, ptr(ws1),
-                 ws1.numel(), _st())
+            call("vt_conv1d_direct_bwd_weight", ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(gw), 0,
+                 ptr(ws1), ws1.numel(), _st())
         return gx, gw, gg, gb, None, None, None, None, None, None, None
 
 
@@ -214,9 +217,10 @@ class LSTMF(torch.autograd.Function):
             call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
             gw_ih, gw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
             gb = torch.empty_like(b_ih)
-            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(gw_ih), 0, ptr(ws), ws.numel(), _st())
-            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(gw_hh), 0, ptr(ws), ws.numel(), _st())
-            call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), 0, ptr(wsb), wsb.numel(), _st())
+            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(gw_ih), ptr(gb), 0, ptr(ws),
+                 ws.numel(), _st())
+            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(gw_hh), None, 0, ptr(ws), ws.numel(),
+                 _st())
             grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, gb, gb.clone()]
             if l > 0 or ctx.needs_input_grad[0]:
                 gin = torch.empty((B, S, In), device=gy.device)
