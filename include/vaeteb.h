@@ -40,11 +40,12 @@ int vt_abi_version(void);
  * Twiddle tables `tw`: float2[n], tw[k] = exp(-2*pi*i*k/n) computed in fp64 on
  * the host; an FFT of length n/stride reads it with that stride.            */
 
-/* Reflect-pad (to n_pad, pad_left on the left) + forward FFT of each row.
+/* Pad (to n_pad, pad_left on the left; pad_mode 0 reflect, 1 constant zero,
+ * 2 circular) + forward FFT of each row.
  * replaces: kymatio pad+rfft  ref/kymatio/kymatio/scattering1d/core/scattering1d.py:288-290,
- *           _pad_signal + fft ref/hdf5_dataset/kymatio_phase_scattering.py:222-223   */
-int vt_fe_spectrum(const float* x, int64_t rows, int N, int n_pad, int pad_left, const void* tw, void* xhat,
-                   void* stream);
+ *           _pad_signal + fft ref/hdf5_dataset/kymatio_phase_scattering.py:162-205,222-223 */
+int vt_fe_spectrum(const float* x, int64_t rows, int N, int n_pad, int pad_left, int pad_mode, const void* tw,
+                   void* xhat, void* stream);
 
 /* S0: phi-lowpass + 2^log2T decimation of the padded signal, as a short
  * correlation with h0 = ifft(phi_0) (even, radius taps each side).
@@ -65,13 +66,15 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
                   int step, int start, int S, float* s1, int s1_channels, void* stream);
 
 /* One workgroup per (sample b, pair p): c = |a_i| e^{i power*arg(a_i)} conj(a_j),
- * reflect-pad to n_pad, FFT, multiply bins [0, n_pad/dec) by phi0 (real),
- * inverse FFT of length n_pad/dec, out[b,p,m] = Re(.)[start+m], m < S.
+ * pad to n_pad (pad_mode as vt_fe_spectrum), FFT, multiply bins [0, n_pad/dec)
+ * by phi0 (real), inverse FFT of length n_pad/dec, out[b,p,m] = Re(.)[start+m],
+ * m < S.  dec == 0: no low-pass, out[b,p,i] = Re(c[i]), S == N
+ * (cross_phase_low_pass=False).
  * replaces: _compute_phase_correlation        kymatio_phase_scattering.py:275-301,
  *           _compute_cross_channel_phase_correlation :303-360, _apply_phi_filter :233-273 */
 int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
                 const int* slot_i, const int* slot_j, const float* power, const void* tw, const float* phi0, int dec,
-                int start, int S, float* out, void* stream);
+                int start, int S, int pad_mode, float* out, void* stream);
 
 /* Per-channel transform (kind 0 none, 1 log(max(x,0)+log_eps), 2 asinh) and
  * z-score (x-mean)/(std+1e-8); in[b, c, s] (batch stride in_C*S) -> out[b, s, out_off + c]

@@ -214,7 +214,13 @@ class PhaseFrontEnd:
         cross = (xi < 0.02)[ii] & ((xi >= 0.04) & (xi <= 0.5))[jj] & (pw >= 1) & (pw <= 32)
         return phase, cross
 
+    border_mode = "reflect"                                                          # :162-172
+
     def _reflect(self, x):                                                           # :174-205
+        if self.border_mode == "constant":
+            return np.pad(x, [(0, 0)] * (x.ndim - 1) + [(self.pl, self.pr)], mode="constant")
+        if self.border_mode == "circular":
+            return np.pad(x, [(0, 0)] * (x.ndim - 1) + [(self.pl, self.pr)], mode="wrap")
         left, right = self.pl, self.pr
         while left > 0:
             c = min(left, x.shape[-1] - 1)

@@ -24,7 +24,7 @@ def test_argument_errors_map_to_value_error():
     import pytest
     # shape validation happens before any device work, so this is safe without a GPU
     with pytest.raises(ValueError):
-        _lib.call("vt_fe_spectrum", None, 0, 4096, 8192, 2048, None, None, None)
+        _lib.call("vt_fe_spectrum", None, 0, 4096, 8192, 2048, 0, None, None, None)
     with pytest.raises(ValueError):
         _lib.call("vt_fft", None, None, 1, 12, 0, None, 1, None)   # not a power of two
 

@@ -69,4 +69,14 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
     return i < n ? i : p - i;
 }
 
+// Source index of padded position i (relative to the signal start) for the
+// front-end border modes of ref/hdf5_dataset/kymatio_phase_scattering.py:162-172:
+// 0 reflect (iterated), 1 constant zero (returns -1), 2 circular.
+__device__ __forceinline__ int pad_src(int i, int n, int mode) {
+    if (mode == 0) return reflect_idx(i, n);
+    if (mode == 1) return (i < 0 || i >= n) ? -1 : i;
+    i %= n;
+    return i < 0 ? i + n : i;
+}
+
 }  // namespace vt

@@ -34,14 +34,18 @@ static constexpr int FE_THREADS = 512;
 
 // ---------------------------------------------------------------- spectrum
 __global__ __launch_bounds__(FE_THREADS) void k_fe_spectrum(const float* __restrict__ x, int N, int n_pad,
-                                                            int pad_left, const float2* __restrict__ tw,
+                                                            int pad_left, int pad_mode,
+                                                            const float2* __restrict__ tw,
                                                             float2* __restrict__ xhat) {
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     float2* X = sm;
     float2* Y = sm + n_pad;
     const int64_t row = blockIdx.x;
     const float* xr = x + row * N;
-    for (int n = threadIdx.x; n < n_pad; n += blockDim.x) X[n] = make_float2(xr[reflect_idx(n - pad_left, N)], 0.f);
+    for (int n = threadIdx.x; n < n_pad; n += blockDim.x) {
+        const int s = pad_src(n - pad_left, N, pad_mode);
+        X[n] = make_float2(s < 0 ? 0.f : xr[s], 0.f);
+    }
     __syncthreads();
     float2* R = fft_lds<false>(X, Y, n_pad, tw, 1);
     float2* o = xhat + row * n_pad;
@@ -121,7 +125,7 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_wavelet(
 __global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
     const float2* __restrict__ analytic, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
     const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
-    const float2* __restrict__ tw, const float* __restrict__ phi0, int dec, int start, int S,
+    const float2* __restrict__ tw, const float* __restrict__ phi0, int dec, int start, int S, int pad_mode,
     float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     float2* X = sm;
@@ -131,6 +135,7 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
     const float2* ai = analytic + (b * n_slots + slot_i[pair]) * (int64_t)N;
     const float2* aj = analytic + (b * n_slots + slot_j[pair]) * (int64_t)N;
     const float pw = power[pair];
+    float* o = out + (b * n_pairs + pair) * (int64_t)S;
     // accelerated product (kymatio_phase_scattering.py:211-218, :282-283)
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
         const float2 u = ai[i], v = aj[i];
@@ -140,9 +145,14 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
         sincosf(ph, &sn, &cs);
         const float2 acc = make_float2(mag * cs, mag * sn);
         Y[i] = cmul(acc, cconj(v));
+        if (dec == 0) o[i] = Y[i].x;  // cross_phase_low_pass=False (:356-360): raw real part
     }
+    if (dec == 0) return;
     __syncthreads();
-    for (int n = threadIdx.x; n < n_pad; n += blockDim.x) X[n] = Y[reflect_idx(n - pad_left, N)];
+    for (int n = threadIdx.x; n < n_pad; n += blockDim.x) {
+        const int s = pad_src(n - pad_left, N, pad_mode);
+        X[n] = s < 0 ? make_float2(0.f, 0.f) : Y[s];
+    }
     __syncthreads();
     float2* R = fft_lds<false>(X, Y, n_pad, tw, 1);
     float2* Z = (R == X) ? Y : X;
@@ -151,7 +161,6 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
     __syncthreads();
     float2* Rs = fft_lds<true>(Z, R, nb, tw, dec);
     const float inv = 1.0f / (float)nb;
-    float* o = out + (b * n_pairs + pair) * (int64_t)S;
     for (int m = threadIdx.x; m < S; m += blockDim.x) o[m] = Rs[start + m].x * inv;
 }
 
@@ -252,12 +261,12 @@ using namespace vt;
 
 extern "C" {
 
-int vt_fe_spectrum(const float* x, int64_t rows, int N, int n_pad, int pad_left, const void* tw, void* xhat,
-                   void* stream) {
+int vt_fe_spectrum(const float* x, int64_t rows, int N, int n_pad, int pad_left, int pad_mode, const void* tw,
+                   void* xhat, void* stream) {
     VT_CHECK_ARG(pow2(n_pad) && n_pad <= VT_FFT_MAX_LDS && n_pad >= N, "vt_fe_spectrum: n_pad=%d", n_pad);
-    VT_CHECK_ARG(rows > 0 && N > 1, "vt_fe_spectrum: rows/N");
+    VT_CHECK_ARG(rows > 0 && N > 1 && pad_mode >= 0 && pad_mode <= 2, "vt_fe_spectrum: rows/N/pad_mode");
     hipLaunchKernelGGL(k_fe_spectrum, dim3((unsigned)rows), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream), x, N,
-                       n_pad, pad_left, (const float2*)tw, (float2*)xhat);
+                       n_pad, pad_left, pad_mode, (const float2*)tw, (float2*)xhat);
     VT_LAUNCH_CHECK("vt_fe_spectrum");
     return VT_OK;
 }
@@ -288,13 +297,14 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
 
 int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
                 const int* slot_i, const int* slot_j, const float* power, const void* tw, const float* phi0, int dec,
-                int start, int S_out, float* out, void* stream) {
+                int start, int S_out, int pad_mode, float* out, void* stream) {
     VT_CHECK_ARG(pow2(n_pad) && n_pad <= VT_FFT_MAX_LDS, "vt_fe_pairs: n_pad=%d", n_pad);
-    VT_CHECK_ARG(dec >= 1 && pow2(dec) && n_pad / dec >= start + S_out, "vt_fe_pairs: dec/start");
-    VT_CHECK_ARG(B > 0 && n_pairs > 0, "vt_fe_pairs: empty");
+    VT_CHECK_ARG(dec == 0 ? S_out == N : (dec >= 1 && pow2(dec) && n_pad / dec >= start + S_out),
+                 "vt_fe_pairs: dec/start (decimation must be a power of two)");
+    VT_CHECK_ARG(B > 0 && n_pairs > 0 && pad_mode >= 0 && pad_mode <= 2, "vt_fe_pairs: empty/pad_mode");
     hipLaunchKernelGGL(k_fe_pairs, dim3(n_pairs, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
                        (const float2*)analytic, n_slots, N, n_pad, pad_left, n_pairs, slot_i, slot_j, power,
-                       (const float2*)tw, phi0, dec, start, S_out, out);
+                       (const float2*)tw, phi0, dec, start, S_out, pad_mode, out);
     VT_LAUNCH_CHECK("vt_fe_pairs");
     return VT_OK;
 }

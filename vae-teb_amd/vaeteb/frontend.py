@@ -130,6 +130,39 @@ class FrontEndPlan:
                     slot_i=_i32(pi, dev), slot_j=_i32(pj, dev), power=_f32(pw, dev), n_pairs=len(pi))
 
 
+PAD_MODES = {"reflect": 0, "constant": 1, "circular": 2}
+
+
+def launch_spectrum(p, x, rows, pad_mode, xhat):
+    """rows of x (each p.N long, contiguous) -> padded spectra xhat (rows, n_pad) complex."""
+    _lib.call("vt_fe_spectrum", _lib.ptr(x), rows, p.N, p.n_pad, p.pad_left, pad_mode, _lib.ptr(p.t_tw),
+              _lib.ptr(xhat), _lib.stream())
+
+
+def launch_lowpass(p, x, rows, x_row_stride, out, out_row_stride):
+    """S0 (order-0 scattering) of each row, written at out[row * out_row_stride + m]."""
+    _lib.call("vt_fe_lowpass", _lib.ptr(x), rows, x_row_stride, p.N, p.n_pad, p.pad_left, _lib.ptr(p.t_h0), p.radius,
+              p.step, p.start, p.S, out.data_ptr(), out_row_stride, _lib.stream())
+
+
+def launch_wavelet(p, xhat, B, C, tab, analytic, s1, s1_channels):
+    _lib.call("vt_fe_wavelet", _lib.ptr(xhat), B, C, p.n_pad, _lib.ptr(p.t_psi), tab["n_items"], _lib.ptr(tab["items"]),
+              _lib.ptr(p.t_tw), p.N, p.pad_left, _lib.ptr(analytic) if analytic is not None else None,
+              max(tab["n_slots"], 1), _lib.ptr(p.t_h0), p.radius, p.step, p.start, p.S,
+              _lib.ptr(s1) if s1 is not None else None, s1_channels, _lib.stream())
+
+
+def launch_pairs(p, analytic, B, tab, out, lowpass=True, pad_mode=0):
+    if lowpass:
+        _lib.call("vt_fe_pairs", _lib.ptr(analytic), B, tab["n_slots"], p.N, p.n_pad, p.pad_left, tab["n_pairs"],
+                  _lib.ptr(tab["slot_i"]), _lib.ptr(tab["slot_j"]), _lib.ptr(tab["power"]), _lib.ptr(p.t_tw),
+                  _lib.ptr(p.t_phi_crop), p.dec, p.pair_start, p.pair_len, pad_mode, _lib.ptr(out), _lib.stream())
+    else:
+        _lib.call("vt_fe_pairs", _lib.ptr(analytic), B, tab["n_slots"], p.N, p.n_pad, p.pad_left, tab["n_pairs"],
+                  _lib.ptr(tab["slot_i"]), _lib.ptr(tab["slot_j"]), _lib.ptr(tab["power"]), _lib.ptr(p.t_tw),
+                  _lib.ptr(p.t_phi_crop), 0, 0, p.N, pad_mode, _lib.ptr(out), _lib.stream())
+
+
 class FrontEnd:
     """Fused training-step front-end: raw windows -> normalised model inputs."""
 
@@ -176,18 +209,13 @@ class FrontEnd:
         B = x.shape[0]
         st = _lib.stream()
         xhat = self._buf("xhat", (B, 2, p.n_pad, 2))
-        _lib.call("vt_fe_spectrum", _lib.ptr(x), B * 2, p.N, p.n_pad, p.pad_left, _lib.ptr(p.t_tw), _lib.ptr(xhat), st)
+        launch_spectrum(p, x, B * 2, 0, xhat)
         s_raw = self._buf("s_raw", (B, self.C_st, p.S))
-        _lib.call("vt_fe_lowpass", _lib.ptr(x), B, 2 * p.N, p.N, p.n_pad, p.pad_left, _lib.ptr(p.t_h0), p.radius,
-                  p.step, p.start, p.S, _lib.ptr(s_raw), self.C_st * p.S, st)
+        launch_lowpass(p, x, B, 2 * p.N, s_raw, self.C_st * p.S)
         an = self._buf("analytic", (B, t["n_slots"], p.N, 2))
-        _lib.call("vt_fe_wavelet", _lib.ptr(xhat), B, 2, p.n_pad, _lib.ptr(p.t_psi), t["n_items"], _lib.ptr(t["items"]),
-                  _lib.ptr(p.t_tw), p.N, p.pad_left, _lib.ptr(an), t["n_slots"], _lib.ptr(p.t_h0), p.radius, p.step,
-                  p.start, p.S, _lib.ptr(s_raw), self.C_st, st)
+        launch_wavelet(p, xhat, B, 2, t, an, s_raw, self.C_st)
         pr = self._buf("pairs", (B, t["n_pairs"], p.pair_len))
-        _lib.call("vt_fe_pairs", _lib.ptr(an), B, t["n_slots"], p.N, p.n_pad, p.pad_left, t["n_pairs"],
-                  _lib.ptr(t["slot_i"]), _lib.ptr(t["slot_j"]), _lib.ptr(t["power"]), _lib.ptr(p.t_tw),
-                  _lib.ptr(p.t_phi_crop), p.dec, p.pair_start, p.pair_len, _lib.ptr(pr), st)
+        launch_pairs(p, an, B, t, pr, lowpass=True, pad_mode=0)
         return {"fhr_st": s_raw, "pairs": pr}
 
     def __call__(self, x, out=None):
@@ -226,3 +254,128 @@ def load_stats(J=11, Q=4, T=16, N=4096):
     import os
     path = os.path.join(os.path.dirname(__file__), "data", f"stats_j{J}q{Q}t{T}_n{N}.npz")
     return dict(np.load(path, allow_pickle=False))
+
+
+class KymatioPhaseScattering1D(torch.nn.Module):
+    """Drop-in for ref/hdf5_dataset/kymatio_phase_scattering.py:11-811 (module
+    API: constructor, forward, masks, selection helpers) on the HIP kernels.
+    forward() returns the reference's dict: 'scattering' (B, 1+F, S) and
+    'phase_corr' or 'cross_phase_corr' (B, 903, S) over all pairs, plus
+    'autoc_idx'.  The fused training path (FrontEnd) computes only the selected
+    pairs; this class exists for code written against the reference module."""
+
+    def __init__(self, J, Q, T, shape, device=None, oversampling=0, max_order=2, border_mode="reflect",
+                 tukey_alpha=None):
+        super().__init__()
+        if isinstance(Q, tuple):
+            self.Q_scattering, self.Q = Q, Q[0]
+        else:
+            self.Q_scattering = self.Q = Q
+        self.J, self.T, self.oversampling, self.max_order = J, T, oversampling, max_order
+        self.border_mode, self.tukey_alpha = border_mode, tukey_alpha
+        self.device = device if device is not None else torch.device("cuda")
+        self.eps = 1e-14
+        self.N = int(shape) if isinstance(shape, (int, float)) else int(shape[0])
+        from .scattering import Scattering1D
+        self.scattering = Scattering1D(J=J, shape=self.N, Q=self.Q, max_order=max_order, average=True,
+                                       oversampling=oversampling, vectorize=True, out_type="array", T=T)
+        self.plan = FrontEndPlan(J, self.Q, T, self.N, device=self.device)
+        p = self.plan
+        self.J_pad, self.pad_left, self.pad_right, self.N_padded = p.pad.J_pad, p.pad_left, p.pad_right, p.n_pad
+        self.ind_start, self.ind_end = p.pad.ind_start, p.pad.ind_end
+        self.center_freqs = torch.from_numpy(p.center_freqs).to(self.device)
+        self.i_idx = torch.from_numpy(p.i_idx).to(self.device)
+        self.j_idx = torch.from_numpy(p.j_idx).to(self.device)
+        self.powers = torch.from_numpy(p.powers).to(self.device)
+        self.autoc_idx = torch.from_numpy(p.autoc_idx).to(self.device)
+
+    # ------------------------------------------------------------ selection
+    def get_optimal_coefficients_for_fhr(self, j_config=11, q_config=4, t_config=16):
+        """Masks of :635-760 (returned in the reference's dict structure, core keys)."""
+        phase, cross = self.plan.fhr_masks()
+        pm = torch.from_numpy(phase).to(self.device)
+        cm = torch.from_numpy(cross).to(self.device)
+        return {"phase_selection": {"optimal_mask": pm}, "cross_selection": {"cross_mask": cm},
+                "recommendations": {"use_phase_mask": pm, "use_cross_mask": cm,
+                                    "total_selected_features": j_config * q_config + 1 + int(pm.sum()) + int(cm.sum())}}
+
+    # ------------------------------------------------------------ forward
+    def _tukey(self, x):
+        a, n = self.tukey_alpha, x.shape[-1]
+        if a is None or not (0 < a <= 1):
+            return x
+        if a >= 1.0:
+            w = torch.hann_window(n, periodic=False, device=x.device)
+        else:
+            tl = int(a * (n - 1) / 2.0)
+            if tl == 0:
+                return x
+            taper = torch.hann_window(2 * tl, periodic=False, device=x.device)
+            w = torch.ones(n, device=x.device)
+            w[:tl] = taper[:tl]
+            w[n - tl:] = taper[tl:]
+        return x * w
+
+    def forward(self, x, compute_phase=True, compute_cross_phase=False, cross_phase_same_pairs_only=False,
+                cross_phase_low_pass=True, scattering_channel=0, phase_channels=None):
+        x = x.to(self.device).float()
+        if self.tukey_alpha is not None:
+            x = self._tukey(x)
+        if x.dim() == 3:
+            B, C, N = x.shape
+            if scattering_channel >= C:
+                raise ValueError(f"scattering_channel {scattering_channel} >= {C}")
+            s_in = x[:, scattering_channel, :].contiguous()
+            if compute_cross_phase:
+                if phase_channels is None:
+                    if C < 2:
+                        raise ValueError("Cross-channel correlation requires at least 2 channels")
+                    phase_channels = [0, 1]
+                if len(phase_channels) != 2 or any(ch >= C for ch in phase_channels):
+                    raise ValueError("Invalid phase_channels for cross-channel correlation")
+                ph = x[:, phase_channels, :].contiguous()
+            elif phase_channels is not None:
+                if len(phase_channels) != 1:
+                    raise ValueError("Single-channel phase correlation requires exactly 1 channel")
+                if phase_channels[0] >= C:
+                    raise ValueError(f"phase_channel {phase_channels[0]} >= {C}")
+                ph = x[:, phase_channels[0], :].contiguous()
+            else:
+                ph = s_in
+        elif x.dim() == 2:
+            if scattering_channel != 0:
+                raise ValueError("scattering_channel must be 0 for single-channel input")
+            if compute_cross_phase:
+                raise ValueError("Cross-channel correlation requires multi-channel input")
+            s_in, ph = x.contiguous(), (x.contiguous() if compute_phase else None)
+        else:
+            raise ValueError(f"Input must be 2D or 3D, got shape {x.shape}")
+        S, _ = self.scattering(s_in)
+        res = {"scattering": S}
+        if S.shape[-1] == 0:
+            raise ValueError(f"Scattering output has zero temporal dimension: {S.shape}")
+        if (compute_phase or compute_cross_phase) and ph is not None:
+            if ph.dim() == 2:
+                ph = ph.unsqueeze(1)
+            if compute_cross_phase and ph.shape[1] != 2:
+                raise ValueError("Cross-channel correlation requires exactly 2 channels")
+            p = self.plan
+            B, C = ph.shape[0], ph.shape[1]
+            if compute_cross_phase:
+                sel = self.autoc_idx.cpu().numpy() if cross_phase_same_pairs_only else np.arange(len(p.i_idx))
+                tab = p.tables([], sel, scattering=False)
+            else:
+                tab = p.tables(np.arange(len(p.i_idx)), [], scattering=False)
+            pm = PAD_MODES.get(self.border_mode)
+            if pm is None:
+                raise ValueError(f"Unsupported border_mode: {self.border_mode}")
+            xhat = torch.empty((B, C, p.n_pad, 2), device=x.device)
+            launch_spectrum(p, ph, B * C, pm, xhat)
+            an = torch.empty((B, tab["n_slots"], p.N, 2), device=x.device)
+            launch_wavelet(p, xhat, B, C, tab, an, None, 0)
+            low = (not compute_cross_phase) or cross_phase_low_pass
+            out = torch.empty((B, tab["n_pairs"], p.pair_len if low else p.N), device=x.device)
+            launch_pairs(p, an, B, tab, out, lowpass=low, pad_mode=pm)
+            res["cross_phase_corr" if compute_cross_phase else "phase_corr"] = out
+            res["autoc_idx"] = self.autoc_idx
+        return res

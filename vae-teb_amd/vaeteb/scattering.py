@@ -1,0 +1,370 @@
+"""kymatio-compatible Scattering1D on MI355X and the `torch_hip` backend plugin.
+
+Two entry points mirror the reference's plugin API:
+
+* `TorchHipBackend1D` — a kymatio backend (name 'torch_hip', accepted by
+  kymatio's frontend check `backend.name.startswith('torch')`,
+  ref/kymatio/kymatio/frontend/base_frontend.py:16-34) whose classmethods
+  (pad, unpad, rfft, irfft, fft, ifft, cdgmm, modulus, subsample_fourier,
+  concatenate, ...) keep the trailing-dim-2 complex convention, the checks and
+  the error messages of ref/kymatio/kymatio/scattering1d/backend/torch_backend.py:17-174
+  and ref/kymatio/kymatio/backend/torch_backend.py:99-219, with the compute
+  in HIP kernels.  It can be handed to the reference's own kymatio
+  `Scattering1D(..., backend=TorchHipBackend1D)`.
+* `Scattering1D` — the frontend (ref/kymatio/kymatio/scattering1d/frontend/torch_frontend.py:10-255):
+  same constructor and `[S, S]` return.  The averaged first-order,
+  oversampling-0 case (the one the VAE-TEB front-end uses) runs the fused
+  kernels of vaeteb.frontend; everything else runs the generic scattering
+  core below over the HIP backend plugin.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .filter_bank import build_bank, padding, twiddles
+
+
+# ------------------------------------------------------------------ backend
+_TW = {}
+
+
+def _tw(n, device):
+    key = (n, str(device))
+    if key not in _TW:
+        _TW[key] = torch.from_numpy(twiddles(n)).to(device)
+    return _TW[key]
+
+
+class _ModulusStable(torch.autograd.Function):
+    """ModulusStable (ref/kymatio/kymatio/backend/torch_backend.py:5-96) on HIP."""
+
+    @staticmethod
+    def forward(ctx, x):
+        out = torch.empty(x.shape[:-1], dtype=x.dtype, device=x.device)
+        _lib.call("vt_modulus", _lib.ptr(x), _lib.ptr(out), out.numel(), _lib.stream())
+        ctx.save_for_backward(x, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, out = ctx.saved_tensors
+        gi = torch.empty_like(x)
+        _lib.call("vt_modulus_bwd", _lib.ptr(x), _lib.ptr(out), _lib.ptr(g.contiguous()), _lib.ptr(gi), out.numel(),
+                  _lib.stream())
+        return gi
+
+
+class TorchHipBackend1D:
+    name = "torch_hip"
+
+    # --- checks (same messages as the reference backend)
+    @classmethod
+    def input_checks(cls, x):
+        if x is None:
+            raise TypeError("The input should be not empty.")
+        cls.contiguous_check(x)
+
+    @staticmethod
+    def contiguous_check(x):
+        if not x.is_contiguous():
+            raise RuntimeError("Tensors must be contiguous.")
+
+    @staticmethod
+    def _is_complex(x):
+        return x.shape[-1] == 2
+
+    @staticmethod
+    def _is_real(x):
+        return x.shape[-1] == 1
+
+    @classmethod
+    def complex_check(cls, x):
+        if not cls._is_complex(x):
+            raise TypeError("The input should be complex (i.e. last dimension is 2).")
+
+    @classmethod
+    def real_check(cls, x):
+        if not cls._is_real(x):
+            raise TypeError("The input should be real.")
+
+    @classmethod
+    def complex_contiguous_check(cls, x):
+        cls.complex_check(x)
+        cls.contiguous_check(x)
+
+    @staticmethod
+    def _device_check(x):
+        if not x.is_cuda:
+            raise TypeError("Input must be on GPU.")
+
+    # --- ops
+    @classmethod
+    def modulus(cls, x):
+        cls.complex_contiguous_check(x)
+        return _ModulusStable.apply(x)[..., None]
+
+    @staticmethod
+    def concatenate(arrays, dim=2):
+        return torch.stack(arrays, dim=dim)
+
+    @staticmethod
+    def reshape(x, shape):
+        return x.reshape(shape)
+
+    @classmethod
+    def cdgmm(cls, A, B):
+        if not cls._is_real(B):
+            cls.complex_contiguous_check(B)
+        else:
+            cls.contiguous_check(B)
+        cls.complex_contiguous_check(A)
+        if A.shape[-len(B.shape):-1] != B.shape[:-1]:
+            raise RuntimeError("The filters are not compatible for multiplication.")
+        if A.dtype is not B.dtype:
+            raise TypeError("Input and filter must be of the same dtype.")
+        if B.is_cuda and (not A.is_cuda or A.device.index != B.device.index):
+            raise TypeError("Input and filter must be on the same GPU." if A.is_cuda else "Input must be on GPU.")
+        if not B.is_cuda and A.is_cuda:
+            raise TypeError("Input must be on CPU.")
+        cls._device_check(A)
+        n = B.numel() // B.shape[-1]
+        C = torch.empty_like(A)
+        _lib.call("vt_cdgmm", _lib.ptr(A), _lib.ptr(B), int(cls._is_real(B)), _lib.ptr(C), A.numel() // (2 * n), n,
+                  _lib.stream())
+        return C
+
+    @classmethod
+    def subsample_fourier(cls, x, k):
+        cls.complex_check(x)
+        cls._device_check(x)
+        x = x.contiguous()
+        N = x.shape[-2]
+        out = torch.empty(x.shape[:-2] + (N // k, 2), dtype=x.dtype, device=x.device)
+        _lib.call("vt_subsample_fourier", _lib.ptr(x), _lib.ptr(out), x.numel() // (2 * N), N, k, _lib.stream())
+        return out
+
+    @staticmethod
+    def pad(x, pad_left, pad_right):
+        if (pad_left >= x.shape[-1]) or (pad_right >= x.shape[-1]):
+            raise ValueError("Indefinite padding size (larger than tensor).")
+        x = x.contiguous()
+        N = x.shape[-1]
+        out = torch.empty(x.shape[:-1] + (N + pad_left + pad_right,), dtype=x.dtype, device=x.device)
+        _lib.call("vt_pad_reflect", _lib.ptr(x), _lib.ptr(out), x.numel() // N, N, pad_left, pad_right, _lib.stream())
+        return out[..., None]
+
+    @staticmethod
+    def unpad(x, i0, i1):
+        x = x.reshape(x.shape[:-1])
+        return x[..., i0:i1]
+
+    @classmethod
+    def _fft(cls, x, inverse):
+        cls._device_check(x)
+        n = x.shape[-2]
+        if n > _lib_max_fft():
+            raise ValueError(f"torch_hip backend: FFT length {n} exceeds the LDS-resident limit {_lib_max_fft()}")
+        out = torch.empty_like(x)
+        _lib.call("vt_fft", _lib.ptr(x), _lib.ptr(out), x.numel() // (2 * n), n, int(inverse), _lib.ptr(_tw(n, x.device)),
+                  1, _lib.stream())
+        return out
+
+    @classmethod
+    def rfft(cls, x):
+        cls.contiguous_check(x)
+        cls.real_check(x)
+        x_r = torch.zeros(x.shape[:-1] + (2,), dtype=x.dtype, device=x.device)
+        x_r[..., 0] = x[..., 0]
+        return cls._fft(x_r, False)
+
+    @classmethod
+    def irfft(cls, x):
+        cls.contiguous_check(x)
+        cls.complex_check(x)
+        return cls._fft(x, True)[..., :1].contiguous()
+
+    @classmethod
+    def ifft(cls, x):
+        cls.contiguous_check(x)
+        cls.complex_check(x)
+        return cls._fft(x, True)
+
+    @classmethod
+    def fft(cls, x):
+        cls.contiguous_check(x)
+        cls.complex_check(x)
+        return cls._fft(x, False)
+
+    @staticmethod
+    def multiply(x, y):
+        return torch.multiply(x, y)
+
+    @classmethod
+    def to_polar(cls, x):
+        cls.complex_check(x)
+        mag = cls.modulus(x)
+        phase = torch.atan2(x[..., 1:2], x[..., 0:1])
+        return mag, phase
+
+    @classmethod
+    def to_cartesian(cls, mag, phase):
+        return torch.cat((torch.cos(phase) * mag, torch.sin(phase) * mag), -1)
+
+
+def _lib_max_fft():
+    return 8192
+
+
+backend = TorchHipBackend1D
+
+
+# ------------------------------------------------------------- generic core
+def scattering1d_core(x, bk, J, T, psi1, psi2, phi, pad_left, pad_right, ind_start, ind_end, oversampling=0,
+                      max_order=2, average=True, vectorize=True, out_type="array"):
+    """The scattering cascade of ref/kymatio/kymatio/scattering1d/core/scattering1d.py:197-399
+    written against a backend object (here the HIP plugin)."""
+    U0h = bk.rfft(bk.pad(x, pad_left=pad_left, pad_right=pad_right))
+    lt = int(math.floor(math.log2(T)))
+    k0 = max(lt - oversampling, 0)
+    s0 = bk.unpad(bk.irfft(bk.subsample_fourier(bk.cdgmm(U0h, phi["levels"][0]), 2 ** k0)), ind_start[k0],
+                  ind_end[k0]) if average else x
+    out = [{"coef": s0, "j": (), "n": ()}]
+    out2 = []
+    for n1, p1 in enumerate(psi1):
+        j1 = p1["j"]
+        k1 = max(min(j1 - oversampling, lt - oversampling), 0)
+        U1c = bk.ifft(bk.subsample_fourier(bk.cdgmm(U0h, p1["levels"][0]), 2 ** k1))
+        U1m = bk.modulus(U1c)
+        U1h = bk.rfft(U1m) if (average or max_order > 1) else None
+        if average:
+            k1J = max(lt - k1 - oversampling, 0)
+            s1 = bk.unpad(bk.irfft(bk.subsample_fourier(bk.cdgmm(U1h, phi["levels"][k1]), 2 ** k1J)),
+                          ind_start[k1J + k1], ind_end[k1J + k1])
+        else:
+            s1 = bk.unpad(U1m, ind_start[k1], ind_end[k1])
+        out.append({"coef": s1, "j": (j1,), "n": (n1,)})
+        if max_order == 2:
+            for n2, p2 in enumerate(psi2):
+                j2 = p2["j"]
+                if j2 <= j1:
+                    continue
+                k2 = max(min(j2 - k1 - oversampling, lt - k1 - oversampling), 0)
+                U2m = bk.modulus(bk.ifft(bk.subsample_fourier(bk.cdgmm(U1h, p2["levels"][k1]), 2 ** k2)))
+                if average:
+                    k2J = max(lt - k2 - k1 - oversampling, 0)
+                    s2 = bk.unpad(bk.irfft(bk.subsample_fourier(bk.cdgmm(bk.rfft(U2m), phi["levels"][k1 + k2]),
+                                                                2 ** k2J)),
+                                  ind_start[k1 + k2 + k2J], ind_end[k1 + k2 + k2J])
+                else:
+                    s2 = bk.unpad(U2m, ind_start[k1 + k2], ind_end[k1 + k2])
+                out2.append({"coef": s2, "j": (j1, j2), "n": (n1, n2)})
+    out += out2
+    if out_type == "array" and vectorize:
+        return bk.concatenate([o["coef"] for o in out])
+    if out_type == "array":
+        return {o["n"]: o["coef"] for o in out}
+    for o in out:
+        o.pop("n")
+    return out
+
+
+# ------------------------------------------------------------------ frontend
+class Scattering1D(nn.Module):
+    """Drop-in for kymatio's (locally modified) ScatteringTorch1D: forward(x)
+    returns [S, S] (ref/kymatio/kymatio/scattering1d/frontend/torch_frontend.py:163-255)."""
+
+    def __init__(self, J, shape, Q=1, max_order=2, average=True, oversampling=0, vectorize=True, out_type="array",
+                 backend="torch_hip", T=None):
+        super().__init__()
+        if backend not in ("torch_hip", TorchHipBackend1D):
+            raise ImportError("Backend " + str(backend) + " not found!")
+        self.backend = TorchHipBackend1D
+        self.J, self.Q, self.max_order, self.average = J, Q, max_order, average
+        self.oversampling, self.vectorize, self.out_type = oversampling, vectorize, out_type
+        if isinstance(shape, int):
+            self.N = shape
+        elif isinstance(shape, tuple):
+            if len(shape) > 1:
+                raise ValueError("If shape is specified as a tuple, it must have exactly one element")
+            self.N = shape[0]
+        else:
+            raise ValueError("shape must be an integer or a 1-tuple")
+        # T=None: kymatio's documented default 2**J (the reference build() sets it,
+        # then its torch frontend resets it to None and crashes)
+        self.T = 2 ** J if T is None else T
+        if self.T > 2 ** J:
+            raise ValueError("The temporal support T of the low-pass filter cannot exceed 2**J (got {} > {})".format(
+                self.T, 2 ** J))
+        pd = padding(self.N, J, Q, self.T)
+        self.J_pad, self.pad_left, self.pad_right = pd.J_pad, pd.pad_left, pd.pad_right
+        self.ind_start, self.ind_end = pd.ind_start, pd.ind_end
+        bank = build_bank(self.J_pad, J, Q, self.T)
+        self._bank = bank
+        self._tables = None
+        self._fused = None
+
+    def _device_tables(self, device):
+        if self._tables is None or self._tables[0] != str(device):
+            f = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).view(-1, 1).to(device)
+            b = self._bank
+            phi = {"levels": [f(l) for l in b.phi_levels]}
+            psi1 = [{"levels": [f(b.psi1[i])], "xi": b.xi1[i], "j": int(b.j1[i])} for i in range(len(b.xi1))]
+            psi2 = [{"levels": [f(l) for l in b.psi2_levels[i]], "xi": b.xi2[i], "j": int(b.j2[i])}
+                    for i in range(len(b.xi2))]
+            self._tables = (str(device), phi, psi1, psi2)
+        return self._tables[1:]
+
+    def _fused_ok(self):
+        return (self.max_order == 1 and self.average and self.oversampling == 0 and self.vectorize
+                and self.out_type == "array" and 2 ** self.J_pad <= 8192)
+
+    def meta(self):
+        raise NotImplementedError("meta() is outside the training path")
+
+    def scattering(self, x):
+        if len(x.shape) < 1:
+            raise ValueError("Input tensor x should have at least one axis, got {}".format(len(x.shape)))
+        if self.out_type not in ("array", "list"):
+            raise RuntimeError("The out_type must be one of 'array' or 'list'.")
+        if not self.average and self.out_type == "array" and self.vectorize:
+            raise ValueError("Options average=False, out_type='array' and vectorize=True are mutually incompatible. "
+                             "Please set out_type to 'list' or vectorize to False.")
+        batch_shape = x.shape[:-1]
+        x2 = x.reshape((-1, x.shape[-1])).contiguous()
+        if self._fused_ok():
+            S = self._fused_forward(x2)
+        else:
+            phi, psi1, psi2 = self._device_tables(x.device)
+            S = scattering1d_core(x2.reshape(-1, 1, x.shape[-1]), self.backend, self.J, self.T, psi1, psi2, phi,
+                                  self.pad_left, self.pad_right, self.ind_start, self.ind_end, self.oversampling,
+                                  self.max_order, self.average, self.vectorize, self.out_type)
+        if self.out_type == "array" and self.vectorize:
+            S = S.reshape(batch_shape + S.shape[-2:])
+        elif self.out_type == "array":
+            S = {k: v.reshape(batch_shape + v.shape[-2:]) for k, v in S.items()}
+        else:
+            for o in S:
+                o["coef"] = o["coef"].reshape(batch_shape + o["coef"].shape[-1:])
+        return [S, S]
+
+    def _fused_forward(self, x2):
+        from .frontend import FrontEndPlan, launch_lowpass, launch_spectrum, launch_wavelet
+        if self._fused is None or self._fused[0].device != x2.device:
+            plan = FrontEndPlan(self.J, self.Q, self.T, self.N, device=x2.device)
+            self._fused = (plan, plan.tables([], [], scattering=True))
+        plan, tab = self._fused
+        B = x2.shape[0]
+        C = 1 + plan.n_filters
+        xhat = torch.empty((B, plan.n_pad, 2), device=x2.device)
+        launch_spectrum(plan, x2, B, 0, xhat)
+        S = torch.empty((B, C, plan.S), device=x2.device)
+        launch_lowpass(plan, x2, B, plan.N, S, C * plan.S)
+        launch_wavelet(plan, xhat, B, 1, tab, None, S, C)
+        return S
+
+    def forward(self, x):
+        self.backend.input_checks(x)
+        return self.scattering(x)
