@@ -39,28 +39,44 @@ FRONTENDS = {"j11": (11, 4, 16), "j6": (6, 1, 16)}
 
 
 class KernelTimer:
-    """HIP events around every launch of one named C-ABI entry point, recorded
-    on the stream the kernel is launched on (the current stream)."""
+    """HIP events around every launch of the named C-ABI entry points, recorded
+    on the stream the kernels are launched on (the current stream); `flops`
+    maps a name to a function of the call's arguments (MFMA accounting)."""
 
-    def __init__(self, name):
-        self.name, self.pairs, self.enabled = name, [], False
+    def __init__(self, names, flops=None):
+        self.names, self.pairs, self.enabled = set(names), {n: [] for n in names}, False
+        self.flops, self.total_flops = flops or {}, {n: 0 for n in names}
         lib = _lib.lib()
         self._orig = lib.call
 
         def call(fname, *args):
-            if self.enabled and fname == self.name:
+            if self.enabled and fname in self.names:
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 rc = self._orig(fname, *args)
                 e.record()
-                self.pairs.append((s, e))
+                self.pairs[fname].append((s, e))
+                if fname in self.flops:
+                    self.total_flops[fname] += self.flops[fname](*args)
                 return rc
             return self._orig(fname, *args)
         lib.call = call
 
-    def mean_ms(self):
-        ts = [s.elapsed_time(e) for s, e in self.pairs]
+    def mean_ms(self, name):
+        ts = [s.elapsed_time(e) for s, e in self.pairs[name]]
         return sum(ts) / len(ts) if ts else float("nan"), len(ts)
+
+    def total_ms(self, names):
+        return sum(s.elapsed_time(e) for n in names for s, e in self.pairs[n])
+
+
+# bf16 MFMA head GEMMs: 2*R*K*N flops per call (arguments as in include/vaeteb.h)
+MFMA_CALLS = {
+    "vt_mfma_linear_fwd": lambda X, R, K, W, N, *a: 2 * R * K * N,
+    "vt_mfma_linear_bwd_data": lambda dY, R, N, W, K, *a: 2 * R * K * N,
+    "vt_mfma_linear_bwd_weight": lambda dY, R, N, X, K, *a: 2 * R * K * N,
+}
+MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 
 
 def pair_kernel_bytes(fe, B):
@@ -114,6 +130,8 @@ def main():
     ap.add_argument("--frontend", choices=list(FRONTENDS), default="j11")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
+    ap.add_argument("--heads", choices=["bf16", "fp32"], default="bf16",
+                    help="decoder R x R head GEMMs: bf16 MFMA (the reference trains under 16-bit autocast) or fp32")
     args = ap.parse_args()
 
     rank, world, local, dev = init_distributed()
@@ -126,7 +144,7 @@ def main():
     S = plan.S
     torch.manual_seed(1234)  # same initial weights on every rank (DDP semantics)
     model = SeqVaeTeb(sequence_length=S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,
-                      cross_phase_channels=fe.C_x).to(dev)
+                      cross_phase_channels=fe.C_x, head_precision=args.heads).to(dev)
     trainer = Trainer(model, lr=1e-3, frontend=fe, world_size=world)
 
     # synthetic windows resident in HBM before timing; global sample index ->
@@ -134,7 +152,7 @@ def main():
     pool = [torch.from_numpy(synthetic.batch((rank + world * i) * B, B, N)).to(dev) for i in range(2)]
     torch.cuda.synchronize()
 
-    timer = KernelTimer("vt_fe_pairs")
+    timer = KernelTimer(["vt_fe_pairs", *MFMA_CALLS], flops=MFMA_CALLS)
     for i in range(args.warmup):
         trainer.step({"x": pool[i % 2]})
     if world > 1:
@@ -157,14 +175,15 @@ def main():
     elbo = {k: round(float(last[k].item()), 6) for k in ("total_loss", "nll_loss", "mse_loss", "kld_loss")}
     samples = args.steps * B * world
     value = samples / dt
-    k_ms, k_n = timer.mean_ms()
+    k_ms, k_n = timer.mean_ms("vt_fe_pairs")
     k_bytes = pair_kernel_bytes(fe, B)
     achieved = k_bytes / (k_ms * 1e-3) / 1e9
     out = {
         "metric": "train samples/sec + ELBO, 4096-pt windows, batch 256, 1/2/4/8 MI355X",
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "vs_baseline": None, "dtype": "fp32" if args.heads == "fp32" else "fp32 (bf16 MFMA heads)",
+        "data": "synthetic",
         "config": {"workload": f"c2: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTeb(R={16 * S}) "
                                f"train step, batch {B}/GPU", "global_batch": B * world, "seq_len": N,
                    "parallelism": f"dp{world}"},
@@ -173,6 +192,12 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "avg_launch_ms": round(k_ms, 4), "launches": k_n, "algorithmic_bytes": k_bytes},
     }
+    mfma_ms = timer.total_ms(list(MFMA_CALLS))
+    if mfma_ms > 0:
+        tf = sum(timer.total_flops.values()) / (mfma_ms * 1e-3) / 1e12
+        out["mfma"] = {"kernels": "vt_mfma_linear_{fwd,bwd_data,bwd_weight} (decoder heads)",
+                       "achieved": round(tf, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                       "frac": round(tf / MFMA_PEAK_TFLOPS, 4), "ms_per_step": round(mfma_ms / args.steps, 3)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline((J, Q, T), batch=args.cpu_batch)
     if rank == 0:

@@ -158,6 +158,26 @@ int vt_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int 
 int vt_colsum(const float* X, int64_t R, int N, float* out, int accumulate, float* ws, int64_t ws_floats,
               void* stream);
 
+/* ------------------------------------------------------- bf16 MFMA (heads)
+ * The decoder's R x R output heads (Decoder.output_mu / output_logvar,
+ * ref/model/vae_teb_model.py:882-897,926-927, R = 16*S; the reference runs
+ * them under 16-bit autocast, ref/model/graph_model.py:510,710) as bf16 MFMA GEMMs
+ * (v_mfma_f32_16x16x32_bf16, fp32 accumulation).  Same meaning as vt_linear_*;
+ * the weight operand is a bf16 shadow of the fp32 master weight W [N][K]:
+ * W16 = bf16(W) [N][K] for the forward, W16t = bf16(W)^T [K][N] for the input
+ * gradient, both written by vt_mfma_weight_shadow (once per optimizer step).
+ * K and N must be multiples of 64 (vt_mfma_supported), any R.  ws: caller
+ * scratch of at least vt_mfma_workspace_floats(R, K, N) floats.                */
+int vt_mfma_supported(int K, int N);
+int vt_mfma_workspace_floats(int64_t R, int K, int N, int64_t* floats);
+int vt_mfma_weight_shadow(const float* W, int N, int K, void* W16, void* W16t, void* stream);
+int vt_mfma_linear_fwd(const float* X, int64_t R, int K, const void* W16, int N, const float* bias, float* Y,
+                       float* ws, int64_t ws_floats, void* stream);
+int vt_mfma_linear_bwd_data(const float* dY, int64_t R, int N, const void* W16t, int K, float* dX, int accumulate,
+                            float* ws, int64_t ws_floats, void* stream);
+int vt_mfma_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
+                              int accumulate, float* ws, int64_t ws_floats, void* stream);
+
 /* ------------------------------------------------------------------ 1-D conv
  * Conv1d(bias=False) over (B, L, C) activations as an implicit GEMM whose
  * operand load performs the padding / upsampling.

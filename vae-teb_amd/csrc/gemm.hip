@@ -243,12 +243,12 @@ __global__ __launch_bounds__(256) void k_colsum_partial(const float* __restrict_
             for (int i = 0; i < rpi; ++i) s += red[i * N + threadIdx.x];
             partial[(int64_t)blockIdx.x * N + threadIdx.x] = s;
         }
-    } else {
-        for (int n = threadIdx.x; n < N; n += 256) {
-            float a = 0.f;
-            for (int64_t r = r0; r < r1; ++r) a += X[r * N + n];
-            partial[(int64_t)blockIdx.x * N + n] = a;
-        }
+    } else {  // one column per thread, grid.y over 256-column chunks
+        const int n = blockIdx.y * 256 + threadIdx.x;
+        if (n >= N) return;
+        float a = 0.f;
+        for (int64_t r = r0; r < r1; ++r) a += X[r * N + n];
+        partial[(int64_t)blockIdx.x * N + n] = a;
     }
 }
 // one workgroup per column
@@ -424,14 +424,16 @@ int vt_conv1d_fold(const float* gpad, int B, int L_in, int Cin, int Cout, int K,
 int vt_colsum(const float* X, int64_t R, int N, float* out, int accumulate, float* ws, int64_t ws_floats,
               void* stream) {
     VT_CHECK_ARG(R > 0 && N > 0, "vt_colsum: shape");
-    int64_t blocks = (R + 255) / 256;
+    // narrow N: 256 rows per block; wide N: a thread per column and 32 rows per block
+    const int64_t rows = N <= 256 ? 256 : 32;
+    int64_t blocks = (R + rows - 1) / rows;
     if (blocks > 1024) blocks = 1024;
     if (blocks * N > ws_floats) blocks = ws_floats / N;
     VT_CHECK_ARG(blocks >= 1, "vt_colsum: workspace too small");
     const int64_t rpb = (R + blocks - 1) / blocks;
     blocks = (R + rpb - 1) / rpb;
-    hipLaunchKernelGGL(k_colsum_partial, dim3((unsigned)blocks), dim3(256), 0,
-                       S(stream), X, R, N, rpb, ws);
+    hipLaunchKernelGGL(k_colsum_partial, dim3((unsigned)blocks, N <= 256 ? 1 : (unsigned)((N + 255) / 256)),
+                       dim3(256), 0, S(stream), X, R, N, rpb, ws);
     hipLaunchKernelGGL(k_colsum_final, dim3(N), dim3(256), 0, S(stream), ws, (int)blocks, N, out,
                        accumulate);
     VT_LAUNCH_CHECK("vt_colsum");

@@ -1,0 +1,302 @@
+// bf16 MFMA GEMM for the decoder's dense R x R output heads
+// (Decoder.output_mu / output_logvar, ref/model/vae_teb_model.py:882-897,926-927
+// with R = 16*S): Y = X W^T + b, dX = dY W, dW = dY^T X — the only true GEMMs of the
+// step (every other layer is <= 130 wide and stays on the fp32 kernels).
+//
+// One kernel, C[M,N] = sum_k A[m,k] B[n,k] with A and B bf16, K-contiguous:
+//   * v_mfma_f32_16x16x32_bf16, fp32 accumulation;
+//   * block tile 256(M) x 64(N) x 64(K), 8 waves stacked in M, each wave
+//     32 x 64 = 2 x 4 MFMA tiles;
+//   * operands reach LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging):
+//     3 LDS stages, tiles t+1 and t+2 in flight while tile t is multiplied,
+//     counted vmcnt + raw s_barrier (the M = 256 shape is load-latency bound);
+//     rows are 128 B, 16-B chunks XOR-swizzled on the SOURCE address so the
+//     ds_read_b128 fragment reads are bank-conflict free;
+//   * split-K with a fixed-order slab reduction (deterministic) so that
+//     tiles x splits ~ the 256 CUs.
+// Operand images: the weight side is a bf16 shadow of the fp32 master weights
+// (W for the forward, W^T for the input gradient) refreshed by
+// vt_mfma_weight_shadow; the activation side (X, dY, X^T, dY^T) is converted by
+// small prep kernels into zero-padded images, so the main loop has no predicates.
+#include "common.h"
+
+namespace vt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int QM = 256, QN = 64, QK = 64, QT = 512, NSTAGE = 3;
+constexpr int ROWB = QK * 2;                      // 128 B per operand row in LDS
+constexpr int A_BYTES = QM * ROWB;                // 32 KB
+constexpr int STAGE_BYTES = A_BYTES + QN * ROWB;  // + 8 KB of B
+
+// 16-B chunk position of chunk c in LDS row r (involution)
+__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+__device__ __forceinline__ void glds16(const __bf16* src, char* lds) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// grid (N/64, Mpad/256, splits); K = reduction length of ONE split (multiple of 64)
+__global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, int64_t lda,
+                                                  const __bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
+                                                  float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
+                                                  int accumulate, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n0 = blockIdx.x * QN, m0 = blockIdx.y * QM;
+    const int64_t kbeg = (int64_t)blockIdx.z * K;
+    const int T = K / QK;
+
+    // LDS-DMA of one k-tile: lane l writes LDS byte (base + 16 l) = row l>>3, position l&7
+    const int rsub = lane >> 3, pos = lane & 7;
+    auto issue = [&](int t, int s) {
+        const int64_t k0 = kbeg + (int64_t)(t < T ? t : T - 1) * QK;  // past the end: re-read, never used
+        char* st = smem + s * STAGE_BYTES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // A rows 32w + 8i .. +7
+            const int r = 32 * w + 8 * i + rsub;
+            glds16(A + (int64_t)(m0 + r) * lda + k0 + 8 * swz(r, pos), st + (32 * w + 8 * i) * ROWB);
+        }
+        const int r = 8 * w + rsub;  // B rows 8w .. 8w+7
+        glds16(B + (int64_t)(n0 + r) * ldb + k0 + 8 * swz(r, pos), st + A_BYTES + 8 * w * ROWB);
+    };
+
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int lr = lane & 15, lc = lane >> 4;
+    auto compute = [&](int s) {
+        const char* st = smem + s * STAGE_BYTES;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // k 0..31, 32..63: chunks 4h + lc
+            const int c = 4 * h + lc;
+            bf16x8 af[2], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = 32 * w + 16 * i + lr;
+                af[i] = *(const bf16x8*)(st + r * ROWB + 16 * swz(r, c));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = 16 * j + lr;
+                bfr[j] = *(const bf16x8*)(st + A_BYTES + r * ROWB + 16 * swz(r, c));
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    issue(0, 0);
+    issue(1, 1);
+    for (int t = 0; t < T; ++t) {
+        // 5 DMAs per wave per tile: tile t has landed once at most tile t+1's 5 are outstanding
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // tile t complete for all waves; all waves done with tile t-1
+        issue(t + 2, (t + 2) % NSTAGE);
+        compute(t % NSTAGE);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the re-read DMAs before the block exits
+
+    // C/D layout of 16x16x32: col = lane & 15, row = 4 * (lane >> 4) + r
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = n0 + 16 * j + lr;
+            const float bcol = (!part && bias) ? bias[col] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + 32 * w + 16 * i + 4 * lc + r;
+                if (row >= M) continue;
+                const float v = acc[i][j][r];
+                if (part) {
+                    part[((int64_t)blockIdx.z * M + row) * N + col] = v;
+                } else {
+                    float o = v + bcol;
+                    if (accumulate) o += C[(int64_t)row * ldc + col];
+                    C[(int64_t)row * ldc + col] = o;
+                }
+            }
+        }
+}
+
+// fixed-order sum of the split slabs (+ bias, + C when accumulating)
+__global__ void k_mfma_reduce(const float* __restrict__ part, int splits, int64_t MN, int N, const float* bias,
+                              float* __restrict__ C, int64_t ldc, int accumulate) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= MN) return;
+    float s = 0.f;
+    for (int p = 0; p < splits; ++p) s += part[p * MN + i];
+    const int64_t row = i / N;
+    const int col = (int)(i - row * N);
+    if (bias) s += bias[col];
+    float* c = C + row * ldc + col;
+    *c = accumulate ? *c + s : s;
+}
+
+// out[m][k] = bf16(X[m][k]) for m < M, k < K; zero in the padding (Mpad x Kpad)
+__global__ void k_bf16_rows(const float* __restrict__ X, int64_t M, int K, __bf16* __restrict__ out, int64_t Mpad,
+                            int Kpad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = Mpad * Kpad;
+    if (i >= total) return;
+    const int64_t m = i / Kpad;
+    const int k = (int)(i - m * Kpad);
+    out[i] = (m < M && k < K) ? (__bf16)X[m * K + k] : (__bf16)0.f;
+}
+
+// out[c][r] = bf16(X[r][c]) (X is R x Cn row-major); zero padded to Cpad x Rpad
+__global__ __launch_bounds__(256) void k_bf16_transpose(const float* __restrict__ X, int64_t R, int Cn,
+                                                        __bf16* __restrict__ out, int64_t Cpad, int64_t Rpad) {
+    __shared__ float tile[64][65];
+    const int64_t r0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t r = r0 + i, c = c0 + tx;
+        tile[i][tx] = (r < R && c < Cn) ? X[r * Cn + c] : 0.f;
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t c = c0 + i, r = r0 + tx;
+        if (c < Cpad && r < Rpad) out[c * Rpad + r] = (__bf16)tile[tx][i];
+    }
+}
+
+// W fp32 [N][K] -> W16 = bf16(W) [N][K] and W16t = bf16(W)^T [K][N]  (N, K multiples of 64)
+__global__ __launch_bounds__(256) void k_bf16_shadow(const float* __restrict__ W, int N, int K,
+                                                     __bf16* __restrict__ W16, __bf16* __restrict__ W16t) {
+    __shared__ float tile[64][65];
+    const int64_t n0 = (int64_t)blockIdx.y * 64, k0 = (int64_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {
+        const float v = W[(n0 + i) * K + k0 + tx];
+        tile[i][tx] = v;
+        W16[(n0 + i) * K + k0 + tx] = (__bf16)v;
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) W16t[(k0 + i) * N + n0 + tx] = (__bf16)tile[tx][i];
+}
+
+static inline int64_t up_to(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// largest divisor s of the k-tile count with tiles * s <= ~1.25 x CU count
+static int mfma_splits(int64_t tiles, int64_t ktiles) {
+    int best = 1;
+    for (int64_t d = 1; d <= ktiles && d <= 64; ++d)
+        if (ktiles % d == 0 && tiles * d <= 320) best = (int)d;
+    return best;
+}
+
+struct MfmaPlan {
+    int64_t Mpad, Kpad, a_floats, part_floats;
+    int splits;
+};
+
+static MfmaPlan plan(int64_t M, int N, int64_t K) {
+    MfmaPlan p;
+    p.Mpad = up_to(M, QM);
+    p.Kpad = up_to(K, QK);
+    p.a_floats = up_to(p.Mpad * p.Kpad / 2, 64);
+    p.splits = mfma_splits((p.Mpad / QM) * (N / QN), p.Kpad / QK);
+    p.part_floats = p.splits > 1 ? (int64_t)p.splits * M * N : 0;
+    return p;
+}
+
+static int run(const char* who, const __bf16* A, const __bf16* B, int64_t ldb, int64_t M, int N, const MfmaPlan& p,
+               float* C, const float* bias, int accumulate, float* part, hipStream_t st) {
+    const int kper = (int)(p.Kpad / p.splits);
+    dim3 grid(N / QN, (unsigned)(p.Mpad / QM), p.splits);
+    hipLaunchKernelGGL(k_mfma_gemm, grid, dim3(QT), 0, st, A, p.Kpad, B, ldb, (int)M, N, kper, C, (int64_t)N, bias,
+                       accumulate, p.splits > 1 ? part : nullptr);
+    if (p.splits > 1) {
+        const int64_t MN = M * N;
+        hipLaunchKernelGGL(k_mfma_reduce, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, part, p.splits, MN, N,
+                           bias, C, (int64_t)N, accumulate);
+    }
+    VT_LAUNCH_CHECK(who);
+    return VT_OK;
+}
+
+}  // namespace vt
+
+using namespace vt;
+
+extern "C" {
+
+int vt_mfma_supported(int K, int N) { return (K > 0 && N > 0 && K % QK == 0 && N % QN == 0) ? 1 : 0; }
+
+int vt_mfma_workspace_floats(int64_t R, int K, int N, int64_t* floats) {
+    VT_CHECK_ARG(R > 0 && K > 0 && N > 0 && floats, "vt_mfma_workspace_floats: shape");
+    MfmaPlan f = plan(R, N, K), d = plan(R, K, N), w = plan(N, K, R);
+    const int64_t wf = w.a_floats + up_to((int64_t)K * w.Kpad / 2, 64) + w.part_floats + N;
+    int64_t m = f.a_floats + f.part_floats;
+    if (d.a_floats + d.part_floats > m) m = d.a_floats + d.part_floats;
+    if (wf > m) m = wf;
+    *floats = m;
+    return VT_OK;
+}
+
+int vt_mfma_weight_shadow(const float* W, int N, int K, void* W16, void* W16t, void* stream) {
+    VT_CHECK_ARG(vt_mfma_supported(K, N) && W && W16 && W16t, "vt_mfma_weight_shadow: K and N must be multiples of 64");
+    hipLaunchKernelGGL(k_bf16_shadow, dim3(K / 64, N / 64), dim3(256), 0, S(stream), W, N, K, (__bf16*)W16,
+                       (__bf16*)W16t);
+    VT_LAUNCH_CHECK("vt_mfma_weight_shadow");
+    return VT_OK;
+}
+
+// Y[R,N] = X[R,K] W[N,K]^T + b     (W16 = bf16 shadow of W, [N][K])
+int vt_mfma_linear_fwd(const float* X, int64_t R, int K, const void* W16, int N, const float* bias, float* Y,
+                       float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(R > 0 && vt_mfma_supported(K, N), "vt_mfma_linear_fwd: K and N must be positive multiples of 64");
+    MfmaPlan p = plan(R, N, K);
+    VT_CHECK_ARG(p.a_floats + p.part_floats <= ws_floats, "vt_mfma_linear_fwd: workspace too small");
+    __bf16* A = (__bf16*)ws;
+    const int64_t tot = p.Mpad * p.Kpad;
+    hipLaunchKernelGGL(k_bf16_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, S(stream), X, R, K, A, p.Mpad,
+                       (int)p.Kpad);
+    return run("vt_mfma_linear_fwd", A, (const __bf16*)W16, K, R, N, p, Y, bias, 0, ws + p.a_floats, S(stream));
+}
+
+// dX[R,K] (+)= dY[R,N] W[N,K]      (W16t = bf16 shadow of W^T, [K][N])
+int vt_mfma_linear_bwd_data(const float* dY, int64_t R, int N, const void* W16t, int K, float* dX, int accumulate,
+                            float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(R > 0 && vt_mfma_supported(N, K), "vt_mfma_linear_bwd_data: K and N must be positive multiples of 64");
+    MfmaPlan p = plan(R, K, N);  // C = dX (M=R, cols=K), reduction over N
+    VT_CHECK_ARG(p.a_floats + p.part_floats <= ws_floats, "vt_mfma_linear_bwd_data: workspace too small");
+    __bf16* A = (__bf16*)ws;
+    const int64_t tot = p.Mpad * p.Kpad;
+    hipLaunchKernelGGL(k_bf16_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, S(stream), dY, R, N, A,
+                       p.Mpad, (int)p.Kpad);
+    return run("vt_mfma_linear_bwd_data", A, (const __bf16*)W16t, N, R, K, p, dX, nullptr, accumulate,
+               ws + p.a_floats, S(stream));
+}
+
+// dW[N,K] (+)= dY[R,N]^T X[R,K];  db (+)= column sums of dY (if db != NULL)
+int vt_mfma_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
+                              int accumulate, float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(R > 0 && vt_mfma_supported(K, N), "vt_mfma_linear_bwd_weight: K and N must be positive multiples of 64");
+    MfmaPlan p = plan(N, K, R);  // C = dW (M=N, cols=K), reduction over R
+    const int64_t b_floats = up_to((int64_t)K * p.Kpad / 2, 64);
+    VT_CHECK_ARG(p.a_floats + b_floats + p.part_floats + N <= ws_floats, "vt_mfma_linear_bwd_weight: workspace too small");
+    __bf16* A = (__bf16*)ws;                   // dY^T  [Npad][Rpad]
+    __bf16* Bt = (__bf16*)(ws + p.a_floats);   // X^T   [K][Rpad]
+    float* part = ws + p.a_floats + b_floats;
+    hipLaunchKernelGGL(k_bf16_transpose, dim3((unsigned)(p.Kpad / 64), (unsigned)(p.Mpad / 64)), dim3(256), 0,
+                       S(stream), dY, R, N, A, p.Mpad, p.Kpad);
+    hipLaunchKernelGGL(k_bf16_transpose, dim3((unsigned)(p.Kpad / 64), (unsigned)(K / 64)), dim3(256), 0, S(stream), X,
+                       R, K, Bt, (int64_t)K, p.Kpad);
+    int rc = run("vt_mfma_linear_bwd_weight", A, Bt, p.Kpad, N, K, p, dW, nullptr, accumulate, part, S(stream));
+    if (rc || !db) return rc;
+    return vt_colsum(dY, R, N, db, accumulate, part, ws_floats - p.a_floats - b_floats, stream);
+}
+
+}  // extern "C"

@@ -36,9 +36,10 @@ class Linear(nn.Module):
         self.weight = nn.Parameter(torch.empty(dout, din))
         self.bias = nn.Parameter(torch.zeros(dout))
         nn.init.xavier_uniform_(self.weight)          # initialization(), vae_teb_model.py:55-59
+        self.mfma = False                             # bf16 MFMA GEMMs (set on the decoder heads)
 
     def forward(self, x):
-        return ops.linear(x, self.weight, self.bias)
+        return ops.linear(x, self.weight, self.bias, self.mfma)
 
 
 class LayerNorm(nn.Module):
@@ -254,7 +255,7 @@ class Decoder(nn.Module):
     SPEC = [(87, 77, 11, False), (77, 66, 9, True), (66, 55, 7, True), (55, 44, 5, False),
             (44, 33, 5, True), (33, 22, 3, True), (22, 11, 3, False), (11, 1, 3, False)]
 
-    def __init__(self, latent_dim=32, sequence_length=300):
+    def __init__(self, latent_dim=32, sequence_length=300, head_precision="fp32"):
         super().__init__()
         self.sequence_length = sequence_length
         R = 16 * sequence_length
@@ -263,6 +264,19 @@ class Decoder(nn.Module):
         self.conv = nn.Sequential(*[ConvBlock(a, b, k, causal=False, up=u) for a, b, k, u in self.SPEC])
         self.output_mu = ResidualMLP(R, (R, R), final_activation=False, use_skip_connection=False)
         self.output_logvar = ResidualMLP(R, (R, R), final_activation=False, use_skip_connection=False)
+        self.set_head_precision(head_precision)
+
+    def set_head_precision(self, precision):
+        """"fp32": every GEMM on the fp32 kernels (parity mode); "bf16": the
+        R x R head GEMMs on bf16 MFMA with fp32 accumulation (the reference
+        trains under 16-bit autocast, ref/model/graph_model.py:510,710)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"head_precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.head_precision = precision
+        for head in (self.output_mu, self.output_logvar):
+            for m in head.modules():
+                if isinstance(m, Linear):
+                    m.mfma = precision == "bf16"
 
     def forward(self, z):
         lin = self.linear(z)                       # (B, S, 87)
@@ -276,7 +290,7 @@ class SeqVaeTeb(nn.Module):
 
     def __init__(self, input_channels=76, sequence_length=300, latent_dim_source=32, latent_dim_target=32,
                  latent_dim_z=32, decimation_factor=16, warmup_period=30, scattering_channels=43,
-                 phase_channels=44, cross_phase_channels=130):
+                 phase_channels=44, cross_phase_channels=130, head_precision="fp32"):
         super().__init__()
         self.latent_dim_source, self.latent_dim_target, self.latent_dim_z = latent_dim_source, latent_dim_target, \
             latent_dim_z
@@ -284,7 +298,7 @@ class SeqVaeTeb(nn.Module):
         self.source_encoder = SourceEncoder(cross_phase_channels)
         self.target_encoder = TargetEncoder(scattering_channels, phase_channels)
         self.conditional_encoder = ConditionalEncoder(latent_dim_source, latent_dim_target)
-        self.decoder = Decoder(latent_dim_z, sequence_length)
+        self.decoder = Decoder(latent_dim_z, sequence_length, head_precision)
 
     def forward(self, y_st, y_ph, x_ph, eps=None):
         mu_x = self.source_encoder(x_ph)

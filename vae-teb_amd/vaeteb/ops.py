@@ -47,43 +47,83 @@ def _check(*ts):
 
 
 # ------------------------------------------------------------------ Linear
+def mfma_ok(K, N):
+    """bf16 MFMA path available for a K -> N linear (vt_mfma_supported)."""
+    return bool(_lib.lib().fns["vt_mfma_supported"](K, N))
+
+
+_SHADOW = {}
+
+
+def _weight_shadow(w):
+    """bf16 images of an fp32 master weight W [N, K]: (W16 [N, K], W16t [K, N]),
+    rewritten from W on every forward (the optimizer updates W in place)."""
+    N, K = w.shape
+    key = (w.data_ptr(), N, K)
+    sh = _SHADOW.get(key)
+    if sh is None:
+        sh = (torch.empty((N, K), dtype=torch.bfloat16, device=w.device),
+              torch.empty((K, N), dtype=torch.bfloat16, device=w.device))
+        _SHADOW[key] = sh
+    call("vt_mfma_weight_shadow", ptr(w), N, K, ptr(sh[0]), ptr(sh[1]), _st())
+    return sh
+
+
 class LinearF(torch.autograd.Function):
+    """nn.Linear; mfma=True routes the three GEMMs to the bf16 MFMA kernels
+    (vt_mfma_linear_*, on bf16 shadows of the fp32 weight), else the fp32
+    kernels (vt_linear_*)."""
+
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, mfma=False):
         _check(x, w, b)
         K = x.shape[-1]
         N = w.shape[0]
         x2 = x.reshape(-1, K).contiguous()
         R = x2.shape[0]
         y = torch.empty((R, N), device=x.device)
-        call("vt_linear_fwd", ptr(x2), R, K, ptr(w), N, ptr(b), ptr(y), _st())
-        ctx.save_for_backward(x2, w)
+        mfma = bool(mfma) and mfma_ok(K, N)
+        w16t = None
+        if mfma:
+            w16, w16t = _weight_shadow(w)
+            ws = WS.get(WS_LINEAR, x.device, 1)
+            call("vt_mfma_linear_fwd", ptr(x2), R, K, ptr(w16), N, ptr(b), ptr(y), ptr(ws), ws.numel(), _st())
+        else:
+            call("vt_linear_fwd", ptr(x2), R, K, ptr(w), N, ptr(b), ptr(y), _st())
+        ctx.save_for_backward(x2, w, w16t)
         ctx.shape = x.shape
         ctx.has_bias = b is not None
+        ctx.mfma = mfma
         return y.reshape(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, gy):
-        x2, w = ctx.saved_tensors
+        x2, w, w16t = ctx.saved_tensors
         N, K = w.shape
         R = x2.shape[0]
         gy2 = gy.reshape(R, N).contiguous()
         gx = gw = gb = None
+        ws = WS.get(WS_LINEAR, w.device, 1)
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x2)
-            call("vt_linear_bwd_data", ptr(gy2), R, N, ptr(w), K, ptr(gx), 0, _st())
+            if ctx.mfma:
+                call("vt_mfma_linear_bwd_data", ptr(gy2), R, N, ptr(w16t), K, ptr(gx), 0, ptr(ws), ws.numel(),
+                     _st())
+            else:
+                call("vt_linear_bwd_data", ptr(gy2), R, N, ptr(w), K, ptr(gx), 0, _st())
             gx = gx.reshape(ctx.shape)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             gw = torch.empty_like(w)
             gb = torch.empty(N, device=w.device) if want_b else None
-            ws = WS.get(WS_LINEAR, w.device, 1)
-            call("vt_linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw), ptr(gb), 0, ptr(ws), ws.numel(), _st())
+            pre = "vt_mfma_" if ctx.mfma else "vt_"
+            call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw), ptr(gb), 0, ptr(ws), ws.numel(),
+                 _st())
         elif want_b:
             gb = torch.empty(N, device=w.device)
             ws = WS.get(2048 * N, w.device, 2)
             call("vt_colsum", ptr(gy2), R, N, ptr(gb), 0, ptr(ws), ws.numel(), _st())
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
 # -------------------------------------------------------- LayerNorm + act
@@ -299,8 +339,8 @@ class OutputLossF(torch.autograd.Function):
 
 
 # ------------------------------------------------------------- functional API
-def linear(x, w, b=None):
-    return LinearF.apply(x, w, b)
+def linear(x, w, b=None, mfma=False):
+    return LinearF.apply(x, w, b, mfma)
 
 
 def layer_norm_act(x, g, b, act="none", eps=1e-5):
