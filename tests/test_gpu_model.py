@@ -97,6 +97,9 @@ def _ref_conv_block(x_blc, w, g, b, rm, rv, causal, up, tanh):
     (2, 3, 8, 6, 5, False, True, False),         # upsample then replicate
     (4, 256, 11, 1, 3, False, False, False),
     (8, 256, 16, 2, 3, False, False, True),
+    (2, 1024, 33, 22, 3, False, True, False),    # decoder L6 geometry (x2 upsample to 2048)
+    (3, 300, 1, 16, 3, True, False, False),      # Cin = 1 (tiny encoder)
+    (2, 512, 55, 44, 5, False, False, False),
 ])
 def test_conv_bn_act(ops, B, L, Cin, Cout, K, causal, up, tanh):
     torch.manual_seed(B * 1000 + L)

@@ -1,29 +1,40 @@
-// Direct 1-D convolution kernels for the encoder / decoder conv stacks
+// 1-D convolution kernels for the encoder / decoder conv stacks
 // (ref/model/vae_teb_model.py:128-253), on (B, L, C)
-// activations.
+// activations, as implicit GEMMs on the exact-fp32 matrix cores
+// (v_mfma_f32_16x16x4_f32: bit-for-bit an fmaf chain, at the 157 TF fp32 rate,
+// ~2x what the VALU reaches on the same tiles).
 //
-// Forward: a workgroup owns (sample b, 64 output positions, 64 output
-// channels).  For each chunk of 16 input channels it stages, in LDS, the input
-// window [t0 - pad, t0 + 64 + K - 1 - pad) — reflect / replicate / causal-zero
-// padding and the x2 linear upsample applied while staging, so no padded copy
-// exists in HBM — and the filter taps W[co][ci][k] of the chunk; each thread
-// then accumulates a 4 (positions) x 4 (channels) register tile over
-// (k, ci) reading both operands from LDS (every staged input sample is reused
-// K times, every tap 64 times).
+// Forward: out[t][co] = sum_{k, ci} xpad[t + k][ci] W[co][ci][k].  A workgroup
+// (4 waves) owns (sample b, TP output positions, TC = 16*NT output channels,
+// NT fitted to Cout so the 77/66/55/.../1-channel layers carry little
+// padding); per chunk of CI input channels it stages in LDS the input window
+// [t0 - pad, t0 + TP + K - 1 - pad) — reflect / replicate / causal-zero padding
+// and the x2 linear upsample applied while staging, so no padded copy exists
+// in HBM — and the taps of the chunk.  Each wave multiplies PM x NT 16x16
+// tiles: per (4 input channels, tap) it reads one A fragment per position
+// tile (the window shifted by the tap) and one B fragment per channel tile.
 // Backward-data is the same kernel on dY with transposed, flipped taps and
 // causal padding (a "full" correlation over the padded input), followed by
 // the fold of the padded/upsampled gradient (gemm.hip k_conv_fold).
-// Backward-weight: a workgroup accumulates dW[64 co][16 ci][K] over a slice of
-// the B*L_out rows from LDS-staged dY rows and input windows; slices are
-// summed in fixed order.
+// Backward-weight: dW[co][ci][k] = sum_rows dY[row][co] xpad[row + k][ci]; a
+// workgroup stages a chunk of dY rows and input rows (all channels) and its 8
+// waves each own up to PPW (16 co x 16 ci) tile pairs with K accumulators,
+// reducing over rows 4 at a time (A = dY rows, B = the input rows shifted by
+// each tap).  Rows are split over workgroups; the partial slabs are summed in
+// fixed order.
 #include "common.h"
 
 namespace vt {
 
-static constexpr int CT = 64;   // output positions per workgroup
-static constexpr int CC = 64;   // output channels per workgroup
-static constexpr int CI = 16;   // input-channel chunk
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 static constexpr int KMAX = 11;
+static constexpr int XS = 18;               // forward window row stride: conflict-free A fragments
+static constexpr int FWD_LDS = 16384;       // forward LDS budget (floats, 64 KB)
+static constexpr int DR = 64;               // dW rows per chunk
+static constexpr int SS = 112;              // dW LDS row stride (== 16 mod 32), max channels
+static constexpr int DW_CMAX = 96;
+static constexpr int SB = 8;                // staging batch (loads in flight per thread)
 
 struct Geo {
     int B, L_in, Cin, Cout, K, up, mode, L_up, pad, L_out;
@@ -49,144 +60,275 @@ __device__ __forceinline__ float src_val(const float* __restrict__ xb, const Geo
     return (1.f - l1) * xb[(int64_t)i0 * g.Cin + ci] + l1 * xb[(int64_t)i1 * g.Cin + ci];
 }
 
-// flip_t: use W[ci][co][K-1-k] (transposed, flipped) instead of W[co][ci][k]
-template <bool FLIP_T>
-__global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ x, Geo g, const float* __restrict__ w,
-                                                  float* __restrict__ y) {
-    __shared__ float xs[(CT + KMAX - 1) * CI];
-    __shared__ __attribute__((aligned(16))) float ws[KMAX * CI * CC];
-    const int tid = threadIdx.x;
-    const int tx = tid & 15, ty = tid >> 4;     // tx: channel group (4), ty: position group (4)
-    const int b = blockIdx.z;
-    const int t0 = blockIdx.x * CT;
-    const int co0 = blockIdx.y * CC;
-    const int K = g.K;
-    const int win = CT + K - 1;
-    const float* xb = x + (int64_t)b * g.L_in * g.Cin;
-    float acc[4][4] = {};
-    for (int c0 = 0; c0 < g.Cin; c0 += CI) {
-        const int cn = g.Cin - c0 < CI ? g.Cin - c0 : CI;
-        for (int i = tid; i < win * CI; i += 256) {
-            const int r = i / CI, c = i - r * CI;
-            const int tp = t0 + r;
-            xs[i] = (c < cn && tp < g.L_out + K - 1) ? src_val(xb, g, tp, c0 + c) : 0.f;
-        }
-        for (int i = tid; i < K * CI * CC; i += 256) {
-            const int co = i % CC, rest = i / CC;
-            const int c = rest % CI, k = rest / CI;
-            float v = 0.f;
-            if (c < cn && co0 + co < g.Cout) {
-                const int gco = co0 + co, gci = c0 + c;
-                v = FLIP_T ? w[((int64_t)gci * g.Cout + gco) * K + (K - 1 - k)]
-                           : w[((int64_t)gco * g.Cin + gci) * K + k];
-            }
-            ws[(k * CI + c) * CC + co] = v;
-        }
-        __syncthreads();
-        for (int k = 0; k < K; ++k) {
-#pragma unroll 4
-            for (int c = 0; c < CI; ++c) {
-                const float4 wv = *reinterpret_cast<const float4*>(&ws[(k * CI + c) * CC + tx * 4]);
-                const float wa[4] = {wv.x, wv.y, wv.z, wv.w};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float a = xs[(ty * 4 + i + k) * CI + c];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a, wa[j], acc[i][j]);
-                }
-            }
-        }
-        __syncthreads();
-    }
-    const int Lo = FLIP_T ? g.L_out + K - 1 : g.L_out;  // bwd-data writes the padded length
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int t = t0 + ty * 4 + i;
-        if (t >= Lo) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int co = co0 + tx * 4 + j;
-            if (co < g.Cout) y[((int64_t)b * Lo + t) * g.Cout + co] = acc[i][j];
-        }
-    }
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// dW partial: ws_out[split][co][ci][k] = sum over the split's rows of
-// dY[b,t,co] * xpad[b, t+k, ci].  Workgroup: 64 co x 16 ci x K, rows in chunks of CT.
-__global__ __launch_bounds__(256) void k_conv_dw(const float* __restrict__ dy, const float* __restrict__ x, Geo g,
-                                                 int64_t rows_per_split, float* __restrict__ part) {
-    __shared__ float ds[CT * CC];                       // dY chunk [t][co]
-    __shared__ float xs[(CT + KMAX - 1) * CI];          // input window [tp][ci]
-    const int tid = threadIdx.x;
-    const int cg = tid & 15;        // co group of 4
-    const int cil = tid >> 4;       // ci within chunk (0..15)
-    const int co0 = blockIdx.x * CC;
-    const int c0 = blockIdx.y * CI;
-    const int K = g.K;
+template <int K, int NT>
+struct FwdCfg {
+    static constexpr int PM = NT <= 3 ? 4 : (NT == 4 ? 3 : 2);         // position tiles per wave
+    static constexpr int TC = 16 * NT, TP = 64 * PM;                     // workgroup tile
+    static constexpr int WIN = TP + K - 1;
+    static constexpr int WS = (K * TC) % 32 == 0 ? K * TC + 16 : K * TC; // tap row stride (== 16 mod 32)
+    static constexpr int XF = (WIN * XS + 3) & ~3;
+    static constexpr int CI = XF + 16 * WS <= FWD_LDS ? 16 : 8;          // input channels per chunk
+    static constexpr int LDS_BYTES = (XF + CI * WS) * 4;
+};
+
+// FLIP_T: taps W[ci][co][K-1-k] (transposed, flipped) instead of W[co][ci][k].
+template <int K, int NT, bool FLIP_T>
+__global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ x, Geo g, const float* __restrict__ w,
+                                                  float* __restrict__ y, int Lo) {
+    using C = FwdCfg<K, NT>;
+    constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN, WS = C::WS, CI = C::CI;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* xs = lds;            // [WIN][XS]   window, channel-fastest
+    float* ws = lds + C::XF;    // [CI][K][TC] taps (row stride WS)
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
+    const int t0 = blockIdx.x * TP, co0 = blockIdx.y * TC, b = blockIdx.z;
+    const float* xb = x + (int64_t)b * g.L_in * g.Cin;
+    f32x4 acc[PM][NT];
+#pragma unroll
+    for (int m = 0; m < PM; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < g.Cin; c0 += CI) {
+        const int cn = g.Cin - c0 < CI ? g.Cin - c0 : CI;
+        // staging in batches of SB elements per thread: a batch's loads are all in
+        // flight before its LDS stores (not one L2 round trip per element)
+        constexpr int UX = (WIN * CI + 255) / 256, UW = (CI * K * TC + 255) / 256;
+#pragma unroll 1
+        for (int u0 = 0; u0 < UX; u0 += SB) {
+            float v[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = tid + 256 * (u0 + u);
+                const int r = i / CI, c = i - r * CI;
+                const int tp = t0 + r;
+                v[u] = (i < WIN * CI && c < cn && tp < Lo + K - 1) ? src_val(xb, g, tp, c0 + c) : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = tid + 256 * (u0 + u);
+                const int r = i / CI, c = i - r * CI;
+                if (i < WIN * CI) xs[r * XS + c] = v[u];
+            }
+        }
+        // taps, read in global order (contiguous (ci, k) runs per co; (co, k) per ci when flipped)
+        auto tap_idx = [&](int i, int& co, int& c, int& k) {
+            if (FLIP_T) {
+                c = i / (TC * K);
+                const int rest = i - c * (TC * K);
+                co = rest / K;
+                k = rest - co * K;
+            } else {
+                co = i / (CI * K);
+                const int rest = i - co * (CI * K);
+                c = rest / K;
+                k = rest - c * K;
+            }
+        };
+#pragma unroll 1
+        for (int u0 = 0; u0 < UW; u0 += SB) {
+            float v[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = tid + 256 * (u0 + u);
+                int co, c, k;
+                tap_idx(i, co, c, k);
+                float val = 0.f;
+                if (i < CI * K * TC && c < cn && co0 + co < g.Cout) {
+                    const int gco = co0 + co, gci = c0 + c;
+                    val = FLIP_T ? w[((int64_t)gci * g.Cout + gco) * K + (K - 1 - k)]
+                                 : w[((int64_t)gco * g.Cin + gci) * K + k];
+                }
+                v[u] = val;
+            }
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = tid + 256 * (u0 + u);
+                int co, c, k;
+                tap_idx(i, co, c, k);
+                if (i < CI * K * TC) ws[c * WS + k * TC + co] = v[u];
+            }
+        }
+        __syncthreads();
+        const int ng = (cn + 3) >> 2;
+        for (int q = 0; q < ng; ++q) {
+            const float* xq = xs + (PM * 16 * wv + lr) * XS + 4 * q + lc;
+            const float* wq = ws + (4 * q + lc) * WS + lr;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                float af[PM], bf[NT];
+#pragma unroll
+                for (int m = 0; m < PM; ++m) af[m] = xq[(16 * m + k) * XS];
+#pragma unroll
+                for (int n = 0; n < NT; ++n) bf[n] = wq[k * TC + 16 * n];
+#pragma unroll
+                for (int m = 0; m < PM; ++m)
+#pragma unroll
+                    for (int n = 0; n < NT; ++n) acc[m][n] = mfma4(af[m], bf[n], acc[m][n]);
+            }
+        }
+        __syncthreads();
+    }
+    // D layout: col (channel) = lane & 15, row (position) = 4 * (lane >> 4) + r
+#pragma unroll
+    for (int m = 0; m < PM; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int t = t0 + PM * 16 * wv + 16 * m + 4 * lc + r;
+            if (t >= Lo) continue;
+            float* yr = y + ((int64_t)b * Lo + t) * g.Cout;
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int co = co0 + 16 * n + lr;
+                if (co < g.Cout) yr[co] = acc[m][n][r];
+            }
+        }
+}
+
+// dW partial slabs: part[split][co][ci][k] over the split's rows.
+// 8 waves; each wave owns PPW (16 co x 16 ci) tile pairs with K accumulators
+// each.  When a layer has fewer pairs than waves, wpp waves share a pair and
+// interleave its row groups.
+template <int K, int PPW>
+__global__ __launch_bounds__(512) void k_conv_dw(const float* __restrict__ dy, const float* __restrict__ x, Geo g,
+                                                 int64_t rows_per_split, int NTc, int npairs, int wpp,
+                                                 float* __restrict__ part) {
+    __shared__ float ds[(DR + 4) * SS];             // dY chunk [row][co]
+    __shared__ float xs[(DR + 4 + KMAX - 1) * SS];  // input window [row][ci]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
+    const int ngroups = 8 / wpp, grp = wv / wpp, sub = wv % wpp;
+    int mt[PPW], nt[PPW];
+    bool act[PPW];
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+        const int p = blockIdx.x * (ngroups * PPW) + grp + ngroups * j;
+        act[j] = grp < ngroups && p < npairs;
+        mt[j] = p / NTc;
+        nt[j] = p - mt[j] * NTc;
+    }
     const int64_t rows = (int64_t)g.B * g.L_out;
-    const int64_t r0 = (int64_t)blockIdx.z * rows_per_split;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
     const int64_t r1 = r0 + rows_per_split < rows ? r0 + rows_per_split : rows;
-    float acc[4][KMAX];
+    f32x4 acc[PPW][K];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < PPW; ++j)
 #pragma unroll
-        for (int k = 0; k < KMAX; ++k) acc[j][k] = 0.f;
+        for (int k = 0; k < K; ++k) acc[j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
     // rows are processed in chunks that never cross a sample boundary
     for (int64_t r = r0; r < r1;) {
         const int b = (int)(r / g.L_out);
         const int t0 = (int)(r - (int64_t)b * g.L_out);
         int n = g.L_out - t0;
-        if (n > CT) n = CT;
+        if (n > DR) n = DR;
         if (r + n > r1) n = (int)(r1 - r);
+        const int n4 = (n + 3) & ~3;  // rows n .. n4-1 are zero (partial last row group)
         const float* xb = x + (int64_t)b * g.L_in * g.Cin;
         const float* dyb = dy + ((int64_t)b * g.L_out + t0) * g.Cout;
-        for (int i = tid; i < CT * CC; i += 256) {
-            const int t = i / CC, co = i - t * CC;
-            ds[i] = (t < n && co0 + co < g.Cout) ? dyb[(int64_t)t * g.Cout + co0 + co] : 0.f;
+        // staging in batches of SB elements per thread (loads in flight before the
+        // LDS stores).  Flat element index -> (row, channel) by a float reciprocal
+        // (exact here: indices < 2^13, the fraction is >= 0.5 / C from an integer).
+        const int nd = n4 * g.Cout, nx = (n4 + K - 1) * g.Cin;
+        const float icout = 1.f / g.Cout, icin = 1.f / g.Cin;
+#pragma unroll 1
+        for (int i0 = 0; i0 < nd; i0 += 512 * SB) {
+            float v[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = i0 + tid + 512 * u;
+                const int t = (int)((i + 0.5f) * icout);
+                v[u] = (i < nd && t < n) ? dyb[i] : 0.f;  // rows of dY are contiguous
+            }
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = i0 + tid + 512 * u;
+                const int t = (int)((i + 0.5f) * icout), c = i - t * g.Cout;
+                if (i < nd) ds[t * SS + c] = v[u];
+            }
         }
-        for (int i = tid; i < (CT + K - 1) * CI; i += 256) {
-            const int tp = i / CI, c = i - tp * CI;
-            xs[i] = (tp < n + K - 1 && c0 + c < g.Cin) ? src_val(xb, g, t0 + tp, c0 + c) : 0.f;
+#pragma unroll 1
+        for (int i0 = 0; i0 < nx; i0 += 512 * SB) {
+            float v[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = i0 + tid + 512 * u;
+                const int tp = (int)((i + 0.5f) * icin), c = i - tp * g.Cin;
+                v[u] = (i < nx && tp < n + K - 1) ? src_val(xb, g, t0 + tp, c) : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = i0 + tid + 512 * u;
+                const int tp = (int)((i + 0.5f) * icin), c = i - tp * g.Cin;
+                if (i < nx) xs[tp * SS + c] = v[u];
+            }
         }
         __syncthreads();
-        for (int t = 0; t < n; ++t) {
-            const float d0 = ds[t * CC + cg * 4 + 0], d1 = ds[t * CC + cg * 4 + 1];
-            const float d2 = ds[t * CC + cg * 4 + 2], d3 = ds[t * CC + cg * 4 + 3];
+        for (int q = sub; q < (n4 >> 2); q += wpp) {
+            const float* dq = ds + (4 * q + lc) * SS + lr;
+            const float* xq = xs + (4 * q + lc) * SS + lr;
 #pragma unroll
-            for (int k = 0; k < KMAX; ++k) {
-                if (k < K) {
-                    const float xv = xs[(t + k) * CI + cil];
-                    acc[0][k] = fmaf(d0, xv, acc[0][k]);
-                    acc[1][k] = fmaf(d1, xv, acc[1][k]);
-                    acc[2][k] = fmaf(d2, xv, acc[2][k]);
-                    acc[3][k] = fmaf(d3, xv, acc[3][k]);
-                }
+            for (int j = 0; j < PPW; ++j) {
+                if (!act[j]) continue;
+                const float a = dq[16 * mt[j]];
+#pragma unroll
+                for (int k = 0; k < K; ++k) acc[j][k] = mfma4(a, xq[k * SS + 16 * nt[j]], acc[j][k]);
             }
         }
         __syncthreads();
         r += n;
     }
-    const int ci = c0 + cil;
-    if (ci >= g.Cin) return;
+    // waves sharing a pair (wpp > 1) combine their accumulators through LDS in
+    // fixed order, one tap at a time; the sub-0 wave then holds the pair's sum
+    if (wpp > 1) {
+        float* red = ds;  // 8 waves x 256 floats
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int co = co0 + cg * 4 + j;
-        if (co >= g.Cout) continue;
+        for (int k = 0; k < K; ++k) {
 #pragma unroll
-        for (int k = 0; k < KMAX; ++k)
-            if (k < K) part[(((int64_t)blockIdx.z * g.Cout + co) * g.Cin + ci) * K + k] = acc[j][k];
+            for (int rr = 0; rr < 4; ++rr) red[wv * 256 + rr * 64 + lane] = acc[0][k][rr];
+            __syncthreads();
+            if (sub == 0)
+                for (int s2 = 1; s2 < wpp; ++s2)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) acc[0][k][rr] += red[(wv + s2) * 256 + rr * 64 + lane];
+            __syncthreads();
+        }
+        if (sub != 0) return;
+    }
+    // D: col (ci) = lane & 15, row (co) = 4 * (lane >> 4) + rr
+    const int64_t slot = blockIdx.y;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+        if (!act[j]) continue;
+        const int ci = 16 * nt[j] + lr;
+        if (ci >= g.Cin) continue;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int co = 16 * mt[j] + 4 * lc + rr;
+            if (co >= g.Cout) continue;
+            float* p = part + ((slot * g.Cout + co) * g.Cin + ci) * K;
+#pragma unroll
+            for (int k = 0; k < K; ++k) p[k] = acc[j][k][rr];
+        }
     }
 }
 
-// out[i] (+)= sum_s part[s][i], i < n (fixed order)
-__global__ void k_sum_splits(const float* __restrict__ part, int splits, int64_t n, float* __restrict__ out,
-                             int accumulate) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// out[i] (+)= sum_s part[s][i] (fixed order): 64 outputs x 4 split lanes per workgroup
+__global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ part, int splits, int64_t n,
+                                                    float* __restrict__ out, int accumulate) {
+    __shared__ float red[4][64];
+    const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 64 + o;
     float a = 0.f;
-#pragma unroll 8
-    for (int s = 0; s < splits; ++s) a += part[(int64_t)s * n + i];
-    out[i] = accumulate ? out[i] + a : a;
+    if (i < n)
+        for (int s = sl; s < splits; s += 4) a += part[(int64_t)s * n + i];
+    red[sl][o] = a;
+    __syncthreads();
+    if (sl == 0 && i < n) {
+        const float s = (red[0][o] + red[1][o]) + (red[2][o] + red[3][o]);
+        out[i] = accumulate ? out[i] + s : s;
+    }
 }
 
 static Geo geo(int B, int L_in, int Cin, int Cout, int K, int mode, int up) {
@@ -196,6 +338,44 @@ static Geo geo(int B, int L_in, int Cin, int Cout, int K, int mode, int up) {
     g.pad = mode == 0 ? K - 1 : (K - 1) / 2;
     g.L_out = mode == 0 ? g.L_up : g.L_up + 2 * g.pad - K + 1;
     return g;
+}
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+template <int K, int NT, bool FLIP_T>
+static void fwd_nt(const float* x, const Geo& g, const float* w, float* y, int Lo, hipStream_t st) {
+    using C = FwdCfg<K, NT>;
+    dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
+    hipLaunchKernelGGL((k_conv_fwd<K, NT, FLIP_T>), grid, dim3(256), C::LDS_BYTES, st, x, g, w, y, Lo);
+}
+
+template <int K, bool FLIP_T>
+static void fwd_k(const float* x, const Geo& g, const float* w, float* y, int Lo, hipStream_t st) {
+    switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
+        case 1: fwd_nt<K, 1, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 2: fwd_nt<K, 2, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 3: fwd_nt<K, 3, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 4: fwd_nt<K, 4, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 5: fwd_nt<K, 5, FLIP_T>(x, g, w, y, Lo, st); break;
+        default: fwd_nt<K, 6, FLIP_T>(x, g, w, y, Lo, st); break;
+    }
+}
+
+template <bool FLIP_T>
+static void launch_fwd(const float* x, const Geo& g, const float* w, float* y, int Lo, hipStream_t st) {
+    switch (g.K) {
+        case 1: fwd_k<1, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 2: fwd_k<2, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 3: fwd_k<3, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 4: fwd_k<4, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 5: fwd_k<5, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 6: fwd_k<6, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 7: fwd_k<7, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 8: fwd_k<8, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 9: fwd_k<9, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 10: fwd_k<10, FLIP_T>(x, g, w, y, Lo, st); break;
+        default: fwd_k<11, FLIP_T>(x, g, w, y, Lo, st); break;
+    }
 }
 
 }  // namespace vt
@@ -209,8 +389,7 @@ int vt_conv1d_direct_fwd(const float* X, int B, int L_in, int Cin, const float* 
     VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAX && (mode == 0 || mode == 1),
                  "vt_conv1d_direct_fwd: shape (K <= %d)", KMAX);
     Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
-    dim3 grid((g.L_out + CT - 1) / CT, (Cout + CC - 1) / CC, B);
-    hipLaunchKernelGGL(k_conv_fwd<false>, grid, dim3(256), 0, S(stream), X, g, W, Y);
+    launch_fwd<false>(X, g, W, Y, g.L_out, S(stream));
     VT_LAUNCH_CHECK("vt_conv1d_direct_fwd");
     return VT_OK;
 }
@@ -220,35 +399,50 @@ int vt_conv1d_direct_fwd(const float* X, int B, int L_in, int Cin, const float* 
 // transposed / flipped taps.
 int vt_conv1d_direct_bwd_gpad(const float* dY, int B, int L_in, int Cin, const float* W, int Cout, int K, int mode,
                               int up, float* gpad, void* stream) {
-    VT_CHECK_ARG(B > 0 && K <= KMAX, "vt_conv1d_direct_bwd_gpad: shape");
+    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAX, "vt_conv1d_direct_bwd_gpad: shape");
     Geo f = geo(B, L_in, Cin, Cout, K, mode, up);
     // geometry of the "full" correlation: input = dY (L_out x Cout), causal pad K-1
     Geo g = geo(B, f.L_out, Cout, Cin, K, 0, 0);
-    g.L_out = f.L_out;  // kernel writes L_out + K - 1 rows (FLIP_T)
-    dim3 grid((f.L_out + K - 1 + CT - 1) / CT, (Cin + CC - 1) / CC, B);
-    hipLaunchKernelGGL(k_conv_fwd<true>, grid, dim3(256), 0, S(stream), dY, g, W, gpad);
+    launch_fwd<true>(dY, g, W, gpad, f.L_out + K - 1, S(stream));
     VT_LAUNCH_CHECK("vt_conv1d_direct_bwd_gpad");
     return VT_OK;
 }
 
 int vt_conv1d_direct_bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode,
                                 int up, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream) {
-    VT_CHECK_ARG(B > 0 && K <= KMAX, "vt_conv1d_direct_bwd_weight: shape");
+    VT_CHECK_ARG(B > 0 && L_in > 0 && K > 0 && K <= KMAX && Cin > 0 && Cout > 0 && Cin <= DW_CMAX &&
+                     Cout <= DW_CMAX,
+                 "vt_conv1d_direct_bwd_weight: shape (K <= %d, channels <= %d)", KMAX, DW_CMAX);
     Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
+    const int NTc = cdiv(Cin, 16), npairs = cdiv(Cout, 16) * NTc;
+    const int ppw = K <= 5 ? 4 : (K == 6 || K == 7 ? 3 : 2);  // pairs per wave (K accumulators each)
+    const int wpp = npairs >= 8 ? 1 : 8 / npairs;               // waves per pair for narrow layers
+    const int per_block = (8 / wpp) * (wpp > 1 ? 1 : ppw);
+    const int bx = cdiv(npairs, per_block);
     const int64_t rows = (int64_t)B * g.L_out;
-    const int tiles = ((Cout + CC - 1) / CC) * ((Cin + CI - 1) / CI);
     const int64_t nout = (int64_t)Cout * Cin * K;
-    int64_t splits = 1024 / tiles;
+    // ~512 workgroups, >= 4 row chunks each, partial slabs <= 8M floats and within the workspace
+    int64_t splits = 512 / bx;
+    if (splits * nout > (int64_t)8 << 20) splits = ((int64_t)8 << 20) / nout;
+    if (splits > rows / (4 * DR)) splits = rows / (4 * DR);
     if (splits < 1) splits = 1;
-    if (splits > rows / CT) splits = rows / CT > 0 ? rows / CT : 1;
     if (splits * nout > ws_floats) splits = ws_floats / nout;
     VT_CHECK_ARG(splits >= 1, "vt_conv1d_direct_bwd_weight: workspace too small");
     int64_t rps = (rows + splits - 1) / splits;
     splits = (rows + rps - 1) / rps;
-    dim3 grid((Cout + CC - 1) / CC, (Cin + CI - 1) / CI, (unsigned)splits);
-    hipLaunchKernelGGL(k_conv_dw, grid, dim3(256), 0, S(stream), dY, X, g, rps, ws);
-    hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, S(stream), ws, (int)splits,
-                       nout, dW, accumulate);
+    dim3 grid(bx, (unsigned)splits);
+    hipStream_t st = S(stream);
+    const int P = wpp > 1 ? 1 : ppw;
+#define VT_CONV_DW(KK, PP) \
+    if (K == KK && P == PP) \
+        hipLaunchKernelGGL((k_conv_dw<KK, PP>), grid, dim3(512), 0, st, dY, X, g, rps, NTc, npairs, wpp, ws);
+    VT_CONV_DW(1, 1) VT_CONV_DW(1, 4) VT_CONV_DW(2, 1) VT_CONV_DW(2, 4) VT_CONV_DW(3, 1) VT_CONV_DW(3, 4)
+    VT_CONV_DW(4, 1) VT_CONV_DW(4, 4) VT_CONV_DW(5, 1) VT_CONV_DW(5, 4) VT_CONV_DW(6, 1) VT_CONV_DW(6, 3)
+    VT_CONV_DW(7, 1) VT_CONV_DW(7, 3) VT_CONV_DW(8, 1) VT_CONV_DW(8, 2) VT_CONV_DW(9, 1) VT_CONV_DW(9, 2)
+    VT_CONV_DW(10, 1) VT_CONV_DW(10, 2) VT_CONV_DW(11, 1) VT_CONV_DW(11, 2)
+#undef VT_CONV_DW
+    hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, st, ws, (int)splits, nout, dW,
+                       accumulate);
     VT_LAUNCH_CHECK("vt_conv1d_direct_bwd_weight");
     return VT_OK;
 }
