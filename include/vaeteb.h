@@ -154,6 +154,12 @@ int vt_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K,
  * ones-column of X); split-K over R with a fixed-order reduction.              */
 int vt_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
                          int accumulate, float* ws, int64_t ws_floats, void* stream);
+/* Y = act(LayerNorm(X W^T + b; gamma, beta, eps)), N <= 256, also xhat and
+ * rstd (saved for vt_layernorm_bwd) — a ResidualMLP hidden layer
+ * Linear -> LayerNorm -> act (ref/model/vae_teb_model.py:336-403) in one pass:
+ * the LN statistics are taken in the GEMM epilogue.  act as vt_act_fwd.        */
+int vt_linear_ln_fwd(const float* X, int64_t R, int K, const float* W, int N, const float* bias, const float* gamma,
+                     const float* beta, int act, float eps, float* Y, float* xhat, float* rstd, void* stream);
 /* out[N] (+)= column sums of X[R,N]                                             */
 int vt_colsum(const float* X, int64_t R, int N, float* out, int accumulate, float* ws, int64_t ws_floats,
               void* stream);

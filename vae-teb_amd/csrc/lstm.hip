@@ -19,15 +19,32 @@ static constexpr int G4 = 4 * H;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic,
+// not for its global stores / prefetch loads (__syncthreads() would drain
+// vmcnt every time step and put an HBM round trip on the recurrence's
+// critical path).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+static constexpr int TS = 16;  // time steps per staged chunk
+
 // gin:   [B, S, 4H]  x W_ih^T + b_ih (precomputed)
 // out_h: [B, S, H]; out_hprev: [B, S, H] (h_{t-1}, zeros at t = 0)
 // out_c: [B, S, H] cell states; gates: [B, S, 4H] post-activation (i, f, g~, o)
+// The recurrence only touches LDS and registers: gin is loaded a chunk of TS
+// steps ahead into registers and the outputs of a chunk are staged in LDS and
+// written in one coalesced burst, so no global round trip sits between steps.
 __global__ __launch_bounds__(G4) void k_lstm_fwd(const float* __restrict__ gin, const float* __restrict__ whh,
                                                  const float* __restrict__ bhh, int S, float* __restrict__ out_h,
                                                  float* __restrict__ out_hprev, float* __restrict__ out_c,
                                                  float* __restrict__ gates) {
     __shared__ __attribute__((aligned(16))) float h[H];
     __shared__ float gb[G4];
+    __shared__ float og[TS * G4];                      // gates of the chunk
+    __shared__ float oh[TS * H], ohp[TS * H], oc[TS * H];
     const int j = threadIdx.x;
     const int64_t b = blockIdx.x;
     float w[H];
@@ -39,45 +56,72 @@ __global__ __launch_bounds__(G4) void k_lstm_fwd(const float* __restrict__ gin, 
     const float* g_in = gin + b * (int64_t)S * G4;
     float* gt = gates + b * (int64_t)S * G4;
     const int64_t hb = b * (int64_t)S * H;
-    float pre_next = g_in[j];
-    __syncthreads();
-    for (int t = 0; t < S; ++t) {
-        const float pre = pre_next;
-        if (t + 1 < S) pre_next = g_in[(int64_t)(t + 1) * G4 + j];
-        float a0 = pre + bias, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    float cur[TS], nxt[TS];
 #pragma unroll
-        for (int k = 0; k < H; k += 4) {
-            const float4 hv = *reinterpret_cast<const float4*>(&h[k]);
-            a0 = fmaf(w[k], hv.x, a0);
-            a1 = fmaf(w[k + 1], hv.y, a1);
-            a2 = fmaf(w[k + 2], hv.z, a2);
-            a3 = fmaf(w[k + 3], hv.w, a3);
+    for (int i = 0; i < TS; ++i) cur[i] = g_in[(int64_t)(i < S ? i : S - 1) * G4 + j];
+    lds_barrier();
+    for (int t0 = 0; t0 < S; t0 += TS) {
+#pragma unroll
+        for (int i = 0; i < TS; ++i) {  // unconditional (clamped) loads: no per-step waits
+            const int t = t0 + TS + i;
+            nxt[i] = g_in[(int64_t)(t < S ? t : S - 1) * G4 + j];
         }
-        const float a = (a0 + a1) + (a2 + a3);
-        const float v = (j >= 2 * H && j < 3 * H) ? tanhf(a) : sigm(a);
-        gb[j] = v;
-        gt[(int64_t)t * G4 + j] = v;
-        __syncthreads();
-        if (j < H) {
-            c = gb[H + j] * c + gb[j] * gb[2 * H + j];
-            const float hn = gb[3 * H + j] * tanhf(c);
-            out_hprev[hb + (int64_t)t * H + j] = h[j];
-            h[j] = hn;
-            out_h[hb + (int64_t)t * H + j] = hn;
-            out_c[hb + (int64_t)t * H + j] = c;
+        const int n = S - t0 < TS ? S - t0 : TS;
+#pragma unroll
+        for (int i = 0; i < TS; ++i) {
+            if (i >= n) continue;  // block-uniform
+            float a0 = cur[i] + bias, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+            for (int k = 0; k < H; k += 4) {
+                const float4 hv = *reinterpret_cast<const float4*>(&h[k]);
+                a0 = fmaf(w[k], hv.x, a0);
+                a1 = fmaf(w[k + 1], hv.y, a1);
+                a2 = fmaf(w[k + 2], hv.z, a2);
+                a3 = fmaf(w[k + 3], hv.w, a3);
+            }
+            const float a = (a0 + a1) + (a2 + a3);
+            const float v = (j >= 2 * H && j < 3 * H) ? tanhf(a) : sigm(a);
+            gb[j] = v;
+            og[i * G4 + j] = v;
+            lds_barrier();
+            if (j < H) {
+                c = gb[H + j] * c + gb[j] * gb[2 * H + j];
+                const float hn = gb[3 * H + j] * tanhf(c);
+                ohp[i * H + j] = h[j];
+                h[j] = hn;
+                oh[i * H + j] = hn;
+                oc[i * H + j] = c;
+            }
+            lds_barrier();
         }
-        __syncthreads();
+        // flush the chunk: contiguous rows of gates / h / h_prev / c
+        for (int idx = j; idx < n * G4; idx += G4) gt[(int64_t)t0 * G4 + idx] = og[idx];
+        for (int idx = j; idx < n * H; idx += G4) {
+            out_h[hb + (int64_t)t0 * H + idx] = oh[idx];
+            out_hprev[hb + (int64_t)t0 * H + idx] = ohp[idx];
+            out_c[hb + (int64_t)t0 * H + idx] = oc[idx];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < TS; ++i) cur[i] = nxt[i];
     }
 }
 
+static constexpr int TB = 8;  // backward steps per staged chunk
+
 // dh_out: [B, S, H] gradient arriving at this layer's outputs.
 // dgates: [B, S, 4H] gradient w.r.t. the gate pre-activations.
+// Chunks of TB steps (walking t downwards) of gates / c / dh_out are loaded
+// into registers one chunk ahead by all 256 threads and handed to LDS at the
+// chunk boundary; dgates of a chunk are staged in LDS and written in a burst.
 __global__ __launch_bounds__(G4) void k_lstm_bwd(const float* __restrict__ dh_out, const float* __restrict__ gates,
                                                  const float* __restrict__ cst, const float* __restrict__ whh, int S,
                                                  float* __restrict__ dgates) {
     __shared__ __attribute__((aligned(16))) float dg[G4];
     __shared__ float part[G4];
     __shared__ float dhr[H];
+    __shared__ float sg[TB * G4], sc[(TB + 1) * H], sdh[TB * H];  // chunk inputs
+    __shared__ float odg[TB * G4];                                 // chunk outputs
     const int j = threadIdx.x;
     const int q = j >> 6, k = j & 63;
     const int64_t b = blockIdx.x;
@@ -89,39 +133,80 @@ __global__ __launch_bounds__(G4) void k_lstm_bwd(const float* __restrict__ dh_ou
     const int64_t hb = b * (int64_t)S * H;
     const float* gt = gates + b * (int64_t)S * G4;
     float* dgo = dgates + b * (int64_t)S * G4;
-    __syncthreads();
-    for (int t = S - 1; t >= 0; --t) {
-        if (j < H) {
-            const float* g = gt + (int64_t)t * G4;
-            const float gi = g[j], gf = g[H + j], gg = g[2 * H + j], go = g[3 * H + j];
-            const float c = cst[hb + (int64_t)t * H + j];
-            const float cp = t > 0 ? cst[hb + (int64_t)(t - 1) * H + j] : 0.f;
-            const float dh = dh_out[hb + (int64_t)t * H + j] + dhr[j];
-            const float tc = tanhf(c);
-            const float d_o = dh * tc;
-            dc = dc + dh * go * (1.f - tc * tc);
-            const float di = dc * gg, dgg = dc * gi, df = dc * cp;
-            dc = dc * gf;
-            const float v0 = di * gi * (1.f - gi), v1 = df * gf * (1.f - gf);
-            const float v2 = dgg * (1.f - gg * gg), v3 = d_o * go * (1.f - go);
-            dg[j] = v0; dg[H + j] = v1; dg[2 * H + j] = v2; dg[3 * H + j] = v3;
-            float* o = dgo + (int64_t)t * G4;
-            o[j] = v0; o[H + j] = v1; o[2 * H + j] = v2; o[3 * H + j] = v3;
-        }
-        __syncthreads();
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    // chunk with steps [lo, lo + TB) (lo may be < 0 at the start of the sequence)
+    float rg[TB], rc[2], rdh[2];
+    auto fetch = [&](int lo) {
 #pragma unroll
-        for (int r = 0; r < H; r += 4) {
-            const float4 d = *reinterpret_cast<const float4*>(&dg[q * H + r]);
-            a0 = fmaf(wc[r], d.x, a0);
-            a1 = fmaf(wc[r + 1], d.y, a1);
-            a2 = fmaf(wc[r + 2], d.z, a2);
-            a3 = fmaf(wc[r + 3], d.w, a3);
+        for (int i = 0; i < TB; ++i) {
+            const int t = lo + i;
+            rg[i] = gt[(int64_t)(t >= 0 ? t : 0) * G4 + j];
         }
-        part[j] = (a0 + a1) + (a2 + a3);
-        __syncthreads();
-        if (j < H) dhr[j] = (part[j] + part[H + j]) + (part[2 * H + j] + part[3 * H + j]);
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // (TB + 1) x H cells (t = lo-1 .. lo+TB-1), TB x H dh
+            const int e = j + G4 * u;
+            const int ee = e < (TB + 1) * H ? e : 0;
+            const int tc = lo - 1 + ee / H;
+            rc[u] = cst[hb + (int64_t)(tc >= 0 ? tc : 0) * H + (ee % H)];
+            const int ed = e < TB * H ? e : 0;
+            const int td = lo + ed / H;
+            rdh[u] = dh_out[hb + (int64_t)(td >= 0 ? td : 0) * H + (ed % H)];
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int i = 0; i < TB; ++i) sg[i * G4 + j] = rg[i];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = j + G4 * u;
+            if (e < (TB + 1) * H) sc[e] = rc[u];
+            if (e < TB * H) sdh[e] = rdh[u];
+        }
+    };
+    int lo = S - TB;
+    fetch(lo);
+    for (; lo > -TB; lo -= TB) {
+        stash();
+        lds_barrier();
+        fetch(lo - TB);  // next chunk in flight during this one
+        for (int i = TB - 1; i >= 0; --i) {
+            const int t = lo + i;
+            if (t < 0) break;
+            if (j < H) {
+                const float gi = sg[i * G4 + j], gf = sg[i * G4 + H + j], gg = sg[i * G4 + 2 * H + j];
+                const float go = sg[i * G4 + 3 * H + j];
+                const float c = sc[(i + 1) * H + j], cp = t > 0 ? sc[i * H + j] : 0.f;
+                const float dh = sdh[i * H + j] + dhr[j];
+                const float tc = tanhf(c);
+                const float d_o = dh * tc;
+                dc = dc + dh * go * (1.f - tc * tc);
+                const float di = dc * gg, dgg = dc * gi, df = dc * cp;
+                dc = dc * gf;
+                const float v0 = di * gi * (1.f - gi), v1 = df * gf * (1.f - gf);
+                const float v2 = dgg * (1.f - gg * gg), v3 = d_o * go * (1.f - go);
+                dg[j] = v0; dg[H + j] = v1; dg[2 * H + j] = v2; dg[3 * H + j] = v3;
+                float* o = odg + i * G4;
+                o[j] = v0; o[H + j] = v1; o[2 * H + j] = v2; o[3 * H + j] = v3;
+            }
+            lds_barrier();
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+            for (int r = 0; r < H; r += 4) {
+                const float4 d = *reinterpret_cast<const float4*>(&dg[q * H + r]);
+                a0 = fmaf(wc[r], d.x, a0);
+                a1 = fmaf(wc[r + 1], d.y, a1);
+                a2 = fmaf(wc[r + 2], d.z, a2);
+                a3 = fmaf(wc[r + 3], d.w, a3);
+            }
+            part[j] = (a0 + a1) + (a2 + a3);
+            lds_barrier();
+            if (j < H) dhr[j] = (part[j] + part[H + j]) + (part[2 * H + j] + part[3 * H + j]);
+            lds_barrier();
+        }
+        // flush dgates of the chunk's valid steps
+        const int t_first = lo < 0 ? 0 : lo;
+        const int i0 = t_first - lo;
+        for (int idx = i0 * G4 + j; idx < TB * G4; idx += G4) dgo[(int64_t)lo * G4 + idx] = odg[idx];
+        lds_barrier();
     }
 }
 

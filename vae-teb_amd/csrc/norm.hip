@@ -169,6 +169,141 @@ __global__ __launch_bounds__(NT) void k_ln_bwd_wide(const float* __restrict__ dy
     }
 }
 
+// ---------------------------------------------- narrow LayerNorm (C <= 256)
+// 16 lanes per row (4 rows per wave, 16 per workgroup), lane l owns columns
+// l&15 + 16 j: the 64-wide ResidualMLP rows of 256 B are covered by one
+// instruction for 4 rows at once instead of a whole wave per row.
+__device__ __forceinline__ float sum16(float v) {
+    v += __shfl_xor(v, 1, 16);
+    v += __shfl_xor(v, 2, 16);
+    v += __shfl_xor(v, 4, 16);
+    v += __shfl_xor(v, 8, 16);
+    return v;
+}
+
+template <int CPL>  // columns per lane, C <= 16 * CPL
+__global__ __launch_bounds__(NT) void k_ln_fwd16(const float* __restrict__ x, int64_t R, int C,
+                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                 int act, float eps, float* __restrict__ y, float* __restrict__ xhat,
+                                                 float* __restrict__ rstd_out) {
+    const int lr = threadIdx.x & 15;
+    const int64_t row = (int64_t)blockIdx.x * (NT / 16) + (threadIdx.x >> 4);
+    const bool ok = row < R;
+    const float* xr = x + (ok ? row : 0) * C;
+    float v[CPL], s = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+        const int c = lr + 16 * j;
+        v[j] = (ok && c < C) ? xr[c] : 0.f;
+        s += v[j];
+    }
+    const float mean = sum16(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+        const int c = lr + 16 * j;
+        const float d = c < C ? v[j] - mean : 0.f;
+        q += d * d;
+    }
+    const float rstd = rsqrtf(sum16(q) / (float)C + eps);
+    if (!ok) return;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+        const int c = lr + 16 * j;
+        if (c >= C) continue;
+        const float h = (v[j] - mean) * rstd;
+        if (xhat) xhat[row * C + c] = h;
+        y[row * C + c] = act_f(h * gamma[c] + beta[c], act);
+    }
+    if (lr == 0 && rstd_out) rstd_out[row] = rstd;
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * act'(z) * gamma;
+// part[block][0:C] = sum dz*xhat, part[block][C:2C] = sum dz over the block's rows.
+template <int CPL>
+__global__ __launch_bounds__(NT) void k_ln_bwd16(const float* __restrict__ dy, const float* __restrict__ xhat,
+                                                 const float* __restrict__ rstd, int64_t R, int C,
+                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                 int act, int64_t rows_per_block, float* __restrict__ dx,
+                                                 float* __restrict__ part) {
+    __shared__ float red[NT / 64][2][16 * CPL];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 15, grp = threadIdx.x >> 4;
+    float gam[CPL], bet[CPL], dg[CPL], db[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+        const int c = lr + 16 * j;
+        gam[j] = c < C ? gamma[c] : 0.f;
+        bet[j] = c < C ? beta[c] : 0.f;
+        dg[j] = db[j] = 0.f;
+    }
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < R ? r0 + rows_per_block : R;
+    for (int64_t rb = r0; rb < r1; rb += NT / 16) {
+        const int64_t row = rb + grp;
+        const bool ok = row < r1;
+        const float* dyr = dy + (ok ? row : 0) * C;
+        const float* hr = xhat + (ok ? row : 0) * C;
+        float gv[CPL], hv[CPL], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+            const int c = lr + 16 * j;
+            gv[j] = hv[j] = 0.f;
+            if (ok && c < C) {
+                const float h = hr[c];
+                const float dz = dyr[c] * act_d(h * gam[j] + bet[j], act);
+                dg[j] += dz * h;
+                db[j] += dz;
+                gv[j] = dz * gam[j];
+                hv[j] = h;
+                s1 += gv[j];
+                s2 += gv[j] * h;
+            }
+        }
+        const float m1 = sum16(s1) / (float)C, m2 = sum16(s2) / (float)C;
+        if (!ok) continue;
+        const float rs = rstd[row];
+        float* dxr = dx + row * C;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+            const int c = lr + 16 * j;
+            if (c < C) dxr[c] = rs * (gv[j] - m1 - hv[j] * m2);
+        }
+    }
+    // column partials: the 4 row groups of a wave (lanes l, l^16, l^32), then the 4 waves
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+        dg[j] += __shfl_xor(dg[j], 16);
+        dg[j] += __shfl_xor(dg[j], 32);
+        db[j] += __shfl_xor(db[j], 16);
+        db[j] += __shfl_xor(db[j], 32);
+        if (lane < 16) {
+            red[w][0][lr + 16 * j] = dg[j];
+            red[w][1][lr + 16 * j] = db[j];
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += NT) {
+        part[(int64_t)blockIdx.x * 2 * C + c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+        part[(int64_t)blockIdx.x * 2 * C + C + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+    }
+}
+
+// out0[c] / out1[c - split] (+)= sum_b part[b][c], c < n: a wave per column
+// (lanes stride over the partial rows, then a fixed shuffle tree), 4 per workgroup
+__global__ __launch_bounds__(NT) void k_colred16(const float* __restrict__ part, int blocks, int n,
+                                                 float* __restrict__ out0, float* __restrict__ out1, int split,
+                                                 int accumulate) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+    if (c >= n) return;
+    float a = 0.f;
+    for (int b = lane; b < blocks; b += 64) a += part[(int64_t)b * n + c];
+    a = wave_sum(a);
+    if (lane != 0) return;
+    float* dst = c < split ? out0 + c : out1 + (c - split);
+    *dst = accumulate ? *dst + a : a;
+}
+
 // out[c] (+)= sum_b part[b][c] for c < n: one workgroup per column, threads
 // stride over the partials, fixed-order tree -> deterministic.
 __global__ __launch_bounds__(NT) void k_reduce_parts(const float* __restrict__ part, int blocks, int n,
@@ -322,6 +457,20 @@ extern "C" {
 int vt_layernorm_fwd(const float* x, int64_t R, int C, const float* gamma, const float* beta, int act, float eps,
                      float* y, float* xhat, float* rstd, void* stream) {
     VT_CHECK_ARG(R > 0 && C > 0 && act >= 0 && act <= 3, "vt_layernorm_fwd: shape/act");
+    if (C <= 256) {
+        const dim3 grid((unsigned)((R + NT / 16 - 1) / (NT / 16)));
+        hipStream_t st = S(stream);
+        if (C <= 32)
+            hipLaunchKernelGGL(k_ln_fwd16<2>, grid, dim3(NT), 0, st, x, R, C, gamma, beta, act, eps, y, xhat, rstd);
+        else if (C <= 64)
+            hipLaunchKernelGGL(k_ln_fwd16<4>, grid, dim3(NT), 0, st, x, R, C, gamma, beta, act, eps, y, xhat, rstd);
+        else if (C <= 128)
+            hipLaunchKernelGGL(k_ln_fwd16<8>, grid, dim3(NT), 0, st, x, R, C, gamma, beta, act, eps, y, xhat, rstd);
+        else
+            hipLaunchKernelGGL(k_ln_fwd16<16>, grid, dim3(NT), 0, st, x, R, C, gamma, beta, act, eps, y, xhat, rstd);
+        VT_LAUNCH_CHECK("vt_layernorm_fwd");
+        return VT_OK;
+    }
     hipLaunchKernelGGL(k_ln_fwd, dim3(blocks_for(R, NT / 64)), dim3(NT), 0, S(stream), x, R, C, gamma, beta, act, eps,
                        y, xhat, rstd);
     VT_LAUNCH_CHECK("vt_layernorm_fwd");
@@ -334,25 +483,32 @@ int vt_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, int6
                      float* ws, int64_t ws_floats, void* stream) {
     VT_CHECK_ARG(R > 0 && C > 0, "vt_layernorm_bwd: shape");
     hipStream_t st = S(stream);
-    if (C <= 512) {
+    if (C <= 256) {
+        int64_t blocks = (R + 63) / 64;  // 64 rows per workgroup (4 passes of 16 rows)
+        if (blocks > 1024) blocks = 1024;
+        if (blocks * 2 * C > ws_floats) blocks = ws_floats / (2 * C);
+        VT_CHECK_ARG(blocks >= 1, "vt_layernorm_bwd: workspace too small");
+        const int64_t rpb = (R + blocks - 1) / blocks;
+        blocks = (R + rpb - 1) / rpb;
+        const dim3 grid((unsigned)blocks);
+#define VT_LNB(CPL) hipLaunchKernelGGL(k_ln_bwd16<CPL>, grid, dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta, act, \
+                                       rpb, dx, ws)
+        if (C <= 32) VT_LNB(2);
+        else if (C <= 64) VT_LNB(4);
+        else if (C <= 128) VT_LNB(8);
+        else VT_LNB(16);
+#undef VT_LNB
+        hipLaunchKernelGGL(k_colred16, dim3((unsigned)((2 * C + 3) / 4)), dim3(NT), 0, st, ws, (int)blocks, 2 * C,
+                           dgamma, dbeta, C, accumulate_params);
+    } else if (C <= 512) {
         int64_t blocks = (R + 63) / 64;
         if (blocks > 1024) blocks = 1024;
         if (blocks * 2 * C > ws_floats) blocks = ws_floats / (2 * C);
         VT_CHECK_ARG(blocks >= 1, "vt_layernorm_bwd: workspace too small");
         const int64_t rpb = (R + blocks - 1) / blocks;
         blocks = (R + rpb - 1) / rpb;
-        if (C <= 64)
-            hipLaunchKernelGGL(k_ln_bwd<1>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
-                               act, rpb, dx, ws);
-        else if (C <= 128)
-            hipLaunchKernelGGL(k_ln_bwd<2>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
-                               act, rpb, dx, ws);
-        else if (C <= 256)
-            hipLaunchKernelGGL(k_ln_bwd<4>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
-                               act, rpb, dx, ws);
-        else
-            hipLaunchKernelGGL(k_ln_bwd<8>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
-                               act, rpb, dx, ws);
+        hipLaunchKernelGGL(k_ln_bwd<8>, dim3((unsigned)blocks), dim3(NT), 0, st, dy, xhat, rstd, R, C, gamma, beta,
+                           act, rpb, dx, ws);
         hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, ws, (int)blocks, 2 * C, dgamma,
                            dbeta, C, accumulate_params);
     } else {

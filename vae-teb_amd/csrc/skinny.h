@@ -1,0 +1,23 @@
+// Skinny fp32-MFMA linear kernels (mlp.hip), dispatched from the vt_linear_*
+// entry points of gemm.hip for widths <= 256.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vt {
+
+constexpr int SK_MAX_N = 256;   // output columns of k_sk_gemm (16 tiles)
+constexpr int SK_MAX_K1 = 144;  // K (+1 bias column) of k_sk_dw (9 tiles)
+
+int sk_linear_fwd(const float* X, int64_t R, int K, const float* W, int N, const float* bias, float* Y,
+                  hipStream_t st);
+int sk_linear_ln_fwd(const float* X, int64_t R, int K, const float* W, int N, const float* bias, const float* g,
+                     const float* beta, int act, float eps, float* Y, float* XH, float* RS, hipStream_t st);
+int sk_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K, float* dX, int accumulate,
+                       hipStream_t st);
+int64_t sk_dw_blocks(int64_t R);
+int64_t sk_dw_workspace(int64_t R, int N, int K);
+int sk_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
+                         int accumulate, float* ws, int64_t ws_floats, hipStream_t st);
+
+}  // namespace vt

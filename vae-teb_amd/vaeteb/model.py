@@ -97,7 +97,12 @@ class ResidualMLP(nn.Module):
         x0 = self.input_norm(x)
         h = x0
         for (idx, has_ln, act) in self._plan:
-            h = self.body[idx](h)
+            lin = self.body[idx]
+            if has_ln and not lin.mfma and ops.linear_ln_fused_ok(lin.in_features, lin.out_features):
+                ln = self.body[idx + 1]   # Linear -> LN -> act in one pass (vt_linear_ln_fwd)
+                h = ops.linear_ln_act(h, lin.weight, lin.bias, ln.weight, ln.bias, act, ln.eps)
+                continue
+            h = lin(h)
             if has_ln:
                 h = self.body[idx + 1](h, act)
         if self.use_skip_connection:

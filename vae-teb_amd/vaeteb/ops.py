@@ -46,6 +46,42 @@ def _check(*ts):
             raise TypeError(f"expected a CUDA float32 tensor, got {t.dtype} on {t.device}")
 
 
+# ----------------------------------------------------------- gradient sink
+# Parameters whose .grad is a persistent view of the trainer's flat gradient
+# buffer (vaeteb.train.FlatState sets p._vt_sink) receive their gradient
+# directly from the kernel, accumulated in place (the buffer is zeroed once
+# per step), and the op returns None to autograd for them: no per-parameter
+# AccumulateGrad add kernel (~540 launches per step).  GRAD_READY(p) is then
+# called instead of the post-accumulate-grad hook (bucketed all-reduce).
+GRAD_READY = None
+
+
+class _ParamGrads:
+    """Gradient destinations of an op's parameters: all their .grad sinks
+    (accumulate = 1) or, if any of them has none, fresh tensors (accumulate = 0)."""
+
+    def __init__(self, params, needed):
+        self.params, self.needed = params, needed
+        sinks = [p.grad if (n and getattr(p, "_vt_sink", False) and p.grad is not None and p.grad.is_contiguous())
+                 else None for p, n in zip(params, needed)]
+        self.direct = all(sk is not None for sk, n in zip(sinks, needed) if n) and any(needed)
+        if self.direct:
+            self.out = sinks
+        else:
+            self.out = [torch.empty_like(p) if n else None for p, n in zip(params, needed)]
+        self.acc = 1 if self.direct else 0
+
+    def result(self):
+        """What backward returns for the parameters (None when written in place)."""
+        if not self.direct:
+            return list(self.out)
+        if GRAD_READY is not None:
+            for p, n in zip(self.params, self.needed):
+                if n:
+                    GRAD_READY(p)
+        return [None] * len(self.params)
+
+
 # ------------------------------------------------------------------ Linear
 def mfma_ok(K, N):
     """bf16 MFMA path available for a K -> N linear (vt_mfma_supported)."""
@@ -90,19 +126,20 @@ class LinearF(torch.autograd.Function):
             call("vt_mfma_linear_fwd", ptr(x2), R, K, ptr(w16), N, ptr(b), ptr(y), ptr(ws), ws.numel(), _st())
         else:
             call("vt_linear_fwd", ptr(x2), R, K, ptr(w), N, ptr(b), ptr(y), _st())
-        ctx.save_for_backward(x2, w, w16t)
+        ctx.save_for_backward(x2, w16t)
+        ctx.w, ctx.b = w, b
         ctx.shape = x.shape
-        ctx.has_bias = b is not None
         ctx.mfma = mfma
         return y.reshape(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, gy):
-        x2, w, w16t = ctx.saved_tensors
+        x2, w16t = ctx.saved_tensors
+        w, b = ctx.w, ctx.b
         N, K = w.shape
         R = x2.shape[0]
         gy2 = gy.reshape(R, N).contiguous()
-        gx = gw = gb = None
+        gx = None
         ws = WS.get(WS_LINEAR, w.device, 1)
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x2)
@@ -112,18 +149,76 @@ class LinearF(torch.autograd.Function):
             else:
                 call("vt_linear_bwd_data", ptr(gy2), R, N, ptr(w), K, ptr(gx), 0, _st())
             gx = gx.reshape(ctx.shape)
-        want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if ctx.needs_input_grad[1]:
-            gw = torch.empty_like(w)
-            gb = torch.empty(N, device=w.device) if want_b else None
+        want_b = b is not None and ctx.needs_input_grad[2]
+        pg = _ParamGrads([w, b], [ctx.needs_input_grad[1], want_b])
+        gw_t, gb_t = pg.out
+        if gw_t is not None:
             pre = "vt_mfma_" if ctx.mfma else "vt_"
-            call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw), ptr(gb), 0, ptr(ws), ws.numel(),
-                 _st())
-        elif want_b:
-            gb = torch.empty(N, device=w.device)
-            ws = WS.get(2048 * N, w.device, 2)
-            call("vt_colsum", ptr(gy2), R, N, ptr(gb), 0, ptr(ws), ws.numel(), _st())
+            call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw_t), ptr(gb_t), pg.acc, ptr(ws),
+                 ws.numel(), _st())
+        elif gb_t is not None:
+            call("vt_colsum", ptr(gy2), R, N, ptr(gb_t), pg.acc, ptr(ws), ws.numel(), _st())
+        gw, gb = pg.result()
         return gx, gw, gb, None
+
+
+# ---------------------------------------------- fused Linear -> LN -> act
+class LinearLNActF(torch.autograd.Function):
+    """act(LayerNorm(x W^T + b)) — a ResidualMLP hidden layer
+    (ref/model/vae_teb_model.py:336-403) in one pass over the rows
+    (vt_linear_ln_fwd: the LN statistics are taken in the GEMM epilogue).
+    Backward: vt_layernorm_bwd, then the linear's input / weight gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, g, beta, act, eps):
+        _check(x, w, b, g, beta)
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = x.reshape(-1, K).contiguous()
+        R = x2.shape[0]
+        y = torch.empty((R, N), device=x.device)
+        xhat = torch.empty_like(y)
+        rstd = torch.empty(R, device=x.device)
+        call("vt_linear_ln_fwd", ptr(x2), R, K, ptr(w), N, ptr(b), ptr(g), ptr(beta), ACT[act], eps, ptr(y),
+             ptr(xhat), ptr(rstd), _st())
+        ctx.save_for_backward(x2, xhat, rstd)
+        ctx.params = (w, b, g, beta)
+        ctx.act, ctx.shape = act, x.shape
+        return y.reshape(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, xhat, rstd = ctx.saved_tensors
+        w, b, g, beta = ctx.params
+        N, K = w.shape
+        R = x2.shape[0]
+        gy2 = gy.reshape(R, N).contiguous()
+        gh = torch.empty_like(xhat)
+        nig = ctx.needs_input_grad
+        pln = _ParamGrads([g, beta], [True, True])
+        ws2 = WS.get(2 * N * max(1024, R if N > 512 else 0), x2.device, 2)
+        call("vt_layernorm_bwd", ptr(gy2), ptr(xhat), ptr(rstd), R, N, ptr(g), ptr(beta), ACT[ctx.act], ptr(gh),
+             ptr(pln.out[0]), ptr(pln.out[1]), pln.acc, ptr(ws2), ws2.numel(), _st())
+        gx = None
+        if nig[0]:
+            gx = torch.empty_like(x2)
+            call("vt_linear_bwd_data", ptr(gh), R, N, ptr(w), K, ptr(gx), 0, _st())
+            gx = gx.reshape(ctx.shape)
+        ws = WS.get(WS_LINEAR, x2.device, 1)
+        pl = _ParamGrads([w, b], [nig[1], b is not None and nig[2]])
+        gw_t, gb_t = pl.out
+        if gw_t is not None:
+            call("vt_linear_bwd_weight", ptr(gh), R, N, ptr(x2), K, ptr(gw_t), ptr(gb_t), pl.acc, ptr(ws), ws.numel(),
+                 _st())
+        elif gb_t is not None:
+            call("vt_colsum", ptr(gh), R, N, ptr(gb_t), pl.acc, ptr(ws), ws.numel(), _st())
+        gw, gb = pl.result()
+        gg, gbeta = pln.result()
+        return gx, gw, gb, gg, gbeta, None, None
+
+
+def linear_ln_fused_ok(K, N):
+    return N <= 256
 
 
 # -------------------------------------------------------- LayerNorm + act
@@ -138,21 +233,24 @@ class LayerNormActF(torch.autograd.Function):
         xhat = torch.empty_like(x2)
         rstd = torch.empty(R, device=x.device)
         call("vt_layernorm_fwd", ptr(x2), R, C, ptr(g), ptr(b), ACT[act], eps, ptr(y), ptr(xhat), ptr(rstd), _st())
-        ctx.save_for_backward(xhat, rstd, g, b)
+        ctx.save_for_backward(xhat, rstd)
+        ctx.params = (g, b)
         ctx.act, ctx.shape = act, x.shape
         return y.reshape(x.shape)
 
     @staticmethod
     def backward(ctx, gy):
-        xhat, rstd, g, b = ctx.saved_tensors
+        xhat, rstd = ctx.saved_tensors
+        g, b = ctx.params
         R, C = xhat.shape
         gy2 = gy.reshape(R, C).contiguous()
         gx = torch.empty_like(xhat)
-        gg, gbeta = torch.empty_like(g), torch.empty_like(b)
+        pg = _ParamGrads([g, b], [True, True])
         need = 2 * C * max(1024, R if C > 512 else 0)
         ws = WS.get(need, xhat.device, 2)
         call("vt_layernorm_bwd", ptr(gy2), ptr(xhat), ptr(rstd), R, C, ptr(g), ptr(b), ACT[ctx.act], ptr(gx),
-             ptr(gg), ptr(gbeta), 0, ptr(ws), ws.numel(), _st())
+             ptr(pg.out[0]), ptr(pg.out[1]), pg.acc, ptr(ws), ws.numel(), _st())
+        gg, gbeta = pg.result()
         return gx.reshape(ctx.shape), gg, gbeta, None, None
 
 
@@ -176,34 +274,38 @@ class ConvBNActF(torch.autograd.Function):
         ws = WS.get(4096 * Cout + 2 * Cout, x.device, 2)
         call("vt_batchnorm_fwd", ptr(conv), B * Lo, Cout, ptr(g), ptr(b), ACT[act], eps, momentum, ptr(y), ptr(mean),
              ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws), ws.numel(), _st())
-        ctx.save_for_backward(x, w, g, b, conv, mean, rstd)
+        ctx.save_for_backward(x, conv, mean, rstd)
+        ctx.params = (w, g, b)
         ctx.cfg = (mode, up, act)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w, g, b, conv, mean, rstd = ctx.saved_tensors
+        x, conv, mean, rstd = ctx.saved_tensors
+        w, g, b = ctx.params
         mode, up, act = ctx.cfg
         B, L, Cin = x.shape
         Cout, _, K = w.shape
         Lo = conv.shape[1]
         gy = gy.contiguous()
         gconv = torch.empty_like(conv)
-        gg, gb = torch.empty_like(g), torch.empty_like(b)
+        pbn = _ParamGrads([g, b], [True, True])
         ws = WS.get(4096 * Cout + 2 * Cout, x.device, 2)
         call("vt_batchnorm_bwd", ptr(gy), ptr(conv), B * Lo, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT[act],
-             ptr(gconv), ptr(gg), ptr(gb), 0, ptr(ws), ws.numel(), _st())
-        gx = gw = None
+             ptr(gconv), ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(ws), ws.numel(), _st())
+        gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             gpad = WS.get(B * (Lo + K - 1) * Cin, x.device, 3)
             call("vt_conv1d_direct_bwd_gpad", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gpad), _st())
             call("vt_conv1d_fold", ptr(gpad), B, L, Cin, Cout, K, mode, up, ptr(gx), 0, _st())
-        if ctx.needs_input_grad[1]:
-            gw = torch.empty_like(w)
+        pw = _ParamGrads([w], [ctx.needs_input_grad[1]])
+        if pw.out[0] is not None:
             ws1 = WS.get(WS_LINEAR, x.device, 1)
-            call("vt_conv1d_direct_bwd_weight", ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(gw), 0,
-                 ptr(ws1), ws1.numel(), _st())
+            call("vt_conv1d_direct_bwd_weight", ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]),
+                 pw.acc, ptr(ws1), ws1.numel(), _st())
+        gw, = pw.result()
+        gg, gb = pbn.result()
         return gx, gw, gg, gb, None, None, None, None, None, None, None
 
 
@@ -233,21 +335,20 @@ class LSTMF(torch.autograd.Function):
                  _st())
             saved += [inp, hp, c, gates]
             inp = h
-        ctx.save_for_backward(*saved, *params)
+        ctx.save_for_backward(*saved)
+        ctx.params = params
         ctx.nl = nl
         return inp
 
     @staticmethod
     def backward(ctx, gy):
-        t = ctx.saved_tensors
+        saved, params = ctx.saved_tensors, ctx.params
         nl = ctx.nl
-        saved, params = t[: 4 * nl], t[4 * nl:]
         gy = gy.contiguous()
         B, S, H = gy.shape
         grads = [None] * len(params)
         dh = gy
         ws = WS.get(WS_LINEAR, gy.device, 1)
-        wsb = WS.get(2048 * 4 * H, gy.device, 2)
         gx = None
         for l in reversed(range(nl)):
             inp, hp, c, gates = saved[4 * l: 4 * l + 4]
@@ -255,12 +356,15 @@ class LSTMF(torch.autograd.Function):
             In = inp.shape[-1]
             dg = torch.empty((B, S, 4 * H), device=gy.device)
             call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
-            gw_ih, gw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
-            gb = torch.empty_like(b_ih)
-            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(gw_ih), ptr(gb), 0, ptr(ws),
+            pw = _ParamGrads([w_ih, w_hh], [True, True])
+            # b_ih and b_hh receive the same gradient (sum of dg over rows): computed
+            # once into a fresh tensor (zeroed when the weights accumulate in place)
+            gb = torch.zeros_like(b_ih) if pw.acc else torch.empty_like(b_ih)
+            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), ptr(gb), pw.acc,
+                 ptr(ws), ws.numel(), _st())
+            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc, ptr(ws),
                  ws.numel(), _st())
-            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(gw_hh), None, 0, ptr(ws), ws.numel(),
-                 _st())
+            gw_ih, gw_hh = pw.result()
             grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, gb, gb.clone()]
             if l > 0 or ctx.needs_input_grad[0]:
                 gin = torch.empty((B, S, In), device=gy.device)
@@ -341,6 +445,10 @@ class OutputLossF(torch.autograd.Function):
 # ------------------------------------------------------------- functional API
 def linear(x, w, b=None, mfma=False):
     return LinearF.apply(x, w, b, mfma)
+
+
+def linear_ln_act(x, w, b, g, beta, act="none", eps=1e-5):
+    return LinearLNActF.apply(x, w, b, g, beta, act, eps)
 
 
 def layer_norm_act(x, g, b, act="none", eps=1e-5):

@@ -42,6 +42,7 @@ class FlatState:
                 self.p[o:o + n].copy_(p.reshape(-1))
                 p.data = self.p[o:o + n].view_as(p)
                 p.grad = self.g[o:o + n].view_as(p)
+                p._vt_sink = True  # HIP ops accumulate this gradient in place (vaeteb.ops._ParamGrads)
                 self.offsets.append((o, n))
                 o += n
 
@@ -74,13 +75,22 @@ class GradBuckets:
                 start, count = cur, 0
         self.pending = [0] * len(self.buckets)
         self.works = []
+        self.ready = set()
+        # torch ops reach the flat gradient through AccumulateGrad (hook); the HIP
+        # ops write it in place and report through vaeteb.ops.GRAD_READY
         self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in state.params]
+        from . import ops
+        ops.GRAD_READY = self._hook
 
     def reset(self):
         self.pending = [b[2] for b in self.buckets]
         self.works = []
+        self.ready = set()
 
     def _hook(self, p):
+        if id(p) in self.ready or id(p) not in self.param_bucket:
+            return  # each parameter counts once per step
+        self.ready.add(id(p))
         b = self.param_bucket[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
