@@ -164,6 +164,147 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
     for (int m = threadIdx.x; m < S; m += blockDim.x) o[m] = Rs[start + m].x * inv;
 }
 
+// ------------------------------------------- pairs, pruned 8192-point FFT
+// The low-pass keeps only bins [0, 512) of the 8192-point FFT of the padded
+// product (dec = 16), so the transform is decomposed 8192 = 16 x 16 x 32 in
+// place (decimation in frequency) and pruned:
+//   pass 1  radix-16 over n2 (stride 512), twiddle W_8192^{n1 k2}   (all data)
+//   pass 2  radix-16 over n1b (stride 32) inside each 512-block,
+//           twiddle W_512^{n1a k'b}                                  (all data)
+//   pass 3  only outputs k'a in {0, 1} of the last radix-32 stage   (2/32 of it)
+// giving X[k2 + 16 k'b + 256 k'a] = X[k], k < 512 — 3 register-DFT passes over
+// LDS instead of 6.5 Stockham passes, in ONE 66 KB buffer (no ping-pong), so
+// two workgroups share a CU.  The LDS image pads every 32 elements by one
+// (index k2*512 + 32 n1b + n1a -> k2*528 + 33 n1b + n1a): passes 2 and 3 read
+// it along n1a and along n1b without bank conflicts.
+static constexpr int PR_N = 8192, PR_NB = 512, PR_IMG = 16 * 16 * 33;
+
+__device__ __forceinline__ int pr_pos(int idx) {  // natural index -> padded LDS position
+    return (idx >> 5) * 33 + (idx & 31);
+}
+
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // a * (-i)
+
+// forward DFT-4 in place: X[k] = sum_n x[n] (-i)^{nk}
+__device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
+    const float2 s02 = cadd(x0, x2), d02 = csub(x0, x2), s13 = cadd(x1, x3), d13 = mul_mi(csub(x1, x3));
+    x0 = cadd(s02, s13);
+    x2 = csub(s02, s13);
+    x1 = cadd(d02, d13);
+    x3 = csub(d02, d13);
+}
+
+// forward DFT-16 in registers, natural order in and out (4 x 4, twiddles W_16)
+__device__ __forceinline__ void dft16(float2 v[16]) {
+#pragma unroll
+    for (int n0 = 0; n0 < 4; ++n0) dft4(v[n0], v[n0 + 4], v[n0 + 8], v[n0 + 12]);  // -> a[n0][k1] at v[n0 + 4 k1]
+    const float c1 = 0.92387953251128674f, s1 = 0.38268343236508977f, r2 = 0.70710678118654752f;
+    // v[n0 + 4 k1] *= W16^{n0 k1}
+    v[5] = cmul(v[5], make_float2(c1, -s1));
+    v[9] = cmul(v[9], make_float2(r2, -r2));
+    v[13] = cmul(v[13], make_float2(s1, -c1));
+    v[6] = cmul(v[6], make_float2(r2, -r2));
+    v[10] = mul_mi(v[10]);
+    v[14] = cmul(v[14], make_float2(-r2, -r2));
+    v[7] = cmul(v[7], make_float2(s1, -c1));
+    v[11] = cmul(v[11], make_float2(-r2, -r2));
+    v[15] = cmul(v[15], make_float2(-c1, s1));
+    float2 o[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        float2 a0 = v[4 * k1], a1 = v[4 * k1 + 1], a2 = v[4 * k1 + 2], a3 = v[4 * k1 + 3];
+        dft4(a0, a1, a2, a3);  // over n0 -> k0
+        o[k1] = a0;
+        o[k1 + 4] = a1;
+        o[k1 + 8] = a2;
+        o[k1 + 12] = a3;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = o[i];
+}
+
+__global__ __launch_bounds__(256) void k_fe_pairs8k(
+    const float2* __restrict__ analytic, int n_slots, int N, int pad_left, int n_pairs,
+    const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
+    const float2* __restrict__ tw, const float* __restrict__ phi0, int start, int S, int pad_mode,
+    float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2* img = sm;               // PR_IMG
+    float2* Z = sm + PR_IMG;        // PR_NB
+    float2* Z2 = Z + PR_NB;         // PR_NB
+    const int t = threadIdx.x;
+    const int pair = blockIdx.x;
+    const int64_t b = blockIdx.y;
+    const float2* ai = analytic + (b * n_slots + slot_i[pair]) * (int64_t)N;
+    const float2* aj = analytic + (b * n_slots + slot_j[pair]) * (int64_t)N;
+    const float pw = power[pair];
+    // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283), compact
+    for (int u = t; u < N; u += 256) {
+        const float2 x = ai[u], v = aj[u];
+        const float mag = sqrtf(x.x * x.x + x.y * x.y);
+        float sn, cs;
+        sincosf(atan2f(x.y, x.x) * pw, &sn, &cs);
+        img[u] = cmul(make_float2(mag * cs, mag * sn), cconj(v));
+    }
+    __syncthreads();
+    // 1: columns n1 = t, t + 256 of the padded signal (reflect / zero / circular)
+    float2 v[2][16];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int n1 = t + 256 * q;
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) {
+            const int s = pad_src(n1 + 512 * n2 - pad_left, N, pad_mode);
+            v[q][n2] = s < 0 ? make_float2(0.f, 0.f) : img[s];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int n1 = t + 256 * q;
+        dft16(v[q]);
+        img[pr_pos(n1)] = v[q][0];
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(n1 + 512 * k2)] = cmul(v[q][k2], tw[(n1 * k2) & (PR_N - 1)]);
+    }
+    __syncthreads();
+    // 2: jobs (k2, n1a): radix-16 over n1b inside block k2, in place
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int job = t + 256 * q, k2 = job >> 5, n1a = job & 31;
+        float2* base = img + k2 * 528 + n1a;
+        float2 w[16];
+#pragma unroll
+        for (int n1b = 0; n1b < 16; ++n1b) w[n1b] = base[33 * n1b];
+        dft16(w);
+        base[0] = w[0];
+#pragma unroll
+        for (int kb = 1; kb < 16; ++kb) base[33 * kb] = cmul(w[kb], tw[(16 * n1a * kb) & (PR_N - 1)]);
+    }
+    __syncthreads();
+    // 3: (k2, k'b) = (t >> 4, t & 15): outputs k'a = 0, 1 of the radix-32 stage
+    {
+        const int k2 = t >> 4, kb = t & 15;
+        const float2* row = img + k2 * 528 + 33 * kb;
+        float2 x0 = make_float2(0.f, 0.f), x1 = make_float2(0.f, 0.f);
+#pragma unroll 8
+        for (int n1a = 0; n1a < 32; ++n1a) {
+            const float2 z = row[n1a];
+            x0 = cadd(x0, z);
+            x1 = cadd(x1, cmul(z, tw[256 * n1a]));  // W_32^{n1a}
+        }
+        const int k = k2 + 16 * kb;
+        Z[k] = cscale(x0, phi0[k]);
+        Z[k + 256] = cscale(x1, phi0[k + 256]);
+    }
+    __syncthreads();
+    // 4: inverse FFT of length 512, keep [start, start + S)
+    float2* Rs = fft_lds<true>(Z, Z2, PR_NB, tw, PR_N / PR_NB);
+    float* o = out + (b * n_pairs + pair) * (int64_t)S;
+    const float inv = 1.0f / (float)PR_NB;
+    for (int m = t; m < S; m += 256) o[m] = Rs[start + m].x * inv;
+}
+
 // ---------------------------------------------------------------- normalise
 // in (B, C, S) raw -> out[b, s, off + c] with row width out_C.
 // kind: 0 = z-score only, 1 = log(max(x,0)+eps) then z, 2 = asinh then z.
@@ -302,9 +443,17 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
     VT_CHECK_ARG(dec == 0 ? S_out == N : (dec >= 1 && pow2(dec) && n_pad / dec >= start + S_out),
                  "vt_fe_pairs: dec/start (decimation must be a power of two)");
     VT_CHECK_ARG(B > 0 && n_pairs > 0 && pad_mode >= 0 && pad_mode <= 2, "vt_fe_pairs: empty/pad_mode");
-    hipLaunchKernelGGL(k_fe_pairs, dim3(n_pairs, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
-                       (const float2*)analytic, n_slots, N, n_pad, pad_left, n_pairs, slot_i, slot_j, power,
-                       (const float2*)tw, phi0, dec, start, S_out, pad_mode, out);
+    if (dec == PR_N / PR_NB && n_pad == PR_N && start + S_out <= PR_NB && N <= PR_IMG) {
+        // the training configuration (n_pad 8192, 512 low-pass bins): pruned transform
+        hipLaunchKernelGGL(k_fe_pairs8k, dim3(n_pairs, (unsigned)B), dim3(256),
+                           (PR_IMG + 2 * PR_NB) * sizeof(float2), S(stream), (const float2*)analytic, n_slots, N,
+                           pad_left, n_pairs, slot_i, slot_j, power, (const float2*)tw, phi0, start, S_out, pad_mode,
+                           out);
+    } else {
+        hipLaunchKernelGGL(k_fe_pairs, dim3(n_pairs, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
+                           (const float2*)analytic, n_slots, N, n_pad, pad_left, n_pairs, slot_i, slot_j, power,
+                           (const float2*)tw, phi0, dec, start, S_out, pad_mode, out);
+    }
     VT_LAUNCH_CHECK("vt_fe_pairs");
     return VT_OK;
 }

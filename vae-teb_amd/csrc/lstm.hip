@@ -107,7 +107,7 @@ __global__ __launch_bounds__(G4) void k_lstm_fwd(const float* __restrict__ gin, 
     }
 }
 
-static constexpr int TB = 8;  // backward steps per staged chunk
+static constexpr int TB = 8;  // backward steps per staged chunk (TB * H == 2 * G4 for the staging)
 
 // dh_out: [B, S, H] gradient arriving at this layer's outputs.
 // dgates: [B, S, 4H] gradient w.r.t. the gate pre-activations.
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(G4) void k_lstm_bwd(const float* __restrict__ dh_ou
     const float* gt = gates + b * (int64_t)S * G4;
     float* dgo = dgates + b * (int64_t)S * G4;
     // chunk with steps [lo, lo + TB) (lo may be < 0 at the start of the sequence)
-    float rg[TB], rc[2], rdh[2];
+    float rg[TB], rc[3], rdh[2];
     auto fetch = [&](int lo) {
 #pragma unroll
         for (int i = 0; i < TB; ++i) {
@@ -142,25 +142,29 @@ __global__ __launch_bounds__(G4) void k_lstm_bwd(const float* __restrict__ dh_ou
             rg[i] = gt[(int64_t)(t >= 0 ? t : 0) * G4 + j];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {  // (TB + 1) x H cells (t = lo-1 .. lo+TB-1), TB x H dh
+        for (int u = 0; u < 3; ++u) {  // (TB + 1) x H cells (t = lo-1 .. lo+TB-1)
             const int e = j + G4 * u;
             const int ee = e < (TB + 1) * H ? e : 0;
             const int tc = lo - 1 + ee / H;
             rc[u] = cst[hb + (int64_t)(tc >= 0 ? tc : 0) * H + (ee % H)];
-            const int ed = e < TB * H ? e : 0;
-            const int td = lo + ed / H;
-            rdh[u] = dh_out[hb + (int64_t)(td >= 0 ? td : 0) * H + (ed % H)];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // TB x H output gradients
+            const int e = j + G4 * u;
+            const int td = lo + e / H;
+            rdh[u] = dh_out[hb + (int64_t)(td >= 0 ? td : 0) * H + (e % H)];
         }
     };
     auto stash = [&]() {
 #pragma unroll
         for (int i = 0; i < TB; ++i) sg[i * G4 + j] = rg[i];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < 3; ++u) {
             const int e = j + G4 * u;
             if (e < (TB + 1) * H) sc[e] = rc[u];
-            if (e < TB * H) sdh[e] = rdh[u];
         }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) sdh[j + G4 * u] = rdh[u];
     };
     int lo = S - TB;
     fetch(lo);
