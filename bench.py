@@ -79,6 +79,20 @@ MFMA_CALLS = {
 MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of the roofline kernel from the latest committed
+    rocprofv3 PMC measurement (profiles/r*/pmc_traffic.json, written by
+    tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes of this
+    same bench command), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        if d.get("kernel") == kernel:
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def pair_kernel_bytes(fe, B):
     """Algorithmic HBM bytes of one vt_fe_pairs launch: read a_i and a_j
     (N complex64 each) per (sample, pair), write S float32 outputs."""
@@ -177,6 +191,7 @@ def main():
     value = samples / dt
     k_ms, k_n = timer.mean_ms("vt_fe_pairs")
     k_bytes = pair_kernel_bytes(fe, B)
+    traffic, traffic_src = pmc_traffic("k_fe_pairs8k") if (J, Q, T, B) == (11, 4, 16, 256) else (None, None)
     achieved = k_bytes / (k_ms * 1e-3) / 1e9
     out = {
         "metric": "train samples/sec + ELBO, 4096-pt windows, batch 256, 1/2/4/8 MI355X",
@@ -188,9 +203,11 @@ def main():
                                f"train step, batch {B}/GPU", "global_batch": B * world, "seq_len": N,
                    "parallelism": f"dp{world}"},
         "elbo": elbo,
-        "roofline": {"bound": "hbm", "kernel": "vt_fe_pairs", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "avg_launch_ms": round(k_ms, 4), "launches": k_n, "algorithmic_bytes": k_bytes},
+        "roofline": {"bound": "hbm", "kernel": "vt_fe_pairs (k_fe_pairs8k)", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_source": traffic_src, "avg_launch_ms": round(k_ms, 4), "launches": k_n,
+                     "algorithmic_bytes": k_bytes},
     }
     mfma_ms = timer.total_ms(list(MFMA_CALLS))
     if mfma_ms > 0:
