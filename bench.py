@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--frontend", choices=list(FRONTENDS), default="j11")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
+    ap.add_argument("--serial-encoders", action="store_true",
+                    help="run the source / target encoders on one stream (default: two HIP streams)")
     ap.add_argument("--heads", choices=["bf16", "fp32"], default="bf16",
                     help="decoder R x R head GEMMs: bf16 MFMA (the reference trains under 16-bit autocast) or fp32")
     args = ap.parse_args()
@@ -158,7 +160,8 @@ def main():
     S = plan.S
     torch.manual_seed(1234)  # same initial weights on every rank (DDP semantics)
     model = SeqVaeTeb(sequence_length=S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,
-                      cross_phase_channels=fe.C_x, head_precision=args.heads).to(dev)
+                      cross_phase_channels=fe.C_x, head_precision=args.heads,
+                      concurrent_encoders=not args.serial_encoders).to(dev)
     trainer = Trainer(model, lr=1e-3, frontend=fe, world_size=world)
 
     # synthetic windows resident in HBM before timing; global sample index ->

@@ -216,3 +216,28 @@ def test_tiny_c1_vs_reference_golden(golden):
     r["total"].backward()
     for i, (k, p) in enumerate(m.named_parameters()):
         assert rel(p.grad, torch.from_numpy(g[f"grad_{i}"])) < 1e-4, k
+
+
+def test_concurrent_encoders_bitwise_identical(golden):
+    """The two encoders on two HIP streams (SeqVaeTeb(concurrent_encoders=True))
+    give bit-identical losses, gradients and updated parameters to the serial
+    run: every reduction has a fixed order, so stream interleaving must not
+    change a single bit — and a missing cross-stream sync would."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    g = golden("model_s16_b4")
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    res = []
+    for conc in (False, True):
+        m = det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=conc)).cuda()
+        tr = Trainer(m, lr=1e-3)
+        batch = {"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}
+        for _ in range(2):
+            L = tr.step(batch, eps=T("eps"))
+        torch.cuda.synchronize()
+        res.append((L["total_loss"].item(), tr.state.g.clone(), tr.state.p.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])

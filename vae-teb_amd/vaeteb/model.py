@@ -295,8 +295,13 @@ class SeqVaeTeb(nn.Module):
 
     def __init__(self, input_channels=76, sequence_length=300, latent_dim_source=32, latent_dim_target=32,
                  latent_dim_z=32, decimation_factor=16, warmup_period=30, scattering_channels=43,
-                 phase_channels=44, cross_phase_channels=130, head_precision="fp32"):
+                 phase_channels=44, cross_phase_channels=130, head_precision="fp32", concurrent_encoders=False):
         super().__init__()
+        # the source and target encoders are independent until the conditional
+        # encoder: on a GPU they can run on two HIP streams (their LSTM
+        # recurrences use one workgroup per sample, a quarter of the chip each)
+        self.concurrent_encoders = concurrent_encoders
+        self._side = {}
         self.latent_dim_source, self.latent_dim_target, self.latent_dim_z = latent_dim_source, latent_dim_target, \
             latent_dim_z
         self.decimation_factor, self.warmup_period = decimation_factor, warmup_period
@@ -305,9 +310,26 @@ class SeqVaeTeb(nn.Module):
         self.conditional_encoder = ConditionalEncoder(latent_dim_source, latent_dim_target)
         self.decoder = Decoder(latent_dim_z, sequence_length, head_precision)
 
+    def side_stream(self, device):
+        s = self._side.get(device)
+        if s is None:
+            s = self._side[device] = torch.cuda.Stream(device=device)
+            ops.SIDE_STREAMS.append(s)
+        return s
+
     def forward(self, y_st, y_ph, x_ph, eps=None):
-        mu_x = self.source_encoder(x_ph)
-        mu_y, logvar_y_full = self.target_encoder(y_st, y_ph)
+        if self.concurrent_encoders and x_ph.is_cuda:
+            main = torch.cuda.current_stream(x_ph.device)
+            side = self.side_stream(x_ph.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                mu_x = self.source_encoder(x_ph)
+            mu_y, logvar_y_full = self.target_encoder(y_st, y_ph)
+            main.wait_stream(side)
+            mu_x.record_stream(main)
+        else:
+            mu_x = self.source_encoder(x_ph)
+            mu_y, logvar_y_full = self.target_encoder(y_st, y_ph)
         logvar_y_prior, c_logvar = torch.split(logvar_y_full, self.latent_dim_target, dim=-1)
         mu_c, logvar_post = self.conditional_encoder(mu_x, c_logvar)
         if eps is None:

@@ -17,14 +17,15 @@ ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 
 # --------------------------------------------------------------- workspace
 class _Workspace:
-    """Grow-only scratch per device; ops are stream-ordered on the current
-    stream, so consecutive ops may reuse it."""
+    """Grow-only scratch per (device, stream); ops are stream-ordered on the
+    current stream, so consecutive ops on one stream may reuse it, and ops on
+    concurrent streams (the two encoders) never share it."""
 
     def __init__(self):
         self.buf = {}
 
     def get(self, nfloats, device, slot=0):
-        key = (str(device), slot)
+        key = (str(device), slot, torch.cuda.current_stream(device).cuda_stream if torch.cuda.is_available() else 0)
         b = self.buf.get(key)
         if b is None or b.numel() < nfloats:
             b = torch.empty(max(int(nfloats), 1 << 20), dtype=torch.float32, device=device)
@@ -54,6 +55,7 @@ def _check(*ts):
 # AccumulateGrad add kernel (~540 launches per step).  GRAD_READY(p) is then
 # called instead of the post-accumulate-grad hook (bucketed all-reduce).
 GRAD_READY = None
+SIDE_STREAMS = []   # extra streams the model runs work on (see SeqVaeTeb.concurrent_encoders)
 
 
 class _ParamGrads:

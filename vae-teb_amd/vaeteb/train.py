@@ -86,6 +86,8 @@ class GradBuckets:
         self.pending = [b[2] for b in self.buckets]
         self.works = []
         self.ready = set()
+        from . import ops
+        self.streams = [torch.cuda.current_stream()] + list(ops.SIDE_STREAMS) if torch.cuda.is_available() else []
 
     def _hook(self, p):
         if id(p) in self.ready or id(p) not in self.param_bucket:
@@ -94,6 +96,12 @@ class GradBuckets:
         b = self.param_bucket[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
+            # a bucket's gradients may have been written on several streams (the
+            # concurrent encoders): the collective waits for all of them
+            cur = torch.cuda.current_stream() if self.streams else None
+            for st in self.streams:
+                if st != cur:
+                    cur.wait_stream(st)
             s, e, _ = self.buckets[b]
             self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
                                               async_op=True))
@@ -147,6 +155,13 @@ class Trainer:
             self.buckets.reset()
         losses = self.loss(batch, eps)
         losses["total_loss"].backward()
+        if torch.cuda.is_available():
+            # gradients written in place on side streams (no AccumulateGrad, so
+            # autograd does not join those streams for us)
+            from . import ops
+            main = torch.cuda.current_stream()
+            for st in ops.SIDE_STREAMS:
+                main.wait_stream(st)
         if self.buckets:
             self.buckets.finish()
         self.steps += 1
