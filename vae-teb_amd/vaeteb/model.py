@@ -18,6 +18,51 @@ import torch.nn as nn
 from . import ops
 
 
+# ----------------------------------------------------------- stream forks
+# SeqVaeTeb(concurrent_encoders=True) runs independent branches of the graph
+# (source / target encoder, the target encoder's scattering / phase branches,
+# the conditional encoder's and the decoder's mu / logvar heads) on side HIP
+# streams.  Every reduction has a fixed order, so results are bit-identical
+# to the serial run (tests/test_gpu_model.py).
+_PAR = {"on": False, "next": 1}
+_SIDE = {}
+
+
+def side_stream(device, i):
+    s = _SIDE.get((device, i))
+    if s is None:
+        s = _SIDE[(device, i)] = torch.cuda.Stream(device=device)
+        ops.SIDE_STREAMS.append(s)
+    return s
+
+
+def fork(*thunks):
+    """Run thunks[0] on the current stream and thunks[i] on side stream i; the
+    current stream waits for all of them.  Serial unless a concurrent model is
+    running on a GPU."""
+    if not _PAR["on"]:
+        return [t() for t in thunks]
+    dev = torch.cuda.current_device()
+    main = torch.cuda.current_stream()
+    outs = [None] * len(thunks)
+    sides = []
+    for i, t in enumerate(thunks[1:], 1):
+        st = side_stream(dev, _PAR["next"])  # each fork of a forward pass gets its own side stream
+        _PAR["next"] += 1
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            outs[i] = t()
+        sides.append(st)
+    outs[0] = thunks[0]()
+    for st in sides:
+        main.wait_stream(st)
+    for o in outs[1:]:
+        for t in (o if isinstance(o, (tuple, list)) else (o,)):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(main)
+    return outs
+
+
 def geometric_schedule(input_size, output_size, n_hidden, round_fn=round):
     """ref/model/vae_teb_model.py:11-44 (repeated-multiplication ratio, as there)."""
     r = (output_size / input_size) ** (1 / (n_hidden + 1))
@@ -232,8 +277,8 @@ class TargetEncoder(nn.Module):
         self.logvar_layer = ResidualMLP(32, geometric_schedule(32, 64, 4), final_activation=False)
 
     def forward(self, y_st, y_ph):
-        a = self.scatter_fused_norm(self.conv_scattering(self.mlp_scattering(y_st)))
-        b = self.phase_fused_norm(self.conv_phase(self.mlp_phase(y_ph)))
+        a, b = fork(lambda: self.scatter_fused_norm(self.conv_scattering(self.mlp_scattering(y_st))),
+                    lambda: self.phase_fused_norm(self.conv_phase(self.mlp_phase(y_ph))))
         h = self.lstm(self.cross_modal_fusion(torch.cat([a, b], dim=-1)))
         h = self.pre_output(self.lstm_norm(h))
         return self.mu_layer(h), torch.clamp(self.logvar_layer(h), -10, 10)
@@ -251,7 +296,8 @@ class ConditionalEncoder(nn.Module):
 
     def forward(self, h_x, h_y):
         h = self.mlp(torch.cat([h_x, h_y], dim=-1))
-        return self.fc_mu(h), self.fc_logvar(h)
+        mu, lv = fork(lambda: self.fc_mu(h), lambda: self.fc_logvar(h))
+        return mu, lv
 
 
 class Decoder(nn.Module):
@@ -287,7 +333,8 @@ class Decoder(nn.Module):
         lin = self.linear(z)                       # (B, S, 87)
         x = self.conv(lin)                         # (B, 16S, 1)
         x = x.reshape(x.shape[0], -1)              # flatten (B, 16S)
-        return lin, self.output_mu(x), self.output_logvar(x)
+        mu, lv = fork(lambda: self.output_mu(x), lambda: self.output_logvar(x))
+        return lin, mu, lv
 
 
 class SeqVaeTeb(nn.Module):
@@ -301,7 +348,6 @@ class SeqVaeTeb(nn.Module):
         # encoder: on a GPU they can run on two HIP streams (their LSTM
         # recurrences use one workgroup per sample, a quarter of the chip each)
         self.concurrent_encoders = concurrent_encoders
-        self._side = {}
         self.latent_dim_source, self.latent_dim_target, self.latent_dim_z = latent_dim_source, latent_dim_target, \
             latent_dim_z
         self.decimation_factor, self.warmup_period = decimation_factor, warmup_period
@@ -310,26 +356,17 @@ class SeqVaeTeb(nn.Module):
         self.conditional_encoder = ConditionalEncoder(latent_dim_source, latent_dim_target)
         self.decoder = Decoder(latent_dim_z, sequence_length, head_precision)
 
-    def side_stream(self, device):
-        s = self._side.get(device)
-        if s is None:
-            s = self._side[device] = torch.cuda.Stream(device=device)
-            ops.SIDE_STREAMS.append(s)
-        return s
-
     def forward(self, y_st, y_ph, x_ph, eps=None):
-        if self.concurrent_encoders and x_ph.is_cuda:
-            main = torch.cuda.current_stream(x_ph.device)
-            side = self.side_stream(x_ph.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                mu_x = self.source_encoder(x_ph)
-            mu_y, logvar_y_full = self.target_encoder(y_st, y_ph)
-            main.wait_stream(side)
-            mu_x.record_stream(main)
-        else:
-            mu_x = self.source_encoder(x_ph)
-            mu_y, logvar_y_full = self.target_encoder(y_st, y_ph)
+        prev = dict(_PAR)
+        _PAR["on"], _PAR["next"] = bool(self.concurrent_encoders and x_ph.is_cuda), 1
+        try:
+            return self._forward(y_st, y_ph, x_ph, eps)
+        finally:
+            _PAR.update(prev)
+
+    def _forward(self, y_st, y_ph, x_ph, eps):
+        (mu_y, logvar_y_full), mu_x = fork(lambda: self.target_encoder(y_st, y_ph),
+                                           lambda: self.source_encoder(x_ph))
         logvar_y_prior, c_logvar = torch.split(logvar_y_full, self.latent_dim_target, dim=-1)
         mu_c, logvar_post = self.conditional_encoder(mu_x, c_logvar)
         if eps is None:
