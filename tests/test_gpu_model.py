@@ -241,3 +241,29 @@ def test_concurrent_encoders_bitwise_identical(golden):
         res.append((L["total_loss"].item(), tr.state.g.clone(), tr.state.p.clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+def test_concurrent_frontend_and_encoders_bitwise_identical():
+    """Raw windows -> front-end (cross pairs on the source encoder's stream) ->
+    model step: bit-identical to the all-serial run."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vaeteb import synthetic
+    from vaeteb.frontend import FrontEnd, FrontEndPlan, load_stats
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    plan = FrontEndPlan(11, 4, 16, 4096, device="cuda")
+    fe = FrontEnd(plan, load_stats(11, 4, 16, 4096))
+    x = torch.from_numpy(synthetic.batch(5, 4, 4096)).cuda()
+    res = []
+    for conc in (False, True):
+        torch.manual_seed(0)
+        m = SeqVaeTeb(sequence_length=plan.S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,
+                      cross_phase_channels=fe.C_x, concurrent_encoders=conc).cuda()
+        tr = Trainer(m, lr=1e-3, frontend=fe)
+        eps = torch.randn(4, plan.S, 32, generator=torch.Generator().manual_seed(1)).cuda()
+        L = tr.step({"x": x}, eps=eps)
+        torch.cuda.synchronize()
+        res.append((L["total_loss"].item(), tr.state.g.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])

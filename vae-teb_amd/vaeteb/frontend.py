@@ -199,31 +199,44 @@ class FrontEnd:
             self._bufs[name] = b
         return b
 
-    def raw(self, x):
+    def raw(self, x, side=None):
         """x (B, 2, N) float32 on device -> raw (un-normalised) features
-        {'fhr_st': (B,43,S), 'pairs': (B, 44+130, S)} as the reference stores them."""
+        {'fhr_st': (B,43,S), 'pairs': (B, 44+130, S)} as the reference stores them.
+        With a side stream, the cross pairs (the source encoder's input) are
+        computed there concurrently with the phase pairs and returned separately
+        as 'cross' (B, 130, S); the caller's stream does not wait for them."""
         p, t = self.plan, self.tab
         if x.dim() != 3 or x.shape[1] != 2 or x.shape[2] != p.N:
             raise ValueError(f"expected (B, 2, {p.N}) windows, got {tuple(x.shape)}")
         x = x.contiguous()
         B = x.shape[0]
-        st = _lib.stream()
         xhat = self._buf("xhat", (B, 2, p.n_pad, 2))
         launch_spectrum(p, x, B * 2, 0, xhat)
         s_raw = self._buf("s_raw", (B, self.C_st, p.S))
         launch_lowpass(p, x, B, 2 * p.N, s_raw, self.C_st * p.S)
         an = self._buf("analytic", (B, t["n_slots"], p.N, 2))
         launch_wavelet(p, xhat, B, 2, t, an, s_raw, self.C_st)
-        pr = self._buf("pairs", (B, t["n_pairs"], p.pair_len))
-        launch_pairs(p, an, B, t, pr, lowpass=True, pad_mode=0)
-        return {"fhr_st": s_raw, "pairs": pr}
+        if side is None or not self.C_ph or not self.C_x:
+            pr = self._buf("pairs", (B, t["n_pairs"], p.pair_len))
+            launch_pairs(p, an, B, t, pr, lowpass=True, pad_mode=0)
+            return {"fhr_st": s_raw, "pairs": pr}
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)               # analytic signals ready
+        pr = self._buf("pairs_ph", (B, self.C_ph, p.pair_len))
+        launch_pairs(p, an, B, _sub_table(t, 0, self.C_ph), pr, lowpass=True, pad_mode=0)
+        with torch.cuda.stream(side):
+            px = self._buf("pairs_x", (B, self.C_x, p.pair_len))
+            launch_pairs(p, an, B, _sub_table(t, self.C_ph, self.C_x), px, lowpass=True, pad_mode=0)
+        return {"fhr_st": s_raw, "pairs": pr, "cross": px}
 
-    def __call__(self, x, out=None):
-        """Normalised model inputs (AttributeDict fields of the reference batch)."""
+    def __call__(self, x, out=None, side=None):
+        """Normalised model inputs (AttributeDict fields of the reference batch).
+        side: optional HIP stream for the source encoder's input (fhr_up_ph is
+        then produced on that stream; see SeqVaeTeb(concurrent_encoders))."""
         if self.stats is None:
             raise RuntimeError("FrontEnd needs normalisation statistics (set_stats)")
         p = self.plan
-        r = self.raw(x)
+        r = self.raw(x, side)
         B, S = x.shape[0], p.S
         st = _lib.stream()
         out = {} if out is None else out
@@ -243,11 +256,25 @@ class FrontEnd:
                       _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(y_ph), self.C_ph, 0, st)
         if self.C_x:
             k, m, s = self.stats["fhr_up_ph"]
-            _lib.call("vt_fe_normalize", pairs[:, self.C_ph:].data_ptr(), B, self.C_x, pairs.shape[1], S,
-                      _lib.ptr(k), _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(x_ph), self.C_x, 0, st)
+            if "cross" in r:
+                with torch.cuda.stream(side):
+                    _lib.call("vt_fe_normalize", r["cross"].data_ptr(), B, self.C_x, self.C_x, S, _lib.ptr(k),
+                              _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(x_ph), self.C_x, 0, _lib.stream())
+                x_ph.record_stream(side)
+            else:
+                _lib.call("vt_fe_normalize", pairs[:, self.C_ph:].data_ptr(), B, self.C_x, pairs.shape[1], S,
+                          _lib.ptr(k), _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(x_ph), self.C_x, 0, st)
         fm, fs = self.stats["fhr"]
         _lib.call("vt_normalize_raw", _lib.ptr(x), B, 2 * p.N, p.N, fm, fs, _lib.ptr(y_raw), st)
         return {"fhr_st": y_st, "fhr_ph": y_ph, "fhr_up_ph": x_ph, "fhr": y_raw}
+
+
+def _sub_table(t, first, count):
+    """Pair table restricted to pairs [first, first + count) (views, no copy)."""
+    s = dict(t)
+    s["slot_i"], s["slot_j"], s["power"] = (t[k][first:first + count] for k in ("slot_i", "slot_j", "power"))
+    s["n_pairs"] = count
+    return s
 
 
 def load_stats(J=11, Q=4, T=16, N=4096):

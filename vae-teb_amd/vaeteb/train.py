@@ -142,7 +142,12 @@ class Trainer:
         fhr_ph, fhr_up_ph (B,S,C) and fhr (B,R) (the reference batch contract,
         ref/model/graph_model.py:702-705), or raw windows under key 'x'."""
         if "x" in batch:
-            batch = self.frontend(batch["x"])
+            side = None
+            if getattr(self.model, "concurrent_encoders", False) and batch["x"].is_cuda:
+                from .model import side_stream
+                side = side_stream(batch["x"].device.index if batch["x"].device.index is not None else
+                                   torch.cuda.current_device(), 1)  # the source encoder's stream
+            batch = self.frontend(batch["x"], side=side)
         fw = self.model(batch["fhr_st"], batch["fhr_ph"], batch["fhr_up_ph"], eps=eps)
         return self.model.compute_loss(fw, batch["fhr_st"], batch["fhr_ph"], batch["fhr"], compute_kld_loss=True,
                                        beta=self.beta_kld)
