@@ -137,6 +137,11 @@ int vt_grad_norm_clip(const float* g, int64_t n, float pre_scale, float max_norm
  *           ref/model/pytorch_lightning_modules.py:540-546                       */
 int vt_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                   float eps, float weight_decay, int step, const float* gscale, void* stream);
+/* Same update with the step counter on the device (int[1], incremented in
+ * place; coef: float[2] scratch) — no host scalar changes between steps, so a
+ * whole training step can be captured once in a hipGraph and replayed.          */
+int vt_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                      float eps, float weight_decay, int* step, float* coef, const float* gscale, void* stream);
 /* bf16 (RNE) shadow copy of fp32 data, for MFMA operands.                         */
 int vt_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
 

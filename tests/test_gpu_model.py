@@ -267,3 +267,35 @@ def test_concurrent_frontend_and_encoders_bitwise_identical():
         res.append((L["total_loss"].item(), tr.state.g.clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("concurrent", [False, True])
+def test_graph_replay_bitwise_identical_to_eager(golden, concurrent):
+    """Trainer.capture/replay (the whole step as one hipGraph) == eager steps,
+    bit for bit, over several steps (device-side AdamW step counter, static
+    inputs refreshed per replay, side streams joined inside the graph)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    g = golden("model_s16_b4")
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    b0 = {"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}
+    b1 = {k: v.flip(0).contiguous() for k, v in b0.items()}
+    eps = T("eps")
+    res = []
+    for graph in (False, True):
+        m = det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=concurrent)).cuda()
+        tr = Trainer(m, lr=1e-3)
+        if graph:
+            tr.capture(b0, eps=eps, warmup=2)
+            outs = [tr.replay(b, eps=eps)["total_loss"].item() for b in (b1, b0, b1)]
+        else:
+            for _ in range(2):
+                tr.step(b0, eps=eps)
+            outs = [tr.step(b, eps=eps)["total_loss"].item() for b in (b1, b0, b1)]
+        torch.cuda.synchronize()
+        res.append((outs, tr.state.p.clone(), tr.state.m.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])

@@ -63,8 +63,13 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw(float* __restrict__ p, co
                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                        float lr, float beta1, float beta2, float eps, float wd,
                                                        float step_size, float bc2_sqrt,
-                                                       const float* __restrict__ gscale) {
+                                                       const float* __restrict__ gscale,
+                                                       const float* __restrict__ coef) {
     const float gs = gscale ? gscale[0] : 1.0f;
+    if (coef) {  // device-side step (graph-capturable): coef = {lr / bc1, sqrt(bc2)}
+        step_size = coef[0];
+        bc2_sqrt = coef[1];
+    }
     const float decay = 1.0f - lr * wd;
     const float w1 = 1.0f - beta1, w2 = 1.0f - beta2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -78,6 +83,16 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw(float* __restrict__ p, co
         m[i] = mi;
         v[i] = vi;
     }
+}
+
+// step += 1; coef = {lr / (1 - b1^step), sqrt(1 - b2^step)} in fp64 (as the host path)
+__global__ void k_adamw_coef(int* step, float lr, float beta1, float beta2, float* coef) {
+    const int s = step[0] + 1;
+    step[0] = s;
+    const double bc1 = 1.0 - pow((double)beta1, (double)s);
+    const double bc2 = 1.0 - pow((double)beta2, (double)s);
+    coef[0] = (float)((double)lr / bc1);
+    coef[1] = (float)sqrt(bc2);
 }
 
 // bf16 shadow of the parameters for the MFMA GEMM operands (round-to-nearest-even).
@@ -117,8 +132,18 @@ int vt_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
     hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, S(stream), p, g, m, v, n, lr, beta1,
-                       beta2, eps, weight_decay, (float)((double)lr / bc1), (float)sqrt(bc2), gscale);
+                       beta2, eps, weight_decay, (float)((double)lr / bc1), (float)sqrt(bc2), gscale, nullptr);
     VT_LAUNCH_CHECK("vt_adamw_step");
+    return VT_OK;
+}
+
+int vt_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                      float eps, float weight_decay, int* step, float* coef, const float* gscale, void* stream) {
+    VT_CHECK_ARG(n > 0 && step && coef, "vt_adamw_step_dev: args");
+    hipLaunchKernelGGL(k_adamw_coef, dim3(1), dim3(1), 0, S(stream), step, lr, beta1, beta2, coef);
+    hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, S(stream), p, g, m, v, n, lr, beta1,
+                       beta2, eps, weight_decay, 0.f, 1.f, gscale, coef);
+    VT_LAUNCH_CHECK("vt_adamw_step_dev");
     return VT_OK;
 }
 

@@ -76,6 +76,7 @@ class GradBuckets:
         self.pending = [0] * len(self.buckets)
         self.works = []
         self.ready = set()
+        self.enabled = True   # False while a hipGraph is captured: no collective inside the graph
         # torch ops reach the flat gradient through AccumulateGrad (hook); the HIP
         # ops write it in place and report through vaeteb.ops.GRAD_READY
         self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in state.params]
@@ -89,8 +90,15 @@ class GradBuckets:
         from . import ops
         self.streams = [torch.cuda.current_stream()] + list(ops.SIDE_STREAMS) if torch.cuda.is_available() else []
 
+    def reduce_all(self):
+        """All buckets at once (after a graph replay of the backward)."""
+        for b, (s, e, _) in enumerate(self.buckets):
+            self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True))
+            self.pending[b] = 0
+
     def _hook(self, p):
-        if id(p) in self.ready or id(p) not in self.param_bucket:
+        if not self.enabled or id(p) in self.ready or id(p) not in self.param_bucket:
             return  # each parameter counts once per step
         self.ready.add(id(p))
         b = self.param_bucket[id(p)]
@@ -134,6 +142,9 @@ class Trainer:
         self.steps = 0
         dev = self.state.p.device
         self.norm_out = torch.zeros(2, device=dev)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)   # AdamW step counter (device side)
+        self.adam_coef = torch.zeros(2, device=dev)
+        self.graph = None
         self.norm_ws = torch.empty(_lib.lib().fns["vt_grad_norm_workspace_floats"](), device=dev)
         self.buckets = GradBuckets(self.state, group, bucket_mb) if world_size > 1 else None
 
@@ -154,10 +165,19 @@ class Trainer:
 
     def step(self, batch, eps=None):
         """One optimisation step; returns the loss dict (device scalars, no sync)."""
+        losses = self._forward_backward(batch, eps, overlap_comm=True)
+        if self.buckets:
+            self.buckets.finish()
+        self._update()
+        losses["grad_norm"] = self.norm_out[0]
+        return losses
+
+    def _forward_backward(self, batch, eps, overlap_comm):
         self.model.train()
         self.state.zero_grad()
         if self.buckets:
             self.buckets.reset()
+            self.buckets.enabled = overlap_comm
         losses = self.loss(batch, eps)
         losses["total_loss"].backward()
         if torch.cuda.is_available():
@@ -167,18 +187,79 @@ class Trainer:
             main = torch.cuda.current_stream()
             for st in ops.SIDE_STREAMS:
                 main.wait_stream(st)
-        if self.buckets:
-            self.buckets.finish()
+        return losses
+
+    def _update(self):
         self.steps += 1
         st = _lib.stream()
         s = self.state
         _lib.call("vt_grad_norm_clip", s.g.data_ptr(), s.numel, 1.0 / self.world, float(self.max_norm),
                   self.norm_out.data_ptr(), self.norm_ws.data_ptr(), st)
-        _lib.call("vt_adamw_step", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(), s.numel,
+        _lib.call("vt_adamw_step_dev", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(), s.numel,
                   float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
-                  self.steps, self.norm_out.data_ptr() + 4, st)
-        losses["grad_norm"] = self.norm_out[0]
-        return losses
+                  self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4, st)
+
+    # ------------------------------------------------------------ hipGraph
+    def capture(self, batch, eps=None, warmup=2, pre_capture=None):
+        """Record the training step as a hipGraph over static input buffers and
+        return it as a `CapturedStep` (also kept as the trainer's default for
+        `replay`).  A replay is one launch instead of ~1200 host-side op
+        dispatches (the eager step is host-bound: ~20 ms of Python/ctypes
+        dispatch for ~22 ms of GPU work).  Every op is stream-ordered, host-sync
+        free and allocation-stable after the first steps, so a replay is the same
+        computation as an eager step (tests/test_gpu_model.py checks bit
+        equality).  Single GPU: the whole step (forward, backward, clip, AdamW)
+        is one graph.  Several GPUs: the graph ends after the backward; the
+        bucketed RCCL all-reduce, clip and AdamW are issued after each replay (a
+        handful of launches), so no collective is captured.  `warmup` eager
+        steps run first (on the capture side stream, as torch requires) and do
+        update the model.  Capture more than once for double-buffered inputs."""
+        static_in = {k: v.clone() for k, v in batch.items()}
+        static_eps = None if eps is None else eps.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.step(static_in, eps=static_eps)
+        torch.cuda.current_stream().wait_stream(side)
+        if pre_capture is not None:
+            pre_capture()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self._forward_backward(static_in, static_eps, overlap_comm=False)
+            if not self.buckets:
+                self._update()
+        out["grad_norm"] = self.norm_out[0]
+        self.captured = CapturedStep(self, graph, static_in, static_eps, out)
+        return self.captured
+
+    def replay(self, batch=None, eps=None):
+        """One step of the last captured graph on `batch` (copied into its static inputs)."""
+        return self.captured.replay(batch, eps)
+
+
+class CapturedStep:
+    """A training step recorded as a hipGraph (Trainer.capture)."""
+
+    def __init__(self, trainer, graph, static_in, static_eps, out):
+        self.trainer, self.graph, self.static_in, self.static_eps, self.out = trainer, graph, static_in, static_eps, out
+
+    def replay(self, batch=None, eps=None):
+        tr = self.trainer
+        if batch is not None:
+            for k, v in batch.items():
+                if v.data_ptr() != self.static_in[k].data_ptr():
+                    self.static_in[k].copy_(v, non_blocking=True)
+        if eps is not None:
+            self.static_eps.copy_(eps, non_blocking=True)
+        self.graph.replay()
+        if tr.buckets:
+            tr.buckets.reduce_all()
+            tr.buckets.finish()
+            tr._update()
+        else:
+            tr.steps += 1
+        return self.out
 
 
 def init_distributed():
