@@ -169,6 +169,31 @@ int vt_linear_ln_fwd(const float* X, int64_t R, int K, const float* W, int N, co
 int vt_colsum(const float* X, int64_t R, int N, float* out, int accumulate, float* ws, int64_t ws_floats,
               void* stream);
 
+/* ------------------------------------------------------- whole ResidualMLP
+ * One ResidualMLP (ref/model/vae_teb_model.py:336-403) per launch sequence:
+ *   x0 = LN_in(x); h_0 = x0; h_l = act_l(LN_l(h_{l-1} W_l^T + b_l)) for the
+ *   layers with layer_ln[l] (every hidden layer; the last one too when
+ *   final_activation), else h_L = h_{L-1} W_L^T + b_L (act must be 0);
+ *   out = h_L + skip, skip 0 none, 1 identity (dims[0] == dims[L]),
+ *   2 projection Linear(dims[0] -> dims[L]) of x0 (use_skip_connection, :398-403).
+ * dims[0..L]: widths (<= VT_MLP_MAX_WIDTH); L <= VT_MLP_MAX_LAYERS; act as vt_act_fwd.
+ * params (4L+4 device pointers): [g_in, b_in, (W_l [N][K], b_l, g_l, beta_l) x L,
+ *   Ws, bs]; g_l/beta_l NULL for a layer without LN, Ws/bs NULL unless skip == 2.
+ * The forward saves xhat (sizes[0] floats) and rstd (sizes[1]) of every LN;
+ * the backward takes dout, writes dx (overwrite) and the parameter gradients
+ * `grads` (same layout as params, NULL entries skipped; accumulate: += else =)
+ * and needs sizes[2] floats of workspace.                                       */
+#define VT_MLP_MAX_LAYERS 34
+#define VT_MLP_MAX_WIDTH 144
+int vt_resmlp_sizes(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                    int64_t rows, int64_t* sizes);
+int vt_resmlp_fwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                  const float* const* params, const float* x, int64_t rows, float* out, float* xhat, float* rstd,
+                  void* stream);
+int vt_resmlp_bwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                  const float* const* params, const float* dout, const float* xhat, const float* rstd, int64_t rows,
+                  float* dx, float* const* grads, int accumulate, float* ws, int64_t ws_floats, void* stream);
+
 /* ------------------------------------------------------- bf16 MFMA (heads)
  * The decoder's R x R output heads (Decoder.output_mu / output_logvar,
  * ref/model/vae_teb_model.py:882-897,926-927, R = 16*S; the reference runs

@@ -132,13 +132,47 @@ class ResidualMLP(nn.Module):
             self._plan.append((idx, ln is not None, act))
             d = h
         self.body = nn.Sequential(*mods)
+        self.fused = True   # whole-stack kernels (vt_resmlp_*); False: one launch sequence per layer
         self.use_skip_connection = use_skip_connection
         if use_skip_connection:
             self.skip_proj = Linear(input_dim, hidden_dims[-1]) if input_dim != hidden_dims[-1] else nn.Identity()
         else:
             self.skip_proj = None
 
+    def _fused_spec(self):
+        """MlpSpec + parameter list for the whole-stack kernels (vt_resmlp_*),
+        or None when a width / depth / the bf16 heads rule them out."""
+        dims, lns, acts, params = [self.input_norm.weight.shape[0]], [], [], [self.input_norm.weight,
+                                                                               self.input_norm.bias]
+        eps = {self.input_norm.eps}
+        for (idx, has_ln, act) in self._plan:
+            lin = self.body[idx]
+            if lin.mfma:
+                return None
+            ln = self.body[idx + 1] if has_ln else None
+            dims.append(lin.out_features)
+            lns.append(has_ln)
+            acts.append(act if has_ln else "none")
+            params += [lin.weight, lin.bias, ln.weight if ln else None, ln.bias if ln else None]
+            if ln is not None:
+                eps.add(ln.eps)
+        if len(eps) != 1 or not ops.MlpSpec.supported(dims):
+            return None
+        skip = 0
+        if self.use_skip_connection:
+            skip = 1 if isinstance(self.skip_proj, nn.Identity) else 2
+        params += [self.skip_proj.weight, self.skip_proj.bias] if skip == 2 else [None, None]
+        key = (tuple(dims), tuple(lns), tuple(acts), skip)
+        if getattr(self, "_spec_key", None) != key:
+            self._spec = ops.MlpSpec(dims, lns, acts, skip, eps.pop())
+            self._spec_key = key
+        return self._spec, params
+
     def forward(self, x):
+        if x.is_cuda and self.fused:
+            fs = self._fused_spec()
+            if fs is not None:
+                return ops.resmlp(x, *fs)
         x0 = self.input_norm(x)
         h = x0
         for (idx, has_ln, act) in self._plan:

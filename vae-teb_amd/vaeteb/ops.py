@@ -223,6 +223,92 @@ def linear_ln_fused_ok(K, N):
     return N <= 256
 
 
+# ------------------------------------------------------- whole ResidualMLP
+class MlpSpec:
+    """Static description of one ResidualMLP for vt_resmlp_* (ctypes arrays
+    built once): widths, LayerNorm / activation per layer, skip kind, eps."""
+
+    MAX_LAYERS, MAX_WIDTH = 34, 144   # VT_MLP_MAX_LAYERS / VT_MLP_MAX_WIDTH
+
+    def __init__(self, dims, layer_ln, layer_act, skip, eps):
+        import ctypes
+        self.L = len(dims) - 1
+        self.dims_l, self.skip, self.eps = list(dims), int(skip), float(eps)
+        self.dims = (ctypes.c_int * len(dims))(*dims)
+        self.ln = (ctypes.c_int * self.L)(*[int(v) for v in layer_ln])
+        self.act = (ctypes.c_int * self.L)(*[ACT[a] if isinstance(a, str) else int(a) for a in layer_act])
+        self.n_params = 4 * self.L + 4
+        self._sizes = {}
+
+    @classmethod
+    def supported(cls, dims):
+        return len(dims) - 1 <= cls.MAX_LAYERS and max(dims) <= cls.MAX_WIDTH
+
+    def sizes(self, rows):
+        s = self._sizes.get(rows)
+        if s is None:
+            import ctypes
+            arr = (ctypes.c_int64 * 3)()
+            call("vt_resmlp_sizes", self.L, self.dims, self.ln, self.act, self.skip, rows, arr)
+            s = self._sizes[rows] = tuple(arr)
+        return s
+
+    @staticmethod
+    def pointers(ts):
+        import ctypes
+        return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+
+
+class ResMLPF(torch.autograd.Function):
+    """A whole ResidualMLP (ref/model/vae_teb_model.py:336-403): one forward
+    launch (vt_resmlp_fwd) and three backward launches (vt_resmlp_bwd: chain,
+    grouped weight gradients, fixed-order sums).  params in MlpSpec order:
+    [g_in, b_in, (W, b, g, beta) per layer, W_skip, b_skip] (None if absent)."""
+
+    @staticmethod
+    def forward(ctx, x, spec, *params):
+        _check(x, *params)
+        d0, DL = spec.dims_l[0], spec.dims_l[-1]
+        x2 = x.reshape(-1, d0).contiguous()
+        R = x2.shape[0]
+        n_xh, n_rs, _ = spec.sizes(R)
+        out = torch.empty((R, DL), device=x.device)
+        xh = torch.empty(n_xh, device=x.device)
+        rs = torch.empty(n_rs, device=x.device)
+        call("vt_resmlp_fwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, spec.pointers(params),
+             ptr(x2), R, ptr(out), ptr(xh), ptr(rs), _st())
+        ctx.save_for_backward(xh, rs)
+        ctx.spec, ctx.params, ctx.shape, ctx.R = spec, params, x.shape, R
+        return out.reshape(*x.shape[:-1], DL)
+
+    @staticmethod
+    def backward(ctx, gout):
+        xh, rs = ctx.saved_tensors
+        spec, params, R = ctx.spec, ctx.params, ctx.R
+        d0, DL = spec.dims_l[0], spec.dims_l[-1]
+        g2 = gout.reshape(R, DL).contiguous()
+        present = [i for i, p in enumerate(params) if p is not None]
+        need = ctx.needs_input_grad[2:]
+        pg = _ParamGrads([params[i] for i in present], [bool(need[i]) for i in present])
+        grads = [None] * len(params)
+        for i, gt in zip(present, pg.out):
+            grads[i] = gt
+        ws_floats = spec.sizes(R)[2]
+        ws = WS.get(ws_floats, xh.device, 5)
+        dx = torch.empty((R, d0), device=xh.device)
+        call("vt_resmlp_bwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, spec.pointers(params),
+             ptr(g2), ptr(xh), ptr(rs), R, ptr(dx), spec.pointers(grads), pg.acc, ptr(ws), ws.numel(), _st())
+        res = pg.result()
+        out = [None] * len(params)
+        for i, gt in zip(present, res):
+            out[i] = gt
+        return (dx.reshape(ctx.shape), None, *out)
+
+
+def resmlp(x, spec, params):
+    return ResMLPF.apply(x, spec, *params)
+
+
 # -------------------------------------------------------- LayerNorm + act
 class LayerNormActF(torch.autograd.Function):
     @staticmethod
