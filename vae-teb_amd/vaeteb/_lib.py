@@ -98,7 +98,9 @@ def ptr(t):
 
 
 def stream():
-    return torch.cuda.current_stream().cuda_stream
+    """Raw handle of the current HIP stream (~0.3 us; torch.cuda.current_stream()
+    builds a Python Stream object per call, ~2.6 us)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def call(name, *args):

@@ -141,7 +141,19 @@ class ResidualMLP(nn.Module):
 
     def _fused_spec(self):
         """MlpSpec + parameter list for the whole-stack kernels (vt_resmlp_*),
-        or None when a width / depth / the bf16 heads rule them out."""
+        or None when a width / depth / the bf16 heads rule them out.  Cached;
+        rebuilt when a parameter tensor is replaced (its storage moves)."""
+        c = getattr(self, "_fs_cache", None)
+        if c is not None and all(p is None or p.data_ptr() == q for p, q in zip(c[1], c[2])):
+            return c[0], c[1]
+        fs = self._build_fused_spec()
+        self._fs_cache = None if fs is None else (fs[0], fs[1], [p.data_ptr() if p is not None else 0
+                                                                  for p in fs[1]])
+        if fs is not None:
+            fs[0].param_ptrs = ops.MlpSpec.pointers(fs[1])
+        return fs
+
+    def _build_fused_spec(self):
         dims, lns, acts, params = [self.input_norm.weight.shape[0]], [], [], [self.input_norm.weight,
                                                                                self.input_norm.bias]
         eps = {self.input_norm.eps}

@@ -25,7 +25,7 @@ class _Workspace:
         self.buf = {}
 
     def get(self, nfloats, device, slot=0):
-        key = (str(device), slot, torch.cuda.current_stream(device).cuda_stream if torch.cuda.is_available() else 0)
+        key = (device.index, slot, _lib.stream() if device.type == "cuda" else 0)
         b = self.buf.get(key)
         if b is None or b.numel() < nfloats:
             b = torch.empty(max(int(nfloats), 1 << 20), dtype=torch.float32, device=device)
@@ -239,6 +239,8 @@ class MlpSpec:
         self.act = (ctypes.c_int * self.L)(*[ACT[a] if isinstance(a, str) else int(a) for a in layer_act])
         self.n_params = 4 * self.L + 4
         self._sizes = {}
+        self.param_ptrs = None           # ctypes array of the parameter pointers (set by the owner)
+        self._grad_key, self._grad_ptrs = None, None
 
     @classmethod
     def supported(cls, dims):
@@ -258,6 +260,16 @@ class MlpSpec:
         import ctypes
         return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
 
+    def grad_pointers(self, ts):
+        """Pointer array of the gradient destinations, reused while they stay put
+        (the trainer's in-place gradient sinks)."""
+        key = tuple(0 if t is None else t.data_ptr() for t in ts)
+        if key != self._grad_key:
+            import ctypes
+            self._grad_key = key
+            self._grad_ptrs = (ctypes.c_void_p * len(ts))(*[k or None for k in key])
+        return self._grad_ptrs
+
 
 class ResMLPF(torch.autograd.Function):
     """A whole ResidualMLP (ref/model/vae_teb_model.py:336-403): one forward
@@ -275,7 +287,8 @@ class ResMLPF(torch.autograd.Function):
         out = torch.empty((R, DL), device=x.device)
         xh = torch.empty(n_xh, device=x.device)
         rs = torch.empty(n_rs, device=x.device)
-        call("vt_resmlp_fwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, spec.pointers(params),
+        pp = spec.param_ptrs if spec.param_ptrs is not None else spec.pointers(params)
+        call("vt_resmlp_fwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp,
              ptr(x2), R, ptr(out), ptr(xh), ptr(rs), _st())
         ctx.save_for_backward(xh, rs)
         ctx.spec, ctx.params, ctx.shape, ctx.R = spec, params, x.shape, R
@@ -296,8 +309,9 @@ class ResMLPF(torch.autograd.Function):
         ws_floats = spec.sizes(R)[2]
         ws = WS.get(ws_floats, xh.device, 5)
         dx = torch.empty((R, d0), device=xh.device)
-        call("vt_resmlp_bwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, spec.pointers(params),
-             ptr(g2), ptr(xh), ptr(rs), R, ptr(dx), spec.pointers(grads), pg.acc, ptr(ws), ws.numel(), _st())
+        pp = spec.param_ptrs if spec.param_ptrs is not None else spec.pointers(params)
+        call("vt_resmlp_bwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp,
+             ptr(g2), ptr(xh), ptr(rs), R, ptr(dx), spec.grad_pointers(grads), pg.acc, ptr(ws), ws.numel(), _st())
         res = pg.result()
         out = [None] * len(params)
         for i, gt in zip(present, res):

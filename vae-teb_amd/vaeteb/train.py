@@ -45,11 +45,13 @@ class FlatState:
                 p._vt_sink = True  # HIP ops accumulate this gradient in place (vaeteb.ops._ParamGrads)
                 self.offsets.append((o, n))
                 o += n
+        self._grad_ptrs = [self.g.data_ptr() + 4 * o for o, _ in self.offsets]
 
     def zero_grad(self):
         self.g.zero_()
-        for p, (o, n) in zip(self.params, self.offsets):
-            if p.grad is None or p.grad.data_ptr() != self.g[o:o + n].data_ptr():
+        for p, (o, n), gp in zip(self.params, self.offsets, self._grad_ptrs):
+            g = p.grad
+            if g is None or g.data_ptr() != gp:
                 p.grad = self.g[o:o + n].view_as(p)
 
 
@@ -173,7 +175,8 @@ class Trainer:
         return losses
 
     def _forward_backward(self, batch, eps, overlap_comm):
-        self.model.train()
+        if not self.model.training:
+            self.model.train()
         self.state.zero_grad()
         if self.buckets:
             self.buckets.reset()
