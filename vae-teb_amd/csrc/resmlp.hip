@@ -18,14 +18,13 @@
 //              every LayerNorm for the backward (h is recomputed from them).
 //  k_mlp_bwd   the chain backward per 16-row wave tile, layers in reverse:
 //              act' and LayerNorm backward in registers, dX = dZ W on MFMA,
-//              dZ of every layer written out for the weight gradients, the
-//              gamma/beta column partials reduced per workgroup in fixed order.
-//  k_mlp_dw    all weight/bias gradients of the stack in one grouped launch:
-//              (layer, row chunk) workgroups, dW = dZ^T h_{l-1} with h_{l-1}
-//              recomputed from the saved xhat while staging (act(xhat*g+b)),
-//              the bias as a ones-column; per-chunk slabs.
-//  k_mlp_sum   every slab (dW, db, gamma, beta of every layer) summed in fixed
-//              order into the parameter gradients (accumulate or overwrite).
+//              and each layer's weight gradient dZ^T h_{l-1} over the
+//              workgroup's 64 rows (h_{l-1} recomputed from the prefetched
+//              xhat as act(xhat*g+b), the bias as a ones column), written with
+//              the gamma/beta column partials as per-workgroup partials.
+//  k_mlp_sum   every partial (dW, db, gamma, beta of every layer) summed over
+//              the workgroups in fixed order into the parameter gradients
+//              (accumulate or overwrite).
 //
 // No atomics anywhere: results are bitwise reproducible run to run.
 #include <math.h>
@@ -144,6 +143,8 @@ struct Cfg {
     static constexpr int TILE = 16 * AS;                               // one wave's 16-row tile
     static constexpr int BFL = KC * BS;                                // staged W chunk
     static constexpr int SU = (KC * W16 + FWD_THREADS - 1) / FWD_THREADS;  // staging loads per thread
+    static constexpr int HS = 16 * (NT + 1) + (((NT + 1) & 1) ? 0 : 16);  // h_{l-1} tile (+ ones column), == 16 mod 32
+    static constexpr int HTILE = 16 * HS;
 };
 
 // Weight chunks are staged through registers: w_load issues the global loads
@@ -504,21 +505,82 @@ __device__ __forceinline__ void flush_red(const float* red, int N, float* __rest
     }
 }
 
+// Partial dW (+ db as the ones column) of one layer over the workgroup's 64
+// rows: dst[n * K1 + k] = sum_rows dZ[row][n] * H[row][k].  dZ rows are the
+// 4 waves' T tiles, H rows their h_{l-1} tiles (both contiguous in LDS); the
+// waves own (16 x 16) output tile pairs, two at a time.
+template <int NT>
+__device__ __forceinline__ void wg_dw(const float* Tall, const float* Hall, int N, int K1, float* __restrict__ dst) {
+    using C = Cfg<NT>;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lr = lane & 15, lc = lane >> 4;
+    const int ntn = (N + 15) >> 4, ntk = (K1 + 15) >> 4, pairs = ntn * ntk;
+    for (int p0 = wv; p0 < pairs; p0 += 8) {
+        const int p1 = p0 + 4;
+        const bool two = p1 < pairs;
+        const int tn0 = p0 / ntk, tk0 = p0 - tn0 * ntk;
+        const int tn1 = two ? p1 / ntk : tn0, tk1 = two ? p1 - tn1 * ntk : tk0;
+        const float* a0 = Tall + lc * C::AS + 16 * tn0 + lr;
+        const float* b0 = Hall + lc * C::HS + 16 * tk0 + lr;
+        const float* a1 = Tall + lc * C::AS + 16 * tn1 + lr;
+        const float* b1 = Hall + lc * C::HS + 16 * tk1 + lr;
+        f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll 4
+        for (int s4 = 0; s4 < 16; ++s4) {
+            c0 = mfma4(a0[4 * s4 * C::AS], b0[4 * s4 * C::HS], c0);
+            if (two) c1 = mfma4(a1[4 * s4 * C::AS], b1[4 * s4 * C::HS], c1);
+        }
+        const int k0c = 16 * tk0 + lr, k1c = 16 * tk1 + lr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n0 = 16 * tn0 + 4 * lc + r, n1 = 16 * tn1 + 4 * lc + r;
+            if (n0 < N && k0c < K1) dst[n0 * K1 + k0c] = c0[r];
+            if (two && n1 < N && k1c < K1) dst[n1 * K1 + k1c] = c1[r];
+        }
+    }
+}
+
+// this wave's h tile for the weight gradient: act(xhat * g + b) on the valid
+// columns, 1 in column K (the bias), 0 beyond
+template <int NT>
+__device__ __forceinline__ void store_h(float* Hw, const float (&xn)[NT][4], const float (&gn)[NT],
+                                        const float (&bn)[NT], int act, int K) {
+    using C = Cfg<NT>;
+    const int lane = threadIdx.x & 63, lr = lane & 15, lc = lane >> 4;
+#pragma unroll
+    for (int n = 0; n <= NT; ++n) {
+        const int col = 16 * n + lr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float h = col == K ? 1.f : 0.f;
+            if (n < NT && col < K) h = mact(xn[n][r] * gn[n] + bn[n], act);
+            Hw[(4 * lc + r) * C::HS + col] = h;
+        }
+    }
+}
+
 // GEMM sequence: the skip projection (skip == 2, A = dout), then layers
 // L-1..0 (A = dZ_l).  While a layer's GEMM runs, the next weight chunk and
-// the next LayerNorm's xhat / rstd / gamma / beta are already loading.
+// the next LayerNorm's xhat / rstd / gamma / beta are already loading; that
+// xhat (-> h_{l-1}) then gives the layer's weight gradient dZ_l^T h_{l-1}
+// over the workgroup's rows, written as a per-workgroup partial.
+// Partial layout per workgroup (P floats): [dgamma0, dbeta0 (2*d0)], then for
+// each LayerNorm layer [dgamma_l, dbeta_l (2*N_l)] (ly.po); then at PL + ly.wo
+// each layer's [N][K+1] dW|db, and the skip projection's [DL][d0+1] last.
 template <int NT>
 __global__ __launch_bounds__(FWD_THREADS) void k_mlp_bwd(MlpDesc d, const float* __restrict__ dout,
                                                          const float* __restrict__ xh, const float* __restrict__ rs,
-                                                         int64_t R, float* __restrict__ dx, float* __restrict__ dz,
-                                                         float* __restrict__ part, int P) {
+                                                         int64_t R, float* __restrict__ dx,
+                                                         float* __restrict__ part, int P, int PL, int wskip) {
     using C = Cfg<NT>;
     extern __shared__ float sm[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
     float* Bs = sm;
-    float* T = sm + C::BFL + wv * C::TILE;
+    float* Tall = sm + C::BFL;
+    float* T = Tall + wv * C::TILE;
     float* G0 = sm + C::BFL + (4 + wv) * C::TILE;       // skip gradient (d.skip)
-    float* red = sm + C::BFL + 8 * C::TILE;             // [4 waves][2][16*NT]
+    float* Hall = sm + C::BFL + 8 * C::TILE;            // [4 waves][16][HS]
+    float* H = Hall + wv * C::HTILE;
+    float* red = Hall + 4 * C::HTILE;                   // [4 waves][2][16*NT]
     float* redw = red + wv * 32 * NT;
     const int64_t rbase = (int64_t)blockIdx.x * 64 + 16 * wv;
     const int L = d.L, d0 = d.d0, DL = d.l[L - 1].N;
@@ -551,7 +613,6 @@ __global__ __launch_bounds__(FWD_THREADS) void k_mlp_bwd(MlpDesc d, const float*
         f32x4 acc[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int nt = (d0 + 15) >> 4;
         for (int k0 = 0; k0 < DL; k0 += KC) {
             lds_barrier();
             w_store<NT>(v, Bs, d0, false);
@@ -562,7 +623,7 @@ __global__ __launch_bounds__(FWD_THREADS) void k_mlp_bwd(MlpDesc d, const float*
                 w_load<NT>(v, d.l[L - 1].W, d.l[L - 1].N, d.l[L - 1].K, false, 0);
                 if (d.l[L - 1].ln) VT_LN_PREFETCH(L - 1);
             }
-            mfma_chunk<NT>(T, Bs, k0, DL - k0 < KC ? DL - k0 : KC, nt, acc);  // d x0 += dout Ws
+            mfma_chunk<NT>(T, Bs, k0, DL - k0 < KC ? DL - k0 : KC, 0, acc);  // d x0 += dout Ws
         }
         float t[NT][4];
 #pragma unroll
@@ -575,14 +636,13 @@ __global__ __launch_bounds__(FWD_THREADS) void k_mlp_bwd(MlpDesc d, const float*
         const MlpLayer& ly = d.l[l];
         const int N = ly.N, K = ly.K;
         if (ly.ln) ln_bwd_tile<NT>(g, N, gn, bn, ly.act, xn, rn, redw);
-        tile_store<NT>(dz + R * ly.dzo, g, N, rbase, R);
+        lds_barrier();  // the previous layer's weight-gradient MFMAs are done with the T tiles
         store_tile<NT>(T, g, N);
         lds_barrier();
         if (ly.ln) flush_red<NT>(red, N, pb + ly.po);
         f32x4 acc[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int nt = (K + 15) >> 4;
         for (int k0 = 0; k0 < N; k0 += KC) {
             lds_barrier();
             w_store<NT>(v, Bs, K, false);
@@ -593,14 +653,26 @@ __global__ __launch_bounds__(FWD_THREADS) void k_mlp_bwd(MlpDesc d, const float*
                 if (l >= 1) w_load<NT>(v, d.l[l - 1].W, d.l[l - 1].N, d.l[l - 1].K, false, 0);
                 VT_LN_PREFETCH(l - 1);  // layer l-1 (a hidden layer: always normalised) or the input LN
             }
-            mfma_chunk<NT>(T, Bs, k0, N - k0 < KC ? N - k0 : KC, nt, acc);  // dh_{l-1} = dZ W
+            mfma_chunk<NT>(T, Bs, k0, N - k0 < KC ? N - k0 : KC, 0, acc);  // dh_{l-1} = dZ W
         }
+        // weight gradient of layer l: dZ_l (T tiles) ^T h_{l-1} (from the prefetched xhat)
+        store_h<NT>(H, xn, gn, bn, l >= 1 ? d.l[l - 1].act : 0, K);
+        lds_barrier();
+        wg_dw<NT>(Tall, Hall, N, K + 1, pb + PL + ly.wo);
 #pragma unroll
         for (int n = 0; n < NT; ++n)
 #pragma unroll
             for (int r = 0; r < 4; ++r) g[n][r] = acc[n][r];
     }
 #undef VT_LN_PREFETCH
+    if (d.skip == 2) {  // dWs = dout^T x0 (H still holds x0)
+        float t[NT][4];
+        tile_load<NT>(t, dout, DL, rbase, R);
+        lds_barrier();
+        store_tile<NT>(T, t, DL);
+        lds_barrier();
+        wg_dw<NT>(Tall, Hall, DL, d0 + 1, pb + PL + wskip);
+    }
     if (d.skip) {
 #pragma unroll
         for (int n = 0; n < NT; ++n)
@@ -613,183 +685,35 @@ __global__ __launch_bounds__(FWD_THREADS) void k_mlp_bwd(MlpDesc d, const float*
     flush_red<NT>(red, d0, pb);
 }
 
-// ----------------------------------------------------------- weight grads
-// group q < L: dW_q = dZ_q^T h_{q-1}, h_{-1} = x0; group L: the skip projection
-// dWs = dout^T x0.  part2[q-th group offset + chunk * N*(K+1) + n*(K+1) + k].
-struct DwGroup {
-    const float* dY;
-    const float* xh;
-    const float* g;
-    const float* be;
-    int N, K, act, pad_;
-    int64_t off;
-};
-
-__device__ __forceinline__ DwGroup dw_group(const MlpDesc& d, int q, const float* dout, const float* xh,
-                                            const float* dz, int64_t R, int C) {
-    DwGroup G;
-    if (q < d.L) {
-        const MlpLayer& ly = d.l[q];
-        G.dY = dz + R * ly.dzo;
-        G.N = ly.N;
-        G.K = ly.K;
-        G.off = (int64_t)C * ly.wo;
-        if (q == 0) {
-            G.xh = xh;
-            G.g = d.g0;
-            G.be = d.be0;
-            G.act = 0;
-        } else {
-            const MlpLayer& lp = d.l[q - 1];
-            G.xh = xh + R * lp.xo;
-            G.g = lp.g;
-            G.be = lp.be;
-            G.act = lp.act;
-        }
-    } else {  // skip projection: dWs = dout^T x0
-        const MlpLayer& ll = d.l[d.L - 1];
-        G.dY = dout;
-        G.N = ll.N;
-        G.K = d.d0;
-        G.off = (int64_t)C * (ll.wo + ll.N * (ll.K + 1));
-        G.xh = xh;
-        G.g = d.g0;
-        G.be = d.be0;
-        G.act = 0;
-    }
-    return G;
-}
-
-template <int NT>
-__global__ __launch_bounds__(DW_THREADS) void k_mlp_dw(MlpDesc d, const float* __restrict__ dout,
-                                                       const float* __restrict__ xh, const float* __restrict__ dz,
-                                                       int64_t R, int64_t rows_per_chunk, float* __restrict__ part2) {
-    constexpr int DW_ROWS = NT >= 9 ? 32 : 64;  // rows per LDS chunk (register double buffer)
-    constexpr int NTK_MAX = NT + 1;
-    constexpr int HS = 16 * NT + ((NT & 1) ? 0 : 16);
-    constexpr int XS = 16 * NTK_MAX + ((NTK_MAX & 1) ? 0 : 16);
-    constexpr int PAIRS_MAX = NT * NTK_MAX, PPW = (PAIRS_MAX + 7) / 8;
-    // rows of a 64-row chunk staged per thread (thread -> column, row offset)
-    constexpr int RH = (DW_ROWS + DW_THREADS / (16 * NT) - 1) / (DW_THREADS / (16 * NT));
-    constexpr int RX = (DW_ROWS + DW_THREADS / (16 * NTK_MAX) - 1) / (DW_THREADS / (16 * NTK_MAX));
-    __shared__ float Hs[DW_ROWS * HS];
-    __shared__ float Xs[DW_ROWS * XS];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
-    const int C = gridDim.x;
-    const DwGroup G = dw_group(d, blockIdx.y, dout, xh, dz, R, C);
-    const int N = G.N, K = G.K, K1 = K + 1;
-    const int ntn = (N + 15) >> 4, ntk = (K1 + 15) >> 4, pairs = ntn * ntk;
-    const int wn = 16 * ntn, wk = 16 * ntk;
-    f32x4 acc[PPW];
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int64_t rb = (int64_t)blockIdx.x * rows_per_chunk;
-    const int64_t re = rb + rows_per_chunk < R ? rb + rows_per_chunk : R;
-    const int sh = DW_THREADS / wn, ch = tid % wn, th = tid / wn;
-    const int sx = DW_THREADS / wk, cx = tid % wk, tx = tid / wk;
-    const float gx = cx < K ? G.g[cx] : 0.f, bx = cx < K ? G.be[cx] : 0.f;
-    // register double buffer: the next 64-row chunk loads while this one is multiplied
-    float vh[RH], vx[RX];
-#define VT_DW_LOAD(c0_)                                                                      \
-    do {                                                                                     \
-        const int64_t cc_ = (c0_);                                                           \
-        _Pragma("unroll") for (int u = 0; u < RH; ++u) {                                     \
-            const int t = th + u * sh;                                                       \
-            vh[u] = (th < sh && t < DW_ROWS && cc_ + t < re && ch < N) ? G.dY[(cc_ + t) * N + ch] : 0.f; \
-        }                                                                                    \
-        _Pragma("unroll") for (int u = 0; u < RX; ++u) {                                     \
-            const int t = tx + u * sx;                                                       \
-            vx[u] = (tx < sx && t < DW_ROWS && cc_ + t < re && cx < K) ? G.xh[(cc_ + t) * K + cx] : 0.f; \
-        }                                                                                    \
-    } while (0)
-    if (rb < re) VT_DW_LOAD(rb);
-    for (int64_t c0 = rb; c0 < re; c0 += DW_ROWS) {
-        const int n = re - c0 < DW_ROWS ? (int)(re - c0) : DW_ROWS;
-        lds_barrier();  // the previous chunk's MFMAs are done with Hs / Xs
-        if (th < sh) {
-#pragma unroll
-            for (int u = 0; u < RH; ++u) {
-                const int t = th + u * sh;
-                if (t < DW_ROWS) Hs[t * HS + ch] = vh[u];
-            }
-        }
-        if (tx < sx) {
-#pragma unroll
-            for (int u = 0; u < RX; ++u) {
-                const int t = tx + u * sx;
-                if (t < DW_ROWS) {
-                    float x = 0.f;
-                    if (t < n) x = cx < K ? mact(vx[u] * gx + bx, G.act) : (cx == K ? 1.f : 0.f);
-                    Xs[t * XS + cx] = x;
-                }
-            }
-        }
-        lds_barrier();
-        if (c0 + DW_ROWS < re) VT_DW_LOAD(c0 + DW_ROWS);
-        const int groups = (n + 3) >> 2;
-        for (int q = 0; q < groups; ++q) {
-            const float* hp = Hs + (4 * q + lc) * HS + lr;
-            const float* xp = Xs + (4 * q + lc) * XS + lr;
-#pragma unroll
-            for (int j = 0; j < PPW; ++j) {
-                const int p = wv + 8 * j;
-                if (p < pairs) {
-                    const int tn = p / ntk, tk = p - tn * ntk;
-                    acc[j] = mfma4(hp[16 * tn], xp[16 * tk], acc[j]);
-                }
-            }
-        }
-    }
-#undef VT_DW_LOAD
-    float* pb = part2 + G.off + (int64_t)blockIdx.x * N * K1;
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-        const int p = wv + 8 * j;
-        if (p >= pairs) continue;
-        const int tn = p / ntk, tk = p - tn * ntk;
-        const int k = 16 * tk + lr;
-        if (k >= K1) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int nn = 16 * tn + 4 * lc + r;
-            if (nn < N) pb[nn * K1 + k] = acc[j][r];
-        }
-    }
-}
-
 // ---------------------------------------------------------------- final sum
-// segment s < G: the dW/db slabs of group s (C chunks); s >= G: the gamma/beta
-// partials of LayerNorm s - G (layer s - G < L, or the input norm when == L)
-// over the nblk chain workgroups.  16 outputs x 16 partial lanes per block.
-__global__ __launch_bounds__(256) void k_mlp_sum(MlpDesc d, MlpGrads gr, int64_t R, int C, int nG,
-                                                 const float* __restrict__ part2, const float* __restrict__ part,
-                                                 int nblk, int P, int accumulate) {
+// segment s < nG: the dW|db partials of layer s (s == L: the skip projection);
+// s >= nG: the gamma/beta partials of LayerNorm s - nG (layer s - nG < L, or
+// the input norm when == L); summed over the nblk chain workgroups in fixed
+// order (16 outputs x 16 partial lanes per block, then a fixed tree).
+__global__ __launch_bounds__(256) void k_mlp_sum(MlpDesc d, MlpGrads gr, int nG, const float* __restrict__ part,
+                                                 int nblk, int P, int PL, int wskip, int accumulate) {
     __shared__ float red[16][17];
     const int s = blockIdx.y;
     const int o = threadIdx.x & 15, sl = threadIdx.x >> 4;
     const float* src;
-    int64_t stride;
-    int count, E, N = 0, K1 = 0;
+    int E, N = 0, K1 = 0;
     float *da, *dbp;
     const bool dwseg = s < nG;
     if (dwseg) {
-        const MlpLayer& ll = d.l[s < d.L ? s : d.L - 1];
         if (s < d.L) {
-            N = ll.N;
-            K1 = ll.K + 1;
+            N = d.l[s].N;
+            K1 = d.l[s].K + 1;
             da = gr.dW[s];
             dbp = gr.db[s];
-            src = part2 + (int64_t)C * ll.wo;
+            src = part + PL + d.l[s].wo;
         } else {
-            N = ll.N;
+            N = d.l[d.L - 1].N;
             K1 = d.d0 + 1;
             da = gr.dWs;
             dbp = gr.dbs;
-            src = part2 + (int64_t)C * (ll.wo + ll.N * (ll.K + 1));
+            src = part + PL + wskip;
         }
         E = N * K1;
-        stride = E;
-        count = C;
     } else {
         const int q = s - nG;
         if (q < d.L) {
@@ -805,16 +729,14 @@ __global__ __launch_bounds__(256) void k_mlp_sum(MlpDesc d, MlpGrads gr, int64_t
             src = part;
         }
         E = 2 * N;
-        stride = P;
-        count = nblk;
     }
-    const int64_t i = (int64_t)blockIdx.x * 16 + o;
     if ((int64_t)blockIdx.x * 16 >= E) return;
+    const int i = blockIdx.x * 16 + o;
     float a = 0.f;
     if (i < E)
-        for (int b = sl; b < count; b += 16) a += src[(int64_t)b * stride + i];
+        for (int b = sl; b < nblk; b += 16) a += src[(int64_t)b * P + i];
     red[sl][o] = a;
-    lds_barrier();
+    __syncthreads();
     if (sl != 0 || i >= E) return;
     float t8[8];
 #pragma unroll
@@ -824,7 +746,7 @@ __global__ __launch_bounds__(256) void k_mlp_sum(MlpDesc d, MlpGrads gr, int64_t
     const float t = (t8[0] + t8[1]) + (t8[2] + t8[3]);
     float* dst;
     if (dwseg) {
-        const int n = (int)(i / K1), k = (int)(i - (int64_t)n * K1);
+        const int n = i / K1, k = i - n * K1;
         const int K = K1 - 1;
         dst = k < K ? (da ? da + (int64_t)n * K + k : nullptr) : (dbp ? dbp + n : nullptr);
     } else {
@@ -837,7 +759,7 @@ __global__ __launch_bounds__(256) void k_mlp_sum(MlpDesc d, MlpGrads gr, int64_t
 struct Plan {
     MlpDesc d;
     int nt;
-    int64_t xh_floats, rs_floats, dz_floats, P, nblk, C, rpc, dw_floats;
+    int64_t xh_floats, rs_floats, P, PL, wskip, nblk;
 };
 
 int make_plan(Plan& p, int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
@@ -897,16 +819,12 @@ int make_plan(Plan& p, int n_layers, const int* dims, const int* layer_ln, const
     p.nt = ntw <= 2 ? 2 : ntw <= 4 ? 4 : ntw <= 6 ? 6 : 9;
     p.xh_floats = R * (dims[0] + sum_ln);
     p.rs_floats = R * (1 + n_ln);
-    p.dz_floats = R * sum_n;
-    p.P = 2 * (dims[0] + sum_ln);
-    p.nblk = (R + 63) / 64;
-    int64_t rpc = (R + 127) / 128;  // 128 row chunks per group: enough workgroups in flight
-    if (rpc < 256) rpc = 256;
-    rpc = (rpc + 3) / 4 * 4;
-    p.rpc = rpc;
-    p.C = (R + rpc - 1) / rpc;
+    p.PL = 2 * (dims[0] + sum_ln);
+    p.wskip = sum_nk;
     if (skip == 2) sum_nk += (int64_t)dims[n_layers] * (dims[0] + 1);
-    p.dw_floats = p.C * sum_nk;
+    p.P = p.PL + sum_nk;
+    p.nblk = (R + 63) / 64;
+    VT_CHECK_ARG(p.xh_floats < (int64_t)1 << 31 && p.nblk * p.P < ((int64_t)1 << 40), "%s: too many rows", who);
     return VT_OK;
 }
 
@@ -916,7 +834,7 @@ size_t fwd_lds(int) {
 }
 template <int NT>
 size_t bwd_lds() {
-    return sizeof(float) * (Cfg<NT>::BFL + 8 * Cfg<NT>::TILE + 4 * 32 * NT);
+    return sizeof(float) * (Cfg<NT>::BFL + 8 * Cfg<NT>::TILE + 4 * Cfg<NT>::HTILE + 4 * 32 * NT);
 }
 
 }  // namespace
@@ -936,7 +854,7 @@ int vt_resmlp_sizes(int n_layers, const int* dims, const int* layer_ln, const in
     if (rc) return rc;
     sizes[0] = p.xh_floats;
     sizes[1] = p.rs_floats;
-    sizes[2] = p.dz_floats + p.nblk * p.P + p.dw_floats;
+    sizes[2] = p.nblk * p.P;
     return VT_OK;
 }
 
@@ -966,9 +884,8 @@ int vt_resmlp_bwd(int n_layers, const int* dims, const int* layer_ln, const int*
     const int rc = make_plan(p, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, "vt_resmlp_bwd");
     if (rc) return rc;
     VT_CHECK_ARG(dout && xhat && rstd && dx && grads, "vt_resmlp_bwd: null buffer");
-    VT_CHECK_ARG(ws && ws_floats >= p.dz_floats + p.nblk * p.P + p.dw_floats,
-                 "vt_resmlp_bwd: workspace %lld floats < %lld", (long long)ws_floats,
-                 (long long)(p.dz_floats + p.nblk * p.P + p.dw_floats));
+    VT_CHECK_ARG(ws && ws_floats >= p.nblk * p.P, "vt_resmlp_bwd: workspace %lld floats < %lld",
+                 (long long)ws_floats, (long long)(p.nblk * p.P));
     MlpGrads g{};
     g.dg0 = grads[0];
     g.dbe0 = grads[1];
@@ -980,20 +897,15 @@ int vt_resmlp_bwd(int n_layers, const int* dims, const int* layer_ln, const int*
     }
     g.dWs = grads[2 + 4 * n_layers];
     g.dbs = grads[3 + 4 * n_layers];
-    float* dz = ws;
-    float* part = dz + p.dz_floats;
-    float* part2 = part + p.nblk * p.P;
     hipStream_t st = S(stream);
     const dim3 grid((unsigned)p.nblk);
-    const int P = (int)p.P;
+    const int P = (int)p.P, PL = (int)p.PL, wskip = (int)p.wskip;
     const int nG = n_layers + (skip == 2 ? 1 : 0);
-    const dim3 gdw((unsigned)p.C, (unsigned)nG);
     switch (p.nt) {
 #define VT_MLPB(NTV)                                                                                               \
     case NTV:                                                                                                      \
         hipLaunchKernelGGL(k_mlp_bwd<NTV>, grid, dim3(FWD_THREADS), bwd_lds<NTV>(), st, p.d, dout, xhat, rstd,     \
-                           rows, dx, dz, part, P);                                                                 \
-        hipLaunchKernelGGL(k_mlp_dw<NTV>, gdw, dim3(DW_THREADS), 0, st, p.d, dout, xhat, dz, rows, p.rpc, part2);   \
+                           rows, dx, ws, P, PL, wskip);                                                            \
         break;
         VT_MLPB(2) VT_MLPB(4) VT_MLPB(6)
         default: VT_MLPB(9)
@@ -1006,8 +918,7 @@ int vt_resmlp_bwd(int n_layers, const int* dims, const int* layer_ln, const int*
     }
     if (skip == 2) emax = dims[n_layers] * (dims[0] + 1) > emax ? dims[n_layers] * (dims[0] + 1) : emax;
     const dim3 gs((unsigned)((emax + 15) / 16), (unsigned)(nG + n_layers + 1));
-    hipLaunchKernelGGL(k_mlp_sum, gs, dim3(256), 0, st, p.d, g, rows, (int)p.C, nG, part2, part, (int)p.nblk, P,
-                       accumulate);
+    hipLaunchKernelGGL(k_mlp_sum, gs, dim3(256), 0, st, p.d, g, nG, ws, (int)p.nblk, P, PL, wskip, accumulate);
     VT_LAUNCH_CHECK("vt_resmlp_bwd");
     return VT_OK;
 }
