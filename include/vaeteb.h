@@ -228,6 +228,18 @@ int vt_conv1d_bwd_data(const float* dY, int B, int L_in, int Cin, const float* W
                        float* dX, int accumulate, float* gpad, void* stream);
 int vt_conv1d_bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode, int up,
                          float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);
+/* Conv1d(bias=False) -> train-mode BatchNorm1d -> act in three launches: the
+ * conv kernel also writes per-tile (sum, sum of squared deviations) of its
+ * outputs, one finalize combines them (Chan, double) into mean / rstd and the
+ * running statistics, one pass applies BN + act.  conv_out (B, L_out, Cout) is
+ * kept for the backward; ws: vt_conv1d_bn_workspace_floats floats.
+ * replaces: CausalMultiChannelConvBlock / MultiChannelConvBlock forward
+ *           (ref/model/vae_teb_model.py:128-212, :214-253)                        */
+int vt_conv1d_bn_workspace_floats(int B, int L_in, int Cin, int Cout, int K, int mode, int up, int64_t* floats);
+int vt_conv1d_bn_fwd(const float* X, int B, int L_in, int Cin, const float* W, int Cout, int K, int mode, int up,
+                     const float* gamma, const float* beta, int act, float eps, float momentum, float* conv_out,
+                     float* Y, float* mean, float* rstd, float* run_mean, float* run_var, float* ws,
+                     int64_t ws_floats, void* stream);
 /* Direct (LDS-windowed) conv kernels used on the training path (conv.hip), K <= 11:
  * forward; bwd-data as a full correlation into gpad (B, L_out+K-1, Cin) + fold;
  * bwd-weight with fixed-order split reduction.                                   */

@@ -77,8 +77,11 @@ struct FwdCfg {
 
 // FLIP_T: taps W[ci][co][K-1-k] (transposed, flipped) instead of W[co][ci][k].
 template <int K, int NT, bool FLIP_T>
+// stats != null: also the BatchNorm statistics of this tile's outputs,
+// stats[tile][0][co] = sum_t y, stats[tile][1][co] = sum_t (y - tile mean)^2
+// (tile = b * gridDim.x + blockIdx.x), combined by k_bn_stats_finalize.
 __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ x, Geo g, const float* __restrict__ w,
-                                                  float* __restrict__ y, int Lo) {
+                                                  float* __restrict__ y, int Lo, float* __restrict__ stats) {
     using C = FwdCfg<K, NT>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN, WS = C::WS, CI = C::CI;
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -186,6 +189,101 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ x, G
                 if (co < g.Cout) yr[co] = acc[m][n][r];
             }
         }
+    if (stats) {
+        // per-column sum, then sum of squared deviations from the tile mean, over
+        // the tile's valid positions (lanes -> wave via shuffles, waves via LDS)
+        float* red1 = lds;           // [4][TC]
+        float* red2 = lds + 4 * TC;  // [4][TC]
+        const int nrow = Lo - t0 < TP ? Lo - t0 : TP;
+        float cs[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            float a = 0.f;
+#pragma unroll
+            for (int m = 0; m < PM; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (t0 + PM * 16 * wv + 16 * m + 4 * lc + r < Lo) a += acc[m][n][r];
+            a += __shfl_xor(a, 16);
+            a += __shfl_xor(a, 32);
+            cs[n] = a;
+        }
+        if (lc == 0)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) red1[wv * TC + 16 * n + lr] = cs[n];
+        __syncthreads();
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int c = 16 * n + lr;
+            const float mu = (((red1[c] + red1[TC + c]) + red1[2 * TC + c]) + red1[3 * TC + c]) / (float)nrow;
+            float q = 0.f;
+#pragma unroll
+            for (int m = 0; m < PM; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (t0 + PM * 16 * wv + 16 * m + 4 * lc + r < Lo) {
+                        const float dlt = acc[m][n][r] - mu;
+                        q += dlt * dlt;
+                    }
+            q += __shfl_xor(q, 16);
+            q += __shfl_xor(q, 32);
+            if (lc == 0) red2[wv * TC + c] = q;
+        }
+        __syncthreads();
+        if (tid < TC && co0 + tid < g.Cout) {
+            const int64_t tile = (int64_t)b * gridDim.x + blockIdx.x;
+            float* sp = stats + tile * 2 * g.Cout + co0 + tid;
+            sp[0] = ((red1[tid] + red1[TC + tid]) + red1[2 * TC + tid]) + red1[3 * TC + tid];
+            sp[g.Cout] = ((red2[tid] + red2[TC + tid]) + red2[2 * TC + tid]) + red2[3 * TC + tid];
+        }
+    }
+}
+
+// BatchNorm batch statistics from the conv tiles' (sum, M2) partials (Chan's
+// parallel combination in double, fixed order): mean, rstd and the running
+// statistics (torch momentum semantics, unbiased running variance).
+// One workgroup per channel.
+__global__ __launch_bounds__(256) void k_bn_stats_finalize(const float* __restrict__ stats, int tiles_per_sample,
+                                                           int B, int TP, int Lo, int C, float eps, float momentum,
+                                                           float* __restrict__ mean, float* __restrict__ rstd,
+                                                           float* __restrict__ run_mean, float* __restrict__ run_var) {
+    __shared__ double red[256];
+    const int c = blockIdx.x, tid = threadIdx.x;
+    const int ntile = B * tiles_per_sample;
+    const double M = (double)B * Lo;
+    double a = 0.0;
+    for (int i = tid; i < ntile; i += 256) a += (double)stats[(int64_t)i * 2 * C + c];
+    red[tid] = a;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
+        __syncthreads();
+    }
+    const double mu = red[0] / M;
+    __syncthreads();
+    double q = 0.0;
+    for (int i = tid; i < ntile; i += 256) {
+        const int tx = i % tiles_per_sample;
+        const int n = Lo - tx * TP < TP ? Lo - tx * TP : TP;
+        const double s1 = (double)stats[(int64_t)i * 2 * C + c];
+        const double dm = s1 / n - mu;
+        q += (double)stats[(int64_t)i * 2 * C + C + c] + n * dm * dm;
+    }
+    red[tid] = q;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
+        __syncthreads();
+    }
+    if (tid != 0) return;
+    const double var = red[0] / M;
+    mean[c] = (float)mu;
+    rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (run_mean) {
+        const double unb = M > 1 ? var * M / (M - 1) : var;
+        run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mu);
+        run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+    }
 }
 
 // dW partial slabs: part[split][co][ci][k] over the split's rows.
@@ -342,47 +440,83 @@ static Geo geo(int B, int L_in, int Cin, int Cout, int K, int mode, int up) {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// launches the forward kernel (stats optional) and returns its position tile TP
 template <int K, int NT, bool FLIP_T>
-static void fwd_nt(const float* x, const Geo& g, const float* w, float* y, int Lo, hipStream_t st) {
+static int fwd_nt(const float* x, const Geo& g, const float* w, float* y, int Lo, float* stats, hipStream_t st) {
     using C = FwdCfg<K, NT>;
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
-    hipLaunchKernelGGL((k_conv_fwd<K, NT, FLIP_T>), grid, dim3(256), C::LDS_BYTES, st, x, g, w, y, Lo);
+    if (x) hipLaunchKernelGGL((k_conv_fwd<K, NT, FLIP_T>), grid, dim3(256), C::LDS_BYTES, st, x, g, w, y, Lo, stats);
+    return C::TP;
 }
 
 template <int K, bool FLIP_T>
-static void fwd_k(const float* x, const Geo& g, const float* w, float* y, int Lo, hipStream_t st) {
+static int fwd_k(const float* x, const Geo& g, const float* w, float* y, int Lo, float* stats, hipStream_t st) {
     switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
-        case 1: fwd_nt<K, 1, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 2: fwd_nt<K, 2, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 3: fwd_nt<K, 3, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 4: fwd_nt<K, 4, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 5: fwd_nt<K, 5, FLIP_T>(x, g, w, y, Lo, st); break;
-        default: fwd_nt<K, 6, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 1: return fwd_nt<K, 1, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 2: return fwd_nt<K, 2, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 3: return fwd_nt<K, 3, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 4: return fwd_nt<K, 4, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 5: return fwd_nt<K, 5, FLIP_T>(x, g, w, y, Lo, stats, st);
+        default: return fwd_nt<K, 6, FLIP_T>(x, g, w, y, Lo, stats, st);
     }
 }
 
+// x == nullptr: no launch, only the position tile TP of this geometry
 template <bool FLIP_T>
-static void launch_fwd(const float* x, const Geo& g, const float* w, float* y, int Lo, hipStream_t st) {
+static int launch_fwd(const float* x, const Geo& g, const float* w, float* y, int Lo, hipStream_t st,
+                      float* stats = nullptr) {
     switch (g.K) {
-        case 1: fwd_k<1, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 2: fwd_k<2, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 3: fwd_k<3, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 4: fwd_k<4, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 5: fwd_k<5, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 6: fwd_k<6, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 7: fwd_k<7, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 8: fwd_k<8, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 9: fwd_k<9, FLIP_T>(x, g, w, y, Lo, st); break;
-        case 10: fwd_k<10, FLIP_T>(x, g, w, y, Lo, st); break;
-        default: fwd_k<11, FLIP_T>(x, g, w, y, Lo, st); break;
+        case 1: return fwd_k<1, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 2: return fwd_k<2, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 3: return fwd_k<3, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 4: return fwd_k<4, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 5: return fwd_k<5, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 6: return fwd_k<6, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 7: return fwd_k<7, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 8: return fwd_k<8, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 9: return fwd_k<9, FLIP_T>(x, g, w, y, Lo, stats, st);
+        case 10: return fwd_k<10, FLIP_T>(x, g, w, y, Lo, stats, st);
+        default: return fwd_k<11, FLIP_T>(x, g, w, y, Lo, stats, st);
     }
 }
+
+// norm.hip: y = act(BN(x)) elementwise
+int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
+                    const float* beta, int act, float* y, hipStream_t st);
 
 }  // namespace vt
 
 using namespace vt;
 
 extern "C" {
+
+int vt_conv1d_bn_workspace_floats(int B, int L_in, int Cin, int Cout, int K, int mode, int up, int64_t* floats) {
+    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAX, "vt_conv1d_bn_workspace_floats");
+    Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
+    const int TP = launch_fwd<false>(nullptr, g, nullptr, nullptr, g.L_out, nullptr);
+    *floats = (int64_t)B * cdiv(g.L_out, TP) * 2 * Cout;
+    return VT_OK;
+}
+
+int vt_conv1d_bn_fwd(const float* X, int B, int L_in, int Cin, const float* W, int Cout, int K, int mode, int up,
+                     const float* gamma, const float* beta, int act, float eps, float momentum, float* conv_out,
+                     float* Y, float* mean, float* rstd, float* run_mean, float* run_var, float* ws,
+                     int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAX && (mode == 0 || mode == 1),
+                 "vt_conv1d_bn_fwd: shape (K <= %d)", KMAX);
+    Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
+    const int TP = launch_fwd<false>(nullptr, g, nullptr, nullptr, g.L_out, nullptr);
+    const int tps = cdiv(g.L_out, TP);
+    VT_CHECK_ARG(ws && ws_floats >= (int64_t)B * tps * 2 * Cout, "vt_conv1d_bn_fwd: workspace too small");
+    hipStream_t st = S(stream);
+    launch_fwd<false>(X, g, W, conv_out, g.L_out, st, ws);
+    hipLaunchKernelGGL(k_bn_stats_finalize, dim3(Cout), dim3(256), 0, st, ws, tps, B, TP, g.L_out, Cout, eps,
+                       momentum, mean, rstd, run_mean, run_var);
+    const int rc = bn_apply_launch(conv_out, (int64_t)B * g.L_out, Cout, mean, rstd, gamma, beta, act, Y, st);
+    if (rc) return rc;
+    VT_LAUNCH_CHECK("vt_conv1d_bn_fwd");
+    return VT_OK;
+}
 
 int vt_conv1d_direct_fwd(const float* X, int B, int L_in, int Cin, const float* W, int Cout, int K, int mode, int up,
                          float* Y, void* stream) {

@@ -448,6 +448,13 @@ __global__ void k_act_bwd(const float* __restrict__ dy, const float* __restrict_
 
 static inline unsigned blocks_for(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
+// y = act(BN(x)) for conv.hip's fused conv + BatchNorm forward
+int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
+                    const float* beta, int act, float* y, hipStream_t st) {
+    hipLaunchKernelGGL(k_bn_apply, dim3(blocks_for(M * C)), dim3(256), 0, st, x, M, C, mean, rstd, gamma, beta, act, y);
+    return VT_OK;
+}
+
 }  // namespace vt
 
 using namespace vt;

@@ -357,6 +357,19 @@ class LayerNormActF(torch.autograd.Function):
 
 
 # ------------------------------------------------- Conv1d + BatchNorm + act
+_CONV_WS = {}
+
+
+def _conv_bn_ws(*shape):
+    n = _CONV_WS.get(shape)
+    if n is None:
+        import ctypes
+        f = ctypes.c_int64()
+        call("vt_conv1d_bn_workspace_floats", *shape, ctypes.byref(f))
+        n = _CONV_WS[shape] = max(int(f.value), 4096 * shape[3] + 2 * shape[3])
+    return n
+
+
 class ConvBNActF(torch.autograd.Function):
     """(B, L, Cin) -> (B, L_out, Cout): conv (implicit GEMM with fused
     padding/upsampling) -> train-mode BatchNorm (running stats updated) -> act."""
@@ -369,13 +382,12 @@ class ConvBNActF(torch.autograd.Function):
         x = x.contiguous()
         Lo = _lib.lib().fns["vt_conv1d_out_len"](L, K, mode, up)
         conv = torch.empty((B, Lo, Cout), device=x.device)
-        call("vt_conv1d_direct_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(conv), _st())
         y = torch.empty_like(conv)
         mean = torch.empty(Cout, device=x.device)
         rstd = torch.empty(Cout, device=x.device)
-        ws = WS.get(4096 * Cout + 2 * Cout, x.device, 2)
-        call("vt_batchnorm_fwd", ptr(conv), B * Lo, Cout, ptr(g), ptr(b), ACT[act], eps, momentum, ptr(y), ptr(mean),
-             ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws), ws.numel(), _st())
+        ws = WS.get(_conv_bn_ws(B, L, Cin, Cout, K, mode, up), x.device, 2)
+        call("vt_conv1d_bn_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(g), ptr(b), ACT[act], eps, momentum,
+             ptr(conv), ptr(y), ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws), ws.numel(), _st())
         ctx.save_for_backward(x, conv, mean, rstd)
         ctx.params = (w, g, b)
         ctx.cfg = (mode, up, act)
