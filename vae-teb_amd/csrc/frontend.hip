@@ -223,6 +223,43 @@ __device__ __forceinline__ void dft16(float2 v[16]) {
     for (int i = 0; i < 16; ++i) v[i] = o[i];
 }
 
+// |a| e^{i p arg(a)} for the phase acceleration, in revolutions: atan2 by an
+// odd minimax polynomial of atan on [0, 1] (max error 1.3e-7 rad, fp32), the
+// angle times p reduced to [-1/2, 1/2] revolution, then the hardware
+// v_sin_f32 / v_cos_f32 (sin(2 pi x)).  Same branch convention as atan2f
+// (torch.angle): (-1, -0) -> -pi.
+__device__ __forceinline__ float2 accel(float2 a, float p) {
+    const float ax = fabsf(a.x), ay = fabsf(a.y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float t = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+    const float s = t * t;
+    float r = 0.000390918023f;
+    r = fmaf(r, s, -0.00229176274f);
+    r = fmaf(r, s, 0.00633099675f);
+    r = fmaf(r, s, -0.0115143927f);
+    r = fmaf(r, s, 0.016709527f);
+    r = fmaf(r, s, -0.0225382969f);
+    r = fmaf(r, s, 0.0318085626f);
+    r = fmaf(r, s, -0.0530504771f);
+    r = fmaf(r, s, 0.159154922f);
+    r *= t;                                  // atan(t) / (2 pi)
+    if (ay > ax) r = 0.25f - r;
+    if (a.x < 0.f) r = 0.5f - r;
+    r = copysignf(r, a.y);
+    float v = r * p;
+    v -= rintf(v);
+    const float mag = sqrtf(a.x * a.x + a.y * a.y);
+    return make_float2(mag * __builtin_amdgcn_cosf(v), mag * __builtin_amdgcn_sinf(v));
+}
+
+// W_32^n = exp(-2 pi i n / 32)
+constexpr float W32_RE[32] = {1.f, 0.980785251f, 0.923879504f, 0.831469595f, 0.707106769f, 0.555570245f,
+                                 0.382683426f, 0.195090324f, 0.f, -0.195090324f, -0.382683426f, -0.555570245f,
+                                 -0.707106769f, -0.831469595f, -0.923879504f, -0.980785251f, -1.f, -0.980785251f,
+                                 -0.923879504f, -0.831469595f, -0.707106769f, -0.555570245f, -0.382683426f,
+                                 -0.195090324f, 0.f, 0.195090324f, 0.382683426f, 0.555570245f, 0.707106769f,
+                                 0.831469595f, 0.923879504f, 0.980785251f};
+
 __global__ __launch_bounds__(256) void k_fe_pairs8k(
     const float2* __restrict__ analytic, int n_slots, int N, int pad_left, int n_pairs,
     const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
@@ -238,23 +275,34 @@ __global__ __launch_bounds__(256) void k_fe_pairs8k(
     const float2* ai = analytic + (b * n_slots + slot_i[pair]) * (int64_t)N;
     const float2* aj = analytic + (b * n_slots + slot_j[pair]) * (int64_t)N;
     const float pw = power[pair];
-    // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283), compact
-    for (int u = t; u < N; u += 256) {
-        const float2 x = ai[u], v = aj[u];
-        const float mag = sqrtf(x.x * x.x + x.y * x.y);
-        float sn, cs;
-        sincosf(atan2f(x.y, x.x) * pw, &sn, &cs);
-        img[u] = cmul(make_float2(mag * cs, mag * sn), cconj(v));
+    // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283), compact;
+    // loads in batches of 8 per thread (all in flight before the first use)
+    for (int u0 = t; u0 < N; u0 += 256 * 8) {
+        float2 xa[8], xb[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int u = u0 + 256 * k;
+            xa[k] = u < N ? ai[u] : make_float2(0.f, 0.f);
+            xb[k] = u < N ? aj[u] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int u = u0 + 256 * k;
+            if (u < N) img[u] = cmul(accel(xa[k], pw), cconj(xb[k]));
+        }
     }
     __syncthreads();
-    // 1: columns n1 = t, t + 256 of the padded signal (reflect / zero / circular)
+    // 1: columns n1 = t, t + 256 of the padded signal (reflect / zero / circular);
+    // one reflection at most on the training geometry (no modulo)
+    const bool single = pad_mode == 0 && pad_left <= N - 1 && PR_N - pad_left - N <= N - 1;
     float2 v[2][16];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int n1 = t + 256 * q;
 #pragma unroll
         for (int n2 = 0; n2 < 16; ++n2) {
-            const int s = pad_src(n1 + 512 * n2 - pad_left, N, pad_mode);
+            const int i = n1 + 512 * n2 - pad_left;
+            const int s = single ? (i < 0 ? -i : (i >= N ? 2 * N - 2 - i : i)) : pad_src(i, N, pad_mode);
             v[q][n2] = s < 0 ? make_float2(0.f, 0.f) : img[s];
         }
     }
@@ -287,11 +335,11 @@ __global__ __launch_bounds__(256) void k_fe_pairs8k(
         const int k2 = t >> 4, kb = t & 15;
         const float2* row = img + k2 * 528 + 33 * kb;
         float2 x0 = make_float2(0.f, 0.f), x1 = make_float2(0.f, 0.f);
-#pragma unroll 8
+#pragma unroll
         for (int n1a = 0; n1a < 32; ++n1a) {
             const float2 z = row[n1a];
             x0 = cadd(x0, z);
-            x1 = cadd(x1, cmul(z, tw[256 * n1a]));  // W_32^{n1a}
+            x1 = cadd(x1, cmul(z, make_float2(W32_RE[n1a], W32_RE[(n1a + 8) & 31])));  // W_32^{n1a}
         }
         const int k = k2 + 16 * kb;
         Z[k] = cscale(x0, phi0[k]);
@@ -303,6 +351,126 @@ __global__ __launch_bounds__(256) void k_fe_pairs8k(
     float* o = out + (b * n_pairs + pair) * (int64_t)S;
     const float inv = 1.0f / (float)PR_NB;
     for (int m = t; m < S; m += 256) o[m] = Rs[start + m].x * inv;
+}
+
+// ------------------------------------------- wavelets, 8192-point register FFT
+// Inverse FFT of xhat * psi for the training geometry (n_pad = 8192) as the
+// forward 16 x 16 x 32 decomposition of the pair kernel on conj(input)
+// (ifft(X) = conj(fft(conj X))), all three passes full: pass 1 reads the
+// spectrum straight from HBM into registers (no LDS staging), passes 2 / 3
+// run on the 33-padded LDS image, the result goes back to LDS in natural order
+// (padded every 32) for the coalesced analytic-signal copy and the S1
+// low-pass.  One 66 KB image: two workgroups per CU (the generic Stockham
+// path ping-pongs two 64 KB buffers: one).
+__device__ __forceinline__ void dft32(float2 v[32]) {
+    float2 e[16], o[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        e[i] = v[2 * i];
+        o[i] = v[2 * i + 1];
+    }
+    dft16(e);
+    dft16(o);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const float2 w = cmul(o[k], make_float2(W32_RE[k], W32_RE[(k + 8) & 31]));
+        v[k] = cadd(e[k], w);
+        v[k + 16] = csub(e[k], w);
+    }
+}
+
+__device__ __forceinline__ int nat_pos(int k) { return k + (k >> 5); }  // natural order, padded every 32
+
+__global__ __launch_bounds__(256) void k_fe_wavelet8k(
+    const float2* __restrict__ xhat, int C, const float* __restrict__ psi, const int* __restrict__ items,
+    const float2* __restrict__ tw, int N, int pad_left, float2* __restrict__ analytic, int n_slots,
+    const float* __restrict__ h0, int radius, int step, int start, int S, float* __restrict__ s1, int s1_channels,
+    int nowrap) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2* img = sm;  // PR_IMG
+    const int t = threadIdx.x;
+    const int item = blockIdx.x;
+    const int64_t b = blockIdx.y;
+    const int chan = items[item * 5 + 0], filt = items[item * 5 + 1], slot = items[item * 5 + 2];
+    const int s1ch = items[item * 5 + 3], k1 = items[item * 5 + 4];
+    const float2* xh = xhat + (b * C + chan) * (int64_t)PR_N;
+    const float* ps = psi + (int64_t)filt * PR_N;
+    // pass 1: columns n1 = t, t + 256 of conj(xhat * psi), straight from HBM
+    float2 v[2][16];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) {
+            const int n = t + 256 * q + 512 * n2;
+            const float2 x = xh[n];
+            const float p = ps[n];
+            v[q][n2] = make_float2(x.x * p, -x.y * p);
+        }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int n1 = t + 256 * q;
+        dft16(v[q]);
+        img[pr_pos(n1)] = v[q][0];
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(n1 + 512 * k2)] = cmul(v[q][k2], tw[(n1 * k2) & (PR_N - 1)]);
+    }
+    __syncthreads();
+    // pass 2: radix-16 over n1b inside block k2 (as k_fe_pairs8k)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int job = t + 256 * q, k2 = job >> 5, n1a = job & 31;
+        float2* base = img + k2 * 528 + n1a;
+        float2 w[16];
+#pragma unroll
+        for (int n1b = 0; n1b < 16; ++n1b) w[n1b] = base[33 * n1b];
+        dft16(w);
+        base[0] = w[0];
+#pragma unroll
+        for (int kb = 1; kb < 16; ++kb) base[33 * kb] = cmul(w[kb], tw[(16 * n1a * kb) & (PR_N - 1)]);
+    }
+    __syncthreads();
+    // pass 3: full radix-32 over n1a: X[k2 + 16 kb + 256 ka]
+    const int k2 = t >> 4, kb = t & 15;
+    float2 r[32];
+    {
+        const float2* row = img + k2 * 528 + 33 * kb;
+#pragma unroll
+        for (int n1a = 0; n1a < 32; ++n1a) r[n1a] = row[n1a];
+    }
+    dft32(r);
+    __syncthreads();
+    const float inv_n = 1.0f / (float)PR_N;
+#pragma unroll
+    for (int ka = 0; ka < 32; ++ka) {
+        const int k = k2 + 16 * kb + 256 * ka;
+        img[nat_pos(k)] = make_float2(r[ka].x * inv_n, -r[ka].y * inv_n);
+    }
+    __syncthreads();
+    if (slot >= 0) {
+        float2* a = analytic + (b * n_slots + slot) * (int64_t)N;
+        for (int i = t; i < N; i += 256) a[i] = img[nat_pos(pad_left + i)];
+    }
+    if (s1ch >= 0) {
+        const int M = PR_N >> k1;
+        for (int m = t; m < S; m += 256) {
+            const int c = step * (m + start);
+            const int lo = (c - radius + (1 << k1) - 1) >> k1;
+            const int hi = (c + radius) >> k1;
+            float acc = 0.f;
+            for (int n = lo; n <= hi; ++n) {
+                int d = c - (n << k1);
+                d = d < 0 ? -d : d;
+                int nn = n;
+                if (!nowrap) {
+                    nn %= M;
+                    if (nn < 0) nn += M;
+                }
+                const float2 u = img[nat_pos(nn << k1)];
+                acc += sqrtf(u.x * u.x + u.y * u.y) * h0[d];
+            }
+            s1[(b * s1_channels + s1ch) * S + m] = acc;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- normalise
@@ -429,9 +597,17 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
     VT_CHECK_ARG(pow2(n_pad) && n_pad <= VT_FFT_MAX_LDS, "vt_fe_wavelet: n_pad=%d", n_pad);
     VT_CHECK_ARG(B > 0 && n_items > 0, "vt_fe_wavelet: empty");
     VT_CHECK_ARG(step * start - radius >= 0, "vt_fe_wavelet: lowpass window leaves the padded support");
-    hipLaunchKernelGGL(k_fe_wavelet, dim3(n_items, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
-                       (const float2*)xhat, C, n_pad, psi, n_items, items, (const float2*)tw, N, pad_left,
-                       (float2*)analytic, n_slots, h0, radius, step, start, S_out, s1, s1_channels);
+    if (n_pad == PR_N && pad_left + N <= PR_N) {
+        // the training geometry: register FFT, one 66 KB image
+        const int nowrap = step * (start + S_out - 1) + radius < n_pad ? 1 : 0;
+        hipLaunchKernelGGL(k_fe_wavelet8k, dim3(n_items, (unsigned)B), dim3(256), PR_IMG * sizeof(float2), S(stream),
+                           (const float2*)xhat, C, psi, items, (const float2*)tw, N, pad_left, (float2*)analytic,
+                           n_slots, h0, radius, step, start, S_out, s1, s1_channels, nowrap);
+    } else {
+        hipLaunchKernelGGL(k_fe_wavelet, dim3(n_items, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad),
+                           S(stream), (const float2*)xhat, C, n_pad, psi, n_items, items, (const float2*)tw, N,
+                           pad_left, (float2*)analytic, n_slots, h0, radius, step, start, S_out, s1, s1_channels);
+    }
     VT_LAUNCH_CHECK("vt_fe_wavelet");
     return VT_OK;
 }
