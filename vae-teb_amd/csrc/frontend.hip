@@ -178,6 +178,7 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
 // (index k2*512 + 32 n1b + n1a -> k2*528 + 33 n1b + n1a): passes 2 and 3 read
 // it along n1a and along n1b without bank conflicts.
 static constexpr int PR_N = 8192, PR_NB = 512, PR_IMG = 16 * 16 * 33;
+static constexpr int PR_T = 512;  // threads of the pair kernel (8 waves: latency hiding at 2 workgroups / CU)
 
 __device__ __forceinline__ int pr_pos(int idx) {  // natural index -> padded LDS position
     return (idx >> 5) * 33 + (idx & 31);
@@ -260,7 +261,7 @@ constexpr float W32_RE[32] = {1.f, 0.980785251f, 0.923879504f, 0.831469595f, 0.7
                                  -0.195090324f, 0.f, 0.195090324f, 0.382683426f, 0.555570245f, 0.707106769f,
                                  0.831469595f, 0.923879504f, 0.980785251f};
 
-__global__ __launch_bounds__(256) void k_fe_pairs8k(
+__global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
     const float2* __restrict__ analytic, int n_slots, int N, int pad_left, int n_pairs,
     const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
     const float2* __restrict__ tw, const float* __restrict__ phi0, int start, int S, int pad_mode,
@@ -277,28 +278,28 @@ __global__ __launch_bounds__(256) void k_fe_pairs8k(
     const float pw = power[pair];
     // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283), compact;
     // loads in batches of 8 per thread (all in flight before the first use)
-    for (int u0 = t; u0 < N; u0 += 256 * 8) {
+    for (int u0 = t; u0 < N; u0 += PR_T * 8) {
         float2 xa[8], xb[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const int u = u0 + 256 * k;
+            const int u = u0 + PR_T * k;
             xa[k] = u < N ? ai[u] : make_float2(0.f, 0.f);
             xb[k] = u < N ? aj[u] : make_float2(0.f, 0.f);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const int u = u0 + 256 * k;
+            const int u = u0 + PR_T * k;
             if (u < N) img[u] = cmul(accel(xa[k], pw), cconj(xb[k]));
         }
     }
     __syncthreads();
-    // 1: columns n1 = t, t + 256 of the padded signal (reflect / zero / circular);
+    // 1: columns n1 = t (+ PR_T) of the padded signal (reflect / zero / circular);
     // one reflection at most on the training geometry (no modulo)
     const bool single = pad_mode == 0 && pad_left <= N - 1 && PR_N - pad_left - N <= N - 1;
-    float2 v[2][16];
+    float2 v[512 / PR_T][16];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int n1 = t + 256 * q;
+    for (int q = 0; q < 512 / PR_T; ++q) {
+        const int n1 = t + PR_T * q;
 #pragma unroll
         for (int n2 = 0; n2 < 16; ++n2) {
             const int i = n1 + 512 * n2 - pad_left;
@@ -308,8 +309,8 @@ __global__ __launch_bounds__(256) void k_fe_pairs8k(
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int n1 = t + 256 * q;
+    for (int q = 0; q < 512 / PR_T; ++q) {
+        const int n1 = t + PR_T * q;
         dft16(v[q]);
         img[pr_pos(n1)] = v[q][0];
 #pragma unroll
@@ -318,8 +319,8 @@ __global__ __launch_bounds__(256) void k_fe_pairs8k(
     __syncthreads();
     // 2: jobs (k2, n1a): radix-16 over n1b inside block k2, in place
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int job = t + 256 * q, k2 = job >> 5, n1a = job & 31;
+    for (int q = 0; q < 512 / PR_T; ++q) {
+        const int job = t + PR_T * q, k2 = job >> 5, n1a = job & 31;
         float2* base = img + k2 * 528 + n1a;
         float2 w[16];
 #pragma unroll
@@ -330,27 +331,28 @@ __global__ __launch_bounds__(256) void k_fe_pairs8k(
         for (int kb = 1; kb < 16; ++kb) base[33 * kb] = cmul(w[kb], tw[(16 * n1a * kb) & (PR_N - 1)]);
     }
     __syncthreads();
-    // 3: (k2, k'b) = (t >> 4, t & 15): outputs k'a = 0, 1 of the radix-32 stage
+    // 3: (k2, k'b) = (j >> 4, j & 15), j = t & 255: output k'a = t >> 8 (0 or 1) of the radix-32 stage
     {
-        const int k2 = t >> 4, kb = t & 15;
+        const int j = t & 255, ka = t >> 8, k2 = j >> 4, kb = j & 15;
         const float2* row = img + k2 * 528 + 33 * kb;
-        float2 x0 = make_float2(0.f, 0.f), x1 = make_float2(0.f, 0.f);
+        float2 x = make_float2(0.f, 0.f);
+        if (ka == 0) {
 #pragma unroll
-        for (int n1a = 0; n1a < 32; ++n1a) {
-            const float2 z = row[n1a];
-            x0 = cadd(x0, z);
-            x1 = cadd(x1, cmul(z, make_float2(W32_RE[n1a], W32_RE[(n1a + 8) & 31])));  // W_32^{n1a}
+            for (int n1a = 0; n1a < 32; ++n1a) x = cadd(x, row[n1a]);
+        } else {
+#pragma unroll
+            for (int n1a = 0; n1a < 32; ++n1a)
+                x = cadd(x, cmul(row[n1a], make_float2(W32_RE[n1a], W32_RE[(n1a + 8) & 31])));  // W_32^{n1a}
         }
-        const int k = k2 + 16 * kb;
-        Z[k] = cscale(x0, phi0[k]);
-        Z[k + 256] = cscale(x1, phi0[k + 256]);
+        const int k = k2 + 16 * kb + 256 * ka;
+        Z[k] = cscale(x, phi0[k]);
     }
     __syncthreads();
     // 4: inverse FFT of length 512, keep [start, start + S)
     float2* Rs = fft_lds<true>(Z, Z2, PR_NB, tw, PR_N / PR_NB);
     float* o = out + (b * n_pairs + pair) * (int64_t)S;
     const float inv = 1.0f / (float)PR_NB;
-    for (int m = t; m < S; m += 256) o[m] = Rs[start + m].x * inv;
+    for (int m = t; m < S; m += PR_T) o[m] = Rs[start + m].x * inv;
 }
 
 // ------------------------------------------- wavelets, 8192-point register FFT
@@ -381,7 +383,7 @@ __device__ __forceinline__ void dft32(float2 v[32]) {
 
 __device__ __forceinline__ int nat_pos(int k) { return k + (k >> 5); }  // natural order, padded every 32
 
-__global__ __launch_bounds__(256) void k_fe_wavelet8k(
+__global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
     const float2* __restrict__ xhat, int C, const float* __restrict__ psi, const int* __restrict__ items,
     const float2* __restrict__ tw, int N, int pad_left, float2* __restrict__ analytic, int n_slots,
     const float* __restrict__ h0, int radius, int step, int start, int S, float* __restrict__ s1, int s1_channels,
@@ -395,20 +397,20 @@ __global__ __launch_bounds__(256) void k_fe_wavelet8k(
     const int s1ch = items[item * 5 + 3], k1 = items[item * 5 + 4];
     const float2* xh = xhat + (b * C + chan) * (int64_t)PR_N;
     const float* ps = psi + (int64_t)filt * PR_N;
-    // pass 1: columns n1 = t, t + 256 of conj(xhat * psi), straight from HBM
-    float2 v[2][16];
+    // pass 1: columns n1 = t (+ PR_T) of conj(xhat * psi), straight from HBM
+    float2 v[512 / PR_T][16];
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 512 / PR_T; ++q)
 #pragma unroll
         for (int n2 = 0; n2 < 16; ++n2) {
-            const int n = t + 256 * q + 512 * n2;
+            const int n = t + PR_T * q + 512 * n2;
             const float2 x = xh[n];
             const float p = ps[n];
             v[q][n2] = make_float2(x.x * p, -x.y * p);
         }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int n1 = t + 256 * q;
+    for (int q = 0; q < 512 / PR_T; ++q) {
+        const int n1 = t + PR_T * q;
         dft16(v[q]);
         img[pr_pos(n1)] = v[q][0];
 #pragma unroll
@@ -417,8 +419,8 @@ __global__ __launch_bounds__(256) void k_fe_wavelet8k(
     __syncthreads();
     // pass 2: radix-16 over n1b inside block k2 (as k_fe_pairs8k)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int job = t + 256 * q, k2 = job >> 5, n1a = job & 31;
+    for (int q = 0; q < 512 / PR_T; ++q) {
+        const int job = t + PR_T * q, k2 = job >> 5, n1a = job & 31;
         float2* base = img + k2 * 528 + n1a;
         float2 w[16];
 #pragma unroll
@@ -429,30 +431,32 @@ __global__ __launch_bounds__(256) void k_fe_wavelet8k(
         for (int kb = 1; kb < 16; ++kb) base[33 * kb] = cmul(w[kb], tw[(16 * n1a * kb) & (PR_N - 1)]);
     }
     __syncthreads();
-    // pass 3: full radix-32 over n1a: X[k2 + 16 kb + 256 ka]
-    const int k2 = t >> 4, kb = t & 15;
+    // pass 3: full radix-32 over n1a: X[k2 + 16 kb + 256 ka] (256 jobs)
+    const int k2 = (t & 255) >> 4, kb = t & 15;
     float2 r[32];
-    {
+    if (t < 256) {
         const float2* row = img + k2 * 528 + 33 * kb;
 #pragma unroll
         for (int n1a = 0; n1a < 32; ++n1a) r[n1a] = row[n1a];
+        dft32(r);
     }
-    dft32(r);
     __syncthreads();
     const float inv_n = 1.0f / (float)PR_N;
+    if (t < 256) {
 #pragma unroll
-    for (int ka = 0; ka < 32; ++ka) {
-        const int k = k2 + 16 * kb + 256 * ka;
-        img[nat_pos(k)] = make_float2(r[ka].x * inv_n, -r[ka].y * inv_n);
+        for (int ka = 0; ka < 32; ++ka) {
+            const int k = k2 + 16 * kb + 256 * ka;
+            img[nat_pos(k)] = make_float2(r[ka].x * inv_n, -r[ka].y * inv_n);
+        }
     }
     __syncthreads();
     if (slot >= 0) {
         float2* a = analytic + (b * n_slots + slot) * (int64_t)N;
-        for (int i = t; i < N; i += 256) a[i] = img[nat_pos(pad_left + i)];
+        for (int i = t; i < N; i += PR_T) a[i] = img[nat_pos(pad_left + i)];
     }
     if (s1ch >= 0) {
         const int M = PR_N >> k1;
-        for (int m = t; m < S; m += 256) {
+        for (int m = t; m < S; m += PR_T) {
             const int c = step * (m + start);
             const int lo = (c - radius + (1 << k1) - 1) >> k1;
             const int hi = (c + radius) >> k1;
@@ -600,7 +604,7 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
     if (n_pad == PR_N && pad_left + N <= PR_N) {
         // the training geometry: register FFT, one 66 KB image
         const int nowrap = step * (start + S_out - 1) + radius < n_pad ? 1 : 0;
-        hipLaunchKernelGGL(k_fe_wavelet8k, dim3(n_items, (unsigned)B), dim3(256), PR_IMG * sizeof(float2), S(stream),
+        hipLaunchKernelGGL(k_fe_wavelet8k, dim3(n_items, (unsigned)B), dim3(PR_T), PR_IMG * sizeof(float2), S(stream),
                            (const float2*)xhat, C, psi, items, (const float2*)tw, N, pad_left, (float2*)analytic,
                            n_slots, h0, radius, step, start, S_out, s1, s1_channels, nowrap);
     } else {
@@ -621,7 +625,7 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
     VT_CHECK_ARG(B > 0 && n_pairs > 0 && pad_mode >= 0 && pad_mode <= 2, "vt_fe_pairs: empty/pad_mode");
     if (dec == PR_N / PR_NB && n_pad == PR_N && start + S_out <= PR_NB && N <= PR_IMG) {
         // the training configuration (n_pad 8192, 512 low-pass bins): pruned transform
-        hipLaunchKernelGGL(k_fe_pairs8k, dim3(n_pairs, (unsigned)B), dim3(256),
+        hipLaunchKernelGGL(k_fe_pairs8k, dim3(n_pairs, (unsigned)B), dim3(PR_T),
                            (PR_IMG + 2 * PR_NB) * sizeof(float2), S(stream), (const float2*)analytic, n_slots, N,
                            pad_left, n_pairs, slot_i, slot_j, power, (const float2*)tw, phi0, start, S_out, pad_mode,
                            out);
