@@ -156,6 +156,8 @@ def main():
                     help="run the source / target encoders on one stream (default: two HIP streams)")
     ap.add_argument("--heads", choices=["bf16", "fp32"], default="bf16",
                     help="decoder R x R head GEMMs: bf16 MFMA (the reference trains under 16-bit autocast) or fp32")
+    ap.add_argument("--conv", choices=["bf16", "fp32"], default="bf16",
+                    help="conv blocks: bf16 MFMA with fp32 accumulation / BatchNorm (16-bit autocast) or exact fp32")
     args = ap.parse_args()
 
     rank, world, local, dev = init_distributed()
@@ -168,7 +170,7 @@ def main():
     S = plan.S
     torch.manual_seed(1234)  # same initial weights on every rank (DDP semantics)
     model = SeqVaeTeb(sequence_length=S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,
-                      cross_phase_channels=fe.C_x, head_precision=args.heads,
+                      cross_phase_channels=fe.C_x, head_precision=args.heads, conv_precision=args.conv,
                       concurrent_encoders=not args.serial_encoders).to(dev)
     trainer = Trainer(model, lr=1e-3, frontend=fe, world_size=world)
 
@@ -248,7 +250,10 @@ def main():
         "metric": "train samples/sec + ELBO, 4096-pt windows, batch 256, 1/2/4/8 MI355X",
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32" if args.heads == "fp32" else "fp32 (bf16 MFMA heads)",
+        "vs_baseline": None,
+        "dtype": "fp32" if (args.heads, args.conv) == ("fp32", "fp32") else
+                 "bf16 MFMA (" + " + ".join(n for n, v in (("decoder heads", args.heads), ("conv blocks", args.conv))
+                                           if v == "bf16") + "), fp32 accumulation; fp32 elsewhere",
         "data": "synthetic",
         "config": {"workload": f"c2: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTeb(R={16 * S}) "
                                f"train step, batch {B}/GPU", "global_batch": B * world, "seq_len": N,

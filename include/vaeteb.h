@@ -240,6 +240,21 @@ int vt_conv1d_bn_fwd(const float* X, int B, int L_in, int Cin, const float* W, i
                      const float* gamma, const float* beta, int act, float eps, float momentum, float* conv_out,
                      float* Y, float* mean, float* rstd, float* run_mean, float* run_var, float* ws,
                      int64_t ws_floats, void* stream);
+/* bf16-MFMA variants (conv_bf16.hip) — the reference trains under 16-bit
+ * autocast (ref/model/graph_model.py:510, :709-711): bf16 operands, fp32
+ * accumulation, fp32 activations and BatchNorm.  Weights come from a bf16
+ * shadow refreshed from the fp32 master weight W [Cout][Cin][K] once per
+ * step: w16 [Cout][K][ceil32(Cin)] (forward), w16t [Cin][K][ceil32(Cout)]
+ * = W[co][ci][K-1-k] (backward-data), zero-padded.                             */
+int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, void* w16t, void* stream);
+int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode,
+                          int up, const float* gamma, const float* beta, int act, float eps, float momentum,
+                          float* conv_out, float* Y, float* mean, float* rstd, float* run_mean, float* run_var,
+                          float* ws, int64_t ws_floats, void* stream);
+int vt_conv1d_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode, int up,
+                       float* Y, void* stream);
+int vt_conv1d_bwd_gpad_bf16(const float* dY, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode,
+                            int up, float* gpad, void* stream);
 /* Direct (LDS-windowed) conv kernels used on the training path (conv.hip), K <= 11:
  * forward; bwd-data as a full correlation into gpad (B, L_out+K-1, Cin) + fold;
  * bwd-weight with fixed-order split reduction.                                   */

@@ -1,0 +1,139 @@
+"""bf16-MFMA conv kernels (csrc/conv_bf16.hip) — the 16-bit-autocast precision
+of the reference's training (ref/model/graph_model.py:510, :709-711).
+
+Per geometry of SeqVaeTeb's conv blocks (causal encoder blocks, reflect /
+replicate decoder blocks with and without the x2 upsample):
+  * exact: small-integer activations and weights are exact in bf16 and their
+    sums exact in fp32, so forward and backward-data must equal the exact-fp32
+    kernels (conv.hip, themselves checked against torch in test_gpu_model.py)
+    bit for bit — this pins fragment maps, tap order / flip, padding, upsample;
+  * bf16 model: random operands vs the fp32 kernels run on the bf16-ROUNDED
+    operands: rel-L2 <= 1e-5 (accumulation order only);
+  * vs fp32: rel-L2 <= 1e-2 (bf16 has an 8-bit mantissa: ~3e-3 expected);
+  * model: a full SeqVaeTeb step with bf16 convs stays within 1e-2 of fp32.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GEOS = [  # B, L, Cin, Cout, K, mode, up
+    (4, 64, 16, 16, 5, 0, 0), (3, 70, 32, 32, 7, 0, 0), (2, 40, 87, 77, 11, 1, 0), (2, 48, 77, 66, 9, 1, 1),
+    (2, 100, 33, 22, 3, 1, 1), (2, 300, 11, 1, 3, 1, 0), (3, 3, 20, 13, 9, 1, 0), (2, 64, 44, 33, 5, 1, 1),
+]
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vaeteb import _lib
+    return _lib
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+
+def _shadow(L, w):
+    Cout, Cin, K = w.shape
+    up = lambda n: (n + 31) // 32 * 32
+    w16 = torch.empty(Cout * K * up(Cin), dtype=torch.bfloat16, device="cuda")
+    w16t = torch.empty(Cin * K * up(Cout), dtype=torch.bfloat16, device="cuda")
+    L.call("vt_conv1d_bf16_shadow", L.ptr(w), Cout, Cin, K, L.ptr(w16), L.ptr(w16t), L.stream())
+    return w16, w16t
+
+
+def _run(L, x, w, mode, up, dy):
+    B, Lin, Cin = x.shape
+    Cout, _, K = w.shape
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    y32, y16 = (torch.empty(B, Lo, Cout, device="cuda") for _ in range(2))
+    L.call("vt_conv1d_direct_fwd", L.ptr(x), B, Lin, Cin, L.ptr(w), Cout, K, mode, up, L.ptr(y32), L.stream())
+    w16, w16t = _shadow(L, w)
+    L.call("vt_conv1d_fwd_bf16", L.ptr(x), B, Lin, Cin, L.ptr(w16), Cout, K, mode, up, L.ptr(y16), L.stream())
+    g32, g16 = (torch.empty(B, Lo + K - 1, Cin, device="cuda") for _ in range(2))
+    L.call("vt_conv1d_direct_bwd_gpad", L.ptr(dy), B, Lin, Cin, L.ptr(w), Cout, K, mode, up, L.ptr(g32), L.stream())
+    L.call("vt_conv1d_bwd_gpad_bf16", L.ptr(dy), B, Lin, Cin, L.ptr(w16t), Cout, K, mode, up, L.ptr(g16),
+           L.stream())
+    return y32, y16, g32, g16
+
+
+def _ints(shape, seed, lo=-3, hi=4):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(lo, hi, shape, generator=g).float().cuda()
+
+
+@pytest.mark.parametrize("geo", GEOS)
+def test_conv_bf16_exact_integer(L, geo):
+    B, Lin, Cin, Cout, K, mode, up = geo
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    # even integers keep the x2 upsample's 1/4, 3/4 weights exact in bf16
+    x = _ints((B, Lin, Cin), 1) * 4
+    w = _ints((Cout, Cin, K), 2)
+    dy = _ints((B, Lo, Cout), 3)
+    y32, y16, g32, g16 = _run(L, x, w, mode, up, dy)
+    assert torch.equal(y16, y32)
+    assert torch.equal(g16, g32)
+
+
+@pytest.mark.parametrize("geo", GEOS)
+def test_conv_bf16_random(L, geo):
+    B, Lin, Cin, Cout, K, mode, up = geo
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    torch.manual_seed(sum(geo))
+    x = torch.randn(B, Lin, Cin, device="cuda")
+    w = torch.randn(Cout, Cin, K, device="cuda") / (Cin * K) ** 0.5
+    dy = torch.randn(B, Lo, Cout, device="cuda")
+    y32, y16, g32, g16 = _run(L, x, w, mode, up, dy)
+    assert _rel(y16, y32) < 1e-2 and _rel(g16, g32) < 1e-2
+    # the bf16 model: fp32 kernels on bf16-rounded operands (the forward rounds
+    # the upsampled / padded window values, so round x before a non-upsampling conv only)
+    rb = lambda t: t.bfloat16().float()
+    if not up:
+        y32b, _, _, _ = _run(L, rb(x), rb(w), mode, up, rb(dy))
+        assert _rel(y16, y32b) < 1e-5
+    _, _, g32b, _ = _run(L, x, rb(w), mode, up, rb(dy))
+    assert _rel(g16, g32b) < 1e-5
+
+
+def test_model_bf16_convs_close_to_fp32(golden):
+    """Full SeqVaeTeb training step (S = 16, reference golden weights/inputs):
+    bf16 convs vs the exact-fp32 step.  The ELBO parts agree within 1e-2.
+    Gradients: this small-batch model is rounding-sensitive (deep LayerNorm /
+    ReLU chains, BatchNorm over B*L = 64 rows: fp32 summation-order changes
+    alone move encoder gradients by 2e-4, test_gpu_model.py), so the bf16
+    gradients are held to the scale of the model's own sensitivity: their
+    deviation from the fp32 step (aggregate rel-L2 over the decoder conv stack
+    and heads, and over all parameters) must not exceed 3x that of an fp32 step
+    whose inputs carry a 4e-3 relative perturbation (bf16's rounding step)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb.model import SeqVaeTeb
+    g = golden("model_s16_b4")
+    batch = {k: torch.from_numpy(g[k]).cuda() for k in ("y_st", "y_ph", "x_ph", "y_raw")}
+    eps = torch.from_numpy(g["eps"]).cuda()
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    pert = {k: v * (1 + 4e-3 * torch.randn(v.shape, device="cuda", generator=gen)) if k != "y_raw" else v
+            for k, v in batch.items()}
+    res = {}
+    for name, prec, b in (("fp32", "fp32", batch), ("bf16", "bf16", batch), ("pert", "fp32", pert)):
+        m = det_fill_(SeqVaeTeb(sequence_length=16)).cuda()
+        m.set_conv_precision(prec)
+        out = m(b["y_st"], b["y_ph"], b["x_ph"], eps=eps)
+        loss = m.compute_loss(out, b["y_st"], b["y_ph"], b["y_raw"], beta=float(g["beta"]))
+        loss["total_loss"].backward()
+        res[name] = (loss, {n: p.grad.detach().double().clone() for n, p in m.named_parameters()})
+    for k in ("total_loss", "nll_loss", "mse_loss", "kld_loss"):
+        a, b = res["bf16"][0][k].item(), res["fp32"][0][k].item()
+        assert abs(a - b) <= 1e-2 * abs(b), (k, a, b)
+
+    def dev(name, prefix):
+        ref = res["fp32"][1]
+        num = sum((res[name][1][n] - v).norm() ** 2 for n, v in ref.items() if n.startswith(prefix))
+        den = sum(v.norm() ** 2 for n, v in ref.items() if n.startswith(prefix))
+        return (num / den).sqrt().item()
+    for prefix in (("decoder.conv.", "decoder.output_"), ""):
+        assert dev("bf16", prefix) <= 3 * dev("pert", prefix) + 1e-3, (prefix, dev("bf16", prefix),
+                                                                         dev("pert", prefix))

@@ -1,0 +1,52 @@
+// Conv1d geometry shared by the fp32 (conv.hip) and bf16 (conv_bf16.hip)
+// kernels: padding / x2 linear upsampling applied while an operand window is
+// staged (ref/model/vae_teb_model.py:128-253).
+#pragma once
+#include "common.h"
+
+namespace vt {
+
+struct Geo {
+    int B, L_in, Cin, Cout, K, up, mode, L_up, pad, L_out;
+};
+
+// input value at padded position tp (upsampled domain) — see gemm.hip conv_src
+__device__ __forceinline__ float src_val(const float* __restrict__ xb, const Geo& g, int tp, int ci) {
+    int t = tp - g.pad;
+    if (g.mode == 0) {
+        if (t < 0 || t >= g.L_up) return 0.f;
+    } else if (g.L_up <= g.pad) {
+        t = t < 0 ? 0 : (t >= g.L_up ? g.L_up - 1 : t);
+    } else {
+        t = t < 0 ? -t : t;
+        t = t >= g.L_up ? 2 * (g.L_up - 1) - t : t;
+    }
+    if (!g.up) return xb[(int64_t)t * g.Cin + ci];
+    float s = (t + 0.5f) * 0.5f - 0.5f;
+    s = s < 0.f ? 0.f : s;
+    const int i0 = (int)s;
+    const int i1 = i0 + 1 < g.L_in ? i0 + 1 : g.L_in - 1;
+    const float l1 = s - (float)i0;
+    return (1.f - l1) * xb[(int64_t)i0 * g.Cin + ci] + l1 * xb[(int64_t)i1 * g.Cin + ci];
+}
+
+
+static inline Geo geo(int B, int L_in, int Cin, int Cout, int K, int mode, int up) {
+    Geo g;
+    g.B = B; g.L_in = L_in; g.Cin = Cin; g.Cout = Cout; g.K = K; g.mode = mode; g.up = up;
+    g.L_up = L_in * (up ? 2 : 1);
+    g.pad = mode == 0 ? K - 1 : (K - 1) / 2;
+    g.L_out = mode == 0 ? g.L_up : g.L_up + 2 * g.pad - K + 1;
+    return g;
+}
+
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+int bn_stats_finalize_launch(const float* stats, int tiles_per_sample, int B, int TP, int Lo, int C, float eps,
+                             float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
+                             hipStream_t st);
+int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
+                    const float* beta, int act, float* y, hipStream_t st);
+
+}  // namespace vt

@@ -1,0 +1,287 @@
+// bf16-MFMA 1-D convolution for the conv blocks (SURVEY.md §8(a) a11, a15;
+// ref/model/vae_teb_model.py:128-253) in the reference's training precision:
+// the reference trains under 16-bit autocast (Lightning precision="16-mixed",
+// ref/model/graph_model.py:510; torch.amp.autocast, :709-711), i.e. conv
+// operands in 16 bits with fp32 accumulation.  Here: bf16 operands on
+// v_mfma_f32_16x16x32_bf16 (16x the fp32 MFMA rate), fp32 accumulation, fp32
+// activations in HBM (the window is converted while it is staged), BatchNorm
+// statistics / apply in fp32 exactly as on the fp32 path.
+//
+// Same implicit GEMM as conv.hip's k_conv_fwd: a workgroup (4 waves) owns
+// (sample, TP output positions, TC = 16*NT output channels); per chunk of 32
+// input channels it stages the input window (padding / x2 upsample applied,
+// -> bf16) and the chunk's taps (from a bf16 weight shadow laid out
+// [out][K][in32], one 16-byte row segment per load), then one MFMA k-step per
+// tap: lane group lc takes input channels 8*lc .. 8*lc+7 of the chunk, so a
+// fragment is one ds_read_b128 of a window row (shifted by the tap) or a tap
+// row.  Rows are 40 bf16 (20 dwords) apart: 16 consecutive rows hit 16
+// distinct 4-bank groups.  Backward-data is the same kernel on dY with the
+// transposed / flipped shadow (causal padding K-1), as in conv.hip.
+#include "conv.h"
+
+namespace vt {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int CB = 32;   // input channels per staged chunk (= one MFMA k-step)
+constexpr int RS = 40;   // bf16 row stride of window and tap rows
+
+template <int K, int NT>
+struct BCfg {
+    static constexpr int PM = NT <= 2 ? 4 : 2;                  // position tiles per wave
+    static constexpr int TC = 16 * NT, TP = 64 * PM, WIN = TP + K - 1;
+    static constexpr int XB = WIN * RS, WB = K * TC * RS;       // bf16 elements
+    static constexpr int LDS_BYTES = (XB + WB) * 2 > 8 * TC * 4 ? (XB + WB) * 2 : 8 * TC * 4;
+};
+
+__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+    return r;
+}
+
+// x: fp32 (B, L_in, g.Cin) activations; w16: [g.Cout][K][cin32] bf16 shadow.
+template <int K, int NT>
+__global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, Geo g, const __bf16* __restrict__ w16,
+                                                   int cin32, float* __restrict__ y, int Lo,
+                                                   float* __restrict__ stats) {
+    using C = BCfg<K, NT>;
+    constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
+    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
+    __bf16* xs = lb;           // [WIN][RS]
+    __bf16* ws = lb + C::XB;   // [K][TC][RS]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
+    const int t0 = blockIdx.x * TP, co0 = blockIdx.y * TC, b = blockIdx.z;
+    const float* xb = x + (int64_t)b * g.L_in * g.Cin;
+    f32x4 acc[PM][NT];
+#pragma unroll
+    for (int m = 0; m < PM; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < g.Cin; c0 += CB) {
+        // window: WIN rows x 4 octets of 8 channels, fp32 -> bf16
+        for (int i = tid; i < WIN * 4; i += 256) {
+            const int row = i >> 2, oct = i & 3;
+            const int tp = t0 + row, cb = c0 + 8 * oct;
+            float v[8];
+            const bool ok = tp < Lo + K - 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (ok && cb + j < g.Cin) ? src_val(xb, g, tp, cb + j) : 0.f;
+            *(bf16x8*)(xs + row * RS + 8 * oct) = pack8(v);
+        }
+        // taps: K x TC rows x 4 octets, 16 B each from the shadow
+        for (int i = tid; i < K * TC * 4; i += 256) {
+            const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
+            bf16x8 val;
+            if (co0 + co < g.Cout) {
+                val = *(const bf16x8*)(w16 + ((int64_t)(co0 + co) * K + k) * cin32 + c0 + 8 * oct);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
+            }
+            *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = val;
+        }
+        __syncthreads();
+        const __bf16* xq = xs + (PM * 16 * wv + lr) * RS + 8 * lc;
+        const __bf16* wq = ws + lr * RS + 8 * lc;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            bf16x8 af[PM], bf[NT];
+#pragma unroll
+            for (int m = 0; m < PM; ++m) af[m] = *(const bf16x8*)(xq + (16 * m + k) * RS);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) bf[n] = *(const bf16x8*)(wq + (k * TC + 16 * n) * RS);
+#pragma unroll
+            for (int m = 0; m < PM; ++m)
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bf[n], acc[m][n], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // D layout: col (channel) = lane & 15, row (position) = 4 * (lane >> 4) + r
+#pragma unroll
+    for (int m = 0; m < PM; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int t = t0 + PM * 16 * wv + 16 * m + 4 * lc + r;
+            if (t >= Lo) continue;
+            float* yr = y + ((int64_t)b * Lo + t) * g.Cout;
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int co = co0 + 16 * n + lr;
+                if (co < g.Cout) yr[co] = acc[m][n][r];
+            }
+        }
+    if (stats) {
+        // BatchNorm tile statistics, as conv.hip k_conv_fwd
+        float* red1 = reinterpret_cast<float*>(lb);  // [4][TC]
+        float* red2 = red1 + 4 * TC;                 // [4][TC]
+        const int nrow = Lo - t0 < TP ? Lo - t0 : TP;
+        float cs[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            float a = 0.f;
+#pragma unroll
+            for (int m = 0; m < PM; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (t0 + PM * 16 * wv + 16 * m + 4 * lc + r < Lo) a += acc[m][n][r];
+            a += __shfl_xor(a, 16);
+            a += __shfl_xor(a, 32);
+            cs[n] = a;
+        }
+        if (lc == 0)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) red1[wv * TC + 16 * n + lr] = cs[n];
+        __syncthreads();
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int c = 16 * n + lr;
+            const float mu = (((red1[c] + red1[TC + c]) + red1[2 * TC + c]) + red1[3 * TC + c]) / (float)nrow;
+            float q = 0.f;
+#pragma unroll
+            for (int m = 0; m < PM; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (t0 + PM * 16 * wv + 16 * m + 4 * lc + r < Lo) {
+                        const float dlt = acc[m][n][r] - mu;
+                        q += dlt * dlt;
+                    }
+            q += __shfl_xor(q, 16);
+            q += __shfl_xor(q, 32);
+            if (lc == 0) red2[wv * TC + c] = q;
+        }
+        __syncthreads();
+        if (tid < TC && co0 + tid < g.Cout) {
+            const int64_t tile = (int64_t)b * gridDim.x + blockIdx.x;
+            float* sp = stats + tile * 2 * g.Cout + co0 + tid;
+            sp[0] = ((red1[tid] + red1[TC + tid]) + red1[2 * TC + tid]) + red1[3 * TC + tid];
+            sp[g.Cout] = ((red2[tid] + red2[TC + tid]) + red2[2 * TC + tid]) + red2[3 * TC + tid];
+        }
+    }
+}
+
+// bf16 shadows of W [Cout][Cin][K]: w16 [Cout][K][cin32] (forward) and
+// w16t [Cin][K][cout32] = W[co][ci][K-1-k] (backward-data), zero-padded.
+__global__ void k_conv_shadow(const float* __restrict__ W, int Cout, int Cin, int K, int cin32, int cout32,
+                              __bf16* __restrict__ w16, __bf16* __restrict__ w16t) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n1 = (int64_t)Cout * K * cin32;
+    if (i < n1) {
+        const int ci = (int)(i % cin32);
+        const int64_t r = i / cin32;
+        const int k = (int)(r % K), co = (int)(r / K);
+        w16[i] = (__bf16)(ci < Cin ? W[((int64_t)co * Cin + ci) * K + k] : 0.f);
+    } else if (i < n1 + (int64_t)Cin * K * cout32) {
+        const int64_t j = i - n1;
+        const int co = (int)(j % cout32);
+        const int64_t r = j / cout32;
+        const int k = (int)(r % K), ci = (int)(r / K);
+        w16t[j] = (__bf16)(co < Cout ? W[((int64_t)co * Cin + ci) * K + (K - 1 - k)] : 0.f);
+    }
+}
+
+template <int K, int NT>
+int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
+          hipStream_t st) {
+    using C = BCfg<K, NT>;
+    dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
+    if (x)
+        hipLaunchKernelGGL((k_conv_bf16<K, NT>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y, Lo, stats);
+    return C::TP;
+}
+
+template <int K>
+int bf_k(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats, hipStream_t st) {
+    switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
+        case 1: return bf_nt<K, 1>(x, g, w16, cin32, y, Lo, stats, st);
+        case 2: return bf_nt<K, 2>(x, g, w16, cin32, y, Lo, stats, st);
+        case 3: return bf_nt<K, 3>(x, g, w16, cin32, y, Lo, stats, st);
+        case 4: return bf_nt<K, 4>(x, g, w16, cin32, y, Lo, stats, st);
+        case 5: return bf_nt<K, 5>(x, g, w16, cin32, y, Lo, stats, st);
+        default: return bf_nt<K, 6>(x, g, w16, cin32, y, Lo, stats, st);
+    }
+}
+
+// x == nullptr: no launch, only the position tile of this geometry
+int bf_launch(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
+              hipStream_t st) {
+    switch (g.K) {
+        case 1: return bf_k<1>(x, g, w16, cin32, y, Lo, stats, st);
+        case 2: return bf_k<2>(x, g, w16, cin32, y, Lo, stats, st);
+        case 3: return bf_k<3>(x, g, w16, cin32, y, Lo, stats, st);
+        case 4: return bf_k<4>(x, g, w16, cin32, y, Lo, stats, st);
+        case 5: return bf_k<5>(x, g, w16, cin32, y, Lo, stats, st);
+        case 6: return bf_k<6>(x, g, w16, cin32, y, Lo, stats, st);
+        case 7: return bf_k<7>(x, g, w16, cin32, y, Lo, stats, st);
+        case 8: return bf_k<8>(x, g, w16, cin32, y, Lo, stats, st);
+        case 9: return bf_k<9>(x, g, w16, cin32, y, Lo, stats, st);
+        case 10: return bf_k<10>(x, g, w16, cin32, y, Lo, stats, st);
+        default: return bf_k<11>(x, g, w16, cin32, y, Lo, stats, st);
+    }
+}
+
+constexpr int KMAXB = 11;
+
+}  // namespace
+}  // namespace vt
+
+using namespace vt;
+
+extern "C" {
+
+int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, void* w16t, void* stream) {
+    VT_CHECK_ARG(Cout > 0 && Cin > 0 && K > 0 && K <= KMAXB, "vt_conv1d_bf16_shadow: shape");
+    const int cin32 = cdiv(Cin, 32) * 32, cout32 = cdiv(Cout, 32) * 32;
+    const int64_t n = (int64_t)Cout * K * cin32 + (int64_t)Cin * K * cout32;
+    hipLaunchKernelGGL(k_conv_shadow, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(stream), W, Cout, Cin, K,
+                       cin32, cout32, (__bf16*)w16, (__bf16*)w16t);
+    VT_LAUNCH_CHECK("vt_conv1d_bf16_shadow");
+    return VT_OK;
+}
+
+int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode,
+                          int up, const float* gamma, const float* beta, int act, float eps, float momentum,
+                          float* conv_out, float* Y, float* mean, float* rstd, float* run_mean, float* run_var,
+                          float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB && (mode == 0 || mode == 1),
+                 "vt_conv1d_bn_fwd_bf16: shape (K <= %d)", KMAXB);
+    Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
+    const int cin32 = cdiv(Cin, 32) * 32;
+    const int TP = bf_launch(nullptr, g, nullptr, cin32, nullptr, g.L_out, nullptr, nullptr);
+    const int tps = cdiv(g.L_out, TP);
+    VT_CHECK_ARG(ws && ws_floats >= (int64_t)B * tps * 2 * Cout, "vt_conv1d_bn_fwd_bf16: workspace too small");
+    hipStream_t st = S(stream);
+    bf_launch(X, g, (const __bf16*)w16, cin32, conv_out, g.L_out, ws, st);
+    bn_stats_finalize_launch(ws, tps, B, TP, g.L_out, Cout, eps, momentum, mean, rstd, run_mean, run_var, st);
+    bn_apply_launch(conv_out, (int64_t)B * g.L_out, Cout, mean, rstd, gamma, beta, act, Y, st);
+    VT_LAUNCH_CHECK("vt_conv1d_bn_fwd_bf16");
+    return VT_OK;
+}
+
+int vt_conv1d_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode, int up,
+                       float* Y, void* stream) {
+    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB && (mode == 0 || mode == 1),
+                 "vt_conv1d_fwd_bf16: shape (K <= %d)", KMAXB);
+    Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
+    bf_launch(X, g, (const __bf16*)w16, cdiv(Cin, 32) * 32, Y, g.L_out, nullptr, S(stream));
+    VT_LAUNCH_CHECK("vt_conv1d_fwd_bf16");
+    return VT_OK;
+}
+
+int vt_conv1d_bwd_gpad_bf16(const float* dY, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode,
+                            int up, float* gpad, void* stream) {
+    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB, "vt_conv1d_bwd_gpad_bf16: shape");
+    Geo f = geo(B, L_in, Cin, Cout, K, mode, up);
+    Geo g = geo(B, f.L_out, Cout, Cin, K, 0, 0);  // input dY (L_out x Cout), causal pad K-1
+    bf_launch(dY, g, (const __bf16*)w16t, cdiv(Cout, 32) * 32, gpad, f.L_out + K - 1, nullptr, S(stream));
+    VT_LAUNCH_CHECK("vt_conv1d_bwd_gpad_bf16");
+    return VT_OK;
+}
+
+}  // extern "C"

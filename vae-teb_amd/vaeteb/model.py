@@ -230,6 +230,7 @@ class ConvBlock(nn.Module):
     def __init__(self, cin, cout, k, causal, up=False, tanh=False):
         super().__init__()
         self.causal, self.up, self.tanh = causal, up, tanh
+        self.bf16 = False  # bf16-MFMA conv (the reference's 16-bit autocast precision); BatchNorm stays fp32
         self.conv = _ConvWeight(cin, cout, k)
         self.bn_layer = _BatchNorm(cout)
 
@@ -239,7 +240,7 @@ class ConvBlock(nn.Module):
             raise NotImplementedError("eval-mode BatchNorm is not on the training path yet")
         y = ops.conv_bn_act(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                             mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
-                            momentum=bn.momentum, eps=bn.eps)
+                            momentum=bn.momentum, eps=bn.eps, bf16=self.bf16)
         bn.num_batches_tracked.add_(1)
         return y
 
@@ -388,7 +389,8 @@ class SeqVaeTeb(nn.Module):
 
     def __init__(self, input_channels=76, sequence_length=300, latent_dim_source=32, latent_dim_target=32,
                  latent_dim_z=32, decimation_factor=16, warmup_period=30, scattering_channels=43,
-                 phase_channels=44, cross_phase_channels=130, head_precision="fp32", concurrent_encoders=False):
+                 phase_channels=44, cross_phase_channels=130, head_precision="fp32", concurrent_encoders=False,
+                 conv_precision="fp32"):
         super().__init__()
         # the source and target encoders are independent until the conditional
         # encoder: on a GPU they can run on two HIP streams (their LSTM
@@ -401,6 +403,18 @@ class SeqVaeTeb(nn.Module):
         self.target_encoder = TargetEncoder(scattering_channels, phase_channels)
         self.conditional_encoder = ConditionalEncoder(latent_dim_source, latent_dim_target)
         self.decoder = Decoder(latent_dim_z, sequence_length, head_precision)
+        self.set_conv_precision(conv_precision)
+
+    def set_conv_precision(self, precision):
+        """"fp32": exact-fp32 MFMA convs (parity mode); "bf16": bf16-MFMA convs with
+        fp32 accumulation and fp32 BatchNorm — the reference trains under 16-bit
+        autocast (ref/model/graph_model.py:510, :709-711)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"conv_precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.conv_precision = precision
+        for m in self.modules():
+            if isinstance(m, ConvBlock):
+                m.bf16 = precision == "bf16"
 
     def forward(self, y_st, y_ph, x_ph, eps=None):
         prev = dict(_PAR)

@@ -358,6 +358,23 @@ class LayerNormActF(torch.autograd.Function):
 
 # ------------------------------------------------- Conv1d + BatchNorm + act
 _CONV_WS = {}
+_CONV_SHADOW = {}
+
+
+def _conv_shadow(w):
+    """bf16 shadows of a conv weight W [Cout][Cin][K] (vt_conv1d_bf16_shadow):
+    w16 [Cout][K][ceil32(Cin)] and the transposed / flipped w16t
+    [Cin][K][ceil32(Cout)], rewritten from W on every forward."""
+    Cout, Cin, K = w.shape
+    key = (w.data_ptr(), Cout, Cin, K)
+    sh = _CONV_SHADOW.get(key)
+    if sh is None:
+        up32 = lambda n: (n + 31) // 32 * 32
+        sh = (torch.empty(Cout * K * up32(Cin), dtype=torch.bfloat16, device=w.device),
+              torch.empty(Cin * K * up32(Cout), dtype=torch.bfloat16, device=w.device))
+        _CONV_SHADOW[key] = sh
+    call("vt_conv1d_bf16_shadow", ptr(w), Cout, Cin, K, ptr(sh[0]), ptr(sh[1]), _st())
+    return sh
 
 
 def _conv_bn_ws(*shape):
@@ -375,7 +392,7 @@ class ConvBNActF(torch.autograd.Function):
     padding/upsampling) -> train-mode BatchNorm (running stats updated) -> act."""
 
     @staticmethod
-    def forward(ctx, x, w, g, b, run_mean, run_var, mode, up, act, momentum, eps):
+    def forward(ctx, x, w, g, b, run_mean, run_var, mode, up, act, momentum, eps, bf16=False):
         _check(x, w, g, b)
         B, L, Cin = x.shape
         Cout, _, K = w.shape
@@ -386,18 +403,26 @@ class ConvBNActF(torch.autograd.Function):
         mean = torch.empty(Cout, device=x.device)
         rstd = torch.empty(Cout, device=x.device)
         ws = WS.get(_conv_bn_ws(B, L, Cin, Cout, K, mode, up), x.device, 2)
-        call("vt_conv1d_bn_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(g), ptr(b), ACT[act], eps, momentum,
-             ptr(conv), ptr(y), ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws), ws.numel(), _st())
-        ctx.save_for_backward(x, conv, mean, rstd)
+        w16t = None
+        if bf16:
+            w16, w16t = _conv_shadow(w)
+            call("vt_conv1d_bn_fwd_bf16", ptr(x), B, L, Cin, ptr(w16), Cout, K, mode, up, ptr(g), ptr(b), ACT[act],
+                 eps, momentum, ptr(conv), ptr(y), ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws),
+                 ws.numel(), _st())
+        else:
+            call("vt_conv1d_bn_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(g), ptr(b), ACT[act], eps,
+                 momentum, ptr(conv), ptr(y), ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws), ws.numel(),
+                 _st())
+        ctx.save_for_backward(x, conv, mean, rstd, w16t)
         ctx.params = (w, g, b)
-        ctx.cfg = (mode, up, act)
+        ctx.cfg = (mode, up, act, bf16)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, conv, mean, rstd = ctx.saved_tensors
+        x, conv, mean, rstd, w16t = ctx.saved_tensors
         w, g, b = ctx.params
-        mode, up, act = ctx.cfg
+        mode, up, act, bf16 = ctx.cfg
         B, L, Cin = x.shape
         Cout, _, K = w.shape
         Lo = conv.shape[1]
@@ -411,7 +436,10 @@ class ConvBNActF(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             gpad = WS.get(B * (Lo + K - 1) * Cin, x.device, 3)
-            call("vt_conv1d_direct_bwd_gpad", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gpad), _st())
+            if bf16:
+                call("vt_conv1d_bwd_gpad_bf16", ptr(gconv), B, L, Cin, ptr(w16t), Cout, K, mode, up, ptr(gpad), _st())
+            else:
+                call("vt_conv1d_direct_bwd_gpad", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gpad), _st())
             call("vt_conv1d_fold", ptr(gpad), B, L, Cin, Cout, K, mode, up, ptr(gx), 0, _st())
         pw = _ParamGrads([w], [ctx.needs_input_grad[1]])
         if pw.out[0] is not None:
@@ -420,7 +448,7 @@ class ConvBNActF(torch.autograd.Function):
                  pw.acc, ptr(ws1), ws1.numel(), _st())
         gw, = pw.result()
         gg, gb = pbn.result()
-        return gx, gw, gg, gb, None, None, None, None, None, None, None
+        return gx, gw, gg, gb, None, None, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------- LSTM
@@ -569,8 +597,8 @@ def layer_norm_act(x, g, b, act="none", eps=1e-5):
     return LayerNormActF.apply(x, g, b, act, eps)
 
 
-def conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momentum=0.9, eps=1e-5):
-    return ConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps)
+def conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momentum=0.9, eps=1e-5, bf16=False):
+    return ConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps, bool(bf16))
 
 
 def lstm(x, params):
