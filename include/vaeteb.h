@@ -255,6 +255,10 @@ int vt_conv1d_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16
                        float* Y, void* stream);
 int vt_conv1d_bwd_gpad_bf16(const float* dY, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode,
                             int up, float* gpad, void* stream);
+/* dW (+)= sum_rows dY^T xpad on bf16 MFMA (transposed LDS reads), fixed-order
+ * split reduction; channels <= 128; ws as vt_conv1d_direct_bwd_weight.          */
+int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode,
+                              int up, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);
 /* Direct (LDS-windowed) conv kernels used on the training path (conv.hip), K <= 11:
  * forward; bwd-data as a full correlation into gpad (B, L_out+K-1, Cin) + fold;
  * bwd-weight with fixed-order split reduction.                                   */

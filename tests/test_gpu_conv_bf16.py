@@ -97,6 +97,32 @@ def test_conv_bf16_random(L, geo):
     assert _rel(g16, g32b) < 1e-5
 
 
+def _dw(L, fn, dy, x, mode, up, Cout, K):
+    B, Lin, Cin = x.shape
+    dw = torch.empty(Cout, Cin, K, device="cuda")
+    ws = torch.empty(1 << 24, device="cuda")
+    L.call(fn, L.ptr(dy), L.ptr(x), B, Lin, Cin, Cout, K, mode, up, L.ptr(dw), 0, L.ptr(ws), ws.numel(), L.stream())
+    return dw
+
+
+@pytest.mark.parametrize("geo", GEOS)
+def test_conv_bf16_weight_grad(L, geo):
+    """dW on bf16 MFMA (transposed LDS reads): exact on small integers, bf16
+    model 1e-5, vs fp32 1e-2."""
+    B, Lin, Cin, Cout, K, mode, up = geo
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    x, dy = _ints((B, Lin, Cin), 4) * 4, _ints((B, Lo, Cout), 5)
+    assert torch.equal(_dw(L, "vt_conv1d_bwd_weight_bf16", dy, x, mode, up, Cout, K),
+                       _dw(L, "vt_conv1d_direct_bwd_weight", dy, x, mode, up, Cout, K))
+    torch.manual_seed(sum(geo) + 1)
+    x, dy = torch.randn(B, Lin, Cin, device="cuda"), torch.randn(B, Lo, Cout, device="cuda")
+    d16 = _dw(L, "vt_conv1d_bwd_weight_bf16", dy, x, mode, up, Cout, K)
+    assert _rel(d16, _dw(L, "vt_conv1d_direct_bwd_weight", dy, x, mode, up, Cout, K)) < 1e-2
+    if not up:
+        rb = lambda t: t.bfloat16().float()
+        assert _rel(d16, _dw(L, "vt_conv1d_direct_bwd_weight", rb(dy), rb(x), mode, up, Cout, K)) < 1e-5
+
+
 def test_model_bf16_convs_close_to_fp32(golden):
     """Full SeqVaeTeb training step (S = 16, reference golden weights/inputs):
     bf16 convs vs the exact-fp32 step.  The ELBO parts agree within 1e-2.

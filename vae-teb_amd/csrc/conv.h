@@ -46,6 +46,7 @@ static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 int bn_stats_finalize_launch(const float* stats, int tiles_per_sample, int B, int TP, int Lo, int C, float eps,
                              float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
                              hipStream_t st);
+int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st);
 int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
                     const float* beta, int act, float* y, hipStream_t st);
 

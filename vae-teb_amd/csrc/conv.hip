@@ -447,6 +447,12 @@ static int launch_fwd(const float* x, const Geo& g, const float* w, float* y, in
     }
 }
 
+int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st) {
+    hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, splits, n, out,
+                       accumulate);
+    return VT_OK;
+}
+
 int bn_stats_finalize_launch(const float* stats, int tiles_per_sample, int B, int TP, int Lo, int C, float eps,
                              float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
                              hipStream_t st) {

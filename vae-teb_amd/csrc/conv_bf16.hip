@@ -186,6 +186,121 @@ __global__ void k_conv_shadow(const float* __restrict__ W, int Cout, int Cin, in
     }
 }
 
+// ------------------------------------------------------------ weight grad
+// dW[co][ci][k] = sum_rows dY[row][co] xpad[row + k][ci] on bf16 MFMA: rows
+// are the MFMA reduction (32 per k-step).  dY rows and the input window are
+// staged row-major in bf16 (fp32 -> bf16 while staging; padding / upsample as
+// in the forward) and both operands are read with the gfx950 transposed read
+// ds_read_b64_tr_b16 (4 rows x 16 channels per 16-lane group, delivered
+// column-major), so the tap shift k is a plain row offset of the window.
+// Each wave owns PPW (16 co x 16 ci) tile pairs with K accumulators; rows
+// are split over workgroups (blockIdx.y), per-split partial slabs are summed
+// in fixed order by conv.hip's k_sum_splits.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+constexpr int DWR = 64;  // rows per staged chunk (2 MFMA k-steps)
+
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int row0, int col0, int stride) {
+    // lane 4q+p of each 16-lane group addresses row (row0 + q), columns col0 + 4p .. +3; two reads
+    // (rows +0..3 and +4..7 of the lane group's 8-row block)
+    const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const __bf16* a0 = img + (row0 + 8 * g + q) * stride + col0 + 4 * p;
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4i16*)(a0 + 4 * stride));
+    // whole-vector concatenation + bit_cast: element-wise bit_casts of the v4i16 results are
+    // miscompiled (each lane's element 0 replicated by v_perm_b32)
+    typedef short v8i16 __attribute__((ext_vector_type(8)));
+    const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int K, int PPW>
+__global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ dy, const float* __restrict__ x, Geo g,
+                                                      int64_t rows_per_split, int NTc, int npairs, int dstride,
+                                                      int xstride, float* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
+    __bf16* ds = lb;                          // [DWR][dstride]   dY rows
+    __bf16* xs = lb + DWR * dstride;          // [DWR + K - 1 (+pad)][xstride] input window
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
+    int mt[PPW], nt[PPW];
+    bool act[PPW];
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+        const int p = blockIdx.x * (4 * PPW) + wv + 4 * j;
+        act[j] = p < npairs;
+        mt[j] = act[j] ? p / NTc : 0;
+        nt[j] = act[j] ? p - mt[j] * NTc : 0;
+    }
+    const int64_t rows = (int64_t)g.B * g.L_out;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
+    const int64_t r1 = r0 + rows_per_split < rows ? r0 + rows_per_split : rows;
+    f32x4 acc[PPW][K];
+#pragma unroll
+    for (int j = 0; j < PPW; ++j)
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int cout16 = (g.Cout + 15) / 16 * 16, cin16 = (g.Cin + 15) / 16 * 16;
+    for (int64_t r = r0; r < r1;) {
+        const int b = (int)(r / g.L_out);
+        const int t0 = (int)(r - (int64_t)b * g.L_out);
+        int n = g.L_out - t0;
+        if (n > DWR) n = DWR;
+        if (r + n > r1) n = (int)(r1 - r);
+        const float* xb = x + (int64_t)b * g.L_in * g.Cin;
+        const float* dyb = dy + ((int64_t)b * g.L_out + t0) * g.Cout;
+        // dY rows (zero rows past n, zero channels past Cout), 4 channels per thread-item
+        for (int i = tid; i < DWR * (cout16 / 4); i += 256) {
+            const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (t < n && c + j < g.Cout) ? dyb[(int64_t)t * g.Cout + c + j] : 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ds[t * dstride + c + j] = (__bf16)v[j];
+        }
+        // input window rows t0 .. t0 + DWR + K - 2 (padding / upsample applied), zero past n + K - 1
+        for (int i = tid; i < (DWR + K - 1) * (cin16 / 4); i += 256) {
+            const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (t < n + K - 1 && c + j < g.Cin) ? src_val(xb, g, t0 + t, c + j) : 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) xs[t * xstride + c + j] = (__bf16)v[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < DWR / 32; ++s) {
+#pragma unroll
+            for (int j = 0; j < PPW; ++j) {
+                // no early-out on inactive pairs: the transposed read needs all 64 lanes (EXEC all ones)
+                const bf16x8 a = tr_frag(ds, 32 * s, 16 * mt[j], dstride);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const bf16x8 bb = tr_frag(xs, 32 * s + k, 16 * nt[j], xstride);
+                    acc[j][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[j][k], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+        r += n;
+    }
+    // D: col (ci) = lane & 15, row (co) = 4 * (lane >> 4) + rr
+    const int64_t slot = blockIdx.y;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+        if (!act[j]) continue;
+        const int ci = 16 * nt[j] + lr;
+        if (ci >= g.Cin) continue;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int co = 16 * mt[j] + 4 * lc + rr;
+            if (co >= g.Cout) continue;
+            float* pp = part + ((slot * g.Cout + co) * g.Cin + ci) * K;
+#pragma unroll
+            for (int k = 0; k < K; ++k) pp[k] = acc[j][k][rr];
+        }
+    }
+}
+
 template <int K, int NT>
 int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
           hipStream_t st) {
@@ -281,6 +396,42 @@ int vt_conv1d_bwd_gpad_bf16(const float* dY, int B, int L_in, int Cin, const voi
     Geo g = geo(B, f.L_out, Cout, Cin, K, 0, 0);  // input dY (L_out x Cout), causal pad K-1
     bf_launch(dY, g, (const __bf16*)w16t, cdiv(Cout, 32) * 32, gpad, f.L_out + K - 1, nullptr, S(stream));
     VT_LAUNCH_CHECK("vt_conv1d_bwd_gpad_bf16");
+    return VT_OK;
+}
+
+int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode,
+                              int up, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(B > 0 && L_in > 0 && K > 0 && K <= KMAXB && Cin > 0 && Cout > 0 && Cin <= 128 && Cout <= 128,
+                 "vt_conv1d_bwd_weight_bf16: shape (K <= %d, channels <= 128)", KMAXB);
+    Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
+    const int NTc = cdiv(Cin, 16), npairs = cdiv(Cout, 16) * NTc;
+    const int ppw = K <= 3 ? 6 : (K <= 5 ? 4 : (K <= 7 ? 3 : 2));
+    const int bx = cdiv(npairs, 4 * ppw);
+    const int64_t rows = (int64_t)B * g.L_out;
+    const int64_t nout = (int64_t)Cout * Cin * K;
+    int64_t splits = 1024 / bx;
+    if (splits * nout > (int64_t)8 << 20) splits = ((int64_t)8 << 20) / nout;
+    if (splits > rows / (4 * DWR)) splits = rows / (4 * DWR);
+    if (splits < 1) splits = 1;
+    if (splits * nout > ws_floats) splits = ws_floats / nout;
+    VT_CHECK_ARG(splits >= 1, "vt_conv1d_bwd_weight_bf16: workspace too small");
+    int64_t rps = (rows + splits - 1) / splits;
+    splits = (rows + rps - 1) / rps;
+    // row strides (bf16): channels rounded to 16, + 8 (rows start 16 B apart mod 64 banks)
+    const int dstride = 16 * cdiv(Cout, 16) + 8, xstride = 16 * cdiv(Cin, 16) + 8;
+    const size_t lds = (size_t)(DWR * dstride + (DWR + KMAXB + 8) * xstride) * 2;
+    dim3 grid(bx, (unsigned)splits);
+    hipStream_t st = S(stream);
+#define VT_DWB(KK, PP)                                                                                         \
+    if (K == KK && ppw == PP)                                                                                  \
+        hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP>), grid, dim3(256), lds, st, dY, X, g, rps, NTc, npairs, dstride, \
+                           xstride, ws);
+    VT_DWB(1, 6) VT_DWB(2, 6) VT_DWB(3, 6) VT_DWB(4, 4) VT_DWB(5, 4) VT_DWB(6, 3) VT_DWB(7, 3)
+    VT_DWB(8, 2) VT_DWB(9, 2) VT_DWB(10, 2) VT_DWB(11, 2)
+#undef VT_DWB
+    const int rc = sum_splits_launch(ws, (int)splits, nout, dW, accumulate, st);
+    if (rc) return rc;
+    VT_LAUNCH_CHECK("vt_conv1d_bwd_weight_bf16");
     return VT_OK;
 }
 

@@ -444,8 +444,9 @@ class ConvBNActF(torch.autograd.Function):
         pw = _ParamGrads([w], [ctx.needs_input_grad[1]])
         if pw.out[0] is not None:
             ws1 = WS.get(WS_LINEAR, x.device, 1)
-            call("vt_conv1d_direct_bwd_weight", ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]),
-                 pw.acc, ptr(ws1), ws1.numel(), _st())
+            fn = "vt_conv1d_bwd_weight_bf16" if bf16 else "vt_conv1d_direct_bwd_weight"
+            call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1), ws1.numel(),
+                 _st())
         gw, = pw.result()
         gg, gb = pbn.result()
         return gx, gw, gg, gb, None, None, None, None, None, None, None, None
