@@ -91,6 +91,12 @@ int vt_normalize_raw(const float* x, int64_t rows, int64_t row_stride, int N, fl
  * backend/torch_backend.py:17-174 and ref/kymatio/kymatio/backend/torch_backend.py:99-219) */
 int vt_fft(const void* in, void* out, int64_t rows, int n, int inverse, const void* tw, int tw_stride,
            void* stream);                                                   /* fft / ifft (1/n)   */
+/* n > VT_FFT_MAX_LDS (pow2, <= 2^21): four-step FFT through HBM, n = 256 x n/256 (column
+ * pass with twiddles, then row pass); ws: rows * n complex64, distinct from in / out;
+ * tw = W_n^k, k < n.  Same contract as vt_fft otherwise (torch.fft / pocketfft in the
+ * reference's torch backend, torch_backend.py:106-121).                                  */
+int vt_fft_large(const void* in, void* out, void* ws, int64_t rows, int n, int inverse, const void* tw,
+                 void* stream);
 int vt_cdgmm(const void* A, const void* B, int b_is_real, void* C, int64_t rows, int n, void* stream);
 int vt_modulus(const void* in, float* out, int64_t count, void* stream);
 int vt_modulus_bwd(const void* in, const float* mod, const float* grad, void* grad_in, int64_t count, void* stream);

@@ -81,6 +81,21 @@ def test_fft_family_and_modulus_grad(bk):
     assert torch.allclose(z.grad, exp, atol=1e-6)
 
 
+@pytest.mark.parametrize("n,rows", [(16384, 3), (32768, 2), (1 << 17, 1)])
+def test_fft_four_step_long(bk, n, rows):
+    """n > 8192 (config 5: n_pad = 32768) runs the four-step vt_fft_large
+    (256-point column FFTs + twiddles, then n/256-point row FFTs): rel-L2 vs
+    numpy fp64 <= 3e-6 (fp32, two passes of log2 n radix-4 stages)."""
+    torch.manual_seed(n)
+    x = torch.randn(rows, n, 2, device="cuda")
+    xc = x[..., 0].double().cpu().numpy() + 1j * x[..., 1].double().cpu().numpy()
+    f = bk.fft(x)
+    assert rel(f[..., 0].cpu() + 1j * f[..., 1].cpu(), np.fft.fft(xc)) < 3e-6
+    i = bk.ifft(x)
+    assert rel(i[..., 0].cpu() + 1j * i[..., 1].cpu(), np.fft.ifft(xc)) < 3e-6
+    assert rel(bk.ifft(f).cpu(), x.cpu()) < 3e-6
+
+
 def test_cdgmm_real_and_complex(bk):
     A = torch.randn(2, 3, 16, 2, device="cuda")
     Br = torch.randn(16, 1, device="cuda")
@@ -110,7 +125,7 @@ def test_kymatio_known_answer_generic_path(golden):
 
 
 @pytest.mark.parametrize("name,fused", [("j11q4t16_n4096_o1", True), ("j6q1t16_n4096_o1", True),
-                                        ("j6q1t16_n4096_o2", False)])
+                                        ("j6q1t16_n4096_o2", False), ("j8q12t256_n16384_o2", False)])
 def test_scattering1d_vs_reference_golden(golden, name, fused):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

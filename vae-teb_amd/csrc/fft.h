@@ -63,4 +63,55 @@ __device__ float2* fft_lds(float2* x, float2* y, int n, const float2* __restrict
     return x;
 }
 
+// Batched variant: nb independent length-n sequences at x + c * pitch
+// (c < nb), for the four-step FFT's column / row passes (an odd pitch in
+// float2 keeps the column-major staging reads and writes conflict-free).
+template <bool INV>
+__device__ float2* fft_lds_batch(float2* x, float2* y, int n, int nb, int pitch, const float2* __restrict__ tw,
+                                 int tw_stride) {
+    int s = 1, log2s = 0, len = n;
+    const int quarter = n >> 2, lq = __builtin_ctz(quarter > 0 ? quarter : 1);
+    while (len >= 4) {
+        const int n1 = len >> 2;
+        for (int it = threadIdx.x; it < nb * quarter; it += blockDim.x) {
+            const int c = it >> lq, idx = it & (quarter - 1);
+            const float2* xc = x + c * pitch;
+            float2* yc = y + c * pitch;
+            const int q = idx & (s - 1);
+            const int p = idx >> log2s;
+            const int base = q + s * p;
+            const float2 a = xc[base], b = xc[base + s * n1], cc = xc[base + 2 * s * n1], d = xc[base + 3 * s * n1];
+            const int k = p * s * tw_stride;
+            const float2 w1 = twiddle<INV>(tw, k), w2 = twiddle<INV>(tw, 2 * k), w3 = twiddle<INV>(tw, 3 * k);
+            const float2 apc = cadd(a, cc), amc = csub(a, cc), bpd = cadd(b, d), bmd = csub(b, d);
+            const float2 jbmd = make_float2(-bmd.y, bmd.x);
+            const int o = q + 4 * s * p;
+            yc[o] = cadd(apc, bpd);
+            yc[o + 2 * s] = cmul(w2, csub(apc, bpd));
+            if (!INV) {
+                yc[o + s] = cmul(w1, csub(amc, jbmd));
+                yc[o + 3 * s] = cmul(w3, cadd(amc, jbmd));
+            } else {
+                yc[o + s] = cmul(w1, cadd(amc, jbmd));
+                yc[o + 3 * s] = cmul(w3, csub(amc, jbmd));
+            }
+        }
+        __syncthreads();
+        float2* t = x; x = y; y = t;
+        s <<= 2; log2s += 2; len >>= 2;
+    }
+    if (len == 2) {
+        const int h = n >> 1, lh = __builtin_ctz(h);
+        for (int it = threadIdx.x; it < nb * h; it += blockDim.x) {
+            const int c = it >> lh, q = it & (h - 1);
+            const float2 a = x[c * pitch + q], b = x[c * pitch + q + h];
+            y[c * pitch + q] = cadd(a, b);
+            y[c * pitch + q + h] = csub(a, b);
+        }
+        __syncthreads();
+        float2* t = x; x = y; y = t;
+    }
+    return x;
+}
+
 }  // namespace vt

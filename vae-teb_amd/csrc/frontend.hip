@@ -516,6 +516,69 @@ __global__ __launch_bounds__(FE_THREADS) void k_fft_rows(const float2* __restric
     for (int i = threadIdx.x; i < n; i += blockDim.x) out[r * n + i] = cscale(R[i], sc);
 }
 
+// Four-step FFT for n > VT_FFT_MAX_LDS (config 5: Scattering1D J=8 Q=12 on
+// N = 16384 -> n_pad = 32768), n = n1 * n2 with n1 = 256 "rows" of n2 columns:
+//   pass 1 (k_fft4_cols): 16 adjacent columns j2 per workgroup (128-byte row
+//     segments from HBM), length-n1 FFTs over j1 in LDS, twiddle W_n^(j2 k1),
+//     write A[k1][j2] (128-byte segments);
+//   pass 2 (k_fft4_rows): RB rows k1 per workgroup, length-n2 FFTs over j2,
+//     write X[k1 + n1 k2] (RB adjacent k1 per k2 -> RB * 8-byte segments), 1/n
+//     for the inverse.
+// LDS images are column-major with an odd float2 pitch: the staging writes /
+// reads (one element per column across lanes) hit distinct banks and the
+// butterflies stay unit-stride within a column.  tw: W_n^k, k < n.
+constexpr int F4_N1 = 256, F4_COLS = 16;
+
+__global__ __launch_bounds__(FE_THREADS) void k_fft4_cols(const float2* __restrict__ in, float2* __restrict__ ws,
+                                                          int n, int n2, const float2* __restrict__ tw, int inverse) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    constexpr int P = F4_N1 + 1;
+    float2* X = sm;
+    float2* Y = sm + F4_COLS * P;
+    const int64_t r = blockIdx.y;
+    const int c0 = blockIdx.x * F4_COLS;
+    const float2* src = in + r * n + c0;
+    for (int i = threadIdx.x; i < F4_N1 * F4_COLS; i += blockDim.x) {
+        const int j1 = i / F4_COLS, c = i % F4_COLS;
+        X[c * P + j1] = src[(int64_t)j1 * n2 + c];
+    }
+    __syncthreads();
+    float2* R = inverse ? fft_lds_batch<true>(X, Y, F4_N1, F4_COLS, P, tw, n2)
+                        : fft_lds_batch<false>(X, Y, F4_N1, F4_COLS, P, tw, n2);
+    float2* dst = ws + r * n + c0;
+    for (int i = threadIdx.x; i < F4_N1 * F4_COLS; i += blockDim.x) {
+        const int k1 = i / F4_COLS, c = i % F4_COLS;
+        const int e = (int)(((int64_t)(c0 + c) * k1) & (n - 1));
+        const float2 w = inverse ? twiddle<true>(tw, e) : twiddle<false>(tw, e);
+        dst[(int64_t)k1 * n2 + c] = cmul(R[c * P + k1], w);
+    }
+}
+
+__global__ __launch_bounds__(FE_THREADS) void k_fft4_rows(const float2* __restrict__ ws, float2* __restrict__ out,
+                                                          int n, int n2, int rb, const float2* __restrict__ tw,
+                                                          int inverse) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int P = n2 + 1;
+    float2* X = sm;
+    float2* Y = sm + rb * P;
+    const int64_t r = blockIdx.y;
+    const int k10 = blockIdx.x * rb;
+    const float2* src = ws + r * n + (int64_t)k10 * n2;
+    for (int i = threadIdx.x; i < rb * n2; i += blockDim.x) {
+        const int rr = i / n2, j2 = i - rr * n2;
+        X[rr * P + j2] = src[i];
+    }
+    __syncthreads();
+    float2* R = inverse ? fft_lds_batch<true>(X, Y, n2, rb, P, tw, F4_N1)
+                        : fft_lds_batch<false>(X, Y, n2, rb, P, tw, F4_N1);
+    const float sc = inverse ? 1.0f / (float)n : 1.0f;
+    float2* dst = out + r * n + k10;
+    for (int i = threadIdx.x; i < rb * n2; i += blockDim.x) {
+        const int k2 = i / rb, rr = i - k2 * rb;
+        dst[(int64_t)k2 * F4_N1 + rr] = cscale(R[rr * P + k2], sc);
+    }
+}
+
 __global__ void k_cdgmm(const float2* __restrict__ A, const float* __restrict__ Bf, int b_real,
                         float2* __restrict__ C, int64_t total, int n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -663,6 +726,25 @@ int vt_fft(const void* in, void* out, int64_t rows, int n, int inverse, const vo
     hipLaunchKernelGGL(k_fft_rows, dim3((unsigned)rows), dim3(FE_THREADS), fft_lds_bytes(n), S(stream),
                        (const float2*)in, (float2*)out, n, (const float2*)tw, tw_stride, inverse);
     VT_LAUNCH_CHECK("vt_fft");
+    return VT_OK;
+}
+
+int vt_fft_large(const void* in, void* out, void* ws, int64_t rows, int n, int inverse, const void* tw,
+                 void* stream) {
+    VT_CHECK_ARG(pow2(n) && n > VT_FFT_MAX_LDS && n <= (1 << 21) && rows > 0 && rows <= 65535,
+                 "vt_fft_large: n=%d rows=%lld (pow2, %d < n <= 2^21)", n, (long long)rows, VT_FFT_MAX_LDS);
+    VT_CHECK_ARG(ws != in && ws != out, "vt_fft_large: workspace aliases in/out");
+    const int n2 = n / F4_N1;
+    int rb = 8192 / n2;
+    if (rb > 16) rb = 16;
+    hipStream_t st = S(stream);
+    hipLaunchKernelGGL(k_fft4_cols, dim3(n2 / F4_COLS, (unsigned)rows), dim3(FE_THREADS),
+                       (size_t)2 * F4_COLS * (F4_N1 + 1) * sizeof(float2), st, (const float2*)in, (float2*)ws, n, n2,
+                       (const float2*)tw, inverse);
+    hipLaunchKernelGGL(k_fft4_rows, dim3(F4_N1 / rb, (unsigned)rows), dim3(FE_THREADS),
+                       (size_t)2 * rb * (n2 + 1) * sizeof(float2), st, (const float2*)ws, (float2*)out, n, n2, rb,
+                       (const float2*)tw, inverse);
+    VT_LAUNCH_CHECK("vt_fft_large");
     return VT_OK;
 }
 

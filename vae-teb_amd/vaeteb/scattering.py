@@ -165,11 +165,17 @@ class TorchHipBackend1D:
     def _fft(cls, x, inverse):
         cls._device_check(x)
         n = x.shape[-2]
-        if n > _lib_max_fft():
-            raise ValueError(f"torch_hip backend: FFT length {n} exceeds the LDS-resident limit {_lib_max_fft()}")
+        if n > _MAX_FFT:
+            raise ValueError(f"torch_hip backend: FFT length {n} exceeds {_MAX_FFT}")
         out = torch.empty_like(x)
-        _lib.call("vt_fft", _lib.ptr(x), _lib.ptr(out), x.numel() // (2 * n), n, int(inverse), _lib.ptr(_tw(n, x.device)),
-                  1, _lib.stream())
+        rows = x.numel() // (2 * n)
+        if n <= _lib_max_fft():
+            _lib.call("vt_fft", _lib.ptr(x), _lib.ptr(out), rows, n, int(inverse), _lib.ptr(_tw(n, x.device)), 1,
+                      _lib.stream())
+        else:   # four-step through HBM (config 5: n_pad = 32768)
+            ws = torch.empty_like(x)
+            _lib.call("vt_fft_large", _lib.ptr(x), _lib.ptr(out), _lib.ptr(ws), rows, n, int(inverse),
+                      _lib.ptr(_tw(n, x.device)), _lib.stream())
         return out
 
     @classmethod
@@ -215,7 +221,10 @@ class TorchHipBackend1D:
 
 
 def _lib_max_fft():
-    return 8192
+    return 8192     # VT_FFT_MAX_LDS: one workgroup's LDS; longer -> vt_fft_large
+
+
+_MAX_FFT = 1 << 21
 
 
 backend = TorchHipBackend1D
