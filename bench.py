@@ -132,8 +132,72 @@ def cpu_baseline(frontend_cfg, batch=8, threads=None):
                       f"SeqVaeTeb(S=256) fwd/bwd/clip/AdamW, torch threads={threads}, {dt:.1f} s"}
 
 
+def run_c5(args, rank, world, dev):
+    """Config 5 (BASELINE.json configs[4]): long-sequence stress, front-end only —
+    Scattering1D(J=8, Q=12, T=256, order 2) on 16384-point windows, batch 64 per
+    GPU; samples are independent, so N GPUs run N replicas on disjoint samples
+    with no collective (weak scaling).  A step = one batch x (B, 16384) resident
+    in HBM -> S (B, 337, 64) through the level-grouped HIP cascade."""
+    from vaeteb.scattering import Scattering1D
+    B, N = args.batch if args.batch != 256 else 64, 16384
+    sc = Scattering1D(J=8, shape=N, Q=12, max_order=2, T=256)
+    pool = [torch.from_numpy(synthetic.batch((rank * 2 + i) * B, B, N)[:, 0].copy()).to(dev) for i in range(2)]
+    # dominant kernel: vt_scat_mod_spec (fold + ifft -> |.| -> fft per (sample, filter) row);
+    # algorithmic bytes = distinct source rows read once (B x a_rows x n c64) + spectra written (B x P x n/k c64)
+    work = {"vt_scat_mod_spec": lambda A, Bb, a_rows, n, a_idx, pool_, f_off, P, k, *a: 8 * Bb * (a_rows * n + P * n // k)}
+    timer = KernelTimer(list(work), flops=work)
+    for i in range(args.warmup):
+        sc(pool[i % 2])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.reset(True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        S, _ = sc(pool[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    k_ms, k_n = timer.mean_ms("vt_scat_mod_spec")
+    k_bytes = timer.total_flops["vt_scat_mod_spec"] / max(k_n, 1)
+    achieved = k_bytes / (k_ms * 1e-3) / 1e9
+    out = {"metric": "scattering samples/sec, Scattering1D(J=8, Q=12) 16384-pt windows, batch 64/GPU",
+           "value": round(args.steps * B * world / dt, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (complex64)", "data": "synthetic",
+           "config": {"workload": "c5: Scattering1D J=8 Q=12 T=256 order 2, N=16384 (n_pad 32768) -> (B, 337, 64), "
+                                  f"batch {B}/GPU, replicas (no collective)", "global_batch": B * world,
+                      "seq_len": N, "parallelism": f"replicas{world}"},
+           "roofline": {"bound": "hbm", "kernel": "vt_scat_mod_spec (k_scat_mod_spec)", "achieved": round(achieved, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": None, "avg_launch_ms": round(k_ms, 4), "launches": k_n,
+                        "algorithmic_bytes": round(k_bytes)},
+           "checksum": float(S.double().abs().sum().item())}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle import frontend_ref as F
+        xs = pool[0].cpu().numpy()   # the whole batch (~15 s single-threaded numpy)
+        t0 = time.perf_counter()
+        F.scattering1d(xs, 8, 12, 256, max_order=2)
+        dtc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(xs) / dtc, 4), "unit": "samples/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle numpy Scattering1D order 2 on {len(xs)} of the same windows, {dtc:.1f} s"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["c2", "c5"], default="c2",
+                    help="c2: the training step (BASELINE.json metric, default); c5: long-sequence scattering front-end")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -155,6 +219,8 @@ def main():
     rank, world, local, dev = init_distributed()
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     torch.cuda.set_device(dev)
+    if args.workload == "c5":
+        return run_c5(args, rank, world, dev)
     J, Q, T = FRONTENDS[args.frontend]
     N, B = 4096, args.batch
     plan = FrontEndPlan(J, Q, T, N, device=dev)

@@ -98,6 +98,23 @@ int vt_fft(const void* in, void* out, int64_t rows, int n, int inverse, const vo
 int vt_fft_large(const void* in, void* out, void* ws, int64_t rows, int n, int inverse, const void* tw,
                  void* stream);
 int vt_cdgmm(const void* A, const void* B, int b_is_real, void* C, int64_t rows, int n, void* stream);
+/* Batched Scattering1D cascade (scatter.hip; the per-filter loop of
+ * ref/kymatio/kymatio/scattering1d/core/scattering1d.py:197-399 regrouped by level):
+ * filter_sub: out[b,p,m] = mean_c A[b, a_idx[p], m + c n/k] * pool[f_off[p] + m + c n/k]
+ *             (cdgmm + subsample_fourier; A (B, a_rows, n) c64, out (B, P, n/k) c64);
+ * mod_spec:   filter_sub fused with ifft -> modulus -> rfft of each row (n/k <= VT_FFT_MAX_LDS,
+ *             tw = W_{n/k}^j table);
+ * lowpass:    out[b, ch[p], t] = real(ifft(subsample(U[b,p] . phi, k)))[i0 + t], t < i1 - i0
+ *             (cdgmm + subsample_fourier + irfft + unpad into the (B, out_C, i1-i0) output);
+ *             tw = W_{n/k}^j table;
+ * modulus_cplx: out = (|in|, 0) complex (modulus + rfft's zero imaginary part).            */
+int vt_scat_filter_sub(const void* A, int B, int64_t a_rows, int n, const int* a_idx, const float* pool,
+                       const int64_t* f_off, int P, int k, void* out, void* stream);
+int vt_scat_mod_spec(const void* A, int B, int64_t a_rows, int n, const int* a_idx, const float* pool,
+                     const int64_t* f_off, int P, int k, const void* tw, void* out, void* stream);
+int vt_scat_lowpass(const void* U, int B, int P, int n, const float* phi, int k, int i0, int i1, const int* ch,
+                    int out_C, const void* tw, float* out, void* stream);
+int vt_modulus_cplx(const void* in, void* out, int64_t count, void* stream);
 int vt_modulus(const void* in, float* out, int64_t count, void* stream);
 int vt_modulus_bwd(const void* in, const float* mod, const float* grad, void* grad_in, int64_t count, void* stream);
 int vt_subsample_fourier(const void* in, void* out, int64_t rows, int n, int k, void* stream);

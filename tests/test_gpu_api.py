@@ -119,9 +119,11 @@ def test_kymatio_known_answer_generic_path(golden):
     d = golden("kymatio_test_data_1d")
     x = torch.from_numpy(d["x"]).cuda()
     sc = Scattering1D(int(d["J"]), x.shape[-1], int(d["Q"]))
-    S, _ = sc(x)
-    assert S.shape == d["Sx"].shape
-    assert np.allclose(S.cpu().numpy(), d["Sx"], rtol=1e-4, atol=1e-6)   # fp32 FFT engine differs from torch's
+    for cascade in (True, False):
+        sc.cascade = cascade
+        S, _ = sc(x)
+        assert S.shape == d["Sx"].shape
+        assert np.allclose(S.cpu().numpy(), d["Sx"], rtol=1e-4, atol=1e-6)   # fp32 FFT engine differs from torch's
 
 
 @pytest.mark.parametrize("name,fused", [("j11q4t16_n4096_o1", True), ("j6q1t16_n4096_o1", True),
@@ -135,12 +137,15 @@ def test_scattering1d_vs_reference_golden(golden, name, fused):
     J, Q, T, N, o = map(int, re.findall(r"\d+", name))
     sc = Scattering1D(J=J, shape=N, Q=Q, max_order=o, T=T)
     assert sc._fused_ok() == fused
-    S, S2 = sc(torch.from_numpy(g["x"]).cuda())
-    assert S is S2 and S.shape == g["S"].shape
-    got, exp64, ref32 = S.cpu().numpy(), g["S64"], g["S"]
-    e = np.sqrt(((got - exp64) ** 2).sum(-1) / (exp64 ** 2).sum(-1))
-    r = np.sqrt(((ref32 - exp64) ** 2).sum(-1) / (exp64 ** 2).sum(-1))
-    assert e.max() <= 2 * r.max() + 1e-6, (e.max(), r.max())
+    # non-fused configurations: the level-grouped cascade and the per-filter generic core
+    for cascade in ((True,) if fused else (True, False)):
+        sc.cascade = cascade
+        S, S2 = sc(torch.from_numpy(g["x"]).cuda())
+        assert S is S2 and S.shape == g["S"].shape
+        got, exp64, ref32 = S.cpu().numpy(), g["S64"], g["S"]
+        e = np.sqrt(((got - exp64) ** 2).sum(-1) / (exp64 ** 2).sum(-1))
+        r = np.sqrt(((ref32 - exp64) ** 2).sum(-1) / (exp64 ** 2).sum(-1))
+        assert e.max() <= 2 * r.max() + 1e-6, (cascade, e.max(), r.max())
 
 
 # ------------------------------------------------ KymatioPhaseScattering1D

@@ -16,4 +16,12 @@ for _ in range(n):
 t_enq = time.perf_counter() - t
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t) / n
-print(f"c5 generic: {dt*1e3:.2f} ms/batch (enqueue {t_enq/n*1e3:.2f}), {64/dt:.1f} samples/s, out {tuple(S.shape)}")
+print(f"c5 cascade: {dt*1e3:.2f} ms/batch (enqueue {t_enq/n*1e3:.2f}), {64/dt:.1f} samples/s, out {tuple(S.shape)}")
+sc.cascade = False
+S2, _ = sc(x)
+torch.cuda.synchronize()
+t = time.perf_counter()
+S2, _ = sc(x)
+torch.cuda.synchronize()
+print(f"c5 per-filter generic core: {(time.perf_counter() - t) * 1e3:.2f} ms/batch; max |cascade - generic| / max|S| = "
+      f"{((S - S2).abs().max() / S2.abs().max()).item():.2e}")

@@ -280,6 +280,123 @@ def scattering1d_core(x, bk, J, T, psi1, psi2, phi, pad_left, pad_right, ind_sta
     return out
 
 
+# ------------------------------------------------------------- batched cascade
+class _Cascade:
+    """The cascade of scattering1d_core (orders 1-2, average=True, array output)
+    regrouped by subsampling level: every (sample, filter) row of a level is one
+    launch of vt_scat_filter_sub (cdgmm + subsample), vt_scat_mod_spec (ifft ->
+    modulus -> rfft in LDS) and vt_scat_lowpass (phi, subsample, irfft, unpad ->
+    its output channel).  Same arithmetic and channel order as the reference
+    loop (ref/kymatio/kymatio/scattering1d/core/scattering1d.py:197-399); ~3
+    launches per level instead of ~6 per filter and per filter pair."""
+
+    def __init__(self, sc, device):
+        b, J, os_ = sc._bank, sc.J, sc.oversampling
+        n = 2 ** sc.J_pad
+        lt = int(math.floor(math.log2(sc.T)))
+        self.n, self.dev = n, device
+        pool, offs = [], {}
+
+        def off(key, arr):
+            if key not in offs:
+                offs[key] = sum(len(a) for a in pool)
+                pool.append(np.asarray(arr, np.float32).reshape(-1))
+            return offs[key]
+
+        i32 = lambda v: torch.tensor(v, dtype=torch.int32, device=device)
+        i64 = lambda v: torch.tensor(v, dtype=torch.int64, device=device)
+        ind0, ind1 = sc.ind_start, sc.ind_end
+        k0 = max(lt - os_, 0)
+        self.S = ind1[k0] - ind0[k0]
+        self.s0 = (off(("phi", 0), b.phi_levels[0]), 2 ** k0, ind0[k0], ind1[k0], i32([0]))
+        n_psi1 = len(b.xi1)
+        groups = {}
+        for n1 in range(n_psi1):
+            k1 = max(min(int(b.j1[n1]) - os_, lt - os_), 0)
+            groups.setdefault(k1, []).append(n1)
+        order2 = []   # channel numbering of the reference loop: S0, S1 (n1), then S2 (n1, n2) in loop order
+        if sc.max_order == 2:
+            for n1 in range(n_psi1):
+                for n2 in range(len(b.xi2)):
+                    if int(b.j2[n2]) > int(b.j1[n1]):
+                        order2.append((n1, n2))
+        ch2 = {pr: 1 + n_psi1 + i for i, pr in enumerate(order2)}
+        self.C = 1 + n_psi1 + len(order2)
+        self.levels = []
+        for k1, members in sorted(groups.items()):
+            L = n // 2 ** k1
+            k1J = max(lt - k1 - os_, 0)
+            lvl = {"L": L, "k": 2 ** k1, "P": len(members), "a_idx": i32([0] * len(members)),
+                   "f_off": i64([off(("psi1", m), b.psi1[m]) for m in members]),
+                   "s1": (off(("phi", k1), b.phi_levels[k1]), 2 ** k1J, ind0[k1J + k1], ind1[k1J + k1],
+                          i32([1 + m for m in members])), "sub": []}
+            pos = {m: i for i, m in enumerate(members)}
+            sub = {}
+            for (n1, n2) in order2:
+                if n1 not in pos:
+                    continue
+                k2 = max(min(int(b.j2[n2]) - k1 - os_, lt - k1 - os_), 0)
+                sub.setdefault(k2, []).append((n1, n2))
+            for k2, prs in sorted(sub.items()):
+                k2J = max(lt - k2 - k1 - os_, 0)
+                lvl["sub"].append({
+                    "L": L // 2 ** k2, "k": 2 ** k2, "P": len(prs), "a_idx": i32([pos[a] for a, _ in prs]),
+                    "f_off": i64([off(("psi2", c, k1), b.psi2_levels[c][k1]) for _, c in prs]),
+                    "s2": (off(("phi", k1 + k2), b.phi_levels[k1 + k2]), 2 ** k2J, ind0[k1 + k2 + k2J],
+                           ind1[k1 + k2 + k2J], i32([ch2[pr] for pr in prs]))})
+            self.levels.append(lvl)
+        self.pool = torch.from_numpy(np.concatenate(pool)).to(device)
+        self.pad = (sc.pad_left, sc.pad_right)
+
+    def _spectrum(self, A, B, a_rows, n_in, g):
+        """U^ = rfft(|ifft(subsample(A[a_idx] . psi, k))|) for every (b, p) row of
+        level g: one fused LDS launch when the row fits, else fold + four-step."""
+        L = g["L"]
+        out = torch.empty((B, g["P"], L, 2), device=self.dev)
+        tw = _lib.ptr(_tw(L, self.dev))
+        if L <= _lib_max_fft():
+            _lib.call("vt_scat_mod_spec", _lib.ptr(A), B, a_rows, n_in, _lib.ptr(g["a_idx"]), _lib.ptr(self.pool),
+                      _lib.ptr(g["f_off"]), g["P"], g["k"], tw, _lib.ptr(out), _lib.stream())
+            return out
+        Y = self._filter_sub(A, B, a_rows, n_in, g)
+        ws = torch.empty_like(Y)
+        rows = B * g["P"]
+        _lib.call("vt_fft_large", _lib.ptr(Y), _lib.ptr(out), _lib.ptr(ws), rows, L, 1, tw, _lib.stream())
+        _lib.call("vt_modulus_cplx", _lib.ptr(out), _lib.ptr(Y), rows * L, _lib.stream())
+        _lib.call("vt_fft_large", _lib.ptr(Y), _lib.ptr(out), _lib.ptr(ws), rows, L, 0, tw, _lib.stream())
+        return out
+
+    def _lowpass(self, U, B, P, L, spec, out):
+        foff, k, i0, i1, ch = spec
+        _lib.call("vt_scat_lowpass", _lib.ptr(U), B, P, L, self.pool.data_ptr() + 4 * foff, k, i0, i1, _lib.ptr(ch),
+                  self.C, _lib.ptr(_tw(L // k, self.dev)), _lib.ptr(out), _lib.stream())
+
+    def _filter_sub(self, A, B, a_rows, L_in, g):
+        Y = torch.empty((B, g["P"], g["L"], 2), device=self.dev)
+        _lib.call("vt_scat_filter_sub", _lib.ptr(A), B, a_rows, L_in, _lib.ptr(g["a_idx"]), _lib.ptr(self.pool),
+                  _lib.ptr(g["f_off"]), g["P"], g["k"], _lib.ptr(Y), _lib.stream())
+        return Y
+
+    def __call__(self, x2):
+        """x2 (B, N) float32 contiguous on device -> S (B, C, S_out)."""
+        B, N = x2.shape
+        n = self.n
+        xp = torch.empty((B, n), device=self.dev)
+        _lib.call("vt_pad_reflect", _lib.ptr(x2), _lib.ptr(xp), B, N, self.pad[0], self.pad[1], _lib.stream())
+        xc = torch.zeros((B, n, 2), device=self.dev)
+        xc[..., 0] = xp
+        U0h = TorchHipBackend1D._fft(xc, False)
+        out = torch.empty((B, self.C, self.S), device=self.dev)
+        self._lowpass(U0h, B, 1, n, self.s0, out)
+        for lvl in self.levels:
+            U1h = self._spectrum(U0h, B, 1, n, lvl)
+            self._lowpass(U1h, B, lvl["P"], lvl["L"], lvl["s1"], out)
+            for g in lvl["sub"]:
+                U2h = self._spectrum(U1h, B, lvl["P"], lvl["L"], g)
+                self._lowpass(U2h, B, g["P"], g["L"], g["s2"], out)
+        return out
+
+
 # ------------------------------------------------------------------ frontend
 class Scattering1D(nn.Module):
     """Drop-in for kymatio's (locally modified) ScatteringTorch1D: forward(x)
@@ -314,6 +431,8 @@ class Scattering1D(nn.Module):
         self._bank = bank
         self._tables = None
         self._fused = None
+        self._cascade = None
+        self.cascade = True     # False: per-filter generic core over the plugin (the reference's loop)
 
     def _device_tables(self, device):
         if self._tables is None or self._tables[0] != str(device):
@@ -330,6 +449,12 @@ class Scattering1D(nn.Module):
         return (self.max_order == 1 and self.average and self.oversampling == 0 and self.vectorize
                 and self.out_type == "array" and 2 ** self.J_pad <= 8192)
 
+    def _cascade_ok(self, x):
+        """Batched level-grouped cascade: average=True, array output, no autograd
+        (the generic core over the plugin keeps the reference's autograd)."""
+        return (self.cascade and self.average and self.out_type == "array" and self.vectorize and self.max_order in (1, 2)
+                and not (torch.is_grad_enabled() and x.requires_grad) and x.is_cuda)
+
     def meta(self):
         raise NotImplementedError("meta() is outside the training path")
 
@@ -345,6 +470,10 @@ class Scattering1D(nn.Module):
         x2 = x.reshape((-1, x.shape[-1])).contiguous()
         if self._fused_ok():
             S = self._fused_forward(x2)
+        elif self._cascade_ok(x2):
+            if self._cascade is None or self._cascade.dev != x2.device:
+                self._cascade = _Cascade(self, x2.device)
+            S = self._cascade(x2)
         else:
             phi, psi1, psi2 = self._device_tables(x.device)
             S = scattering1d_core(x2.reshape(-1, 1, x.shape[-1]), self.backend, self.J, self.T, psi1, psi2, phi,
