@@ -328,6 +328,67 @@ int vt_lstm_layer_fwd(const float* gin, const float* w_hh, const float* b_hh, in
 int vt_lstm_layer_bwd(const float* dh_out, const float* gates, const float* cst, const float* w_hh, int B, int S,
                       int hidden, float* dgates, void* stream);
 
+/* ---------------------------------------------------------- classifier (c4)
+ * FHRInceptionTimeClassifier (ref/model/inception_time.py:185-333) on
+ * (B, L, C) activations; every X / Y below is a row-major (B*L, ld) matrix
+ * whose first / [col, col+C) columns are the operand (concatenations are
+ * column slices of one buffer, no copies).                                     */
+/* Zero-padded Conv1d(bias=False), output length L:
+ *   Y[b,t,o] (+)= sum_{i,k} W[o][i][k] X[b, t+k-pad_left, i]
+ * Cin, Cout multiples of 16, Cout <= 128, K in {1, 5, 15, 40}.  conv_long
+ * (K 40, padding 20) yields L+1 positions in the reference, which then fails to
+ * concatenate; the first L are kept (the documented crop).
+ * replaces: FHRInception bottleneck1/conv_short/conv_medium/conv_long/bottleneck2,
+ *           FHRResidual.bottleneck (ref/model/inception_time.py:21-71, :131-138) */
+int vt_zconv_fwd(const float* X, int ldx, int B, int L, int Cin, const float* W, int Cout, int K, int pad_left,
+                 float* Y, int ldy, int accumulate, void* stream);
+/* dX (+)= conv of dY with the transposed, flipped taps (pad K-1-pad_left)      */
+int vt_zconv_bwd_data(const float* dY, int ldy, int B, int L, int Cin, const float* W, int Cout, int K, int pad_left,
+                      float* dX, int ldx, int accumulate, void* stream);
+/* dW (+)= sum_{b,t} dY[b,t,o] X[b,t+k-pad_left,i]: per-workgroup slabs summed in
+ * fixed order; ws >= vt_zconv_bwd_weight_ws_floats(...) floats.                */
+int vt_zconv_bwd_weight_ws_floats(int B, int Cin, int Cout, int K, int64_t* floats);
+int vt_zconv_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int B, int L, int Cin, int Cout, int K,
+                        int pad_left, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);
+/* MaxPool1d(kernel 3, stride 1, padding 1) over t (first maximum wins, as
+ * torch's CPU kernel), and its backward (dX (+)= routed dY).
+ * replaces: FHRInception.max_pool (ref/model/inception_time.py:60-64)           */
+int vt_maxpool3_fwd(const float* X, int B, int L, int C, float* Y, void* stream);
+int vt_maxpool3_bwd(const float* dY, const float* X, int B, int L, int C, float* dX, int accumulate, void* stream);
+/* Y = act(A + Bm) elementwise (act as vt_act_fwd; backward: vt_act_bwd on Y).
+ * replaces: y + residual -> relu (ref/model/inception_time.py:165-167),
+ *           y_seq + attn_out (:310)                                            */
+int vt_add_act_fwd(const float* A, const float* Bm, int64_t n, int act, float* Y, void* stream);
+/* Dropout with a stateless counter hash: keep element i iff hash(seed, m(i)) >=
+ * p * 2^32, kept values scaled by 1/(1-p); m(i) = i (nn.Dropout) or, with
+ * L > 0 on (B, L, C) data, the (sample, channel) pair (nn.Dropout1d drops whole
+ * channels).  The same call with the same seed is the backward (in place ok).
+ * replaces: nn.Dropout / nn.Dropout1d in ref/model/inception_time.py:78,139,209,247,251 */
+int vt_dropout_apply(const float* X, int64_t n, int C, int L, float p, int64_t seed, float* Y, void* stream);
+/* Mean over t of (B, L, C) -> (B, C); backward dX (+)= dY / L broadcast.
+ * replaces: AdaptiveAvgPool1d(1) + squeeze (ref/model/inception_time.py:243,320-321) */
+int vt_time_mean_fwd(const float* X, int B, int L, int C, float* Y, void* stream);
+int vt_time_mean_bwd(const float* dY, int B, int L, int C, float* dX, int accumulate, void* stream);
+/* Multi-head self-attention core on packed in-projections qkv (B*S, 3E),
+ * E = H*32 (head dim 32), S a multiple of 16, S <= 256:
+ *   O_h = dropout(softmax(Q_h K_h^T * scale)) V_h   -> out (B*S, E);  lse (B, H, S)
+ * Backward writes dqkv (B*S, 3E) completely.  Attention-weight dropout uses the
+ * vt_dropout_apply hash over (b, h, query, key).
+ * replaces: nn.MultiheadAttention(128, 4, dropout, batch_first=True) core
+ *           (ref/model/inception_time.py:236-242, :306-309)                     */
+int vt_attn_fwd(const float* qkv, int B, int S, int H, float scale, float p, int64_t seed, float* out, float* lse,
+                void* stream);
+int vt_attn_bwd(const float* qkv, const float* out, const float* dout, const float* lse, int B, int S, int H,
+                float scale, float p, int64_t seed, float* dqkv, void* stream);
+/* nn.CrossEntropyLoss (mean) over logits (B, C), int64 labels: loss[0] and the
+ * softmax probabilities; backward dlogits = g[0] * (probs - onehot) / B with
+ * g a device scalar (the upstream gradient).
+ * replaces: SeqVaeTebClassifier.classification_criterion (ref/model/vae_teb_model.py:1332,1488) */
+int vt_cross_entropy_fwd(const float* logits, const int64_t* labels, int B, int C, float* loss, float* probs,
+                         void* stream);
+int vt_cross_entropy_bwd(const float* probs, const int64_t* labels, int B, int C, const float* g, float* dlogits,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

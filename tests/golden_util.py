@@ -16,6 +16,8 @@ Rule per key (state_dict order is irrelevant, every key has its own stream):
     sqrt(6/(fan_in+fan_out)) (ref/model/vae_teb_model.py:55-59)
   * 1-D ``weight`` (LayerNorm/BatchNorm gamma) -> 1 + U(-0.1, 0.1)
   * 1-D ``bias`` -> U(-0.05, 0.05)
+  * MultiheadAttention ``in_proj_weight`` -> Xavier-uniform over (3E, E),
+    ``in_proj_bias`` -> U(-0.05, 0.05)
 """
 import zlib
 
@@ -48,6 +50,11 @@ def det_value(key, shape, lstm_hidden=None):
             h = shape[0] // 4
             v[h:2 * h] += 1.0
         return v
+    if base == "in_proj_weight":          # nn.MultiheadAttention packed q|k|v projection
+        b = np.sqrt(6.0 / (shape[0] + shape[1]))
+        return rng.uniform(-b, b, size=shape)
+    if base == "in_proj_bias":
+        return rng.uniform(-0.05, 0.05, size=shape)
     if base == "weight" and len(shape) >= 2:
         fi, fo = _fans(shape)
         b = np.sqrt(6.0 / (fi + fo))

@@ -129,3 +129,49 @@ def test_tiny_c1(golden):
     assert abs(r["total"].item() - float(g["total"])) < 1e-5
     for i, (k, p) in enumerate(m.named_parameters()):
         assert np.allclose(p.grad.numpy(), g[f"grad_{i}"], rtol=1e-5, atol=1e-6), k
+
+
+def test_classifier(golden):
+    """Config 4 head: the oracle vs the reference FHRInceptionTimeClassifier
+    (conv_long cropped to L) — logits, CE, dz, every gradient, BN stats."""
+    from oracle import classifier_ref as C
+    g = golden("classifier_s64_b4")
+    m = det_fill_(C.InceptionTimeClassifier(dropout=0.0))
+    names = [k for k, _ in m.named_parameters()]
+    assert names == list(g["param_names"])
+    m.train()
+    z = torch.from_numpy(g["z"]).requires_grad_(True)
+    logits = m(z)
+    loss = torch.nn.functional.cross_entropy(logits, torch.from_numpy(g["labels"]))
+    loss.backward()
+    assert np.allclose(logits.detach().numpy(), g["logits"], rtol=1e-5, atol=1e-6)
+    assert abs(loss.item() - float(g["loss"])) < 1e-6
+    assert np.allclose(z.grad.numpy(), g["dz"], rtol=1e-4, atol=1e-7)
+    for i, (k, p) in enumerate(m.named_parameters()):
+        ref = g[f"grad_{i}"]
+        err = np.linalg.norm(p.grad.numpy() - ref) / max(np.linalg.norm(ref), 1e-30)
+        assert err < 1e-5, (k, err)
+    sd = m.state_dict()
+    for i, k in enumerate(g["bn_names"]):
+        assert np.allclose(sd[k].numpy(), g[f"bn_{i}"], rtol=1e-5, atol=1e-7), k
+
+
+def test_seqvae_classifier_loss(golden):
+    """SeqVaeTebClassifier.compute_loss (ELBO beta 1 + CE, end to end) at S=16."""
+    from oracle import classifier_ref as C
+    g = golden("seqvae_classifier_s16_b4")
+    S = int(g["S"])
+    vae = det_fill_(M.SeqVaeTebRef(S))
+    clf = det_fill_(C.InceptionTimeClassifier(dropout=0.0))
+    vae.train()
+    clf.train()
+    T = lambda k: torch.from_numpy(g[k])
+    out = C.seqvae_classifier_loss(vae, clf, T("y_st"), T("y_ph"), T("x_ph"), T("labels"), T("y_raw"), T("eps"))
+    out["total_loss"].backward()
+    for k in ("classification_loss", "vae_loss", "total_loss"):
+        assert abs(out[k].item() - float(g[k])) <= 1e-5 * abs(float(g[k])), k
+    params = [("vae_model." + k, p) for k, p in vae.named_parameters()] + \
+             [("classifier." + k, p) for k, p in clf.named_parameters()]
+    assert [k for k, _ in params] == list(g["param_names"])
+    gl2 = np.array([p.grad.norm().item() for _, p in params])
+    assert np.allclose(gl2, g["grad_l2"], rtol=2e-4, atol=1e-8)

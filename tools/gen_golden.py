@@ -346,8 +346,84 @@ def gen_tiny():
     save("tiny_c1.npz", **d)
 
 
+def _crop_conv_long_(clf):
+    """The reference's conv_long (k 40, padding 20) returns L+1 positions and
+    torch.concat then fails (ref/model/inception_time.py:51-57,113; SURVEY.md
+    §0.7): keep the first L, the documented deviation the build adopts."""
+    for blk in clf.inception_blocks:
+        conv = blk.conv_long
+        orig = conv.forward
+        conv.forward = lambda x, _o=orig: _o(x)[..., :x.shape[-1]]
+    return clf
+
+
+def gen_classifier():
+    """Config 4 (SURVEY.md §8c fixture 8): FHRInceptionTimeClassifier alone and
+    SeqVaeTebClassifier.compute_loss (ELBO beta 1 + CE, end-to-end)."""
+    import torch.nn.functional as Fn
+    import inception_time as IT
+    import vae_teb_model as V
+
+    B, S = 4, 64
+    rng = np.random.Generator(np.random.PCG64(44))
+    z = rng.standard_normal((B, S, 32)).astype(np.float32)
+    labels = np.array([0, 1, 1, 0], dtype=np.int64)
+    clf = _crop_conv_long_(IT.FHRInceptionTimeClassifier(input_size=32, num_classes=2, filters=32, depth=6,
+                                                         dropout=0.0, use_attention=True))
+    det_fill_(clf)
+    clf.train()
+    zt = torch.from_numpy(z).requires_grad_(True)
+    logits = clf(zt)
+    loss = Fn.cross_entropy(logits, torch.from_numpy(labels))
+    loss.backward()
+    d = dict(B=B, S=S, z=z, labels=labels, logits=logits.detach().numpy(), loss=loss.item(), dz=zt.grad.numpy())
+    names = [k for k, _ in clf.named_parameters()]
+    d["param_names"] = np.array(names)
+    for i, (k, p) in enumerate(clf.named_parameters()):
+        d[f"grad_{i}"] = p.grad.numpy()
+    sd = clf.state_dict()
+    bn_keys = [k for k in sd if k.endswith("running_mean") or k.endswith("running_var")]
+    d["bn_names"] = np.array(bn_keys)
+    for i, k in enumerate(bn_keys):
+        d[f"bn_{i}"] = sd[k].numpy()
+    print(f"classifier B={B} S={S}: loss={loss.item():.6f}")
+    save("classifier_s64_b4.npz", **d)
+
+    # SeqVaeTebClassifier end to end (freeze_vae=False), S = 16
+    B, S = 4, 16
+    rng = np.random.Generator(np.random.PCG64(45))
+    y_st = rng.standard_normal((B, S, 43)).astype(np.float32)
+    y_ph = rng.standard_normal((B, S, 44)).astype(np.float32)
+    x_ph = rng.standard_normal((B, S, 130)).astype(np.float32)
+    y_raw = rng.standard_normal((B, 16 * S)).astype(np.float32)
+    eps = rng.standard_normal((B, S, 32)).astype(np.float32)
+    labels = np.array([1, 0, 0, 1], dtype=np.int64)
+    m = V.SeqVaeTebClassifier(sequence_length=S, freeze_vae=False, classifier_dropout=0.0)
+    m.vae_model = build_ref_model(S)
+    _crop_conv_long_(m.classifier)
+    det_fill_(m.classifier)
+    m.train()
+    m.vae_model.reparameterize = lambda mu, lv: mu + torch.from_numpy(eps) * torch.exp(0.5 * lv)
+    out = m.compute_loss(torch.from_numpy(y_st), torch.from_numpy(y_ph), torch.from_numpy(x_ph),
+                         torch.from_numpy(labels), y_raw=torch.from_numpy(y_raw), compute_vae_loss=True,
+                         vae_loss_weight=0.1)
+    out["total_loss"].backward()
+    d = dict(B=B, S=S, y_st=y_st, y_ph=y_ph, x_ph=x_ph, y_raw=y_raw, eps=eps, labels=labels,
+             logits=out["logits"].detach().numpy(), classification_loss=out["classification_loss"].item(),
+             vae_loss=out["vae_loss"].item(), total_loss=out["total_loss"].item())
+    names = [k for k, _ in m.named_parameters()]
+    d["param_names"] = np.array(names)
+    d["grad_l2"] = np.array([p.grad.norm().item() for _, p in m.named_parameters()])
+    for i, (k, p) in enumerate(m.named_parameters()):
+        if k.startswith("classifier."):
+            d[f"grad_{i}"] = p.grad.numpy()
+    print(f"SeqVaeTebClassifier B={B} S={S}: total={d['total_loss']:.6f} ce={d['classification_loss']:.6f}")
+    save("seqvae_classifier_s16_b4.npz", **d)
+
+
 GENS = dict(kat=gen_kymatio_kat, filters=gen_filters, scattering=gen_scattering, frontend=gen_frontend,
-            stats=gen_stats_and_norm, model=gen_model, tiny=gen_tiny)
+            stats=gen_stats_and_norm, model=gen_model, tiny=gen_tiny,
+            classifier=gen_classifier)
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
