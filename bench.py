@@ -9,7 +9,7 @@ gradient all-reduce (N > 1) -> grad-norm clip -> AdamW.  Data are synthetic
 fetal-monitoring windows (vaeteb.synthetic; the clinical HDF5 records are not
 available), weights are the reference architecture's random init.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--frontend j11|j6] [--batch B]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--frontend j11|j6] [--batch B] [--workload c2|c4|c5]
   N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel, timed
@@ -98,7 +98,7 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def cpu_baseline(frontend_cfg, batch=8, threads=None):
+def cpu_baseline(frontend_cfg, batch=8, threads=None, classifier=False):
     """Faithful CPU restatement (oracle): front-end called twice per window with
     all 903 pairs then masked (create_hdf5_dataset.py:418-441), torch.fft as in
     the reference, + SeqVaeTeb(S=256) fwd/bwd/clip/AdamW on torch-CPU fp32."""
@@ -124,12 +124,23 @@ def cpu_baseline(frontend_cfg, batch=8, threads=None):
     y_raw = F.normalize(x[:, 0], "fhr", st["fhr_mean"], st["fhr_variance"])
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(a.transpose(0, 2, 1)))
     b = dict(y_st=tt(y_st), y_ph=tt(y_ph), x_ph=tt(x_ph), y_raw=torch.from_numpy(y_raw))
-    M.train_step(model, b, torch.randn(batch, 256, 32), 1e-5)
+    if classifier:
+        from oracle import classifier_ref as C
+        clf = C.InceptionTimeClassifier(dropout=0.2).train()
+        params = list(model.parameters()) + list(clf.parameters())
+        out = C.seqvae_classifier_loss(model, clf, b["y_st"], b["y_ph"], b["x_ph"],
+                                       torch.randint(0, 2, (batch,)), b["y_raw"], torch.randn(batch, 256, 32))
+        out["total_loss"].backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        torch.optim.AdamW(params, lr=1e-3, weight_decay=1e-4, eps=1e-8, betas=(0.9, 0.98)).step()
+    else:
+        M.train_step(model, b, torch.randn(batch, 256, 32), 1e-5)
     dt = time.perf_counter() - t0
     F.FFT_ENGINE = "numpy"
     return {"value": round(batch / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
             "sample": f"1 faithful CPU step at batch {batch}: front-end x2 calls with all 903 pairs + "
-                      f"SeqVaeTeb(S=256) fwd/bwd/clip/AdamW, torch threads={threads}, {dt:.1f} s"}
+                      f"SeqVaeTeb(S=256){' + classifier' if classifier else ''} fwd/bwd/clip/AdamW, "
+                      f"torch threads={threads}, {dt:.1f} s"}
 
 
 def run_c5(args, rank, world, dev):
@@ -196,8 +207,9 @@ def run_c5(args, rank, world, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c5"], default="c2",
-                    help="c2: the training step (BASELINE.json metric, default); c5: long-sequence scattering front-end")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2",
+                    help="c2: the training step (BASELINE.json metric, default); c4: the same step with the "
+                         "classification head trained jointly (CE + 0.1 ELBO); c5: long-sequence scattering front-end")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -227,14 +239,23 @@ def main():
     fe = FrontEnd(plan, load_stats(J, Q, T, N))
     S = plan.S
     torch.manual_seed(1234)  # same initial weights on every rank (DDP semantics)
-    model = SeqVaeTeb(sequence_length=S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,
-                      cross_phase_channels=fe.C_x, head_precision=args.heads, conv_precision=args.conv,
-                      concurrent_encoders=not args.serial_encoders).to(dev)
+    vae_kw = dict(scattering_channels=fe.C_st, phase_channels=fe.C_ph, cross_phase_channels=fe.C_x,
+                  head_precision=args.heads, conv_precision=args.conv, concurrent_encoders=not args.serial_encoders)
+    c4 = args.workload == "c4"
+    if c4:
+        # config 4: SeqVaeTebClassifier end to end (freeze_vae=False), the reference's default classifier
+        # (filters 32, depth 6, dropout 0.2, attention), total = CE + 0.1 * ELBO(beta 1)
+        from vaeteb.classifier import SeqVaeTebClassifier
+        assert not args.graph, "--graph is not wired for the classifier workload"
+        model = SeqVaeTebClassifier(sequence_length=S, freeze_vae=False, **vae_kw).to(dev)
+    else:
+        model = SeqVaeTeb(sequence_length=S, **vae_kw).to(dev)
     trainer = Trainer(model, lr=1e-3, frontend=fe, world_size=world)
 
     # synthetic windows resident in HBM before timing; global sample index ->
     # rank sharding as DistributedSampler (each rank its own B windows per step)
     pool = [torch.from_numpy(synthetic.batch((rank + world * i) * B, B, N)).to(dev) for i in range(2)]
+    labels = [torch.from_numpy(np.random.default_rng(rank + world * i).integers(0, 2, B)).to(dev) for i in range(2)]
     torch.cuda.synchronize()
 
     # vt_fe_pairs work = algorithmic HBM bytes of the call: B x n_pairs x (read a_i, a_j: 2 N complex64; write
@@ -279,7 +300,7 @@ def main():
             return out
         step.first = True
     else:
-        step = lambda i, last=False: trainer.step({"x": pool[i % 2]})
+        step = lambda i, last=False: trainer.step({"x": pool[i % 2], "labels": labels[i % 2]})
     for i in range(args.warmup):
         step(i, last=i == args.warmup - 1)
     if graph:
@@ -302,7 +323,9 @@ def main():
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    elbo = {k: round(float(last[k].item()), 6) for k in ("total_loss", "nll_loss", "mse_loss", "kld_loss")}
+    keys = ("total_loss", "classification_loss", "vae_loss") if c4 else ("total_loss", "nll_loss", "mse_loss",
+                                                                          "kld_loss")
+    elbo = {k: round(float(last[k].item()), 6) for k in keys}
     samples = args.steps * B * world
     value = samples / dt
     k_ms, k_n = timer.mean_ms("vt_fe_pairs")
@@ -318,8 +341,11 @@ def main():
                  "bf16 MFMA (" + " + ".join(n for n, v in (("decoder heads", args.heads), ("conv blocks", args.conv))
                                            if v == "bf16") + "), fp32 accumulation; fp32 elsewhere",
         "data": "synthetic",
-        "config": {"workload": f"c2: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTeb(R={16 * S}) "
-                               f"train step, batch {B}/GPU", "global_batch": B * world, "seq_len": N,
+        "config": {"workload": (f"c4: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTebClassifier("
+                                f"R={16 * S}, FHRInceptionTimeClassifier f32 d6 attention, dropout 0.2) end-to-end "
+                                f"train step, CE + 0.1 ELBO, batch {B}/GPU") if c4 else
+                               (f"c2: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTeb(R={16 * S}) "
+                                f"train step, batch {B}/GPU"), "global_batch": B * world, "seq_len": N,
                    "parallelism": f"dp{world}"},
         "elbo": elbo,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
@@ -350,7 +376,7 @@ def main():
                        "frac": round(tf / MFMA_PEAK_TFLOPS, 4), "ms_per_step": round(mfma_ms / mfma_steps, 3),
                        "timed_in": "eager steps after the timed region" if graph else "timed region"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline((J, Q, T), batch=args.cpu_batch)
+        out["cpu_baseline"] = cpu_baseline((J, Q, T), batch=args.cpu_batch, classifier=c4)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -134,8 +134,9 @@ class Trainer:
     over flat buffers (ref/model/graph_model.py:654-660, :724)."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=1e-4, max_norm=1.0, beta_kld=1e-5,
-                 frontend=None, world_size=1, group=None, bucket_mb=64.0):
+                 frontend=None, world_size=1, group=None, bucket_mb=64.0, vae_loss_weight=0.1):
         self.model = model
+        self.vae_loss_weight = vae_loss_weight
         self.frontend = frontend
         self.state = FlatState(model)
         self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_norm
@@ -154,13 +155,20 @@ class Trainer:
         """Forward + loss for an AttributeDict-like batch with fields fhr_st,
         fhr_ph, fhr_up_ph (B,S,C) and fhr (B,R) (the reference batch contract,
         ref/model/graph_model.py:702-705), or raw windows under key 'x'."""
+        vae = getattr(self.model, "vae_model", self.model)   # SeqVaeTebClassifier (config 4) wraps the VAE
+        labels = batch.get("labels") if hasattr(batch, "get") else None
         if "x" in batch:
             side = None
-            if getattr(self.model, "concurrent_encoders", False) and batch["x"].is_cuda:
+            if getattr(vae, "concurrent_encoders", False) and batch["x"].is_cuda:
                 from .model import side_stream
                 side = side_stream(batch["x"].device.index if batch["x"].device.index is not None else
                                    torch.cuda.current_device(), 1)  # the source encoder's stream
             batch = self.frontend(batch["x"], side=side)
+        if vae is not self.model:
+            # SeqVaeTebClassifier.compute_loss (ref/model/vae_teb_model.py:1440-1498): CE + w * ELBO(beta 1)
+            return self.model.compute_loss(batch["fhr_st"], batch["fhr_ph"], batch["fhr_up_ph"], labels,
+                                           y_raw=batch["fhr"], compute_vae_loss=True,
+                                           vae_loss_weight=self.vae_loss_weight, eps=eps)
         fw = self.model(batch["fhr_st"], batch["fhr_ph"], batch["fhr_up_ph"], eps=eps)
         return self.model.compute_loss(fw, batch["fhr_st"], batch["fhr_ph"], batch["fhr"], compute_kld_loss=True,
                                        beta=self.beta_kld)
