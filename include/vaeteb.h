@@ -313,6 +313,11 @@ int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const
 int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, int act, float* dx, float* dgamma, float* dbeta,
                      int accumulate_params, float* ws, int64_t ws_floats, void* stream);
+/* Eval-mode BatchNorm1d (running statistics) + activation, elementwise on (M, C).
+ * replaces: model.eval() BatchNorm in ref/model/vae_teb_model.py:175,:230 and
+ *           ref/model/inception_time.py:77,:139 (validation, frozen VAE, predict) */
+int vt_batchnorm_eval(const float* x, int64_t M, int C, const float* run_mean, const float* run_var, float eps,
+                      const float* gamma, const float* beta, int act, float* y, void* stream);
 int vt_act_fwd(const float* x, int64_t n, int act, float* y, void* stream);
 int vt_act_bwd(const float* dy, const float* x, int64_t n, int act, float* dx, void* stream);
 

@@ -422,6 +422,16 @@ __global__ void k_bn_apply(const float* __restrict__ x, int64_t M, int C, const 
     y[i] = act_f((x[i] - mean[c]) * rstd[c] * gamma[c] + beta[c], act);
 }
 
+// eval-mode BatchNorm: running statistics
+__global__ void k_bn_eval(const float* __restrict__ x, int64_t M, int C, const float* __restrict__ run_mean,
+                          const float* __restrict__ run_var, float eps, const float* __restrict__ gamma,
+                          const float* __restrict__ beta, int act, float* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M * C) return;
+    const int c = (int)(i % C);
+    y[i] = act_f((x[i] - run_mean[c]) * (1.f / sqrtf(run_var[c] + eps)) * gamma[c] + beta[c], act);
+}
+
 // dx = gamma*rstd*(dz - dbeta/M - xhat*dgamma/M)
 __global__ void k_bn_dx(const float* __restrict__ dy, const float* __restrict__ x, int64_t M, int C,
                         const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -582,6 +592,15 @@ int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const fl
     hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
                        accumulate_params);
     VT_LAUNCH_CHECK("vt_batchnorm_bwd");
+    return VT_OK;
+}
+
+int vt_batchnorm_eval(const float* x, int64_t M, int C, const float* run_mean, const float* run_var, float eps,
+                      const float* gamma, const float* beta, int act, float* y, void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0, "vt_batchnorm_eval: shape");
+    hipLaunchKernelGGL(k_bn_eval, dim3(blocks_for(M * C)), dim3(256), 0, S(stream), x, M, C, run_mean, run_var, eps,
+                       gamma, beta, act, y);
+    VT_LAUNCH_CHECK("vt_batchnorm_eval");
     return VT_OK;
 }
 

@@ -319,6 +319,49 @@ def _dropout(x, p, training):
     return _DropoutF.apply(x, p, _seed()) if (training and p > 0) else x
 
 
+def _no_grad_check(*ts):
+    if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
+        raise RuntimeError("eval-mode classifier blocks are inference-only (run under torch.no_grad())")
+
+
+def _inception_eval(m, x):
+    """FHRInception in eval mode: BatchNorm with the running statistics, no dropout."""
+    _no_grad_check(x, m.bottleneck1.weight)
+    x = x.contiguous()
+    B, L, Cin = x.shape
+    f = m.bottleneck1.weight.shape[0]
+    C4 = 4 * f
+    st = _st()
+    x0 = torch.empty((B, L, f), device=x.device)
+    call("vt_zconv_fwd", ptr(x), Cin, B, L, Cin, ptr(m.bottleneck1.weight), f, 1, 0, ptr(x0), f, 0, st)
+    cat = torch.empty((B, L, C4), device=x.device)
+    for j, (w, K, P) in enumerate(((m.conv_short.weight, 5, 2), (m.conv_medium.weight, 15, 7),
+                                   (m.conv_long.weight, 40, 20))):
+        call("vt_zconv_fwd", ptr(x0), f, B, L, f, ptr(w), f, K, P, _col(cat, j * f), C4, 0, st)
+    mp = torch.empty_like(x)
+    call("vt_maxpool3_fwd", ptr(x), B, L, Cin, ptr(mp), st)
+    call("vt_zconv_fwd", ptr(mp), Cin, B, L, Cin, ptr(m.bottleneck2.weight), f, 1, 0, _col(cat, 3 * f), C4, 0, st)
+    bn = m.batch_norm
+    call("vt_batchnorm_eval", ptr(cat), B * L, C4, ptr(bn.running_mean), ptr(bn.running_var), bn.eps, ptr(bn.weight),
+         ptr(bn.bias), ACT["relu"], ptr(cat), st)
+    return cat
+
+
+def _residual_eval(m, x, y):
+    _no_grad_check(x, y, m.bottleneck.weight)
+    x, y = x.contiguous(), y.contiguous()
+    B, L, Cin = x.shape
+    C4 = m.bottleneck.weight.shape[0]
+    st = _st()
+    r = torch.empty((B, L, C4), device=x.device)
+    call("vt_zconv_fwd", ptr(x), Cin, B, L, Cin, ptr(m.bottleneck.weight), C4, 1, 0, ptr(r), C4, 0, st)
+    bn = m.batch_norm
+    call("vt_batchnorm_eval", ptr(r), B * L, C4, ptr(bn.running_mean), ptr(bn.running_var), bn.eps, ptr(bn.weight),
+         ptr(bn.bias), ACT["none"], ptr(r), st)
+    call("vt_add_act_fwd", ptr(y), ptr(r), r.numel(), ACT["relu"], ptr(r), st)
+    return r
+
+
 # -------------------------------------------------------------- modules
 class FHRInception(nn.Module):
     """ref/model/inception_time.py:9-117 (kaiming fan_out init, :80-87)."""
@@ -337,7 +380,7 @@ class FHRInception(nn.Module):
 
     def forward(self, x):
         if not self.training:
-            raise NotImplementedError("eval-mode BatchNorm is not on the training path yet")
+            return _inception_eval(self, x)
         bn = self.batch_norm
         p = self.dropout
         y = _InceptionF.apply(x, self.bottleneck1.weight, self.conv_short.weight, self.conv_medium.weight,
@@ -359,6 +402,8 @@ class FHRResidual(nn.Module):
 
     def forward(self, x, y):
         bn = self.batch_norm
+        if not self.training:
+            return _residual_eval(self, x, y)
         p = self.dropout
         out = _ResidualF.apply(x, y, self.bottleneck.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.momentum, bn.eps, p, _seed() if p > 0 else 0)
@@ -443,10 +488,10 @@ class FHRInceptionTimeClassifier(nn.Module):
 
 
 class SeqVaeTebClassifier(nn.Module):
-    """ref/model/vae_teb_model.py:1248-1526 (training path).  freeze_vae=False
-    is the multi-task configuration of BASELINE.json config 4 (ELBO with beta 1
-    + CE, end to end); freeze_vae=True needs the VAE in eval mode, whose
-    BatchNorm is not on the training path yet, and raises."""
+    """ref/model/vae_teb_model.py:1248-1526.  freeze_vae=False is the multi-task
+    configuration of BASELINE.json config 4 (ELBO with beta 1 + CE, end to end);
+    freeze_vae=True (the reference default) runs the VAE in eval mode without
+    gradients and trains the classifier only."""
 
     def __init__(self, input_channels=76, sequence_length=300, latent_dim_source=32, latent_dim_target=32,
                  latent_dim_z=32, decimation_factor=16, warmup_period=30, num_classes=2, classifier_filters=32,
@@ -481,11 +526,19 @@ class SeqVaeTebClassifier(nn.Module):
             p.requires_grad = True
 
     def extract_latent_features(self, y_st, y_ph, x_ph, return_all_outputs=False, eps=None):
+        """ref :1350-1390: a frozen VAE runs in eval mode without gradients."""
         if self.freeze_vae:
-            raise NotImplementedError("freeze_vae=True needs eval-mode BatchNorm in the VAE (not on the "
-                                      "training path yet); use freeze_vae=False (end-to-end multi-task)")
-        out = self.vae_model(y_st, y_ph, x_ph, eps=eps)
+            self.vae_model.eval()
+        with torch.set_grad_enabled(torch.is_grad_enabled() and not self.freeze_vae):
+            out = self.vae_model(y_st, y_ph, x_ph, eps=eps)
         return (out["z"], out) if return_all_outputs else out["z"]
+
+    def predict(self, y_st, y_ph, x_ph, return_probabilities=True):
+        """ref :1500-1526."""
+        self.eval()
+        with torch.no_grad():
+            out = self.forward(y_st, y_ph, x_ph)
+        return (out["predictions"], out["probabilities"]) if return_probabilities else out["predictions"]
 
     def forward(self, y_st, y_ph, x_ph, labels=None, return_latent=False, eps=None):
         z = self.extract_latent_features(y_st, y_ph, x_ph, eps=eps)

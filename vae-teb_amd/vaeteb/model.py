@@ -236,8 +236,10 @@ class ConvBlock(nn.Module):
 
     def forward(self, x):
         bn = self.bn_layer
-        if not self.training:
-            raise NotImplementedError("eval-mode BatchNorm is not on the training path yet")
+        if not self.training:   # model.eval(): running statistics (validation, frozen VAE, predict)
+            return ops.conv_bn_eval(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                    mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
+                                    eps=bn.eps, bf16=self.bf16)
         y = ops.conv_bn_act(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                             mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
                             momentum=bn.momentum, eps=bn.eps, bf16=self.bf16)

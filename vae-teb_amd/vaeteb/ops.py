@@ -452,6 +452,27 @@ class ConvBNActF(torch.autograd.Function):
         return gx, gw, gg, gb, None, None, None, None, None, None, None, None
 
 
+def conv_bn_eval(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", eps=1e-5, bf16=False):
+    """Eval-mode ConvBlock: conv -> BatchNorm with the running statistics -> act
+    (validation / frozen-VAE / predict path; not differentiable)."""
+    _check(x, w, g, b)
+    if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
+        raise RuntimeError("eval-mode conv blocks are inference-only (run under torch.no_grad())")
+    B, L, Cin = x.shape
+    Cout, _, K = w.shape
+    x = x.contiguous()
+    Lo = _lib.lib().fns["vt_conv1d_out_len"](L, K, mode, up)
+    conv = torch.empty((B, Lo, Cout), device=x.device)
+    if bf16:
+        w16, _ = _conv_shadow(w)
+        call("vt_conv1d_fwd_bf16", ptr(x), B, L, Cin, ptr(w16), Cout, K, mode, up, ptr(conv), _st())
+    else:
+        call("vt_conv1d_direct_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(conv), _st())
+    call("vt_batchnorm_eval", ptr(conv), B * Lo, Cout, ptr(run_mean), ptr(run_var), eps, ptr(g), ptr(b), ACT[act],
+         ptr(conv), _st())
+    return conv
+
+
 # ---------------------------------------------------------------------- LSTM
 class LSTMF(torch.autograd.Function):
     """Multi-layer unidirectional LSTM, batch_first, zero initial state.
