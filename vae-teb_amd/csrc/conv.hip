@@ -447,9 +447,49 @@ static int launch_fwd(const float* x, const Geo& g, const float* w, float* y, in
     }
 }
 
+// Two-stage fixed-order reduction for many splits: stage 1 sums groups of SG_GRP
+// consecutive slabs per output (one thread per output, coalesced across
+// outputs, grid (outputs / 256, groups) — enough workgroups for the
+// 2-6 K-output conv gradients whose one-stage sum ran on ~30 workgroups) and
+// leaves each group's sum in place in the group's first slab; stage 2 sums the
+// groups in order.
+static constexpr int SG_GRP = 32;
+
+__global__ __launch_bounds__(256) void k_sum_splits_grp(float* __restrict__ part, int splits, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int s0 = blockIdx.y * SG_GRP;
+    const int s1 = s0 + SG_GRP < splits ? s0 + SG_GRP : splits;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int s = s0;
+    for (; s + 4 <= s1; s += 4)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] += part[(int64_t)(s + u) * n + i];
+    for (; s < s1; ++s) a[0] += part[(int64_t)s * n + i];
+    part[(int64_t)s0 * n + i] = (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+__global__ __launch_bounds__(256) void k_sum_splits_fin(const float* __restrict__ part, int splits, int64_t n,
+                                                        float* __restrict__ out, int accumulate) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float a = 0.f;
+    for (int s0 = 0; s0 < splits; s0 += SG_GRP) a += part[(int64_t)s0 * n + i];
+    out[i] = accumulate ? out[i] + a : a;
+}
+
+// part is scratch: the two-stage path overwrites it
 int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st) {
-    hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, splits, n, out,
-                       accumulate);
+    if (splits <= 2 * SG_GRP || n >= (int64_t)64 * 1024) {
+        hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, splits, n, out,
+                           accumulate);
+        return VT_OK;
+    }
+    float* p = const_cast<float*>(part);
+    const unsigned bx = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_sum_splits_grp, dim3(bx, (unsigned)((splits + SG_GRP - 1) / SG_GRP)), dim3(256), 0, st, p,
+                       splits, n);
+    hipLaunchKernelGGL(k_sum_splits_fin, dim3(bx), dim3(256), 0, st, p, splits, n, out, accumulate);
     return VT_OK;
 }
 
@@ -552,8 +592,7 @@ int vt_conv1d_direct_bwd_weight(const float* dY, const float* X, int B, int L_in
     VT_CONV_DW(7, 1) VT_CONV_DW(7, 3) VT_CONV_DW(8, 1) VT_CONV_DW(8, 2) VT_CONV_DW(9, 1) VT_CONV_DW(9, 2)
     VT_CONV_DW(10, 1) VT_CONV_DW(10, 2) VT_CONV_DW(11, 1) VT_CONV_DW(11, 2)
 #undef VT_CONV_DW
-    hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, st, ws, (int)splits, nout, dW,
-                       accumulate);
+    sum_splits_launch(ws, (int)splits, nout, dW, accumulate, st);
     VT_LAUNCH_CHECK("vt_conv1d_direct_bwd_weight");
     return VT_OK;
 }

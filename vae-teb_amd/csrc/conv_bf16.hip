@@ -269,6 +269,7 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < DWR / 32; ++s) {
+            if (!act[0]) break;  // wave-uniform: a wave without pairs only stages
 #pragma unroll
             for (int j = 0; j < PPW; ++j) {
                 // no early-out on inactive pairs: the transposed read needs all 64 lanes (EXEC all ones)
@@ -405,7 +406,10 @@ int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, 
                  "vt_conv1d_bwd_weight_bf16: shape (K <= %d, channels <= 128)", KMAXB);
     Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
     const int NTc = cdiv(Cin, 16), npairs = cdiv(Cout, 16) * NTc;
-    const int ppw = K <= 3 ? 6 : (K <= 5 ? 4 : (K <= 7 ? 3 : 2));
+    // pairs per wave: at most what the accumulators allow, and no more than the
+    // 4 waves of one workgroup need (small layers: no MFMAs on empty pairs)
+    const int ppw_max = K <= 3 ? 6 : (K <= 5 ? 4 : (K <= 7 ? 3 : 2));
+    const int ppw = cdiv(npairs, 4) < ppw_max ? cdiv(npairs, 4) : ppw_max;
     const int bx = cdiv(npairs, 4 * ppw);
     const int64_t rows = (int64_t)B * g.L_out;
     const int64_t nout = (int64_t)Cout * Cin * K;
@@ -426,8 +430,16 @@ int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, 
     if (K == KK && ppw == PP)                                                                                  \
         hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP>), grid, dim3(256), lds, st, dY, X, g, rps, NTc, npairs, dstride, \
                            xstride, ws);
-    VT_DWB(1, 6) VT_DWB(2, 6) VT_DWB(3, 6) VT_DWB(4, 4) VT_DWB(5, 4) VT_DWB(6, 3) VT_DWB(7, 3)
-    VT_DWB(8, 2) VT_DWB(9, 2) VT_DWB(10, 2) VT_DWB(11, 2)
+#define VT_DWB6(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3) VT_DWB(KK, 4) VT_DWB(KK, 5) VT_DWB(KK, 6)
+#define VT_DWB4(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3) VT_DWB(KK, 4)
+#define VT_DWB3(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3)
+#define VT_DWB2(KK) VT_DWB(KK, 1) VT_DWB(KK, 2)
+    VT_DWB6(1) VT_DWB6(2) VT_DWB6(3) VT_DWB4(4) VT_DWB4(5) VT_DWB3(6) VT_DWB3(7)
+    VT_DWB2(8) VT_DWB2(9) VT_DWB2(10) VT_DWB2(11)
+#undef VT_DWB6
+#undef VT_DWB4
+#undef VT_DWB3
+#undef VT_DWB2
 #undef VT_DWB
     const int rc = sum_splits_launch(ws, (int)splits, nout, dW, accumulate, st);
     if (rc) return rc;

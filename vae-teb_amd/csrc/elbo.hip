@@ -59,8 +59,13 @@ __global__ __launch_bounds__(ELBO_THREADS) void k_latent_bwd(
         // d/dmu_post: from z (gz), from the KL (dm * ip), plus direct upstream
         const float g_mq = gz + gmp + gk * dm * ip;
         g_mu_c[i] = g_mq;
-        // mu_prior is mu_y itself: KL's -(dm*ip) plus the residual path via mu_post
-        g_mu_y[i] = g_mq - gk * dm * ip;
+        // mu_prior is mu_y itself and mu_post - mu_prior = mu_c: the KL does not depend
+        // on mu_y, so its two terms (via mu_post and via mu_prior) cancel exactly.  Written
+        // as gz + gmp instead of g_mq - gk*dm*ip: at beta = 1 the rounding residue of that
+        // cancellation (~ulp of the KL term) swamps the decoder's gradient into the
+        // 33-layer target mu_layer (the reference's fp32 autograd carries such a residue;
+        // tests compare against the fp64 oracle with the reference's own error as the bound)
+        g_mu_y[i] = gz + gmp;
         g_lv_q[i] = gz * 0.5f * eps[i] * expf(0.5f * lq) + gk * 0.5f * (eq * ip - 1.f);
         g_lv_p[i] = gk * 0.5f * (1.f - (eq + dm * dm) * ip);
     }

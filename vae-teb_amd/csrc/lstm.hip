@@ -17,7 +17,30 @@ namespace vt {
 static constexpr int H = 64;
 static constexpr int G4 = 4 * H;
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// Recurrence-latency transcendentals on the hardware v_exp_f32 / v_rcp_f32
+// (~1 ulp each) — the libm expf / tanhf / IEEE divide sequences are dozens of
+// dependent instructions on the per-step critical path:
+//   sigmoid(x) = 1 / (1 + 2^(-x log2 e))                (relative error ~2 ulp)
+//   tanh(x)    = odd Taylor polynomial to x^11 for |x| < 0.3 (truncation 2e-9),
+//                else sign(x) (1 - 2 / (e^{2|x|} + 1))   (relative error < 4e-7)
+// Relative (not just absolute) accuracy near 0 matters: h = o tanh(c) feeds
+// deep LayerNorm stacks whose gradients amplify relative input errors
+// (the 33-layer target mu_layer; tests/test_gpu_classifier.py).
+__device__ __forceinline__ float sigm(float x) {
+    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+__device__ __forceinline__ float ftanh(float x) {
+    const float ax = fabsf(x), x2 = x * x;
+    float p = -0.00886323552990220f;            // -1382/155925
+    p = fmaf(p, x2, 0.0218694885361552f);       //  62/2835
+    p = fmaf(p, x2, -0.0539682539682540f);      // -17/315
+    p = fmaf(p, x2, 0.133333333333333f);        //  2/15
+    p = fmaf(p, x2, -0.333333333333333f);       // -1/3
+    const float small = fmaf(x * x2, p, x);
+    const float e = __builtin_amdgcn_exp2f(2.88539008177792681f * ax);   // e^{2|x|}
+    const float big = copysignf(fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f), x);
+    return ax < 0.3f ? small : big;
+}
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic,
 // not for its global stores / prefetch loads (__syncthreads() would drain
@@ -31,66 +54,102 @@ __device__ __forceinline__ void lds_barrier() {
 
 static constexpr int TS = 16;  // time steps per staged chunk
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// DPP quad broadcast: every lane of a 4-lane quad receives lane Q's value
+template <int Q>
+__device__ __forceinline__ float quad_bcast(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), Q * 0x55, 0xF, 0xF,
+                                                                 false));
+}
+
+// fixed-order quad sum ((l0 + l1) + (l2 + l3)), the same value in all 4 lanes
+__device__ __forceinline__ float quad_sum(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+    return v;
+}
+
+// h / dg vectors in LDS are stored in 16-float segments padded to 20 floats,
+// so float4 reads of different segments by the lanes of a wave hit distinct
+// banks (at most 2-way on 16 segments).
+__device__ __forceinline__ int seg_pos(int k) { return k + ((k >> 4) << 2); }
+
+// Forward.  Thread j = 4u + q computes, for the 4 gate rows of unit u, the
+// partial dot products over k in [16q, 16q + 16) (W_hh[g*H + u][16q .. +16) in
+// 32 packed VGPR pairs): only 4 float4 LDS reads of h per thread and step (the
+// LDS return path, not the FMAs, bounded the full 64-long per-thread dots).  A
+// DPP quad all-reduce completes the 4 gate pre-activations in every lane of
+// the quad; each lane then has all gates of its unit (c is carried in every
+// lane) and lane 0 publishes h (double-buffered: ONE barrier per time step).
 // gin:   [B, S, 4H]  x W_ih^T + b_ih (precomputed)
 // out_h: [B, S, H]; out_hprev: [B, S, H] (h_{t-1}, zeros at t = 0)
 // out_c: [B, S, H] cell states; gates: [B, S, 4H] post-activation (i, f, g~, o)
-// The recurrence only touches LDS and registers: gin is loaded a chunk of TS
-// steps ahead into registers and the outputs of a chunk are staged in LDS and
-// written in one coalesced burst, so no global round trip sits between steps.
+// gin is loaded a chunk of TS steps ahead into registers and a chunk's outputs
+// are staged in LDS and written in one coalesced burst.
 __global__ __launch_bounds__(G4) void k_lstm_fwd(const float* __restrict__ gin, const float* __restrict__ whh,
                                                  const float* __restrict__ bhh, int S, float* __restrict__ out_h,
                                                  float* __restrict__ out_hprev, float* __restrict__ out_c,
                                                  float* __restrict__ gates) {
-    __shared__ __attribute__((aligned(16))) float h[H];
-    __shared__ float gb[G4];
+    __shared__ __attribute__((aligned(16))) float hbuf[2][80];
     __shared__ float og[TS * G4];                      // gates of the chunk
     __shared__ float oh[TS * H], ohp[TS * H], oc[TS * H];
-    const int j = threadIdx.x;
+    const int j = threadIdx.x, u = j >> 2, q = j & 3;
+    const int row = q * H + u;                         // this lane's gate row (gin / gates column)
     const int64_t b = blockIdx.x;
-    float w[H];
+    f2 w[4][8];
 #pragma unroll
-    for (int k = 0; k < H; ++k) w[k] = whh[j * H + k];
-    const float bias = bhh[j];
-    if (j < H) h[j] = 0.f;
-    float c = 0.f;
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            w[g][k] = f2{whh[(g * H + u) * H + 16 * q + 2 * k], whh[(g * H + u) * H + 16 * q + 2 * k + 1]};
+    const float bias = bhh[row];
+    if (j < 80) hbuf[0][j] = 0.f;
+    float c = 0.f, hprev = 0.f;  // h_{t-1} of unit u, kept in the publishing lane (no LDS read back)
     const float* g_in = gin + b * (int64_t)S * G4;
     float* gt = gates + b * (int64_t)S * G4;
     const int64_t hb = b * (int64_t)S * H;
     float cur[TS], nxt[TS];
 #pragma unroll
-    for (int i = 0; i < TS; ++i) cur[i] = g_in[(int64_t)(i < S ? i : S - 1) * G4 + j];
+    for (int i = 0; i < TS; ++i) cur[i] = g_in[(int64_t)(i < S ? i : S - 1) * G4 + row];
     lds_barrier();
     for (int t0 = 0; t0 < S; t0 += TS) {
 #pragma unroll
         for (int i = 0; i < TS; ++i) {  // unconditional (clamped) loads: no per-step waits
             const int t = t0 + TS + i;
-            nxt[i] = g_in[(int64_t)(t < S ? t : S - 1) * G4 + j];
+            nxt[i] = g_in[(int64_t)(t < S ? t : S - 1) * G4 + row];
         }
         const int n = S - t0 < TS ? S - t0 : TS;
 #pragma unroll
         for (int i = 0; i < TS; ++i) {
             if (i >= n) continue;  // block-uniform
-            float a0 = cur[i] + bias, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            const float* hc = hbuf[i & 1];   // TS even: parity of i == parity of t
+            const float* hq = hc + 20 * q;
+            const float x = cur[i] + bias;
+            f2 a[4];
 #pragma unroll
-            for (int k = 0; k < H; k += 4) {
-                const float4 hv = *reinterpret_cast<const float4*>(&h[k]);
-                a0 = fmaf(w[k], hv.x, a0);
-                a1 = fmaf(w[k + 1], hv.y, a1);
-                a2 = fmaf(w[k + 2], hv.z, a2);
-                a3 = fmaf(w[k + 3], hv.w, a3);
+            for (int g = 0; g < 4; ++g) a[g] = f2{g == q ? x : 0.f, 0.f};
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const float4 hv = *reinterpret_cast<const float4*>(&hq[4 * m]);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    a[g] = __builtin_elementwise_fma(w[g][2 * m], f2{hv.x, hv.y}, a[g]);
+                    a[g] = __builtin_elementwise_fma(w[g][2 * m + 1], f2{hv.z, hv.w}, a[g]);
+                }
             }
-            const float a = (a0 + a1) + (a2 + a3);
-            const float v = (j >= 2 * H && j < 3 * H) ? tanhf(a) : sigm(a);
-            gb[j] = v;
-            og[i * G4 + j] = v;
-            lds_barrier();
-            if (j < H) {
-                c = gb[H + j] * c + gb[j] * gb[2 * H + j];
-                const float hn = gb[3 * H + j] * tanhf(c);
-                ohp[i * H + j] = h[j];
-                h[j] = hn;
-                oh[i * H + j] = hn;
-                oc[i * H + j] = c;
+            const float pi = quad_sum(a[0].x + a[0].y), pf = quad_sum(a[1].x + a[1].y);
+            const float pg = quad_sum(a[2].x + a[2].y), po = quad_sum(a[3].x + a[3].y);
+            const float gi = sigm(pi), gf = sigm(pf), gg = ftanh(pg), go = sigm(po);
+            og[i * G4 + row] = q == 0 ? gi : (q == 1 ? gf : (q == 2 ? gg : go));
+            c = gf * c + gi * gg;
+            if (q == 0) {
+                const float hn = go * ftanh(c);
+                ohp[i * H + u] = hprev;
+                hprev = hn;
+                hbuf[(i + 1) & 1][seg_pos(u)] = hn;
+                oh[i * H + u] = hn;
+                oc[i * H + u] = c;
             }
             lds_barrier();
         }
@@ -107,64 +166,81 @@ __global__ __launch_bounds__(G4) void k_lstm_fwd(const float* __restrict__ gin, 
     }
 }
 
-static constexpr int TB = 8;  // backward steps per staged chunk (TB * H == 2 * G4 for the staging)
+static constexpr int TB = 8;   // backward steps per staged chunk (TB * H == 2 * G4 for the staging)
 
+// row all-reduce over the 16 lanes of a DPP row (quad sums, then row_ror 4 and 8)
+__device__ __forceinline__ float row16_sum(float v) {
+    v = quad_sum(v);
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+    return v;
+}
+
+// Backward.  dh_rec[u] = sum over the 256 gate rows of W_hh[row][u] dg[row]:
+// thread j = 16 ug + rg computes the partial sums of units 4ug .. 4ug+3 over
+// rows [16 rg, 16 rg + 16) (W_hh slice in 32 packed VGPR pairs, 4 float4 LDS
+// reads of dg), a 16-lane DPP row all-reduce completes them, and lane rg < 4
+// of the row owns unit u = 4ug + rg: it computes the unit's cell / gate
+// derivatives (dc carried in that lane) and publishes the 4 gate derivatives
+// (double-buffered: ONE barrier per time step).
 // dh_out: [B, S, H] gradient arriving at this layer's outputs.
 // dgates: [B, S, 4H] gradient w.r.t. the gate pre-activations.
 // Chunks of TB steps (walking t downwards) of gates / c / dh_out are loaded
-// into registers one chunk ahead by all 256 threads and handed to LDS at the
-// chunk boundary; dgates of a chunk are staged in LDS and written in a burst.
+// into registers one chunk ahead and handed to LDS at the chunk boundary;
+// dgates of a chunk are staged in LDS and written in a burst.
 __global__ __launch_bounds__(G4) void k_lstm_bwd(const float* __restrict__ dh_out, const float* __restrict__ gates,
                                                  const float* __restrict__ cst, const float* __restrict__ whh, int S,
                                                  float* __restrict__ dgates) {
-    __shared__ __attribute__((aligned(16))) float dg[G4];
-    __shared__ float part[G4];
-    __shared__ float dhr[H];
+    __shared__ __attribute__((aligned(16))) float dg[2][320];
     __shared__ float sg[TB * G4], sc[(TB + 1) * H], sdh[TB * H];  // chunk inputs
     __shared__ float odg[TB * G4];                                 // chunk outputs
     const int j = threadIdx.x;
-    const int q = j >> 6, k = j & 63;
+    const int ug = j >> 4, rg = j & 15;
+    const int u = 4 * ug + (rg & 3);                               // the unit of lanes rg < 4
+    const bool owner = rg < 4;
     const int64_t b = blockIdx.x;
-    float wc[H];  // W_hh[q*64 + r][k], r = 0..63
+    f2 wc[4][8];  // W_hh[16 rg + r][4 ug + m]
 #pragma unroll
-    for (int r = 0; r < H; ++r) wc[r] = whh[(q * H + r) * H + k];
-    if (j < H) dhr[j] = 0.f;
-    float dc = 0.f;
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            wc[m][r] = f2{whh[(16 * rg + 2 * r) * H + 4 * ug + m], whh[(16 * rg + 2 * r + 1) * H + 4 * ug + m]};
+    float dhr = 0.f, dc = 0.f;
     const int64_t hb = b * (int64_t)S * H;
     const float* gt = gates + b * (int64_t)S * G4;
     float* dgo = dgates + b * (int64_t)S * G4;
     // chunk with steps [lo, lo + TB) (lo may be < 0 at the start of the sequence)
-    float rg[TB], rc[3], rdh[2];
+    float rgv[TB], rc[3], rdh[2];
     auto fetch = [&](int lo) {
 #pragma unroll
         for (int i = 0; i < TB; ++i) {
             const int t = lo + i;
-            rg[i] = gt[(int64_t)(t >= 0 ? t : 0) * G4 + j];
+            rgv[i] = gt[(int64_t)(t >= 0 ? t : 0) * G4 + j];
         }
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {  // (TB + 1) x H cells (t = lo-1 .. lo+TB-1)
-            const int e = j + G4 * u;
+        for (int m = 0; m < 3; ++m) {  // (TB + 1) x H cells (t = lo-1 .. lo+TB-1)
+            const int e = j + G4 * m;
             const int ee = e < (TB + 1) * H ? e : 0;
             const int tc = lo - 1 + ee / H;
-            rc[u] = cst[hb + (int64_t)(tc >= 0 ? tc : 0) * H + (ee % H)];
+            rc[m] = cst[hb + (int64_t)(tc >= 0 ? tc : 0) * H + (ee % H)];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {  // TB x H output gradients
-            const int e = j + G4 * u;
+        for (int m = 0; m < 2; ++m) {  // TB x H output gradients
+            const int e = j + G4 * m;
             const int td = lo + e / H;
-            rdh[u] = dh_out[hb + (int64_t)(td >= 0 ? td : 0) * H + (e % H)];
+            rdh[m] = dh_out[hb + (int64_t)(td >= 0 ? td : 0) * H + (e % H)];
         }
     };
     auto stash = [&]() {
 #pragma unroll
-        for (int i = 0; i < TB; ++i) sg[i * G4 + j] = rg[i];
+        for (int i = 0; i < TB; ++i) sg[i * G4 + j] = rgv[i];
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int e = j + G4 * u;
-            if (e < (TB + 1) * H) sc[e] = rc[u];
+        for (int m = 0; m < 3; ++m) {
+            const int e = j + G4 * m;
+            if (e < (TB + 1) * H) sc[e] = rc[m];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) sdh[j + G4 * u] = rdh[u];
+        for (int m = 0; m < 2; ++m) sdh[j + G4 * m] = rdh[m];
     };
     int lo = S - TB;
     fetch(lo);
@@ -172,41 +248,59 @@ __global__ __launch_bounds__(G4) void k_lstm_bwd(const float* __restrict__ dh_ou
         stash();
         lds_barrier();
         fetch(lo - TB);  // next chunk in flight during this one
+        // the owner lanes' step inputs (gates, c_t, c_{t-1}, dh_out) are read from LDS one
+        // step ahead, during the previous step's matvec: no LDS round trip on the recurrence
+        float gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f, c = 0.f, cp = 0.f, dho = 0.f;
+        auto load_in = [&](int i) {
+            gi = sg[i * G4 + u];
+            gf = sg[i * G4 + H + u];
+            gg = sg[i * G4 + 2 * H + u];
+            go = sg[i * G4 + 3 * H + u];
+            c = sc[(i + 1) * H + u];
+            cp = lo + i > 0 ? sc[i * H + u] : 0.f;
+            dho = sdh[i * H + u];
+        };
+        if (owner) load_in(TB - 1);
         for (int i = TB - 1; i >= 0; --i) {
             const int t = lo + i;
             if (t < 0) break;
-            if (j < H) {
-                const float gi = sg[i * G4 + j], gf = sg[i * G4 + H + j], gg = sg[i * G4 + 2 * H + j];
-                const float go = sg[i * G4 + 3 * H + j];
-                const float c = sc[(i + 1) * H + j], cp = t > 0 ? sc[i * H + j] : 0.f;
-                const float dh = sdh[i * H + j] + dhr[j];
-                const float tc = tanhf(c);
+            float* dgb = dg[t & 1];
+            if (owner) {
+                const float dh = dho + dhr;
+                const float tc = ftanh(c);
                 const float d_o = dh * tc;
                 dc = dc + dh * go * (1.f - tc * tc);
                 const float di = dc * gg, dgg = dc * gi, df = dc * cp;
                 dc = dc * gf;
                 const float v0 = di * gi * (1.f - gi), v1 = df * gf * (1.f - gf);
                 const float v2 = dgg * (1.f - gg * gg), v3 = d_o * go * (1.f - go);
-                dg[j] = v0; dg[H + j] = v1; dg[2 * H + j] = v2; dg[3 * H + j] = v3;
+                dgb[seg_pos(u)] = v0;
+                dgb[seg_pos(H + u)] = v1;
+                dgb[seg_pos(2 * H + u)] = v2;
+                dgb[seg_pos(3 * H + u)] = v3;
                 float* o = odg + i * G4;
-                o[j] = v0; o[H + j] = v1; o[2 * H + j] = v2; o[3 * H + j] = v3;
+                o[u] = v0; o[H + u] = v1; o[2 * H + u] = v2; o[3 * H + u] = v3;
             }
             lds_barrier();
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            const float* dq = dgb + 20 * rg;
+            f2 a[4] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
-            for (int r = 0; r < H; r += 4) {
-                const float4 d = *reinterpret_cast<const float4*>(&dg[q * H + r]);
-                a0 = fmaf(wc[r], d.x, a0);
-                a1 = fmaf(wc[r + 1], d.y, a1);
-                a2 = fmaf(wc[r + 2], d.z, a2);
-                a3 = fmaf(wc[r + 3], d.w, a3);
+            for (int r = 0; r < 4; ++r) {
+                const float4 d = *reinterpret_cast<const float4*>(&dq[4 * r]);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    a[m] = __builtin_elementwise_fma(wc[m][2 * r], f2{d.x, d.y}, a[m]);
+                    a[m] = __builtin_elementwise_fma(wc[m][2 * r + 1], f2{d.z, d.w}, a[m]);
+                }
             }
-            part[j] = (a0 + a1) + (a2 + a3);
-            lds_barrier();
-            if (j < H) dhr[j] = (part[j] + part[H + j]) + (part[2 * H + j] + part[3 * H + j]);
-            lds_barrier();
+            if (owner && i > 0) load_in(i - 1);   // queued behind this step's dg reads
+            const float s0 = row16_sum(a[0].x + a[0].y), s1 = row16_sum(a[1].x + a[1].y);
+            const float s2 = row16_sum(a[2].x + a[2].y), s3 = row16_sum(a[3].x + a[3].y);
+            const int m = rg & 3;
+            dhr = m == 0 ? s0 : (m == 1 ? s1 : (m == 2 ? s2 : s3));
         }
         // flush dgates of the chunk's valid steps
+        lds_barrier();
         const int t_first = lo < 0 ? 0 : lo;
         const int i0 = t_first - lo;
         for (int idx = i0 * G4 + j; idx < TB * G4; idx += G4) dgo[(int64_t)lo * G4 + idx] = odg[idx];
