@@ -135,6 +135,16 @@ __device__ __forceinline__ float mact_d(float z, int act) {
     }
 }
 
+// minimum workgroups per CU requested from the register allocator (4 waves
+// each): the narrow stacks are latency-bound and gain from a second / third
+// resident workgroup; the wide ones (NT >= 6) need their registers
+#ifndef VT_MLP_FWD_OCC
+#define VT_MLP_FWD_OCC(nt) ((nt) <= 2 ? 4 : ((nt) <= 4 ? 3 : 1))
+#endif
+#ifndef VT_MLP_BWD_OCC
+#define VT_MLP_BWD_OCC(nt) ((nt) <= 4 ? 2 : 1)
+#endif
+
 template <int NT>
 struct Cfg {
     static constexpr int W16 = 16 * NT;
@@ -355,7 +365,7 @@ __device__ __forceinline__ void store_tile(float* Tw, const float (&z)[NT][4], i
 // GEMM sequence: layers 0..L-1 (A = the activation tile T), then the skip
 // projection (A = the x0 tile) when skip == 2.
 template <int NT>
-__global__ __launch_bounds__(FWD_THREADS) void k_mlp_fwd(MlpDesc d, const float* __restrict__ X, int64_t R,
+__global__ __launch_bounds__(FWD_THREADS, VT_MLP_FWD_OCC(NT)) void k_mlp_fwd(MlpDesc d, const float* __restrict__ X, int64_t R,
                                                          float* __restrict__ out, float* __restrict__ xh,
                                                          float* __restrict__ rs) {
     using C = Cfg<NT>;
@@ -567,7 +577,7 @@ __device__ __forceinline__ void store_h(float* Hw, const float (&xn)[NT][4], con
 // each LayerNorm layer [dgamma_l, dbeta_l (2*N_l)] (ly.po); then at PL + ly.wo
 // each layer's [N][K+1] dW|db, and the skip projection's [DL][d0+1] last.
 template <int NT>
-__global__ __launch_bounds__(FWD_THREADS) void k_mlp_bwd(MlpDesc d, const float* __restrict__ dout,
+__global__ __launch_bounds__(FWD_THREADS, VT_MLP_BWD_OCC(NT)) void k_mlp_bwd(MlpDesc d, const float* __restrict__ dout,
                                                          const float* __restrict__ xh, const float* __restrict__ rs,
                                                          int64_t R, float* __restrict__ dx,
                                                          float* __restrict__ part, int P, int PL, int wskip) {
