@@ -742,9 +742,17 @@ __global__ __launch_bounds__(256) void k_mlp_sum(MlpDesc d, MlpGrads gr, int nG,
     }
     if ((int64_t)blockIdx.x * 16 >= E) return;
     const int i = blockIdx.x * 16 + o;
-    float a = 0.f;
-    if (i < E)
-        for (int b = sl; b < nblk; b += 16) a += src[(int64_t)b * P + i];
+    // 4 interleaved accumulators, 4 loads in flight per thread (a single
+    // dependent chain of nblk/16 loads was latency-bound)
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (i < E) {
+        int b = sl;
+        for (; b + 48 < nblk; b += 64)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a4[u] += src[(int64_t)(b + 16 * u) * P + i];
+        for (int u = 0; b < nblk; b += 16, ++u) a4[u & 3] += src[(int64_t)b * P + i];
+    }
+    const float a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
     red[sl][o] = a;
     __syncthreads();
     if (sl != 0 || i >= E) return;
