@@ -220,6 +220,10 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the model step as a captured hipGraph (double-buffered, front-end one step ahead) "
                          "instead of dispatching every op from Python (default: eager, currently faster)")
+    ap.add_argument("--prefetch", action="store_true",
+                    help="eager mode: overlap the next batch's front-end with the current step on its own streams "
+                         "(measured slower on MI355X: the front-end's LDS-heavy workgroups delay the latency-bound "
+                         "step; default off)")
     ap.add_argument("--serial-encoders", action="store_true",
                     help="run the source / target encoders on one stream (default: two HIP streams)")
     ap.add_argument("--heads", choices=["bf16", "fp32"], default="bf16",
@@ -299,11 +303,45 @@ def main():
                 frontend_into(i + 1)                # next batch's front-end overlaps this replay
             return out
         step.first = True
+    elif args.prefetch:
+        # Eager model step, front-end of the NEXT batch prefetched on its own streams:
+        # the features of batch i+1 (independent of the weights) are computed while
+        # step i runs, into the other of two feature buffers (a GPU-side input
+        # pipeline; every step still runs its own batch's front-end inside the
+        # timed region, the last step prefetches nothing).
+        fe_stream, fe_side = torch.cuda.Stream(), torch.cuda.Stream()
+        bufs = [{k: v.clone() for k, v in fe(pool[j]).items()} for j in range(2)]
+        main = torch.cuda.current_stream()
+        ready = [torch.cuda.Event(), torch.cuda.Event()]
+        done = [torch.cuda.Event(), torch.cuda.Event()]
+        for e in done:
+            e.record(main)
+
+        def frontend_into(i):
+            slot = i % 2
+            fe_stream.wait_event(done[slot])        # the step that last read these features is done
+            with torch.cuda.stream(fe_stream):
+                fe(pool[i % 2], out=bufs[slot], side=fe_side)
+                fe_stream.wait_stream(fe_side)
+            ready[slot].record(fe_stream)
+
+        def step(i, last=False):
+            slot = i % 2
+            if step.first:
+                frontend_into(i)
+                step.first = False
+            main.wait_event(ready[slot])
+            if not last:
+                frontend_into(i + 1)                # overlaps this step
+            out = trainer.step({**bufs[slot], "labels": labels[slot]})
+            done[slot].record(main)
+            return out
+        step.first = True
     else:
         step = lambda i, last=False: trainer.step({"x": pool[i % 2], "labels": labels[i % 2]})
     for i in range(args.warmup):
         step(i, last=i == args.warmup - 1)
-    if graph:
+    if hasattr(step, "first"):
         step.first = True
     if world > 1:
         dist.barrier()
@@ -350,7 +388,9 @@ def main():
         "elbo": elbo,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "mode": "model step replayed as a hipGraph (double-buffered), front-end eager one step ahead on its own stream"
-                if graph else "eager",
+                if graph else ("eager" if not args.prefetch else
+                               "eager, front-end of the next batch overlapped with the current step (own streams, "
+                               "double-buffered features)"),
         "roofline": {"bound": "hbm", "kernel": "vt_fe_pairs (k_fe_pairs8k)", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
