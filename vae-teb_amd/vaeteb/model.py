@@ -25,6 +25,7 @@ from . import ops
 # streams.  Every reduction has a fixed order, so results are bit-identical
 # to the serial run (tests/test_gpu_model.py).
 _PAR = {"on": False, "next": 1}
+MAX_SIDE = int(__import__("os").environ.get("VAETEB_MAX_SIDE_STREAMS", "3"))
 _SIDE = {}
 
 
@@ -47,7 +48,10 @@ def fork(*thunks):
     outs = [None] * len(thunks)
     sides = []
     for i, t in enumerate(thunks[1:], 1):
-        st = side_stream(dev, _PAR["next"])  # each fork of a forward pass gets its own side stream
+        # fork k of a forward pass runs on side stream min(k, MAX_SIDE): with HIP's
+        # default 4 hardware queues per process, main + 3 side streams each own a
+        # queue (a 5th stream would share one and serialise behind its work)
+        st = side_stream(dev, min(_PAR["next"], MAX_SIDE))
         _PAR["next"] += 1
         st.wait_stream(main)
         with torch.cuda.stream(st):
