@@ -224,6 +224,9 @@ def main():
                     help="eager mode: overlap the next batch's front-end with the current step on its own streams "
                          "(measured slower on MI355X: the front-end's LDS-heavy workgroups delay the latency-bound "
                          "step; default off)")
+    ap.add_argument("--overlap-update", action="store_true",
+                    help="eager mode: start the next batch's front-end after the backward, overlapping the "
+                         "memory-bound clip + AdamW of the current step")
     ap.add_argument("--serial-encoders", action="store_true",
                     help="run the source / target encoders on one stream (default: two HIP streams)")
     ap.add_argument("--heads", choices=["bf16", "fp32"], default="bf16",
@@ -303,13 +306,16 @@ def main():
                 frontend_into(i + 1)                # next batch's front-end overlaps this replay
             return out
         step.first = True
-    elif args.prefetch:
+    elif args.prefetch or args.overlap_update:
         # Eager model step, front-end of the NEXT batch prefetched on its own streams:
         # the features of batch i+1 (independent of the weights) are computed while
         # step i runs, into the other of two feature buffers (a GPU-side input
         # pipeline; every step still runs its own batch's front-end inside the
         # timed region, the last step prefetches nothing).
-        fe_stream, fe_side = torch.cuda.Stream(), torch.cuda.Stream()
+        # reuse the model's side streams: HIP maps a process's streams onto 4 hardware
+        # queues, and a 5th / 6th stream would share (and serialise behind) one of them
+        from vaeteb.model import side_stream
+        fe_stream, fe_side = side_stream(dev.index or 0, 1), side_stream(dev.index or 0, 2)
         bufs = [{k: v.clone() for k, v in fe(pool[j]).items()} for j in range(2)]
         main = torch.cuda.current_stream()
         ready = [torch.cuda.Event(), torch.cuda.Event()]
@@ -331,9 +337,16 @@ def main():
                 frontend_into(i)
                 step.first = False
             main.wait_event(ready[slot])
-            if not last:
-                frontend_into(i + 1)                # overlaps this step
-            out = trainer.step({**bufs[slot], "labels": labels[slot]})
+            if not last and not args.overlap_update:
+                frontend_into(i + 1)                # overlaps this whole step
+            nxt = None
+            if not last and args.overlap_update:
+                def nxt():                          # overlaps only this step's clip + AdamW
+                    done_bwd = torch.cuda.Event()
+                    done_bwd.record(main)
+                    fe_stream.wait_event(done_bwd)
+                    frontend_into(i + 1)
+            out = trainer.step({**bufs[slot], "labels": labels[slot]}, before_update=nxt)
             done[slot].record(main)
             return out
         step.first = True
@@ -388,9 +401,10 @@ def main():
         "elbo": elbo,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "mode": "model step replayed as a hipGraph (double-buffered), front-end eager one step ahead on its own stream"
-                if graph else ("eager" if not args.prefetch else
-                               "eager, front-end of the next batch overlapped with the current step (own streams, "
-                               "double-buffered features)"),
+                if graph else ("eager, next batch's front-end overlapped with clip + AdamW (own streams, "
+                               "double-buffered features)" if args.overlap_update else
+                               "eager, next batch's front-end overlapped with the whole step" if args.prefetch
+                               else "eager"),
         "roofline": {"bound": "hbm", "kernel": "vt_fe_pairs (k_fe_pairs8k)", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",

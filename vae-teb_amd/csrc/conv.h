@@ -31,6 +31,32 @@ __device__ __forceinline__ float src_val(const float* __restrict__ xb, const Geo
 }
 
 
+// Source row(s) of padded position tp, the per-row part of src_val: false for
+// a zero-padded position; else x row i0 (and i1 with weight l1 when
+// upsampling: value = (1 - l1) x[i0] + l1 x[i1], as src_val).
+__device__ __forceinline__ bool src_row(const Geo& g, int tp, int& i0, int& i1, float& l1) {
+    int t = tp - g.pad;
+    if (g.mode == 0) {
+        if (t < 0 || t >= g.L_up) return false;
+    } else if (g.L_up <= g.pad) {
+        t = t < 0 ? 0 : (t >= g.L_up ? g.L_up - 1 : t);
+    } else {
+        t = t < 0 ? -t : t;
+        t = t >= g.L_up ? 2 * (g.L_up - 1) - t : t;
+    }
+    if (!g.up) {
+        i0 = i1 = t;
+        l1 = 0.f;
+        return true;
+    }
+    float s = (t + 0.5f) * 0.5f - 0.5f;
+    s = s < 0.f ? 0.f : s;
+    i0 = (int)s;
+    i1 = i0 + 1 < g.L_in ? i0 + 1 : g.L_in - 1;
+    l1 = s - (float)i0;
+    return true;
+}
+
 static inline Geo geo(int B, int L_in, int Cin, int Cout, int K, int mode, int up) {
     Geo g;
     g.B = B; g.L_in = L_in; g.Cin = Cin; g.Cout = Cout; g.K = K; g.mode = mode; g.up = up;

@@ -26,6 +26,7 @@ from . import ops
 # to the serial run (tests/test_gpu_model.py).
 _PAR = {"on": False, "next": 1}
 MAX_SIDE = int(__import__("os").environ.get("VAETEB_MAX_SIDE_STREAMS", "3"))
+GRAD_SIDE = int(__import__("os").environ.get("VAETEB_GRAD_SIDE_STREAM", "3"))  # conv weight-gradient stream (measured: 3 < 2 < 1)
 _SIDE = {}
 
 
@@ -425,6 +426,9 @@ class SeqVaeTeb(nn.Module):
     def forward(self, y_st, y_ph, x_ph, eps=None):
         prev = dict(_PAR)
         _PAR["on"], _PAR["next"] = bool(self.concurrent_encoders and x_ph.is_cuda), 1
+        # conv weight gradients of this step's backward go to side stream GRAD_SIDE (off the
+        # data-gradient chain; bit-identical, only their timing moves)
+        ops.GRAD_STREAM = side_stream(torch.cuda.current_device(), GRAD_SIDE) if _PAR["on"] else None
         try:
             return self._forward(y_st, y_ph, x_ph, eps)
         finally:

@@ -56,6 +56,7 @@ def _check(*ts):
 # called instead of the post-accumulate-grad hook (bucketed all-reduce).
 GRAD_READY = None
 SIDE_STREAMS = []   # extra streams the model runs work on (see SeqVaeTeb.concurrent_encoders)
+GRAD_STREAM = None  # side stream for weight gradients off the data-gradient chain (set by SeqVaeTeb)
 
 
 class _ParamGrads:
@@ -443,10 +444,23 @@ class ConvBNActF(torch.autograd.Function):
             call("vt_conv1d_fold", ptr(gpad), B, L, Cin, Cout, K, mode, up, ptr(gx), 0, _st())
         pw = _ParamGrads([w], [ctx.needs_input_grad[1]])
         if pw.out[0] is not None:
-            ws1 = WS.get(WS_LINEAR, x.device, 1)
             fn = "vt_conv1d_bwd_weight_bf16" if bf16 else "vt_conv1d_direct_bwd_weight"
-            call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1), ws1.numel(),
-                 _st())
+            side = GRAD_STREAM if (pw.direct and GRAD_STREAM is not None) else None
+            if side is not None and side != torch.cuda.current_stream():
+                # the weight gradient is off the data-gradient chain: compute it on a
+                # side stream (written in place into the flat gradient buffer, joined
+                # at the end of the backward / before a bucket's all-reduce)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    ws1 = WS.get(WS_LINEAR, x.device, 1)
+                    call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1),
+                         ws1.numel(), _st())
+                gconv.record_stream(side)
+                x.record_stream(side)
+            else:
+                ws1 = WS.get(WS_LINEAR, x.device, 1)
+                call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1),
+                     ws1.numel(), _st())
         gw, = pw.result()
         gg, gb = pbn.result()
         return gx, gw, gg, gb, None, None, None, None, None, None, None, None
@@ -524,6 +538,8 @@ class LSTMF(torch.autograd.Function):
             # b_ih and b_hh receive the same gradient (sum of dg over rows): computed
             # once into a fresh tensor (zeroed when the weights accumulate in place)
             gb = torch.zeros_like(b_ih) if pw.acc else torch.empty_like(b_ih)
+            # (kept on this stream: moving these to the conv weight-gradient side stream
+            # measured slower — it delays the target encoder's phase branch queued there)
             call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), ptr(gb), pw.acc,
                  ptr(ws), ws.numel(), _st())
             call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc, ptr(ws),

@@ -173,11 +173,16 @@ class Trainer:
         return self.model.compute_loss(fw, batch["fhr_st"], batch["fhr_ph"], batch["fhr"], compute_kld_loss=True,
                                        beta=self.beta_kld)
 
-    def step(self, batch, eps=None):
-        """One optimisation step; returns the loss dict (device scalars, no sync)."""
+    def step(self, batch, eps=None, before_update=None):
+        """One optimisation step; returns the loss dict (device scalars, no sync).
+        before_update(): optional host callback between the backward and the
+        clip + AdamW launches (e.g. to enqueue the next batch's front-end on
+        another stream, so it overlaps the memory-bound optimizer)."""
         losses = self._forward_backward(batch, eps, overlap_comm=True)
         if self.buckets:
             self.buckets.finish()
+        if before_update is not None:
+            before_update()
         self._update()
         losses["grad_norm"] = self.norm_out[0]
         return losses
