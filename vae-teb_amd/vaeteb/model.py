@@ -27,6 +27,7 @@ from . import ops
 _PAR = {"on": False, "next": 1}
 MAX_SIDE = int(__import__("os").environ.get("VAETEB_MAX_SIDE_STREAMS", "3"))
 GRAD_SIDE = int(__import__("os").environ.get("VAETEB_GRAD_SIDE_STREAM", "3"))  # conv weight-gradient stream (measured: 3 < 2 < 1)
+LSTM_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_LSTM_GRAD_SIDE_STREAM", "0"))  # 0: inline (side streams measured no faster)
 _SIDE = {}
 
 
@@ -429,6 +430,11 @@ class SeqVaeTeb(nn.Module):
         # conv weight gradients of this step's backward go to side stream GRAD_SIDE (off the
         # data-gradient chain; bit-identical, only their timing moves)
         ops.GRAD_STREAM = side_stream(torch.cuda.current_device(), GRAD_SIDE) if _PAR["on"] else None
+        # the head weight gradients go to side stream 1 (the source encoder's, idle
+        # until the encoders' backward, long after the heads')
+        ops.HEAD_GRAD_STREAM = side_stream(torch.cuda.current_device(), 1) if _PAR["on"] else None
+        ops.LSTM_GRAD_STREAM = (side_stream(torch.cuda.current_device(), LSTM_GRAD_SIDE)
+                                if _PAR["on"] and LSTM_GRAD_SIDE > 0 else None)
         try:
             return self._forward(y_st, y_ph, x_ph, eps)
         finally:

@@ -57,6 +57,8 @@ def _check(*ts):
 GRAD_READY = None
 SIDE_STREAMS = []   # extra streams the model runs work on (see SeqVaeTeb.concurrent_encoders)
 GRAD_STREAM = None  # side stream for weight gradients off the data-gradient chain (set by SeqVaeTeb)
+HEAD_GRAD_STREAM = None  # ... for the bf16-MFMA decoder-head weight gradients (set by SeqVaeTeb)
+LSTM_GRAD_STREAM = None  # ... for the LSTM weight gradients (set by SeqVaeTeb)
 
 
 class _ParamGrads:
@@ -157,8 +159,20 @@ class LinearF(torch.autograd.Function):
         gw_t, gb_t = pg.out
         if gw_t is not None:
             pre = "vt_mfma_" if ctx.mfma else "vt_"
-            call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw_t), ptr(gb_t), pg.acc, ptr(ws),
-                 ws.numel(), _st())
+            side = HEAD_GRAD_STREAM if (ctx.mfma and pg.direct and HEAD_GRAD_STREAM is not None) else None
+            if side is not None and side != torch.cuda.current_stream():
+                # the decoder heads' 4096 x 4096 weight gradients are off the data-gradient
+                # chain: a side stream idle during the decoder backward (in-place sinks)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    ws_s = WS.get(WS_LINEAR, w.device, 1)
+                    call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw_t), ptr(gb_t), pg.acc,
+                         ptr(ws_s), ws_s.numel(), _st())
+                gy2.record_stream(side)
+                x2.record_stream(side)
+            else:
+                call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw_t), ptr(gb_t), pg.acc, ptr(ws),
+                     ws.numel(), _st())
         elif gb_t is not None:
             call("vt_colsum", ptr(gy2), R, N, ptr(gb_t), pg.acc, ptr(ws), ws.numel(), _st())
         gw, gb = pg.result()
@@ -538,12 +552,26 @@ class LSTMF(torch.autograd.Function):
             # b_ih and b_hh receive the same gradient (sum of dg over rows): computed
             # once into a fresh tensor (zeroed when the weights accumulate in place)
             gb = torch.zeros_like(b_ih) if pw.acc else torch.empty_like(b_ih)
-            # (kept on this stream: moving these to the conv weight-gradient side stream
-            # measured slower — it delays the target encoder's phase branch queued there)
-            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), ptr(gb), pw.acc,
-                 ptr(ws), ws.numel(), _st())
-            call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc, ptr(ws),
-                 ws.numel(), _st())
+            side = LSTM_GRAD_STREAM if (pw.direct and LSTM_GRAD_STREAM is not None) else None
+            if side is not None and side != torch.cuda.current_stream():
+                # weight gradients (in-place sinks) off the recurrence chain on a side
+                # stream; the returned bias gradient stays here (same kernels and
+                # summation orders as the serial branch below: bitwise equal)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    ws_s = WS.get(WS_LINEAR, gy.device, 1)
+                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
+                         ptr(ws_s), ws_s.numel(), _st())
+                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
+                         ptr(ws_s), ws_s.numel(), _st())
+                for t in (dg, inp, hp):
+                    t.record_stream(side)
+            else:
+                call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
+                     ptr(ws), ws.numel(), _st())
+                call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
+                     ptr(ws), ws.numel(), _st())
+            call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), 0, ptr(ws), ws.numel(), _st())
             gw_ih, gw_hh = pw.result()
             grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, gb, gb.clone()]
             if l > 0 or ctx.needs_input_grad[0]:
