@@ -73,6 +73,56 @@ __global__ __launch_bounds__(NT) void k_ln_fwd(const float* __restrict__ x, int6
     if (lane == 0 && rstd_out) rstd_out[row] = rstd;
 }
 
+// Wide rows (C >= 1024, the decoder heads' 4096): one workgroup per row, the row
+// held in registers (V4 float4 per thread, one HBM read), block reductions via
+// LDS — the wave-per-row kernel above ran 3 dependent 64-step loops per wave on
+// only R/4 workgroups (74 us for 256 x 4096).
+template <int V4>
+__global__ __launch_bounds__(NT) void k_ln_fwd_wide(const float* __restrict__ x, int C, const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, int act, float eps,
+                                                    float* __restrict__ y, float* __restrict__ xhat,
+                                                    float* __restrict__ rstd_out) {
+    __shared__ float red[16];
+    const int64_t row = blockIdx.x;
+    const float4* xr = reinterpret_cast<const float4*>(x + row * C);
+    const int C4 = C >> 2;
+    float4 v[V4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < V4; ++j) {
+        const int c4 = threadIdx.x + NT * j;
+        v[j] = c4 < C4 ? xr[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    }
+    const float mean = block_sum(s, red) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < V4; ++j) {
+        const int c4 = threadIdx.x + NT * j;
+        if (c4 < C4) {
+            const float a = v[j].x - mean, b = v[j].y - mean, c = v[j].z - mean, d = v[j].w - mean;
+            q += (a * a + b * b) + (c * c + d * d);
+        }
+    }
+    const float rstd = rsqrtf(block_sum(q, red) / (float)C + eps);
+    const float4* g4 = reinterpret_cast<const float4*>(gamma);
+    const float4* b4 = reinterpret_cast<const float4*>(beta);
+    float4* yr = reinterpret_cast<float4*>(y + row * C);
+    float4* hr = xhat ? reinterpret_cast<float4*>(xhat + row * C) : nullptr;
+#pragma unroll
+    for (int j = 0; j < V4; ++j) {
+        const int c4 = threadIdx.x + NT * j;
+        if (c4 >= C4) continue;
+        const float4 h = make_float4((v[j].x - mean) * rstd, (v[j].y - mean) * rstd, (v[j].z - mean) * rstd,
+                                     (v[j].w - mean) * rstd);
+        if (hr) hr[c4] = h;
+        const float4 g = g4[c4], bb = b4[c4];
+        yr[c4] = make_float4(act_f(h.x * g.x + bb.x, act), act_f(h.y * g.y + bb.y, act), act_f(h.z * g.z + bb.z, act),
+                             act_f(h.w * g.w + bb.w, act));
+    }
+    if (threadIdx.x == 0 && rstd_out) rstd_out[row] = rstd;
+}
+
 // ------------------------------------------------------------- LayerNorm bwd
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * act'(z) * gamma.
 // gamma/beta column partials per block: part[block][0:C] = sum dz*xhat,
@@ -485,6 +535,18 @@ int vt_layernorm_fwd(const float* x, int64_t R, int C, const float* gamma, const
             hipLaunchKernelGGL(k_ln_fwd16<8>, grid, dim3(NT), 0, st, x, R, C, gamma, beta, act, eps, y, xhat, rstd);
         else
             hipLaunchKernelGGL(k_ln_fwd16<16>, grid, dim3(NT), 0, st, x, R, C, gamma, beta, act, eps, y, xhat, rstd);
+        VT_LAUNCH_CHECK("vt_layernorm_fwd");
+        return VT_OK;
+    }
+    if (C >= 1024 && C % 4 == 0 && C <= 4 * 4 * NT && ((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma |
+                                                       (uintptr_t)beta | (uintptr_t)xhat) % 16 == 0) {
+        const int v4 = (C / 4 + NT - 1) / NT;
+        hipStream_t st = S(stream);
+#define VT_LNW(V)                                                                                              \
+    if (v4 == V) hipLaunchKernelGGL(k_ln_fwd_wide<V>, dim3((unsigned)R), dim3(NT), 0, st, x, C, gamma, beta, act, eps, \
+                                    y, xhat, rstd);
+        VT_LNW(1) VT_LNW(2) VT_LNW(3) VT_LNW(4)
+#undef VT_LNW
         VT_LAUNCH_CHECK("vt_layernorm_fwd");
         return VT_OK;
     }
