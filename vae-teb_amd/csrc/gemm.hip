@@ -234,9 +234,19 @@ __global__ __launch_bounds__(256) void k_colsum_partial(const float* __restrict_
     if (N <= 256) {
         const int rpi = 256 / N;
         const int c = threadIdx.x % N, ro = threadIdx.x / N;
-        float a = 0.f;
-        if (ro < rpi)
-            for (int64_t r = r0 + ro; r < r1; r += rpi) a += X[r * N + c];
+        // four independent accumulators: four loads in flight per thread
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        if (ro < rpi) {
+            int64_t r = r0 + ro;
+            for (; r + 3 * rpi < r1; r += 4 * rpi) {
+                a0 += X[r * N + c];
+                a1 += X[(r + rpi) * N + c];
+                a2 += X[(r + 2 * rpi) * N + c];
+                a3 += X[(r + 3 * rpi) * N + c];
+            }
+            for (; r < r1; r += rpi) a0 += X[r * N + c];
+        }
+        const float a = (a0 + a1) + (a2 + a3);
         red[threadIdx.x] = a;
         __syncthreads();
         if (threadIdx.x < N) {
@@ -451,8 +461,9 @@ int vt_linear_ln_fwd(const float* X, int64_t R, int K, const float* W, int N, co
 int vt_colsum(const float* X, int64_t R, int N, float* out, int accumulate, float* ws, int64_t ws_floats,
               void* stream) {
     VT_CHECK_ARG(R > 0 && N > 0, "vt_colsum: shape");
-    // narrow N: 256 rows per block; wide N: a thread per column and 32 rows per block
-    const int64_t rows = N <= 256 ? 256 : 32;
+    // narrow N: 64 rows per block (1024 blocks at 65,536 rows); wide N: a thread per
+    // column and 8 rows per block (512 workgroups for the 256 x 4096 head gradients)
+    const int64_t rows = N <= 256 ? 64 : 8;
     int64_t blocks = (R + rows - 1) / rows;
     if (blocks > 1024) blocks = 1024;
     if (blocks * N > ws_floats) blocks = ws_floats / N;

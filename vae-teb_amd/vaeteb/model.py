@@ -11,6 +11,7 @@ widths and the decoder head size R = 16*S are constructor parameters so the
 J=6/Q=1 front-end variant and other sequence lengths work unchanged.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -61,6 +62,58 @@ def fork(*thunks):
         sides.append(st)
     outs[0] = thunks[0]()
     for st in sides:
+        main.wait_stream(st)
+    for o in outs[1:]:
+        for t in (o if isinstance(o, (tuple, list)) else (o,)):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(main)
+    return outs
+
+
+LOCKSTEP = os.environ.get("VAETEB_LOCKSTEP", "1") != "0"
+
+
+def _drain(gen):
+    """Run a stage generator to completion; its return value."""
+    try:
+        while True:
+            next(gen)
+    except StopIteration as e:
+        return e.value
+
+
+def fork_lockstep(*gens):
+    """fork() for stage generators: the branches advance one stage at a time in
+    turn (side branches first), so their autograd nodes are created interleaved.
+    The backward replays nodes in reverse creation order, so it then alternates
+    between the branches and the two streams' backward kernels overlap, instead
+    of one branch's whole backward being enqueued before the other's starts
+    (what a plain fork gives: every node of the later branch outranks every
+    node of the earlier one).  Same kernels on the same streams; serial runs
+    each generator to completion."""
+    if not _PAR["on"]:
+        return [_drain(g) for g in gens]
+    if not LOCKSTEP:   # A/B switch: plain fork() order (each branch whole, side branches first)
+        return fork(*[(lambda g=g: _drain(g)) for g in gens])
+    dev = torch.cuda.current_device()
+    main = torch.cuda.current_stream()
+    streams = [main]
+    for _ in gens[1:]:
+        st = side_stream(dev, min(_PAR["next"], MAX_SIDE))
+        _PAR["next"] += 1
+        st.wait_stream(main)
+        streams.append(st)
+    outs = [None] * len(gens)
+    live = list(range(len(gens) - 1, -1, -1))        # side branches first, as fork()
+    while live:
+        for i in list(live):
+            with torch.cuda.stream(streams[i]):
+                try:
+                    next(gens[i])
+                except StopIteration as e:
+                    outs[i] = e.value
+                    live.remove(i)
+    for st in streams[1:]:
         main.wait_stream(st)
     for o in outs[1:]:
         for t in (o if isinstance(o, (tuple, list)) else (o,)):
@@ -187,6 +240,10 @@ class ResidualMLP(nn.Module):
         return self._spec, params
 
     def forward(self, x):
+        return _drain(self.stages(x))
+
+    def stages(self, x):
+        """forward() as a stage generator (fork_lockstep): one stage per layer."""
         if x.is_cuda and self.fused:
             fs = self._fused_spec()
             if fs is not None:
@@ -194,6 +251,7 @@ class ResidualMLP(nn.Module):
         x0 = self.input_norm(x)
         h = x0
         for (idx, has_ln, act) in self._plan:
+            yield
             lin = self.body[idx]
             if has_ln and not lin.mfma and ops.linear_ln_fused_ok(lin.in_features, lin.out_features):
                 ln = self.body[idx + 1]   # Linear -> LN -> act in one pass (vt_linear_ln_fwd)
@@ -307,9 +365,19 @@ class SourceEncoder(nn.Module):
         self.mu_layer = ResidualMLP(32, geometric_schedule(32, 32, 4), final_activation=False)
 
     def forward(self, x):
-        h = self.conv(self.mlp(x))
+        return _drain(self.stages(x))
+
+    def stages(self, x):
+        """forward() as a stage generator (fork_lockstep)."""
+        h = self.mlp(x)
+        yield
+        h = self.conv(h)
+        yield
         h = self.lstm(self.fused_norm(h))
-        return self.mu_layer(self.pre_output(self.lstm_norm(h)))
+        yield
+        h = self.pre_output(self.lstm_norm(h))
+        yield
+        return self.mu_layer(h)
 
 
 class TargetEncoder(nn.Module):
@@ -332,10 +400,19 @@ class TargetEncoder(nn.Module):
         self.logvar_layer = ResidualMLP(32, geometric_schedule(32, 64, 4), final_activation=False)
 
     def forward(self, y_st, y_ph):
+        return _drain(self.stages(y_st, y_ph))
+
+    def stages(self, y_st, y_ph):
+        """forward() as a stage generator (fork_lockstep)."""
         a, b = fork(lambda: self.scatter_fused_norm(self.conv_scattering(self.mlp_scattering(y_st))),
                     lambda: self.phase_fused_norm(self.conv_phase(self.mlp_phase(y_ph))))
-        h = self.lstm(self.cross_modal_fusion(torch.cat([a, b], dim=-1)))
+        yield
+        h = self.cross_modal_fusion(torch.cat([a, b], dim=-1))
+        yield
+        h = self.lstm(h)
+        yield
         h = self.pre_output(self.lstm_norm(h))
+        yield
         return self.mu_layer(h), torch.clamp(self.logvar_layer(h), -10, 10)
 
 
@@ -388,7 +465,7 @@ class Decoder(nn.Module):
         lin = self.linear(z)                       # (B, S, 87)
         x = self.conv(lin)                         # (B, 16S, 1)
         x = x.reshape(x.shape[0], -1)              # flatten (B, 16S)
-        mu, lv = fork(lambda: self.output_mu(x), lambda: self.output_logvar(x))
+        mu, lv = fork_lockstep(self.output_mu.stages(x), self.output_logvar.stages(x))
         return lin, mu, lv
 
 
@@ -441,8 +518,8 @@ class SeqVaeTeb(nn.Module):
             _PAR.update(prev)
 
     def _forward(self, y_st, y_ph, x_ph, eps):
-        (mu_y, logvar_y_full), mu_x = fork(lambda: self.target_encoder(y_st, y_ph),
-                                           lambda: self.source_encoder(x_ph))
+        (mu_y, logvar_y_full), mu_x = fork_lockstep(self.target_encoder.stages(y_st, y_ph),
+                                                    self.source_encoder.stages(x_ph))
         logvar_y_prior, c_logvar = torch.split(logvar_y_full, self.latent_dim_target, dim=-1)
         mu_c, logvar_post = self.conditional_encoder(mu_x, c_logvar)
         if eps is None:
