@@ -249,7 +249,7 @@ __device__ __forceinline__ float2 accel(float2 a, float p) {
     r = copysignf(r, a.y);
     float v = r * p;
     v -= rintf(v);
-    const float mag = sqrtf(a.x * a.x + a.y * a.y);
+    const float mag = __builtin_amdgcn_sqrtf(a.x * a.x + a.y * a.y);  // v_sqrt_f32 (1 ulp), no IEEE fix-up
     return make_float2(mag * __builtin_amdgcn_cosf(v), mag * __builtin_amdgcn_sinf(v));
 }
 
@@ -261,11 +261,16 @@ constexpr float W32_RE[32] = {1.f, 0.980785251f, 0.923879504f, 0.831469595f, 0.7
                                  -0.195090324f, 0.f, 0.195090324f, 0.382683426f, 0.555570245f, 0.707106769f,
                                  0.831469595f, 0.923879504f, 0.980785251f};
 
+// G: the training geometry (N 4096, reflect pad 2048 each side) with every
+// length and pad index a compile-time constant (no bounds checks, the reflection
+// of each radix-16 column is known per n2); otherwise the runtime arguments.
+template <bool G>
 __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
-    const float2* __restrict__ analytic, int n_slots, int N, int pad_left, int n_pairs,
+    const float2* __restrict__ analytic, int n_slots, int N_, int pad_left_, int n_pairs,
     const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
-    const float2* __restrict__ tw, const float* __restrict__ phi0, int start, int S, int pad_mode,
+    const float2* __restrict__ tw, const float* __restrict__ phi0, int start, int S, int pad_mode_,
     float* __restrict__ out) {
+    const int N = G ? 4096 : N_, pad_left = G ? 2048 : pad_left_, pad_mode = G ? 0 : pad_mode_;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     float2* img = sm;               // PR_IMG
     float2* Z = sm + PR_IMG;        // PR_NB
@@ -303,7 +308,8 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
 #pragma unroll
         for (int n2 = 0; n2 < 16; ++n2) {
             const int i = n1 + 512 * n2 - pad_left;
-            const int s = single ? (i < 0 ? -i : (i >= N ? 2 * N - 2 - i : i)) : pad_src(i, N, pad_mode);
+            const int s = G ? (n2 < 4 ? -i : (n2 < 12 ? i : 2 * N - 2 - i))
+                            : single ? (i < 0 ? -i : (i >= N ? 2 * N - 2 - i : i)) : pad_src(i, N, pad_mode);
             v[q][n2] = s < 0 ? make_float2(0.f, 0.f) : img[s];
         }
     }
@@ -688,7 +694,8 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
     VT_CHECK_ARG(B > 0 && n_pairs > 0 && pad_mode >= 0 && pad_mode <= 2, "vt_fe_pairs: empty/pad_mode");
     if (dec == PR_N / PR_NB && n_pad == PR_N && start + S_out <= PR_NB && N <= PR_IMG) {
         // the training configuration (n_pad 8192, 512 low-pass bins): pruned transform
-        hipLaunchKernelGGL(k_fe_pairs8k, dim3(n_pairs, (unsigned)B), dim3(PR_T),
+        const bool geo = N == 4096 && pad_left == 2048 && pad_mode == 0;
+        hipLaunchKernelGGL(geo ? k_fe_pairs8k<true> : k_fe_pairs8k<false>, dim3(n_pairs, (unsigned)B), dim3(PR_T),
                            (PR_IMG + 2 * PR_NB) * sizeof(float2), S(stream), (const float2*)analytic, n_slots, N,
                            pad_left, n_pairs, slot_i, slot_j, power, (const float2*)tw, phi0, start, S_out, pad_mode,
                            out);
