@@ -24,6 +24,7 @@
 // path's crop-to-n_pad/dec low-pass is NOT Gaussian in time (one-sided
 // spectrum -> slowly decaying imaginary tail), so it stays in the FFT domain.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 #include "fft.h"
@@ -264,7 +265,7 @@ constexpr float W32_RE[32] = {1.f, 0.980785251f, 0.923879504f, 0.831469595f, 0.7
 // G: the training geometry (N 4096, reflect pad 2048 each side) with every
 // length and pad index a compile-time constant (no bounds checks, the reflection
 // of each radix-16 column is known per n2); otherwise the runtime arguments.
-template <bool G>
+template <bool G, bool D = false>
 __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
     const float2* __restrict__ analytic, int n_slots, int N_, int pad_left_, int n_pairs,
     const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
@@ -281,6 +282,29 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
     const float2* ai = analytic + (b * n_slots + slot_i[pair]) * (int64_t)N;
     const float2* aj = analytic + (b * n_slots + slot_j[pair]) * (int64_t)N;
     const float pw = power[pair];
+    if constexpr (D) {
+        // 0+1 fused (training geometry only): column n1 = t of the reflect-padded product
+        // straight from HBM / L2, the product formed in registers (each sample of the
+        // signal is visited twice, once per reflection), first radix-16 pass, no staging
+        static_assert(G && PR_T == 512, "direct columns: training geometry, one column per thread");
+        float2 v[16];
+        {
+            float2 xa[16], xb[16];
+#pragma unroll
+            for (int n2 = 0; n2 < 16; ++n2) {
+                const int i = t + 512 * n2 - 2048;
+                const int s = n2 < 4 ? -i : (n2 < 12 ? i : 2 * 4096 - 2 - i);
+                xa[n2] = ai[s];
+                xb[n2] = aj[s];
+            }
+#pragma unroll
+            for (int n2 = 0; n2 < 16; ++n2) v[n2] = cmul(accel(xa[n2], pw), cconj(xb[n2]));
+        }
+        dft16(v);
+        img[pr_pos(t)] = v[0];
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(t + 512 * k2)] = cmul(v[k2], tw[(t * k2) & (PR_N - 1)]);
+    } else {
     // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283), compact;
     // loads in batches of 8 per thread (all in flight before the first use)
     for (int u0 = t; u0 < N; u0 += PR_T * 8) {
@@ -321,6 +345,7 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
         img[pr_pos(n1)] = v[q][0];
 #pragma unroll
         for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(n1 + 512 * k2)] = cmul(v[q][k2], tw[(n1 * k2) & (PR_N - 1)]);
+    }
     }
     __syncthreads();
     // 2: jobs (k2, n1a): radix-16 over n1b inside block k2, in place
@@ -695,7 +720,11 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
     if (dec == PR_N / PR_NB && n_pad == PR_N && start + S_out <= PR_NB && N <= PR_IMG) {
         // the training configuration (n_pad 8192, 512 low-pass bins): pruned transform
         const bool geo = N == 4096 && pad_left == 2048 && pad_mode == 0;
-        hipLaunchKernelGGL(geo ? k_fe_pairs8k<true> : k_fe_pairs8k<false>, dim3(n_pairs, (unsigned)B), dim3(PR_T),
+        static const bool direct = [] {
+            const char* e = getenv("VAETEB_PAIRS_DIRECT");
+            return e == nullptr || e[0] != '0';
+        }();
+        hipLaunchKernelGGL(geo ? (direct ? k_fe_pairs8k<true, true> : k_fe_pairs8k<true, false>) : k_fe_pairs8k<false>, dim3(n_pairs, (unsigned)B), dim3(PR_T),
                            (PR_IMG + 2 * PR_NB) * sizeof(float2), S(stream), (const float2*)analytic, n_slots, N,
                            pad_left, n_pairs, slot_i, slot_j, power, (const float2*)tw, phi0, start, S_out, pad_mode,
                            out);

@@ -71,6 +71,10 @@ def fork(*thunks):
 
 
 LOCKSTEP = os.environ.get("VAETEB_LOCKSTEP", "1") != "0"
+# which branch creates its autograd nodes first in each lockstep stage: "enc" = the main
+# branch first in the encoder fork only (its side branch's nodes then outrank the main
+# branch's in every stage of the backward), "all" = in every fork, "none" = side first
+LOCKSTEP_MAIN_FIRST = os.environ.get("VAETEB_LOCKSTEP_MAIN_FIRST", "enc")
 
 
 def _drain(gen):
@@ -82,7 +86,7 @@ def _drain(gen):
         return e.value
 
 
-def fork_lockstep(*gens):
+def fork_lockstep(*gens, main_first=False):
     """fork() for stage generators: the branches advance one stage at a time in
     turn (side branches first), so their autograd nodes are created interleaved.
     The backward replays nodes in reverse creation order, so it then alternates
@@ -90,7 +94,9 @@ def fork_lockstep(*gens):
     of one branch's whole backward being enqueued before the other's starts
     (what a plain fork gives: every node of the later branch outranks every
     node of the earlier one).  Same kernels on the same streams; serial runs
-    each generator to completion."""
+    each generator to completion.  main_first: the main branch advances first in every
+    stage, so in the backward the side branch's node of a stage is enqueued first (the
+    side branch's long first-stage backward then overlaps the main branch's tail)."""
     if not _PAR["on"]:
         return [_drain(g) for g in gens]
     if not LOCKSTEP:   # A/B switch: plain fork() order (each branch whole, side branches first)
@@ -105,6 +111,8 @@ def fork_lockstep(*gens):
         streams.append(st)
     outs = [None] * len(gens)
     live = list(range(len(gens) - 1, -1, -1))        # side branches first, as fork()
+    if main_first:
+        live.reverse()
     while live:
         for i in list(live):
             with torch.cuda.stream(streams[i]):
@@ -465,7 +473,8 @@ class Decoder(nn.Module):
         lin = self.linear(z)                       # (B, S, 87)
         x = self.conv(lin)                         # (B, 16S, 1)
         x = x.reshape(x.shape[0], -1)              # flatten (B, 16S)
-        mu, lv = fork_lockstep(self.output_mu.stages(x), self.output_logvar.stages(x))
+        mu, lv = fork_lockstep(self.output_mu.stages(x), self.output_logvar.stages(x),
+                               main_first=LOCKSTEP_MAIN_FIRST == "all")
         return lin, mu, lv
 
 
@@ -519,7 +528,8 @@ class SeqVaeTeb(nn.Module):
 
     def _forward(self, y_st, y_ph, x_ph, eps):
         (mu_y, logvar_y_full), mu_x = fork_lockstep(self.target_encoder.stages(y_st, y_ph),
-                                                    self.source_encoder.stages(x_ph))
+                                                    self.source_encoder.stages(x_ph),
+                                                    main_first=LOCKSTEP_MAIN_FIRST in ("enc", "all"))
         logvar_y_prior, c_logvar = torch.split(logvar_y_full, self.latent_dim_target, dim=-1)
         mu_c, logvar_post = self.conditional_encoder(mu_x, c_logvar)
         if eps is None:
