@@ -76,6 +76,13 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
                 const int* slot_i, const int* slot_j, const float* power, const void* tw, const float* phi0, int dec,
                 int start, int S, int pad_mode, float* out, void* stream);
 
+/* Product staging of vt_fe_pairs on the training geometry (N 4096, n_pad 8192, dec 16):
+ * 0 = the product is formed once per sample into LDS (default), 1 = each thread forms
+ * its padded column straight from HBM/L2 (faster alone, slower when the phase and cross
+ * launches run concurrently).  Initial value from VAETEB_PAIRS_DIRECT; returns the
+ * previous setting (not an error code).  Not thread-safe: set before launching. */
+int vt_fe_set_pairs_direct(int on);
+
 /* Per-channel transform (kind 0 none, 1 log(max(x,0)+log_eps), 2 asinh) and
  * z-score (x-mean)/(std+1e-8); in[b, c, s] (batch stride in_C*S) -> out[b, s, out_off + c]
  * (row width out_C).

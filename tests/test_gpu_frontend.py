@@ -192,3 +192,23 @@ def test_normalised_outputs(fe11):
 def test_wrong_shape_raises(fe11):
     with pytest.raises(ValueError):
         fe11.raw(torch.zeros(2, 1, 4096, device="cuda"))
+
+
+def test_pairs_direct_columns_match_staged(fe11):
+    """vt_fe_set_pairs_direct(1) (padded product columns formed in registers from
+    HBM) against the default LDS-staged product: same per-sample arithmetic and
+    FFT; the compiler contracts the product differently in the two paths, so they
+    agree to fp32 rounding (1e-5 of the batch's largest coefficient), not bitwise."""
+    from vaeteb import _lib, synthetic
+    fns = _lib.lib().fns
+    x = torch.from_numpy(synthetic.batch(901, 4, 4096)).cuda()
+    prev = fns["vt_fe_set_pairs_direct"](0)
+    try:
+        staged = fe11.raw(x)["pairs"].clone()
+        fns["vt_fe_set_pairs_direct"](1)
+        direct = fe11.raw(x)["pairs"].clone()
+    finally:
+        fns["vt_fe_set_pairs_direct"](prev)
+    torch.cuda.synchronize()
+    diff = (staged - direct).abs().max().item()
+    assert diff <= 1e-5 * staged.abs().max().item(), diff

@@ -710,6 +710,23 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
     return VT_OK;
 }
 
+static int g_pairs_direct = -1;  // -1: not yet read from VAETEB_PAIRS_DIRECT
+static int pairs_direct() {
+    if (g_pairs_direct < 0) {
+        const char* e = getenv("VAETEB_PAIRS_DIRECT");
+        g_pairs_direct = e != nullptr && e[0] == '1';
+    }
+    return g_pairs_direct;
+}
+
+// Select the pair kernel's product staging on the training geometry (0: LDS-staged
+// product, the default; 1: direct columns).  Returns the previous setting.
+int vt_fe_set_pairs_direct(int on) {
+    const int prev = pairs_direct();
+    g_pairs_direct = on ? 1 : 0;
+    return prev;
+}
+
 int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
                 const int* slot_i, const int* slot_j, const float* power, const void* tw, const float* phi0, int dec,
                 int start, int S_out, int pad_mode, float* out, void* stream) {
@@ -720,10 +737,10 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
     if (dec == PR_N / PR_NB && n_pad == PR_N && start + S_out <= PR_NB && N <= PR_IMG) {
         // the training configuration (n_pad 8192, 512 low-pass bins): pruned transform
         const bool geo = N == 4096 && pad_left == 2048 && pad_mode == 0;
-        static const bool direct = [] {
-            const char* e = getenv("VAETEB_PAIRS_DIRECT");
-            return e == nullptr || e[0] != '0';
-        }();
+        // direct product columns: faster alone (front-end 2.27 -> 2.10 ms per batch) but
+        // slower in the training step, where the phase and cross launches run concurrently
+        // and the doubled L2 reads compete (1.19 -> 1.32 ms per launch): opt-in
+        const bool direct = pairs_direct() != 0;
         hipLaunchKernelGGL(geo ? (direct ? k_fe_pairs8k<true, true> : k_fe_pairs8k<true, false>) : k_fe_pairs8k<false>, dim3(n_pairs, (unsigned)B), dim3(PR_T),
                            (PR_IMG + 2 * PR_NB) * sizeof(float2), S(stream), (const float2*)analytic, n_slots, N,
                            pad_left, n_pairs, slot_i, slot_j, power, (const float2*)tw, phi0, start, S_out, pad_mode,
