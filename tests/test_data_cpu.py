@@ -73,3 +73,38 @@ def test_deferred_normalisation_keeps_file_layout(files, tmp_path):
     assert ds.is_normalization_enabled() and ds[0].fhr_st.shape == (43, 256)   # (C, S): the GPU transposes
     ds2 = CombinedHDF5Dataset(files, stats_path=str(stats), normalize_on_gpu=False)
     assert ds2[0].fhr_st.shape == (256, 43)
+
+
+def _stats(tmp_path):
+    import os
+    d = dict(np.load(os.path.join(os.path.dirname(__file__), "..", "vae-teb_amd", "vaeteb", "data",
+                                  "stats_j11q4t16_n4096.npz")))
+    p = tmp_path / "stats.npz"
+    np.savez(p, **d)
+    return str(p)
+
+
+def test_fields_not_normalised_on_gpu_are_transposed(files, tmp_path):
+    """A feature field that GpuNormalizer leaves alone (excluded by
+    normalize_fields) still reaches the batch as (S, C), as in the reference
+    (hdf5_dataset.py:758-759 transposes whether or not it normalises)."""
+    from vaeteb.data import CombinedHDF5Dataset
+    ds = CombinedHDF5Dataset(files, stats_path=_stats(tmp_path), normalize_fields={"fhr_st"})
+    s = ds[0]
+    assert s.fhr_st.shape == (43, 256)                 # normalised + transposed on the device
+    assert s.fhr_ph.shape == (256, 44) and s.fhr_up_ph.shape == (256, 130)
+    raw = np.load(files[0])["fhr_ph"][0]
+    assert np.array_equal(s.fhr_ph.numpy(), raw.T)
+
+
+def test_dataset_pickles_and_loads_with_workers(files, tmp_path):
+    """The dataset holds no open handles or locks across pickling, so the
+    default spawn DataLoader workers start (advisor round 1)."""
+    import pickle
+    from vaeteb.data import CombinedHDF5Dataset, create_optimized_dataloader
+    ds = CombinedHDF5Dataset(files, cache_size=4)
+    ds2 = pickle.loads(pickle.dumps(ds))
+    assert len(ds2) == 16 and ds2[5].guid == ds[5].guid
+    dl = create_optimized_dataloader(files, batch_size=4, num_workers=2, load_fields=["guid", "fhr_ph"])
+    got = [b for b in dl]
+    assert sum(len(b.guid) for b in got) == 16 and got[0].fhr_ph.shape == (4, 256, 44)

@@ -1,0 +1,94 @@
+"""Bucketed gradient all-reduce with the side-stream weight gradients
+(concurrent encoders, bf16-MFMA decoder heads whose weight gradients run on a
+side stream): two ranks on one MI355X, gloo over CUDA tensors (RCCL refuses two
+ranks on one device; the stream ordering under test — the collective's stream
+waiting on every stream that wrote the bucket — is the same).  Each rank's
+reduced gradient must equal the sum of both ranks' locally computed gradients
+bit for bit, and the parameters must stay identical across ranks.
+(Advisor round 1: the side streams were snapshotted before the first forward
+created them, so the first step's head-weight buckets raced the reduce.)"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(rank):
+    import numpy as np
+    g = np.load(os.path.join(ROOT, "tests", "golden", "model_s16_b4.npz"), allow_pickle=False)
+    b = {"fhr_st": g["y_st"], "fhr_ph": g["y_ph"], "fhr_up_ph": g["x_ph"], "fhr": g["y_raw"]}
+    b = {k: torch.from_numpy(v.copy()).cuda() for k, v in b.items()}
+    if rank:
+        b = {k: v.flip(0).contiguous() for k, v in b.items()}
+    return b, torch.from_numpy(g["eps"].copy()).cuda()
+
+
+def _model():
+    from golden_util import det_fill_
+    from vaeteb.model import SeqVaeTeb
+    return det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=True, head_precision="bf16",
+                               conv_precision="bf16")).cuda()
+
+
+def _worker(rank, world, port, q):
+    sys.path[:0] = [os.path.join(ROOT, "vae-teb_amd"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vaeteb.train import Trainer
+    batch, eps = _batch(rank)
+    # this rank's own gradient (no collective)
+    loc = Trainer(_model(), lr=1e-3)
+    loc._forward_backward(batch, eps, overlap_comm=False)
+    torch.cuda.synchronize()
+    g_local = loc.state.g.cpu()
+    del loc
+    # a fresh process-group-wide step; small buckets so several fire from the hooks
+    tr = Trainer(_model(), lr=1e-3, world_size=world, bucket_mb=0.5)
+    tr._forward_backward(batch, eps, overlap_comm=True)
+    fired = len(tr.buckets.works)
+    tr.buckets.finish()
+    torch.cuda.synchronize()
+    g_red = tr.state.g.cpu()
+    tr._update()
+    tr.step(batch, eps=eps)
+    torch.cuda.synchronize()
+    q.put((rank, g_local, g_red, tr.state.p.cpu(), fired, len(tr.buckets.buckets)))
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_waits_for_side_stream_gradients():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=150) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = out[0][1] + out[1][1]
+    assert not torch.equal(out[0][1], out[1][1])          # the ranks' local gradients differ
+    for rank in range(world):
+        assert torch.equal(out[rank][2], expect), rank
+    assert out[0][4] > 1 and out[0][5] > 1                # buckets launched from the backward hooks
+    assert torch.equal(out[0][3], out[1][3])

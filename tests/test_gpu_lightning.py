@@ -123,3 +123,22 @@ def test_light_module_fit_step_vs_oracle(batch):
     sd, rsd = model.state_dict(), ref.state_dict()
     worst = max((rel(sd[k], v), k) for k, v in rsd.items() if v.dtype == torch.float32)
     assert worst[0] < 1e-4, worst
+
+
+def test_fit_validation_runs_in_eval_mode(batch):
+    """fit() validates in eval mode (Lightning semantics): BatchNorm running
+    statistics are untouched by validation batches, and training mode is
+    restored afterwards (advisor round 1)."""
+    from vaeteb.lightning import LightSeqVaeTeb, fit
+    from vaeteb.model import SeqVaeTeb
+    model = det_fill_(SeqVaeTeb(sequence_length=16)).cuda()
+    _random_running_stats_(model)
+    before = {k: v.clone() for k, v in model.state_dict().items() if k.endswith(("running_mean", "running_var"))}
+    lm = LightSeqVaeTeb(model, lr=1e-3, beta_schedule="constant", beta_const_val=1e-5)
+    cb = {"fhr_st": batch["y_st"].cuda(), "fhr_ph": batch["y_ph"].cuda(), "fhr_up_ph": batch["x_ph"].cuda(),
+          "fhr": batch["y_raw"].cuda()}
+    logged = fit(lm, [], max_epochs=1, val_loader=[cb])
+    assert "val/total_loss" in logged
+    sd = model.state_dict()
+    assert all(torch.equal(sd[k], v) for k, v in before.items())
+    assert model.training

@@ -299,3 +299,40 @@ def test_graph_replay_bitwise_identical_to_eager(golden, concurrent):
         res.append((outs, tr.state.p.clone(), tr.state.m.clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+def test_graph_capture_bf16_paths_after_eager_steps(golden):
+    """Capture after eager steps (a loss kept from them must not tie the
+    parameters' AccumulateGrad nodes to another stream) with the bf16-MFMA
+    decoder heads and bf16 conv blocks, concurrent encoders: replay == eager
+    bit for bit (advisor round 1: this configuration crashed in
+    hipStreamEndCapture)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb import ops
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    g = golden("model_s16_b4")
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    b0 = {"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}
+    b1 = {k: v.flip(0).contiguous() for k, v in b0.items()}
+    eps = T("eps")
+    assert ops.mfma_ok(256, 256)   # R = 16 S = 256: the heads take the bf16 MFMA path
+    res = []
+    for graph in (False, True):
+        m = det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=True, head_precision="bf16",
+                                conv_precision="bf16")).cuda()
+        tr = Trainer(m, lr=1e-3)
+        kept = tr.step(b0, eps=eps)          # an eager step whose losses stay referenced
+        if graph:
+            tr.capture(b0, eps=eps, warmup=1)
+            outs = [tr.replay(b, eps=eps)["total_loss"].item() for b in (b1, b0, b1)]
+        else:
+            tr.step(b0, eps=eps)
+            outs = [tr.step(b, eps=eps)["total_loss"].item() for b in (b1, b0, b1)]
+        torch.cuda.synchronize()
+        assert kept["total_loss"].grad_fn is None
+        res.append((outs, tr.state.p.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])

@@ -104,8 +104,34 @@ class CombinedHDF5Dataset(Dataset):
         self._cache, self._cache_lock = {}, threading.Lock()
         self.index_map = []
         self._build_index()
+        self._close_stores()   # the reference closes its file after indexing (ref :593-643)
         if not self.index_map:
             raise ValueError("No samples match the specified filters.")
+
+    def _close_stores(self):
+        for i, f in enumerate(self._stores):
+            if f is not None and hasattr(f, "close"):
+                f.close()
+            self._stores[i] = None
+
+    def __getstate__(self):
+        # picklable for DataLoader workers (spawn): no open file handles, locks or cache
+        st = dict(self.__dict__)
+        st["_stores"] = [None] * len(self.paths)
+        st["_locks"] = None
+        st["_cache"], st["_cache_lock"] = {}, None
+        return st
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+        self._locks = [threading.Lock() for _ in self.paths]
+        self._cache_lock = threading.Lock()
+
+    def gpu_normalizes(self, name):
+        """True when `name` is normalised (and transposed) by GpuNormalizer on the
+        device instead of here: the same condition GpuNormalizer applies."""
+        return (self.normalization_enabled and self.normalize_on_gpu and name + "_mean" in self.normalization_stats
+                and (self.normalize_fields is None or name in self.normalize_fields))
 
     def _store(self, i):
         with self._locks[i]:
@@ -175,9 +201,10 @@ class CombinedHDF5Dataset(Dataset):
                 out[name] = bool(data)
             else:
                 t = torch.from_numpy(np.ascontiguousarray(data, dtype=np.float32)).to(self.dtype)
-                if name in FEATURE_FIELDS and t.dim() == 2 and not (self.normalization_enabled and
-                                                                     self.normalize_on_gpu):
-                    t = t.transpose(0, 1).contiguous()   # (C, S) -> (S, C) as the reference returns it
+                if name in FEATURE_FIELDS and t.dim() == 2 and not self.gpu_normalizes(name):
+                    # (C, S) -> (S, C) as the reference returns it (ref :758-759, normalised
+                    # or not); GpuNormalizer transposes the fields it normalises
+                    t = t.transpose(0, 1).contiguous()
                 out[name] = t
         sample = AttributeDict(out)
         if self.cache_size > 0:

@@ -260,7 +260,11 @@ def fit(module, train_loader, max_epochs=1, gradient_clip_val=0.5, val_loader=No
                 sched.step()
             module.global_step += 1
         if val_loader is not None:
+            # Lightning validates in eval mode: BatchNorm uses (and does not update)
+            # its running statistics
+            module.eval()
             for i, batch in enumerate(val_loader):
                 with torch.no_grad():
                     module.validation_step(mv(batch), i)
+            module.train()
     return module.logged

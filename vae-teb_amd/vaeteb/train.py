@@ -89,8 +89,6 @@ class GradBuckets:
         self.pending = [b[2] for b in self.buckets]
         self.works = []
         self.ready = set()
-        from . import ops
-        self.streams = [torch.cuda.current_stream()] + list(ops.SIDE_STREAMS) if torch.cuda.is_available() else []
 
     def reduce_all(self):
         """All buckets at once (after a graph replay of the backward)."""
@@ -107,11 +105,17 @@ class GradBuckets:
         self.pending[b] -= 1
         if self.pending[b] == 0:
             # a bucket's gradients may have been written on several streams (the
-            # concurrent encoders): the collective waits for all of them
-            cur = torch.cuda.current_stream() if self.streams else None
-            for st in self.streams:
-                if st != cur:
-                    cur.wait_stream(st)
+            # concurrent encoders, the side-stream weight gradients): the collective
+            # waits for all of them.  The side streams are read here, not at
+            # reset(): the model creates them lazily during the first forward, and
+            # a head weight gradient queued on one just before this hook must be
+            # covered by the wait
+            if self.state.g.is_cuda:
+                from . import ops
+                cur = torch.cuda.current_stream()
+                for st in ops.SIDE_STREAMS:
+                    if st != cur:
+                        cur.wait_stream(st)
             s, e, _ = self.buckets[b]
             self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
                                               async_op=True))
@@ -191,6 +195,14 @@ class Trainer:
         if not self.model.training:
             self.model.train()
         self.state.zero_grad()
+        if self.state.g.is_cuda:
+            # every side stream joins the step at its start: under hipGraph capture a
+            # stream the step never forked to would otherwise be joined at the end
+            # from outside the capture
+            from . import ops
+            main = torch.cuda.current_stream()
+            for st in ops.SIDE_STREAMS:
+                st.wait_stream(main)
         if self.buckets:
             self.buckets.reset()
             self.buckets.enabled = overlap_comm
@@ -203,7 +215,10 @@ class Trainer:
             main = torch.cuda.current_stream()
             for st in ops.SIDE_STREAMS:
                 main.wait_stream(st)
-        return losses
+        # detached: a returned loss must not keep this step's autograd graph (and
+        # with it the parameters' AccumulateGrad nodes, bound to this step's
+        # stream) alive into the next step or a hipGraph capture
+        return {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in losses.items()}
 
     def _update(self):
         self.steps += 1
