@@ -272,11 +272,6 @@ def main():
     work["vt_fe_pairs"] = lambda an, B, n_slots, N, n_pad, pad_left, n_pairs, *a: B * n_pairs * (2 * N * 8 + a[7] * 4)
     timer = KernelTimer(["vt_fe_pairs", *MFMA_CALLS], flops=work)
     graph = args.graph
-    if graph and (args.heads == "bf16" or args.conv == "bf16"):
-        # measured on MI355X: capturing the step with the bf16 head / conv paths ends in a
-        # crash inside hipStreamEndCapture, and at fp32 the replay is slower than eager
-        # (19.47 vs 17.65 ms per step): the eager step is the measured path
-        raise SystemExit("bench.py --graph: only with --heads fp32 --conv fp32 (see DESIGN.md §9)")
     if graph:
         # The model step (forward, backward, clip, AdamW) is replayed as a
         # hipGraph.  The front-end (~10 launches, independent of the weights)

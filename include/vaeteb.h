@@ -224,6 +224,26 @@ int vt_resmlp_bwd(int n_layers, const int* dims, const int* layer_ln, const int*
                   const float* const* params, const float* dout, const float* xhat, const float* rstd, int64_t rows,
                   float* dx, float* const* grads, int accumulate, float* ws, int64_t ws_floats, void* stream);
 
+/* ------------------------------------------- whole ResidualMLP, bf16 MFMA
+ * The same ResidualMLP (ref/model/vae_teb_model.py:336-403, same arguments and
+ * parameter / gradient layout as vt_resmlp_*) with every Linear on bf16 MFMA
+ * (v_mfma_f32_16x16x32_bf16, fp32 accumulation) — the reference trains under
+ * 16-bit autocast (ref/model/graph_model.py:510, :709-711): Linear in 16 bit,
+ * LayerNorm, activations, the saved state and every reduction in fp32.  The
+ * saved xhat / rstd (sizes[0], sizes[1] floats) use this family's own layout
+ * (pass them only to vt_resmlp_bf16_bwd); the backward needs sizes[2] floats of
+ * workspace.  Widths <= VT_MLP_MAX_WIDTH, the weights must fit the LDS budget
+ * (VT_ERR_ARG otherwise).                                                       */
+int vt_resmlp_bf16_sizes(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                         int64_t rows, int64_t* sizes);
+int vt_resmlp_bf16_fwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                       const float* const* params, const float* x, int64_t rows, float* out, float* xhat, float* rstd,
+                       void* stream);
+int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                       const float* const* params, const float* dout, const float* xhat, const float* rstd,
+                       int64_t rows, float* dx, float* const* grads, int accumulate, float* ws, int64_t ws_floats,
+                       void* stream);
+
 /* ------------------------------------------------------- bf16 MFMA (heads)
  * The decoder's R x R output heads (Decoder.output_mu / output_logvar,
  * ref/model/vae_teb_model.py:882-897,926-927, R = 16*S; the reference runs

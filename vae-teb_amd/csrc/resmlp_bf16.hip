@@ -1,0 +1,1012 @@
+// Whole-ResidualMLP kernels on bf16 MFMA (ref/model/vae_teb_model.py:336-403),
+// the 16-bit-autocast counterpart of resmlp.hip (the reference trains under
+// fp16 autocast, ref/model/graph_model.py:510,709-711: Linear in 16-bit, LayerNorm
+// in fp32).  Linear layers multiply bf16 operands with fp32 accumulation
+// (v_mfma_f32_16x16x32_bf16); LayerNorm, activations, the saved state and every
+// reduction stay fp32.
+//
+// Orientation.  Every activation tile is kept TRANSPOSED: a wave owns 16 rows,
+// lane (g = lane>>4, r = lane&15) holds row r, features 16t + 4g + i (i < 4) in
+// a[t][i] — exactly the accumulator (D) layout of Z^T = W H^T.  So the D tile of
+// one layer is, after a pairwise bf16 conversion, the B operand of the next
+// (k-step s of 32 features = {a[2s][0..3], a[2s+1][0..3]}, no lane movement);
+// the A operand (weights) is staged in LDS with the matching permutation of its
+// k index inside each 32-block:  image[n][32s + 8g + j] = W[n][32s + 16(j>>2) + 4g + (j&3)].
+// LayerNorm statistics of a row are a register sum + two cross-group shuffles.
+//
+// k_mlpb_fwd  1 workgroup per CU (8 waves), every layer's weight image resident
+//             in LDS (staged once), waves independent over 16-row tiles.  Saves
+//             xhat feature-major (xh[f][row], 64-B row segments) and rstd.
+// k_mlpb_bwd  layer-major over a 256-row block per workgroup (wave w owns rows
+//             128u + 16w + r, u = 0, 1): per GEMM, LayerNorm backward in
+//             registers -> dZ; dZ^T and H^T (recomputed from xhat) go to LDS
+//             images, dW|db = dZ^T H over the block on MFMA (rows as the
+//             contraction); dH_prev = W^T dZ with dZ as the B operand.  One
+//             dW|db + gamma|beta partial per workgroup.
+// k_mlpb_sum  fixed-order sum of the partials into the parameter gradients.
+// No atomics: bitwise reproducible run to run.
+#include <math.h>
+#include <string.h>
+
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+
+namespace vt {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int MAXL = VT_MLP_MAX_LAYERS;
+constexpr int MAXG = MAXL + 1;   // layers + skip projection
+constexpr int BT = 512;          // threads per workgroup (8 waves)
+constexpr int NW = BT / 64;
+constexpr int IMR = 128;         // rows of one dZ / H image (half a block)
+constexpr int IMS = IMR + 16;    // image row stride (bf16): == 16 mod 32 -> conflict-free fragment reads
+
+struct BG {                      // one GEMM: z = h W^T + b, W [N][K]
+    int K, N;
+    int fo, fs;                  // forward image (bf16 offset, row stride): rows pad16(N), cols pad32(K)
+    int bw, bs;                  // backward image W^T: bf16 element count, row stride: rows pad16(K), cols pad32(N)
+    int po;                      // fp32 params in LDS: bias[pad16 N], gamma, beta
+    int wo;                      // dW|db partial offset (floats), N x (K + 1)
+    const float* W;
+    const float* b;
+};
+struct BL {                      // LayerNorm (+ act) after GEMM l
+    int ln, act, xo, ri, lpo, bpo;   // xo: saved-xhat region (x Rp floats); bpo: backward LDS params
+    const float* g;
+    const float* be;
+};
+struct BDesc {
+    int L, d0, skip, nG;
+    float eps;
+    int fimg;                    // forward: bytes of all weight images (params follow)
+    int fbytes;                  // forward LDS bytes
+    int pin;                     // LDS float offset of the input LN gamma / beta (pad16 d0 each)
+    int bwimg;                   // backward: bf16 elements of the largest W^T image
+    int bhrows;                  // backward: rows of the H image (max pad16(K))
+    int bzrows;                  // backward: rows of the dZ image (max pad16(N))
+    int bprm;                    // backward: floats of LN parameters in LDS
+    int bbytes;                  // backward LDS bytes
+    int P;                       // partial floats per workgroup
+    int lpo0;                    // LN partial offset of the input LN
+    int bpin;                    // backward LDS float offset of the input LN gamma / beta
+    const float* g0;
+    const float* be0;
+    BG G[MAXG];
+    BL l[MAXL];
+};
+
+__device__ __forceinline__ int p16(int n) { return (n + 15) & ~15; }
+__device__ __forceinline__ int p32(int n) { return (n + 31) & ~31; }
+
+__device__ __forceinline__ float bact(float z, int act) {
+    switch (act) {
+        case 1: return z > 0.f ? z : 0.f;
+        case 2: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+        case 3: return tanhf(z);
+        default: return z;
+    }
+}
+
+__device__ __forceinline__ float bact_d(float z, int act) {
+    switch (act) {
+        case 1: return z > 0.f ? 1.f : 0.f;
+        case 2: {
+            const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+            const float pdf = 0.39894228040143268f * expf(-0.5f * z * z);
+            return cdf + z * pdf;
+        }
+        case 3: {
+            const float t = tanhf(z);
+            return 1.f - t * t;
+        }
+        default: return 1.f;
+    }
+}
+
+// k position p (0..31) of a 32-block -> feature offset inside the block
+__device__ __forceinline__ int kperm(int p) {
+    const int g = p >> 3, j = p & 7;
+    return 16 * (j >> 2) + 4 * g + (j & 3);
+}
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// act over a whole tile (one uniform switch, not one per element)
+template <int NT>
+__device__ __forceinline__ void act_tile(f32x4 (&z)[NT], int act) {
+    switch (act) {
+        case 1:
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) z[t][i] = fmaxf(z[t][i], 0.f);
+            break;
+        case 2:
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) z[t][i] = bact(z[t][i], 2);
+            break;
+        case 3:
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) z[t][i] = tanhf(z[t][i]);
+            break;
+        default:
+            break;
+    }
+}
+
+// act'(z) over a whole tile
+template <int NT>
+__device__ __forceinline__ void actd_tile(f32x4 (&z)[NT], int act) {
+    switch (act) {
+        case 1:
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) z[t][i] = z[t][i] > 0.f ? 1.f : 0.f;
+            break;
+        case 2:
+        case 3:
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) z[t][i] = bact_d(z[t][i], act);
+            break;
+        default:
+#pragma unroll
+            for (int t = 0; t < NT; ++t) z[t] = f32x4{1.f, 1.f, 1.f, 1.f};
+            break;
+    }
+}
+
+// B fragments of a transposed activation tile (k-step s = features 32s..32s+31)
+template <int NT>
+__device__ __forceinline__ void frags(const f32x4 (&a)[NT], bf16x8 (&b)[(NT + 1) / 2]) {
+#pragma unroll
+    for (int s = 0; s < (NT + 1) / 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            b[s][j] = (__bf16)a[2 * s][j];
+            b[s][4 + j] = (2 * s + 1 < NT) ? (__bf16)a[2 * s + 1][j] : (__bf16)0.f;
+        }
+    }
+}
+
+// acc[t] = sum_s (image rows 16t..16t+15) x b[s];  nt output tiles, ks k-steps (runtime, <= template bounds)
+template <int NT, int KS>
+__device__ __forceinline__ void tile_gemm(const __bf16* img, int stride, int nt, int ks, const bf16x8 (&b)[KS],
+                                          f32x4 (&acc)[NT]) {
+    const int lane = threadIdx.x & 63;
+    const __bf16* p = img + (lane & 15) * stride + 8 * (lane >> 4);
+    const int step = 16 * stride;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (t < nt) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                if (s < ks) c = mfma(*(const bf16x8*)(p + 32 * s), b[s], c);
+        }
+        acc[t] = c;
+        p += step;
+    }
+}
+
+// row-major [rows][C] tile (any C) -> transposed layout (0 past C / for invalid rows)
+template <int NT>
+__device__ __forceinline__ void load_rows(f32x4 (&a)[NT], const float* __restrict__ src, int C, int64_t row, bool rok) {
+    const int g4 = (threadIdx.x & 63) >> 4;
+    const float* p = src + (rok ? row : 0) * (int64_t)C + 4 * g4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float v = 0.f;
+            if (rok && 16 * t + 4 * g4 + i < C) v = p[16 * t + i];
+            a[t][i] = v;
+        }
+}
+
+template <int NT>
+__device__ __forceinline__ void store_rows(float* __restrict__ dst, const f32x4 (&a)[NT], int C, int64_t row, bool rok) {
+    const int g4 = (threadIdx.x & 63) >> 4;
+    if (!rok) return;
+    float* p = dst + row * (int64_t)C + 4 * g4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (16 * t + 4 * g4 + i < C) p[16 * t + i] = a[t][i];
+}
+
+// saved state, row-major with the row padded to 16 (float4 per lane and tile)
+template <int NT>
+__device__ __forceinline__ void load_sv(f32x4 (&a)[NT], const float* __restrict__ src, int C, int64_t row, bool rok) {
+    const int g4 = (threadIdx.x & 63) >> 4;
+    const int nt = (C + 15) >> 4;
+    const f32x4* p = reinterpret_cast<const f32x4*>(src + row * (int64_t)(16 * nt) + 4 * g4);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (rok && t < nt) v = p[4 * t];
+        a[t] = v;
+    }
+}
+
+__device__ __forceinline__ float sum_groups(float v) {  // over the 4 lane groups (same row)
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+// LayerNorm (+ act) of a transposed tile, fp32: saves xhat (row-major, rows
+// padded to 16 features; 0 in the padding) and rstd; z is 0 past C on entry;
+// leaves h (0 past C).
+template <int NT>
+__device__ __forceinline__ void ln_fwd(f32x4 (&z)[NT], int C, const float* gl, const float* bl, int act, float eps,
+                                       float* __restrict__ xh, float* __restrict__ rs, int64_t row, bool rok) {
+    const int lane = threadIdx.x & 63, g4 = lane >> 4;
+    const int nt = (C + 15) >> 4;
+    const float invC = 1.f / (float)C;
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+        if (t < nt) s += (z[t][0] + z[t][1]) + (z[t][2] + z[t][3]);
+    const float mean = sum_groups(s) * invC;
+    float v = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float dlt = (16 * t + 4 * g4 + i < C) ? z[t][i] - mean : 0.f;
+            z[t][i] = dlt;
+            v += dlt * dlt;
+        }
+    const float rstd = rsqrtf(sum_groups(v) * invC + eps);
+    if (rok && g4 == 0) rs[row] = rstd;
+    f32x4* px = reinterpret_cast<f32x4*>(xh + row * (int64_t)(16 * nt) + 4 * g4);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        if (t >= nt) continue;
+        z[t] *= rstd;                                   // xhat (0 past C)
+        if (rok) px[4 * t] = z[t];
+        const f32x4 gv = *(const f32x4*)(gl + 16 * t + 4 * g4);
+        const f32x4 bv = *(const f32x4*)(bl + 16 * t + 4 * g4);
+        z[t] = z[t] * gv + bv;                          // gamma / beta are 0 past C
+    }
+    act_tile<NT>(z, act);
+}
+
+// ------------------------------------------------------------------ forward
+__device__ void stage_fwd(const BDesc& d, __bf16* img, float* prm) {
+    for (int g = 0; g < d.nG; ++g) {
+        const BG& G = d.G[g];
+        const int Np = p16(G.N), Kp = p32(G.K);
+        __bf16* dst = img + G.fo;
+        for (int idx = threadIdx.x; idx < Np * Kp; idx += BT) {
+            const int n = idx / Kp, p = idx - n * Kp;
+            const int k = (p & ~31) + kperm(p & 31);
+            const float v = (n < G.N && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f;
+            dst[n * G.fs + p] = (__bf16)v;
+        }
+        const bool lnl = g < d.L && d.l[g].ln;
+        for (int c = threadIdx.x; c < 3 * Np; c += BT) {
+            const int w = c / Np, f = c - w * Np;
+            const float* src = w == 0 ? G.b : (lnl ? (w == 1 ? d.l[g].g : d.l[g].be) : nullptr);
+            prm[G.po + c] = (src && f < G.N) ? src[f] : 0.f;
+        }
+    }
+    const int d0p = p16(d.d0);
+    for (int c = threadIdx.x; c < 2 * d0p; c += BT) {
+        const int w = c / d0p, f = c - w * d0p;
+        prm[d.pin + c] = f < d.d0 ? (w == 0 ? d.g0 : d.be0)[f] : 0.f;
+    }
+}
+
+// ID: identity skip (out += x0); otherwise skip 0 / 2 (projection of x0 at the end)
+template <int NT, bool ID>
+__global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp, const float* __restrict__ X, int64_t R,
+                                                    float* __restrict__ out, float* __restrict__ xh,
+                                                    float* __restrict__ rs, int64_t Rp) {
+    const BDesc& d = *dp;   // device-resident (uniform scalar loads; a by-value descriptor indexed
+                            // by layer is copied to scratch)
+    constexpr int KS = (NT + 1) / 2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const __bf16* img = reinterpret_cast<const __bf16*>(smem);
+    float* prm = reinterpret_cast<float*>(smem + d.fimg);
+    stage_fwd(d, reinterpret_cast<__bf16*>(smem), prm);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4, lr = lane & 15;
+    const int L = d.L, d0 = d.d0, DL = d.G[L - 1].N;
+    const int64_t ntiles = (R + 15) / 16;
+    for (int64_t tile = (int64_t)blockIdx.x * NW + wv; tile < ntiles; tile += (int64_t)gridDim.x * NW) {
+        const int64_t row = tile * 16 + lr;
+        const bool rok = row < R;
+        f32x4 a[NT];
+        load_rows<NT>(a, X, d0, row, rok);
+        ln_fwd<NT>(a, d0, prm + d.pin, prm + d.pin + p16(d0), 0, d.eps, xh, rs, row, rok);
+        f32x4 x0[ID ? NT : 1];
+        if constexpr (ID) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) x0[t] = a[t];
+        }
+        bf16x8 bx[KS], b[KS];
+        frags<NT>(a, bx);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) b[s] = bx[s];
+        for (int l = 0; l < L; ++l) {
+            const int K = d.G[l].K, N = d.G[l].N, fo = d.G[l].fo, fs = d.G[l].fs, po = d.G[l].po;
+            tile_gemm<NT, KS>(img + fo, fs, (N + 15) >> 4, (K + 31) >> 5, b, a);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) a[t] += *(const f32x4*)(prm + po + 16 * t + 4 * g4);   // bias (0 past N)
+            if (d.l[l].ln)
+                ln_fwd<NT>(a, N, prm + po + p16(N), prm + po + 2 * p16(N), d.l[l].act, d.eps,
+                           xh + (int64_t)d.l[l].xo * Rp, rs + (int64_t)d.l[l].ri * Rp, row, rok);
+            if (l < L - 1) frags<NT>(a, b);
+        }
+        if constexpr (ID) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) a[t] += x0[t];
+        } else if (d.skip == 2) {
+            const BG& G = d.G[L];
+            f32x4 sk[NT];
+            tile_gemm<NT, KS>(img + G.fo, G.fs, (G.N + 15) >> 4, (G.K + 31) >> 5, bx, sk);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) a[t] += sk[t] + *(const f32x4*)(prm + G.po + 16 * t + 4 * g4);
+        }
+        store_rows<NT>(out, a, DL, row, rok);
+    }
+}
+
+// ----------------------------------------------------------------- backward
+// W^T image of GEMM G: img[k][32s + 8g + j] = W[32s + kperm(8g + j)][k]
+__device__ void stage_wt(const BG& G, __bf16* img) {
+    const int Kp = p16(G.K), Np = p32(G.N);
+    for (int idx = threadIdx.x; idx < Kp * Np; idx += BT) {
+        const int p = idx / Kp, k = idx - p * Kp;   // consecutive threads: consecutive k (coalesced W rows)
+        const int n = (p & ~31) + kperm(p & 31);
+        const float v = (n < G.N && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f;
+        img[k * G.bs + p] = (__bf16)v;
+    }
+}
+
+// LayerNorm(+act) backward of a transposed tile (fp32): dh -> dz in place
+// (xv = xhat, 0 past C and for invalid rows; rstd 0 for invalid rows); adds the
+// tile's gamma / beta column sums (over its 16 rows) to la[t]: lane (g, r)
+// accumulates value v = r >> 1 of feature block 16t + 4g: v < 4 -> dgamma of
+// feature 16t + 4g + v, else dbeta of feature 16t + 4g + v - 4.
+template <int NT>
+__device__ __forceinline__ void ln_bwd(f32x4 (&dh)[NT], const f32x4 (&xv)[NT], float rstd, int C, const float* gl,
+                                       const float* bl, int act, float (&la)[NT]) {
+    const int lane = threadIdx.x & 63, g4 = lane >> 4, lr = lane & 15;
+    const int nt = (C + 15) >> 4;
+    const float invC = 1.f / (float)C;
+    if (act) {
+        f32x4 pre[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            pre[t] = xv[t] * *(const f32x4*)(gl + 16 * t + 4 * g4) + *(const f32x4*)(bl + 16 * t + 4 * g4);
+        actd_tile<NT>(pre, act);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) dh[t] *= pre[t];   // du (dh is 0 past C)
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        if (t >= nt) continue;
+        const f32x4 gv = *(const f32x4*)(gl + 16 * t + 4 * g4);
+        float pq[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float du = dh[t][i];
+            pq[i] = du * xv[t][i];
+            pq[4 + i] = du;
+            const float gd = du * gv[i];
+            dh[t][i] = gd;
+            s1 += gd;
+            s2 += gd * xv[t][i];
+        }
+        // reduce-scatter of the 8 column values over the 16 rows of the group
+        float q4[4], q2[2];
+        const bool h8 = lr & 8, h4 = lr & 4, h2 = lr & 2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q4[i] = (h8 ? pq[4 + i] : pq[i]) + __shfl_xor(h8 ? pq[i] : pq[4 + i], 8);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) q2[i] = (h4 ? q4[2 + i] : q4[i]) + __shfl_xor(h4 ? q4[i] : q4[2 + i], 4);
+        float q = (h2 ? q2[1] : q2[0]) + __shfl_xor(h2 ? q2[0] : q2[1], 2);
+        q += __shfl_xor(q, 1);
+        la[t] += q;
+    }
+    const float m1 = sum_groups(s1) * invC, m2 = sum_groups(s2) * invC;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool ok = 16 * t + 4 * g4 + i < C;
+            dh[t][i] = ok ? rstd * (dh[t][i] - m1 - xv[t][i] * m2) : 0.f;
+        }
+}
+
+// transposed tile -> bf16 image rows [f][col0 + r] for the tiles covering C
+template <int NT>
+__device__ __forceinline__ void put_img(__bf16* im, const f32x4 (&a)[NT], int C, int col0) {
+    const int lane = threadIdx.x & 63, g4 = lane >> 4, lr = lane & 15;
+    const int nt = (C + 15) >> 4;
+    __bf16* p = im + 4 * g4 * IMS + col0 + lr;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        if (t >= nt) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[(16 * t + i) * IMS] = (__bf16)a[t][i];
+    }
+}
+
+// column sums of a transposed tile over its 16 rows (fp32), added to lb[t]:
+// after the reduce-scatter lane (g, r) holds feature 16t + 4g + (r >> 2)
+template <int NT>
+__device__ __forceinline__ void colsum(const f32x4 (&z)[NT], int C, float (&lb)[NT]) {
+    const int lr = threadIdx.x & 15;
+    const int nt = (C + 15) >> 4;
+    const bool h8 = lr & 8, h4 = lr & 4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        if (t >= nt) continue;
+        float w[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) w[i] = (h8 ? z[t][2 + i] : z[t][i]) + __shfl_xor(h8 ? z[t][i] : z[t][2 + i], 8);
+        float q = (h4 ? w[1] : w[0]) + __shfl_xor(h4 ? w[0] : w[1], 4);
+        q += __shfl_xor(q, 2);
+        q += __shfl_xor(q, 1);
+        lb[t] += q;
+    }
+}
+
+// workgroup partials of the column sums, fixed-order sum over the waves:
+// LayerNorm gamma | beta (la, if ln) -> dln[0 .. 2C); bias (lb, if db) -> db[f * dbs]
+template <int NT>
+__device__ __forceinline__ void flush_cols(float* red, const float (&la)[NT], const float (&lb)[NT], int C, bool ln,
+                                           float* __restrict__ dln, float* __restrict__ db, int dbs) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4, lr = lane & 15;
+    const int nt = (C + 15) >> 4;
+    float* rw = red + wv * (48 * NT);
+    if (ln && !(lr & 1)) {
+        const int v = lr >> 1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            if (t < nt) rw[t * 32 + (v >> 2) * 16 + 4 * g4 + (v & 3)] = la[t];
+    }
+    if (db && !(lr & 3)) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            if (t < nt) rw[32 * NT + t * 16 + 4 * g4 + (lr >> 2)] = lb[t];
+    }
+    __syncthreads();
+    if (ln) {
+        for (int idx = threadIdx.x; idx < nt * 32; idx += BT) {
+            const int t = idx >> 5, which = (idx >> 4) & 1, f = 16 * t + (idx & 15);
+            float s = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) s += red[w * (48 * NT) + idx];
+            if (f < C) dln[which * C + f] = s;
+        }
+    }
+    if (db) {
+        for (int f = threadIdx.x; f < C; f += BT) {
+            float s = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) s += red[w * (48 * NT) + 32 * NT + f];
+            db[(int64_t)f * dbs] = s;
+        }
+    }
+}
+
+// dW|db partial of one GEMM over the images of IMR rows, accumulated in acc:
+// wave (wn = w >> 2, wk = w & 3) owns output tiles tn = wn + 2a, tk = wk + 4c
+template <int TNS, int TKS>
+__device__ __forceinline__ void dw_half(const __bf16* zi, const __bf16* hi, int ntn, int ntk, f32x4 (&acc)[TNS][TKS]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wn = wv >> 2, wk = wv & 3;
+    const int off = (lane & 15) * IMS + 8 * (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < IMR / 32; ++s) {
+        bf16x8 bf[TKS];
+#pragma unroll
+        for (int c = 0; c < TKS; ++c) {
+            const int tk = wk + 4 * c;
+            if (tk < ntk) bf[c] = *(const bf16x8*)(hi + 16 * tk * IMS + off + 32 * s);
+        }
+#pragma unroll
+        for (int a = 0; a < TNS; ++a) {
+            const int tn = wn + 2 * a;
+            if (tn >= ntn) continue;
+            const bf16x8 af = *(const bf16x8*)(zi + 16 * tn * IMS + off + 32 * s);
+#pragma unroll
+            for (int c = 0; c < TKS; ++c)
+                if (wk + 4 * c < ntk) acc[a][c] = mfma(af, bf[c], acc[a][c]);
+        }
+    }
+}
+
+// TPW: 16-row tiles per wave (the workgroup's block is 128 TPW rows)
+template <int NT, int TPW>
+__global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp, const float* __restrict__ dout,
+                                                    const float* __restrict__ xh, const float* __restrict__ rs,
+                                                    int64_t R, int64_t Rp, float* __restrict__ dx,
+                                                    float* __restrict__ part) {
+    const BDesc& d = *dp;
+    constexpr int KS = (NT + 1) / 2;
+    constexpr int TNS = (NT + 1) / 2;          // dW output tiles per wave along n
+    constexpr int TKS = (NT + 3) / 4;          // ... along k
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __bf16* wimg = reinterpret_cast<__bf16*>(smem);
+    __bf16* zimg = wimg + d.bwimg;
+    __bf16* himg = zimg + d.bzrows * IMS;
+    float* prm = reinterpret_cast<float*>(himg + d.bhrows * IMS);   // [LN params per LN layer][input LN]
+    float* red = prm + d.bprm;                                      // [NW][48 NT]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4, lr = lane & 15;
+    const int L = d.L, d0 = d.d0, DL = d.G[L - 1].N;
+    const int64_t rbase = (int64_t)blockIdx.x * (IMR * TPW) + 16 * wv + lr;
+    float* pb = part + (int64_t)blockIdx.x * d.P;
+
+    // gamma / beta of every LayerNorm (+ the input LN), staged once; layer l's at prm + l.lpo... (lnp offsets)
+    for (int l = 0; l <= L; ++l) {
+        const bool inl = l == L;
+        if (!inl && !d.l[l].ln) continue;
+        const int C = inl ? d0 : d.G[l].N, Np = p16(C), o = inl ? d.bpin : d.l[l].bpo;
+        const float* g = inl ? d.g0 : d.l[l].g;
+        const float* be = inl ? d.be0 : d.l[l].be;
+        for (int c = threadIdx.x; c < 2 * Np; c += BT) {
+            const int w = c / Np, f = c - w * Np;
+            prm[o + c] = f < C ? (w == 0 ? g : be)[f] : 0.f;
+        }
+    }
+    const float* prm_in = prm + d.bpin;
+
+    f32x4 dh[TPW][NT];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int64_t row = rbase + IMR * u;
+        load_rows<NT>(dh[u], dout, DL, row, row < R);
+    }
+
+    // GEMM steps: layers L-1 .. 0, then the skip projection (G[L])
+    const int nsteps = L + (d.skip == 2 ? 1 : 0);
+    for (int step = 0; step < nsteps; ++step) {
+        const bool skp = step == L;
+        const int l = skp ? -1 : L - 1 - step;
+        const BG& G = d.G[skp ? L : l];
+        const int N = G.N, K = G.K, bs = G.bs;
+        const bool ln = !skp && d.l[l].ln;
+        const int hsrc = skp ? -1 : l - 1;    // H = output of layer hsrc (-1: x0, the input LN output)
+        const float* gH = hsrc >= 0 ? prm + d.l[hsrc].bpo : prm_in;
+        const int CH = hsrc >= 0 ? d.G[hsrc].N : d0, actH = hsrc >= 0 ? d.l[hsrc].act : 0;
+        const float* xH = xh + (hsrc >= 0 ? (int64_t)d.l[hsrc].xo * Rp : 0);
+        __syncthreads();                      // previous step done with the W^T / dZ / H images and red
+        stage_wt(G, wimg);
+        float la[NT], lb[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
+        const int ntn = (N + 15) >> 4, ntk = (K + 15) >> 4;
+        f32x4 acc[TNS][TKS];
+#pragma unroll
+        for (int a = 0; a < TNS; ++a)
+#pragma unroll
+            for (int c = 0; c < TKS; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int64_t row = rbase + IMR * u;
+            const bool rok = row < R;
+            f32x4 dz[NT];
+            if (skp) {
+                load_rows<NT>(dz, dout, DL, row, rok);
+            } else {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) dz[t] = dh[u][t];
+                if (ln) {
+                    f32x4 xv[NT];
+                    load_sv<NT>(xv, xh + (int64_t)d.l[l].xo * Rp, N, row, rok);
+                    const float rstd = rok ? rs[(int64_t)d.l[l].ri * Rp + row] : 0.f;
+                    const float* gl = prm + d.l[l].bpo;
+                    ln_bwd<NT>(dz, xv, rstd, N, gl, gl + p16(N), d.l[l].act, la);
+                }
+            }
+            colsum<NT>(dz, N, lb);            // the bias gradient: fp32 sum of dZ (not of its bf16 image)
+            if (u > 0) __syncthreads();       // the dW MFMAs of the previous half are done with the images
+            put_img<NT>(zimg, dz, N, 16 * wv);
+            {
+                // H = act(xhat_hsrc * gamma + beta) (the GEMM's input)
+                f32x4 hv[NT];
+                load_sv<NT>(hv, xH, CH, row, rok);
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                    hv[t] = hv[t] * *(const f32x4*)(gH + 16 * t + 4 * g4) + *(const f32x4*)(gH + p16(CH) + 16 * t + 4 * g4);
+                act_tile<NT>(hv, actH);
+                if (!rok) {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) hv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+                put_img<NT>(himg, hv, K, 16 * wv);
+            }
+            // dH_prev = W^T dz (dz as the B operand; the W^T image rows = K features)
+            bf16x8 b[KS];
+            frags<NT>(dz, b);
+            __syncthreads();   // images (W^T, dZ, H) complete
+            f32x4 nh[NT];
+            tile_gemm<NT, KS>(wimg, bs, (K + 15) >> 4, (N + 31) >> 5, b, nh);
+            if (skp) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) dh[u][t] += nh[t];
+            } else {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) dh[u][t] = nh[t];
+            }
+            dw_half<TNS, TKS>(zimg, himg, ntn, ntk, acc);
+        }
+        // dW | db partial of this workgroup
+        {
+            const int wn = wv >> 2, wk = wv & 3, K1 = K + 1;
+            float* dst = pb + G.wo;
+#pragma unroll
+            for (int a = 0; a < TNS; ++a)
+#pragma unroll
+                for (int c = 0; c < TKS; ++c) {
+                    const int tn = wn + 2 * a, tk = wk + 4 * c;
+                    if (tn >= ntn || tk >= ntk) continue;
+                    const int k = 16 * tk + lr;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int n = 16 * tn + 4 * g4 + i;
+                        if (n < N && k < K) dst[n * K1 + k] = acc[a][c][i];
+                    }
+                }
+        }
+        flush_cols<NT>(red, la, lb, N, ln, ln ? pb + d.l[l].lpo : nullptr, pb + G.wo + K, K + 1);
+    }
+    // identity skip: d x0 += dout
+    if (d.skip == 1) {
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int64_t row = rbase + IMR * u;
+            f32x4 t2[NT];
+            load_rows<NT>(t2, dout, DL, row, row < R);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) dh[u][t] += t2[t];
+        }
+    }
+    // input LayerNorm backward -> dx
+    float la[NT], lb[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int64_t row = rbase + IMR * u;
+        const bool rok = row < R;
+        f32x4 xv[NT];
+        load_sv<NT>(xv, xh, d0, row, rok);
+        const float rstd = rok ? rs[row] : 0.f;
+        ln_bwd<NT>(dh[u], xv, rstd, d0, prm_in, prm_in + p16(d0), 0, la);
+        store_rows<NT>(dx, dh[u], d0, row, rok);
+    }
+    __syncthreads();
+    flush_cols<NT>(red, la, lb, d0, true, pb + d.lpo0, nullptr, 0);
+}
+
+// ---------------------------------------------------------------- final sum
+// one segment per dW|db slab (E = N (K + 1), K1 = K + 1) or gamma|beta pair
+// (E = 2N, K1 = 0), summed over the nblk workgroup partials in fixed order
+struct SumSeg {
+    int E, N, K1, src;
+    float* da;
+    float* db;
+};
+constexpr int MAXSEG = MAXG + MAXL + 1;
+struct SumArgs {
+    int nseg, P;
+    SumSeg s[MAXSEG];
+};
+
+__global__ __launch_bounds__(256) void k_mlpb_sum(SumArgs sa, const float* __restrict__ part, int nblk, int accumulate) {
+    __shared__ float red[16][17];
+    const SumSeg& sg = sa.s[blockIdx.y];
+    const int o = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int E = sg.E, P = sa.P;
+    if ((int64_t)blockIdx.x * 16 >= E) return;
+    const float* src = part + sg.src;
+    const int i = blockIdx.x * 16 + o;
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (i < E) {
+        int b = sl;
+        for (; b + 48 < nblk; b += 64)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a4[u] += src[(int64_t)(b + 16 * u) * P + i];
+        for (int u = 0; b < nblk; b += 16, ++u) a4[u & 3] += src[(int64_t)b * P + i];
+    }
+    red[sl][o] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    __syncthreads();
+    if (sl != 0 || i >= E) return;
+    float t8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t8[j] = red[2 * j][o] + red[2 * j + 1][o];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t8[j] = t8[2 * j] + t8[2 * j + 1];
+    const float t = (t8[0] + t8[1]) + (t8[2] + t8[3]);
+    float* dst;
+    if (sg.K1) {
+        const int n = i / sg.K1, k = i - n * sg.K1;
+        dst = k < sg.K1 - 1 ? (sg.da ? sg.da + (int64_t)n * (sg.K1 - 1) + k : nullptr) : (sg.db ? sg.db + n : nullptr);
+    } else {
+        dst = i < sg.N ? (sg.da ? sg.da + i : nullptr) : (sg.db ? sg.db + (i - sg.N) : nullptr);
+    }
+    if (dst) *dst = accumulate ? *dst + t : t;
+}
+
+// ---------------------------------------------------------------- host side
+inline int h16(int n) { return (n + 15) & ~15; }
+inline int h32(int n) { return (n + 31) & ~31; }
+
+struct BPlan {
+    BDesc d;
+    int nt, tpw;
+    int64_t Rp, xh_floats, rs_floats, nblk;
+};
+
+int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+               const float* const* params, int64_t R, const char* who) {
+    VT_CHECK_ARG(n_layers >= 1 && n_layers <= MAXL, "%s: n_layers %d not in [1, %d]", who, n_layers, MAXL);
+    VT_CHECK_ARG(skip >= 0 && skip <= 2, "%s: skip %d", who, skip);
+    VT_CHECK_ARG(R >= 1, "%s: rows %lld", who, (long long)R);
+    BDesc& d = p.d;
+    d = BDesc{};
+    d.L = n_layers;
+    d.d0 = dims[0];
+    d.skip = skip;
+    d.eps = eps;
+    d.nG = n_layers + (skip == 2 ? 1 : 0);
+    int wmax = dims[0], n_ln = 0, xo = h16(dims[0]), lnp = 0;
+    for (int l = 0; l < n_layers; ++l) {
+        const int K = dims[l], N = dims[l + 1];
+        VT_CHECK_ARG(K >= 1 && N >= 1 && K <= VT_MLP_MAX_WIDTH && N <= VT_MLP_MAX_WIDTH,
+                     "%s: layer %d width %d -> %d outside [1, %d]", who, l, K, N, VT_MLP_MAX_WIDTH);
+        VT_CHECK_ARG(layer_ln[l] || l == n_layers - 1, "%s: hidden layer %d without LayerNorm", who, l);
+        VT_CHECK_ARG(layer_ln[l] || layer_act[l] == 0, "%s: activation without LayerNorm (layer %d)", who, l);
+        VT_CHECK_ARG(layer_act[l] >= 0 && layer_act[l] <= 3, "%s: act %d", who, layer_act[l]);
+        BL& ly = d.l[l];
+        ly.ln = layer_ln[l] ? 1 : 0;
+        ly.act = layer_act[l];
+        ly.g = params[4 + 4 * l];
+        ly.be = params[5 + 4 * l];
+        BG& G = d.G[l];
+        G.K = K;
+        G.N = N;
+        G.W = params[2 + 4 * l];
+        G.b = params[3 + 4 * l];
+        VT_CHECK_ARG(G.W && (!ly.ln || (ly.g && ly.be)), "%s: missing parameter of layer %d", who, l);
+        wmax = N > wmax ? N : wmax;
+        if (ly.ln) {
+            ly.xo = xo;
+            ly.ri = 1 + n_ln;
+            ++n_ln;
+            xo += h16(N);
+        } else {
+            ly.xo = ly.ri = -1;
+        }
+    }
+    d.g0 = params[0];
+    d.be0 = params[1];
+    VT_CHECK_ARG(d.g0 && d.be0, "%s: missing input LayerNorm parameters", who);
+    VT_CHECK_ARG(skip != 1 || dims[0] == dims[n_layers], "%s: identity skip needs in == out width", who);
+    if (skip == 2) {
+        BG& G = d.G[n_layers];
+        G.K = dims[0];
+        G.N = dims[n_layers];
+        G.W = params[2 + 4 * n_layers];
+        G.b = params[3 + 4 * n_layers];
+        VT_CHECK_ARG(G.W, "%s: projection skip without weight", who);
+    }
+    // forward LDS: images, then [bias, gamma, beta] per GEMM, then the input LN
+    int off = 0, po = 0, bw = 0, bh = 0, bz = 0;
+    for (int g = 0; g < d.nG; ++g) {
+        BG& G = d.G[g];
+        G.fo = off;
+        G.fs = h32(G.K) + 16;
+        off += h16(G.N) * G.fs;
+        off = (off + 7) & ~7;                 // 16-B aligned images
+        G.po = po;
+        po += 3 * h16(G.N);
+        G.bs = h32(G.N) + 16;
+        const int e = h16(G.K) * G.bs;
+        bw = e > bw ? e : bw;
+        bh = h16(G.K) > bh ? h16(G.K) : bh;
+        bz = h16(G.N) > bz ? h16(G.N) : bz;
+    }
+    d.fimg = 2 * off;
+    d.pin = po;
+    d.fbytes = d.fimg + 4 * (po + 2 * h16(dims[0]));
+    const int ntw = (wmax + 15) / 16;
+    p.nt = ntw <= 2 ? 2 : ntw <= 4 ? 4 : ntw <= 6 ? 6 : 9;
+    d.bwimg = (bw + 7) & ~7;
+    d.bhrows = bh;
+    d.bzrows = bz;
+    int bprm = 0;
+    for (int l = 0; l < n_layers; ++l) {
+        d.l[l].bpo = d.l[l].ln ? bprm : -1;
+        if (d.l[l].ln) bprm += 2 * h16(d.G[l].N);
+    }
+    d.bpin = bprm;
+    bprm += 2 * h16(dims[0]);
+    d.bprm = bprm;
+    d.bbytes = 2 * (d.bwimg + (bz + bh) * IMS) + 4 * (bprm + NW * 48 * p.nt);
+    // partials: dW|db of every GEMM, then gamma|beta of every LN and the input LN
+    int P = 0;
+    for (int g = 0; g < d.nG; ++g) {
+        d.G[g].wo = P;
+        P += d.G[g].N * (d.G[g].K + 1);
+    }
+    for (int l = 0; l < n_layers; ++l) {
+        d.l[l].lpo = d.l[l].ln ? P : -1;
+        if (d.l[l].ln) P += 2 * d.G[l].N;
+    }
+    d.lpo0 = P;
+    P += 2 * dims[0];
+    d.P = P;
+    (void)lnp;
+    p.tpw = p.nt >= 9 ? 1 : 2;
+    const int blk = IMR * p.tpw;
+    p.Rp = (R + 2 * IMR - 1) / (2 * IMR) * (2 * IMR);   // the saved state is padded for either block size
+    p.nblk = (R + blk - 1) / blk;
+    p.xh_floats = (int64_t)xo * p.Rp;
+    p.rs_floats = (int64_t)(1 + n_ln) * p.Rp;
+    VT_CHECK_ARG(d.fbytes <= 160 * 1024, "%s: weights need %d bytes of LDS (> 160 KiB)", who, d.fbytes);
+    VT_CHECK_ARG(d.bbytes <= 160 * 1024, "%s: backward needs %d bytes of LDS (> 160 KiB)", who, d.bbytes);
+    return VT_OK;
+}
+
+int n_fwd_blocks(int64_t R) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount,
+                                                                      dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const int64_t tiles = (R + 15) / 16, need = (tiles + NW - 1) / NW;
+    return (int)(need < ncu ? need : ncu);
+}
+
+// Device copies of the descriptors, keyed by content: a plan's descriptor is
+// uploaded once (stream-ordered copy from pinned host memory, so it is also
+// valid under hipGraph capture) and reused by every later launch.
+const BDesc* device_desc(const BDesc& d, hipStream_t st) {
+    struct Entry {
+        BDesc* host;
+        BDesc* dev;
+    };
+    static std::unordered_map<uint64_t, std::vector<Entry>> cache;
+    static std::mutex mu;
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(&d);
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(BDesc); ++i) h = (h ^ b[i]) * 1099511628211ull;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& v = cache[h];
+    for (const Entry& e : v)
+        if (!memcmp(e.host, &d, sizeof(BDesc))) return e.dev;
+    Entry e{nullptr, nullptr};
+    if (hipHostMalloc(reinterpret_cast<void**>(&e.host), sizeof(BDesc), 0) != hipSuccess) return nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&e.dev), sizeof(BDesc)) != hipSuccess) return nullptr;
+    memcpy(e.host, &d, sizeof(BDesc));
+    if (hipMemcpyAsync(e.dev, e.host, sizeof(BDesc), hipMemcpyHostToDevice, st) != hipSuccess) return nullptr;
+    v.push_back(e);
+    return e.dev;
+}
+
+template <typename Kern>
+void set_lds(Kern k, int bytes) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+}  // namespace
+}  // namespace vt
+
+using namespace vt;
+
+extern "C" {
+
+int vt_resmlp_bf16_sizes(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                         int64_t rows, int64_t* sizes) {
+    const float* dummy[4 * MAXL + 4];
+    for (int i = 0; i < 4 * MAXL + 4; ++i) dummy[i] = reinterpret_cast<const float*>(16);
+    BPlan p;
+    const int rc = make_bplan(p, n_layers, dims, layer_ln, layer_act, skip, 1e-5f, dummy, rows, "vt_resmlp_bf16_sizes");
+    if (rc) return rc;
+    sizes[0] = p.xh_floats;
+    sizes[1] = p.rs_floats;
+    sizes[2] = p.nblk * p.d.P;
+    return VT_OK;
+}
+
+int vt_resmlp_bf16_fwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                       const float* const* params, const float* x, int64_t rows, float* out, float* xhat, float* rstd,
+                       void* stream) {
+    BPlan p;
+    const int rc = make_bplan(p, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, "vt_resmlp_bf16_fwd");
+    if (rc) return rc;
+    VT_CHECK_ARG(x && out && xhat && rstd, "vt_resmlp_bf16_fwd: null buffer");
+    const dim3 grid((unsigned)n_fwd_blocks(rows));
+    hipStream_t st = S(stream);
+    const BDesc* ddev = device_desc(p.d, st);
+    VT_CHECK_ARG(ddev, "vt_resmlp_bf16_fwd: descriptor upload failed");
+    const bool id = skip == 1;
+    switch (p.nt * 2 + (id ? 1 : 0)) {
+#define VT_MBF(NTV, IDV)                                                                                   \
+    case NTV * 2 + IDV:                                                                                    \
+        set_lds(k_mlpb_fwd<NTV, IDV>, p.d.fbytes);                                                        \
+        hipLaunchKernelGGL((k_mlpb_fwd<NTV, IDV>), grid, dim3(BT), p.d.fbytes, st, ddev, x, rows, out, xhat, rstd, \
+                           p.Rp);                                                                          \
+        break;
+        VT_MBF(2, 0) VT_MBF(2, 1) VT_MBF(4, 0) VT_MBF(4, 1) VT_MBF(6, 0) VT_MBF(6, 1) VT_MBF(9, 0)
+        default: VT_MBF(9, 1)
+#undef VT_MBF
+    }
+    VT_LAUNCH_CHECK("vt_resmlp_bf16_fwd");
+    return VT_OK;
+}
+
+int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                       const float* const* params, const float* dout, const float* xhat, const float* rstd,
+                       int64_t rows, float* dx, float* const* grads, int accumulate, float* ws, int64_t ws_floats,
+                       void* stream) {
+    BPlan p;
+    const int rc = make_bplan(p, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, "vt_resmlp_bf16_bwd");
+    if (rc) return rc;
+    VT_CHECK_ARG(dout && xhat && rstd && dx && grads, "vt_resmlp_bf16_bwd: null buffer");
+    VT_CHECK_ARG(ws && ws_floats >= p.nblk * p.d.P, "vt_resmlp_bf16_bwd: workspace %lld floats < %lld",
+                 (long long)ws_floats, (long long)(p.nblk * p.d.P));
+    SumArgs sa{};
+    sa.P = p.d.P;
+    int emax = 0;
+    auto add = [&](int E, int N, int K1, int src, float* da, float* db) {
+        if (!da && !db) return;
+        sa.s[sa.nseg++] = SumSeg{E, N, K1, src, da, db};
+        emax = E > emax ? E : emax;
+    };
+    for (int q = 0; q < p.d.nG; ++q) {
+        const int gi = q < n_layers ? 2 + 4 * q : 2 + 4 * n_layers;
+        add(p.d.G[q].N * (p.d.G[q].K + 1), p.d.G[q].N, p.d.G[q].K + 1, p.d.G[q].wo, grads[gi], grads[gi + 1]);
+    }
+    for (int l = 0; l < n_layers; ++l)
+        if (p.d.l[l].ln) add(2 * p.d.G[l].N, p.d.G[l].N, 0, p.d.l[l].lpo, grads[4 + 4 * l], grads[5 + 4 * l]);
+    add(2 * dims[0], dims[0], 0, p.d.lpo0, grads[0], grads[1]);
+    hipStream_t st = S(stream);
+    const dim3 grid((unsigned)p.nblk);
+    const BDesc* ddev = device_desc(p.d, st);
+    VT_CHECK_ARG(ddev, "vt_resmlp_bf16_bwd: descriptor upload failed");
+    switch (p.nt) {
+#define VT_MBB(NTV, TPWV)                                                                                        \
+    case NTV:                                                                                              \
+        set_lds(k_mlpb_bwd<NTV, TPWV>, p.d.bbytes);                                                        \
+        hipLaunchKernelGGL((k_mlpb_bwd<NTV, TPWV>), grid, dim3(BT), p.d.bbytes, st, ddev, dout, xhat, rstd, rows, \
+                           p.Rp, dx, ws);                                                                  \
+        break;
+        VT_MBB(2, 2) VT_MBB(4, 2) VT_MBB(6, 2)
+        default: VT_MBB(9, 1)
+#undef VT_MBB
+    }
+    if (sa.nseg) {
+        const dim3 gs((unsigned)((emax + 15) / 16), (unsigned)sa.nseg);
+        hipLaunchKernelGGL(k_mlpb_sum, gs, dim3(256), 0, st, sa, ws, (int)p.nblk, accumulate);
+    }
+    VT_LAUNCH_CHECK("vt_resmlp_bf16_bwd");
+    return VT_OK;
+}
+
+}  // extern "C"

@@ -201,6 +201,7 @@ class ResidualMLP(nn.Module):
             d = h
         self.body = nn.Sequential(*mods)
         self.fused = True   # whole-stack kernels (vt_resmlp_*); False: one launch sequence per layer
+        self.bf16 = False   # whole-stack kernels on bf16 MFMA (vt_resmlp_bf16_*, 16-bit autocast precision)
         self.use_skip_connection = use_skip_connection
         if use_skip_connection:
             self.skip_proj = Linear(input_dim, hidden_dims[-1]) if input_dim != hidden_dims[-1] else nn.Identity()
@@ -256,7 +257,7 @@ class ResidualMLP(nn.Module):
         if x.is_cuda and self.fused:
             fs = self._fused_spec()
             if fs is not None:
-                return ops.resmlp(x, *fs)
+                return ops.resmlp(x, *fs, bf16=self.bf16)
         x0 = self.input_norm(x)
         h = x0
         for (idx, has_ln, act) in self._plan:
@@ -485,7 +486,7 @@ class SeqVaeTeb(nn.Module):
     def __init__(self, input_channels=76, sequence_length=300, latent_dim_source=32, latent_dim_target=32,
                  latent_dim_z=32, decimation_factor=16, warmup_period=30, scattering_channels=43,
                  phase_channels=44, cross_phase_channels=130, head_precision="fp32", concurrent_encoders=False,
-                 conv_precision="fp32"):
+                 conv_precision="fp32", mlp_precision="fp32"):
         super().__init__()
         # the source and target encoders are independent until the conditional
         # encoder: on a GPU they can run on two HIP streams (their LSTM
@@ -499,6 +500,19 @@ class SeqVaeTeb(nn.Module):
         self.conditional_encoder = ConditionalEncoder(latent_dim_source, latent_dim_target)
         self.decoder = Decoder(latent_dim_z, sequence_length, head_precision)
         self.set_conv_precision(conv_precision)
+        self.set_mlp_precision(mlp_precision)
+
+    def set_mlp_precision(self, precision):
+        """"fp32": the ResidualMLP stacks on exact-fp32 MFMA (parity mode); "bf16":
+        their Linear layers on bf16 MFMA with fp32 accumulation, LayerNorm and
+        reductions fp32 — the reference trains under 16-bit autocast
+        (ref/model/graph_model.py:510, :709-711)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"mlp_precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.mlp_precision = precision
+        for m in self.modules():
+            if isinstance(m, ResidualMLP):
+                m.bf16 = precision == "bf16"
 
     def set_conv_precision(self, precision):
         """"fp32": exact-fp32 MFMA convs (parity mode); "bf16": bf16-MFMA convs with

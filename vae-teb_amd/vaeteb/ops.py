@@ -261,13 +261,14 @@ class MlpSpec:
     def supported(cls, dims):
         return len(dims) - 1 <= cls.MAX_LAYERS and max(dims) <= cls.MAX_WIDTH
 
-    def sizes(self, rows):
-        s = self._sizes.get(rows)
+    def sizes(self, rows, bf16=False):
+        s = self._sizes.get((rows, bf16))
         if s is None:
             import ctypes
             arr = (ctypes.c_int64 * 3)()
-            call("vt_resmlp_sizes", self.L, self.dims, self.ln, self.act, self.skip, rows, arr)
-            s = self._sizes[rows] = tuple(arr)
+            call("vt_resmlp_bf16_sizes" if bf16 else "vt_resmlp_sizes", self.L, self.dims, self.ln, self.act,
+                 self.skip, rows, arr)
+            s = self._sizes[(rows, bf16)] = tuple(arr)
         return s
 
     @staticmethod
@@ -288,54 +289,57 @@ class MlpSpec:
 
 class ResMLPF(torch.autograd.Function):
     """A whole ResidualMLP (ref/model/vae_teb_model.py:336-403): one forward
-    launch (vt_resmlp_fwd) and three backward launches (vt_resmlp_bwd: chain,
-    grouped weight gradients, fixed-order sums).  params in MlpSpec order:
+    launch (vt_resmlp_fwd) and the backward launches of vt_resmlp_bwd (chain,
+    fixed-order sums).  bf16=True: the bf16-MFMA family (vt_resmlp_bf16_*: the
+    Linear layers in 16 bit as under the reference's autocast, LayerNorm and
+    every reduction fp32).  params in MlpSpec order:
     [g_in, b_in, (W, b, g, beta) per layer, W_skip, b_skip] (None if absent)."""
 
     @staticmethod
-    def forward(ctx, x, spec, *params):
+    def forward(ctx, x, spec, bf16, *params):
         _check(x, *params)
         d0, DL = spec.dims_l[0], spec.dims_l[-1]
         x2 = x.reshape(-1, d0).contiguous()
         R = x2.shape[0]
-        n_xh, n_rs, _ = spec.sizes(R)
+        n_xh, n_rs, _ = spec.sizes(R, bf16)
         out = torch.empty((R, DL), device=x.device)
         xh = torch.empty(n_xh, device=x.device)
         rs = torch.empty(n_rs, device=x.device)
         pp = spec.param_ptrs if spec.param_ptrs is not None else spec.pointers(params)
-        call("vt_resmlp_fwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp,
-             ptr(x2), R, ptr(out), ptr(xh), ptr(rs), _st())
+        call("vt_resmlp_bf16_fwd" if bf16 else "vt_resmlp_fwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip,
+             spec.eps, pp, ptr(x2), R, ptr(out), ptr(xh), ptr(rs), _st())
         ctx.save_for_backward(xh, rs)
-        ctx.spec, ctx.params, ctx.shape, ctx.R = spec, params, x.shape, R
+        ctx.spec, ctx.params, ctx.shape, ctx.R, ctx.bf16 = spec, params, x.shape, R, bf16
         return out.reshape(*x.shape[:-1], DL)
 
     @staticmethod
     def backward(ctx, gout):
         xh, rs = ctx.saved_tensors
-        spec, params, R = ctx.spec, ctx.params, ctx.R
+        spec, params, R, bf16 = ctx.spec, ctx.params, ctx.R, ctx.bf16
         d0, DL = spec.dims_l[0], spec.dims_l[-1]
         g2 = gout.reshape(R, DL).contiguous()
         present = [i for i, p in enumerate(params) if p is not None]
-        need = ctx.needs_input_grad[2:]
+        need = ctx.needs_input_grad[3:]
         pg = _ParamGrads([params[i] for i in present], [bool(need[i]) for i in present])
         grads = [None] * len(params)
         for i, gt in zip(present, pg.out):
             grads[i] = gt
-        ws_floats = spec.sizes(R)[2]
+        ws_floats = spec.sizes(R, bf16)[2]
         ws = WS.get(ws_floats, xh.device, 5)
         dx = torch.empty((R, d0), device=xh.device)
         pp = spec.param_ptrs if spec.param_ptrs is not None else spec.pointers(params)
-        call("vt_resmlp_bwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp,
-             ptr(g2), ptr(xh), ptr(rs), R, ptr(dx), spec.grad_pointers(grads), pg.acc, ptr(ws), ws.numel(), _st())
+        call("vt_resmlp_bf16_bwd" if bf16 else "vt_resmlp_bwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip,
+             spec.eps, pp, ptr(g2), ptr(xh), ptr(rs), R, ptr(dx), spec.grad_pointers(grads), pg.acc, ptr(ws),
+             ws.numel(), _st())
         res = pg.result()
         out = [None] * len(params)
         for i, gt in zip(present, res):
             out[i] = gt
-        return (dx.reshape(ctx.shape), None, *out)
+        return (dx.reshape(ctx.shape), None, None, *out)
 
 
-def resmlp(x, spec, params):
-    return ResMLPF.apply(x, spec, *params)
+def resmlp(x, spec, params, bf16=False):
+    return ResMLPF.apply(x, spec, bool(bf16), *params)
 
 
 # -------------------------------------------------------- LayerNorm + act
