@@ -233,6 +233,9 @@ def main():
                     help="decoder R x R head GEMMs: bf16 MFMA (the reference trains under 16-bit autocast) or fp32")
     ap.add_argument("--conv", choices=["bf16", "fp32"], default="bf16",
                     help="conv blocks: bf16 MFMA with fp32 accumulation / BatchNorm (16-bit autocast) or exact fp32")
+    ap.add_argument("--mlp", choices=["bf16", "fp32"], default="bf16",
+                    help="ResidualMLP stacks: Linear layers on bf16 MFMA with fp32 accumulation, LayerNorm fp32 "
+                         "(16-bit autocast) or exact fp32")
     args = ap.parse_args()
 
     rank, world, local, dev = init_distributed()
@@ -247,7 +250,8 @@ def main():
     S = plan.S
     torch.manual_seed(1234)  # same initial weights on every rank (DDP semantics)
     vae_kw = dict(scattering_channels=fe.C_st, phase_channels=fe.C_ph, cross_phase_channels=fe.C_x,
-                  head_precision=args.heads, conv_precision=args.conv, concurrent_encoders=not args.serial_encoders)
+                  head_precision=args.heads, conv_precision=args.conv, mlp_precision=args.mlp,
+                  concurrent_encoders=not args.serial_encoders)
     c4 = args.workload == "c4"
     if c4:
         # config 4: SeqVaeTebClassifier end to end (freeze_vae=False), the reference's default classifier
@@ -388,9 +392,10 @@ def main():
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32" if (args.heads, args.conv) == ("fp32", "fp32") else
-                 "bf16 MFMA (" + " + ".join(n for n, v in (("decoder heads", args.heads), ("conv blocks", args.conv))
-                                           if v == "bf16") + "), fp32 accumulation; fp32 elsewhere",
+        "dtype": "fp32" if (args.heads, args.conv, args.mlp) == ("fp32", "fp32", "fp32") else
+                 "bf16 MFMA (" + " + ".join(n for n, v in (("decoder heads", args.heads), ("conv blocks", args.conv),
+                                                         ("ResidualMLP linears", args.mlp)) if v == "bf16")
+                 + "), fp32 accumulation; fp32 LayerNorm / BatchNorm / LSTM / front-end / optimizer",
         "data": "synthetic",
         "config": {"workload": (f"c4: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTebClassifier("
                                 f"R={16 * S}, FHRInceptionTimeClassifier f32 d6 attention, dropout 0.2) end-to-end "

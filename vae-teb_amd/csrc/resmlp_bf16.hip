@@ -44,13 +44,12 @@ constexpr int MAXL = VT_MLP_MAX_LAYERS;
 constexpr int MAXG = MAXL + 1;   // layers + skip projection
 constexpr int BT = 512;          // threads per workgroup (8 waves)
 constexpr int NW = BT / 64;
-constexpr int IMR = 128;         // rows of one dZ / H image (half a block)
-constexpr int IMS = IMR + 16;    // image row stride (bf16): == 16 mod 32 -> conflict-free fragment reads
+constexpr int IMR = 128;         // backward rows per workgroup and tile-per-wave (8 waves x 16)
 
 struct BG {                      // one GEMM: z = h W^T + b, W [N][K]
     int K, N;
     int fo, fs;                  // forward image (bf16 offset, row stride): rows pad16(N), cols pad32(K)
-    int bw, bs;                  // backward image W^T: bf16 element count, row stride: rows pad16(K), cols pad32(N)
+    int bw, bs;                  // backward image W^T: LDS offset (bf16), row stride: rows pad16(K), cols pad32(N)
     int po;                      // fp32 params in LDS: bias[pad16 N], gamma, beta
     int wo;                      // dW|db partial offset (floats), N x (K + 1)
     const float* W;
@@ -69,6 +68,7 @@ struct BDesc {
     int pin;                     // LDS float offset of the input LN gamma / beta (pad16 d0 each)
     int bwimg;                   // backward: bf16 elements of the largest W^T image
     int bhrows;                  // backward: rows of the H image (max pad16(K))
+    int bres;                    // backward: every W^T image resident in LDS (else one at a time, at offset 0)
     int bzrows;                  // backward: rows of the dZ image (max pad16(N))
     int bprm;                    // backward: floats of LN parameters in LDS
     int bbytes;                  // backward LDS bytes
@@ -200,48 +200,85 @@ __device__ __forceinline__ void tile_gemm(const __bf16* img, int stride, int nt,
         }
         acc[t] = c;
         p += step;
+        __builtin_amdgcn_sched_barrier(0);   // bound the fragment loads in flight (registers)
     }
 }
 
-// row-major [rows][C] tile (any C) -> transposed layout (0 past C / for invalid rows)
-template <int NT>
-__device__ __forceinline__ void load_rows(f32x4 (&a)[NT], const float* __restrict__ src, int C, int64_t row, bool rok) {
-    const int g4 = (threadIdx.x & 63) >> 4;
-    const float* p = src + (rok ? row : 0) * (int64_t)C + 4 * g4;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float v = 0.f;
-            if (rok && 16 * t + 4 * g4 + i < C) v = p[16 * t + i];
-            a[t][i] = v;
-        }
+// Global memory through raw buffer descriptors: an access past num_records
+// returns 0 / is dropped by the hardware, so rows past R and masked lanes need
+// no branches (OOB: an offset past any buffer here, < 2 GiB each).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr unsigned OOB = 0x80000000u;
+
+__device__ __forceinline__ rsrc_t brs(const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                             (int)(bytes < 0x7ffffff0 ? bytes : 0x7ffffff0), 0x00020000);
+}
+__device__ __forceinline__ float bld(rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void bst(rsrc_t r, unsigned off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ f32x4 bld4(rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void bst4(rsrc_t r, unsigned off, f32x4 v) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, 0);
 }
 
+// row-major [R][C] tile (any C) -> transposed layout (0 past C and for rows >= R).
+// Element masks only in the one partial 16-feature tile (uniform branches on
+// full / partial / empty tiles: per-element masks of every tile, hoisted out of
+// the layer loop, exhaust the scalar registers).
 template <int NT>
-__device__ __forceinline__ void store_rows(float* __restrict__ dst, const f32x4 (&a)[NT], int C, int64_t row, bool rok) {
+__device__ __forceinline__ void load_rows(f32x4 (&a)[NT], const float* src, int C, int64_t R, int64_t row) {
     const int g4 = (threadIdx.x & 63) >> 4;
-    if (!rok) return;
-    float* p = dst + row * (int64_t)C + 4 * g4;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (16 * t + 4 * g4 + i < C) p[16 * t + i] = a[t][i];
-}
-
-// saved state, row-major with the row padded to 16 (float4 per lane and tile)
-template <int NT>
-__device__ __forceinline__ void load_sv(f32x4 (&a)[NT], const float* __restrict__ src, int C, int64_t row, bool rok) {
-    const int g4 = (threadIdx.x & 63) >> 4;
-    const int nt = (C + 15) >> 4;
-    const f32x4* p = reinterpret_cast<const f32x4*>(src + row * (int64_t)(16 * nt) + 4 * g4);
+    const rsrc_t r = brs(src, R * C * 4);
+    const unsigned base = row < R ? (unsigned)((row * C + 4 * g4) * 4) : OOB;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (rok && t < nt) v = p[4 * t];
+        if (16 * t < C) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = bld(r, base + 4 * (16 * t + i));
+            if (16 * t + 16 > C) {
+                const int lim = C - 16 * t - 4 * g4;   // valid elements of this lane's quad
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = i < lim ? v[i] : 0.f;
+            }
+        }
         a[t] = v;
     }
+}
+
+template <int NT>
+__device__ __forceinline__ void store_rows(float* dst, const f32x4 (&a)[NT], int C, int64_t R, int64_t row) {
+    const int g4 = (threadIdx.x & 63) >> 4;
+    const rsrc_t r = brs(dst, R * C * 4);
+    const unsigned base = row < R ? (unsigned)((row * C + 4 * g4) * 4) : OOB;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        if (16 * t + 16 <= C) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bst(r, base + 4 * (16 * t + i), a[t][i]);
+        } else if (16 * t < C) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bst(r, 16 * t + 4 * g4 + i < C ? base + 4 * (16 * t + i) : OOB, a[t][i]);
+        }
+    }
+}
+
+// saved state: row-major [Rp][pad16(C)] (float4 per lane and tile), rows past R read 0
+template <int NT>
+__device__ __forceinline__ void load_sv(f32x4 (&a)[NT], const float* src, int C, int64_t Rp, int64_t row, bool rok) {
+    const int g4 = (threadIdx.x & 63) >> 4;
+    const int nt = (C + 15) >> 4;
+    const rsrc_t r = brs(src, Rp * 64 * nt);
+    const unsigned base = rok ? (unsigned)((row * 16 * nt + 4 * g4) * 4) : OOB;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a[t] = t < nt ? bld4(r, base + 64 * t) : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
 __device__ __forceinline__ float sum_groups(float v) {  // over the 4 lane groups (same row)
@@ -255,7 +292,7 @@ __device__ __forceinline__ float sum_groups(float v) {  // over the 4 lane group
 // leaves h (0 past C).
 template <int NT>
 __device__ __forceinline__ void ln_fwd(f32x4 (&z)[NT], int C, const float* gl, const float* bl, int act, float eps,
-                                       float* __restrict__ xh, float* __restrict__ rs, int64_t row, bool rok) {
+                                       float* xh, float* rs, int64_t Rp, int64_t row, bool rok) {
     const int lane = threadIdx.x & 63, g4 = lane >> 4;
     const int nt = (C + 15) >> 4;
     const float invC = 1.f / (float)C;
@@ -266,50 +303,75 @@ __device__ __forceinline__ void ln_fwd(f32x4 (&z)[NT], int C, const float* gl, c
     const float mean = sum_groups(s) * invC;
     float v = 0.f;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t) {
+        if (t < nt) {
+            z[t] -= mean;
+            if (16 * t + 16 > C) {   // the partial tile: 0 past C
+                const int lim = C - 16 * t - 4 * g4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float dlt = (16 * t + 4 * g4 + i < C) ? z[t][i] - mean : 0.f;
-            z[t][i] = dlt;
-            v += dlt * dlt;
+                for (int i = 0; i < 4; ++i) z[t][i] = i < lim ? z[t][i] : 0.f;
+            }
+            v += (z[t][0] * z[t][0] + z[t][1] * z[t][1]) + (z[t][2] * z[t][2] + z[t][3] * z[t][3]);
         }
+    }
     const float rstd = rsqrtf(sum_groups(v) * invC + eps);
-    if (rok && g4 == 0) rs[row] = rstd;
-    f32x4* px = reinterpret_cast<f32x4*>(xh + row * (int64_t)(16 * nt) + 4 * g4);
+    bst(brs(rs, Rp * 4), (rok && g4 == 0) ? (unsigned)(row * 4) : OOB, rstd);
+    const rsrc_t rx = brs(xh, Rp * 64 * nt);
+    const unsigned bx = rok ? (unsigned)((row * 16 * nt + 4 * g4) * 4) : OOB;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        if (t >= nt) continue;
-        z[t] *= rstd;                                   // xhat (0 past C)
-        if (rok) px[4 * t] = z[t];
-        const f32x4 gv = *(const f32x4*)(gl + 16 * t + 4 * g4);
-        const f32x4 bv = *(const f32x4*)(bl + 16 * t + 4 * g4);
-        z[t] = z[t] * gv + bv;                          // gamma / beta are 0 past C
+        if (t < nt) {
+            z[t] *= rstd;                               // xhat (0 past C)
+            bst4(rx, bx + 64 * t, z[t]);
+            const f32x4 gv = *(const f32x4*)(gl + 16 * t + 4 * g4);
+            const f32x4 bv = *(const f32x4*)(bl + 16 * t + 4 * g4);
+            z[t] = z[t] * gv + bv;                      // gamma / beta are 0 past C
+        }
     }
     act_tile<NT>(z, act);
 }
 
 // ------------------------------------------------------------------ forward
+// the weight images are built from the fp32 master weights at every launch
+// (the optimizer rewrites them each step); loads in batches of SB per thread,
+// all in flight before the first conversion
+
 __device__ void stage_fwd(const BDesc& d, __bf16* img, float* prm) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int g = 0; g < d.nG; ++g) {
         const BG& G = d.G[g];
         const int Np = p16(G.N), Kp = p32(G.K);
+        const float* __restrict__ W = G.W;
         __bf16* dst = img + G.fo;
-        for (int idx = threadIdx.x; idx < Np * Kp; idx += BT) {
-            const int n = idx / Kp, p = idx - n * Kp;
-            const int k = (p & ~31) + kperm(p & 31);
-            const float v = (n < G.N && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f;
-            dst[n * G.fs + p] = (__bf16)v;
+        // wave w: rows n = w, w + 8, ... (two per pass); lane: columns p = lane + 64 j
+        for (int n0 = wv; n0 < Np; n0 += 2 * NW) {
+            float v[2][3];
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int n = n0 + NW * r, p = lane + 64 * j;
+                    const int k = (p & ~31) + kperm(p & 31);
+                    v[r][j] = (n < G.N && p < Kp && k < G.K) ? W[(int64_t)n * G.K + k] : 0.f;
+                }
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int n = n0 + NW * r, p = lane + 64 * j;
+                    if (n < Np && p < Kp) dst[n * G.fs + p] = (__bf16)v[r][j];
+                }
         }
         const bool lnl = g < d.L && d.l[g].ln;
         for (int c = threadIdx.x; c < 3 * Np; c += BT) {
-            const int w = c / Np, f = c - w * Np;
+            const int w = c >= 2 * Np ? 2 : (c >= Np ? 1 : 0), f = c - w * Np;
             const float* src = w == 0 ? G.b : (lnl ? (w == 1 ? d.l[g].g : d.l[g].be) : nullptr);
             prm[G.po + c] = (src && f < G.N) ? src[f] : 0.f;
         }
     }
     const int d0p = p16(d.d0);
     for (int c = threadIdx.x; c < 2 * d0p; c += BT) {
-        const int w = c / d0p, f = c - w * d0p;
+        const int w = c >= d0p, f = c - w * d0p;
         prm[d.pin + c] = f < d.d0 ? (w == 0 ? d.g0 : d.be0)[f] : 0.f;
     }
 }
@@ -334,8 +396,8 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
         const int64_t row = tile * 16 + lr;
         const bool rok = row < R;
         f32x4 a[NT];
-        load_rows<NT>(a, X, d0, row, rok);
-        ln_fwd<NT>(a, d0, prm + d.pin, prm + d.pin + p16(d0), 0, d.eps, xh, rs, row, rok);
+        load_rows<NT>(a, X, d0, R, row);
+        ln_fwd<NT>(a, d0, prm + d.pin, prm + d.pin + p16(d0), 0, d.eps, xh, rs, Rp, row, rok);
         f32x4 x0[ID ? NT : 1];
         if constexpr (ID) {
 #pragma unroll
@@ -352,7 +414,7 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
             for (int t = 0; t < NT; ++t) a[t] += *(const f32x4*)(prm + po + 16 * t + 4 * g4);   // bias (0 past N)
             if (d.l[l].ln)
                 ln_fwd<NT>(a, N, prm + po + p16(N), prm + po + 2 * p16(N), d.l[l].act, d.eps,
-                           xh + (int64_t)d.l[l].xo * Rp, rs + (int64_t)d.l[l].ri * Rp, row, rok);
+                           xh + (int64_t)d.l[l].xo * Rp, rs + (int64_t)d.l[l].ri * Rp, Rp, row, rok);
             if (l < L - 1) frags<NT>(a, b);
         }
         if constexpr (ID) {
@@ -365,19 +427,34 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
 #pragma unroll
             for (int t = 0; t < NT; ++t) a[t] += sk[t] + *(const f32x4*)(prm + G.po + 16 * t + 4 * g4);
         }
-        store_rows<NT>(out, a, DL, row, rok);
+        store_rows<NT>(out, a, DL, R, row);
     }
 }
 
 // ----------------------------------------------------------------- backward
 // W^T image of GEMM G: img[k][32s + 8g + j] = W[32s + kperm(8g + j)][k]
+// (column p = n-position of the permuted image per wave, lanes over k: coalesced W rows)
 __device__ void stage_wt(const BG& G, __bf16* img) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int Kp = p16(G.K), Np = p32(G.N);
-    for (int idx = threadIdx.x; idx < Kp * Np; idx += BT) {
-        const int p = idx / Kp, k = idx - p * Kp;   // consecutive threads: consecutive k (coalesced W rows)
-        const int n = (p & ~31) + kperm(p & 31);
-        const float v = (n < G.N && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f;
-        img[k * G.bs + p] = (__bf16)v;
+    const float* __restrict__ W = G.W;
+    for (int p0 = wv; p0 < Np; p0 += 2 * NW) {
+        float v[2][3];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int p = p0 + NW * r, k = lane + 64 * j;
+                const int n = (p & ~31) + kperm(p & 31);
+                v[r][j] = (p < Np && n < G.N && k < G.K) ? W[(int64_t)n * G.K + k] : 0.f;
+            }
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int p = p0 + NW * r, k = lane + 64 * j;
+                if (p < Np && k < Kp) img[G.bw + k * G.bs + p] = (__bf16)v[r][j];
+            }
     }
 }
 
@@ -430,25 +507,31 @@ __device__ __forceinline__ void ln_bwd(f32x4 (&dh)[NT], const f32x4 (&xv)[NT], f
     }
     const float m1 = sum_groups(s1) * invC, m2 = sum_groups(s2) * invC;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const bool ok = 16 * t + 4 * g4 + i < C;
-            dh[t][i] = ok ? rstd * (dh[t][i] - m1 - xv[t][i] * m2) : 0.f;
+    for (int t = 0; t < NT; ++t) {
+        if (t >= nt) {
+            dh[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            continue;
         }
+        dh[t] = rstd * (dh[t] - m1 - xv[t] * m2);
+        if (16 * t + 16 > C) {
+            const int lim = C - 16 * t - 4 * g4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dh[t][i] = i < lim ? dh[t][i] : 0.f;
+        }
+    }
 }
 
-// transposed tile -> bf16 image rows [f][col0 + r] for the tiles covering C
-template <int NT>
+// transposed tile -> bf16 image rows [f][col0 + r] (row stride S) for the tiles covering C
+template <int NT, int S>
 __device__ __forceinline__ void put_img(__bf16* im, const f32x4 (&a)[NT], int C, int col0) {
     const int lane = threadIdx.x & 63, g4 = lane >> 4, lr = lane & 15;
     const int nt = (C + 15) >> 4;
-    __bf16* p = im + 4 * g4 * IMS + col0 + lr;
+    __bf16* p = im + 4 * g4 * S + col0 + lr;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         if (t >= nt) continue;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) p[(16 * t + i) * IMS] = (__bf16)a[t][i];
+        for (int i = 0; i < 4; ++i) p[(16 * t + i) * S] = (__bf16)a[t][i];
     }
 }
 
@@ -511,33 +594,47 @@ __device__ __forceinline__ void flush_cols(float* red, const float (&la)[NT], co
     }
 }
 
-// dW|db partial of one GEMM over the images of IMR rows, accumulated in acc:
-// wave (wn = w >> 2, wk = w & 3) owns output tiles tn = wn + 2a, tk = wk + 4c
-template <int TNS, int TKS>
-__device__ __forceinline__ void dw_half(const __bf16* zi, const __bf16* hi, int ntn, int ntk, f32x4 (&acc)[TNS][TKS]) {
+// dW partial of one GEMM over images of ROWS rows (row stride S) -> dst[n * K1 + k]
+// (k < K): wave (wn = w >> 2, wk = w & 3) owns output tiles tn = wn + 2a,
+// tk = wk + 4c, one tn at a time (TKS accumulators live)
+template <int TNS, int TKS, int ROWS, int S>
+__device__ __forceinline__ void dw_img(const __bf16* zi, const __bf16* hi, int N, int K, float* __restrict__ dst) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wn = wv >> 2, wk = wv & 3;
-    const int off = (lane & 15) * IMS + 8 * (lane >> 4);
+    const int g4 = lane >> 4, lr = lane & 15, K1 = K + 1;
+    const int ntn = (N + 15) >> 4, ntk = (K + 15) >> 4;
+    const int off = lr * S + 8 * g4;
+    for (int a = 0; a < TNS; ++a) {
+        const int tn = wn + 2 * a;
+        if (tn >= ntn) break;
+        f32x4 acc[TKS];
 #pragma unroll
-    for (int s = 0; s < IMR / 32; ++s) {
-        bf16x8 bf[TKS];
+        for (int c = 0; c < TKS; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+        for (int s = 0; s < ROWS / 32; ++s) {
+            const bf16x8 af = *(const bf16x8*)(zi + 16 * tn * S + off + 32 * s);
 #pragma unroll
-        for (int c = 0; c < TKS; ++c) {
-            const int tk = wk + 4 * c;
-            if (tk < ntk) bf[c] = *(const bf16x8*)(hi + 16 * tk * IMS + off + 32 * s);
+            for (int c = 0; c < TKS; ++c) {
+                const int tk = wk + 4 * c;
+                if (tk < ntk) acc[c] = mfma(af, *(const bf16x8*)(hi + 16 * tk * S + off + 32 * s), acc[c]);
+            }
         }
 #pragma unroll
-        for (int a = 0; a < TNS; ++a) {
-            const int tn = wn + 2 * a;
-            if (tn >= ntn) continue;
-            const bf16x8 af = *(const bf16x8*)(zi + 16 * tn * IMS + off + 32 * s);
+        for (int c = 0; c < TKS; ++c) {
+            const int k = 16 * (wk + 4 * c) + lr;
 #pragma unroll
-            for (int c = 0; c < TKS; ++c)
-                if (wk + 4 * c < ntk) acc[a][c] = mfma(af, bf[c], acc[a][c]);
+            for (int i = 0; i < 4; ++i) {
+                const int n = 16 * tn + 4 * g4 + i;
+                if (n < N && k < K) dst[n * K1 + k] = acc[c][i];
+            }
         }
     }
 }
 
-// TPW: 16-row tiles per wave (the workgroup's block is 128 TPW rows)
+// TPW: 16-row tiles per wave; the workgroup's block is 128 TPW rows, all of it in
+// one dZ / H image (row stride IS).  Per GEMM step (layer l, last to first, then the
+// skip projection) with ONE global round trip, overlapped with the LayerNorm
+// backward: the raw xhat of the step's H source (layer l-1's LN output) is loaded
+// at the step start, used for H, and carried to the next step as its LN input.
 template <int NT, int TPW>
 __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp, const float* __restrict__ dout,
                                                     const float* __restrict__ xh, const float* __restrict__ rs,
@@ -547,18 +644,22 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
     constexpr int KS = (NT + 1) / 2;
     constexpr int TNS = (NT + 1) / 2;          // dW output tiles per wave along n
     constexpr int TKS = (NT + 3) / 4;          // ... along k
+    constexpr int ROWS = IMR * TPW;            // rows per workgroup (one image)
+    constexpr int IS = ROWS + 16;              // image row stride: == 16 mod 32 -> conflict-free fragments
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* wimg = reinterpret_cast<__bf16*>(smem);
     __bf16* zimg = wimg + d.bwimg;
-    __bf16* himg = zimg + d.bzrows * IMS;
-    float* prm = reinterpret_cast<float*>(himg + d.bhrows * IMS);   // [LN params per LN layer][input LN]
-    float* red = prm + d.bprm;                                      // [NW][48 NT]
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4, lr = lane & 15;
+    __bf16* himg = zimg + d.bzrows * IS;
+    float* prm = reinterpret_cast<float*>(himg + d.bhrows * IS);   // [LN params per LN layer][input LN]
+    float* red = prm + d.bprm;                                     // [NW][48 NT]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4;
     const int L = d.L, d0 = d.d0, DL = d.G[L - 1].N;
-    const int64_t rbase = (int64_t)blockIdx.x * (IMR * TPW) + 16 * wv + lr;
+    const int64_t rbase = (int64_t)blockIdx.x * ROWS + 16 * wv + (lane & 15);
     float* pb = part + (int64_t)blockIdx.x * d.P;
 
-    // gamma / beta of every LayerNorm (+ the input LN), staged once; layer l's at prm + l.lpo... (lnp offsets)
+    if (d.bres)
+        for (int g = 0; g < d.nG; ++g) stage_wt(d.G[g], wimg);
+    // gamma / beta of every LayerNorm (+ the input LN), staged once; layer l's at prm + l.bpo
     for (int l = 0; l <= L; ++l) {
         const bool inl = l == L;
         if (!inl && !d.l[l].ln) continue;
@@ -566,20 +667,20 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
         const float* g = inl ? d.g0 : d.l[l].g;
         const float* be = inl ? d.be0 : d.l[l].be;
         for (int c = threadIdx.x; c < 2 * Np; c += BT) {
-            const int w = c / Np, f = c - w * Np;
+            const int w = c >= Np, f = c - w * Np;
             prm[o + c] = f < C ? (w == 0 ? g : be)[f] : 0.f;
         }
     }
     const float* prm_in = prm + d.bpin;
 
-    f32x4 dh[TPW][NT];
+    f32x4 dh[TPW][NT], xc[TPW][NT];            // output gradient / raw xhat of the current layer
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
         const int64_t row = rbase + IMR * u;
-        load_rows<NT>(dh[u], dout, DL, row, row < R);
+        load_rows<NT>(dh[u], dout, DL, R, row);
+        if (d.l[L - 1].ln) load_sv<NT>(xc[u], xh + (int64_t)d.l[L - 1].xo * Rp, DL, Rp, row, row < R);
     }
 
-    // GEMM steps: layers L-1 .. 0, then the skip projection (G[L])
     const int nsteps = L + (d.skip == 2 ? 1 : 0);
     for (int step = 0; step < nsteps; ++step) {
         const bool skp = step == L;
@@ -591,58 +692,73 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
         const float* gH = hsrc >= 0 ? prm + d.l[hsrc].bpo : prm_in;
         const int CH = hsrc >= 0 ? d.G[hsrc].N : d0, actH = hsrc >= 0 ? d.l[hsrc].act : 0;
         const float* xH = xh + (hsrc >= 0 ? (int64_t)d.l[hsrc].xo * Rp : 0);
+        // the H source rows: in flight during the LayerNorm backward below (the
+        // widest stacks load them after it, for registers)
+        constexpr bool PF = NT <= 6;
+        f32x4 xn[TPW][NT];
+        if constexpr (PF) {
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                const int64_t row = rbase + IMR * u;
+                load_sv<NT>(xn[u], xH, CH, Rp, row, row < R);
+            }
+        }
         __syncthreads();                      // previous step done with the W^T / dZ / H images and red
-        stage_wt(G, wimg);
+        if (!d.bres) stage_wt(G, wimg);
         float la[NT], lb[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
-        const int ntn = (N + 15) >> 4, ntk = (K + 15) >> 4;
-        f32x4 acc[TNS][TKS];
-#pragma unroll
-        for (int a = 0; a < TNS; ++a)
-#pragma unroll
-            for (int c = 0; c < TKS; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bf16x8 b[TPW][KS];
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             const int64_t row = rbase + IMR * u;
             const bool rok = row < R;
             f32x4 dz[NT];
             if (skp) {
-                load_rows<NT>(dz, dout, DL, row, rok);
+                load_rows<NT>(dz, dout, DL, R, row);
             } else {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) dz[t] = dh[u][t];
                 if (ln) {
-                    f32x4 xv[NT];
-                    load_sv<NT>(xv, xh + (int64_t)d.l[l].xo * Rp, N, row, rok);
-                    const float rstd = rok ? rs[(int64_t)d.l[l].ri * Rp + row] : 0.f;
+                    const float rstd = bld(brs(rs + (int64_t)d.l[l].ri * Rp, Rp * 4), rok ? (unsigned)(row * 4) : OOB);
                     const float* gl = prm + d.l[l].bpo;
-                    ln_bwd<NT>(dz, xv, rstd, N, gl, gl + p16(N), d.l[l].act, la);
+                    ln_bwd<NT>(dz, xc[u], rstd, N, gl, gl + p16(N), d.l[l].act, la);
                 }
             }
             colsum<NT>(dz, N, lb);            // the bias gradient: fp32 sum of dZ (not of its bf16 image)
-            if (u > 0) __syncthreads();       // the dW MFMAs of the previous half are done with the images
-            put_img<NT>(zimg, dz, N, 16 * wv);
-            {
-                // H = act(xhat_hsrc * gamma + beta) (the GEMM's input)
-                f32x4 hv[NT];
-                load_sv<NT>(hv, xH, CH, row, rok);
+            put_img<NT, IS>(zimg, dz, N, 128 * u + 16 * wv);
+            frags<NT>(dz, b[u]);
+        }
+        if constexpr (!PF) {
 #pragma unroll
-                for (int t = 0; t < NT; ++t)
-                    hv[t] = hv[t] * *(const f32x4*)(gH + 16 * t + 4 * g4) + *(const f32x4*)(gH + p16(CH) + 16 * t + 4 * g4);
-                act_tile<NT>(hv, actH);
-                if (!rok) {
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) hv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-                }
-                put_img<NT>(himg, hv, K, 16 * wv);
+            for (int u = 0; u < TPW; ++u) {
+                const int64_t row = rbase + IMR * u;
+                load_sv<NT>(xn[u], xH, CH, Rp, row, row < R);
             }
-            // dH_prev = W^T dz (dz as the B operand; the W^T image rows = K features)
-            bf16x8 b[KS];
-            frags<NT>(dz, b);
-            __syncthreads();   // images (W^T, dZ, H) complete
+        }
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            // H = act(xhat_hsrc * gamma + beta) (0 for rows past R)
+            const bool rok = rbase + IMR * u < R;
+            f32x4 hv[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                hv[t] = xn[u][t] * *(const f32x4*)(gH + 16 * t + 4 * g4) + *(const f32x4*)(gH + p16(CH) + 16 * t + 4 * g4);
+            act_tile<NT>(hv, actH);
+            if (!rok) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) hv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            put_img<NT, IS>(himg, hv, K, 128 * u + 16 * wv);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) xc[u][t] = xn[u][t];   // the next step's LN input
+        }
+        __syncthreads();   // images (W^T, dZ, H) complete
+        // dH_prev = W^T dz (dz as the B operand; the W^T image rows = K features)
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
             f32x4 nh[NT];
-            tile_gemm<NT, KS>(wimg, bs, (K + 15) >> 4, (N + 31) >> 5, b, nh);
+            tile_gemm<NT, KS>(wimg + G.bw, bs, (K + 15) >> 4, (N + 31) >> 5, b[u], nh);
             if (skp) {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) dh[u][t] += nh[t];
@@ -650,26 +766,9 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
 #pragma unroll
                 for (int t = 0; t < NT; ++t) dh[u][t] = nh[t];
             }
-            dw_half<TNS, TKS>(zimg, himg, ntn, ntk, acc);
         }
-        // dW | db partial of this workgroup
-        {
-            const int wn = wv >> 2, wk = wv & 3, K1 = K + 1;
-            float* dst = pb + G.wo;
-#pragma unroll
-            for (int a = 0; a < TNS; ++a)
-#pragma unroll
-                for (int c = 0; c < TKS; ++c) {
-                    const int tn = wn + 2 * a, tk = wk + 4 * c;
-                    if (tn >= ntn || tk >= ntk) continue;
-                    const int k = 16 * tk + lr;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int n = 16 * tn + 4 * g4 + i;
-                        if (n < N && k < K) dst[n * K1 + k] = acc[a][c][i];
-                    }
-                }
-        }
+        // dW over the block's rows -> this workgroup's partial (db: column K, from the column sums)
+        dw_img<TNS, TKS, ROWS, IS>(zimg, himg, N, K, pb + G.wo);
         flush_cols<NT>(red, la, lb, N, ln, ln ? pb + d.l[l].lpo : nullptr, pb + G.wo + K, K + 1);
     }
     // identity skip: d x0 += dout
@@ -678,12 +777,12 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
         for (int u = 0; u < TPW; ++u) {
             const int64_t row = rbase + IMR * u;
             f32x4 t2[NT];
-            load_rows<NT>(t2, dout, DL, row, row < R);
+            load_rows<NT>(t2, dout, DL, R, row);
 #pragma unroll
             for (int t = 0; t < NT; ++t) dh[u][t] += t2[t];
         }
     }
-    // input LayerNorm backward -> dx
+    // input LayerNorm backward -> dx (xc holds the input LN's xhat: the last step's H source)
     float la[NT], lb[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
@@ -691,11 +790,9 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
     for (int u = 0; u < TPW; ++u) {
         const int64_t row = rbase + IMR * u;
         const bool rok = row < R;
-        f32x4 xv[NT];
-        load_sv<NT>(xv, xh, d0, row, rok);
-        const float rstd = rok ? rs[row] : 0.f;
-        ln_bwd<NT>(dh[u], xv, rstd, d0, prm_in, prm_in + p16(d0), 0, la);
-        store_rows<NT>(dx, dh[u], d0, row, rok);
+        const float rstd = bld(brs(rs, Rp * 4), rok ? (unsigned)(row * 4) : OOB);
+        ln_bwd<NT>(dh[u], xc[u], rstd, d0, prm_in, prm_in + p16(d0), 0, la);
+        store_rows<NT>(dx, dh[u], d0, R, row);
     }
     __syncthreads();
     flush_cols<NT>(red, la, lb, d0, true, pb + d.lpo0, nullptr, 0);
@@ -814,7 +911,7 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
         VT_CHECK_ARG(G.W, "%s: projection skip without weight", who);
     }
     // forward LDS: images, then [bias, gamma, beta] per GEMM, then the input LN
-    int off = 0, po = 0, bw = 0, bh = 0, bz = 0;
+    int off = 0, po = 0, bw = 0, bwtot = 0, bh = 0, bz = 0;
     for (int g = 0; g < d.nG; ++g) {
         BG& G = d.G[g];
         G.fo = off;
@@ -824,7 +921,9 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
         G.po = po;
         po += 3 * h16(G.N);
         G.bs = h32(G.N) + 16;
-        const int e = h16(G.K) * G.bs;
+        const int e = (h16(G.K) * G.bs + 7) & ~7;
+        G.bw = bwtot;
+        bwtot += e;
         bw = e > bw ? e : bw;
         bh = h16(G.K) > bh ? h16(G.K) : bh;
         bz = h16(G.N) > bz ? h16(G.N) : bz;
@@ -834,7 +933,6 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
     d.fbytes = d.fimg + 4 * (po + 2 * h16(dims[0]));
     const int ntw = (wmax + 15) / 16;
     p.nt = ntw <= 2 ? 2 : ntw <= 4 ? 4 : ntw <= 6 ? 6 : 9;
-    d.bwimg = (bw + 7) & ~7;
     d.bhrows = bh;
     d.bzrows = bz;
     int bprm = 0;
@@ -845,7 +943,14 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
     d.bpin = bprm;
     bprm += 2 * h16(dims[0]);
     d.bprm = bprm;
-    d.bbytes = 2 * (d.bwimg + (bz + bh) * IMS) + 4 * (bprm + NW * 48 * p.nt);
+    p.tpw = p.nt >= 6 ? 1 : 2;
+    const int ims = IMR * p.tpw + 16;
+    const int rest = 2 * (bz + bh) * ims + 4 * (bprm + NW * 48 * p.nt);
+    d.bres = 2 * bwtot + rest <= 160 * 1024;  // all W^T images resident when they fit
+    if (!d.bres)
+        for (int g = 0; g < d.nG; ++g) d.G[g].bw = 0;
+    d.bwimg = d.bres ? bwtot : bw;
+    d.bbytes = 2 * d.bwimg + rest;
     // partials: dW|db of every GEMM, then gamma|beta of every LN and the input LN
     int P = 0;
     for (int g = 0; g < d.nG; ++g) {
@@ -860,7 +965,6 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
     P += 2 * dims[0];
     d.P = P;
     (void)lnp;
-    p.tpw = p.nt >= 9 ? 1 : 2;
     const int blk = IMR * p.tpw;
     p.Rp = (R + 2 * IMR - 1) / (2 * IMR) * (2 * IMR);   // the saved state is padded for either block size
     p.nblk = (R + blk - 1) / blk;
@@ -909,9 +1013,60 @@ const BDesc* device_desc(const BDesc& d, hipStream_t st) {
     return e.dev;
 }
 
+// every kernel may use the whole LDS: set once per instantiation
 template <typename Kern>
-void set_lds(Kern k, int bytes) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+void set_lds(Kern k, int) {
+    static bool done = false;
+    if (!done) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        done = true;
+    }
+}
+
+// Plans (host descriptor + device copy) cached by their arguments: the training
+// step calls every stack with the same widths, parameter pointers and rows.
+struct PlanEntry {
+    std::vector<int64_t> key;
+    BPlan plan;
+    const BDesc* dev;
+};
+
+int get_plan(const BPlan*& out, const BDesc*& dev, int n_layers, const int* dims, const int* layer_ln,
+             const int* layer_act, int skip, float eps, const float* const* params, int64_t R, hipStream_t st,
+             const char* who) {
+    static std::unordered_map<uint64_t, std::vector<PlanEntry>> cache;
+    static std::mutex mu;
+    VT_CHECK_ARG(n_layers >= 1 && n_layers <= MAXL, "%s: n_layers %d not in [1, %d]", who, n_layers, MAXL);
+    std::vector<int64_t> key;
+    key.reserve(8 + 3 * n_layers + 4 * n_layers + 4);
+    key.push_back(n_layers);
+    key.push_back(skip);
+    key.push_back(R);
+    key.push_back(__builtin_bit_cast(int, eps));
+    for (int i = 0; i <= n_layers; ++i) key.push_back(dims[i]);
+    for (int i = 0; i < n_layers; ++i) key.push_back(layer_ln[i] * 16 + layer_act[i]);
+    for (int i = 0; i < 4 * n_layers + 4; ++i) key.push_back(reinterpret_cast<int64_t>(params[i]));
+    uint64_t h = 1469598103934665603ull;
+    for (int64_t v : key) h = (h ^ (uint64_t)v) * 1099511628211ull;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& bucket = cache[h];
+    for (const PlanEntry& e : bucket)
+        if (e.key == key) {
+            out = &e.plan;
+            dev = e.dev;
+            return VT_OK;
+        }
+    PlanEntry e;
+    const int rc = make_bplan(e.plan, n_layers, dims, layer_ln, layer_act, skip, eps, params, R, who);
+    if (rc) return rc;
+    e.dev = device_desc(e.plan.d, st);
+    VT_CHECK_ARG(e.dev, "%s: descriptor upload failed", who);
+    e.key = std::move(key);
+    bucket.push_back(std::move(e));
+    out = &bucket.back().plan;
+    dev = bucket.back().dev;
+    return VT_OK;
 }
 
 }  // namespace
@@ -937,14 +1092,15 @@ int vt_resmlp_bf16_sizes(int n_layers, const int* dims, const int* layer_ln, con
 int vt_resmlp_bf16_fwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
                        const float* const* params, const float* x, int64_t rows, float* out, float* xhat, float* rstd,
                        void* stream) {
-    BPlan p;
-    const int rc = make_bplan(p, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, "vt_resmlp_bf16_fwd");
+    hipStream_t st = S(stream);
+    const BPlan* pp;
+    const BDesc* ddev;
+    const int rc = get_plan(pp, ddev, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, st,
+                            "vt_resmlp_bf16_fwd");
     if (rc) return rc;
+    const BPlan& p = *pp;
     VT_CHECK_ARG(x && out && xhat && rstd, "vt_resmlp_bf16_fwd: null buffer");
     const dim3 grid((unsigned)n_fwd_blocks(rows));
-    hipStream_t st = S(stream);
-    const BDesc* ddev = device_desc(p.d, st);
-    VT_CHECK_ARG(ddev, "vt_resmlp_bf16_fwd: descriptor upload failed");
     const bool id = skip == 1;
     switch (p.nt * 2 + (id ? 1 : 0)) {
 #define VT_MBF(NTV, IDV)                                                                                   \
@@ -965,9 +1121,13 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
                        const float* const* params, const float* dout, const float* xhat, const float* rstd,
                        int64_t rows, float* dx, float* const* grads, int accumulate, float* ws, int64_t ws_floats,
                        void* stream) {
-    BPlan p;
-    const int rc = make_bplan(p, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, "vt_resmlp_bf16_bwd");
+    hipStream_t st = S(stream);
+    const BPlan* pp;
+    const BDesc* ddev;
+    const int rc = get_plan(pp, ddev, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, st,
+                            "vt_resmlp_bf16_bwd");
     if (rc) return rc;
+    const BPlan& p = *pp;
     VT_CHECK_ARG(dout && xhat && rstd && dx && grads, "vt_resmlp_bf16_bwd: null buffer");
     VT_CHECK_ARG(ws && ws_floats >= p.nblk * p.d.P, "vt_resmlp_bf16_bwd: workspace %lld floats < %lld",
                  (long long)ws_floats, (long long)(p.nblk * p.d.P));
@@ -986,10 +1146,7 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
     for (int l = 0; l < n_layers; ++l)
         if (p.d.l[l].ln) add(2 * p.d.G[l].N, p.d.G[l].N, 0, p.d.l[l].lpo, grads[4 + 4 * l], grads[5 + 4 * l]);
     add(2 * dims[0], dims[0], 0, p.d.lpo0, grads[0], grads[1]);
-    hipStream_t st = S(stream);
     const dim3 grid((unsigned)p.nblk);
-    const BDesc* ddev = device_desc(p.d, st);
-    VT_CHECK_ARG(ddev, "vt_resmlp_bf16_bwd: descriptor upload failed");
     switch (p.nt) {
 #define VT_MBB(NTV, TPWV)                                                                                        \
     case NTV:                                                                                              \
@@ -997,7 +1154,7 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
         hipLaunchKernelGGL((k_mlpb_bwd<NTV, TPWV>), grid, dim3(BT), p.d.bbytes, st, ddev, dout, xhat, rstd, rows, \
                            p.Rp, dx, ws);                                                                  \
         break;
-        VT_MBB(2, 2) VT_MBB(4, 2) VT_MBB(6, 2)
+        VT_MBB(2, 2) VT_MBB(4, 2) VT_MBB(6, 1)
         default: VT_MBB(9, 1)
 #undef VT_MBB
     }
