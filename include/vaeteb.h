@@ -83,6 +83,11 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
  * previous setting (not an error code).  Not thread-safe: set before launching. */
 int vt_fe_set_pairs_direct(int on);
 
+/* Diagnostic (tools/pairs_phases.py): while buf != NULL, training-geometry vt_fe_pairs
+ * launches stamp wave 0's wall clock (100 MHz) at each phase boundary into
+ * buf[(b * n_pairs + pair) * 8 + phase] (uint64).  NULL turns it off. */
+int vt_fe_set_pairs_stamps(void* buf);
+
 /* Per-channel transform (kind 0 none, 1 log(max(x,0)+log_eps), 2 asinh) and
  * z-score (x-mean)/(std+1e-8); in[b, c, s] (batch stride in_C*S) -> out[b, s, out_off + c]
  * (row width out_C).

@@ -26,7 +26,11 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <mutex>
+#include <vector>
+
 #include "common.h"
+#include "cfft.h"
 #include "fft.h"
 
 namespace vt {
@@ -185,46 +189,6 @@ __device__ __forceinline__ int pr_pos(int idx) {  // natural index -> padded LDS
     return (idx >> 5) * 33 + (idx & 31);
 }
 
-__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // a * (-i)
-
-// forward DFT-4 in place: X[k] = sum_n x[n] (-i)^{nk}
-__device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
-    const float2 s02 = cadd(x0, x2), d02 = csub(x0, x2), s13 = cadd(x1, x3), d13 = mul_mi(csub(x1, x3));
-    x0 = cadd(s02, s13);
-    x2 = csub(s02, s13);
-    x1 = cadd(d02, d13);
-    x3 = csub(d02, d13);
-}
-
-// forward DFT-16 in registers, natural order in and out (4 x 4, twiddles W_16)
-__device__ __forceinline__ void dft16(float2 v[16]) {
-#pragma unroll
-    for (int n0 = 0; n0 < 4; ++n0) dft4(v[n0], v[n0 + 4], v[n0 + 8], v[n0 + 12]);  // -> a[n0][k1] at v[n0 + 4 k1]
-    const float c1 = 0.92387953251128674f, s1 = 0.38268343236508977f, r2 = 0.70710678118654752f;
-    // v[n0 + 4 k1] *= W16^{n0 k1}
-    v[5] = cmul(v[5], make_float2(c1, -s1));
-    v[9] = cmul(v[9], make_float2(r2, -r2));
-    v[13] = cmul(v[13], make_float2(s1, -c1));
-    v[6] = cmul(v[6], make_float2(r2, -r2));
-    v[10] = mul_mi(v[10]);
-    v[14] = cmul(v[14], make_float2(-r2, -r2));
-    v[7] = cmul(v[7], make_float2(s1, -c1));
-    v[11] = cmul(v[11], make_float2(-r2, -r2));
-    v[15] = cmul(v[15], make_float2(-c1, s1));
-    float2 o[16];
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) {
-        float2 a0 = v[4 * k1], a1 = v[4 * k1 + 1], a2 = v[4 * k1 + 2], a3 = v[4 * k1 + 3];
-        dft4(a0, a1, a2, a3);  // over n0 -> k0
-        o[k1] = a0;
-        o[k1 + 4] = a1;
-        o[k1 + 8] = a2;
-        o[k1 + 12] = a3;
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = o[i];
-}
-
 // |a| e^{i p arg(a)} for the phase acceleration, in revolutions: atan2 by an
 // odd minimax polynomial of atan on [0, 1] (max error 1.3e-7 rad, fp32), the
 // angle times p reduced to [-1/2, 1/2] revolution, then the hardware
@@ -254,137 +218,159 @@ __device__ __forceinline__ float2 accel(float2 a, float p) {
     return make_float2(mag * __builtin_amdgcn_cosf(v), mag * __builtin_amdgcn_sinf(v));
 }
 
-// W_32^n = exp(-2 pi i n / 32)
-constexpr float W32_RE[32] = {1.f, 0.980785251f, 0.923879504f, 0.831469595f, 0.707106769f, 0.555570245f,
-                                 0.382683426f, 0.195090324f, 0.f, -0.195090324f, -0.382683426f, -0.555570245f,
-                                 -0.707106769f, -0.831469595f, -0.923879504f, -0.980785251f, -1.f, -0.980785251f,
-                                 -0.923879504f, -0.831469595f, -0.707106769f, -0.555570245f, -0.382683426f,
-                                 -0.195090324f, 0.f, 0.195090324f, 0.382683426f, 0.555570245f, 0.707106769f,
-                                 0.831469595f, 0.923879504f, 0.980785251f};
+// XCD-aware workgroup order: the hardware deals consecutive workgroups round-robin
+// to the 8 XCDs, so the linear id is remapped to give each XCD a contiguous run of
+// (sample, pair) items — the pairs of one sample then share that XCD's L2 copy of
+// the sample's analytic signals instead of every XCD fetching them.
+__device__ __forceinline__ int xcd_item(int L, int total) {
+    return (total & 7) == 0 ? (L & 7) * (total >> 3) + (L >> 3) : L;
+}
 
 // G: the training geometry (N 4096, reflect pad 2048 each side) with every
 // length and pad index a compile-time constant (no bounds checks, the reflection
 // of each radix-16 column is known per n2); otherwise the runtime arguments.
-template <bool G, bool D = false>
+// D: product columns formed straight from HBM / L2 (no LDS staging pass).
+// P: diagnostic build stamping wave 0's wall clock at each phase boundary into
+// stamps[(b * n_pairs + pair) * 8 + phase] (vt_fe_set_pairs_stamps).
+// tab: the TW8K_* tables (cfft.h).  One (sample, pair) per workgroup, 1-D grid.
+#define PR_STAMP(i)                                                                           \
+    do {                                                                                      \
+        if constexpr (P) {                                                                    \
+            if (t == 0) stamps[((int64_t)b * n_pairs + pair) * 8 + (i)] = wall_clock64();    \
+        }                                                                                     \
+    } while (0)
+static constexpr int PR_ZP = PR_NB + PR_NB / 8;  // padded 512-point buffer (z512_pos)
+template <bool G, bool D = false, bool P = false>
 __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
-    const float2* __restrict__ analytic, int n_slots, int N_, int pad_left_, int n_pairs,
+    const float2* __restrict__ analytic, int n_slots, int N_, int pad_left_, int n_pairs, int B,
     const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
-    const float2* __restrict__ tw, const float* __restrict__ phi0, int start, int S, int pad_mode_,
-    float* __restrict__ out) {
+    const float2* __restrict__ tab, const float* __restrict__ phi0, int start, int S, int pad_mode_,
+    float* __restrict__ out, unsigned long long* __restrict__ stamps) {
+    static_assert(PR_T == 512, "one padded column per thread");
     const int N = G ? 4096 : N_, pad_left = G ? 2048 : pad_left_, pad_mode = G ? 0 : pad_mode_;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     float2* img = sm;               // PR_IMG
-    float2* Z = sm + PR_IMG;        // PR_NB
-    float2* Z2 = Z + PR_NB;         // PR_NB
+    float2* Z = sm + PR_IMG;        // PR_ZP
     const int t = threadIdx.x;
-    const int pair = blockIdx.x;
-    const int64_t b = blockIdx.y;
+    const int item = xcd_item(blockIdx.x, n_pairs * B);
+    const int pair = item % n_pairs;
+    const int64_t b = item / n_pairs;
     const float2* ai = analytic + (b * n_slots + slot_i[pair]) * (int64_t)N;
     const float2* aj = analytic + (b * n_slots + slot_j[pair]) * (int64_t)N;
     const float pw = power[pair];
+    // pass-3 output bin of this thread and its low-pass weight (loaded up front)
+    const int j3 = t & 255, ka = t >> 8, k2_3 = j3 >> 4, kb_3 = j3 & 15;
+    const int k3 = k2_3 + 16 * kb_3 + 256 * ka;
+    const float ph3 = phi0[k3];
+    PR_STAMP(0);
+    c2 v[16];
     if constexpr (D) {
         // 0+1 fused (training geometry only): column n1 = t of the reflect-padded product
         // straight from HBM / L2, the product formed in registers (each sample of the
         // signal is visited twice, once per reflection), first radix-16 pass, no staging
-        static_assert(G && PR_T == 512, "direct columns: training geometry, one column per thread");
-        float2 v[16];
-        {
-            float2 xa[16], xb[16];
-#pragma unroll
-            for (int n2 = 0; n2 < 16; ++n2) {
-                const int i = t + 512 * n2 - 2048;
-                const int s = n2 < 4 ? -i : (n2 < 12 ? i : 2 * 4096 - 2 - i);
-                xa[n2] = ai[s];
-                xb[n2] = aj[s];
-            }
-#pragma unroll
-            for (int n2 = 0; n2 < 16; ++n2) v[n2] = cmul(accel(xa[n2], pw), cconj(xb[n2]));
-        }
-        dft16(v);
-        img[pr_pos(t)] = v[0];
-#pragma unroll
-        for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(t + 512 * k2)] = cmul(v[k2], tw[(t * k2) & (PR_N - 1)]);
-    } else {
-    // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283), compact;
-    // loads in batches of 8 per thread (all in flight before the first use)
-    for (int u0 = t; u0 < N; u0 += PR_T * 8) {
-        float2 xa[8], xb[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int u = u0 + PR_T * k;
-            xa[k] = u < N ? ai[u] : make_float2(0.f, 0.f);
-            xb[k] = u < N ? aj[u] : make_float2(0.f, 0.f);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int u = u0 + PR_T * k;
-            if (u < N) img[u] = cmul(accel(xa[k], pw), cconj(xb[k]));
-        }
-    }
-    __syncthreads();
-    // 1: columns n1 = t (+ PR_T) of the padded signal (reflect / zero / circular);
-    // one reflection at most on the training geometry (no modulo)
-    const bool single = pad_mode == 0 && pad_left <= N - 1 && PR_N - pad_left - N <= N - 1;
-    float2 v[512 / PR_T][16];
-#pragma unroll
-    for (int q = 0; q < 512 / PR_T; ++q) {
-        const int n1 = t + PR_T * q;
+        static_assert(G, "direct columns: training geometry");
+        float2 xa[16], xb[16];
 #pragma unroll
         for (int n2 = 0; n2 < 16; ++n2) {
-            const int i = n1 + 512 * n2 - pad_left;
+            const int i = t + 512 * n2 - 2048;
+            const int s = n2 < 4 ? -i : (n2 < 12 ? i : 2 * 4096 - 2 - i);
+            xa[n2] = ai[s];
+            xb[n2] = aj[s];
+        }
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) v[n2] = pmulc(C2(accel(xa[n2], pw)), C2(xb[n2]));
+    } else {
+        // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283), compact;
+        // loads in batches of 8 per thread (all in flight before the first use)
+        for (int u0 = t; u0 < N; u0 += PR_T * 8) {
+            float2 xa[8], xb[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int u = u0 + PR_T * k;
+                xa[k] = (G || u < N) ? ai[u] : make_float2(0.f, 0.f);
+                xb[k] = (G || u < N) ? aj[u] : make_float2(0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int u = u0 + PR_T * k;
+                if (G || u < N) img[u] = F2(pmulc(C2(accel(xa[k], pw)), C2(xb[k])));
+            }
+        }
+        PR_STAMP(1);
+        __syncthreads();
+        // 1: column n1 = t of the padded signal (reflect / zero / circular); one
+        // reflection at most on the training geometry (no modulo)
+        const bool single = pad_mode == 0 && pad_left <= N - 1 && PR_N - pad_left - N <= N - 1;
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) {
+            const int i = t + 512 * n2 - pad_left;
             const int s = G ? (n2 < 4 ? -i : (n2 < 12 ? i : 2 * N - 2 - i))
                             : single ? (i < 0 ? -i : (i >= N ? 2 * N - 2 - i : i)) : pad_src(i, N, pad_mode);
-            v[q][n2] = s < 0 ? make_float2(0.f, 0.f) : img[s];
+            v[n2] = s < 0 ? c2{0.f, 0.f} : C2(img[s]);
         }
+        __syncthreads();
     }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 512 / PR_T; ++q) {
-        const int n1 = t + PR_T * q;
-        dft16(v[q]);
-        img[pr_pos(n1)] = v[q][0];
-#pragma unroll
-        for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(n1 + 512 * k2)] = cmul(v[q][k2], tw[(n1 * k2) & (PR_N - 1)]);
-    }
-    }
-    __syncthreads();
-    // 2: jobs (k2, n1a): radix-16 over n1b inside block k2, in place
-#pragma unroll
-    for (int q = 0; q < 512 / PR_T; ++q) {
-        const int job = t + PR_T * q, k2 = job >> 5, n1a = job & 31;
-        float2* base = img + k2 * 528 + n1a;
-        float2 w[16];
-#pragma unroll
-        for (int n1b = 0; n1b < 16; ++n1b) w[n1b] = base[33 * n1b];
-        dft16(w);
-        base[0] = w[0];
-#pragma unroll
-        for (int kb = 1; kb < 16; ++kb) base[33 * kb] = cmul(w[kb], tw[(16 * n1a * kb) & (PR_N - 1)]);
-    }
-    __syncthreads();
-    // 3: (k2, k'b) = (j >> 4, j & 15), j = t & 255: output k'a = t >> 8 (0 or 1) of the radix-32 stage
     {
-        const int j = t & 255, ka = t >> 8, k2 = j >> 4, kb = j & 15;
-        const float2* row = img + k2 * 528 + 33 * kb;
-        float2 x = make_float2(0.f, 0.f);
+        c2 w[15];
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) w[k2 - 1] = C2(tab[TW8K_T1 + 512 * (k2 - 1) + t]);
+        pdft16(v);
+        img[pr_pos(t)] = F2(v[0]);
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(t + 512 * k2)] = F2(pmul(v[k2], w[k2 - 1]));
+    }
+    PR_STAMP(2);
+    __syncthreads();
+    // 2: job (k2, n1a) = (t >> 5, t & 31): radix-16 over n1b inside block k2, in place
+    {
+        const int k2 = t >> 5, n1a = t & 31;
+        float2* base = img + k2 * 528 + n1a;
+        c2 w[15], x[16];
+#pragma unroll
+        for (int kb = 1; kb < 16; ++kb) w[kb - 1] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
+#pragma unroll
+        for (int n1b = 0; n1b < 16; ++n1b) x[n1b] = C2(base[33 * n1b]);
+        pdft16(x);
+        base[0] = F2(x[0]);
+#pragma unroll
+        for (int kb = 1; kb < 16; ++kb) base[33 * kb] = F2(pmul(x[kb], w[kb - 1]));
+    }
+    PR_STAMP(3);
+    __syncthreads();
+    // 3: (k2, k'b) = (j >> 4, j & 15), j = t & 255: output k'a = t >> 8 (0 or 1) of the
+    // radix-32 stage; Z holds conj(X phi0) so that the 512-point inverse below is a
+    // forward transform whose real part is the result
+    {
+        const float2* row = img + k2_3 * 528 + 33 * kb_3;
+        c2 x = C2(row[0]);
         if (ka == 0) {
 #pragma unroll
-            for (int n1a = 0; n1a < 32; ++n1a) x = cadd(x, row[n1a]);
+            for (int n1a = 1; n1a < 32; ++n1a) x += C2(row[n1a]);
         } else {
 #pragma unroll
-            for (int n1a = 0; n1a < 32; ++n1a)
-                x = cadd(x, cmul(row[n1a], make_float2(W32_RE[n1a], W32_RE[(n1a + 8) & 31])));  // W_32^{n1a}
+            for (int n1a = 1; n1a < 32; ++n1a) x = pmac(x, C2(row[n1a]), w32(n1a));  // W_32^{n1a}
         }
-        const int k = k2 + 16 * kb + 256 * ka;
-        Z[k] = cscale(x, phi0[k]);
+        Z[z512_pos(k3)] = make_float2(x.x * ph3, -x.y * ph3);
     }
+    PR_STAMP(4);
     __syncthreads();
-    // 4: inverse FFT of length 512, keep [start, start + S)
-    float2* Rs = fft_lds<true>(Z, Z2, PR_NB, tw, PR_N / PR_NB);
-    float* o = out + (b * n_pairs + pair) * (int64_t)S;
-    const float inv = 1.0f / (float)PR_NB;
-    for (int m = t; m < S; m += PR_T) o[m] = Rs[start + m].x * inv;
+    // 4: inverse FFT of length 512 by wave 0, keep the real part of [start, start + S)
+    if (t < 64) {
+        c2 r[8];
+        wave_fft512(Z, tab, r);
+        PR_STAMP(5);
+        float* o = out + (b * n_pairs + pair) * (int64_t)S;
+        const float inv = 1.0f / (float)PR_NB;
+        const int k0 = (t >> 3) + 8 * (t & 7);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int m = k0 + 64 * j - start;
+            if (m >= 0 && m < S) o[m] = r[j].x * inv;
+        }
+        PR_STAMP(6);
+    }
 }
+#undef PR_STAMP
 
 // ------------------------------------------- wavelets, 8192-point register FFT
 // Inverse FFT of xhat * psi for the training geometry (n_pad = 8192) as the
@@ -395,81 +381,65 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
 // (padded every 32) for the coalesced analytic-signal copy and the S1
 // low-pass.  One 66 KB image: two workgroups per CU (the generic Stockham
 // path ping-pongs two 64 KB buffers: one).
-__device__ __forceinline__ void dft32(float2 v[32]) {
-    float2 e[16], o[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        e[i] = v[2 * i];
-        o[i] = v[2 * i + 1];
-    }
-    dft16(e);
-    dft16(o);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const float2 w = cmul(o[k], make_float2(W32_RE[k], W32_RE[(k + 8) & 31]));
-        v[k] = cadd(e[k], w);
-        v[k + 16] = csub(e[k], w);
-    }
-}
-
 __device__ __forceinline__ int nat_pos(int k) { return k + (k >> 5); }  // natural order, padded every 32
 
 __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
-    const float2* __restrict__ xhat, int C, const float* __restrict__ psi, const int* __restrict__ items,
-    const float2* __restrict__ tw, int N, int pad_left, float2* __restrict__ analytic, int n_slots,
+    const float2* __restrict__ xhat, int C, const float* __restrict__ psi, const int* __restrict__ items, int n_items,
+    int B, const float2* __restrict__ tab, int N, int pad_left, float2* __restrict__ analytic, int n_slots,
     const float* __restrict__ h0, int radius, int step, int start, int S, float* __restrict__ s1, int s1_channels,
     int nowrap) {
+    static_assert(PR_T == 512, "one column per thread");
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     float2* img = sm;  // PR_IMG
     const int t = threadIdx.x;
-    const int item = blockIdx.x;
-    const int64_t b = blockIdx.y;
+    const int L = xcd_item(blockIdx.x, n_items * B);  // XCD-aware: one sample's items share an L2
+    const int item = L % n_items;
+    const int64_t b = L / n_items;
     const int chan = items[item * 5 + 0], filt = items[item * 5 + 1], slot = items[item * 5 + 2];
     const int s1ch = items[item * 5 + 3], k1 = items[item * 5 + 4];
     const float2* xh = xhat + (b * C + chan) * (int64_t)PR_N;
     const float* ps = psi + (int64_t)filt * PR_N;
-    // pass 1: columns n1 = t (+ PR_T) of conj(xhat * psi), straight from HBM
-    float2 v[512 / PR_T][16];
-#pragma unroll
-    for (int q = 0; q < 512 / PR_T; ++q)
+    // pass 1: column n1 = t of conj(xhat * psi), straight from HBM
+    {
+        c2 v[16], w[15];
 #pragma unroll
         for (int n2 = 0; n2 < 16; ++n2) {
-            const int n = t + PR_T * q + 512 * n2;
+            const int n = t + 512 * n2;
             const float2 x = xh[n];
             const float p = ps[n];
-            v[q][n2] = make_float2(x.x * p, -x.y * p);
+            v[n2] = c2{x.x * p, -x.y * p};
         }
 #pragma unroll
-    for (int q = 0; q < 512 / PR_T; ++q) {
-        const int n1 = t + PR_T * q;
-        dft16(v[q]);
-        img[pr_pos(n1)] = v[q][0];
+        for (int k2 = 1; k2 < 16; ++k2) w[k2 - 1] = C2(tab[TW8K_T1 + 512 * (k2 - 1) + t]);
+        pdft16(v);
+        img[pr_pos(t)] = F2(v[0]);
 #pragma unroll
-        for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(n1 + 512 * k2)] = cmul(v[q][k2], tw[(n1 * k2) & (PR_N - 1)]);
+        for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(t + 512 * k2)] = F2(pmul(v[k2], w[k2 - 1]));
     }
     __syncthreads();
     // pass 2: radix-16 over n1b inside block k2 (as k_fe_pairs8k)
-#pragma unroll
-    for (int q = 0; q < 512 / PR_T; ++q) {
-        const int job = t + PR_T * q, k2 = job >> 5, n1a = job & 31;
+    {
+        const int k2 = t >> 5, n1a = t & 31;
         float2* base = img + k2 * 528 + n1a;
-        float2 w[16];
+        c2 w[15], x[16];
 #pragma unroll
-        for (int n1b = 0; n1b < 16; ++n1b) w[n1b] = base[33 * n1b];
-        dft16(w);
-        base[0] = w[0];
+        for (int kb = 1; kb < 16; ++kb) w[kb - 1] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
 #pragma unroll
-        for (int kb = 1; kb < 16; ++kb) base[33 * kb] = cmul(w[kb], tw[(16 * n1a * kb) & (PR_N - 1)]);
+        for (int n1b = 0; n1b < 16; ++n1b) x[n1b] = C2(base[33 * n1b]);
+        pdft16(x);
+        base[0] = F2(x[0]);
+#pragma unroll
+        for (int kb = 1; kb < 16; ++kb) base[33 * kb] = F2(pmul(x[kb], w[kb - 1]));
     }
     __syncthreads();
     // pass 3: full radix-32 over n1a: X[k2 + 16 kb + 256 ka] (256 jobs)
     const int k2 = (t & 255) >> 4, kb = t & 15;
-    float2 r[32];
+    c2 r[32];
     if (t < 256) {
         const float2* row = img + k2 * 528 + 33 * kb;
 #pragma unroll
-        for (int n1a = 0; n1a < 32; ++n1a) r[n1a] = row[n1a];
-        dft32(r);
+        for (int n1a = 0; n1a < 32; ++n1a) r[n1a] = C2(row[n1a]);
+        pdft32(r);
     }
     __syncthreads();
     const float inv_n = 1.0f / (float)PR_N;
@@ -660,6 +630,42 @@ __global__ void k_pad_reflect(const float* __restrict__ in, float* __restrict__ 
 }
 
 static inline bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+
+// The TW8K_* twiddle tables (cfft.h) of the current device, built in fp64 on the
+// first training-geometry call (69 KB, synchronous copy: that call must not be
+// under stream capture — the first front-end call of a run is eager).
+static const float2* tw8k_tables(hipStream_t st) {
+    static std::mutex mu;
+    static float2* tabs[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (tabs[dev] == nullptr) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+        std::vector<float2> h(TW8K_N);
+        auto w = [](long m, long n) {
+            const double a = -2.0 * M_PI * (double)(m % n) / (double)n;
+            return make_float2((float)cos(a), (float)sin(a));
+        };
+        for (int k = 1; k < 16; ++k)
+            for (int n = 0; n < 512; ++n) h[TW8K_T1 + 512 * (k - 1) + n] = w((long)n * k, 8192);
+        for (int k = 1; k < 16; ++k)
+            for (int n = 0; n < 32; ++n) h[TW8K_T2 + 32 * (k - 1) + n] = w((long)n * k, 512);
+        for (int q = 1; q < 8; ++q)
+            for (int l = 0; l < 64; ++l) h[TW8K_TA + 64 * (q - 1) + l] = w((long)l * q, 512);
+        for (int r = 1; r < 8; ++r)
+            for (int l = 0; l < 8; ++l) h[TW8K_TB + 8 * (r - 1) + l] = w((long)l * r, 64);
+        float2* d = nullptr;
+        if (hipMalloc(&d, sizeof(float2) * TW8K_N) != hipSuccess) return nullptr;
+        if (hipMemcpy(d, h.data(), sizeof(float2) * TW8K_N, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return nullptr;
+        }
+        tabs[dev] = d;
+    }
+    return tabs[dev];
+}
 static inline size_t fft_lds_bytes(int n) { return (size_t)2 * n * sizeof(float2); }
 
 }  // namespace vt
@@ -698,9 +704,12 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
     if (n_pad == PR_N && pad_left + N <= PR_N) {
         // the training geometry: register FFT, one 66 KB image
         const int nowrap = step * (start + S_out - 1) + radius < n_pad ? 1 : 0;
-        hipLaunchKernelGGL(k_fe_wavelet8k, dim3(n_items, (unsigned)B), dim3(PR_T), PR_IMG * sizeof(float2), S(stream),
-                           (const float2*)xhat, C, psi, items, (const float2*)tw, N, pad_left, (float2*)analytic,
-                           n_slots, h0, radius, step, start, S_out, s1, s1_channels, nowrap);
+        const float2* tab = tw8k_tables(S(stream));
+        VT_CHECK_ARG(tab != nullptr, "vt_fe_wavelet: twiddle tables unavailable (first call under stream capture?)");
+        VT_CHECK_ARG((int64_t)n_items * B < (1ll << 31), "vt_fe_wavelet: grid");
+        hipLaunchKernelGGL(k_fe_wavelet8k, dim3((unsigned)(n_items * B)), dim3(PR_T), PR_IMG * sizeof(float2),
+                           S(stream), (const float2*)xhat, C, psi, items, n_items, (int)B, tab, N, pad_left,
+                           (float2*)analytic, n_slots, h0, radius, step, start, S_out, s1, s1_channels, nowrap);
     } else {
         hipLaunchKernelGGL(k_fe_wavelet, dim3(n_items, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad),
                            S(stream), (const float2*)xhat, C, n_pad, psi, n_items, items, (const float2*)tw, N,
@@ -710,6 +719,7 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
     return VT_OK;
 }
 
+static unsigned long long* g_pairs_stamps = nullptr;  // diagnostic phase stamps (nullptr: off)
 static int g_pairs_direct = -1;  // -1: not yet read from VAETEB_PAIRS_DIRECT
 static int pairs_direct() {
     if (g_pairs_direct < 0) {
@@ -727,6 +737,14 @@ int vt_fe_set_pairs_direct(int on) {
     return prev;
 }
 
+// Diagnostic: stamp the phase boundaries of the training-geometry pair kernel
+// (LDS-staged variant) into buf, 8 uint64 per (sample, pair), successive launches
+// one after the other; nullptr turns it off.
+int vt_fe_set_pairs_stamps(void* buf) {
+    g_pairs_stamps = (unsigned long long*)buf;
+    return VT_OK;
+}
+
 int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
                 const int* slot_i, const int* slot_j, const float* power, const void* tw, const float* phi0, int dec,
                 int start, int S_out, int pad_mode, float* out, void* stream) {
@@ -741,10 +759,15 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
         // slower in the training step, where the phase and cross launches run concurrently
         // and the doubled L2 reads compete (1.19 -> 1.32 ms per launch): opt-in
         const bool direct = pairs_direct() != 0;
-        hipLaunchKernelGGL(geo ? (direct ? k_fe_pairs8k<true, true> : k_fe_pairs8k<true, false>) : k_fe_pairs8k<false>, dim3(n_pairs, (unsigned)B), dim3(PR_T),
-                           (PR_IMG + 2 * PR_NB) * sizeof(float2), S(stream), (const float2*)analytic, n_slots, N,
-                           pad_left, n_pairs, slot_i, slot_j, power, (const float2*)tw, phi0, start, S_out, pad_mode,
-                           out);
+        auto kern = geo ? (direct ? k_fe_pairs8k<true, true> : k_fe_pairs8k<true, false>) : k_fe_pairs8k<false>;
+        if (g_pairs_stamps != nullptr) kern = geo && !direct ? k_fe_pairs8k<true, false, true> : kern;
+        const float2* tab = tw8k_tables(S(stream));
+        VT_CHECK_ARG(tab != nullptr, "vt_fe_pairs: twiddle tables unavailable (first call under stream capture?)");
+        VT_CHECK_ARG((int64_t)n_pairs * B < (1ll << 31), "vt_fe_pairs: grid");
+        hipLaunchKernelGGL(kern, dim3((unsigned)(n_pairs * B)), dim3(PR_T), (PR_IMG + PR_ZP) * sizeof(float2),
+                           S(stream), (const float2*)analytic, n_slots, N, pad_left, n_pairs, (int)B, slot_i, slot_j,
+                           power, tab, phi0, start, S_out, pad_mode, out, g_pairs_stamps);
+        if (g_pairs_stamps != nullptr && geo && !direct) g_pairs_stamps += (size_t)B * n_pairs * 8;  // next launch after
     } else {
         hipLaunchKernelGGL(k_fe_pairs, dim3(n_pairs, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
                            (const float2*)analytic, n_slots, N, n_pad, pad_left, n_pairs, slot_i, slot_j, power,
