@@ -220,6 +220,13 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the model step as a captured hipGraph (double-buffered, front-end one step ahead) "
                          "instead of dispatching every op from Python (default: eager, currently faster)")
+    ap.add_argument("--native", action="store_true",
+                    help="graph mode replayed by the library's multi-stream executor (vt_stepgraph_*) instead of "
+                         "hipGraphLaunch; the reparameterisation noise is drawn eagerly each step")
+    ap.add_argument("--streams", type=int, default=4, help="--native: executor streams")
+    ap.add_argument("--overlap-fe", action="store_true",
+                    help="--native: run the next batch's front-end one step ahead on its own stream (as --graph) "
+                         "instead of inline before each replay")
     ap.add_argument("--prefetch", action="store_true",
                     help="eager mode: overlap the next batch's front-end with the current step on its own streams "
                          "(measured slower on MI355X: the front-end's LDS-heavy workgroups delay the latency-bound "
@@ -275,7 +282,7 @@ def main():
     work = dict(MFMA_CALLS)
     work["vt_fe_pairs"] = lambda an, B, n_slots, N, n_pad, pad_left, n_pairs, *a: B * n_pairs * (2 * N * 8 + a[7] * 4)
     timer = KernelTimer(["vt_fe_pairs", *MFMA_CALLS], flops=work)
-    graph = args.graph
+    graph = args.graph or args.native
     if graph:
         # The model step (forward, backward, clip, AdamW) is replayed as a
         # hipGraph.  The front-end (~10 launches, independent of the weights)
@@ -284,7 +291,12 @@ def main():
         # previous step's replay; the roofline kernel is still timed live with
         # HIP events in every step.
         fe_stream = torch.cuda.Stream()
-        caps = [trainer.capture(fe(pool[0])), trainer.capture(fe(pool[1]))]
+        if args.native:
+            eps_shape = (B, S, model.latent_dim_z)
+            caps = [trainer.capture(fe(pool[j]), eps=torch.randn(eps_shape, device=dev), native=True,
+                                    n_streams=args.streams) for j in range(2)]
+        else:
+            caps = [trainer.capture(fe(pool[0])), trainer.capture(fe(pool[1]))]
         main = torch.cuda.current_stream()
         ready = [torch.cuda.Event(), torch.cuda.Event()]
         done = [torch.cuda.Event(), torch.cuda.Event()]
@@ -300,10 +312,18 @@ def main():
 
         def step(i, last=False):
             slot = i % 2
+            if args.native and not args.overlap_fe:
+                # the step's own front-end first, on the same stream (as the eager step), then
+                # this step's noise (drawn outside the graph) and the replay
+                fe(pool[i % 2], out=caps[0].static_in)
+                torch.randn(caps[0].static_eps.shape, out=caps[0].static_eps)
+                return caps[0].replay()
             if i == 0 or step.first:
                 frontend_into(i)
                 step.first = False
             main.wait_event(ready[slot])
+            if args.native:                         # this step's noise, drawn outside the graph
+                torch.randn(caps[slot].static_eps.shape, out=caps[slot].static_eps)
             out = caps[slot].replay()
             done[slot].record(main)
             if not last:
@@ -405,7 +425,10 @@ def main():
                    "parallelism": f"dp{world}"},
         "elbo": elbo,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
-        "mode": "model step replayed as a hipGraph (double-buffered), front-end eager one step ahead on its own stream"
+        "mode": (f"model step captured once, replayed by the native {args.streams}-stream executor "
+                 "(vt_stepgraph); front-end eager " + ("one step ahead on its own stream" if args.overlap_fe else
+                                                      "before each replay on the same stream")) if args.native else
+                "model step replayed as a hipGraph (double-buffered), front-end eager one step ahead on its own stream"
                 if graph else ("eager, next batch's front-end overlapped with clip + AdamW (own streams, "
                                "double-buffered features)" if args.overlap_update else
                                "eager, next batch's front-end overlapped with the whole step" if args.prefetch

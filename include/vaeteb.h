@@ -426,6 +426,21 @@ int vt_cross_entropy_fwd(const float* logits, const int64_t* labels, int B, int 
 int vt_cross_entropy_bwd(const float* probs, const int64_t* labels, int B, int C, const float* g, float* dlogits,
                          void* stream);
 
+/* ---- native step executor (csrc/stepgraph.cpp) ----------------------------------------
+ * Runs a captured training step (a hipGraph_t, e.g. torch.cuda.CUDAGraph(keep_graph=True)
+ * .raw_cuda_graph()) as a multi-stream launch list: nodes in capture order, assigned to
+ * n_streams caller-provided streams, cross-stream dependencies as event waits.  The graph (its node storage and memory pool) must outlive the handle.
+ * Supported nodes: kernel, 1-D memcpy / memset, empty.  In-graph RNG offsets are NOT
+ * advanced (draw random inputs outside the graph).
+ * replaces: the per-op Python dispatch of the eager step (ref/model/graph_model.py:692-760
+ *           training_step / Lightning's optimizer loop) and ROCm's hipGraphLaunch        */
+int vt_stepgraph_build(void* graph, int n_streams, void** handle);
+/* enqueue one step: streams[0..n_streams) are distinct hipStream_t; the step forks
+ * from streams[0] and joins back into it (stream-ordered there) */
+int vt_stepgraph_launch(void* handle, void* const* streams);
+int vt_stepgraph_info(void* handle, int* n_kernel, int* n_memcpy, int* n_memset, int* n_waits);
+int vt_stepgraph_destroy(void* handle);
+
 #ifdef __cplusplus
 }
 #endif

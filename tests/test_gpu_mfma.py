@@ -83,8 +83,11 @@ def _bwd_weight(L, gy, x, with_bias=True, acc=None):
 
 
 # (R, K, N): the S=16 head (256), a ragged batch, the S=256 head at batch 256
-# (4096: split-K 4), and the S=300 reference head (4800: split-K 3)
-SHAPES = [(64, 256, 256), (7, 128, 192), (256, 4096, 4096), (256, 4800, 4800), (300, 640, 320)]
+# (4096: split-K 4), and the S=300 reference head (4800: split-K 3); the weight
+# gradient takes the direct kernel (k_mfma_dw) when N and K are multiples of 128
+# (ragged 37 / 300 rows: masked chunk rows) and the split-K path otherwise
+SHAPES = [(64, 256, 256), (7, 128, 192), (256, 4096, 4096), (256, 4800, 4800), (300, 640, 320), (37, 128, 256),
+          (300, 384, 640)]
 
 
 @pytest.mark.parametrize("R,K,N", SHAPES)
@@ -100,8 +103,8 @@ def test_mfma_exact_integer(L, R, K, N):
     assert torch.equal(gb, gy.double().sum(0).float())
 
 
-def test_mfma_accumulate(L):
-    R, K, N = 32, 128, 64
+@pytest.mark.parametrize("R,K,N", [(32, 128, 64), (100, 256, 128)])
+def test_mfma_accumulate(L, R, K, N):
     x, w, gy = _ints(R, K, seed=5), _ints(N, K, seed=6), _ints(R, N, seed=7)
     a0, w0 = _ints(R, K, seed=8), _ints(N, K, seed=9)
     gx = _bwd_data(L, gy, w, acc=a0)

@@ -336,3 +336,56 @@ def test_graph_capture_bf16_paths_after_eager_steps(golden):
         res.append((outs, tr.state.p.clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("n_streams", [1, 2, 4])
+def test_native_executor_bitwise_identical_to_eager(golden, n_streams):
+    """The library's multi-stream executor over the captured step
+    (Trainer.capture(native=True), csrc/stepgraph.cpp) == eager steps bit for bit:
+    the same kernels and arguments, the capture's cross-stream dependencies kept
+    as event waits whatever the stream count (concurrent encoders, bf16 heads /
+    convs / MLPs: every side stream of the step)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    g = golden("model_s16_b4")
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    b0 = {"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}
+    b1 = {k: v.flip(0).contiguous() for k, v in b0.items()}
+    eps0 = T("eps")
+    eps1 = eps0.flip(0).contiguous()
+    res = []
+    for native in (False, True):
+        m = det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=True, head_precision="bf16",
+                                conv_precision="bf16", mlp_precision="bf16")).cuda()
+        tr = Trainer(m, lr=1e-3)
+        if native:
+            cap = tr.capture(b0, eps=eps0, warmup=2, native=True, n_streams=n_streams)
+            n_kernel, n_memcpy, n_memset, n_waits = cap.info()
+            assert n_kernel > 100 and (n_streams > 1 or n_waits == 0)
+            outs = [tr.replay(b, eps=e)["total_loss"].item() for b, e in ((b1, eps1), (b0, eps0), (b1, eps1))]
+        else:
+            for _ in range(2):
+                tr.step(b0, eps=eps0)
+            outs = [tr.step(b, eps=e)["total_loss"].item() for b, e in ((b1, eps1), (b0, eps0), (b1, eps1))]
+        torch.cuda.synchronize()
+        res.append((outs, tr.state.p.clone(), tr.state.m.clone(), tr.state.v.clone()))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, b)
+
+
+def test_native_executor_requires_eps(golden):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    g = golden("model_s16_b4")
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    b0 = {"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}
+    tr = Trainer(det_fill_(SeqVaeTeb(sequence_length=16)).cuda(), lr=1e-3)
+    with pytest.raises(ValueError):
+        tr.capture(b0, native=True)

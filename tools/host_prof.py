@@ -18,7 +18,8 @@ plan = FrontEndPlan(11, 4, 16, 4096, device=dev)
 fe = FrontEnd(plan, load_stats(11, 4, 16, 4096))
 torch.manual_seed(1234)
 model = SeqVaeTeb(sequence_length=plan.S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,
-                  cross_phase_channels=fe.C_x, head_precision="bf16", concurrent_encoders=True).to(dev)
+                  cross_phase_channels=fe.C_x, head_precision="bf16", conv_precision="bf16",
+                  mlp_precision="bf16", concurrent_encoders=True).to(dev)
 tr = Trainer(model, lr=1e-3, frontend=fe)
 x = torch.from_numpy(synthetic.batch(0, 256, 4096)).to(dev)
 for _ in range(3):
@@ -31,4 +32,5 @@ for _ in range(5):
 pr.disable()
 torch.cuda.synchronize()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(35)
+st.sort_stats("tottime").print_stats(45)
+st.sort_stats("cumulative").print_stats(60)

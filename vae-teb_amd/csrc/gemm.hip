@@ -276,29 +276,29 @@ __global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ 
 // conv bwd-data fold: gradient of the padded / upsampled input (B, Lp, Cin)
 // back onto the real input (B, L_in, Cin): sum over the padded positions that
 // read each upsampled sample, then through the linear-interpolation weights.
+// One sample per grid row (blockIdx.y), 32-bit position / channel arithmetic
+// within it (host check: Lp * Cin < 2^31).
 __global__ void k_conv_fold(const float* __restrict__ gpad, ConvGeom g, float* __restrict__ dx, int accumulate) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)g.B * g.L_in * g.Cin;
-    if (i >= total) return;
-    const int ci = (int)(i % g.Cin);
-    const int64_t r = i / g.Cin;
-    const int b = (int)(r / g.L_in), s = (int)(r - (int64_t)b * g.L_in);
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // s * Cin + ci within sample b
+    if (i >= g.L_in * g.Cin) return;
+    const int b = blockIdx.y;
+    const int s = i / g.Cin, ci = i - s * g.Cin;
     const int Lp = g.L_out + g.K - 1;  // padded length the bwd-data GEMM produced
     const float* gb = gpad + (int64_t)b * Lp * g.Cin + ci;
     // gradient of upsampled position t: sum of padded positions tp with map(tp) == t
     auto gup = [&](int t) -> float {
-        float v = gb[(int64_t)(t + g.pad) * g.Cin];  // the direct copy
+        float v = gb[(t + g.pad) * g.Cin];  // the direct copy
         if (g.mode == 0) return v;
         if (g.L_up <= g.pad) {  // replicate: edges collect the pads
             if (t == 0)
-                for (int tp = 0; tp < g.pad; ++tp) v += gb[(int64_t)tp * g.Cin];
+                for (int tp = 0; tp < g.pad; ++tp) v += gb[tp * g.Cin];
             if (t == g.L_up - 1)
-                for (int tp = g.pad + g.L_up; tp < Lp; ++tp) v += gb[(int64_t)tp * g.Cin];
+                for (int tp = g.pad + g.L_up; tp < Lp; ++tp) v += gb[tp * g.Cin];
             return v;
         }
-        if (t >= 1 && t <= g.pad) v += gb[(int64_t)(g.pad - t) * g.Cin];               // left mirror
+        if (t >= 1 && t <= g.pad) v += gb[(g.pad - t) * g.Cin];                        // left mirror
         const int tr = g.pad + 2 * (g.L_up - 1) - t;                                   // right mirror
-        if (t <= g.L_up - 2 && tr < Lp && tr >= g.pad + g.L_up) v += gb[(int64_t)tr * g.Cin];
+        if (t <= g.L_up - 2 && tr < Lp && tr >= g.pad + g.L_up) v += gb[tr * g.Cin];
         return v;
     };
     float out;
@@ -321,8 +321,15 @@ __global__ void k_conv_fold(const float* __restrict__ gpad, ConvGeom g, float* _
             if (w != 0.f) out += w * gup(t);
         }
     }
-    float* o = dx + i;
+    float* o = dx + (int64_t)b * g.L_in * g.Cin + i;
     *o = accumulate ? *o + out : out;
+}
+
+static int fold_launch(const float* gpad, const ConvGeom& g, float* dX, int accumulate, hipStream_t st) {
+    VT_CHECK_ARG((int64_t)(g.L_out + g.K - 1) * g.Cin < (1ll << 31) && g.B <= 65535, "conv fold: shape");
+    hipLaunchKernelGGL(k_conv_fold, dim3((unsigned)((g.L_in * g.Cin + 255) / 256), (unsigned)g.B), dim3(256), 0, st,
+                       gpad, g, dX, accumulate);
+    return VT_OK;
 }
 
 static inline dim3 gemm_grid(int64_t M, int N, int splits) {
@@ -440,9 +447,8 @@ int vt_conv1d_fold(const float* gpad, int B, int L_in, int Cin, int Cout, int K,
                    int accumulate, void* stream) {
     VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0, "vt_conv1d_fold: shape");
     ConvGeom g = make_geom(B, L_in, Cin, Cout, K, mode, up);
-    const int64_t total = (int64_t)B * L_in * Cin;
-    hipLaunchKernelGGL(k_conv_fold, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream), gpad, g, dX,
-                       accumulate);
+    const int rc = fold_launch(gpad, g, dX, accumulate, S(stream));
+    if (rc) return rc;
     VT_LAUNCH_CHECK("vt_conv1d_fold");
     return VT_OK;
 }
@@ -507,9 +513,8 @@ int vt_conv1d_bwd_data(const float* dY, int B, int L_in, int Cin, const float* W
                                                    ConvWT{W, Cin, Cout, K}, M, Cin, (int64_t)K * Cout, gpad, Cin,
                                                    nullptr, 0, nullptr, 0, 1, 0, 0, 0, S(stream));
     if (rc) return rc;
-    const int64_t total = (int64_t)B * L_in * Cin;
-    hipLaunchKernelGGL(k_conv_fold, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream), gpad, g, dX,
-                       accumulate);
+    rc = fold_launch(gpad, g, dX, accumulate, S(stream));
+    if (rc) return rc;
     VT_LAUNCH_CHECK("vt_conv1d_bwd_data(fold)");
     return VT_OK;
 }

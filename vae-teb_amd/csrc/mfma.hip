@@ -186,6 +186,102 @@ __global__ __launch_bounds__(256) void k_bf16_shadow(const float* __restrict__ W
     for (int i = ty; i < 64; i += 4) W16t[(k0 + i) * N + n0 + tx] = (__bf16)tile[tx][i];
 }
 
+// ------------------------------------------------------------ weight gradient
+// dW[n][k] (+)= sum_r dY[r][n] X[r][k] with the batch rows r as the (short)
+// reduction (R = 256 for the heads): a 128 x 128 tile per workgroup of 4
+// waves (2 x 2, 64 x 64 each), 64-row chunks of dY and X staged from fp32 to
+// bf16 row-major images in LDS (the next chunk prefetched into registers while
+// the current one is multiplied) and read as MFMA fragments with the gfx950
+// transposed read ds_read_b64_tr_b16 (r contiguous per fragment) — no
+// transposed bf16 copies in HBM, no split-K slabs.  39 KB of LDS and 256
+// threads: it runs beside the decoder's backward on the other stream instead of
+// waiting for a whole CU.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+constexpr int DWT = 128, DWC = 64;              // tile edge, rows per chunk
+constexpr int DWS = DWT + 16;                   // bf16 row stride (72 dwords == 8 mod 64 banks)
+constexpr int DWIMG = DWC * DWS + (DWC / 8) * 64;  // + 32 dwords every 8 rows: rows 8 apart -> banks +32
+
+__device__ __forceinline__ int dw_pos(int r, int c) { return r * DWS + (r >> 3) * 64 + c; }
+
+// 16 x 32 fragment (16 columns col0.., 32 rows row0..) of a [r][col] image, r the reduction:
+// lane 4q + p of 16-lane group g reads rows row0 + 8g + q (+4), columns col0 + 4p .. +3
+__device__ __forceinline__ bf16x8 dw_frag(const __bf16* img, int row0, int col0) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const __bf16* a0 = img + dw_pos(row0 + 8 * g + q, col0 + 4 * p);
+    const __bf16* a1 = img + dw_pos(row0 + 8 * g + q + 4, col0 + 4 * p);
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a1);
+    const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+__global__ __launch_bounds__(256) void k_mfma_dw(const float* __restrict__ dY, int64_t R, int N,
+                                                 const float* __restrict__ X, int K, float* __restrict__ dW,
+                                                 int accumulate) {
+    __shared__ __attribute__((aligned(16))) __bf16 img[2][DWIMG];  // [0] dY chunk, [1] X chunk
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+    const int n0 = blockIdx.y * DWT, k0 = blockIdx.x * DWT;
+    // staging: chunk rows r0 .. r0 + 63, 32 float4 per row per operand; thread -> (row, quad) pairs
+    float4 pf[2][8];
+    auto load = [&](int64_t r0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = tid + 256 * i, row = e >> 5, q4 = e & 31;
+            const bool ok = r0 + row < R;
+            pf[0][i] = ok ? *(const float4*)(dY + (r0 + row) * N + n0 + 4 * q4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            pf[1][i] = ok ? *(const float4*)(X + (r0 + row) * K + k0 + 4 * q4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = tid + 256 * i, row = e >> 5, q4 = e & 31;
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                const bf16x4 v = {(__bf16)pf[o][i].x, (__bf16)pf[o][i].y, (__bf16)pf[o][i].z, (__bf16)pf[o][i].w};
+                *(bf16x4*)(img[o] + dw_pos(row, 4 * q4)) = v;
+            }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    load(0);
+    for (int64_t r0 = 0; r0 < R; r0 += DWC) {
+        store();
+        __syncthreads();
+        if (r0 + DWC < R) load(r0 + DWC);
+#pragma unroll
+        for (int s = 0; s < DWC / 32; ++s) {
+            bf16x8 a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = dw_frag(img[0], 32 * s, 64 * wm + 16 * i);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = dw_frag(img[1], 32 * s, 64 * wn + 16 * j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // D: col (k) = lane & 15, row (n) = 4 * (lane >> 4) + rr
+    const int lr = lane & 15, lc = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                float* c = dW + (int64_t)(n0 + 64 * wm + 16 * i + 4 * lc + rr) * K + k0 + 64 * wn + 16 * j + lr;
+                *c = accumulate ? *c + acc[i][j][rr] : acc[i][j][rr];
+            }
+}
+
 static inline int64_t up_to(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // largest divisor s of the k-tile count with tiles * s <= ~1.25 x CU count
@@ -284,6 +380,13 @@ int vt_mfma_linear_bwd_data(const float* dY, int64_t R, int N, const void* W16t,
 int vt_mfma_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
                               int accumulate, float* ws, int64_t ws_floats, void* stream) {
     VT_CHECK_ARG(R > 0 && vt_mfma_supported(K, N), "vt_mfma_linear_bwd_weight: K and N must be positive multiples of 64");
+    if (N % DWT == 0 && K % DWT == 0) {
+        // direct: fp32 operands staged and transposed in LDS, no split (k_mfma_dw)
+        hipLaunchKernelGGL(k_mfma_dw, dim3(K / DWT, N / DWT), dim3(256), 0, S(stream), dY, R, N, X, K, dW,
+                           accumulate);
+        VT_LAUNCH_CHECK("vt_mfma_linear_bwd_weight");
+        return db ? vt_colsum(dY, R, N, db, accumulate, ws, ws_floats, stream) : VT_OK;
+    }
     MfmaPlan p = plan(N, K, R);  // C = dW (M=N, cols=K), reduction over R
     const int64_t b_floats = up_to((int64_t)K * p.Kpad / 2, 64);
     VT_CHECK_ARG(p.a_floats + b_floats + p.part_floats + N <= ws_floats, "vt_mfma_linear_bwd_weight: workspace too small");

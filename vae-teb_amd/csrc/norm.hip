@@ -371,55 +371,6 @@ __global__ __launch_bounds__(NT) void k_reduce_parts(const float* __restrict__ p
 }
 
 // ------------------------------------------------------------- BatchNorm
-// column partial sums over (M, C) row-major data; value per element chosen by `kind`:
-//   0: x         1: (x - mean)^2         2: (dz, dz*xhat) [two outputs]
-__global__ __launch_bounds__(NT) void k_col_partial(const float* __restrict__ x, const float* __restrict__ dy,
-                                                    int64_t M, int C, int64_t rows_per_block, int kind,
-                                                    const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                    int act, float* __restrict__ part) {
-    __shared__ float red0[NT], red1[NT];
-    const int rpi = C <= NT ? NT / C : 1;  // rows per iteration
-    const int c = threadIdx.x % C;
-    const int ro = threadIdx.x / C;
-    const bool active = C <= NT ? ro < rpi : true;
-    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-    const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
-    float a0 = 0.f, a1 = 0.f;
-    if (active && C <= NT) {
-        const float mu = mean ? mean[c] : 0.f;
-        const float rs = rstd ? rstd[c] : 0.f;
-        for (int64_t r = r0 + ro; r < r1; r += rpi) {
-            const float v = x[r * C + c];
-            if (kind == 0) {
-                a0 += v;
-            } else if (kind == 1) {
-                const float d = v - mu;
-                a0 += d * d;
-            } else {
-                const float h = (v - mu) * rs;
-                const float dz = dy[r * C + c] * act_d(h * gamma[c] + beta[c], act);
-                a0 += dz;
-                a1 += dz * h;
-            }
-        }
-    }
-    red0[threadIdx.x] = a0;
-    red1[threadIdx.x] = a1;
-    __syncthreads();
-    if (C <= NT) {
-        for (int cc = threadIdx.x; cc < C; cc += NT) {
-            float s0 = 0.f, s1 = 0.f;
-            for (int i = 0; i < rpi; ++i) {
-                s0 += red0[i * C + cc];
-                s1 += red1[i * C + cc];
-            }
-            part[(int64_t)blockIdx.x * 2 * C + cc] = s0;
-            part[(int64_t)blockIdx.x * 2 * C + C + cc] = s1;
-        }
-    }
-}
-
 // mode 0: mean[c] = S/M.  mode 1: var = S/M -> rstd, running stats update.
 // mode 2: dbeta = S0, dgamma = S1.
 // one workgroup per channel; double accumulation, fixed-order tree
@@ -482,20 +433,6 @@ __global__ void k_bn_eval(const float* __restrict__ x, int64_t M, int C, const f
     y[i] = act_f((x[i] - run_mean[c]) * (1.f / sqrtf(run_var[c] + eps)) * gamma[c] + beta[c], act);
 }
 
-// dx = gamma*rstd*(dz - dbeta/M - xhat*dgamma/M)
-__global__ void k_bn_dx(const float* __restrict__ dy, const float* __restrict__ x, int64_t M, int C,
-                        const float* __restrict__ mean, const float* __restrict__ rstd,
-                        const float* __restrict__ gamma, const float* __restrict__ beta, int act,
-                        const float* __restrict__ dgamma, const float* __restrict__ dbeta, float* __restrict__ dx) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M * C) return;
-    const int c = (int)(i % C);
-    const float h = (x[i] - mean[c]) * rstd[c];
-    const float dz = dy[i] * act_d(h * gamma[c] + beta[c], act);
-    const float inv = 1.f / (float)M;
-    dx[i] = gamma[c] * rstd[c] * (dz - dbeta[c] * inv - h * dgamma[c] * inv);
-}
-
 __global__ void k_act_fwd(const float* __restrict__ x, int64_t n, int act, float* __restrict__ y) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) y[i] = act_f(x[i], act);
@@ -506,12 +443,249 @@ __global__ void k_act_bwd(const float* __restrict__ dy, const float* __restrict_
     if (i < n) dx[i] = dy[i] * act_d(x[i], act);
 }
 
+// ---------------------------------------------- BatchNorm, vectorised paths
+// The element-wise BatchNorm passes over the conv blocks' (B*L, C) activations
+// (C = 1..87 channels, up to 23 M elements) are HBM streams: 16-byte loads and
+// stores, four elements per thread-step, the per-channel parameters staged once
+// per workgroup in LDS, the activation a template parameter, 32-bit channel
+// arithmetic (the flat index's channel advances by a fixed step per thread-step
+// instead of a 64-bit modulo per element).
+//   apply: y = act((x - mean) rstd gamma + beta)
+//   dx:    dx = gamma rstd (dz - dbeta/M - xhat dgamma/M), dz = dy act'(xhat gamma + beta)
+//   column partials, kind 0: x; 1: (x - mean)^2; 2: (dz, dz xhat)
+static constexpr int BNV_C = 1024;  // max channels of the vectorised paths (LDS staging)
+static constexpr int BNV_V = 4;     // float4 per thread per workgroup
+
+__device__ __forceinline__ int wrapc(int c, int C) { return c >= C ? c - C : c; }
+
+// channels of the 4 elements starting at channel c (C >= 4: one wrap at most)
+__device__ __forceinline__ void chan4(int c, int C, int (&ce)[4]) {
+    if (C >= 4) {
+        ce[0] = c;
+        ce[1] = wrapc(c + 1, C);
+        ce[2] = wrapc(ce[1] + 1, C);
+        ce[3] = wrapc(ce[2] + 1, C);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ce[e] = (c + e) % C;
+    }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(NT) void k_bn_apply4(const float* __restrict__ x, int64_t n, int C,
+                                                  const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  float* __restrict__ y) {
+    __shared__ float p[4][BNV_C];
+    for (int c = threadIdx.x; c < C; c += NT) {
+        p[0][c] = mean[c];
+        p[1][c] = rstd[c];
+        p[2][c] = gamma[c];
+        p[3][c] = beta[c];
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * (NT * 4 * BNV_V);
+    const int step = (NT * 4) % C;
+    int c = (int)((base + 4 * threadIdx.x) % C);
+#pragma unroll
+    for (int v = 0; v < BNV_V; ++v, c = wrapc(c + step, C)) {
+        const int64_t j = base + 4 * (threadIdx.x + NT * v);
+        if (j >= n) break;
+        int ce[4];
+        chan4(c, C, ce);
+        if (j + 4 <= n) {
+            const float4 xv = *(const float4*)(x + j);
+            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = act_f((xs[e] - p[0][ce[e]]) * p[1][ce[e]] * p[2][ce[e]] + p[3][ce[e]], ACT);
+            *(float4*)(y + j) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (int e = 0; e < (int)(n - j); ++e)
+                y[j + e] = act_f((x[j + e] - p[0][ce[e]]) * p[1][ce[e]] * p[2][ce[e]] + p[3][ce[e]], ACT);
+        }
+    }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(NT) void k_bn_dx4(const float* __restrict__ dy, const float* __restrict__ x, int64_t n,
+                                               int64_t M, int C, const float* __restrict__ mean,
+                                               const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                               const float* __restrict__ beta, const float* __restrict__ dgamma,
+                                               const float* __restrict__ dbeta, float* __restrict__ dx) {
+    __shared__ float p[6][BNV_C];
+    for (int c = threadIdx.x; c < C; c += NT) {
+        p[0][c] = mean[c];
+        p[1][c] = rstd[c];
+        p[2][c] = gamma[c];
+        p[3][c] = beta[c];
+        p[4][c] = dgamma[c];
+        p[5][c] = dbeta[c];
+    }
+    __syncthreads();
+    const float inv = 1.f / (float)M;
+    const int64_t base = (int64_t)blockIdx.x * (NT * 4 * BNV_V);
+    const int step = (NT * 4) % C;
+    int c = (int)((base + 4 * threadIdx.x) % C);
+    auto one = [&](float xe, float dye, int cc) {
+        const float h = (xe - p[0][cc]) * p[1][cc];
+        const float dz = dye * act_d(h * p[2][cc] + p[3][cc], ACT);
+        return p[2][cc] * p[1][cc] * (dz - p[5][cc] * inv - h * p[4][cc] * inv);
+    };
+#pragma unroll
+    for (int v = 0; v < BNV_V; ++v, c = wrapc(c + step, C)) {
+        const int64_t j = base + 4 * (threadIdx.x + NT * v);
+        if (j >= n) break;
+        int ce[4];
+        chan4(c, C, ce);
+        if (j + 4 <= n) {
+            const float4 xv = *(const float4*)(x + j), gv = *(const float4*)(dy + j);
+            *(float4*)(dx + j) = make_float4(one(xv.x, gv.x, ce[0]), one(xv.y, gv.y, ce[1]), one(xv.z, gv.z, ce[2]),
+                                             one(xv.w, gv.w, ce[3]));
+        } else {
+            for (int e = 0; e < (int)(n - j); ++e) dx[j + e] = one(x[j + e], dy[j + e], ce[e]);
+        }
+    }
+}
+
+// Column partial sums (kinds as k_col_partial) over rows [r0, r1) of block b,
+// r0 a multiple of 4: thread tid < T' reads the float4s at flat offsets
+// r0*C + 4 tid + 4T' k, 4T' a multiple of C, so its four channels never change;
+// the per-thread sums are combined in LDS in fixed order.
+template <int KIND, int ACT>
+__global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x, const float* __restrict__ dy,
+                                                     int64_t M, int C, int64_t rows_per_block, int Tp,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float* __restrict__ part) {
+    __shared__ float red0[4 * NT], red1[4 * NT];
+    const int tid = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
+    float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tid < Tp) {
+        int ce[4];
+        chan4((4 * tid) % C, C, ce);
+        float mu[4], rs[4], ga[4], be[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            mu[e] = KIND >= 1 ? mean[ce[e]] : 0.f;
+            rs[e] = KIND == 2 ? rstd[ce[e]] : 0.f;
+            ga[e] = KIND == 2 ? gamma[ce[e]] : 0.f;
+            be[e] = KIND == 2 ? beta[ce[e]] : 0.f;
+        }
+        const int64_t end = r1 * C;
+        auto acc = [&](int e, float v, float g) {
+            if (KIND == 0) {
+                a0[e] += v;
+            } else if (KIND == 1) {
+                const float d = v - mu[e];
+                a0[e] += d * d;
+            } else {
+                const float h = (v - mu[e]) * rs[e];
+                const float dz = g * act_d(h * ga[e] + be[e], ACT);
+                a0[e] += dz;
+                a1[e] += dz * h;
+            }
+        };
+        for (int64_t f = r0 * C + 4 * tid; f < end; f += 4 * Tp) {
+            if (f + 4 <= end) {
+                const float4 xv = *(const float4*)(x + f);
+                float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (KIND == 2) gv = *(const float4*)(dy + f);
+                acc(0, xv.x, gv.x);
+                acc(1, xv.y, gv.y);
+                acc(2, xv.z, gv.z);
+                acc(3, xv.w, gv.w);
+            } else {
+                for (int e = 0; e < (int)(end - f); ++e) acc(e, x[f + e], KIND == 2 ? dy[f + e] : 0.f);
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        red0[4 * tid + e] = a0[e];
+        red1[4 * tid + e] = a1[e];
+    }
+    __syncthreads();
+    const int groups = 4 * Tp / C;
+    for (int cc = tid; cc < C; cc += NT) {
+        float s0 = 0.f, s1 = 0.f;
+        for (int q = 0; q < groups; ++q) {
+            s0 += red0[q * C + cc];
+            s1 += red1[q * C + cc];
+        }
+        part[(int64_t)blockIdx.x * 2 * C + cc] = s0;
+        part[(int64_t)blockIdx.x * 2 * C + C + cc] = s1;
+    }
+}
+
+// active threads of k_col_partial4: the largest multiple of C / gcd(C, 4) within NT
+static inline int colp_threads(int C) {
+    const int g = C % 4 == 0 ? 4 : (C % 2 == 0 ? 2 : 1);
+    const int P = C / g;
+    return P <= NT ? NT / P * P : 0;
+}
+
+#define VT_ACT_SWITCH(act, F) \
+    switch (act) {            \
+        case ACT_RELU: F(ACT_RELU); break; \
+        case ACT_GELU: F(ACT_GELU); break; \
+        case ACT_TANH: F(ACT_TANH); break; \
+        default: F(ACT_NONE); break;       \
+    }
+
+static inline unsigned bnv_blocks(int64_t n) { return (unsigned)((n + NT * 4 * BNV_V - 1) / (NT * 4 * BNV_V)); }
+
+static void bn_apply_vec(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
+                         const float* beta, int act, float* y, hipStream_t st) {
+    const int64_t n = M * C;
+#define VT_F(A) hipLaunchKernelGGL(k_bn_apply4<A>, dim3(bnv_blocks(n)), dim3(NT), 0, st, x, n, C, mean, rstd, gamma, beta, y)
+    VT_ACT_SWITCH(act, VT_F)
+#undef VT_F
+}
+
+static void bn_dx_vec(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                      const float* gamma, const float* beta, int act, const float* dgamma, const float* dbeta,
+                      float* dx, hipStream_t st) {
+    const int64_t n = M * C;
+#define VT_F(A)                                                                                                   \
+    hipLaunchKernelGGL(k_bn_dx4<A>, dim3(bnv_blocks(n)), dim3(NT), 0, st, dy, x, n, M, C, mean, rstd, gamma, beta, \
+                       dgamma, dbeta, dx)
+    VT_ACT_SWITCH(act, VT_F)
+#undef VT_F
+}
+
+static void col_partial_vec(int kind, const float* x, const float* dy, int64_t M, int C, int64_t rpb, int blocks,
+                            const float* mean, const float* rstd, const float* gamma, const float* beta, int act,
+                            float* part, hipStream_t st) {
+    const int Tp = colp_threads(C);
+    if (kind == 0) {
+        hipLaunchKernelGGL((k_col_partial4<0, ACT_NONE>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean,
+                           rstd, gamma, beta, part);
+    } else if (kind == 1) {
+        hipLaunchKernelGGL((k_col_partial4<1, ACT_NONE>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean,
+                           rstd, gamma, beta, part);
+    } else {
+#define VT_F(A)                                                                                                       \
+    hipLaunchKernelGGL((k_col_partial4<2, A>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean, rstd, gamma, \
+                       beta, part)
+        VT_ACT_SWITCH(act, VT_F)
+#undef VT_F
+    }
+}
+
 static inline unsigned blocks_for(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
 // y = act(BN(x)) for conv.hip's fused conv + BatchNorm forward
 int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
                     const float* beta, int act, float* y, hipStream_t st) {
-    hipLaunchKernelGGL(k_bn_apply, dim3(blocks_for(M * C)), dim3(256), 0, st, x, M, C, mean, rstd, gamma, beta, act, y);
+    if (C <= BNV_C)
+        bn_apply_vec(x, M, C, mean, rstd, gamma, beta, act, y, st);
+    else
+        hipLaunchKernelGGL(k_bn_apply, dim3(blocks_for(M * C)), dim3(256), 0, st, x, M, C, mean, rstd, gamma, beta,
+                           act, y);
     return VT_OK;
 }
 
@@ -606,7 +780,7 @@ static int bn_blocks(int64_t M, int64_t ws_floats, int C, int64_t* rpb) {
     if (blocks > 2048) blocks = 2048;
     if (blocks * 2 * C > ws_floats) blocks = ws_floats / (2 * C);
     if (blocks < 1) return 0;
-    *rpb = (M + blocks - 1) / blocks;
+    *rpb = ((M + blocks - 1) / blocks + 3) / 4 * 4;  // a multiple of 4 (k_col_partial4's float4 rows)
     return (int)((M + *rpb - 1) / *rpb);
 }
 
@@ -621,15 +795,13 @@ int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const
     const int blocks = bn_blocks(M, ws_floats, C, &rpb);
     VT_CHECK_ARG(blocks >= 1, "vt_batchnorm_fwd: workspace too small");
     hipStream_t st = S(stream);
-    hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, nullptr, M, C, rpb, 0, nullptr, nullptr,
-                       nullptr, nullptr, 0, ws);
+    col_partial_vec(0, x, nullptr, M, C, rpb, blocks, nullptr, nullptr, nullptr, nullptr, 0, ws, st);
     hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 0, eps, momentum, mean,
                        rstd, nullptr, nullptr, nullptr, nullptr, 0);
-    hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, nullptr, M, C, rpb, 1, mean, nullptr, nullptr,
-                       nullptr, 0, ws);
+    col_partial_vec(1, x, nullptr, M, C, rpb, blocks, mean, nullptr, nullptr, nullptr, 0, ws, st);
     hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 1, eps, momentum, mean,
                        rstd, run_mean, run_var, nullptr, nullptr, 0);
-    hipLaunchKernelGGL(k_bn_apply, dim3(blocks_for(M * C)), dim3(256), 0, st, x, M, C, mean, rstd, gamma, beta, act, y);
+    bn_apply_vec(x, M, C, mean, rstd, gamma, beta, act, y, st);
     VT_LAUNCH_CHECK("vt_batchnorm_fwd");
     return VT_OK;
 }
@@ -645,12 +817,10 @@ int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const fl
     // fresh sums for the dx formula live at the end of ws; params may accumulate
     float* dg_now = ws + (ws_floats - 2 * C);
     float* db_now = dg_now + C;
-    hipLaunchKernelGGL(k_col_partial, dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, 2, mean, rstd, gamma, beta, act,
-                       ws);
+    col_partial_vec(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st);
     hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 2, 0.f, 0.f, nullptr,
                        nullptr, nullptr, nullptr, dg_now, db_now, 0);
-    hipLaunchKernelGGL(k_bn_dx, dim3(blocks_for(M * C)), dim3(256), 0, st, dy, x, M, C, mean, rstd, gamma, beta, act,
-                       dg_now, db_now, dx);
+    bn_dx_vec(dy, x, M, C, mean, rstd, gamma, beta, act, dg_now, db_now, dx, st);
     hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
                        accumulate_params);
     VT_LAUNCH_CHECK("vt_batchnorm_bwd");

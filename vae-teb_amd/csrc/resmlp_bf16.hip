@@ -32,6 +32,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace vt {
@@ -943,7 +945,12 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
     d.bpin = bprm;
     bprm += 2 * h16(dims[0]);
     d.bprm = bprm;
-    p.tpw = p.nt >= 6 ? 1 : 2;
+    static int tpw_env = -1;  // VAETEB_MLPB_TPW: 1 / 2 force the backward block (tuning experiments)
+    if (tpw_env < 0) {
+        const char* e = getenv("VAETEB_MLPB_TPW");
+        tpw_env = e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
+    }
+    p.tpw = p.nt >= 6 ? 1 : (tpw_env ? tpw_env : 2);
     const int ims = IMR * p.tpw + 16;
     const int rest = 2 * (bz + bh) * ims + 4 * (bprm + NW * 48 * p.nt);
     d.bres = 2 * bwtot + rest <= 160 * 1024;  // all W^T images resident when they fit
@@ -1147,17 +1154,14 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
         if (p.d.l[l].ln) add(2 * p.d.G[l].N, p.d.G[l].N, 0, p.d.l[l].lpo, grads[4 + 4 * l], grads[5 + 4 * l]);
     add(2 * dims[0], dims[0], 0, p.d.lpo0, grads[0], grads[1]);
     const dim3 grid((unsigned)p.nblk);
-    switch (p.nt) {
 #define VT_MBB(NTV, TPWV)                                                                                        \
-    case NTV:                                                                                              \
+    if (p.nt == NTV && p.tpw == TPWV) {                                                                    \
         set_lds(k_mlpb_bwd<NTV, TPWV>, p.d.bbytes);                                                        \
         hipLaunchKernelGGL((k_mlpb_bwd<NTV, TPWV>), grid, dim3(BT), p.d.bbytes, st, ddev, dout, xhat, rstd, rows, \
                            p.Rp, dx, ws);                                                                  \
-        break;
-        VT_MBB(2, 2) VT_MBB(4, 2) VT_MBB(6, 1)
-        default: VT_MBB(9, 1)
-#undef VT_MBB
     }
+    VT_MBB(2, 2) VT_MBB(4, 2) VT_MBB(2, 1) VT_MBB(4, 1) VT_MBB(6, 1) VT_MBB(9, 1)
+#undef VT_MBB
     if (sa.nseg) {
         const dim3 gs((unsigned)((emax + 15) / 16), (unsigned)sa.nseg);
         hipLaunchKernelGGL(k_mlpb_sum, gs, dim3(256), 0, st, sa, ws, (int)p.nblk, accumulate);

@@ -553,9 +553,10 @@ class LSTMF(torch.autograd.Function):
             dg = torch.empty((B, S, 4 * H), device=gy.device)
             call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
             pw = _ParamGrads([w_ih, w_hh], [True, True])
-            # b_ih and b_hh receive the same gradient (sum of dg over rows): computed
-            # once into a fresh tensor (zeroed when the weights accumulate in place)
-            gb = torch.zeros_like(b_ih) if pw.acc else torch.empty_like(b_ih)
+            # b_ih and b_hh receive the same gradient (the sum of dg over rows), written
+            # by one column sum per bias straight into its gradient sink (no device copy:
+            # a memcpy node would not survive the native step executor, csrc/stepgraph.cpp)
+            pb = _ParamGrads([b_ih, b_hh], [True, True])
             side = LSTM_GRAD_STREAM if (pw.direct and LSTM_GRAD_STREAM is not None) else None
             if side is not None and side != torch.cuda.current_stream():
                 # weight gradients (in-place sinks) off the recurrence chain on a side
@@ -575,9 +576,10 @@ class LSTMF(torch.autograd.Function):
                      ptr(ws), ws.numel(), _st())
                 call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
                      ptr(ws), ws.numel(), _st())
-            call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), 0, ptr(ws), ws.numel(), _st())
+            for gb in pb.out:
+                call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), pb.acc, ptr(ws), ws.numel(), _st())
             gw_ih, gw_hh = pw.result()
-            grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, gb, gb.clone()]
+            grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, *pb.result()]
             if l > 0 or ctx.needs_input_grad[0]:
                 gin = torch.empty((B, S, In), device=gy.device)
                 call("vt_linear_bwd_data", ptr(dg), B * S, 4 * H, ptr(w_ih), In, ptr(gin), 0, _st())

@@ -231,7 +231,7 @@ class Trainer:
                   self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4, st)
 
     # ------------------------------------------------------------ hipGraph
-    def capture(self, batch, eps=None, warmup=2, pre_capture=None):
+    def capture(self, batch, eps=None, warmup=2, pre_capture=None, native=False, n_streams=4):
         """Record the training step as a hipGraph over static input buffers and
         return it as a `CapturedStep` (also kept as the trainer's default for
         `replay`).  A replay is one launch instead of ~1200 host-side op
@@ -244,7 +244,16 @@ class Trainer:
         bucketed RCCL all-reduce, clip and AdamW are issued after each replay (a
         handful of launches), so no collective is captured.  `warmup` eager
         steps run first (on the capture side stream, as torch requires) and do
-        update the model.  Capture more than once for double-buffered inputs."""
+        update the model.  Capture more than once for double-buffered inputs.
+
+        native=True: the replay is the library's multi-stream executor
+        (vt_stepgraph_*, csrc/stepgraph.cpp) over the captured graph instead of
+        hipGraphLaunch — the eager step's stream concurrency at graph-replay host
+        cost.  It does not advance in-graph RNG offsets, so `eps` (the
+        reparameterisation noise) must be given: the caller draws each step's
+        noise into `CapturedStep.static_eps` before the replay."""
+        if native and eps is None:
+            raise ValueError("native replay needs an explicit eps buffer (in-graph RNG is not advanced)")
         static_in = {k: v.clone() for k, v in batch.items()}
         static_eps = None if eps is None else eps.clone()
         side = torch.cuda.Stream()
@@ -255,13 +264,13 @@ class Trainer:
         torch.cuda.current_stream().wait_stream(side)
         if pre_capture is not None:
             pre_capture()
-        graph = torch.cuda.CUDAGraph()
+        graph = torch.cuda.CUDAGraph(keep_graph=native)
         with torch.cuda.graph(graph):
             out = self._forward_backward(static_in, static_eps, overlap_comm=False)
             if not self.buckets:
                 self._update()
         out["grad_norm"] = self.norm_out[0]
-        self.captured = CapturedStep(self, graph, static_in, static_eps, out)
+        self.captured = CapturedStep(self, graph, static_in, static_eps, out, native=native, n_streams=n_streams)
         return self.captured
 
     def replay(self, batch=None, eps=None):
@@ -272,8 +281,34 @@ class Trainer:
 class CapturedStep:
     """A training step recorded as a hipGraph (Trainer.capture)."""
 
-    def __init__(self, trainer, graph, static_in, static_eps, out):
+    def __init__(self, trainer, graph, static_in, static_eps, out, native=False, n_streams=4):
         self.trainer, self.graph, self.static_in, self.static_eps, self.out = trainer, graph, static_in, static_eps, out
+        self.handle = None
+        if native:
+            import ctypes
+            from .model import side_stream
+            h = ctypes.c_void_p()
+            _lib.call("vt_stepgraph_build", graph.raw_cuda_graph(), n_streams, ctypes.addressof(h))
+            self.handle = h.value
+            # the executor runs on the caller's stream plus the eager step's side streams
+            # (each bound to its own hardware queue)
+            dev = torch.cuda.current_device()
+            self.side = [side_stream(dev, i) for i in range(1, n_streams)]
+            self.streams = (ctypes.c_void_p * n_streams)()
+            self._st_addr = ctypes.addressof(self.streams)
+            self._destroy = _lib.lib().fns["vt_stepgraph_destroy"]
+
+    def info(self):
+        """(kernels, memcpys, memsets, cross-stream waits) of the native executor's launch list."""
+        import ctypes
+        v = [ctypes.c_int() for _ in range(4)]
+        _lib.call("vt_stepgraph_info", self.handle, *[ctypes.addressof(x) for x in v])
+        return tuple(x.value for x in v)
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            self._destroy(self.handle)   # bound at build time: safe during interpreter shutdown
+            self.handle = None
 
     def replay(self, batch=None, eps=None):
         tr = self.trainer
@@ -283,7 +318,14 @@ class CapturedStep:
                     self.static_in[k].copy_(v, non_blocking=True)
         if eps is not None:
             self.static_eps.copy_(eps, non_blocking=True)
-        self.graph.replay()
+        if self.handle is not None:
+            st = self.streams
+            st[0] = _lib.stream()
+            for i, sd in enumerate(self.side, 1):
+                st[i] = sd.cuda_stream
+            _lib.call("vt_stepgraph_launch", self.handle, self._st_addr)
+        else:
+            self.graph.replay()
         if tr.buckets:
             tr.buckets.reduce_all()
             tr.buckets.finish()
