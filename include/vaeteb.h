@@ -248,6 +248,9 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
                        const float* const* params, const float* dout, const float* xhat, const float* rstd,
                        int64_t rows, float* dx, float* const* grads, int accumulate, float* ws, int64_t ws_floats,
                        void* stream);
+/* Diagnostic (tools/mlpb_phases.py): while buf != NULL, vt_resmlp_bf16_bwd launches stamp
+ * wave 0's wall clock at the kernel's phase boundaries, 256 uint64 per workgroup. */
+int vt_resmlp_bf16_set_stamps(void* buf);
 
 /* ------------------------------------------------------- bf16 MFMA (heads)
  * The decoder's R x R output heads (Decoder.output_mu / output_logvar,

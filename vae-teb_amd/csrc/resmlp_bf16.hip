@@ -54,6 +54,7 @@ struct BG {                      // one GEMM: z = h W^T + b, W [N][K]
     int bw, bs;                  // backward image W^T: LDS offset (bf16), row stride: rows pad16(K), cols pad32(N)
     int po;                      // fp32 params in LDS: bias[pad16 N], gamma, beta
     int wo;                      // dW|db partial offset (floats), N x (K + 1)
+    int gbw;                     // W^T image offset (bf16) in the global image's backward region
     const float* W;
     const float* b;
 };
@@ -77,6 +78,8 @@ struct BDesc {
     int P;                       // partial floats per workgroup
     int lpo0;                    // LN partial offset of the input LN
     int bpin;                    // backward LDS float offset of the input LN gamma / beta
+    int gbo, gpo;                // global image: byte offsets of the W^T region and of the backward params
+    char* gimg;                  // global image (k_mlpb_prep): [forward LDS image | W^T images | backward params]
     const float* g0;
     const float* be0;
     BG G[MAXG];
@@ -333,6 +336,79 @@ __device__ __forceinline__ void ln_fwd(f32x4 (&z)[NT], int C, const float* gl, c
     act_tile<NT>(z, act);
 }
 
+// ------------------------------------------------------------ global images
+// k_mlpb_prep builds, once per forward call (the optimizer rewrites the master
+// weights every step), the stack's bf16 weight images and staged parameters in
+// the exact LDS layouts: [0, fbytes) the forward LDS image (W images, bias |
+// gamma | beta, input LN), then the W^T images (at G.gbw) and the backward LN
+// parameters.  One element per thread, a segment per blockIdx.y.  The forward /
+// backward workgroups then copy them to LDS with LDS-DMA (global_load_lds, no
+// VGPR round trip), instead of every workgroup re-gathering and converting the
+// fp32 weights (18 us of a 92 us backward workgroup, tools/mlpb_phases.py).
+__global__ __launch_bounds__(256) void k_mlpb_prep(const BDesc* __restrict__ dp) {
+    const BDesc& d = *dp;
+    const int seg = blockIdx.y, e = blockIdx.x * 256 + threadIdx.x;
+    __bf16* fimg = reinterpret_cast<__bf16*>(d.gimg);
+    float* fprm = reinterpret_cast<float*>(d.gimg + d.fimg);
+    __bf16* bimg = reinterpret_cast<__bf16*>(d.gimg + d.gbo);
+    float* bprm = reinterpret_cast<float*>(d.gimg + d.gpo);
+    if (seg < d.nG) {                                  // forward image of GEMM seg: [pad16 N][fs]
+        const BG& G = d.G[seg];
+        if (e >= p16(G.N) * G.fs) return;
+        const int n = e / G.fs, q = e - n * G.fs;
+        const int k = (q & ~31) + kperm(q & 31);
+        fimg[G.fo + e] = (__bf16)((n < G.N && q < p32(G.K) && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f);
+    } else if (seg == d.nG) {                          // forward params
+        const int d0p = p16(d.d0);
+        if (e < d.pin) {
+            int g = 0;
+            while (g + 1 < d.nG && e >= d.G[g + 1].po) ++g;
+            const BG& G = d.G[g];
+            const int Np = p16(G.N), c = e - G.po, w = c >= 2 * Np ? 2 : (c >= Np ? 1 : 0), f = c - w * Np;
+            const bool lnl = g < d.L && d.l[g].ln;
+            const float* src = w == 0 ? G.b : (lnl ? (w == 1 ? d.l[g].g : d.l[g].be) : nullptr);
+            fprm[e] = (src && f < G.N) ? src[f] : 0.f;
+        } else if (e < d.pin + 2 * d0p) {
+            const int c = e - d.pin, w = c >= d0p, f = c - w * d0p;
+            fprm[e] = f < d.d0 ? (w == 0 ? d.g0 : d.be0)[f] : 0.f;
+        }
+    } else if (seg <= 2 * d.nG) {                      // W^T image: [pad16 K][bs], img[k][p] = W[perm p][k]
+        const BG& G = d.G[seg - d.nG - 1];
+        if (e >= p16(G.K) * G.bs) return;
+        const int k = e / G.bs, q = e - k * G.bs;
+        const int n = (q & ~31) + kperm(q & 31);
+        bimg[G.gbw + e] = (__bf16)((q < p32(G.N) && n < G.N && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f);
+    } else {                                           // backward LN params (+ the input LN)
+        if (e >= d.bprm) return;
+        if (e >= d.bpin) {
+            const int d0p = p16(d.d0), c = e - d.bpin, w = c >= d0p, f = c - w * d0p;
+            bprm[e] = f < d.d0 ? (w == 0 ? d.g0 : d.be0)[f] : 0.f;
+            return;
+        }
+        int l = -1;
+        for (int i = 0; i < d.L; ++i)
+            if (d.l[i].ln && e >= d.l[i].bpo) l = i;
+        const int Np = p16(d.G[l].N), c = e - d.l[l].bpo, w = c >= Np, f = c - w * Np;
+        bprm[e] = f < d.G[l].N ? (w == 0 ? d.l[l].g : d.l[l].be)[f] : 0.f;
+    }
+}
+
+// bytes [0, nbytes) of global src -> LDS dst (16-B aligned, nbytes a multiple of 16)
+// by LDS-DMA: each wave moves 1 KB per instruction (lane l -> dst + 16 l); the caller
+// waits (vmcnt) and synchronises
+__device__ __forceinline__ void lds_copy(char* dst, const char* src, int nbytes) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int c = 1024 * wv; c < nbytes; c += 1024 * NW) {
+        if (c + 16 * lane < nbytes)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c + 16 * lane),
+                                             (__attribute__((address_space(3))) void*)(dst + c), 16, 0, 0);
+    }
+}
+__device__ __forceinline__ void lds_copy_wait() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
 // ------------------------------------------------------------------ forward
 // the weight images are built from the fp32 master weights at every launch
 // (the optimizer rewrites them each step); loads in batches of SB per thread,
@@ -389,8 +465,13 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const __bf16* img = reinterpret_cast<const __bf16*>(smem);
     float* prm = reinterpret_cast<float*>(smem + d.fimg);
-    stage_fwd(d, reinterpret_cast<__bf16*>(smem), prm);
-    __syncthreads();
+    if (d.gimg) {
+        lds_copy(smem, d.gimg, d.fbytes);
+        lds_copy_wait();
+    } else {
+        stage_fwd(d, reinterpret_cast<__bf16*>(smem), prm);
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4, lr = lane & 15;
     const int L = d.L, d0 = d.d0, DL = d.G[L - 1].N;
     const int64_t ntiles = (R + 15) / 16;
@@ -637,11 +718,18 @@ __device__ __forceinline__ void dw_img(const __bf16* zi, const __bf16* hi, int N
 // skip projection) with ONE global round trip, overlapped with the LayerNorm
 // backward: the raw xhat of the step's H source (layer l-1's LN output) is loaded
 // at the step start, used for H, and carried to the next step as its LN input.
+// stamps (diagnostic, vt_resmlp_bf16_set_stamps; nullptr normally): wave 0's wall clock at
+// the start, after the staging, per step after the first barrier, the dZ pass, the H pass, the
+// image barrier, the GEMM + dW and the flush, and at the end (255): 256 entries per workgroup
+#define MB_STAMP(k)                                                                          \
+    do {                                                                                     \
+        if (stamps && threadIdx.x == 0) stamps[(int64_t)blockIdx.x * 256 + (k)] = wall_clock64(); \
+    } while (0)
 template <int NT, int TPW>
 __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp, const float* __restrict__ dout,
                                                     const float* __restrict__ xh, const float* __restrict__ rs,
                                                     int64_t R, int64_t Rp, float* __restrict__ dx,
-                                                    float* __restrict__ part) {
+                                                    float* __restrict__ part, unsigned long long* __restrict__ stamps) {
     const BDesc& d = *dp;
     constexpr int KS = (NT + 1) / 2;
     constexpr int TNS = (NT + 1) / 2;          // dW output tiles per wave along n
@@ -658,7 +746,13 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
     const int L = d.L, d0 = d.d0, DL = d.G[L - 1].N;
     const int64_t rbase = (int64_t)blockIdx.x * ROWS + 16 * wv + (lane & 15);
     float* pb = part + (int64_t)blockIdx.x * d.P;
+    MB_STAMP(0);
 
+    if (d.gimg) {   // W^T images (if resident) and LN parameters from the global image
+        if (d.bres) lds_copy(reinterpret_cast<char*>(wimg), d.gimg + d.gbo, 2 * d.bwimg);
+        lds_copy(reinterpret_cast<char*>(prm), d.gimg + d.gpo, 4 * d.bprm);
+        lds_copy_wait();
+    } else {
     if (d.bres)
         for (int g = 0; g < d.nG; ++g) stage_wt(d.G[g], wimg);
     // gamma / beta of every LayerNorm (+ the input LN), staged once; layer l's at prm + l.bpo
@@ -673,14 +767,21 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
             prm[o + c] = f < C ? (w == 0 ? g : be)[f] : 0.f;
         }
     }
+    }
     const float* prm_in = prm + d.bpin;
+    MB_STAMP(1);
 
     f32x4 dh[TPW][NT], xc[TPW][NT];            // output gradient / raw xhat of the current layer
+    float rsc[TPW];                            // rstd of the current layer's LayerNorm (prefetched with xc)
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
         const int64_t row = rbase + IMR * u;
         load_rows<NT>(dh[u], dout, DL, R, row);
-        if (d.l[L - 1].ln) load_sv<NT>(xc[u], xh + (int64_t)d.l[L - 1].xo * Rp, DL, Rp, row, row < R);
+        rsc[u] = 0.f;
+        if (d.l[L - 1].ln) {
+            load_sv<NT>(xc[u], xh + (int64_t)d.l[L - 1].xo * Rp, DL, Rp, row, row < R);
+            rsc[u] = bld(brs(rs + (int64_t)d.l[L - 1].ri * Rp, Rp * 4), row < R ? (unsigned)(row * 4) : OOB);
+        }
     }
 
     const int nsteps = L + (d.skip == 2 ? 1 : 0);
@@ -694,10 +795,17 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
         const float* gH = hsrc >= 0 ? prm + d.l[hsrc].bpo : prm_in;
         const int CH = hsrc >= 0 ? d.G[hsrc].N : d0, actH = hsrc >= 0 ? d.l[hsrc].act : 0;
         const float* xH = xh + (hsrc >= 0 ? (int64_t)d.l[hsrc].xo * Rp : 0);
+        const rsrc_t rH = brs(rs + (hsrc >= 0 ? (int64_t)d.l[hsrc].ri * Rp : 0), Rp * 4);   // its rstd
         // the H source rows: in flight during the LayerNorm backward below (the
         // widest stacks load them after it, for registers)
         constexpr bool PF = NT <= 6;
         f32x4 xn[TPW][NT];
+        float rsn[TPW];
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int64_t row = rbase + IMR * u;
+            rsn[u] = bld(rH, row < R ? (unsigned)(row * 4) : OOB);
+        }
         if constexpr (PF) {
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
@@ -706,7 +814,13 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
             }
         }
         __syncthreads();                      // previous step done with the W^T / dZ / H images and red
-        if (!d.bres) stage_wt(G, wimg);
+        MB_STAMP(2 + 6 * step);
+        if (!d.bres) {
+            if (d.gimg)
+                lds_copy(reinterpret_cast<char*>(wimg), d.gimg + d.gbo + 2 * G.gbw, 2 * ((p16(K) * G.bs + 7) & ~7));
+            else
+                stage_wt(G, wimg);
+        }
         float la[NT], lb[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
@@ -714,7 +828,6 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             const int64_t row = rbase + IMR * u;
-            const bool rok = row < R;
             f32x4 dz[NT];
             if (skp) {
                 load_rows<NT>(dz, dout, DL, R, row);
@@ -722,15 +835,15 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
 #pragma unroll
                 for (int t = 0; t < NT; ++t) dz[t] = dh[u][t];
                 if (ln) {
-                    const float rstd = bld(brs(rs + (int64_t)d.l[l].ri * Rp, Rp * 4), rok ? (unsigned)(row * 4) : OOB);
                     const float* gl = prm + d.l[l].bpo;
-                    ln_bwd<NT>(dz, xc[u], rstd, N, gl, gl + p16(N), d.l[l].act, la);
+                    ln_bwd<NT>(dz, xc[u], rsc[u], N, gl, gl + p16(N), d.l[l].act, la);
                 }
             }
             colsum<NT>(dz, N, lb);            // the bias gradient: fp32 sum of dZ (not of its bf16 image)
             put_img<NT, IS>(zimg, dz, N, 128 * u + 16 * wv);
             frags<NT>(dz, b[u]);
         }
+        MB_STAMP(3 + 6 * step);
         if constexpr (!PF) {
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
@@ -754,8 +867,12 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
             put_img<NT, IS>(himg, hv, K, 128 * u + 16 * wv);
 #pragma unroll
             for (int t = 0; t < NT; ++t) xc[u][t] = xn[u][t];   // the next step's LN input
+            rsc[u] = rsn[u];
         }
+        MB_STAMP(4 + 6 * step);
+        if (!d.bres && d.gimg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this step's W^T image
         __syncthreads();   // images (W^T, dZ, H) complete
+        MB_STAMP(5 + 6 * step);
         // dH_prev = W^T dz (dz as the B operand; the W^T image rows = K features)
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
@@ -771,7 +888,9 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
         }
         // dW over the block's rows -> this workgroup's partial (db: column K, from the column sums)
         dw_img<TNS, TKS, ROWS, IS>(zimg, himg, N, K, pb + G.wo);
+        MB_STAMP(6 + 6 * step);
         flush_cols<NT>(red, la, lb, N, ln, ln ? pb + d.l[l].lpo : nullptr, pb + G.wo + K, K + 1);
+        MB_STAMP(7 + 6 * step);
     }
     // identity skip: d x0 += dout
     if (d.skip == 1) {
@@ -791,14 +910,14 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
         const int64_t row = rbase + IMR * u;
-        const bool rok = row < R;
-        const float rstd = bld(brs(rs, Rp * 4), rok ? (unsigned)(row * 4) : OOB);
-        ln_bwd<NT>(dh[u], xc[u], rstd, d0, prm_in, prm_in + p16(d0), 0, la);
+        ln_bwd<NT>(dh[u], xc[u], rsc[u], d0, prm_in, prm_in + p16(d0), 0, la);   // rsc: the input LN's rstd
         store_rows<NT>(dx, dh[u], d0, R, row);
     }
     __syncthreads();
     flush_cols<NT>(red, la, lb, d0, true, pb + d.lpo0, nullptr, 0);
+    MB_STAMP(255);
 }
+#undef MB_STAMP
 
 // ---------------------------------------------------------------- final sum
 // one segment per dW|db slab (E = N (K + 1), K1 = K + 1) or gamma|beta pair
@@ -857,6 +976,8 @@ struct BPlan {
     BDesc d;
     int nt, tpw;
     int64_t Rp, xh_floats, rs_floats, nblk;
+    int gbytes;                  // global image bytes
+    int prep_x, prep_y;          // k_mlpb_prep grid
 };
 
 int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
@@ -924,7 +1045,7 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
         po += 3 * h16(G.N);
         G.bs = h32(G.N) + 16;
         const int e = (h16(G.K) * G.bs + 7) & ~7;
-        G.bw = bwtot;
+        G.bw = G.gbw = bwtot;
         bwtot += e;
         bw = e > bw ? e : bw;
         bh = h16(G.K) > bh ? h16(G.K) : bh;
@@ -932,7 +1053,7 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
     }
     d.fimg = 2 * off;
     d.pin = po;
-    d.fbytes = d.fimg + 4 * (po + 2 * h16(dims[0]));
+    d.fbytes = (d.fimg + 4 * (po + 2 * h16(dims[0])) + 15) & ~15;   // 16-B multiple: copied by LDS-DMA
     const int ntw = (wmax + 15) / 16;
     p.nt = ntw <= 2 ? 2 : ntw <= 4 ? 4 : ntw <= 6 ? 6 : 9;
     d.bhrows = bh;
@@ -958,6 +1079,10 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
         for (int g = 0; g < d.nG; ++g) d.G[g].bw = 0;
     d.bwimg = d.bres ? bwtot : bw;
     d.bbytes = 2 * d.bwimg + rest;
+    // global image (k_mlpb_prep): forward LDS image | W^T images | backward params
+    d.gbo = (d.fbytes + 15) & ~15;
+    d.gpo = d.gbo + ((2 * bwtot + 15) & ~15);
+    p.gbytes = d.gpo + ((4 * bprm + 15) & ~15);
     // partials: dW|db of every GEMM, then gamma|beta of every LN and the input LN
     int P = 0;
     for (int g = 0; g < d.nG; ++g) {
@@ -981,6 +1106,8 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
     VT_CHECK_ARG(d.bbytes <= 160 * 1024, "%s: backward needs %d bytes of LDS (> 160 KiB)", who, d.bbytes);
     return VT_OK;
 }
+
+unsigned long long* g_mlpb_stamps = nullptr;  // diagnostic (vt_resmlp_bf16_set_stamps)
 
 int n_fwd_blocks(int64_t R) {
     static int ncu = 0;
@@ -1067,6 +1194,23 @@ int get_plan(const BPlan*& out, const BDesc*& dev, int n_layers, const int* dims
     PlanEntry e;
     const int rc = make_bplan(e.plan, n_layers, dims, layer_ln, layer_act, skip, eps, params, R, who);
     if (rc) return rc;
+    {
+        BPlan& p = e.plan;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        VT_CHECK_ARG(hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone,
+                     "%s: new stack shape under stream capture (run one eager step first)", who);
+        VT_CHECK_ARG(hipMalloc(reinterpret_cast<void**>(&p.d.gimg), p.gbytes) == hipSuccess,
+                     "%s: global image allocation (%d bytes)", who, p.gbytes);
+        int emax = p.d.pin + 2 * h16(dims[0]);
+        emax = p.d.bprm > emax ? p.d.bprm : emax;
+        for (int g = 0; g < p.d.nG; ++g) {
+            const BG& G = p.d.G[g];
+            emax = h16(G.N) * G.fs > emax ? h16(G.N) * G.fs : emax;
+            emax = h16(G.K) * G.bs > emax ? h16(G.K) * G.bs : emax;
+        }
+        p.prep_x = (emax + 255) / 256;
+        p.prep_y = 2 * p.d.nG + 2;
+    }
     e.dev = device_desc(e.plan.d, st);
     VT_CHECK_ARG(e.dev, "%s: descriptor upload failed", who);
     e.key = std::move(key);
@@ -1107,6 +1251,8 @@ int vt_resmlp_bf16_fwd(int n_layers, const int* dims, const int* layer_ln, const
     if (rc) return rc;
     const BPlan& p = *pp;
     VT_CHECK_ARG(x && out && xhat && rstd, "vt_resmlp_bf16_fwd: null buffer");
+    // the weight images of this step (read again by the backward of this forward)
+    hipLaunchKernelGGL(k_mlpb_prep, dim3((unsigned)p.prep_x, (unsigned)p.prep_y), dim3(256), 0, st, ddev);
     const dim3 grid((unsigned)n_fwd_blocks(rows));
     const bool id = skip == 1;
     switch (p.nt * 2 + (id ? 1 : 0)) {
@@ -1158,7 +1304,7 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
     if (p.nt == NTV && p.tpw == TPWV) {                                                                    \
         set_lds(k_mlpb_bwd<NTV, TPWV>, p.d.bbytes);                                                        \
         hipLaunchKernelGGL((k_mlpb_bwd<NTV, TPWV>), grid, dim3(BT), p.d.bbytes, st, ddev, dout, xhat, rstd, rows, \
-                           p.Rp, dx, ws);                                                                  \
+                           p.Rp, dx, ws, g_mlpb_stamps);                                                   \
     }
     VT_MBB(2, 2) VT_MBB(4, 2) VT_MBB(2, 1) VT_MBB(4, 1) VT_MBB(6, 1) VT_MBB(9, 1)
 #undef VT_MBB
@@ -1167,6 +1313,13 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
         hipLaunchKernelGGL(k_mlpb_sum, gs, dim3(256), 0, st, sa, ws, (int)p.nblk, accumulate);
     }
     VT_LAUNCH_CHECK("vt_resmlp_bf16_bwd");
+    return VT_OK;
+}
+
+// Diagnostic: while buf != NULL, backward launches stamp their phase boundaries
+// (128 uint64 per workgroup, k_mlpb_bwd's MB_STAMP points) into buf.
+int vt_resmlp_bf16_set_stamps(void* buf) {
+    g_mlpb_stamps = (unsigned long long*)buf;
     return VT_OK;
 }
 
