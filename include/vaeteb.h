@@ -317,6 +317,21 @@ int vt_conv1d_bwd_gpad_bf16(const float* dY, int B, int L_in, int Cin, const voi
  * split reduction; channels <= 128; ws as vt_conv1d_direct_bwd_weight.          */
 int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode,
                               int up, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);
+/* Fused BatchNorm backward: as vt_conv1d_bwd_gpad_bf16 on the BN input gradient
+ * gamma rstd (dz - dbeta/M - xhat dgamma/M), dz = dY act'(xhat gamma + beta),
+ * xhat = (Xc - mean) rstd, formed while the operand is staged from the block output
+ * gradient dY (B, L_out, Cout), the pre-BN conv output Xc and bnp (vt_batchnorm_bwd_coef):
+ * the same values as vt_batchnorm_bwd's dx, never written in fp32.  dxbn16 (nullable):
+ * receives that gradient in bf16, rows of ceil8(Cout) (padding 0) — the operand of
+ * vt_conv1d_bwd_weight_bf16_dy16, which then equals vt_conv1d_bwd_weight_bf16 on dx.
+ * replaces: the BatchNorm1d backward feeding the conv input / weight gradients
+ *           (ref/model/vae_teb_model.py:175, :230 under autograd)                       */
+int vt_conv1d_bwd_gpad_bf16_bn(const float* dY, const float* Xc, const float* bnp, int act, int64_t M, int B,
+                               int L_in, int Cin, const void* w16t, int Cout, int K, int mode, int up, float* gpad,
+                               void* dxbn16, void* stream);
+int vt_conv1d_bwd_weight_bf16_dy16(const void* dY16, const float* X, int B, int L_in, int Cin, int Cout, int K,
+                                   int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
+                                   void* stream);
 /* Direct (LDS-windowed) conv kernels used on the training path (conv.hip), K <= 11:
  * forward; bwd-data as a full correlation into gpad (B, L_out+K-1, Cin) + fold;
  * bwd-weight with fixed-order split reduction.                                   */
@@ -348,6 +363,12 @@ int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const
 int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, int act, float* dx, float* dgamma, float* dbeta,
                      int accumulate_params, float* ws, int64_t ws_floats, void* stream);
+/* The column-sum half of vt_batchnorm_bwd (dgamma / dbeta (+)= their sums) with no dx:
+ * bnp = [mean | rstd | gamma | beta | dgamma_now | dbeta_now] (6 x C floats) for the bf16
+ * conv backward kernels that form dx while staging their operand (*_bf16_bn below). */
+int vt_batchnorm_bwd_coef(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                          const float* gamma, const float* beta, int act, float* dgamma, float* dbeta,
+                          int accumulate_params, float* bnp, float* ws, int64_t ws_floats, void* stream);
 /* Eval-mode BatchNorm1d (running statistics) + activation, elementwise on (M, C).
  * replaces: model.eval() BatchNorm in ref/model/vae_teb_model.py:175,:230 and
  *           ref/model/inception_time.py:77,:139 (validation, frozen VAE, predict) */

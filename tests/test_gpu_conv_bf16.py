@@ -163,3 +163,58 @@ def test_model_bf16_convs_close_to_fp32(golden):
     for prefix in (("decoder.conv.", "decoder.output_"), ""):
         assert dev("bf16", prefix) <= 3 * dev("pert", prefix) + 1e-3, (prefix, dev("bf16", prefix),
                                                                          dev("pert", prefix))
+
+
+@pytest.mark.parametrize("geo", GEOS)
+@pytest.mark.parametrize("act", [1, 3])
+def test_fused_batchnorm_backward_bitwise(L, geo, act):
+    """vt_batchnorm_bwd_coef + vt_conv1d_bwd_gpad_bf16_bn (the BN input gradient formed
+    while the backward-data conv stages its operand, also left in bf16) +
+    vt_conv1d_bwd_weight_bf16_dy16 == vt_batchnorm_bwd's materialised dx fed to the
+    unfused bf16 kernels, bit for bit; dgamma / dbeta equal."""
+    B, Lin, Cin, Cout, K, mode, up = geo
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    M = B * Lo
+    torch.manual_seed(sum(geo) + act)
+    x = torch.randn(B, Lin, Cin, device="cuda")
+    w = torch.randn(Cout, Cin, K, device="cuda") / (Cin * K) ** 0.5
+    conv = torch.randn(B, Lo, Cout, device="cuda") * 2 + 0.3
+    gy = torch.randn(B, Lo, Cout, device="cuda")
+    mean = conv.reshape(-1, Cout).mean(0)
+    rstd = 1 / (conv.reshape(-1, Cout).var(0, unbiased=False) + 1e-5).sqrt()
+    gam = 1 + 0.1 * torch.randn(Cout, device="cuda")
+    bet = 0.1 * torch.randn(Cout, device="cuda")
+    _, w16t = _shadow(L, w)
+    ws = torch.empty(4096 * Cout + 2 * Cout, device="cuda")
+    wsw = torch.empty(8 << 20, device="cuda")
+    # unfused reference
+    dx = torch.empty_like(conv)
+    dg0, db0 = torch.empty(Cout, device="cuda"), torch.empty(Cout, device="cuda")
+    L.call("vt_batchnorm_bwd", L.ptr(gy), L.ptr(conv), M, Cout, L.ptr(mean), L.ptr(rstd), L.ptr(gam), L.ptr(bet), act,
+           L.ptr(dx), L.ptr(dg0), L.ptr(db0), 0, L.ptr(ws), ws.numel(), L.stream())
+    gp0 = torch.empty(B, Lo + K - 1, Cin, device="cuda")
+    L.call("vt_conv1d_bwd_gpad_bf16", L.ptr(dx), B, Lin, Cin, L.ptr(w16t), Cout, K, mode, up, L.ptr(gp0), L.stream())
+    dw0 = torch.empty(Cout, Cin, K, device="cuda")
+    L.call("vt_conv1d_bwd_weight_bf16", L.ptr(dx), L.ptr(x), B, Lin, Cin, Cout, K, mode, up, L.ptr(dw0), 0,
+           L.ptr(wsw), wsw.numel(), L.stream())
+    # fused
+    bnp = torch.empty(6 * Cout, device="cuda")
+    dg1, db1 = torch.empty(Cout, device="cuda"), torch.empty(Cout, device="cuda")
+    L.call("vt_batchnorm_bwd_coef", L.ptr(gy), L.ptr(conv), M, Cout, L.ptr(mean), L.ptr(rstd), L.ptr(gam),
+           L.ptr(bet), act, L.ptr(dg1), L.ptr(db1), 0, L.ptr(bnp), L.ptr(ws), ws.numel(), L.stream())
+    gp1 = torch.empty_like(gp0)
+    cp = (Cout + 7) // 8 * 8
+    dxbn = torch.full((M, cp), float("nan"), dtype=torch.bfloat16, device="cuda")
+    L.call("vt_conv1d_bwd_gpad_bf16_bn", L.ptr(gy), L.ptr(conv), L.ptr(bnp), act, M, B, Lin, Cin, L.ptr(w16t), Cout,
+           K, mode, up, L.ptr(gp1), L.ptr(dxbn), L.stream())
+    dw1 = torch.empty_like(dw0)
+    L.call("vt_conv1d_bwd_weight_bf16_dy16", L.ptr(dxbn), L.ptr(x), B, Lin, Cin, Cout, K, mode, up, L.ptr(dw1), 0,
+           L.ptr(wsw), wsw.numel(), L.stream())
+    torch.cuda.synchronize()
+    # the bf16 side output is dx rounded to bf16, zero in the channel padding, every row written
+    assert torch.equal(dxbn[:, :Cout].float(), dx.reshape(M, Cout).bfloat16().float())
+    assert (dxbn[:, Cout:] == 0).all()
+    assert torch.equal(dg0, dg1) and torch.equal(db0, db1)
+    assert torch.equal(gp0, gp1), ((gp0 != gp1).sum().item(), gp0.numel(), (gp0 - gp1).abs().max().item(),
+                                   gp0.abs().max().item(), (dw0 != dw1).sum().item())
+    assert torch.equal(dw0, dw1)

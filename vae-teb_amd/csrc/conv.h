@@ -2,6 +2,7 @@
 // kernels: padding / x2 linear upsampling applied while an operand window is
 // staged (ref/model/vae_teb_model.py:128-253).
 #pragma once
+#include "bnbwd.h"
 #include "common.h"
 
 namespace vt {

@@ -45,10 +45,18 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
 }
 
 // x: fp32 (B, L_in, g.Cin) activations; w16: [g.Cout][K][cin32] bf16 shadow.
-template <int K, int NT>
+// BNB (backward-data only: causal geometry, no upsample): x is the block output
+// gradient dy and the staged operand is the BatchNorm input gradient computed on
+// the fly from dy, the pre-BN conv output x2 and bnp (conv.h bn_bwd_val).
+// dbf (BNB, nullable): the staged BN input gradient, bf16, is also written to
+// dbf[(b L_in + t) cpad + c] (cpad = ceil8(Cin)) by the blockIdx.y == 0 workgroups
+// for their own rows t0 .. t0 + TP - 1 (each row once) — the weight gradient's operand.
+template <int K, int NT, bool BNB = false>
 __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, Geo g, const __bf16* __restrict__ w16,
                                                    int cin32, float* __restrict__ y, int Lo,
-                                                   float* __restrict__ stats) {
+                                                   float* __restrict__ stats, const float* __restrict__ x2,
+                                                   const float* __restrict__ bnp, int act, float invM,
+                                                   __bf16* __restrict__ dbf) {
     using C = BCfg<K, NT>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
     extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
@@ -57,6 +65,12 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
     const int t0 = blockIdx.x * TP, co0 = blockIdx.y * TC, b = blockIdx.z;
     const float* xb = x + (int64_t)b * g.L_in * g.Cin;
+    float* bp = reinterpret_cast<float*>(reinterpret_cast<char*>(lb) + C::LDS_BYTES);  // BNB: 6 x Cin params
+    if constexpr (BNB) {
+        for (int i = tid; i < 6 * g.Cin; i += 256) bp[i] = bnp[i];
+        __syncthreads();
+    }
+    const float* x2b = BNB ? x2 + (int64_t)b * g.L_in * g.Cin : nullptr;
     f32x4 acc[PM][NT];
 #pragma unroll
     for (int m = 0; m < PM; ++m)
@@ -69,8 +83,24 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
             const int tp = t0 + row, cb = c0 + 8 * oct;
             float v[8];
             const bool ok = tp < Lo + K - 1;
+            if constexpr (BNB) {
+                const int t = tp - g.pad;   // causal geometry: zero outside [0, L_in)
+                const bool in = ok && t >= 0 && t < g.L_in;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (ok && cb + j < g.Cin) ? src_val(xb, g, tp, cb + j) : 0.f;
+                for (int j = 0; j < 8; ++j) {
+                    const int c = cb + j;
+                    v[j] = (in && c < g.Cin) ? bn_bwd_val(xb[(int64_t)t * g.Cin + c], x2b[(int64_t)t * g.Cin + c], bp,
+                                                           g.Cin, c, act, invM)
+                                             : 0.f;
+                }
+                if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
+                    const int cpad = (g.Cin + 7) & ~7;   // cb < Cin and cb % 8 == 0: the octet fits the padded row
+                    *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (ok && cb + j < g.Cin) ? src_val(xb, g, tp, cb + j) : 0.f;
+            }
             *(bf16x8*)(xs + row * RS + 8 * oct) = pack8(v);
         }
         // taps: K x TC rows x 4 octets, 16 B each from the shadow
@@ -214,10 +244,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int row0, int col0,
     return __builtin_bit_cast(bf16x8, r);
 }
 
-template <int K, int PPW>
+// DYB: dY given in bf16 (dyb16, row stride dys = ceil8(Cout)), e.g. the BN input
+// gradient written by the fused backward-data kernel (k_conv_bf16 BNB + dbf).
+template <int K, int PPW, bool DYB = false>
 __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ dy, const float* __restrict__ x, Geo g,
                                                       int64_t rows_per_split, int NTc, int npairs, int dstride,
-                                                      int xstride, float* __restrict__ part) {
+                                                      int xstride, float* __restrict__ part,
+                                                      const __bf16* __restrict__ dyb16, int dys) {
     extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
     __bf16* ds = lb;                          // [DWR][dstride]   dY rows
     __bf16* xs = lb + DWR * dstride;          // [DWR + K - 1 (+pad)][xstride] input window
@@ -247,13 +280,25 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
         if (n > DWR) n = DWR;
         if (r + n > r1) n = (int)(r1 - r);
         const float* xb = x + (int64_t)b * g.L_in * g.Cin;
-        const float* dyb = dy + ((int64_t)b * g.L_out + t0) * g.Cout;
+        const float* dyb = DYB ? nullptr : dy + ((int64_t)b * g.L_out + t0) * g.Cout;
         // dY rows (zero rows past n, zero channels past Cout), 4 channels per thread-item
+        if constexpr (DYB) {
+            const __bf16* db16 = dyb16 + ((int64_t)b * g.L_out + t0) * dys;
+            typedef short v4s __attribute__((ext_vector_type(4)));
+            for (int i = tid; i < DWR * (cout16 / 4); i += 256) {
+                const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
+                v4s v = v4s{0, 0, 0, 0};
+                if (t < n && c < dys) v = *(const v4s*)(db16 + (int64_t)t * dys + c);   // pad channels are 0
+                *(v4s*)(ds + t * dstride + c) = v;
+            }
+        } else
         for (int i = tid; i < DWR * (cout16 / 4); i += 256) {
             const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
             float v[4];
+            {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (t < n && c + j < g.Cout) ? dyb[(int64_t)t * g.Cout + c + j] : 0.f;
+                for (int j = 0; j < 4; ++j) v[j] = (t < n && c + j < g.Cout) ? dyb[(int64_t)t * g.Cout + c + j] : 0.f;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) ds[t * dstride + c + j] = (__bf16)v[j];
         }
@@ -302,43 +347,58 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
     }
 }
 
+// BatchNorm-backward staging (k_conv_bf16 / k_conv_dw_bf16 BNB): dy, the pre-BN
+// conv output, the packed per-channel parameters (6 x C), activation and 1/M
+struct BnB {
+    const float* x2;
+    const float* bnp;
+    int act;
+    float invM;
+    __bf16* dbf;   // nullable: bf16 copy of the BN input gradient (the weight gradient's operand)
+};
+
 template <int K, int NT>
 int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
-          hipStream_t st) {
+          hipStream_t st, const BnB* bn) {
     using C = BCfg<K, NT>;
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
-    if (x)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y, Lo, stats);
+    if (x && bn)
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
+                           cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf);
+    else if (x)
+        hipLaunchKernelGGL((k_conv_bf16<K, NT>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y, Lo, stats,
+                           nullptr, nullptr, 0, 0.f, nullptr);
     return C::TP;
 }
 
 template <int K>
-int bf_k(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats, hipStream_t st) {
+int bf_k(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats, hipStream_t st,
+         const BnB* bn) {
     switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
-        case 1: return bf_nt<K, 1>(x, g, w16, cin32, y, Lo, stats, st);
-        case 2: return bf_nt<K, 2>(x, g, w16, cin32, y, Lo, stats, st);
-        case 3: return bf_nt<K, 3>(x, g, w16, cin32, y, Lo, stats, st);
-        case 4: return bf_nt<K, 4>(x, g, w16, cin32, y, Lo, stats, st);
-        case 5: return bf_nt<K, 5>(x, g, w16, cin32, y, Lo, stats, st);
-        default: return bf_nt<K, 6>(x, g, w16, cin32, y, Lo, stats, st);
+        case 1: return bf_nt<K, 1>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 2: return bf_nt<K, 2>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 3: return bf_nt<K, 3>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 4: return bf_nt<K, 4>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 5: return bf_nt<K, 5>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        default: return bf_nt<K, 6>(x, g, w16, cin32, y, Lo, stats, st, bn);
     }
 }
 
 // x == nullptr: no launch, only the position tile of this geometry
 int bf_launch(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
-              hipStream_t st) {
+              hipStream_t st, const BnB* bn = nullptr) {
     switch (g.K) {
-        case 1: return bf_k<1>(x, g, w16, cin32, y, Lo, stats, st);
-        case 2: return bf_k<2>(x, g, w16, cin32, y, Lo, stats, st);
-        case 3: return bf_k<3>(x, g, w16, cin32, y, Lo, stats, st);
-        case 4: return bf_k<4>(x, g, w16, cin32, y, Lo, stats, st);
-        case 5: return bf_k<5>(x, g, w16, cin32, y, Lo, stats, st);
-        case 6: return bf_k<6>(x, g, w16, cin32, y, Lo, stats, st);
-        case 7: return bf_k<7>(x, g, w16, cin32, y, Lo, stats, st);
-        case 8: return bf_k<8>(x, g, w16, cin32, y, Lo, stats, st);
-        case 9: return bf_k<9>(x, g, w16, cin32, y, Lo, stats, st);
-        case 10: return bf_k<10>(x, g, w16, cin32, y, Lo, stats, st);
-        default: return bf_k<11>(x, g, w16, cin32, y, Lo, stats, st);
+        case 1: return bf_k<1>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 2: return bf_k<2>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 3: return bf_k<3>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 4: return bf_k<4>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 5: return bf_k<5>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 6: return bf_k<6>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 7: return bf_k<7>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 8: return bf_k<8>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 9: return bf_k<9>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 10: return bf_k<10>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        default: return bf_k<11>(x, g, w16, cin32, y, Lo, stats, st, bn);
     }
 }
 
@@ -390,18 +450,31 @@ int vt_conv1d_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16
     return VT_OK;
 }
 
-int vt_conv1d_bwd_gpad_bf16(const float* dY, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode,
-                            int up, float* gpad, void* stream) {
-    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB, "vt_conv1d_bwd_gpad_bf16: shape");
+static int bwd_gpad(const float* dY, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode, int up,
+                    float* gpad, hipStream_t st, const BnB* bn, const char* who) {
+    VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB, "%s: shape", who);
     Geo f = geo(B, L_in, Cin, Cout, K, mode, up);
     Geo g = geo(B, f.L_out, Cout, Cin, K, 0, 0);  // input dY (L_out x Cout), causal pad K-1
-    bf_launch(dY, g, (const __bf16*)w16t, cdiv(Cout, 32) * 32, gpad, f.L_out + K - 1, nullptr, S(stream));
-    VT_LAUNCH_CHECK("vt_conv1d_bwd_gpad_bf16");
+    bf_launch(dY, g, (const __bf16*)w16t, cdiv(Cout, 32) * 32, gpad, f.L_out + K - 1, nullptr, st, bn);
+    VT_LAUNCH_CHECK(who);
     return VT_OK;
 }
 
-int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode,
-                              int up, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream) {
+int vt_conv1d_bwd_gpad_bf16(const float* dY, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode,
+                            int up, float* gpad, void* stream) {
+    return bwd_gpad(dY, B, L_in, Cin, w16t, Cout, K, mode, up, gpad, S(stream), nullptr, "vt_conv1d_bwd_gpad_bf16");
+}
+
+int vt_conv1d_bwd_gpad_bf16_bn(const float* dY, const float* Xc, const float* bnp, int act, int64_t M, int B,
+                               int L_in, int Cin, const void* w16t, int Cout, int K, int mode, int up, float* gpad,
+                               void* dxbn16, void* stream) {
+    VT_CHECK_ARG(Xc && bnp && act >= 0 && act <= 3 && M > 0, "vt_conv1d_bwd_gpad_bf16_bn: BatchNorm arguments");
+    const BnB bn{Xc, bnp, act, 1.f / (float)M, (__bf16*)dxbn16};
+    return bwd_gpad(dY, B, L_in, Cin, w16t, Cout, K, mode, up, gpad, S(stream), &bn, "vt_conv1d_bwd_gpad_bf16_bn");
+}
+
+static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode, int up,
+                      float* dW, int accumulate, float* ws, int64_t ws_floats, hipStream_t st, const __bf16* dy16) {
     VT_CHECK_ARG(B > 0 && L_in > 0 && K > 0 && K <= KMAXB && Cin > 0 && Cout > 0 && Cin <= 128 && Cout <= 128,
                  "vt_conv1d_bwd_weight_bf16: shape (K <= %d, channels <= 128)", KMAXB);
     Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
@@ -424,12 +497,17 @@ int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, 
     // row strides (bf16): channels rounded to 16, + 8 (rows start 16 B apart mod 64 banks)
     const int dstride = 16 * cdiv(Cout, 16) + 8, xstride = 16 * cdiv(Cin, 16) + 8;
     const size_t lds = (size_t)(DWR * dstride + (DWR + KMAXB + 8) * xstride) * 2;
+    const int dys = (Cout + 7) & ~7;
     dim3 grid(bx, (unsigned)splits);
-    hipStream_t st = S(stream);
 #define VT_DWB(KK, PP)                                                                                         \
-    if (K == KK && ppw == PP)                                                                                  \
-        hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP>), grid, dim3(256), lds, st, dY, X, g, rps, NTc, npairs, dstride, \
-                           xstride, ws);
+    if (K == KK && ppw == PP) {                                                                                \
+        if (dy16)                                                                                              \
+            hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true>), grid, dim3(256), lds, st, dY, X, g, rps, NTc, npairs, \
+                               dstride, xstride, ws, dy16, dys);                                              \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP>), grid, dim3(256), lds, st, dY, X, g, rps, NTc, npairs, \
+                               dstride, xstride, ws, nullptr, 0);                                             \
+    }
 #define VT_DWB6(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3) VT_DWB(KK, 4) VT_DWB(KK, 5) VT_DWB(KK, 6)
 #define VT_DWB4(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3) VT_DWB(KK, 4)
 #define VT_DWB3(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3)
@@ -445,6 +523,19 @@ int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, 
     if (rc) return rc;
     VT_LAUNCH_CHECK("vt_conv1d_bwd_weight_bf16");
     return VT_OK;
+}
+
+int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode,
+                              int up, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream) {
+    return bwd_weight(dY, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream), nullptr);
+}
+
+int vt_conv1d_bwd_weight_bf16_dy16(const void* dY16, const float* X, int B, int L_in, int Cin, int Cout, int K,
+                                   int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
+                                   void* stream) {
+    VT_CHECK_ARG(dY16 != nullptr, "vt_conv1d_bwd_weight_bf16_dy16: null dY16");
+    return bwd_weight(nullptr, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream),
+                      (const __bf16*)dY16);
 }
 
 }  // extern "C"

@@ -12,6 +12,7 @@
 // (ref/model/vae_teb_model.py:175, :206-210, :230, :252-253).
 #include <math.h>
 
+#include "bnbwd.h"
 #include "common.h"
 
 namespace vt {
@@ -378,7 +379,11 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ pa
                                                     int mode, float eps, float momentum, float* __restrict__ mean,
                                                     float* __restrict__ rstd, float* __restrict__ run_mean,
                                                     float* __restrict__ run_var, float* __restrict__ dgamma,
-                                                    float* __restrict__ dbeta, int accumulate) {
+                                                    float* __restrict__ dbeta, int accumulate,
+                                                    float* __restrict__ bnp = nullptr, const float* __restrict__ gamma = nullptr,
+                                                    const float* __restrict__ beta = nullptr,
+                                                    float* __restrict__ pg = nullptr, float* __restrict__ pb = nullptr,
+                                                    int pacc = 0) {
     __shared__ double r0[NT], r1[NT];
     const int c = blockIdx.x;
     double a0 = 0.0, a1 = 0.0;
@@ -411,6 +416,14 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ pa
     } else {
         dbeta[c] = accumulate ? dbeta[c] + (float)s0 : (float)s0;
         dgamma[c] = accumulate ? dgamma[c] + (float)s1 : (float)s1;
+        if (bnp) {   // vt_batchnorm_bwd_coef: the packed parameters and the parameter gradients
+            bnp[c] = mean[c];
+            bnp[C + c] = rstd[c];
+            bnp[2 * C + c] = gamma[c];
+            bnp[3 * C + c] = beta[c];
+            pb[c] = pacc ? pb[c] + (float)s0 : (float)s0;
+            pg[c] = pacc ? pg[c] + (float)s1 : (float)s1;
+        }
     }
 }
 
@@ -528,11 +541,7 @@ __global__ __launch_bounds__(NT) void k_bn_dx4(const float* __restrict__ dy, con
     const int64_t base = (int64_t)blockIdx.x * (NT * 4 * BNV_V);
     const int step = (NT * 4) % C;
     int c = (int)((base + 4 * threadIdx.x) % C);
-    auto one = [&](float xe, float dye, int cc) {
-        const float h = (xe - p[0][cc]) * p[1][cc];
-        const float dz = dye * act_d(h * p[2][cc] + p[3][cc], ACT);
-        return p[2][cc] * p[1][cc] * (dz - p[5][cc] * inv - h * p[4][cc] * inv);
-    };
+    auto one = [&](float xe, float dye, int cc) { return bn_bwd_val(dye, xe, &p[0][0], BNV_C, cc, ACT, inv); };
 #pragma unroll
     for (int v = 0; v < BNV_V; ++v, c = wrapc(c + step, C)) {
         const int64_t j = base + 4 * (threadIdx.x + NT * v);
@@ -824,6 +833,28 @@ int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const fl
     hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
                        accumulate_params);
     VT_LAUNCH_CHECK("vt_batchnorm_bwd");
+    return VT_OK;
+}
+
+// The column sums of the BatchNorm backward without the element-wise pass: dgamma /
+// dbeta (+)= the sums, and bnp = [mean | rstd | gamma | beta | dgamma_now | dbeta_now]
+// (6 x C) for the bf16 conv backward kernels that apply the BN input gradient while
+// staging their operand (vt_conv1d_bwd_*_bf16_bn).
+int vt_batchnorm_bwd_coef(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                          const float* gamma, const float* beta, int act, float* dgamma, float* dbeta,
+                          int accumulate_params, float* bnp, float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0 && C <= 256 && bnp, "vt_batchnorm_bwd_coef: shape");
+    int64_t rpb;
+    const int blocks = bn_blocks(M, ws_floats, C, &rpb);
+    VT_CHECK_ARG(blocks >= 1, "vt_batchnorm_bwd_coef: workspace too small");
+    hipStream_t st = S(stream);
+    float* dg_now = bnp + 4 * C;
+    float* db_now = bnp + 5 * C;
+    col_partial_vec(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st);
+    hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 2, 0.f, 0.f,
+                       const_cast<float*>(mean), const_cast<float*>(rstd), nullptr, nullptr, dg_now, db_now, 0, bnp,
+                       gamma, beta, dgamma, dbeta, accumulate_params);
+    VT_LAUNCH_CHECK("vt_batchnorm_bwd_coef");
     return VT_OK;
 }
 

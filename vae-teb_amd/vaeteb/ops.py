@@ -446,23 +446,42 @@ class ConvBNActF(torch.autograd.Function):
         Cout, _, K = w.shape
         Lo = conv.shape[1]
         gy = gy.contiguous()
-        gconv = torch.empty_like(conv)
         pbn = _ParamGrads([g, b], [True, True])
         ws = WS.get(4096 * Cout + 2 * Cout, x.device, 2)
-        call("vt_batchnorm_bwd", ptr(gy), ptr(conv), B * Lo, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT[act],
-             ptr(gconv), ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(ws), ws.numel(), _st())
+        M = B * Lo
+        fused = bf16 and ctx.needs_input_grad[0]
+        if fused:
+            # fused BatchNorm backward: only the column sums here; the bf16 backward-data
+            # conv forms the BN input gradient while staging its operand from (gy, conv,
+            # bnp) and leaves it in bf16 (dxbn) for the weight gradient
+            bnp = torch.empty(6 * Cout, device=x.device)
+            call("vt_batchnorm_bwd_coef", ptr(gy), ptr(conv), M, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b),
+                 ACT[act], ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(bnp), ptr(ws), ws.numel(), _st())
+            dxbn = torch.empty(M * ((Cout + 7) // 8 * 8), dtype=torch.bfloat16, device=x.device)
+            srcs = (dxbn,)
+            dw_args = lambda wsx: (ptr(dxbn), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc,
+                                   ptr(wsx), wsx.numel(), _st())
+            fn = "vt_conv1d_bwd_weight_bf16_dy16"
+        else:
+            gconv = torch.empty_like(conv)
+            call("vt_batchnorm_bwd", ptr(gy), ptr(conv), M, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT[act],
+                 ptr(gconv), ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(ws), ws.numel(), _st())
+            srcs = (gconv,)
+            dw_args = lambda wsx: (ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc,
+                                   ptr(wsx), wsx.numel(), _st())
+            fn = "vt_conv1d_bwd_weight_bf16" if bf16 else "vt_conv1d_direct_bwd_weight"
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             gpad = WS.get(B * (Lo + K - 1) * Cin, x.device, 3)
-            if bf16:
-                call("vt_conv1d_bwd_gpad_bf16", ptr(gconv), B, L, Cin, ptr(w16t), Cout, K, mode, up, ptr(gpad), _st())
+            if fused:
+                call("vt_conv1d_bwd_gpad_bf16_bn", ptr(gy), ptr(conv), ptr(bnp), ACT[act], M, B, L, Cin, ptr(w16t),
+                     Cout, K, mode, up, ptr(gpad), ptr(dxbn), _st())
             else:
                 call("vt_conv1d_direct_bwd_gpad", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gpad), _st())
             call("vt_conv1d_fold", ptr(gpad), B, L, Cin, Cout, K, mode, up, ptr(gx), 0, _st())
         pw = _ParamGrads([w], [ctx.needs_input_grad[1]])
         if pw.out[0] is not None:
-            fn = "vt_conv1d_bwd_weight_bf16" if bf16 else "vt_conv1d_direct_bwd_weight"
             side = GRAD_STREAM if (pw.direct and GRAD_STREAM is not None) else None
             if side is not None and side != torch.cuda.current_stream():
                 # the weight gradient is off the data-gradient chain: compute it on a
@@ -471,14 +490,12 @@ class ConvBNActF(torch.autograd.Function):
                 side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(side):
                     ws1 = WS.get(WS_LINEAR, x.device, 1)
-                    call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1),
-                         ws1.numel(), _st())
-                gconv.record_stream(side)
-                x.record_stream(side)
+                    call(fn, *dw_args(ws1))
+                for t in (*srcs, x):
+                    t.record_stream(side)
             else:
                 ws1 = WS.get(WS_LINEAR, x.device, 1)
-                call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1),
-                     ws1.numel(), _st())
+                call(fn, *dw_args(ws1))
         gw, = pw.result()
         gg, gb = pbn.result()
         return gx, gw, gg, gb, None, None, None, None, None, None, None, None
