@@ -388,6 +388,18 @@ int vt_lstm_layer_fwd(const float* gin, const float* w_hh, const float* b_hh, in
 /* dgates = d(loss)/d(gate pre-activations) given d(loss)/d(h_t) of this layer.     */
 int vt_lstm_layer_bwd(const float* dh_out, const float* gates, const float* cst, const float* w_hh, int B, int S,
                       int hidden, float* dgates, void* stream);
+/* The same layer with its input projection inside the recurrence kernel (input
+ * size In <= 64, exact-fp32 MFMA): x [B, S, In] -> h, h_{t-1}, c, gates; the
+ * results are bitwise those of vt_linear_fwd + vt_lstm_layer_fwd.
+ * replaces: one layer of nn.LSTM (ref/model/vae_teb_model.py:474-480, :647-653),
+ *           input GEMM and recurrence together                                     */
+int vt_lstm_layer_fwd_x(const float* x, int In, const float* w_ih, const float* b_ih, const float* w_hh,
+                        const float* b_hh, int B, int S, int hidden, float* out_h, float* out_hprev, float* out_c,
+                        float* gates, void* stream);
+/* Backward with dx = dgates W_ih inside (dx may be null; dgates may be null when
+ * no weight gradient is wanted); bitwise vt_lstm_layer_bwd + vt_linear_bwd_data.  */
+int vt_lstm_layer_bwd_x(const float* dh_out, const float* gates, const float* cst, const float* w_hh,
+                        const float* w_ih, int In, int B, int S, int hidden, float* dgates, float* dx, void* stream);
 
 /* ---------------------------------------------------------- classifier (c4)
  * FHRInceptionTimeClassifier (ref/model/inception_time.py:185-333) on

@@ -170,6 +170,26 @@ def test_lstm(ops, In, B, S):
         assert rel(p.grad, pr.grad) < 2e-5
 
 
+@pytest.mark.parametrize("In,B,S", [(20, 3, 33), (32, 2, 16), (64, 2, 47), (64, 3, 256), (7, 2, 5), (48, 2, 18)])
+def test_lstm_fused_projection_bitwise(ops, In, B, S, monkeypatch):
+    """vt_lstm_layer_{fwd,bwd}_x (input projections inside the recurrence) give
+    the bits of the separate skinny GEMM + recurrence path: the same MFMA chains."""
+    torch.manual_seed(100 + In)
+    ref = torch.nn.LSTM(In, 64, 4, batch_first=True)
+    x = torch.randn(B, S, In)
+    gy = torch.randn(B, S, 64).cuda()
+    outs = []
+    for fused in (0, 1):
+        monkeypatch.setattr(ops, "LSTM_FUSED", fused)
+        params = [_leaf(p) for p in ref.parameters()]
+        xd = _leaf(x)
+        y = ops.lstm(xd, params)
+        (y * gy).sum().backward()
+        outs.append([y.detach(), xd.grad] + [p.grad for p in params])
+    for i, (a, e) in enumerate(zip(*outs)):
+        assert torch.equal(a, e), i
+
+
 def _load_model(S):
     from golden_util import det_fill_
     from vaeteb.model import SeqVaeTeb

@@ -7,6 +7,8 @@ so no transposes are needed between the MLP, conv and LSTM stages (the
 reference transposes to (B, C, L) for torch's conv1d at
 ref/model/vae_teb_model.py:539,545,693,917).
 """
+import os
+
 import torch
 
 from . import _lib
@@ -59,6 +61,9 @@ SIDE_STREAMS = []   # extra streams the model runs work on (see SeqVaeTeb.concur
 GRAD_STREAM = None  # side stream for weight gradients off the data-gradient chain (set by SeqVaeTeb)
 HEAD_GRAD_STREAM = None  # ... for the bf16-MFMA decoder-head weight gradients (set by SeqVaeTeb)
 LSTM_GRAD_STREAM = None  # ... for the LSTM weight gradients (set by SeqVaeTeb)
+# LSTM input projections inside the recurrence kernels (vt_lstm_layer_{fwd,bwd}_x) for
+# input sizes <= 64; 0: separate skinny GEMMs (the same results bit for bit)
+LSTM_FUSED = int(os.environ.get("VAETEB_LSTM_FUSED", "1"))
 
 
 class _ParamGrads:
@@ -538,14 +543,19 @@ class LSTMF(torch.autograd.Function):
         for l in range(nl):
             w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
             In = inp.shape[-1]
-            gin = torch.empty((B, S, 4 * H), device=x.device)
-            call("vt_linear_fwd", ptr(inp), B * S, In, ptr(w_ih), 4 * H, ptr(b_ih), ptr(gin), _st())
             h = torch.empty((B, S, H), device=x.device)
             hp = torch.empty_like(h)
             c = torch.empty_like(h)
-            gates = gin  # overwritten in place by the post-activation gates
-            call("vt_lstm_layer_fwd", ptr(gin), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h), ptr(hp), ptr(c), ptr(gates),
-                 _st())
+            gates = torch.empty((B, S, 4 * H), device=x.device)
+            if LSTM_FUSED and In <= 64:
+                # input projection inside the recurrence kernel (bitwise the unfused result)
+                call("vt_lstm_layer_fwd_x", ptr(inp), In, ptr(w_ih), ptr(b_ih), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h),
+                     ptr(hp), ptr(c), ptr(gates), _st())
+            else:
+                # gin = X W_ih^T + b_ih, overwritten in place by the post-activation gates
+                call("vt_linear_fwd", ptr(inp), B * S, In, ptr(w_ih), 4 * H, ptr(b_ih), ptr(gates), _st())
+                call("vt_lstm_layer_fwd", ptr(gates), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h), ptr(hp), ptr(c),
+                     ptr(gates), _st())
             saved += [inp, hp, c, gates]
             inp = h
         ctx.save_for_backward(*saved)
@@ -568,7 +578,17 @@ class LSTMF(torch.autograd.Function):
             w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
             In = inp.shape[-1]
             dg = torch.empty((B, S, 4 * H), device=gy.device)
-            call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
+            need_dx = l > 0 or ctx.needs_input_grad[0]
+            fused = LSTM_FUSED and In <= 64
+            gin = torch.empty((B, S, In), device=gy.device) if need_dx else None
+            if fused:
+                # dX = dG W_ih inside the recurrence kernel (bitwise the unfused result)
+                call("vt_lstm_layer_bwd_x", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), ptr(w_ih), In, B, S, H, ptr(dg),
+                     ptr(gin) if need_dx else None, _st())
+            else:
+                call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
+                if need_dx:
+                    call("vt_linear_bwd_data", ptr(dg), B * S, 4 * H, ptr(w_ih), In, ptr(gin), 0, _st())
             pw = _ParamGrads([w_ih, w_hh], [True, True])
             # b_ih and b_hh receive the same gradient (the sum of dg over rows), written
             # by one column sum per bias straight into its gradient sink (no device copy:
@@ -597,9 +617,7 @@ class LSTMF(torch.autograd.Function):
                 call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), pb.acc, ptr(ws), ws.numel(), _st())
             gw_ih, gw_hh = pw.result()
             grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, *pb.result()]
-            if l > 0 or ctx.needs_input_grad[0]:
-                gin = torch.empty((B, S, In), device=gy.device)
-                call("vt_linear_bwd_data", ptr(dg), B * S, 4 * H, ptr(w_ih), In, ptr(gin), 0, _st())
+            if need_dx:
                 dh = gin
                 gx = gin
         return (gx, *grads)
