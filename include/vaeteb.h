@@ -400,6 +400,13 @@ int vt_lstm_layer_fwd_x(const float* x, int In, const float* w_ih, const float* 
  * no weight gradient is wanted); bitwise vt_lstm_layer_bwd + vt_linear_bwd_data.  */
 int vt_lstm_layer_bwd_x(const float* dh_out, const float* gates, const float* cst, const float* w_hh,
                         const float* w_ih, int In, int B, int S, int hidden, float* dgates, float* dx, void* stream);
+/* All of a layer's parameter gradients in one pass over dgates [B*S, 4H]:
+ * dw_ih (+)= dgates^T x, dw_hh (+)= dgates^T h_{t-1}, db_ih and db_hh (may be
+ * null) (+)= column sums of dgates.  In + hidden + 1 <= 144; ws: at least
+ * min(256, B*S/256) * 4H * (In + hidden + 1) floats.                              */
+int vt_lstm_layer_bwd_weight(const float* dgates, const float* x, int In, const float* hprev, int B, int S,
+                             int hidden, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate,
+                             float* ws, int64_t ws_floats, void* stream);
 
 /* ---------------------------------------------------------- classifier (c4)
  * FHRInceptionTimeClassifier (ref/model/inception_time.py:185-333) on

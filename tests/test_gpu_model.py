@@ -173,7 +173,9 @@ def test_lstm(ops, In, B, S):
 @pytest.mark.parametrize("In,B,S", [(20, 3, 33), (32, 2, 16), (64, 2, 47), (64, 3, 256), (7, 2, 5), (48, 2, 18)])
 def test_lstm_fused_projection_bitwise(ops, In, B, S, monkeypatch):
     """vt_lstm_layer_{fwd,bwd}_x (input projections inside the recurrence) give
-    the bits of the separate skinny GEMM + recurrence path: the same MFMA chains."""
+    the bits of the separate skinny GEMM + recurrence path: the same MFMA chains.
+    vt_lstm_layer_bwd_weight gives the weight gradients of the two separate
+    vt_linear_bwd_weight calls bit for bit."""
     torch.manual_seed(100 + In)
     ref = torch.nn.LSTM(In, 64, 4, batch_first=True)
     x = torch.randn(B, S, In)
@@ -186,8 +188,14 @@ def test_lstm_fused_projection_bitwise(ops, In, B, S, monkeypatch):
         y = ops.lstm(xd, params)
         (y * gy).sum().backward()
         outs.append([y.detach(), xd.grad] + [p.grad for p in params])
+    # y, dx and the weight gradients: the same MFMA chains (bitwise); the bias
+    # gradients come from vt_lstm_layer_bwd_weight's ones-column instead of a
+    # column-sum kernel (another fixed summation order)
     for i, (a, e) in enumerate(zip(*outs)):
-        assert torch.equal(a, e), i
+        if i >= 2 and (i - 2) % 4 >= 2:
+            assert rel(a, e) < 1e-6, i
+        else:
+            assert torch.equal(a, e), i
 
 
 def _load_model(S):

@@ -201,11 +201,13 @@ static constexpr int DW_ROWS = 64;   // rows per LDS chunk
 static constexpr int DW_THREADS = 512;
 
 // part[blk][n][k'] = sum over the workgroup's rows of dY[r][n] * X1[r][k'], where
-// X1 = [X | 1] (k' = K is the bias column when with_bias).  NTN x NTK tile pairs
-// over 8 waves, PPW pairs per wave.
+// X1 = [X | X2 | 1] (X2 [R, K2] optional, K2 = 0 without; k' = K + K2 is the
+// bias column when with_bias).  NTN x NTK tile pairs over 8 waves, PPW pairs
+// per wave.
 template <int NTN, int NTK>
 __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ dY, const float* __restrict__ X,
-                                                      int64_t R, int N, int K, int with_bias, int64_t rows_per_block,
+                                                      int64_t R, int N, int K, const float* __restrict__ X2, int K2,
+                                                      int with_bias, int64_t rows_per_block,
                                                       float* __restrict__ part) {
     constexpr int HS = 16 * NTN + ((NTN & 1) ? 0 : 16);  // == 16 mod 32
     constexpr int XS2 = 16 * NTK + ((NTK & 1) ? 0 : 16);
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ 
     __shared__ float Hs[DW_ROWS * HS];
     __shared__ float Xs[DW_ROWS * XS2];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
-    const int K1 = K + (with_bias ? 1 : 0);
+    const int KX = K + K2, K1 = KX + (with_bias ? 1 : 0);
     f32x4 acc[PPW];
 #pragma unroll
     for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -251,7 +253,9 @@ __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ 
                     const int i = tid + DW_THREADS * (u0 + u);
                     const int t = i / (16 * NTK), c = i - t * (16 * NTK);
                     float x = 0.f;
-                    if (i < TOT && t < n) x = c < K ? X[(c0 + t) * K + c] : (c == K && with_bias ? 1.f : 0.f);
+                    if (i < TOT && t < n)
+                        x = c < K ? X[(c0 + t) * K + c]
+                                  : (c < KX ? X2[(c0 + t) * K2 + (c - K)] : (c == KX && with_bias ? 1.f : 0.f));
                     v[u] = x;
                 }
 #pragma unroll
@@ -294,10 +298,12 @@ __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ 
     }
 }
 
-// dW[n][k] (+)= sum_b part[b][n][k]; db[n] (+)= sum_b part[b][n][K] (fixed order:
-// 16 outputs x 16 block lanes per workgroup, lane sums then a fixed tree)
-__global__ __launch_bounds__(256) void k_sk_sum(const float* __restrict__ part, int blocks, int N, int K, int K1,
-                                                float* __restrict__ dW, float* __restrict__ db, int accumulate) {
+// dW[n][k] (+)= sum_b part[b][n][k] (k < K), dW2[n][k - K] (k < K + K2), db[n]
+// (and db2[n], when given) (+)= sum_b part[b][n][K + K2] (fixed order: 16 outputs
+// x 16 block lanes per workgroup, lane sums then a fixed tree)
+__global__ __launch_bounds__(256) void k_sk_sum(const float* __restrict__ part, int blocks, int N, int K, int K2,
+                                                int K1, float* __restrict__ dW, float* __restrict__ dW2,
+                                                float* __restrict__ db, float* __restrict__ db2, int accumulate) {
     __shared__ float red[16][17];
     const int o = threadIdx.x & 15, sl = threadIdx.x >> 4;
     const int64_t total = (int64_t)N * K1;
@@ -315,8 +321,9 @@ __global__ __launch_bounds__(256) void k_sk_sum(const float* __restrict__ part, 
     for (int j = 0; j < 4; ++j) s[j] = s[2 * j] + s[2 * j + 1];
     const float t = (s[0] + s[1]) + (s[2] + s[3]);
     const int n = (int)(i / K1), k = (int)(i - (int64_t)n * K1);
-    float* dst = k < K ? dW + (int64_t)n * K + k : db + n;
+    float* dst = k < K ? dW + (int64_t)n * K + k : (k < K + K2 ? dW2 + (int64_t)n * K2 + (k - K) : db + n);
     *dst = accumulate ? *dst + t : t;
+    if (k == K + K2 && db2) db2[n] = accumulate ? db2[n] + t : t;
 }
 
 // ------------------------------------------------------------------- launchers
@@ -359,9 +366,11 @@ int sk_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K,
 
 template <int NTN>
 static void sk_dw_k(int NTK, dim3 grid, hipStream_t st, const float* dY, const float* X, int64_t R, int N, int K,
-                    int wb, int64_t rpb, float* part) {
+                    const float* X2, int K2, int wb, int64_t rpb, float* part) {
 #define VT_DWK(K_)                                                                                                 \
-    case K_: hipLaunchKernelGGL((k_sk_dw<NTN, K_>), grid, dim3(DW_THREADS), 0, st, dY, X, R, N, K, wb, rpb, part); \
+    case K_:                                                                                                       \
+        hipLaunchKernelGGL((k_sk_dw<NTN, K_>), grid, dim3(DW_THREADS), 0, st, dY, X, R, N, K, X2, K2, wb, rpb,     \
+                           part);                                                                                  \
         break;
     switch (NTK) {
         VT_DWK(1) VT_DWK(2) VT_DWK(3) VT_DWK(4) VT_DWK(5) VT_DWK(6) VT_DWK(7) VT_DWK(8) VT_DWK(9)
@@ -376,9 +385,10 @@ int64_t sk_dw_blocks(int64_t R) {
 
 int64_t sk_dw_workspace(int64_t R, int N, int K) { return sk_dw_blocks(R) * N * (K + 1); }
 
-int sk_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
-                         int accumulate, float* ws, int64_t ws_floats, hipStream_t st) {
-    const int K1 = K + (db ? 1 : 0);
+int sk_linear_bwd_weight2(const float* dY, int64_t R, int N, const float* X, int K, const float* X2, int K2,
+                          float* dW, float* dW2, float* db, float* db2, int accumulate, float* ws, int64_t ws_floats,
+                          hipStream_t st) {
+    const int K1 = K + K2 + (db ? 1 : 0);
     const int NTN = (N + 15) / 16, NTK = (K1 + 15) / 16;
     if (NTN > 16 || NTK > 9) return VT_ERR_ARG;
     int64_t blocks = sk_dw_blocks(R);
@@ -388,22 +398,28 @@ int sk_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int 
     rpb = (rpb + 3) / 4 * 4;
     blocks = (R + rpb - 1) / rpb;
     dim3 grid((unsigned)blocks);
+    const int wb = db != nullptr;
     switch (NTN) {
-        case 1: sk_dw_k<1>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        case 2: sk_dw_k<2>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        case 3: sk_dw_k<3>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        case 4: sk_dw_k<4>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        case 5: sk_dw_k<5>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        case 6: sk_dw_k<6>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        case 7: sk_dw_k<7>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        case 8: sk_dw_k<8>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        case 9: sk_dw_k<9>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
-        default: sk_dw_k<16>(NTK, grid, st, dY, X, R, N, K, db != nullptr, rpb, ws); break;
+        case 1: sk_dw_k<1>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 2: sk_dw_k<2>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 3: sk_dw_k<3>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 4: sk_dw_k<4>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 5: sk_dw_k<5>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 6: sk_dw_k<6>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 7: sk_dw_k<7>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 8: sk_dw_k<8>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 9: sk_dw_k<9>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        default: sk_dw_k<16>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
     }
     const int64_t total = (int64_t)N * K1;
-    hipLaunchKernelGGL(k_sk_sum, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, st, ws, (int)blocks, N, K, K1, dW,
-                       db, accumulate);
+    hipLaunchKernelGGL(k_sk_sum, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, st, ws, (int)blocks, N, K, K2, K1,
+                       dW, dW2, db, db2, accumulate);
     return VT_OK;
+}
+
+int sk_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
+                         int accumulate, float* ws, int64_t ws_floats, hipStream_t st) {
+    return sk_linear_bwd_weight2(dY, R, N, X, K, nullptr, 0, dW, nullptr, db, nullptr, accumulate, ws, ws_floats, st);
 }
 
 }  // namespace vt

@@ -589,34 +589,41 @@ class LSTMF(torch.autograd.Function):
                 call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
                 if need_dx:
                     call("vt_linear_bwd_data", ptr(dg), B * S, 4 * H, ptr(w_ih), In, ptr(gin), 0, _st())
-            pw = _ParamGrads([w_ih, w_hh], [True, True])
-            # b_ih and b_hh receive the same gradient (the sum of dg over rows), written
-            # by one column sum per bias straight into its gradient sink (no device copy:
-            # a memcpy node would not survive the native step executor, csrc/stepgraph.cpp)
-            pb = _ParamGrads([b_ih, b_hh], [True, True])
-            side = LSTM_GRAD_STREAM if (pw.direct and LSTM_GRAD_STREAM is not None) else None
-            if side is not None and side != torch.cuda.current_stream():
-                # weight gradients (in-place sinks) off the recurrence chain on a side
-                # stream; the returned bias gradient stays here (same kernels and
-                # summation orders as the serial branch below: bitwise equal)
-                side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(side):
-                    ws_s = WS.get(WS_LINEAR, gy.device, 1)
-                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
-                         ptr(ws_s), ws_s.numel(), _st())
-                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
-                         ptr(ws_s), ws_s.numel(), _st())
-                for t in (dg, inp, hp):
-                    t.record_stream(side)
+            if LSTM_FUSED and In + H + 1 <= 144:
+                # every parameter gradient of the layer in one pass over dg
+                pg = _ParamGrads([w_ih, w_hh, b_ih, b_hh], [True] * 4)
+                call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H, *[ptr(t) for t in pg.out],
+                     pg.acc, ptr(ws), ws.numel(), _st())
+                grads[4 * l: 4 * l + 4] = pg.result()
             else:
-                call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
-                     ptr(ws), ws.numel(), _st())
-                call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
-                     ptr(ws), ws.numel(), _st())
-            for gb in pb.out:
-                call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), pb.acc, ptr(ws), ws.numel(), _st())
-            gw_ih, gw_hh = pw.result()
-            grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, *pb.result()]
+                pw = _ParamGrads([w_ih, w_hh], [True, True])
+                # b_ih and b_hh receive the same gradient (the sum of dg over rows), written
+                # by one column sum per bias straight into its gradient sink (no device copy:
+                # a memcpy node would not survive the native step executor, csrc/stepgraph.cpp)
+                pb = _ParamGrads([b_ih, b_hh], [True, True])
+                side = LSTM_GRAD_STREAM if (pw.direct and LSTM_GRAD_STREAM is not None) else None
+                if side is not None and side != torch.cuda.current_stream():
+                    # weight gradients (in-place sinks) off the recurrence chain on a side
+                    # stream; the returned bias gradient stays here (same kernels and
+                    # summation orders as the serial branch below: bitwise equal)
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):
+                        ws_s = WS.get(WS_LINEAR, gy.device, 1)
+                        call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
+                             ptr(ws_s), ws_s.numel(), _st())
+                        call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
+                             ptr(ws_s), ws_s.numel(), _st())
+                    for t in (dg, inp, hp):
+                        t.record_stream(side)
+                else:
+                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
+                         ptr(ws), ws.numel(), _st())
+                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
+                         ptr(ws), ws.numel(), _st())
+                for gb in pb.out:
+                    call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), pb.acc, ptr(ws), ws.numel(), _st())
+                gw_ih, gw_hh = pw.result()
+                grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, *pb.result()]
             if need_dx:
                 dh = gin
                 gx = gin
