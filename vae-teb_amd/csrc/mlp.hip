@@ -197,13 +197,16 @@ __global__ __launch_bounds__(256) void k_sk_gemm(const float* __restrict__ A, in
 }
 
 // ---------------------------------------------------------------- weight grad
-static constexpr int DW_ROWS = 64;   // rows per LDS chunk
+static constexpr int DW_ROWS = 32;   // rows per LDS chunk
 static constexpr int DW_THREADS = 512;
 
 // part[blk][n][k'] = sum over the workgroup's rows of dY[r][n] * X1[r][k'], where
 // X1 = [X | X2 | 1] (X2 [R, K2] optional, K2 = 0 without; k' = K + K2 is the
 // bias column when with_bias).  NTN x NTK tile pairs over 8 waves, PPW pairs
-// per wave.
+// per wave: when PPW is a multiple of NTK a wave owns PPW / NTK whole tile rows
+// (its A fragments are read once per k-step for all NTK pairs of a row), else
+// pairs are dealt round-robin.  The next 64-row chunk is loaded into registers
+// while the MFMAs consume the current one from LDS.
 template <int NTN, int NTK>
 __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ dY, const float* __restrict__ X,
                                                       int64_t R, int N, int K, const float* __restrict__ X2, int K2,
@@ -212,71 +215,77 @@ __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ 
     constexpr int HS = 16 * NTN + ((NTN & 1) ? 0 : 16);  // == 16 mod 32
     constexpr int XS2 = 16 * NTK + ((NTK & 1) ? 0 : 16);
     constexpr int PAIRS = NTN * NTK, PPW = (PAIRS + 7) / 8;
+    constexpr bool ROWS_OWNED = PAIRS % 8 == 0 && PPW % NTK == 0;
+    constexpr int HT = DW_ROWS * 16 * NTN, UH = (HT + DW_THREADS - 1) / DW_THREADS;
+    constexpr int XT = DW_ROWS * 16 * NTK, UX = (XT + DW_THREADS - 1) / DW_THREADS;
     __shared__ float Hs[DW_ROWS * HS];
     __shared__ float Xs[DW_ROWS * XS2];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
     const int KX = K + K2, K1 = KX + (with_bias ? 1 : 0);
+    auto pair_tn = [&](int j) { return ROWS_OWNED ? wv * (PPW / NTK) + j / NTK : (wv + 8 * j) / NTK; };
+    auto pair_tk = [&](int j) { return ROWS_OWNED ? j % NTK : (wv + 8 * j) % NTK; };
     f32x4 acc[PPW];
 #pragma unroll
     for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int64_t rb = (int64_t)blockIdx.x * rows_per_block;
     const int64_t re = rb + rows_per_block < R ? rb + rows_per_block : R;
+    float vh[UH], vx[UX];
+    auto load = [&](int64_t c0) {  // dY rows [t][n] and X1 rows [t][k'] of the chunk at c0
+        const int n = re - c0 < DW_ROWS ? (int)(re - c0) : DW_ROWS;
+#pragma unroll
+        for (int u = 0; u < UH; ++u) {
+            const int i = tid + DW_THREADS * u;
+            const int t = i / (16 * NTN), c = i - t * (16 * NTN);
+            vh[u] = (i < HT && t < n && c < N) ? dY[(c0 + t) * N + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < UX; ++u) {
+            const int i = tid + DW_THREADS * u;
+            const int t = i / (16 * NTK), c = i - t * (16 * NTK);
+            float x = 0.f;
+            if (i < XT && t < n)
+                x = c < K ? X[(c0 + t) * K + c]
+                          : (c < KX ? X2[(c0 + t) * K2 + (c - K)] : (c == KX && with_bias ? 1.f : 0.f));
+            vx[u] = x;
+        }
+    };
+    if (rb < re) load(rb);
     for (int64_t c0 = rb; c0 < re; c0 += DW_ROWS) {
         const int n = re - c0 < DW_ROWS ? (int)(re - c0) : DW_ROWS;
-        // stage dY rows [t][n] and X rows [t][k] (+ ones column), 8 loads in flight per thread
-        {
-            constexpr int TOT = DW_ROWS * 16 * NTN, U = (TOT + DW_THREADS - 1) / DW_THREADS;
-#pragma unroll 1
-            for (int u0 = 0; u0 < U; u0 += 8) {
-                float v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int i = tid + DW_THREADS * (u0 + u);
-                    const int t = i / (16 * NTN), c = i - t * (16 * NTN);
-                    v[u] = (i < TOT && t < n && c < N) ? dY[(c0 + t) * N + c] : 0.f;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int i = tid + DW_THREADS * (u0 + u);
-                    const int t = i / (16 * NTN), c = i - t * (16 * NTN);
-                    if (i < TOT) Hs[t * HS + c] = v[u];
-                }
-            }
+        for (int u = 0; u < UH; ++u) {
+            const int i = tid + DW_THREADS * u;
+            const int t = i / (16 * NTN), c = i - t * (16 * NTN);
+            if (i < HT) Hs[t * HS + c] = vh[u];
         }
-        {
-            constexpr int TOT = DW_ROWS * 16 * NTK, U = (TOT + DW_THREADS - 1) / DW_THREADS;
-#pragma unroll 1
-            for (int u0 = 0; u0 < U; u0 += 8) {
-                float v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int i = tid + DW_THREADS * (u0 + u);
-                    const int t = i / (16 * NTK), c = i - t * (16 * NTK);
-                    float x = 0.f;
-                    if (i < TOT && t < n)
-                        x = c < K ? X[(c0 + t) * K + c]
-                                  : (c < KX ? X2[(c0 + t) * K2 + (c - K)] : (c == KX && with_bias ? 1.f : 0.f));
-                    v[u] = x;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int i = tid + DW_THREADS * (u0 + u);
-                    const int t = i / (16 * NTK), c = i - t * (16 * NTK);
-                    if (i < TOT) Xs[t * XS2 + c] = v[u];
-                }
-            }
+        for (int u = 0; u < UX; ++u) {
+            const int i = tid + DW_THREADS * u;
+            const int t = i / (16 * NTK), c = i - t * (16 * NTK);
+            if (i < XT) Xs[t * XS2 + c] = vx[u];
         }
         __syncthreads();
+        if (c0 + DW_ROWS < re) load(c0 + DW_ROWS);  // in flight during this chunk's MFMAs
         const int groups = (n + 3) >> 2;
         for (int q = 0; q < groups; ++q) {
             const float* hp = Hs + (4 * q + lc) * HS + lr;
             const float* xp = Xs + (4 * q + lc) * XS2 + lr;
+            if (ROWS_OWNED) {
+                float xa[NTK];
 #pragma unroll
-            for (int j = 0; j < PPW; ++j) {
-                const int p = wv + 8 * j;
-                if (PAIRS % 8 != 0 && p >= PAIRS) continue;
-                const int tn = p / NTK, tk = p - tn * NTK;
-                acc[j] = mfma4(hp[16 * tn], xp[16 * tk], acc[j]);
+                for (int tk = 0; tk < NTK; ++tk) xa[tk] = xp[16 * tk];
+#pragma unroll
+                for (int jr = 0; jr < PPW / NTK; ++jr) {
+                    const float ha = hp[16 * (wv * (PPW / NTK) + jr)];
+#pragma unroll
+                    for (int tk = 0; tk < NTK; ++tk) acc[jr * NTK + tk] = mfma4(ha, xa[tk], acc[jr * NTK + tk]);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < PPW; ++j) {
+                    if (PAIRS % 8 != 0 && wv + 8 * j >= PAIRS) continue;
+                    acc[j] = mfma4(hp[16 * pair_tn(j)], xp[16 * pair_tk(j)], acc[j]);
+                }
             }
         }
         __syncthreads();
@@ -285,9 +294,8 @@ __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ 
     float* pb = part + (int64_t)blockIdx.x * N * K1;
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
-        const int p = wv + 8 * j;
-        if (p >= PAIRS) continue;
-        const int tn = p / NTK, tk = p - tn * NTK;
+        if (!ROWS_OWNED && wv + 8 * j >= PAIRS) continue;
+        const int tn = pair_tn(j), tk = pair_tk(j);
         const int k = 16 * tk + lr;
         if (k >= K1) continue;
 #pragma unroll
@@ -299,27 +307,33 @@ __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ 
 }
 
 // dW[n][k] (+)= sum_b part[b][n][k] (k < K), dW2[n][k - K] (k < K + K2), db[n]
-// (and db2[n], when given) (+)= sum_b part[b][n][K + K2] (fixed order: 16 outputs
-// x 16 block lanes per workgroup, lane sums then a fixed tree)
+// (and db2[n], when given) (+)= sum_b part[b][n][K + K2].  Fixed order: 64
+// outputs per workgroup, wave w sums blocks w, w + 4, w + 8, ... in sequence
+// (coalesced 256-byte rows, 16 loads in flight), then (w0 + w1) + (w2 + w3).
 __global__ __launch_bounds__(256) void k_sk_sum(const float* __restrict__ part, int blocks, int N, int K, int K2,
                                                 int K1, float* __restrict__ dW, float* __restrict__ dW2,
                                                 float* __restrict__ db, float* __restrict__ db2, int accumulate) {
-    __shared__ float red[16][17];
-    const int o = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t total = (int64_t)N * K1;
-    const int64_t i = (int64_t)blockIdx.x * 16 + o;
+    const int64_t i = (int64_t)blockIdx.x * 64 + lane;
     float a = 0.f;
-    if (i < total)
-        for (int b = sl; b < blocks; b += 16) a += part[(int64_t)b * total + i];
-    red[sl][o] = a;
+    if (i < total) {
+        const float* p = part + i;
+        int b = w;
+        for (; b + 60 < blocks; b += 64) {
+            float v[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) v[m] = p[(int64_t)(b + 4 * m) * total];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) a += v[m];
+        }
+        for (; b < blocks; b += 4) a += p[(int64_t)b * total];
+    }
+    red[w][lane] = a;
     __syncthreads();
-    if (sl != 0 || i >= total) return;
-    float s[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] = red[2 * j][o] + red[2 * j + 1][o];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] = s[2 * j] + s[2 * j + 1];
-    const float t = (s[0] + s[1]) + (s[2] + s[3]);
+    if (w != 0 || i >= total) return;
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
     const int n = (int)(i / K1), k = (int)(i - (int64_t)n * K1);
     float* dst = k < K ? dW + (int64_t)n * K + k : (k < K + K2 ? dW2 + (int64_t)n * K2 + (k - K) : db + n);
     *dst = accumulate ? *dst + t : t;
@@ -412,7 +426,7 @@ int sk_linear_bwd_weight2(const float* dY, int64_t R, int N, const float* X, int
         default: sk_dw_k<16>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
     }
     const int64_t total = (int64_t)N * K1;
-    hipLaunchKernelGGL(k_sk_sum, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, st, ws, (int)blocks, N, K, K2, K1,
+    hipLaunchKernelGGL(k_sk_sum, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, ws, (int)blocks, N, K, K2, K1,
                        dW, dW2, db, db2, accumulate);
     return VT_OK;
 }
