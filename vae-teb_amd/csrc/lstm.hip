@@ -43,6 +43,27 @@ __device__ __forceinline__ float ftanh(float x) {
     return ax < 0.3f ? small : big;
 }
 
+// The cell arithmetic of one step, shared by the plain and the fused kernels so
+// both give the same bits wherever they are inlined: contraction is spelled out
+// (fmaf) and otherwise off, so the compiler's choice cannot depend on context.
+__device__ __forceinline__ float cell_fwd_c(float c, float gi, float gf, float gg) {
+#pragma clang fp contract(off)
+    return fmaf(gf, c, gi * gg);
+}
+__device__ __forceinline__ void cell_bwd(float dh, float gi, float gf, float gg, float go, float c, float cp, float& dc,
+                                         float& v0, float& v1, float& v2, float& v3) {
+#pragma clang fp contract(off)
+    const float tc = ftanh(c);
+    const float d_o = dh * tc;
+    dc = fmaf(dh * go, fmaf(-tc, tc, 1.f), dc);
+    const float di = dc * gg, dgg = dc * gi, df = dc * cp;
+    dc = dc * gf;
+    v0 = di * gi * (1.f - gi);
+    v1 = df * gf * (1.f - gf);
+    v2 = dgg * fmaf(-gg, gg, 1.f);
+    v3 = d_o * go * (1.f - go);
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic,
 // not for its global stores / prefetch loads (__syncthreads() would drain
 // vmcnt every time step and put an HBM round trip on the recurrence's
@@ -143,7 +164,7 @@ __global__ __launch_bounds__(G4) void k_lstm_fwd(const float* __restrict__ gin, 
             const float pg = quad_sum(a[2].x + a[2].y), po = quad_sum(a[3].x + a[3].y);
             const float gi = sigm(pi), gf = sigm(pf), gg = ftanh(pg), go = sigm(po);
             og[i * G4 + row] = q == 0 ? gi : (q == 1 ? gf : (q == 2 ? gg : go));
-            c = gf * c + gi * gg;
+            c = cell_fwd_c(c, gi, gf, gg);
             if (q == 0) {
                 const float hn = go * ftanh(c);
                 ohp[i * H + u] = hprev;
@@ -268,13 +289,8 @@ __global__ __launch_bounds__(G4) void k_lstm_bwd(const float* __restrict__ dh_ou
             float* dgb = dg[t & 1];
             if (owner) {
                 const float dh = dho + dhr;
-                const float tc = ftanh(c);
-                const float d_o = dh * tc;
-                dc = dc + dh * go * (1.f - tc * tc);
-                const float di = dc * gg, dgg = dc * gi, df = dc * cp;
-                dc = dc * gf;
-                const float v0 = di * gi * (1.f - gi), v1 = df * gf * (1.f - gf);
-                const float v2 = dgg * (1.f - gg * gg), v3 = d_o * go * (1.f - go);
+                float v0, v1, v2, v3;
+                cell_bwd(dh, gi, gf, gg, go, c, cp, dc, v0, v1, v2, v3);
                 dgb[seg_pos(u)] = v0;
                 dgb[seg_pos(H + u)] = v1;
                 dgb[seg_pos(2 * H + u)] = v2;
@@ -430,11 +446,13 @@ __global__ __launch_bounds__(G4) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const float* xn = xs[cb];
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // the next chunk's projection, a few MFMAs behind each step's barrier (measured:
+        // as fast as, or faster than, interleaving them into the step's FMA chain or
+        // issuing all of them at the chunk's end)
 #pragma unroll
         for (int i = 0; i < TS; ++i) {
             if (i >= n) continue;  // block-uniform
-            const float* hc = hbuf[i & 1];
-            const float* hq = hc + 20 * q;
+            const float* hq = hbuf[i & 1] + 20 * q;
             const float xv = og[i * G4 + row] + bias;
             f2 a[4];
 #pragma unroll
@@ -452,7 +470,7 @@ __global__ __launch_bounds__(G4) __attribute__((amdgpu_waves_per_eu(2))) void k_
             const float pg = quad_sum(a[2].x + a[2].y), po = quad_sum(a[3].x + a[3].y);
             const float gi = sigm(pi), gf = sigm(pf), gg = ftanh(pg), go = sigm(po);
             og[i * G4 + row] = q == 0 ? gi : (q == 1 ? gf : (q == 2 ? gg : go));
-            c = gf * c + gi * gg;
+            c = cell_fwd_c(c, gi, gf, gg);
             if (q == 0) {
                 const float hn = go * ftanh(c);
                 ohp[i * H + u] = hprev;
@@ -585,62 +603,65 @@ __global__ __launch_bounds__(G4) __attribute__((amdgpu_waves_per_eu(2))) void k_
             cp = lo + i > 0 ? sc[i * H + u] : 0.f;
             dho = sdh[i * H + u];
         };
-        if (owner) load_in(TB2 - 1);
+        load_in(TB2 - 1);
         float* ob = odg[cbuf];
         const float* op = odg[cbuf ^ 1];
-        const bool mf = prev && dxw;
         acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        float pa[4];  // A operands of the previous chunk's dX tile, one step ahead
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pa[k] = op[lr * ODS + 4 * k + lc];
+        // Straight-line steps (no per-step branches: the scheduler slots the dX MFMAs
+        // into the recurrence's latency gaps).  Steps with t < 0 (last chunk) run on
+        // finite clamped inputs after t = 0 and are not stored; in the first chunk the
+        // MFMAs consume stale LDS and their tile is not stored either.
 #pragma unroll
         for (int i = TB2 - 1; i >= 0; --i) {
             const int t = lo + i;
-            if (t >= 0) {  // block-uniform
-                float* dgb = dg[t & 1];
-                if (owner) {
-                    const float dh = dho + dhr;
-                    const float tc = ftanh(c);
-                    const float d_o = dh * tc;
-                    dc = dc + dh * go * (1.f - tc * tc);
-                    const float di = dc * gg, dgg = dc * gi, df = dc * cp;
-                    dc = dc * gf;
-                    const float v0 = di * gi * (1.f - gi), v1 = df * gf * (1.f - gf);
-                    const float v2 = dgg * (1.f - gg * gg), v3 = d_o * go * (1.f - go);
-                    dgb[seg_pos(u)] = v0;
-                    dgb[seg_pos(H + u)] = v1;
-                    dgb[seg_pos(2 * H + u)] = v2;
-                    dgb[seg_pos(3 * H + u)] = v3;
-                    float* o = ob + i * ODS;
-                    o[u] = v0; o[H + u] = v1; o[2 * H + u] = v2; o[3 * H + u] = v3;
-                }
-                lds_barrier();
-                const float* dq = dgb + 20 * rg;
-                f2 a[4] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float4 d = *reinterpret_cast<const float4*>(&dq[4 * r]);
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        a[m] = __builtin_elementwise_fma(wc[m][2 * r], f2{d.x, d.y}, a[m]);
-                        a[m] = __builtin_elementwise_fma(wc[m][2 * r + 1], f2{d.z, d.w}, a[m]);
-                    }
-                }
-                if (owner && i > 0) load_in(i - 1);
-                const float s0 = row16_sum(a[0].x + a[0].y), s1 = row16_sum(a[1].x + a[1].y);
-                const float s2 = row16_sum(a[2].x + a[2].y), s3 = row16_sum(a[3].x + a[3].y);
-                const int m = rg & 3;
-                dhr = m == 0 ? s0 : (m == 1 ? s1 : (m == 2 ? s2 : s3));
+            float* dgb = dg[t & 1];
+            const float dh = dho + dhr;
+            float v0, v1, v2, v3;
+            cell_bwd(dh, gi, gf, gg, go, c, cp, dc, v0, v1, v2, v3);
+            if (owner) {
+                dgb[seg_pos(u)] = v0;
+                dgb[seg_pos(H + u)] = v1;
+                dgb[seg_pos(2 * H + u)] = v2;
+                dgb[seg_pos(3 * H + u)] = v3;
+                float* o = ob + i * ODS;
+                o[u] = v0; o[H + u] = v1; o[2 * H + u] = v2; o[3 * H + u] = v3;
             }
-            if (mf) {  // the previous chunk's dX tile, k-steps 4 p .. 4 p + 3
-                const int p = TB2 - 1 - i;
+            const int p = TB2 - 1 - i;  // the previous chunk's dX tile, k-steps 4 p .. 4 p + 3
 #pragma unroll
-                for (int k = 4 * p; k < 4 * p + 4; ++k) acc = mfma4(op[lr * ODS + 4 * k + lc], wx[k], acc);
+            for (int k = 0; k < 4; ++k) acc = mfma4(pa[k], wx[4 * p + k], acc);
+            lds_barrier();
+            const float* dq = dgb + 20 * rg;
+            float4 dv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dv[r] = *reinterpret_cast<const float4*>(&dq[4 * r]);
+            if (p + 1 < TB2) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) pa[k] = op[lr * ODS + 4 * (4 * (p + 1) + k) + lc];
             }
+            if (i > 0) load_in(i - 1);
+            f2 a[4] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    a[m] = __builtin_elementwise_fma(wc[m][2 * r], f2{dv[r].x, dv[r].y}, a[m]);
+                    a[m] = __builtin_elementwise_fma(wc[m][2 * r + 1], f2{dv[r].z, dv[r].w}, a[m]);
+                }
+            }
+            const float s0 = row16_sum(a[0].x + a[0].y), s1 = row16_sum(a[1].x + a[1].y);
+            const float s2 = row16_sum(a[2].x + a[2].y), s3 = row16_sum(a[3].x + a[3].y);
+            const int m = rg & 3;
+            dhr = m == 0 ? s0 : (m == 1 ? s1 : (m == 2 ? s2 : s3));
         }
         if (dgo) {
             const int t_first = lo < 0 ? 0 : lo;
             for (int idx = (t_first - lo) * G4 + j; idx < TB2 * G4; idx += G4)
                 dgo[(int64_t)lo * G4 + idx] = ob[(idx >> 8) * ODS + (idx & (G4 - 1))];
         }
-        if (mf) dx_write(plo);
+        if (prev && dxw) dx_write(plo);
         lds_barrier();
         prev = true;
         plo = lo;
