@@ -277,48 +277,54 @@ __global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ 
 // back onto the real input (B, L_in, Cin): sum over the padded positions that
 // read each upsampled sample, then through the linear-interpolation weights.
 // One sample per grid row (blockIdx.y), 32-bit position / channel arithmetic
-// within it (host check: Lp * Cin < 2^31).
-__global__ void k_conv_fold(const float* __restrict__ gpad, ConvGeom g, float* __restrict__ dx, int accumulate) {
+// within it (host check: Lp * Cin < 2^31); (s, ci) through a float reciprocal
+// while positions are exact in fp32 (rcin = 0: integer division).
+template <bool UP>
+__global__ void k_conv_fold(const float* __restrict__ gpad, ConvGeom g, float rcin, float* __restrict__ dx,
+                            int accumulate) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;  // s * Cin + ci within sample b
     if (i >= g.L_in * g.Cin) return;
     const int b = blockIdx.y;
-    const int s = i / g.Cin, ci = i - s * g.Cin;
     const int Lp = g.L_out + g.K - 1;  // padded length the bwd-data GEMM produced
-    const float* gb = gpad + (int64_t)b * Lp * g.Cin + ci;
-    // gradient of upsampled position t: sum of padded positions tp with map(tp) == t
-    auto gup = [&](int t) -> float {
-        float v = gb[(t + g.pad) * g.Cin];  // the direct copy
-        if (g.mode == 0) return v;
-        if (g.L_up <= g.pad) {  // replicate: edges collect the pads
-            if (t == 0)
-                for (int tp = 0; tp < g.pad; ++tp) v += gb[tp * g.Cin];
-            if (t == g.L_up - 1)
-                for (int tp = g.pad + g.L_up; tp < Lp; ++tp) v += gb[tp * g.Cin];
-            return v;
-        }
-        if (t >= 1 && t <= g.pad) v += gb[(g.pad - t) * g.Cin];                        // left mirror
-        const int tr = g.pad + 2 * (g.L_up - 1) - t;                                   // right mirror
-        if (t <= g.L_up - 2 && tr < Lp && tr >= g.pad + g.L_up) v += gb[tr * g.Cin];
-        return v;
-    };
+    const float* gb0 = gpad + (int64_t)b * Lp * g.Cin;
     float out;
-    if (!g.up) {
-        out = gup(s);
+    if (!UP && g.mode == 0) {
+        out = gb0[g.pad * g.Cin + i];  // causal: padded rows [pad, pad + L) are the input rows, a flat copy
     } else {
-        // upsampled t reads input i0 = floor(max((t+.5)/2-.5, 0)) with 1-lambda, i1 = min(i0+1, L-1) with lambda
-        out = 0.f;
-        const int tlo = 2 * s - 2 < 0 ? 0 : 2 * s - 2;
-        const int thi = 2 * s + 2 < g.L_up - 1 ? 2 * s + 2 : g.L_up - 1;
-        for (int t = tlo; t <= thi; ++t) {
-            float src = (t + 0.5f) * 0.5f - 0.5f;
-            src = src < 0.f ? 0.f : src;
-            const int i0 = (int)src;
-            const int i1 = i0 + 1 < g.L_in ? i0 + 1 : g.L_in - 1;
-            const float l1 = src - (float)i0;
-            float w = 0.f;
-            if (i0 == s) w += 1.f - l1;
-            if (i1 == s) w += l1;
-            if (w != 0.f) out += w * gup(t);
+        // (s, ci) = divmod(i, Cin) through the reciprocal, corrected by one either way
+        int s = rcin != 0.f ? (int)((float)i * rcin) : i / g.Cin;
+        if (s * g.Cin > i) --s;
+        else if ((s + 1) * g.Cin <= i) ++s;
+        const int ci = i - s * g.Cin;
+        const float* gb = gb0 + ci;
+        // gradient of upsampled position t: sum of padded positions tp with map(tp) == t
+        auto gup = [&](int t) -> float {
+            float v = gb[(t + g.pad) * g.Cin];  // the direct copy
+            if (g.mode == 0) return v;
+            if (g.L_up <= g.pad) {  // replicate: edges collect the pads
+                if (t == 0)
+                    for (int tp = 0; tp < g.pad; ++tp) v += gb[tp * g.Cin];
+                if (t == g.L_up - 1)
+                    for (int tp = g.pad + g.L_up; tp < Lp; ++tp) v += gb[tp * g.Cin];
+                return v;
+            }
+            if (t >= 1 && t <= g.pad) v += gb[(g.pad - t) * g.Cin];                        // left mirror
+            const int tr = g.pad + 2 * (g.L_up - 1) - t;                                   // right mirror
+            if (t <= g.L_up - 2 && tr < Lp && tr >= g.pad + g.L_up) v += gb[tr * g.Cin];
+            return v;
+        };
+        if (!UP) {
+            out = gup(s);
+        } else {
+            // adjoint of the x2 linear upsample (align_corners=False): upsampled t reads
+            // i0 = floor(max((t + .5) / 2 - .5, 0)) with 1 - l and i1 = min(i0 + 1, L - 1) with l, so input s
+            // collects t = 2s - 1 (1/4), 2s (3/4; 1 at s = 0), 2s + 1 (3/4; 1 at s = L - 1), 2s + 2 (1/4),
+            // summed in increasing t
+            out = 0.f;
+            if (s >= 1) out = fmaf(0.25f, gup(2 * s - 1), out);
+            out = fmaf(s == 0 ? 1.f : 0.75f, gup(2 * s), out);
+            out = fmaf(s == g.L_in - 1 ? 1.f : 0.75f, gup(2 * s + 1), out);
+            if (2 * s + 2 <= g.L_up - 1) out = fmaf(0.25f, gup(2 * s + 2), out);
         }
     }
     float* o = dx + (int64_t)b * g.L_in * g.Cin + i;
@@ -327,8 +333,12 @@ __global__ void k_conv_fold(const float* __restrict__ gpad, ConvGeom g, float* _
 
 static int fold_launch(const float* gpad, const ConvGeom& g, float* dX, int accumulate, hipStream_t st) {
     VT_CHECK_ARG((int64_t)(g.L_out + g.K - 1) * g.Cin < (1ll << 31) && g.B <= 65535, "conv fold: shape");
-    hipLaunchKernelGGL(k_conv_fold, dim3((unsigned)((g.L_in * g.Cin + 255) / 256), (unsigned)g.B), dim3(256), 0, st,
-                       gpad, g, dX, accumulate);
+    const dim3 grid((unsigned)((g.L_in * g.Cin + 255) / 256), (unsigned)g.B);
+    const float rcin = (int64_t)g.L_in * g.Cin < (1 << 24) ? 1.f / (float)g.Cin : 0.f;
+    if (g.up)
+        hipLaunchKernelGGL(k_conv_fold<true>, grid, dim3(256), 0, st, gpad, g, rcin, dX, accumulate);
+    else
+        hipLaunchKernelGGL(k_conv_fold<false>, grid, dim3(256), 0, st, gpad, g, rcin, dX, accumulate);
     return VT_OK;
 }
 
