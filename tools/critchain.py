@@ -41,3 +41,9 @@ end = K[path[-1]][1]
 print(f"critical chain {len(path)} kernels, {busy / 1e3:.1f} us busy of {(end - K[path[0]][0]) / 1e3:.1f} us")
 for n, v in agg.most_common(30):
     print(f"{v:8.1f} us  {n[:80]}")
+if len(sys.argv) > 2 and sys.argv[2] == "timeline":
+    # the chain in order: runs of kernels with their span (us from the step start)
+    print("\ntimeline (start us, duration us, kernel)")
+    for i in path:
+        s, e, q, n = K[i]
+        print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  q{q} {n[:70]}")

@@ -934,30 +934,32 @@ struct SumArgs {
 };
 
 __global__ __launch_bounds__(256) void k_mlpb_sum(SumArgs sa, const float* __restrict__ part, int nblk, int accumulate) {
-    __shared__ float red[16][17];
+    // 64 outputs per workgroup; wave w sums partials w, w + 4, w + 8, ... in sequence
+    // (coalesced 256-byte rows, 16 loads in flight), then (w0 + w1) + (w2 + w3)
+    __shared__ float red[4][64];
     const SumSeg& sg = sa.s[blockIdx.y];
-    const int o = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int E = sg.E, P = sa.P;
-    if ((int64_t)blockIdx.x * 16 >= E) return;
+    if ((int64_t)blockIdx.x * 64 >= E) return;
     const float* src = part + sg.src;
-    const int i = blockIdx.x * 16 + o;
-    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    const int i = blockIdx.x * 64 + lane;
+    float a = 0.f;
     if (i < E) {
-        int b = sl;
-        for (; b + 48 < nblk; b += 64)
+        const float* q = src + i;
+        int b = w;
+        for (; b + 60 < nblk; b += 64) {
+            float v[16];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) a4[u] += src[(int64_t)(b + 16 * u) * P + i];
-        for (int u = 0; b < nblk; b += 16, ++u) a4[u & 3] += src[(int64_t)b * P + i];
+            for (int m = 0; m < 16; ++m) v[m] = q[(int64_t)(b + 4 * m) * P];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) a += v[m];
+        }
+        for (; b < nblk; b += 4) a += q[(int64_t)b * P];
     }
-    red[sl][o] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    red[w][lane] = a;
     __syncthreads();
-    if (sl != 0 || i >= E) return;
-    float t8[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t8[j] = red[2 * j][o] + red[2 * j + 1][o];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) t8[j] = t8[2 * j] + t8[2 * j + 1];
-    const float t = (t8[0] + t8[1]) + (t8[2] + t8[3]);
+    if (w != 0 || i >= E) return;
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
     float* dst;
     if (sg.K1) {
         const int n = i / sg.K1, k = i - n * sg.K1;
@@ -1309,7 +1311,7 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
     VT_MBB(2, 2) VT_MBB(4, 2) VT_MBB(2, 1) VT_MBB(4, 1) VT_MBB(6, 1) VT_MBB(9, 1)
 #undef VT_MBB
     if (sa.nseg) {
-        const dim3 gs((unsigned)((emax + 15) / 16), (unsigned)sa.nseg);
+        const dim3 gs((unsigned)((emax + 63) / 64), (unsigned)sa.nseg);
         hipLaunchKernelGGL(k_mlpb_sum, gs, dim3(256), 0, st, sa, ws, (int)p.nblk, accumulate);
     }
     VT_LAUNCH_CHECK("vt_resmlp_bf16_bwd");

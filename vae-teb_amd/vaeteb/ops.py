@@ -592,8 +592,19 @@ class LSTMF(torch.autograd.Function):
             if LSTM_FUSED and In + H + 1 <= 144:
                 # every parameter gradient of the layer in one pass over dg
                 pg = _ParamGrads([w_ih, w_hh, b_ih, b_hh], [True] * 4)
-                call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H, *[ptr(t) for t in pg.out],
-                     pg.acc, ptr(ws), ws.numel(), _st())
+                side = LSTM_GRAD_STREAM if (pg.direct and LSTM_GRAD_STREAM is not None) else None
+                if side is not None and side != torch.cuda.current_stream():
+                    # off the layer-to-layer chain (in-place sinks; same kernels, same bits)
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):
+                        ws_s = WS.get(WS_LINEAR, gy.device, 1)
+                        call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                             *[ptr(t) for t in pg.out], pg.acc, ptr(ws_s), ws_s.numel(), _st())
+                    for t in (dg, inp, hp):
+                        t.record_stream(side)
+                else:
+                    call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                         *[ptr(t) for t in pg.out], pg.acc, ptr(ws), ws.numel(), _st())
                 grads[4 * l: 4 * l + 4] = pg.result()
             else:
                 pw = _ParamGrads([w_ih, w_hh], [True, True])
