@@ -58,6 +58,31 @@ __device__ __forceinline__ bool src_row(const Geo& g, int tp, int& i0, int& i1, 
     return true;
 }
 
+// NC consecutive channels cb .. cb + NC - 1 of padded position tp (src_val for each,
+// 0 where !ok or past Cin) with every load issued before any use: the row mapping
+// is computed once, addresses are clamped into the sample and the values masked
+// afterwards, so a staging loop keeps all its loads in flight instead of waiting
+// on each element.
+template <int NC>
+__device__ __forceinline__ void src_vec(const float* __restrict__ xb, const Geo& g, int tp, int cb, bool ok,
+                                        float (&v)[NC]) {
+    int i0 = 0, i1 = 0;
+    float l1 = 0.f;
+    const bool in = ok && src_row(g, tp, i0, i1, l1);
+    const float* p0 = xb + (int64_t)(in ? i0 : 0) * g.Cin;
+    const float* p1 = xb + (int64_t)(in ? i1 : 0) * g.Cin;
+    float a[NC], b[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
+        a[j] = p0[c];
+        b[j] = g.up ? p1[c] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+        v[j] = (in && cb + j < g.Cin) ? (g.up ? (1.f - l1) * a[j] + l1 * b[j] : a[j]) : 0.f;
+}
+
 static inline Geo geo(int B, int L_in, int Cin, int Cout, int K, int mode, int up) {
     Geo g;
     g.B = B; g.L_in = L_in; g.Cin = Cin; g.Cout = Cout; g.K = K; g.mode = mode; g.up = up;

@@ -77,39 +77,62 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int c0 = 0; c0 < g.Cin; c0 += CB) {
-        // window: WIN rows x 4 octets of 8 channels, fp32 -> bf16
-        for (int i = tid; i < WIN * 4; i += 256) {
+        // window: WIN rows x 4 octets of 8 channels, fp32 -> bf16, and the chunk's taps
+        // (K x TC rows x 4 octets, 16 B each from the shadow): every load of the thread
+        // issued before the first store (clamped addresses, masked values)
+        constexpr int NI = (WIN * 4 + 255) / 256, NWI = (K * TC * 4 + 255) / 256;
+        float v[NI][8];
+#pragma unroll
+        for (int it = 0; it < NI; ++it) {
+            const int i = tid + 256 * it;
             const int row = i >> 2, oct = i & 3;
             const int tp = t0 + row, cb = c0 + 8 * oct;
-            float v[8];
-            const bool ok = tp < Lo + K - 1;
+            const bool ok = i < WIN * 4 && tp < Lo + K - 1;
             if constexpr (BNB) {
                 const int t = tp - g.pad;   // causal geometry: zero outside [0, L_in)
                 const bool in = ok && t >= 0 && t < g.L_in;
+                const int64_t ro = (int64_t)(in ? t : 0) * g.Cin;
+                float xa[8], xq[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const int c = cb + j;
-                    v[j] = (in && c < g.Cin) ? bn_bwd_val(xb[(int64_t)t * g.Cin + c], x2b[(int64_t)t * g.Cin + c], bp,
-                                                           g.Cin, c, act, invM)
-                                             : 0.f;
+                    const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
+                    xa[j] = xb[ro + c];
+                    xq[j] = x2b[ro + c];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
+                    v[it][j] = (in && cb + j < g.Cin) ? bn_bwd_val(xa[j], xq[j], bp, g.Cin, c, act, invM) : 0.f;
                 }
                 if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
                     const int cpad = (g.Cin + 7) & ~7;   // cb < Cin and cb % 8 == 0: the octet fits the padded row
-                    *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v);
+                    *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v[it]);
                 }
             } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = (ok && cb + j < g.Cin) ? src_val(xb, g, tp, cb + j) : 0.f;
+                src_vec<8>(xb, g, tp, cb, ok, v[it]);
             }
-            *(bf16x8*)(xs + row * RS + 8 * oct) = pack8(v);
         }
-        // taps: K x TC rows x 4 octets, 16 B each from the shadow
-        for (int i = tid; i < K * TC * 4; i += 256) {
+        bf16x8 wt[NWI];
+#pragma unroll
+        for (int it = 0; it < NWI; ++it) {
+            const int i = tid + 256 * it;
+            const int ic = i < K * TC * 4 ? i : K * TC * 4 - 1;
+            const int oct = ic & 3, r = ic >> 2, k = r / TC, co = r - k * TC;
+            const int coc = co0 + co < g.Cout ? co0 + co : g.Cout - 1;
+            wt[it] = *(const bf16x8*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
+        }
+#pragma unroll
+        for (int it = 0; it < NI; ++it) {
+            const int i = tid + 256 * it;
+            if (i < WIN * 4) *(bf16x8*)(xs + (i >> 2) * RS + 8 * (i & 3)) = pack8(v[it]);
+        }
+#pragma unroll
+        for (int it = 0; it < NWI; ++it) {
+            const int i = tid + 256 * it;
+            if (i >= K * TC * 4) continue;
             const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
-            bf16x8 val;
-            if (co0 + co < g.Cout) {
-                val = *(const bf16x8*)(w16 + ((int64_t)(co0 + co) * K + k) * cin32 + c0 + 8 * oct);
-            } else {
+            bf16x8 val = wt[it];
+            if (co0 + co >= g.Cout) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
             }
@@ -281,35 +304,73 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
         if (r + n > r1) n = (int)(r1 - r);
         const float* xb = x + (int64_t)b * g.L_in * g.Cin;
         const float* dyb = DYB ? nullptr : dy + ((int64_t)b * g.L_out + t0) * g.Cout;
-        // dY rows (zero rows past n, zero channels past Cout), 4 channels per thread-item
+        // dY rows (zero rows past n, zero channels past Cout), 4 channels per thread-item,
+        // and the input window rows t0 .. t0 + DWR + K - 2 (padding / upsample applied,
+        // zero past n + K - 1): items in rounds of 4 per thread, every load of a round
+        // issued before its stores (clamped addresses, masked values)
+        constexpr int UR = 4;
+        const int nd = DWR * (cout16 / 4), nx = (DWR + K - 1) * (cin16 / 4);
         if constexpr (DYB) {
             const __bf16* db16 = dyb16 + ((int64_t)b * g.L_out + t0) * dys;
             typedef short v4s __attribute__((ext_vector_type(4)));
-            for (int i = tid; i < DWR * (cout16 / 4); i += 256) {
-                const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
-                v4s v = v4s{0, 0, 0, 0};
-                if (t < n && c < dys) v = *(const v4s*)(db16 + (int64_t)t * dys + c);   // pad channels are 0
-                *(v4s*)(ds + t * dstride + c) = v;
-            }
-        } else
-        for (int i = tid; i < DWR * (cout16 / 4); i += 256) {
-            const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
-            float v[4];
-            {
+            for (int i0 = tid; i0 < nd; i0 += 256 * UR) {
+                v4s v[UR];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (t < n && c + j < g.Cout) ? dyb[(int64_t)t * g.Cout + c + j] : 0.f;
-            }
+                for (int u = 0; u < UR; ++u) {
+                    const int i = i0 + 256 * u;
+                    const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
+                    const bool ok = i < nd && t < n && c < dys;   // pad channels are 0
+                    v[u] = *(const v4s*)(db16 + (int64_t)(ok ? t : 0) * dys + (ok ? c : 0));
+                    if (!ok) v[u] = v4s{0, 0, 0, 0};
+                }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) ds[t * dstride + c + j] = (__bf16)v[j];
+                for (int u = 0; u < UR; ++u) {
+                    const int i = i0 + 256 * u;
+                    const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
+                    if (i < nd) *(v4s*)(ds + t * dstride + c) = v[u];
+                }
+            }
+        } else {
+            for (int i0 = tid; i0 < nd; i0 += 256 * UR) {
+                float v[UR][4];
+#pragma unroll
+                for (int u = 0; u < UR; ++u) {
+                    const int i = i0 + 256 * u;
+                    const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
+                    const bool ok = i < nd && t < n;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int cc = c + j < g.Cout ? c + j : g.Cout - 1;
+                        v[u][j] = dyb[(int64_t)(ok ? t : 0) * g.Cout + cc];
+                        v[u][j] = (ok && c + j < g.Cout) ? v[u][j] : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UR; ++u) {
+                    const int i = i0 + 256 * u;
+                    const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
+                    if (i < nd)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) ds[t * dstride + c + j] = (__bf16)v[u][j];
+                }
+            }
         }
-        // input window rows t0 .. t0 + DWR + K - 2 (padding / upsample applied), zero past n + K - 1
-        for (int i = tid; i < (DWR + K - 1) * (cin16 / 4); i += 256) {
-            const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
-            float v[4];
+        for (int i0 = tid; i0 < nx; i0 += 256 * UR) {
+            float v[UR][4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (t < n + K - 1 && c + j < g.Cin) ? src_val(xb, g, t0 + t, c + j) : 0.f;
+            for (int u = 0; u < UR; ++u) {
+                const int i = i0 + 256 * u;
+                const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
+                src_vec<4>(xb, g, t0 + t, c, i < nx && t < n + K - 1, v[u]);
+            }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) xs[t * xstride + c + j] = (__bf16)v[j];
+            for (int u = 0; u < UR; ++u) {
+                const int i = i0 + 256 * u;
+                const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
+                if (i < nx)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) xs[t * xstride + c + j] = (__bf16)v[u][j];
+            }
         }
         __syncthreads();
 #pragma unroll
