@@ -77,66 +77,112 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int c0 = 0; c0 < g.Cin; c0 += CB) {
-        // window: WIN rows x 4 octets of 8 channels, fp32 -> bf16, and the chunk's taps
-        // (K x TC rows x 4 octets, 16 B each from the shadow): every load of the thread
-        // issued before the first store (clamped addresses, masked values)
-        constexpr int NI = (WIN * 4 + 255) / 256, NWI = (K * TC * 4 + 255) / 256;
-        float v[NI][8];
+        if constexpr (K <= 3) {
+            // small K (few taps, little MFMA work per staged row): the per-element staging
+            // keeps the register count, and with it the occupancy, low (measured faster)
+            for (int i = tid; i < WIN * 4; i += 256) {
+                const int row = i >> 2, oct = i & 3;
+                const int tp = t0 + row, cb = c0 + 8 * oct;
+                float v[8];
+                const bool ok = tp < Lo + K - 1;
+                if constexpr (BNB) {
+                    const int t = tp - g.pad;   // causal geometry: zero outside [0, L_in)
+                    const bool in = ok && t >= 0 && t < g.L_in;
 #pragma unroll
-        for (int it = 0; it < NI; ++it) {
-            const int i = tid + 256 * it;
-            const int row = i >> 2, oct = i & 3;
-            const int tp = t0 + row, cb = c0 + 8 * oct;
-            const bool ok = i < WIN * 4 && tp < Lo + K - 1;
-            if constexpr (BNB) {
-                const int t = tp - g.pad;   // causal geometry: zero outside [0, L_in)
-                const bool in = ok && t >= 0 && t < g.L_in;
-                const int64_t ro = (int64_t)(in ? t : 0) * g.Cin;
-                float xa[8], xq[8];
+                    for (int j = 0; j < 8; ++j) {
+                        const int c = cb + j;
+                        v[j] = (in && c < g.Cin) ? bn_bwd_val(xb[(int64_t)t * g.Cin + c], x2b[(int64_t)t * g.Cin + c],
+                                                               bp, g.Cin, c, act, invM)
+                                                 : 0.f;
+                    }
+                    if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
+                        const int cpad = (g.Cin + 7) & ~7;
+                        *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v);
+                    }
+                } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
-                    xa[j] = xb[ro + c];
-                    xq[j] = x2b[ro + c];
+                    for (int j = 0; j < 8; ++j) v[j] = (ok && cb + j < g.Cin) ? src_val(xb, g, tp, cb + j) : 0.f;
                 }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
-                    v[it][j] = (in && cb + j < g.Cin) ? bn_bwd_val(xa[j], xq[j], bp, g.Cin, c, act, invM) : 0.f;
-                }
-                if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
-                    const int cpad = (g.Cin + 7) & ~7;   // cb < Cin and cb % 8 == 0: the octet fits the padded row
-                    *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v[it]);
-                }
-            } else {
-                src_vec<8>(xb, g, tp, cb, ok, v[it]);
+                *(bf16x8*)(xs + row * RS + 8 * oct) = pack8(v);
             }
-        }
-        bf16x8 wt[NWI];
+            for (int i = tid; i < K * TC * 4; i += 256) {
+                const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
+                bf16x8 val;
+                if (co0 + co < g.Cout) {
+                    val = *(const bf16x8*)(w16 + ((int64_t)(co0 + co) * K + k) * cin32 + c0 + 8 * oct);
+                } else {
 #pragma unroll
-        for (int it = 0; it < NWI; ++it) {
-            const int i = tid + 256 * it;
-            const int ic = i < K * TC * 4 ? i : K * TC * 4 - 1;
-            const int oct = ic & 3, r = ic >> 2, k = r / TC, co = r - k * TC;
-            const int coc = co0 + co < g.Cout ? co0 + co : g.Cout - 1;
-            wt[it] = *(const bf16x8*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
-        }
-#pragma unroll
-        for (int it = 0; it < NI; ++it) {
-            const int i = tid + 256 * it;
-            if (i < WIN * 4) *(bf16x8*)(xs + (i >> 2) * RS + 8 * (i & 3)) = pack8(v[it]);
-        }
-#pragma unroll
-        for (int it = 0; it < NWI; ++it) {
-            const int i = tid + 256 * it;
-            if (i >= K * TC * 4) continue;
-            const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
-            bf16x8 val = wt[it];
-            if (co0 + co >= g.Cout) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
+                    for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
+                }
+                *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = val;
             }
-            *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = val;
+        } else {
+            // window: WIN rows x 4 octets of 8 channels, fp32 -> bf16, and the chunk's taps
+            // (K x TC rows x 4 octets, 16 B each from the shadow): every load of the thread
+            // issued before the first store (clamped addresses, masked values)
+            constexpr int NI = (WIN * 4 + 255) / 256, NWI = (K * TC * 4 + 255) / 256;
+            bf16x8 wt[NWI];
+    #pragma unroll
+            for (int it = 0; it < NWI; ++it) {
+                const int i = tid + 256 * it;
+                const int ic = i < K * TC * 4 ? i : K * TC * 4 - 1;
+                const int oct = ic & 3, r = ic >> 2, k = r / TC, co = r - k * TC;
+                const int coc = co0 + co < g.Cout ? co0 + co : g.Cout - 1;
+                wt[it] = *(const bf16x8*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
+            }
+            // window items in rounds of NB (all loads of a round in flight together)
+            constexpr int NB = BNB ? (NI < 2 ? NI : 2) : (NI < 3 ? NI : 3);
+    #pragma unroll
+            for (int r0 = 0; r0 < NI; r0 += NB) {
+            float v[NB][8];
+    #pragma unroll
+            for (int it = 0; it < NB; ++it) {
+                const int i = tid + 256 * (r0 + it);
+                const int row = i >> 2, oct = i & 3;
+                const int tp = t0 + row, cb = c0 + 8 * oct;
+                const bool ok = r0 + it < NI && i < WIN * 4 && tp < Lo + K - 1;
+                if constexpr (BNB) {
+                    const int t = tp - g.pad;   // causal geometry: zero outside [0, L_in)
+                    const bool in = ok && t >= 0 && t < g.L_in;
+                    const int64_t ro = (int64_t)(in ? t : 0) * g.Cin;
+                    float xa[8], xq[8];
+    #pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
+                        xa[j] = xb[ro + c];
+                        xq[j] = x2b[ro + c];
+                    }
+    #pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
+                        v[it][j] = (in && cb + j < g.Cin) ? bn_bwd_val(xa[j], xq[j], bp, g.Cin, c, act, invM) : 0.f;
+                    }
+                    if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
+                        const int cpad = (g.Cin + 7) & ~7;   // cb < Cin and cb % 8 == 0: the octet fits the padded row
+                        *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v[it]);
+                    }
+                } else {
+                    src_vec<8>(xb, g, tp, cb, ok, v[it]);
+                }
+            }
+    #pragma unroll
+            for (int it = 0; it < NB; ++it) {
+                const int i = tid + 256 * (r0 + it);
+                if (r0 + it < NI && i < WIN * 4) *(bf16x8*)(xs + (i >> 2) * RS + 8 * (i & 3)) = pack8(v[it]);
+            }
+            }
+    #pragma unroll
+            for (int it = 0; it < NWI; ++it) {
+                const int i = tid + 256 * it;
+                if (i >= K * TC * 4) continue;
+                const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
+                bf16x8 val = wt[it];
+                if (co0 + co >= g.Cout) {
+    #pragma unroll
+                    for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
+                }
+                *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = val;
+            }
         }
         __syncthreads();
         const __bf16* xq = xs + (PM * 16 * wv + lr) * RS + 8 * lc;
@@ -246,9 +292,11 @@ __global__ void k_conv_shadow(const float* __restrict__ W, int Cout, int Cin, in
 // in the forward) and both operands are read with the gfx950 transposed read
 // ds_read_b64_tr_b16 (4 rows x 16 channels per 16-lane group, delivered
 // column-major), so the tap shift k is a plain row offset of the window.
-// Each wave owns PPW (16 co x 16 ci) tile pairs with K accumulators; rows
-// are split over workgroups (blockIdx.y), per-split partial slabs are summed
-// in fixed order by conv.hip's k_sum_splits.
+// Each wave owns PPW (16 co x 16 ci) tile pairs with K accumulators; NWV waves
+// per workgroup (4 or 8: 8 halves the workgroups that stage the same rows when 4
+// waves do not cover every pair); rows are split over workgroups
+// (blockIdx.y), per-split partial slabs are summed in fixed order by conv.hip's
+// k_sum_splits.
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 constexpr int DWR = 64;  // rows per staged chunk (2 MFMA k-steps)
 
@@ -269,8 +317,8 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int row0, int col0,
 
 // DYB: dY given in bf16 (dyb16, row stride dys = ceil8(Cout)), e.g. the BN input
 // gradient written by the fused backward-data kernel (k_conv_bf16 BNB + dbf).
-template <int K, int PPW, bool DYB = false>
-__global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ dy, const float* __restrict__ x, Geo g,
+template <int K, int PPW, bool DYB = false, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restrict__ dy, const float* __restrict__ x, Geo g,
                                                       int64_t rows_per_split, int NTc, int npairs, int dstride,
                                                       int xstride, float* __restrict__ part,
                                                       const __bf16* __restrict__ dyb16, int dys) {
@@ -282,7 +330,7 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
     bool act[PPW];
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
-        const int p = blockIdx.x * (4 * PPW) + wv + 4 * j;
+        const int p = blockIdx.x * (NWV * PPW) + wv + NWV * j;
         act[j] = p < npairs;
         mt[j] = act[j] ? p / NTc : 0;
         nt[j] = act[j] ? p - mt[j] * NTc : 0;
@@ -308,16 +356,16 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
         // and the input window rows t0 .. t0 + DWR + K - 2 (padding / upsample applied,
         // zero past n + K - 1): items in rounds of 4 per thread, every load of a round
         // issued before its stores (clamped addresses, masked values)
-        constexpr int UR = 4;
+        constexpr int UR = K <= 3 ? 1 : 4;   // small K: registers (occupancy) first
         const int nd = DWR * (cout16 / 4), nx = (DWR + K - 1) * (cin16 / 4);
         if constexpr (DYB) {
             const __bf16* db16 = dyb16 + ((int64_t)b * g.L_out + t0) * dys;
             typedef short v4s __attribute__((ext_vector_type(4)));
-            for (int i0 = tid; i0 < nd; i0 += 256 * UR) {
+            for (int i0 = tid; i0 < nd; i0 += 64 * NWV * UR) {
                 v4s v[UR];
 #pragma unroll
                 for (int u = 0; u < UR; ++u) {
-                    const int i = i0 + 256 * u;
+                    const int i = i0 + 64 * NWV * u;
                     const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
                     const bool ok = i < nd && t < n && c < dys;   // pad channels are 0
                     v[u] = *(const v4s*)(db16 + (int64_t)(ok ? t : 0) * dys + (ok ? c : 0));
@@ -325,17 +373,17 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
                 }
 #pragma unroll
                 for (int u = 0; u < UR; ++u) {
-                    const int i = i0 + 256 * u;
+                    const int i = i0 + 64 * NWV * u;
                     const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
                     if (i < nd) *(v4s*)(ds + t * dstride + c) = v[u];
                 }
             }
         } else {
-            for (int i0 = tid; i0 < nd; i0 += 256 * UR) {
+            for (int i0 = tid; i0 < nd; i0 += 64 * NWV * UR) {
                 float v[UR][4];
 #pragma unroll
                 for (int u = 0; u < UR; ++u) {
-                    const int i = i0 + 256 * u;
+                    const int i = i0 + 64 * NWV * u;
                     const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
                     const bool ok = i < nd && t < n;
 #pragma unroll
@@ -347,7 +395,7 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
                 }
 #pragma unroll
                 for (int u = 0; u < UR; ++u) {
-                    const int i = i0 + 256 * u;
+                    const int i = i0 + 64 * NWV * u;
                     const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
                     if (i < nd)
 #pragma unroll
@@ -355,17 +403,17 @@ __global__ __launch_bounds__(256) void k_conv_dw_bf16(const float* __restrict__ 
                 }
             }
         }
-        for (int i0 = tid; i0 < nx; i0 += 256 * UR) {
+        for (int i0 = tid; i0 < nx; i0 += 64 * NWV * UR) {
             float v[UR][4];
 #pragma unroll
             for (int u = 0; u < UR; ++u) {
-                const int i = i0 + 256 * u;
+                const int i = i0 + 64 * NWV * u;
                 const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
                 src_vec<4>(xb, g, t0 + t, c, i < nx && t < n + K - 1, v[u]);
             }
 #pragma unroll
             for (int u = 0; u < UR; ++u) {
-                const int i = i0 + 256 * u;
+                const int i = i0 + 64 * NWV * u;
                 const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
                 if (i < nx)
 #pragma unroll
@@ -544,10 +592,14 @@ static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin,
     // 4 waves of one workgroup need (small layers: no MFMAs on empty pairs)
     const int ppw_max = K <= 3 ? 6 : (K <= 5 ? 4 : (K <= 7 ? 3 : 2));
     const int ppw = cdiv(npairs, 4) < ppw_max ? cdiv(npairs, 4) : ppw_max;
-    const int bx = cdiv(npairs, 4 * ppw);
+    // waves per workgroup (dy16 path): 8 when 4 do not own every pair, so each row is
+    // staged by half as many workgroups (16 waves would cap the accumulators at 128 VGPRs)
+    const int need = cdiv(npairs, ppw);
+    const int nwv = !dy16 || need <= 4 ? 4 : 8;
+    const int bx = cdiv(npairs, nwv * ppw);
     const int64_t rows = (int64_t)B * g.L_out;
     const int64_t nout = (int64_t)Cout * Cin * K;
-    int64_t splits = 1024 / bx;
+    int64_t splits = 4096 / (nwv * bx);
     if (splits * nout > (int64_t)8 << 20) splits = ((int64_t)8 << 20) / nout;
     if (splits > rows / (4 * DWR)) splits = rows / (4 * DWR);
     if (splits < 1) splits = 1;
@@ -562,7 +614,10 @@ static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin,
     dim3 grid(bx, (unsigned)splits);
 #define VT_DWB(KK, PP)                                                                                         \
     if (K == KK && ppw == PP) {                                                                                \
-        if (dy16)                                                                                              \
+        if (dy16 && nwv == 8)                                                                             \
+            hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true, 8>), grid, dim3(512), lds, st, dY, X, g, rps, NTc,  \
+                               npairs, dstride, xstride, ws, dy16, dys);                                      \
+        else if (dy16)                                                                                         \
             hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true>), grid, dim3(256), lds, st, dY, X, g, rps, NTc, npairs, \
                                dstride, xstride, ws, dy16, dys);                                              \
         else                                                                                                   \
