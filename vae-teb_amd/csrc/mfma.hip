@@ -269,17 +269,31 @@ __global__ __launch_bounds__(256) void k_mfma_dw(const float* __restrict__ dY, i
         }
         __syncthreads();
     }
-    // D: col (k) = lane & 15, row (n) = 4 * (lane >> 4) + rr
+    // D: col (k) = lane & 15, row (n) = 4 * (lane >> 4) + rr.  Accumulating: every
+    // old value is loaded before the first store (one round trip, not 64: the compiler
+    // cannot prove the 64 addresses distinct for a runtime K, so an interleaved
+    // load / store sequence would serialise)
     const int lr = lane & 15, lc = lane >> 4;
+    float* c0 = dW + (int64_t)(n0 + 64 * wm + 4 * lc) * K + k0 + 64 * wn + lr;
+    if (accumulate) {
+        f32x4 old[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) old[i][j][rr] = c0[(int64_t)(16 * i + rr) * K + 16 * j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] += old[i][j];
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                float* c = dW + (int64_t)(n0 + 64 * wm + 16 * i + 4 * lc + rr) * K + k0 + 64 * wn + 16 * j + lr;
-                *c = accumulate ? *c + acc[i][j][rr] : acc[i][j][rr];
-            }
+            for (int rr = 0; rr < 4; ++rr) c0[(int64_t)(16 * i + rr) * K + 16 * j] = acc[i][j][rr];
 }
 
 static inline int64_t up_to(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
