@@ -329,6 +329,13 @@ int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, 
 int vt_conv1d_bwd_gpad_bf16_bn(const float* dY, const float* Xc, const float* bnp, int act, int64_t M, int B,
                                int L_in, int Cin, const void* w16t, int Cout, int K, int mode, int up, float* gpad,
                                void* dxbn16, void* stream);
+/* The same backward-data conv writing dX directly (no gpad + vt_conv1d_fold pass)
+ * for the geometries whose fold is a crop: no upsample; causal, or reflect with
+ * L_in > pad, whose 2 pad mirrored rows per sample go through edge [B][2 pad][Cin]
+ * and are added back by a small second kernel (the fold's order: same bits).     */
+int vt_conv1d_bwd_dx_bf16_bn(const float* dY, const float* Xc, const float* bnp, int act, int64_t M, int B, int L_in,
+                             int Cin, const void* w16t, int Cout, int K, int mode, int up, float* dX, float* edge,
+                             void* dxbn16, void* stream);
 int vt_conv1d_bwd_weight_bf16_dy16(const void* dY16, const float* X, int B, int L_in, int Cin, int Cout, int K,
                                    int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
                                    void* stream);

@@ -218,3 +218,43 @@ def test_fused_batchnorm_backward_bitwise(L, geo, act):
     assert torch.equal(gp0, gp1), ((gp0 != gp1).sum().item(), gp0.numel(), (gp0 - gp1).abs().max().item(),
                                    gp0.abs().max().item(), (dw0 != dw1).sum().item())
     assert torch.equal(dw0, dw1)
+
+
+@pytest.mark.parametrize("geo", [(2, 40, 20, 17, 5, 0, 0), (3, 33, 33, 22, 3, 1, 0), (2, 256, 87, 77, 11, 1, 0),
+                                 (2, 6, 9, 7, 11, 1, 0), (2, 3, 5, 6, 5, 1, 0), (2, 1024, 55, 44, 5, 1, 0),
+                                 (1, 7, 16, 16, 7, 0, 0)])
+def test_backward_data_direct_dx_bitwise(L, geo):
+    """vt_conv1d_bwd_dx_bf16_bn (dX written by the conv, reflect edges added back)
+    == vt_conv1d_bwd_gpad_bf16_bn + vt_conv1d_fold, bit for bit; dxbn equal."""
+    B, Lin, Cin, Cout, K, mode, up = geo
+    pad = K - 1 if mode == 0 else (K - 1) // 2
+    if mode == 1 and Lin <= pad:
+        with pytest.raises(ValueError):
+            L.call("vt_conv1d_bwd_dx_bf16_bn", None, None, None, 1, 1, B, Lin, Cin, None, Cout, K, mode, up, None,
+                   None, None, L.stream())
+        return
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    M = B * Lo
+    torch.manual_seed(sum(geo))
+    w = torch.randn(Cout, Cin, K, device="cuda") / (Cin * K) ** 0.5
+    conv = torch.randn(B, Lo, Cout, device="cuda") * 2 + 0.3
+    gy = torch.randn(B, Lo, Cout, device="cuda")
+    bnp = torch.cat([conv.reshape(-1, Cout).mean(0), 1 / (conv.reshape(-1, Cout).var(0) + 1e-5).sqrt(),
+                     1 + 0.1 * torch.randn(Cout, device="cuda"), 0.1 * torch.randn(Cout, device="cuda"),
+                     torch.randn(Cout, device="cuda"), torch.randn(Cout, device="cuda")]).contiguous()
+    _, w16t = _shadow(L, w)
+    cp = (Cout + 7) // 8 * 8
+    gp = torch.empty(B, Lo + K - 1, Cin, device="cuda")
+    d0 = torch.full((M, cp), float("nan"), dtype=torch.bfloat16, device="cuda")
+    L.call("vt_conv1d_bwd_gpad_bf16_bn", L.ptr(gy), L.ptr(conv), L.ptr(bnp), 1, M, B, Lin, Cin, L.ptr(w16t), Cout,
+           K, mode, up, L.ptr(gp), L.ptr(d0), L.stream())
+    dx0 = torch.empty(B, Lin, Cin, device="cuda")
+    L.call("vt_conv1d_fold", L.ptr(gp), B, Lin, Cin, Cout, K, mode, up, L.ptr(dx0), 0, L.stream())
+    dx1 = torch.full((B, Lin, Cin), float("nan"), device="cuda")
+    edge = torch.full((max(B * 2 * pad * Cin, 1),), float("nan"), device="cuda")
+    d1 = torch.full((M, cp), float("nan"), dtype=torch.bfloat16, device="cuda")
+    L.call("vt_conv1d_bwd_dx_bf16_bn", L.ptr(gy), L.ptr(conv), L.ptr(bnp), 1, M, B, Lin, Cin, L.ptr(w16t), Cout, K,
+           mode, up, L.ptr(dx1), L.ptr(edge), L.ptr(d1), L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1), ((dx0 != dx1).sum().item(), dx0.numel())
+    assert torch.equal(d0, d1)

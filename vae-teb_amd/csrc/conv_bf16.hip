@@ -37,6 +37,15 @@ struct BCfg {
     static constexpr int LDS_BYTES = (XB + WB) * 2 > 8 * TC * 4 ? (XB + WB) * 2 : 8 * TC * 4;
 };
 
+// Backward-data output written straight into dX (no padded gpad pass + fold):
+// padded row t goes to dX row t - pad when it lies in [0, L), to edge row t (t < pad)
+// or t - L (t >= pad + L) otherwise (reflect padding: k_conv_fold_edges adds those
+// back); pad < 0: the plain [B][Lo] output.
+struct FoldOut {
+    int pad, L;
+    float* edge;   // nullable: the edge rows are dropped (causal padding)
+};
+
 __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
     bf16x8 r;
 #pragma unroll
@@ -56,7 +65,7 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
                                                    int cin32, float* __restrict__ y, int Lo,
                                                    float* __restrict__ stats, const float* __restrict__ x2,
                                                    const float* __restrict__ bnp, int act, float invM,
-                                                   __bf16* __restrict__ dbf) {
+                                                   __bf16* __restrict__ dbf, FoldOut fo) {
     using C = BCfg<K, NT>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
     extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
@@ -210,6 +219,12 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
             const int t = t0 + PM * 16 * wv + 16 * m + 4 * lc + r;
             if (t >= Lo) continue;
             float* yr = y + ((int64_t)b * Lo + t) * g.Cout;
+            if (fo.pad >= 0) {
+                const int sx = t - fo.pad;
+                if (sx >= 0 && sx < fo.L) yr = y + ((int64_t)b * fo.L + sx) * g.Cout;
+                else if (fo.edge) yr = fo.edge + ((int64_t)b * 2 * fo.pad + (sx < 0 ? t : t - fo.L)) * g.Cout;
+                else continue;
+            }
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
                 const int co = co0 + 16 * n + lr;
@@ -468,47 +483,67 @@ struct BnB {
 
 template <int K, int NT>
 int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
-          hipStream_t st, const BnB* bn) {
+          hipStream_t st, const BnB* bn, FoldOut fo) {
     using C = BCfg<K, NT>;
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
     if (x && bn)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
-                           cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf);
+                           cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo);
     else if (x)
         hipLaunchKernelGGL((k_conv_bf16<K, NT>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y, Lo, stats,
-                           nullptr, nullptr, 0, 0.f, nullptr);
+                           nullptr, nullptr, 0, 0.f, nullptr, fo);
     return C::TP;
 }
 
 template <int K>
 int bf_k(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats, hipStream_t st,
-         const BnB* bn) {
+         const BnB* bn, FoldOut fo) {
     switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
-        case 1: return bf_nt<K, 1>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 2: return bf_nt<K, 2>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 3: return bf_nt<K, 3>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 4: return bf_nt<K, 4>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 5: return bf_nt<K, 5>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        default: return bf_nt<K, 6>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 1: return bf_nt<K, 1>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 2: return bf_nt<K, 2>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 3: return bf_nt<K, 3>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 4: return bf_nt<K, 4>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 5: return bf_nt<K, 5>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        default: return bf_nt<K, 6>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
     }
 }
 
 // x == nullptr: no launch, only the position tile of this geometry
 int bf_launch(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
-              hipStream_t st, const BnB* bn = nullptr) {
+              hipStream_t st, const BnB* bn = nullptr, FoldOut fo = FoldOut{-1, 0, nullptr}) {
     switch (g.K) {
-        case 1: return bf_k<1>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 2: return bf_k<2>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 3: return bf_k<3>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 4: return bf_k<4>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 5: return bf_k<5>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 6: return bf_k<6>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 7: return bf_k<7>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 8: return bf_k<8>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 9: return bf_k<9>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        case 10: return bf_k<10>(x, g, w16, cin32, y, Lo, stats, st, bn);
-        default: return bf_k<11>(x, g, w16, cin32, y, Lo, stats, st, bn);
+        case 1: return bf_k<1>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 2: return bf_k<2>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 3: return bf_k<3>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 4: return bf_k<4>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 5: return bf_k<5>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 6: return bf_k<6>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 7: return bf_k<7>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 8: return bf_k<8>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 9: return bf_k<9>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 10: return bf_k<10>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        default: return bf_k<11>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
     }
+}
+
+// reflect padding without upsampling: the mirrored padded rows (edge, see FoldOut)
+// added onto dX rows 1 .. pad and max(0, L - 1 - pad) .. L - 2, in the order of gemm.hip's
+// k_conv_fold (direct, left mirror, right mirror: the same bits)
+__global__ void k_conv_fold_edges(float* __restrict__ dx, const float* __restrict__ edge, int L, int pad, int C) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // (row slot, channel) within sample blockIdx.y
+    if (i >= 2 * pad * C) return;
+    const int r = i / C, c = i - r * C, b = blockIdx.y;
+    const int s = r < pad ? 1 + r : L - 1 - pad + (r - pad);
+    // left set: rows 1 .. pad; right set: rows L - 1 - pad .. L - 2 (row 0 included when L <= pad + 1),
+    // its rows inside 1 .. pad already handled by the left set
+    if (s < 0 || s > L - 1 || (r < pad && s < 1) || (r >= pad && s >= 1 && s <= pad)) return;
+    const float* eb = edge + (int64_t)b * 2 * pad * C + c;
+    float* o = dx + ((int64_t)b * L + s) * C + c;
+    float v = *o;
+    if (s >= 1 && s <= pad) v += eb[(pad - s) * C];              // left mirror: padded row pad - s
+    const int tr = pad + 2 * (L - 1) - s;                        // right mirror: padded row tr
+    if (s <= L - 2 && tr < L + 2 * pad && tr >= pad + L) v += eb[(tr - L) * C];
+    *o = v;
 }
 
 constexpr int KMAXB = 11;
@@ -560,11 +595,12 @@ int vt_conv1d_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16
 }
 
 static int bwd_gpad(const float* dY, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode, int up,
-                    float* gpad, hipStream_t st, const BnB* bn, const char* who) {
+                    float* gpad, hipStream_t st, const BnB* bn, const char* who,
+                    FoldOut fo = FoldOut{-1, 0, nullptr}) {
     VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB, "%s: shape", who);
     Geo f = geo(B, L_in, Cin, Cout, K, mode, up);
     Geo g = geo(B, f.L_out, Cout, Cin, K, 0, 0);  // input dY (L_out x Cout), causal pad K-1
-    bf_launch(dY, g, (const __bf16*)w16t, cdiv(Cout, 32) * 32, gpad, f.L_out + K - 1, nullptr, st, bn);
+    bf_launch(dY, g, (const __bf16*)w16t, cdiv(Cout, 32) * 32, gpad, f.L_out + K - 1, nullptr, st, bn, fo);
     VT_LAUNCH_CHECK(who);
     return VT_OK;
 }
@@ -580,6 +616,27 @@ int vt_conv1d_bwd_gpad_bf16_bn(const float* dY, const float* Xc, const float* bn
     VT_CHECK_ARG(Xc && bnp && act >= 0 && act <= 3 && M > 0, "vt_conv1d_bwd_gpad_bf16_bn: BatchNorm arguments");
     const BnB bn{Xc, bnp, act, 1.f / (float)M, (__bf16*)dxbn16};
     return bwd_gpad(dY, B, L_in, Cin, w16t, Cout, K, mode, up, gpad, S(stream), &bn, "vt_conv1d_bwd_gpad_bf16_bn");
+}
+
+int vt_conv1d_bwd_dx_bf16_bn(const float* dY, const float* Xc, const float* bnp, int act, int64_t M, int B, int L_in,
+                             int Cin, const void* w16t, int Cout, int K, int mode, int up, float* dX, float* edge,
+                             void* dxbn16, void* stream) {
+    VT_CHECK_ARG(Xc && bnp && act >= 0 && act <= 3 && M > 0, "vt_conv1d_bwd_dx_bf16_bn: BatchNorm arguments");
+    const Geo f = geo(B, L_in, Cin, Cout, K, mode, up);
+    VT_CHECK_ARG(!up && (mode == 0 || f.L_up > f.pad) && (mode == 0 || f.pad == 0 || edge),
+                 "vt_conv1d_bwd_dx_bf16_bn: geometry (no upsample, reflect needs L > pad and an edge buffer)");
+    const BnB bn{Xc, bnp, act, 1.f / (float)M, (__bf16*)dxbn16};
+    const FoldOut fo{f.pad, L_in, mode == 0 ? nullptr : edge};
+    const int rc = bwd_gpad(dY, B, L_in, Cin, w16t, Cout, K, mode, up, dX, S(stream), &bn,
+                            "vt_conv1d_bwd_dx_bf16_bn", fo);
+    if (rc) return rc;
+    if (mode == 1 && f.pad > 0) {
+        VT_CHECK_ARG(B <= 65535, "vt_conv1d_bwd_dx_bf16_bn: batch");
+        hipLaunchKernelGGL(k_conv_fold_edges, dim3((unsigned)((2 * f.pad * Cin + 255) / 256), (unsigned)B), dim3(256),
+                           0, S(stream), dX, edge, L_in, f.pad, Cin);
+        VT_LAUNCH_CHECK("vt_conv1d_bwd_dx_bf16_bn");
+    }
+    return VT_OK;
 }
 
 static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode, int up,

@@ -64,6 +64,8 @@ LSTM_GRAD_STREAM = None  # ... for the LSTM weight gradients (set by SeqVaeTeb)
 # LSTM input projections inside the recurrence kernels (vt_lstm_layer_{fwd,bwd}_x) for
 # input sizes <= 64; 0: separate skinny GEMMs (the same results bit for bit)
 LSTM_FUSED = int(os.environ.get("VAETEB_LSTM_FUSED", "1"))
+# bf16 conv backward-data written straight into dX where the fold is a crop; 0: gpad + fold
+CONV_DIRECT_DX = int(os.environ.get("VAETEB_CONV_DIRECT_DX", "1"))
 
 
 class _ParamGrads:
@@ -478,13 +480,21 @@ class ConvBNActF(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
-            gpad = WS.get(B * (Lo + K - 1) * Cin, x.device, 3)
-            if fused:
-                call("vt_conv1d_bwd_gpad_bf16_bn", ptr(gy), ptr(conv), ptr(bnp), ACT[act], M, B, L, Cin, ptr(w16t),
-                     Cout, K, mode, up, ptr(gpad), ptr(dxbn), _st())
+            pad = K - 1 if mode == 0 else (K - 1) // 2
+            if fused and CONV_DIRECT_DX and not up and (mode == 0 or L > pad):
+                # the fold is a crop: the conv writes gx itself (reflect: + the mirrored edge rows)
+                edge = WS.get(max(B * 2 * pad * Cin, 1), x.device, 3)
+                call("vt_conv1d_bwd_dx_bf16_bn", ptr(gy), ptr(conv), ptr(bnp), ACT[act], M, B, L, Cin, ptr(w16t),
+                     Cout, K, mode, up, ptr(gx), ptr(edge), ptr(dxbn), _st())
             else:
-                call("vt_conv1d_direct_bwd_gpad", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gpad), _st())
-            call("vt_conv1d_fold", ptr(gpad), B, L, Cin, Cout, K, mode, up, ptr(gx), 0, _st())
+                gpad = WS.get(B * (Lo + K - 1) * Cin, x.device, 3)
+                if fused:
+                    call("vt_conv1d_bwd_gpad_bf16_bn", ptr(gy), ptr(conv), ptr(bnp), ACT[act], M, B, L, Cin,
+                         ptr(w16t), Cout, K, mode, up, ptr(gpad), ptr(dxbn), _st())
+                else:
+                    call("vt_conv1d_direct_bwd_gpad", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gpad),
+                         _st())
+                call("vt_conv1d_fold", ptr(gpad), B, L, Cin, Cout, K, mode, up, ptr(gx), 0, _st())
         pw = _ParamGrads([w], [ctx.needs_input_grad[1]])
         if pw.out[0] is not None:
             side = GRAD_STREAM if (pw.direct and GRAD_STREAM is not None) else None
