@@ -177,6 +177,10 @@ int vt_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float
  * whole training step can be captured once in a hipGraph and replayed.          */
 int vt_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                       float eps, float weight_decay, int* step, float* coef, const float* gscale, void* stream);
+/* Tuning switch: 1 (default) = the float4 AdamW kernel when p, g, m, v are all
+ * 16-byte aligned, 0 = the scalar kernel.  Same per-element expression: the
+ * two give the same bits (tested).  Env override: VAETEB_ADAMW_SCALAR=1.         */
+int vt_adamw_set_vector(int on);
 /* bf16 (RNE) shadow copy of fp32 data, for MFMA operands.                         */
 int vt_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
 

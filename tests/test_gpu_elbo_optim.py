@@ -105,3 +105,29 @@ def test_grad_norm_and_adamw_match_torch(L):
     got = flat_p.cpu()
     exp = torch.cat([p.detach().reshape(-1) for p in ref])
     assert torch.allclose(got, exp, rtol=1e-5, atol=1e-6), (got - exp).abs().max()
+
+
+def test_adamw_vector_equals_scalar(L):
+    """The float4 AdamW kernel (aligned buffers) gives the scalar kernel's bits,
+    including the < 4 tail elements; a misaligned view takes the scalar kernel."""
+    torch.manual_seed(3)
+    for n in (4099, 1 << 20):
+        p0, g = torch.randn(n + 1, device="cuda"), torch.randn(n + 1, device="cuda") * 3
+        m0, v0 = torch.randn(n + 1, device="cuda") * 0.1, torch.rand(n + 1, device="cuda") * 0.1
+        gscale = torch.tensor([0.7], device="cuda")
+        outs = []
+        for vec in (1, 0):
+            L.call("vt_adamw_set_vector", vec)
+            p, m, v = p0.clone(), m0.clone(), v0.clone()
+            for step in (1, 2):
+                L.call("vt_adamw_step", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999,
+                       1e-8, 1e-4, step, gscale.data_ptr(), L.stream())
+            outs.append((p, m, v))
+        L.call("vt_adamw_set_vector", 1)
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
+        # misaligned (offset by one float): the launcher falls back to the scalar kernel
+        p, m, v = p0.clone(), m0.clone(), v0.clone()
+        L.call("vt_adamw_step", p.data_ptr() + 4, g.data_ptr() + 4, m.data_ptr() + 4, v.data_ptr() + 4, n, 1e-3, 0.9,
+               0.999, 1e-8, 1e-4, 1, gscale.data_ptr(), L.stream())
+        assert torch.equal(p[0], p0[0]) and not torch.equal(p[1:], p0[1:])

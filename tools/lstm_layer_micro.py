@@ -80,3 +80,18 @@ for name, fn in (("fwd_x", fwd), ("bwd_x", bwd), ("bwd_weight", bww)):
     two = timed(pair(fn))
     print(f"In={In} {name:11s}: alone {one:7.1f} us ({one / S * 1e3:6.1f} ns/step)   two streams {two:7.1f} us",
           flush=True)
+
+
+def mixed():
+    # one encoder's recurrence beside the other encoder's weight gradient (the step's overlap)
+    s1.wait_stream(torch.cuda.current_stream())
+    s2.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s1):
+        bwd(a)
+    with torch.cuda.stream(s2):
+        bww(b)
+    torch.cuda.current_stream().wait_stream(s1)
+    torch.cuda.current_stream().wait_stream(s2)
+
+
+print(f"In={In} bwd_x || bwd_weight: {timed(mixed):7.1f} us", flush=True)

@@ -59,31 +59,99 @@ __global__ void k_norm_finalize(const float* __restrict__ partial, int count, fl
     }
 }
 
+// One element of the torch.optim.AdamW single-tensor update, shared by the
+// scalar and the float4 kernels.  Contraction is off (every multiply and add
+// rounded, as torch's separate lerp_ / mul_ / addcmul_ / addcdiv_ ops), so the
+// compiler's fma choices cannot differ between the two: the same bits.
+struct AdamwK {
+    float gs, decay, w1, w2, beta2, eps, step_size, bc2_sqrt;
+};
+__device__ __forceinline__ void adamw_elem(const AdamwK& k, float& p, float g, float& m, float& v) {
+#pragma clang fp contract(off)
+    const float gi = g * k.gs;
+    const float pi = p * k.decay;
+    const float mi = m + k.w1 * (gi - m);                 // exp_avg.lerp_(grad, 1-beta1)
+    const float vi = v * k.beta2 + k.w2 * gi * gi;        // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+    const float denom = sqrtf(vi) / k.bc2_sqrt + k.eps;
+    p = pi - k.step_size * (mi / denom);                  // param.addcdiv_(m, denom, -step_size)
+    m = mi;
+    v = vi;
+}
+
+__device__ __forceinline__ AdamwK adamw_consts(float lr, float beta1, float beta2, float eps, float wd,
+                                               float step_size, float bc2_sqrt, const float* gscale,
+                                               const float* coef) {
+    AdamwK k;
+    k.gs = gscale ? gscale[0] : 1.0f;
+    if (coef) {  // device-side step (graph-capturable): coef = {lr / bc1, sqrt(bc2)}
+        step_size = coef[0];
+        bc2_sqrt = coef[1];
+    }
+    k.decay = 1.0f - lr * wd;
+    k.w1 = 1.0f - beta1;
+    k.w2 = 1.0f - beta2;
+    k.beta2 = beta2;
+    k.eps = eps;
+    k.step_size = step_size;
+    k.bc2_sqrt = bc2_sqrt;
+    return k;
+}
+
 __global__ __launch_bounds__(OPT_THREADS) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                        float lr, float beta1, float beta2, float eps, float wd,
                                                        float step_size, float bc2_sqrt,
                                                        const float* __restrict__ gscale,
                                                        const float* __restrict__ coef) {
-    const float gs = gscale ? gscale[0] : 1.0f;
-    if (coef) {  // device-side step (graph-capturable): coef = {lr / bc1, sqrt(bc2)}
-        step_size = coef[0];
-        bc2_sqrt = coef[1];
-    }
-    const float decay = 1.0f - lr * wd;
-    const float w1 = 1.0f - beta1, w2 = 1.0f - beta2;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float gi = g[i] * gs;
-        float pi = p[i] * decay;
-        const float mi = m[i] + w1 * (gi - m[i]);          // exp_avg.lerp_(grad, 1-beta1)
-        const float vi = v[i] * beta2 + w2 * gi * gi;      // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-        const float denom = sqrtf(vi) / bc2_sqrt + eps;
-        pi = pi - step_size * (mi / denom);                // param.addcdiv_(m, denom, -step_size)
-        p[i] = pi;
-        m[i] = mi;
-        v[i] = vi;
-    }
+    const AdamwK k = adamw_consts(lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        adamw_elem(k, p[i], g[i], m[i], v[i]);
 }
+
+// The same update over 16-byte vectors (all four buffers 16-byte aligned):
+// 2 float4 of each stream in flight per thread and iteration (8 x 16 B loads
+// issued before the first use), the < 4 tail elements by the first threads.
+__global__ __launch_bounds__(OPT_THREADS) void k_adamw4(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                        float lr, float beta1, float beta2, float eps, float wd,
+                                                        float step_size, float bc2_sqrt,
+                                                        const float* __restrict__ gscale,
+                                                        const float* __restrict__ coef) {
+    const AdamwK k = adamw_consts(lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
+    float4* p4 = reinterpret_cast<float4*>(p);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+    auto upd = [&](float4& pp, const float4& gg, float4& mm, float4& vv) {
+        adamw_elem(k, pp.x, gg.x, mm.x, vv.x);
+        adamw_elem(k, pp.y, gg.y, mm.y, vv.y);
+        adamw_elem(k, pp.z, gg.z, mm.z, vv.z);
+        adamw_elem(k, pp.w, gg.w, mm.w, vv.w);
+    };
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + stride < n4; i += 2 * stride) {
+        float4 pa = p4[i], pb = p4[i + stride];
+        const float4 ga = g4[i], gb = g4[i + stride];
+        float4 ma = m4[i], mb = m4[i + stride];
+        float4 va = v4[i], vb = v4[i + stride];
+        upd(pa, ga, ma, va);
+        upd(pb, gb, mb, vb);
+        p4[i] = pa; m4[i] = ma; v4[i] = va;
+        p4[i + stride] = pb; m4[i + stride] = mb; v4[i + stride] = vb;
+    }
+    if (i < n4) {
+        float4 pa = p4[i];
+        const float4 ga = g4[i];
+        float4 ma = m4[i], va = v4[i];
+        upd(pa, ga, ma, va);
+        p4[i] = pa; m4[i] = ma; v4[i] = va;
+    }
+    const int64_t t = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) adamw_elem(k, p[t], g[t], m[t], v[t]);
+}
+
+static inline bool aligned16(const void* a) { return ((uintptr_t)a & 15u) == 0; }
 
 // step += 1; coef = {lr / (1 - b1^step), sqrt(1 - b2^step)} in fp64 (as the host path)
 __global__ void k_adamw_coef(int* step, float lr, float beta1, float beta2, float* coef) {
@@ -106,6 +174,25 @@ __global__ void k_cast_bf16(const float* __restrict__ src, uint16_t* __restrict_
 static inline int grid_for(int64_t n, int cap) {
     int64_t b = (n + OPT_THREADS - 1) / OPT_THREADS;
     return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+static int g_adamw_vec = -1;  // -1: from VAETEB_ADAMW_SCALAR (unset: vector kernel when aligned)
+
+static void adamw_launch(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                         float eps, float wd, float step_size, float bc2_sqrt, const float* gscale, const float* coef,
+                         hipStream_t st) {
+    if (g_adamw_vec < 0) {
+        const char* e = getenv("VAETEB_ADAMW_SCALAR");
+        g_adamw_vec = (e && e[0] == '1') ? 0 : 1;
+    }
+    if (g_adamw_vec && aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v)) {
+        // ~2 float4 per thread and iteration, at most 2048 x 256 threads (8 per CU)
+        hipLaunchKernelGGL(k_adamw4, dim3(grid_for((n / 4 + 1) / 2, 2048)), dim3(OPT_THREADS), 0, st, p, g, m, v, n,
+                           lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
+    } else {
+        hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, st, p, g, m, v, n, lr, beta1,
+                           beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
+    }
 }
 
 }  // namespace vt
@@ -131,8 +218,8 @@ int vt_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float
     VT_CHECK_ARG(n > 0 && step >= 1, "vt_adamw_step: n=%lld step=%d", (long long)n, step);
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
-    hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, S(stream), p, g, m, v, n, lr, beta1,
-                       beta2, eps, weight_decay, (float)((double)lr / bc1), (float)sqrt(bc2), gscale, nullptr);
+    adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, (float)((double)lr / bc1), (float)sqrt(bc2),
+                 gscale, nullptr, S(stream));
     VT_LAUNCH_CHECK("vt_adamw_step");
     return VT_OK;
 }
@@ -141,9 +228,13 @@ int vt_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, f
                       float eps, float weight_decay, int* step, float* coef, const float* gscale, void* stream) {
     VT_CHECK_ARG(n > 0 && step && coef, "vt_adamw_step_dev: args");
     hipLaunchKernelGGL(k_adamw_coef, dim3(1), dim3(1), 0, S(stream), step, lr, beta1, beta2, coef);
-    hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, S(stream), p, g, m, v, n, lr, beta1,
-                       beta2, eps, weight_decay, 0.f, 1.f, gscale, coef);
+    adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, S(stream));
     VT_LAUNCH_CHECK("vt_adamw_step_dev");
+    return VT_OK;
+}
+
+int vt_adamw_set_vector(int on) {
+    g_adamw_vec = on ? 1 : 0;
     return VT_OK;
 }
 

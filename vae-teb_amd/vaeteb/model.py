@@ -30,6 +30,10 @@ MAX_SIDE = int(__import__("os").environ.get("VAETEB_MAX_SIDE_STREAMS", "3"))
 GRAD_SIDE = int(__import__("os").environ.get("VAETEB_GRAD_SIDE_STREAM", "3"))  # conv weight-gradient stream (measured: 3 < 2 < 1)
 HEAD_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_HEAD_GRAD_SIDE_STREAM", "1"))  # 0: inline
 LSTM_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_LSTM_GRAD_SIDE_STREAM", "0"))  # 0: inline (side streams measured no faster)
+# weight-only forward work (bf16 shadows, BatchNorm counters) on this side stream at the
+# start of a concurrent training forward; 0: in line (VAETEB_PREPASS=0)
+PREPASS = int(__import__("os").environ.get("VAETEB_PREPASS", "1"))
+PREPASS_SIDE = 3
 _SIDE = {}
 
 
@@ -317,7 +321,8 @@ class ConvBlock(nn.Module):
         y = ops.conv_bn_act(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                             mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
                             momentum=bn.momentum, eps=bn.eps, bf16=self.bf16)
-        bn.num_batches_tracked.add_(1)
+        if not getattr(bn, "_vt_batched", False):   # else counted by SeqVaeTeb in one launch
+            bn.num_batches_tracked.add_(1)
         return y
 
 
@@ -540,10 +545,41 @@ class SeqVaeTeb(nn.Module):
                                 else None)
         ops.LSTM_GRAD_STREAM = (side_stream(torch.cuda.current_device(), LSTM_GRAD_SIDE)
                                 if _PAR["on"] and LSTM_GRAD_SIDE > 0 else None)
+        if _PAR["on"] and self.training and PREPASS:
+            self._prepass()
         try:
             return self._forward(y_st, y_ph, x_ph, eps)
         finally:
             _PAR.update(prev)
+
+    def _bn_counters(self):
+        """The num_batches_tracked buffers of every BatchNorm as views of one int64
+        vector (state_dict keys and values unchanged), so a training forward counts
+        all 17 in one launch instead of one add per block.  Rebound whenever a
+        buffer was replaced (.to(), load_state_dict(assign=True))."""
+        bns = [m.bn_layer for m in self.modules() if isinstance(m, ConvBlock)]
+        flat = getattr(self, "_bn_flat", None)
+        if flat is None or len(flat) != len(bns) or any(
+                bn.num_batches_tracked.data_ptr() != flat[i].data_ptr() for i, bn in enumerate(bns)):
+            dev = bns[0].num_batches_tracked.device
+            flat = torch.stack([bn.num_batches_tracked.detach().to(dev) for bn in bns])
+            for i, bn in enumerate(bns):
+                bn._buffers["num_batches_tracked"] = flat[i]
+                bn._vt_batched = True
+            self._bn_flat = flat
+        return flat
+
+    def _prepass(self):
+        """Weight-only work of the forward on a side stream at its start: the bf16
+        shadows of the MFMA heads and bf16 convs, and the BatchNorm step counters
+        (ops.prepare_shadows)."""
+        heads = [m.weight for h in (self.decoder.output_mu, self.decoder.output_logvar)
+                 for m in h.modules() if isinstance(m, Linear) and m.mfma
+                 and ops.mfma_ok(m.in_features, m.out_features)]
+        convs = [m.conv.weight for m in self.modules() if isinstance(m, ConvBlock) and m.bf16]
+        flat = self._bn_counters()
+        ops.prepare_shadows(heads, convs, side_stream(torch.cuda.current_device(), PREPASS_SIDE),
+                            extra=lambda: flat.add_(1))
 
     def _forward(self, y_st, y_ph, x_ph, eps):
         (mu_y, logvar_y_full), mu_x = fork_lockstep(self.target_encoder.stages(y_st, y_ph),

@@ -101,9 +101,21 @@ def mfma_ok(K, N):
 
 
 _SHADOW = {}
+# Shadows written ahead by prepare_shadows(): key -> event recorded after them on the
+# prepass stream.  A forward that finds its weight here waits on the event instead of
+# rewriting the shadow on its own (critical-path) stream; each entry serves one use.
+_PREPARED = {}
 
 
-def _weight_shadow(w):
+def _take_prepared(key):
+    ev = _PREPARED.pop(key, None)
+    if ev is None:
+        return False
+    torch.cuda.current_stream().wait_event(ev)
+    return True
+
+
+def _weight_shadow(w, prepass=False):
     """bf16 images of an fp32 master weight W [N, K]: (W16 [N, K], W16t [K, N]),
     rewritten from W on every forward (the optimizer updates W in place)."""
     N, K = w.shape
@@ -113,8 +125,35 @@ def _weight_shadow(w):
         sh = (torch.empty((N, K), dtype=torch.bfloat16, device=w.device),
               torch.empty((K, N), dtype=torch.bfloat16, device=w.device))
         _SHADOW[key] = sh
-    call("vt_mfma_weight_shadow", ptr(w), N, K, ptr(sh[0]), ptr(sh[1]), _st())
+    if prepass or not _take_prepared(key):
+        call("vt_mfma_weight_shadow", ptr(w), N, K, ptr(sh[0]), ptr(sh[1]), _st())
     return sh
+
+
+def prepare_shadows(head_weights, conv_weights, stream, extra=None):
+    """Write the bf16 shadows of this forward's MFMA head weights and bf16 conv
+    weights on `stream` at the start of the forward (they depend only on the
+    weights, which change only in the optimizer step), off the activation chain;
+    the ops then wait on one event instead of shadowing in line.  extra(): more
+    weight-only work for the same stream (the BatchNorm step counters).  Same
+    kernels, same bits."""
+    _PREPARED.clear()
+    main = torch.cuda.current_stream()
+    stream.wait_stream(main)
+    keys = []
+    with torch.cuda.stream(stream):
+        for w in head_weights:
+            _weight_shadow(w, prepass=True)
+            keys.append((w.data_ptr(), *w.shape))
+        for w in conv_weights:
+            _conv_shadow(w, prepass=True)
+            keys.append((w.data_ptr(), *w.shape))
+        if extra is not None:
+            extra()
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    for k in keys:
+        _PREPARED[k] = ev
 
 
 class LinearF(torch.autograd.Function):
@@ -387,7 +426,7 @@ _CONV_WS = {}
 _CONV_SHADOW = {}
 
 
-def _conv_shadow(w):
+def _conv_shadow(w, prepass=False):
     """bf16 shadows of a conv weight W [Cout][Cin][K] (vt_conv1d_bf16_shadow):
     w16 [Cout][K][ceil32(Cin)] and the transposed / flipped w16t
     [Cin][K][ceil32(Cout)], rewritten from W on every forward."""
@@ -399,7 +438,8 @@ def _conv_shadow(w):
         sh = (torch.empty(Cout * K * up32(Cin), dtype=torch.bfloat16, device=w.device),
               torch.empty(Cin * K * up32(Cout), dtype=torch.bfloat16, device=w.device))
         _CONV_SHADOW[key] = sh
-    call("vt_conv1d_bf16_shadow", ptr(w), Cout, Cin, K, ptr(sh[0]), ptr(sh[1]), _st())
+    if prepass or not _take_prepared(key):
+        call("vt_conv1d_bf16_shadow", ptr(w), Cout, Cin, K, ptr(sh[0]), ptr(sh[1]), _st())
     return sh
 
 
