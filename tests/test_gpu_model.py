@@ -417,3 +417,39 @@ def test_native_executor_requires_eps(golden):
     tr = Trainer(det_fill_(SeqVaeTeb(sequence_length=16)).cuda(), lr=1e-3)
     with pytest.raises(ValueError):
         tr.capture(b0, native=True)
+
+
+@pytest.mark.parametrize("defer", [0, 1])
+def test_prepass_and_deferred_lstm_grads_bitwise(golden, monkeypatch, defer):
+    """bf16 heads / convs with the weight-only prepass (shadows + BatchNorm counters
+    ahead of the forward on a side stream) and the LSTM parameter gradients deferred
+    to a side stream: bit-identical losses, gradients and parameters to the serial
+    in-line run, and every BatchNorm counted exactly once per step."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb import model as MD, ops
+    from vaeteb.model import ConvBlock, SeqVaeTeb
+    from vaeteb.train import Trainer
+    monkeypatch.setattr(ops, "LSTM_GRAD_DEFER", defer)
+    g = golden("model_s16_b4")
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    res = []
+    for conc, prepass in ((False, 0), (True, 1), (True, 0)):
+        monkeypatch.setattr(MD, "PREPASS", prepass)
+        m = det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=conc, head_precision="bf16",
+                                conv_precision="bf16")).cuda()
+        tr = Trainer(m, lr=1e-3)
+        batch = {"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}
+        for i in range(3):
+            if i == 1:
+                m.prepass()   # ahead of the forward, as Trainer.loss does before the front-end
+            L = tr.step(batch, eps=T("eps"))
+        torch.cuda.synchronize()
+        counts = {int(mm.bn_layer.num_batches_tracked) for mm in m.modules() if isinstance(mm, ConvBlock)}
+        assert counts == {3}, counts
+        assert set(m.state_dict().keys()) == set(det_fill_(SeqVaeTeb(sequence_length=16)).state_dict().keys())
+        res.append((L["total_loss"].item(), tr.state.g.clone(), tr.state.p.clone()))
+    for r in res[1:]:
+        assert res[0][0] == r[0]
+        assert torch.equal(res[0][1], r[1]) and torch.equal(res[0][2], r[2])

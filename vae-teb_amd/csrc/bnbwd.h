@@ -28,11 +28,16 @@ __device__ __forceinline__ float bn_actd(float z, int act) {
         default: return 1.f;
     }
 }
-__device__ __forceinline__ float bn_bwd_val(float dy, float x, const float* p, int C, int c, int act, float invM) {
+// the same with the six parameters of channel c already in registers
+__device__ __forceinline__ float bn_bwd_val_r(float dy, float x, float mean, float rstd, float gam, float bet,
+                                              float dgam, float dbet, int act, float invM) {
 #pragma clang fp contract(off)
-    const float h = (x - p[c]) * p[C + c];
-    const float dz = dy * bn_actd(h * p[2 * C + c] + p[3 * C + c], act);
-    return p[2 * C + c] * p[C + c] * (dz - p[5 * C + c] * invM - h * p[4 * C + c] * invM);
+    const float h = (x - mean) * rstd;
+    const float dz = dy * bn_actd(h * gam + bet, act);
+    return gam * rstd * (dz - dbet * invM - h * dgam * invM);
+}
+__device__ __forceinline__ float bn_bwd_val(float dy, float x, const float* p, int C, int c, int act, float invM) {
+    return bn_bwd_val_r(dy, x, p[c], p[C + c], p[2 * C + c], p[3 * C + c], p[4 * C + c], p[5 * C + c], act, invM);
 }
 
 }  // namespace vt

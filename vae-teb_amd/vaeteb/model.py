@@ -29,7 +29,9 @@ _PAR = {"on": False, "next": 1}
 MAX_SIDE = int(__import__("os").environ.get("VAETEB_MAX_SIDE_STREAMS", "3"))
 GRAD_SIDE = int(__import__("os").environ.get("VAETEB_GRAD_SIDE_STREAM", "3"))  # conv weight-gradient stream (measured: 3 < 2 < 1)
 HEAD_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_HEAD_GRAD_SIDE_STREAM", "1"))  # 0: inline
-LSTM_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_LSTM_GRAD_SIDE_STREAM", "0"))  # 0: inline (side streams measured no faster)
+# LSTM parameter gradients (deferred after the recurrence chain, ops.LSTM_GRAD_DEFER) on this side
+# stream; 0: in line (per layer, without deferral, side streams measured no faster)
+LSTM_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_LSTM_GRAD_SIDE_STREAM", "3"))
 # weight-only forward work (bf16 shadows, BatchNorm counters) on this side stream at the
 # start of a concurrent training forward; 0: in line (VAETEB_PREPASS=0)
 PREPASS = int(__import__("os").environ.get("VAETEB_PREPASS", "1"))
@@ -544,42 +546,69 @@ class SeqVaeTeb(nn.Module):
                                 if _PAR["on"] and HEAD_GRAD_SIDE > 0 and not torch.cuda.is_current_stream_capturing()
                                 else None)
         ops.LSTM_GRAD_STREAM = (side_stream(torch.cuda.current_device(), LSTM_GRAD_SIDE)
-                                if _PAR["on"] and LSTM_GRAD_SIDE > 0 else None)
-        if _PAR["on"] and self.training and PREPASS:
+                                if _PAR["on"] and LSTM_GRAD_SIDE > 0 and not torch.cuda.is_current_stream_capturing()
+                                else None)
+        # (not under hipGraph capture: an extra side-stream branch at the start of the graph
+        # makes ROCm 7's hipStreamEndCapture segfault, as the head-gradient branch below)
+        if getattr(self, "_prepassed", False):
+            self._prepassed = False            # done ahead of this forward (prepass())
+        elif _PAR["on"] and self.training and PREPASS and not torch.cuda.is_current_stream_capturing():
             self._prepass()
+        else:
+            ops._PREPARED.clear()   # no stale shadow events outlive the forward they were made for
         try:
             return self._forward(y_st, y_ph, x_ph, eps)
         finally:
             _PAR.update(prev)
+            for bn in getattr(self, "_bn_list", ()):
+                bn._vt_batched = False   # counted by this forward's prepass only
 
     def _bn_counters(self):
         """The num_batches_tracked buffers of every BatchNorm as views of one int64
         vector (state_dict keys and values unchanged), so a training forward counts
         all 17 in one launch instead of one add per block.  Rebound whenever a
         buffer was replaced (.to(), load_state_dict(assign=True))."""
-        bns = [m.bn_layer for m in self.modules() if isinstance(m, ConvBlock)]
-        flat = getattr(self, "_bn_flat", None)
-        if flat is None or len(flat) != len(bns) or any(
-                bn.num_batches_tracked.data_ptr() != flat[i].data_ptr() for i, bn in enumerate(bns)):
+        bns = getattr(self, "_bn_list", None)
+        if bns is None:
+            bns = self._bn_list = [m.bn_layer for m in self.modules() if isinstance(m, ConvBlock)]
+        flat, views = getattr(self, "_bn_flat", None), getattr(self, "_bn_views", None)
+        if flat is None or len(views) != len(bns) or any(
+                bn._buffers["num_batches_tracked"] is not v for bn, v in zip(bns, views)):
             dev = bns[0].num_batches_tracked.device
             flat = torch.stack([bn.num_batches_tracked.detach().to(dev) for bn in bns])
-            for i, bn in enumerate(bns):
-                bn._buffers["num_batches_tracked"] = flat[i]
-                bn._vt_batched = True
-            self._bn_flat = flat
+            views = [flat[i] for i in range(len(bns))]
+            for bn, v in zip(bns, views):
+                bn._buffers["num_batches_tracked"] = v
+            self._bn_flat, self._bn_views = flat, views
         return flat
+
+    def prepass(self):
+        """Run the weight-only prepass now, ahead of the next training forward (the
+        trainer calls it before the front-end, so it overlaps that); the forward
+        then skips its own."""
+        if (self.concurrent_encoders and self.training and PREPASS and torch.cuda.is_available()
+                and next(self.parameters()).is_cuda and not torch.cuda.is_current_stream_capturing()):
+            self._prepass()
+            self._prepassed = True
 
     def _prepass(self):
         """Weight-only work of the forward on a side stream at its start: the bf16
         shadows of the MFMA heads and bf16 convs, and the BatchNorm step counters
         (ops.prepare_shadows)."""
-        heads = [m.weight for h in (self.decoder.output_mu, self.decoder.output_logvar)
-                 for m in h.modules() if isinstance(m, Linear) and m.mfma
-                 and ops.mfma_ok(m.in_features, m.out_features)]
-        convs = [m.conv.weight for m in self.modules() if isinstance(m, ConvBlock) and m.bf16]
+        key = (self.decoder.head_precision, self.conv_precision)
+        if getattr(self, "_prep_key", None) != key:   # module lists walked once per precision setting
+            self._prep_key = key
+            self._prep_heads = [m for h in (self.decoder.output_mu, self.decoder.output_logvar)
+                                for m in h.modules() if isinstance(m, Linear) and m.mfma
+                                and ops.mfma_ok(m.in_features, m.out_features)]
+            self._prep_convs = [m for m in self.modules() if isinstance(m, ConvBlock) and m.bf16]
+        heads = [m.weight for m in self._prep_heads]
+        convs = [m.conv.weight for m in self._prep_convs]
         flat = self._bn_counters()
         ops.prepare_shadows(heads, convs, side_stream(torch.cuda.current_device(), PREPASS_SIDE),
                             extra=lambda: flat.add_(1))
+        for bn in self._bn_list:
+            bn._vt_batched = True    # the blocks of the next forward skip their own count
 
     def _forward(self, y_st, y_ph, x_ph, eps):
         (mu_y, logvar_y_full), mu_x = fork_lockstep(self.target_encoder.stages(y_st, y_ph),

@@ -64,6 +64,9 @@ LSTM_GRAD_STREAM = None  # ... for the LSTM weight gradients (set by SeqVaeTeb)
 # LSTM input projections inside the recurrence kernels (vt_lstm_layer_{fwd,bwd}_x) for
 # input sizes <= 64; 0: separate skinny GEMMs (the same results bit for bit)
 LSTM_FUSED = int(os.environ.get("VAETEB_LSTM_FUSED", "1"))
+# LSTM parameter gradients (in-place sinks) issued after the whole backward recurrence
+# chain (on LSTM_GRAD_STREAM when set) instead of after each layer's recurrence
+LSTM_GRAD_DEFER = int(os.environ.get("VAETEB_LSTM_GRAD_DEFER", "1"))
 # bf16 conv backward-data written straight into dX where the fold is a crop; 0: gpad + fold
 CONV_DIRECT_DX = int(os.environ.get("VAETEB_CONV_DIRECT_DX", "1"))
 
@@ -131,29 +134,27 @@ def _weight_shadow(w, prepass=False):
 
 
 def prepare_shadows(head_weights, conv_weights, stream, extra=None):
-    """Write the bf16 shadows of this forward's MFMA head weights and bf16 conv
-    weights on `stream` at the start of the forward (they depend only on the
-    weights, which change only in the optimizer step), off the activation chain;
-    the ops then wait on one event instead of shadowing in line.  extra(): more
-    weight-only work for the same stream (the BatchNorm step counters).  Same
-    kernels, same bits."""
+    """Write the bf16 shadows of this forward's bf16 conv weights and MFMA head
+    weights on `stream` ahead of the forward (they depend only on the weights,
+    which change only in the optimizer step), off the activation chain; the ops
+    then wait on an event instead of shadowing in line (the convs' event first:
+    they are needed early, the 4096^2 heads late).  extra(): more weight-only work
+    for the same stream (the BatchNorm step counters).  Same kernels, same bits."""
     _PREPARED.clear()
     main = torch.cuda.current_stream()
     stream.wait_stream(main)
-    keys = []
     with torch.cuda.stream(stream):
-        for w in head_weights:
-            _weight_shadow(w, prepass=True)
-            keys.append((w.data_ptr(), *w.shape))
-        for w in conv_weights:
-            _conv_shadow(w, prepass=True)
-            keys.append((w.data_ptr(), *w.shape))
+        for group, fn in ((conv_weights, _conv_shadow), (head_weights, _weight_shadow)):
+            if not group:
+                continue
+            for w in group:
+                fn(w, prepass=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            for w in group:
+                _PREPARED[(w.data_ptr(), *w.shape)] = ev
         if extra is not None:
             extra()
-        ev = torch.cuda.Event()
-        ev.record(stream)
-    for k in keys:
-        _PREPARED[k] = ev
 
 
 class LinearF(torch.autograd.Function):
@@ -623,6 +624,7 @@ class LSTMF(torch.autograd.Function):
         dh = gy
         ws = WS.get(WS_LINEAR, gy.device, 1)
         gx = None
+        deferred = []
         for l in reversed(range(nl)):
             inp, hp, c, gates = saved[4 * l: 4 * l + 4]
             w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
@@ -642,20 +644,25 @@ class LSTMF(torch.autograd.Function):
             if LSTM_FUSED and In + H + 1 <= 144:
                 # every parameter gradient of the layer in one pass over dg
                 pg = _ParamGrads([w_ih, w_hh, b_ih, b_hh], [True] * 4)
-                side = LSTM_GRAD_STREAM if (pg.direct and LSTM_GRAD_STREAM is not None) else None
-                if side is not None and side != torch.cuda.current_stream():
-                    # off the layer-to-layer chain (in-place sinks; same kernels, same bits)
-                    side.wait_stream(torch.cuda.current_stream())
-                    with torch.cuda.stream(side):
-                        ws_s = WS.get(WS_LINEAR, gy.device, 1)
-                        call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
-                             *[ptr(t) for t in pg.out], pg.acc, ptr(ws_s), ws_s.numel(), _st())
-                    for t in (dg, inp, hp):
-                        t.record_stream(side)
+                if pg.direct and LSTM_GRAD_DEFER:
+                    # in-place sinks: issued after the last layer's recurrence (below), so
+                    # the layer-to-layer dh chain is not interrupted by them
+                    deferred.append((dg, inp, In, hp, pg))
                 else:
-                    call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
-                         *[ptr(t) for t in pg.out], pg.acc, ptr(ws), ws.numel(), _st())
-                grads[4 * l: 4 * l + 4] = pg.result()
+                    side = LSTM_GRAD_STREAM if (pg.direct and LSTM_GRAD_STREAM is not None) else None
+                    if side is not None and side != torch.cuda.current_stream():
+                        # off the layer-to-layer chain (in-place sinks; same kernels, same bits)
+                        side.wait_stream(torch.cuda.current_stream())
+                        with torch.cuda.stream(side):
+                            ws_s = WS.get(WS_LINEAR, gy.device, 1)
+                            call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                                 *[ptr(t) for t in pg.out], pg.acc, ptr(ws_s), ws_s.numel(), _st())
+                        for t in (dg, inp, hp):
+                            t.record_stream(side)
+                    else:
+                        call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                             *[ptr(t) for t in pg.out], pg.acc, ptr(ws), ws.numel(), _st())
+                    grads[4 * l: 4 * l + 4] = pg.result()
             else:
                 pw = _ParamGrads([w_ih, w_hh], [True, True])
                 # b_ih and b_hh receive the same gradient (the sum of dg over rows), written
@@ -688,6 +695,26 @@ class LSTMF(torch.autograd.Function):
             if need_dx:
                 dh = gin
                 gx = gin
+        if deferred:
+            # the layers' parameter gradients after the whole recurrence chain, on the
+            # weight-gradient side stream when there is one (joined before the bucket
+            # all-reduce / the end of the backward), else in line; same kernels and
+            # summation orders as in line per layer: the same bits
+            side = LSTM_GRAD_STREAM
+            cur = torch.cuda.current_stream()
+            on_side = side is not None and side != cur
+            if on_side:
+                side.wait_stream(cur)
+            with torch.cuda.stream(side if on_side else cur):
+                ws_d = WS.get(WS_LINEAR, gy.device, 1)
+                for dg, inp, In, hp, pg in deferred:
+                    call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                         *[ptr(t) for t in pg.out], pg.acc, ptr(ws_d), ws_d.numel(), _st())
+            for dg, inp, In, hp, pg in deferred:
+                if on_side:
+                    for t in (dg, inp, hp):
+                        t.record_stream(side)
+                pg.result()
         return (gx, *grads)
 
 

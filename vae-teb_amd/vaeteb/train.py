@@ -162,6 +162,8 @@ class Trainer:
         vae = getattr(self.model, "vae_model", self.model)   # SeqVaeTebClassifier (config 4) wraps the VAE
         labels = batch.get("labels") if hasattr(batch, "get") else None
         if "x" in batch:
+            if hasattr(vae, "prepass"):
+                vae.prepass()   # weight-only forward work on a side stream, overlapping the front-end
             side = None
             if getattr(vae, "concurrent_encoders", False) and batch["x"].is_cuda:
                 from .model import side_stream
