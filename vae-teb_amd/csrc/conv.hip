@@ -55,7 +55,7 @@ struct FwdCfg {
 // FLIP_T: taps W[ci][co][K-1-k] (transposed, flipped) instead of W[co][ci][k].
 template <int K, int NT, bool FLIP_T>
 // stats != null: also the BatchNorm statistics of this tile's outputs,
-// stats[tile][0][co] = sum_t y, stats[tile][1][co] = sum_t (y - tile mean)^2
+// stats[0][co][tile] = sum_t y, stats[1][co][tile] = sum_t (y - tile mean)^2 (channel-major)
 // (tile = b * gridDim.x + blockIdx.x), combined by k_bn_stats_finalize.
 __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ x, Geo g, const float* __restrict__ w,
                                                   float* __restrict__ y, int Lo, float* __restrict__ stats) {
@@ -209,9 +209,11 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ x, G
         __syncthreads();
         if (tid < TC && co0 + tid < g.Cout) {
             const int64_t tile = (int64_t)b * gridDim.x + blockIdx.x;
-            float* sp = stats + tile * 2 * g.Cout + co0 + tid;
+            // channel-major [2][Cout][tiles] (k_bn_stats_finalize reads a channel as one run)
+            const int64_t ntile = (int64_t)gridDim.z * gridDim.x;
+            float* sp = stats + (int64_t)(co0 + tid) * ntile + tile;
             sp[0] = ((red1[tid] + red1[TC + tid]) + red1[2 * TC + tid]) + red1[3 * TC + tid];
-            sp[g.Cout] = ((red2[tid] + red2[TC + tid]) + red2[2 * TC + tid]) + red2[3 * TC + tid];
+            sp[(int64_t)g.Cout * ntile] = ((red2[tid] + red2[TC + tid]) + red2[2 * TC + tid]) + red2[3 * TC + tid];
         }
     }
 }
@@ -228,8 +230,18 @@ __global__ __launch_bounds__(256) void k_bn_stats_finalize(const float* __restri
     const int c = blockIdx.x, tid = threadIdx.x;
     const int ntile = B * tiles_per_sample;
     const double M = (double)B * Lo;
+    const float* s0p = stats + (int64_t)c * ntile;        // channel-major [2][C][tiles]
+    const float* s1p = stats + (int64_t)(C + c) * ntile;
     double a = 0.0;
-    for (int i = tid; i < ntile; i += 256) a += (double)stats[(int64_t)i * 2 * C + c];
+    int i = tid;
+    for (; i + 768 < ntile; i += 1024) {   // four coalesced loads in flight, same order
+        float u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = s0p[i + 256 * k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a += (double)u[k];
+    }
+    for (; i < ntile; i += 256) a += (double)s0p[i];
     red[tid] = a;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
@@ -242,9 +254,9 @@ __global__ __launch_bounds__(256) void k_bn_stats_finalize(const float* __restri
     for (int i = tid; i < ntile; i += 256) {
         const int tx = i % tiles_per_sample;
         const int n = Lo - tx * TP < TP ? Lo - tx * TP : TP;
-        const double s1 = (double)stats[(int64_t)i * 2 * C + c];
+        const double s1 = (double)s0p[i];
         const double dm = s1 / n - mu;
-        q += (double)stats[(int64_t)i * 2 * C + C + c] + n * dm * dm;
+        q += (double)s1p[i] + n * dm * dm;
     }
     red[tid] = q;
     __syncthreads();

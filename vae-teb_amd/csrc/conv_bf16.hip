@@ -292,9 +292,11 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
         __syncthreads();
         if (tid < TC && co0 + tid < g.Cout) {
             const int64_t tile = (int64_t)b * gridDim.x + blockIdx.x;
-            float* sp = stats + tile * 2 * g.Cout + co0 + tid;
+            // channel-major [2][Cout][tiles] (k_bn_stats_finalize reads a channel as one run)
+            const int64_t ntile = (int64_t)gridDim.z * gridDim.x;
+            float* sp = stats + (int64_t)(co0 + tid) * ntile + tile;
             sp[0] = ((red1[tid] + red1[TC + tid]) + red1[2 * TC + tid]) + red1[3 * TC + tid];
-            sp[g.Cout] = ((red2[tid] + red2[TC + tid]) + red2[2 * TC + tid]) + red2[3 * TC + tid];
+            sp[(int64_t)g.Cout * ntile] = ((red2[tid] + red2[TC + tid]) + red2[2 * TC + tid]) + red2[3 * TC + tid];
         }
     }
 }

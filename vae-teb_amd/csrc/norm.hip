@@ -374,7 +374,9 @@ __global__ __launch_bounds__(NT) void k_reduce_parts(const float* __restrict__ p
 // ------------------------------------------------------------- BatchNorm
 // mode 0: mean[c] = S/M.  mode 1: var = S/M -> rstd, running stats update.
 // mode 2: dbeta = S0, dgamma = S1.
-// one workgroup per channel; double accumulation, fixed-order tree
+// one workgroup per channel; double accumulation, fixed-order tree.  part is
+// channel-major ([2][C][blocks], k_col_partial4): thread t sums blocks t, t + NT, ...
+// in that order with four coalesced loads in flight.
 __global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ part, int blocks, int C, int64_t M,
                                                     int mode, float eps, float momentum, float* __restrict__ mean,
                                                     float* __restrict__ rstd, float* __restrict__ run_mean,
@@ -387,9 +389,25 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ pa
     __shared__ double r0[NT], r1[NT];
     const int c = blockIdx.x;
     double a0 = 0.0, a1 = 0.0;
-    for (int b = threadIdx.x; b < blocks; b += NT) {
-        a0 += (double)part[(int64_t)b * 2 * C + c];
-        a1 += (double)part[(int64_t)b * 2 * C + C + c];
+    const float* p0 = part + (int64_t)c * blocks;
+    const float* p1 = part + (int64_t)(C + c) * blocks;
+    int b = threadIdx.x;
+    for (; b + 3 * NT < blocks; b += 4 * NT) {
+        float u[4], v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            u[k] = p0[b + k * NT];
+            v[k] = p1[b + k * NT];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            a0 += (double)u[k];
+            a1 += (double)v[k];
+        }
+    }
+    for (; b < blocks; b += NT) {
+        a0 += (double)p0[b];
+        a1 += (double)p1[b];
     }
     r0[threadIdx.x] = a0;
     r1[threadIdx.x] = a1;
@@ -625,8 +643,10 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
             s0 += red0[q * C + cc];
             s1 += red1[q * C + cc];
         }
-        part[(int64_t)blockIdx.x * 2 * C + cc] = s0;
-        part[(int64_t)blockIdx.x * 2 * C + C + cc] = s1;
+        // channel-major (part[k][c][block]): k_bn_finalize reads a channel's partials
+        // as one contiguous run
+        part[(int64_t)cc * gridDim.x + blockIdx.x] = s0;
+        part[(int64_t)(C + cc) * gridDim.x + blockIdx.x] = s1;
     }
 }
 
