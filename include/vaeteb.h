@@ -34,6 +34,14 @@ extern "C" {
 #define VT_FFT_MAX_LDS 8192 /* longest FFT held in one workgroup's LDS     */
 
 const char* vt_last_error(void);
+/* Stream `to` waits for the work enqueued on stream `from` so far (pooled event
+ * record + wait; hipGraph-capturable).  Host-side helper for the model's side-stream
+ * forks and joins (torch.cuda.Stream.wait_stream without a Python Event).        */
+int vt_stream_fork(void* from, void* to);
+/* The same in two halves: mark = record a pooled event on `stream` (its slot in
+ * *slot), wait_mark = `stream` waits for a marked point.                          */
+int vt_stream_mark(void* stream, int* slot);
+int vt_stream_wait_mark(void* stream, int slot);
 int vt_abi_version(void);
 
 /* ------------------------------------------------------------------ front-end

@@ -22,6 +22,9 @@ model = SeqVaeTeb(sequence_length=plan.S, scattering_channels=fe.C_st, phase_cha
                   mlp_precision="bf16", concurrent_encoders=True).to(dev)
 tr = Trainer(model, lr=1e-3, frontend=fe)
 x = torch.from_numpy(synthetic.batch(0, 256, 4096)).to(dev)
+if os.environ.get("SINGLE_THREAD_BACKWARD", "1") == "1":
+    # run the autograd backward on this thread, so cProfile sees the ops' backward functions
+    torch.autograd.set_multithreading_enabled(False)
 for _ in range(3):
     tr.step({"x": x})
 torch.cuda.synchronize()
@@ -32,5 +35,5 @@ for _ in range(5):
 pr.disable()
 torch.cuda.synchronize()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(45)
+st.sort_stats("tottime").print_stats(60)
 st.sort_stats("cumulative").print_stats(60)

@@ -105,3 +105,28 @@ def stream():
 
 def call(name, *args):
     return lib().call(name, *args)
+
+
+def wait_for(waiter, src=None):
+    """Stream `waiter` waits for the work enqueued so far on `src` (default: the
+    current stream) — torch's `waiter.wait_stream(src)` through the library's
+    pooled events (vt_stream_fork), without a Python Event per fork."""
+    w = waiter if isinstance(waiter, int) else waiter.cuda_stream
+    s = stream() if src is None else (src if isinstance(src, int) else src.cuda_stream)
+    if w != s:
+        rc = lib().fns["vt_stream_fork"](s, w)
+        if rc != 0:
+            raise RuntimeError(f"vt_stream_fork: {lib().last_error()}")
+
+
+def mark(src=None):
+    """A pooled event recorded on `src` (default: the current stream); see wait_mark."""
+    import ctypes
+    slot = ctypes.c_int()
+    call("vt_stream_mark", stream() if src is None else src.cuda_stream, ctypes.byref(slot))
+    return slot.value
+
+
+def wait_mark(slot, waiter=None):
+    """`waiter` (default: the current stream) waits for the point `mark` recorded."""
+    call("vt_stream_wait_mark", stream() if waiter is None else waiter.cuda_stream, slot)

@@ -16,7 +16,7 @@ import os
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 
 
 # ----------------------------------------------------------- stream forks
@@ -63,13 +63,13 @@ def fork(*thunks):
         # queue (a 5th stream would share one and serialise behind its work)
         st = side_stream(dev, min(_PAR["next"], MAX_SIDE))
         _PAR["next"] += 1
-        st.wait_stream(main)
+        _lib.wait_for(st, main)
         with torch.cuda.stream(st):
             outs[i] = t()
         sides.append(st)
     outs[0] = thunks[0]()
     for st in sides:
-        main.wait_stream(st)
+        _lib.wait_for(main, st)
     for o in outs[1:]:
         for t in (o if isinstance(o, (tuple, list)) else (o,)):
             if isinstance(t, torch.Tensor) and t.is_cuda:
@@ -114,7 +114,7 @@ def fork_lockstep(*gens, main_first=False):
     for _ in gens[1:]:
         st = side_stream(dev, min(_PAR["next"], MAX_SIDE))
         _PAR["next"] += 1
-        st.wait_stream(main)
+        _lib.wait_for(st, main)
         streams.append(st)
     outs = [None] * len(gens)
     live = list(range(len(gens) - 1, -1, -1))        # side branches first, as fork()
@@ -129,7 +129,7 @@ def fork_lockstep(*gens, main_first=False):
                     outs[i] = e.value
                     live.remove(i)
     for st in streams[1:]:
-        main.wait_stream(st)
+        _lib.wait_for(main, st)
     for o in outs[1:]:
         for t in (o if isinstance(o, (tuple, list)) else (o,)):
             if isinstance(t, torch.Tensor) and t.is_cuda:

@@ -111,10 +111,10 @@ _PREPARED = {}
 
 
 def _take_prepared(key):
-    ev = _PREPARED.pop(key, None)
-    if ev is None:
+    slot = _PREPARED.pop(key, None)
+    if slot is None:
         return False
-    torch.cuda.current_stream().wait_event(ev)
+    _lib.wait_mark(slot)
     return True
 
 
@@ -141,18 +141,16 @@ def prepare_shadows(head_weights, conv_weights, stream, extra=None):
     they are needed early, the 4096^2 heads late).  extra(): more weight-only work
     for the same stream (the BatchNorm step counters).  Same kernels, same bits."""
     _PREPARED.clear()
-    main = torch.cuda.current_stream()
-    stream.wait_stream(main)
+    _lib.wait_for(stream)
     with torch.cuda.stream(stream):
         for group, fn in ((conv_weights, _conv_shadow), (head_weights, _weight_shadow)):
             if not group:
                 continue
             for w in group:
                 fn(w, prepass=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
+            slot = _lib.mark(stream)
             for w in group:
-                _PREPARED[(w.data_ptr(), *w.shape)] = ev
+                _PREPARED[(w.data_ptr(), *w.shape)] = slot
         if extra is not None:
             extra()
 
@@ -207,10 +205,10 @@ class LinearF(torch.autograd.Function):
         if gw_t is not None:
             pre = "vt_mfma_" if ctx.mfma else "vt_"
             side = HEAD_GRAD_STREAM if (ctx.mfma and pg.direct and HEAD_GRAD_STREAM is not None) else None
-            if side is not None and side != torch.cuda.current_stream():
+            if side is not None and side.cuda_stream != _lib.stream():
                 # the decoder heads' 4096 x 4096 weight gradients are off the data-gradient
                 # chain: a side stream idle during the decoder backward (in-place sinks)
-                side.wait_stream(torch.cuda.current_stream())
+                _lib.wait_for(side)
                 with torch.cuda.stream(side):
                     ws_s = WS.get(WS_LINEAR, w.device, 1)
                     call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw_t), ptr(gb_t), pg.acc,
@@ -539,11 +537,11 @@ class ConvBNActF(torch.autograd.Function):
         pw = _ParamGrads([w], [ctx.needs_input_grad[1]])
         if pw.out[0] is not None:
             side = GRAD_STREAM if (pw.direct and GRAD_STREAM is not None) else None
-            if side is not None and side != torch.cuda.current_stream():
+            if side is not None and side.cuda_stream != _lib.stream():
                 # the weight gradient is off the data-gradient chain: compute it on a
                 # side stream (written in place into the flat gradient buffer, joined
                 # at the end of the backward / before a bucket's all-reduce)
-                side.wait_stream(torch.cuda.current_stream())
+                _lib.wait_for(side)
                 with torch.cuda.stream(side):
                     ws1 = WS.get(WS_LINEAR, x.device, 1)
                     call(fn, *dw_args(ws1))
@@ -650,9 +648,9 @@ class LSTMF(torch.autograd.Function):
                     deferred.append((dg, inp, In, hp, pg))
                 else:
                     side = LSTM_GRAD_STREAM if (pg.direct and LSTM_GRAD_STREAM is not None) else None
-                    if side is not None and side != torch.cuda.current_stream():
+                    if side is not None and side.cuda_stream != _lib.stream():
                         # off the layer-to-layer chain (in-place sinks; same kernels, same bits)
-                        side.wait_stream(torch.cuda.current_stream())
+                        _lib.wait_for(side)
                         with torch.cuda.stream(side):
                             ws_s = WS.get(WS_LINEAR, gy.device, 1)
                             call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
@@ -670,11 +668,11 @@ class LSTMF(torch.autograd.Function):
                 # a memcpy node would not survive the native step executor, csrc/stepgraph.cpp)
                 pb = _ParamGrads([b_ih, b_hh], [True, True])
                 side = LSTM_GRAD_STREAM if (pw.direct and LSTM_GRAD_STREAM is not None) else None
-                if side is not None and side != torch.cuda.current_stream():
+                if side is not None and side.cuda_stream != _lib.stream():
                     # weight gradients (in-place sinks) off the recurrence chain on a side
                     # stream; the returned bias gradient stays here (same kernels and
                     # summation orders as the serial branch below: bitwise equal)
-                    side.wait_stream(torch.cuda.current_stream())
+                    _lib.wait_for(side)
                     with torch.cuda.stream(side):
                         ws_s = WS.get(WS_LINEAR, gy.device, 1)
                         call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
@@ -701,11 +699,10 @@ class LSTMF(torch.autograd.Function):
             # all-reduce / the end of the backward), else in line; same kernels and
             # summation orders as in line per layer: the same bits
             side = LSTM_GRAD_STREAM
-            cur = torch.cuda.current_stream()
-            on_side = side is not None and side != cur
+            on_side = side is not None and side.cuda_stream != _lib.stream()
             if on_side:
-                side.wait_stream(cur)
-            with torch.cuda.stream(side if on_side else cur):
+                _lib.wait_for(side)
+            with torch.cuda.stream(side if on_side else torch.cuda.current_stream()):
                 ws_d = WS.get(WS_LINEAR, gy.device, 1)
                 for dg, inp, In, hp, pg in deferred:
                     call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,

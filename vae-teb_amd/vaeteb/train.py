@@ -19,6 +19,9 @@ import torch.distributed as dist
 
 from . import _lib
 
+# run the autograd backward on the calling thread (host-cost A/B switch)
+BWD_SAME_THREAD = int(os.environ.get("VAETEB_BWD_SAME_THREAD", "0"))
+
 
 class FlatState:
     """Flat parameter / gradient / moment storage for a module's parameters.
@@ -202,21 +205,25 @@ class Trainer:
             # stream the step never forked to would otherwise be joined at the end
             # from outside the capture
             from . import ops
-            main = torch.cuda.current_stream()
             for st in ops.SIDE_STREAMS:
-                st.wait_stream(main)
+                _lib.wait_for(st)
         if self.buckets:
             self.buckets.reset()
             self.buckets.enabled = overlap_comm
         losses = self.loss(batch, eps)
-        losses["total_loss"].backward()
+        if BWD_SAME_THREAD:
+            # the backward on this thread instead of autograd's device worker thread
+            with torch.autograd.set_multithreading_enabled(False):
+                losses["total_loss"].backward()
+        else:
+            losses["total_loss"].backward()
         if torch.cuda.is_available():
             # gradients written in place on side streams (no AccumulateGrad, so
             # autograd does not join those streams for us)
             from . import ops
-            main = torch.cuda.current_stream()
+            cur = _lib.stream()
             for st in ops.SIDE_STREAMS:
-                main.wait_stream(st)
+                _lib.wait_for(cur, st)
         # detached: a returned loss must not keep this step's autograd graph (and
         # with it the parameters' AccumulateGrad nodes, bound to this step's
         # stream) alive into the next step or a hipGraph capture
