@@ -19,8 +19,9 @@ import torch.distributed as dist
 
 from . import _lib
 
-# run the autograd backward on the calling thread (host-cost A/B switch)
-BWD_SAME_THREAD = int(os.environ.get("VAETEB_BWD_SAME_THREAD", "0"))
+# run the autograd backward on the calling thread instead of autograd's device worker thread
+# (measured: ~1 ms/step less host enqueue; 0 = torch default)
+BWD_SAME_THREAD = int(os.environ.get("VAETEB_BWD_SAME_THREAD", "1"))
 
 
 class FlatState:
