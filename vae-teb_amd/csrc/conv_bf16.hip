@@ -75,14 +75,8 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
     const int t0 = blockIdx.x * TP, co0 = blockIdx.y * TC, b = blockIdx.z;
     const float* xb = x + (int64_t)b * g.L_in * g.Cin;
     float* bp = reinterpret_cast<float*>(reinterpret_cast<char*>(lb) + C::LDS_BYTES);  // BNB: 6 x Cin params
-    // BNB: the 6 parameter rows in LDS at stride CP = ceil8(Cin), zero past Cin, so a
-    // thread reads its octet's 8 channels of each row as two float4 once per chunk
-    const int CP = (g.Cin + 7) & ~7;
     if constexpr (BNB) {
-        for (int i = tid; i < 6 * CP; i += 256) {
-            const int k = i / CP, c = i - k * CP;
-            bp[i] = c < g.Cin ? bnp[k * g.Cin + c] : 0.f;
-        }
+        for (int i = tid; i < 6 * g.Cin; i += 256) bp[i] = bnp[i];
         __syncthreads();
     }
     const float* x2b = BNB ? x2 + (int64_t)b * g.L_in * g.Cin : nullptr;
@@ -92,18 +86,6 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int c0 = 0; c0 < g.Cin; c0 += CB) {
-        // BNB: this thread's octet of channels is c0 + 8 (tid & 3) in every staging item
-        float pr[BNB ? 6 : 1][BNB ? 8 : 1];
-        if constexpr (BNB) {
-            const int cbt = c0 + 8 * (tid & 3);
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const float4 lo = cbt < CP ? *reinterpret_cast<const float4*>(bp + k * CP + cbt) : float4{0.f, 0.f, 0.f, 0.f};
-                const float4 hi = cbt < CP ? *reinterpret_cast<const float4*>(bp + k * CP + cbt + 4) : float4{0.f, 0.f, 0.f, 0.f};
-                pr[k][0] = lo.x; pr[k][1] = lo.y; pr[k][2] = lo.z; pr[k][3] = lo.w;
-                pr[k][4] = hi.x; pr[k][5] = hi.y; pr[k][6] = hi.z; pr[k][7] = hi.w;
-            }
-        }
         if constexpr (K <= 3) {
             // small K (few taps, little MFMA work per staged row): the per-element staging
             // keeps the register count, and with it the occupancy, low (measured faster)
@@ -118,9 +100,8 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const int c = cb + j;
-                        v[j] = (in && c < g.Cin) ? bn_bwd_val_r(xb[(int64_t)t * g.Cin + c], x2b[(int64_t)t * g.Cin + c],
-                                                                 pr[0][j], pr[1][j], pr[2][j], pr[3][j], pr[4][j],
-                                                                 pr[5][j], act, invM)
+                        v[j] = (in && c < g.Cin) ? bn_bwd_val(xb[(int64_t)t * g.Cin + c], x2b[(int64_t)t * g.Cin + c],
+                                                               bp, g.Cin, c, act, invM)
                                                  : 0.f;
                     }
                     if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
@@ -181,10 +162,10 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
                         xq[j] = x2b[ro + c];
                     }
     #pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        v[it][j] = (in && cb + j < g.Cin) ? bn_bwd_val_r(xa[j], xq[j], pr[0][j], pr[1][j], pr[2][j],
-                                                                         pr[3][j], pr[4][j], pr[5][j], act, invM)
-                                                          : 0.f;
+                    for (int j = 0; j < 8; ++j) {
+                        const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
+                        v[it][j] = (in && cb + j < g.Cin) ? bn_bwd_val(xa[j], xq[j], bp, g.Cin, c, act, invM) : 0.f;
+                    }
                     if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
                         const int cpad = (g.Cin + 7) & ~7;   // cb < Cin and cb % 8 == 0: the octet fits the padded row
                         *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v[it]);
@@ -508,8 +489,7 @@ int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, 
     using C = BCfg<K, NT>;
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
     if (x && bn)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT, true>), grid, dim3(256), C::LDS_BYTES + 24 * ((g.Cin + 7) & ~7), st,
-                           x, g, w16,
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
                            cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo);
     else if (x)
         hipLaunchKernelGGL((k_conv_bf16<K, NT>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y, Lo, stats,
