@@ -14,6 +14,8 @@
 //             contiguous row range through LDS and its 8 waves own the
 //             16x16 (n, k) tile pairs (db as an extra ones-column of X);
 //             per-workgroup slabs are summed in fixed order (k_sk_sum).
+#include <stdlib.h>
+
 #include "common.h"
 #include "skinny.h"
 
@@ -392,9 +394,16 @@ static void sk_dw_k(int NTK, dim3 grid, hipStream_t st, const float* dY, const f
 #undef VT_DWK
 }
 
+static int g_sk_dw_cap = 0;   // workgroup cap of k_sk_dw (VAETEB_SKDW_BLOCKS, default 256)
+
 int64_t sk_dw_blocks(int64_t R) {
-    int64_t blocks = (R + 255) / 256;  // >= 256 rows each, at most one workgroup per CU
-    return blocks > 256 ? 256 : (blocks < 1 ? 1 : blocks);
+    if (g_sk_dw_cap == 0) {
+        const char* e = getenv("VAETEB_SKDW_BLOCKS");
+        g_sk_dw_cap = e ? atoi(e) : 256;
+        if (g_sk_dw_cap < 1) g_sk_dw_cap = 256;
+    }
+    int64_t blocks = (R + 255) / 256;  // >= 256 rows each, at most g_sk_dw_cap workgroups
+    return blocks > g_sk_dw_cap ? g_sk_dw_cap : (blocks < 1 ? 1 : blocks);
 }
 
 int64_t sk_dw_workspace(int64_t R, int N, int K) { return sk_dw_blocks(R) * N * (K + 1); }

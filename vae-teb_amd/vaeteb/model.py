@@ -33,9 +33,9 @@ HEAD_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_HEAD_GRAD_SIDE_STREAM"
 # stream; 0: in line after the chain (measured fastest: GPU-only step 10.22 vs 10.42 ms on stream 3
 # and 10.45 ms per layer in line)
 LSTM_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_LSTM_GRAD_SIDE_STREAM", "0"))
-# weight-only forward work (bf16 shadows, BatchNorm counters) on this side stream at the
-# start of a concurrent training forward; 0: in line (VAETEB_PREPASS=0)
-PREPASS = int(__import__("os").environ.get("VAETEB_PREPASS", "1"))
+# weight-only forward work (bf16 shadows, BatchNorm counters) on this side stream ahead of a
+# concurrent training forward; 0 (default): shadows in line, counters in one launch
+PREPASS = int(__import__("os").environ.get("VAETEB_PREPASS", "0"))   # measured: GPU-neutral, +1 ms host
 PREPASS_SIDE = 3
 _SIDE = {}
 
@@ -557,6 +557,8 @@ class SeqVaeTeb(nn.Module):
             self._prepass()
         else:
             ops._PREPARED.clear()   # no stale shadow events outlive the forward they were made for
+            if self.training:
+                self._count_bn()
         try:
             return self._forward(y_st, y_ph, x_ph, eps)
         finally:
@@ -582,6 +584,12 @@ class SeqVaeTeb(nn.Module):
                 bn._buffers["num_batches_tracked"] = v
             self._bn_flat, self._bn_views = flat, views
         return flat
+
+    def _count_bn(self):
+        """All BatchNorm step counters of this training forward in one launch."""
+        self._bn_counters().add_(1)
+        for bn in self._bn_list:
+            bn._vt_batched = True    # the blocks of this forward skip their own count
 
     def prepass(self):
         """Run the weight-only prepass now, ahead of the next training forward (the
