@@ -440,53 +440,30 @@ __global__ __launch_bounds__(G4) __attribute__((amdgpu_waves_per_eu(2))) void k_
     for (int mm = 0; mm < NM; ++mm) acc[mm / KS] = mfma4(xs[0][lr * XSS + 4 * (mm % KS) + lc], wf[mm / KS][mm % KS], acc[mm / KS]);
     publish();
     int cb = 1;  // buffer holding the next chunk's input
-    // The next chunk's projection is spread over the TS steps in (k-step s, gate g)
-    // order with g fastest (mm = 4 s + g): a step's MFMAs feed distinct accumulators
-    // (no dependent MFMA blocks the step's issue) and share one A operand, which is
-    // read from LDS one step ahead (no LDS round trip between a step's barrier and
-    // its h reads).  Each accumulator still sums its k-steps in increasing order
-    // from zero: the same bits as the skinny GEMM.
-    constexpr int MPS = (NM + TS - 1) / TS;  // MFMAs per step (at most)
-    float xa[MPS];
-    auto xa_load = [&](const float* xn, int i) {
-#pragma unroll
-        for (int e = 0; e < MPS; ++e) {
-            const int mm = i * NM / TS + e;
-            if (mm < (i + 1) * NM / TS) xa[e] = xn[lr * XSS + 4 * (mm >> 2) + lc];
-        }
-    };
     for (int t0 = 0; t0 < S; t0 += TS) {
         const int n = S - t0 < TS ? S - t0 : TS;
         const bool more = t0 + TS < S;
         const float* xn = xs[cb];
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (more) xa_load(xn, 0);
+        // the next chunk's projection, a few MFMAs behind each step's barrier (measured:
+        // as fast as, or faster than, interleaving them into the step's FMA chain or
+        // issuing all of them at the chunk's end)
 #pragma unroll
         for (int i = 0; i < TS; ++i) {
             if (i >= n) continue;  // block-uniform
             const float* hq = hbuf[i & 1] + 20 * q;
-            float4 hv[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) hv[m] = *reinterpret_cast<const float4*>(&hq[4 * m]);
             const float xv = og[i * G4 + row] + bias;
-            if (more) {
-#pragma unroll
-                for (int e = 0; e < MPS; ++e) {
-                    const int mm = i * NM / TS + e;
-                    if (mm < (i + 1) * NM / TS) acc[mm & 3] = mfma4(xa[e], wf[mm & 3][mm >> 2], acc[mm & 3]);
-                }
-                if (i + 1 < TS) xa_load(xn, i + 1);
-            }
             f2 a[4];
 #pragma unroll
             for (int g = 0; g < 4; ++g) a[g] = f2{g == q ? xv : 0.f, 0.f};
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
+                const float4 hv = *reinterpret_cast<const float4*>(&hq[4 * m]);
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    a[g] = __builtin_elementwise_fma(w[g][2 * m], f2{hv[m].x, hv[m].y}, a[g]);
-                    a[g] = __builtin_elementwise_fma(w[g][2 * m + 1], f2{hv[m].z, hv[m].w}, a[g]);
+                    a[g] = __builtin_elementwise_fma(w[g][2 * m], f2{hv.x, hv.y}, a[g]);
+                    a[g] = __builtin_elementwise_fma(w[g][2 * m + 1], f2{hv.z, hv.w}, a[g]);
                 }
             }
             const float pi = quad_sum(a[0].x + a[0].y), pf = quad_sum(a[1].x + a[1].y);
@@ -503,6 +480,11 @@ __global__ __launch_bounds__(G4) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 oc[i * H + u] = c;
             }
             lds_barrier();
+            if (more) {
+#pragma unroll
+                for (int mm = i * NM / TS; mm < (i + 1) * NM / TS; ++mm)
+                    acc[mm / KS] = mfma4(xn[lr * XSS + 4 * (mm % KS) + lc], wf[mm / KS][mm % KS], acc[mm / KS]);
+            }
         }
         for (int idx = j; idx < n * G4; idx += G4) gt[(int64_t)t0 * G4 + idx] = og[idx];
         for (int idx = j; idx < n * H; idx += G4) {

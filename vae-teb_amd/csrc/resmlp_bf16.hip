@@ -541,6 +541,27 @@ __device__ void stage_wt(const BG& G, __bf16* img) {
     }
 }
 
+// lane l of a 16-lane row receives lane l ^ M's value (M = 1, 2, 4, 8) by DPP: the
+// same value as __shfl_xor(v, M) (ds_bpermute through the LDS crossbar) without an
+// LDS round trip.  M = 4 writes the two bank pairs of the row in two moves.
+template <int M>
+__device__ __forceinline__ float xshfl(float v) {
+    const int x = __builtin_bit_cast(int, v);
+    int r;
+    if constexpr (M == 1) {
+        r = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    } else if constexpr (M == 2) {
+        r = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    } else if constexpr (M == 4) {
+        r = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xF, 0x5, false);   // row_shl:4 into banks 0, 2
+        r = __builtin_amdgcn_update_dpp(r, x, 0x114, 0xF, 0xA, false);   // row_shr:4 into banks 1, 3
+    } else {
+        static_assert(M == 8, "xshfl: M in {1, 2, 4, 8}");
+        r = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);   // row_ror:8
+    }
+    return __builtin_bit_cast(float, r);
+}
+
 // LayerNorm(+act) backward of a transposed tile (fp32): dh -> dz in place
 // (xv = xhat, 0 past C and for invalid rows; rstd 0 for invalid rows); adds the
 // tile's gamma / beta column sums (over its 16 rows) to la[t]: lane (g, r)
@@ -581,11 +602,11 @@ __device__ __forceinline__ void ln_bwd(f32x4 (&dh)[NT], const f32x4 (&xv)[NT], f
         float q4[4], q2[2];
         const bool h8 = lr & 8, h4 = lr & 4, h2 = lr & 2;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) q4[i] = (h8 ? pq[4 + i] : pq[i]) + __shfl_xor(h8 ? pq[i] : pq[4 + i], 8);
+        for (int i = 0; i < 4; ++i) q4[i] = (h8 ? pq[4 + i] : pq[i]) + xshfl<8>(h8 ? pq[i] : pq[4 + i]);
 #pragma unroll
         for (int i = 0; i < 2; ++i) q2[i] = (h4 ? q4[2 + i] : q4[i]) + __shfl_xor(h4 ? q4[i] : q4[2 + i], 4);
-        float q = (h2 ? q2[1] : q2[0]) + __shfl_xor(h2 ? q2[0] : q2[1], 2);
-        q += __shfl_xor(q, 1);
+        float q = (h2 ? q2[1] : q2[0]) + xshfl<2>(h2 ? q2[0] : q2[1]);
+        q += xshfl<1>(q);
         la[t] += q;
     }
     const float m1 = sum_groups(s1) * invC, m2 = sum_groups(s2) * invC;
@@ -630,10 +651,10 @@ __device__ __forceinline__ void colsum(const f32x4 (&z)[NT], int C, float (&lb)[
         if (t >= nt) continue;
         float w[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) w[i] = (h8 ? z[t][2 + i] : z[t][i]) + __shfl_xor(h8 ? z[t][i] : z[t][2 + i], 8);
+        for (int i = 0; i < 2; ++i) w[i] = (h8 ? z[t][2 + i] : z[t][i]) + xshfl<8>(h8 ? z[t][i] : z[t][2 + i]);
         float q = (h4 ? w[1] : w[0]) + __shfl_xor(h4 ? w[0] : w[1], 4);
-        q += __shfl_xor(q, 2);
-        q += __shfl_xor(q, 1);
+        q += xshfl<2>(q);
+        q += xshfl<1>(q);
         lb[t] += q;
     }
 }
