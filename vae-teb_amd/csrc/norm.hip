@@ -224,11 +224,21 @@ __global__ __launch_bounds__(NT) void k_ln_bwd_wide(const float* __restrict__ dy
 // 16 lanes per row (4 rows per wave, 16 per workgroup), lane l owns columns
 // l&15 + 16 j: the 64-wide ResidualMLP rows of 256 B are covered by one
 // instruction for 4 rows at once instead of a whole wave per row.
+// butterfly sum over a row's 16 lanes, v + lane (l ^ m) for m = 1, 2, 4, 8 — the same
+// values as the __shfl_xor(., m, 16) chain, with DPP moves instead of ds_bpermute.
+// xor 4: the row rotated by 4 and by 12, both moved with every lane active (a DPP
+// under a divergent branch would read inactive source lanes), then selected by lane bit 2
+// (bit 2 clear: lane l + 4 = rotation by 12; set: lane l - 4 = rotation by 4).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float sum16(float v) {
-    v += __shfl_xor(v, 1, 16);
-    v += __shfl_xor(v, 2, 16);
-    v += __shfl_xor(v, 4, 16);
-    v += __shfl_xor(v, 8, 16);
+    v += dppf<0xB1>(v);                        // quad_perm [1,0,3,2]: l ^ 1
+    v += dppf<0x4E>(v);                        // quad_perm [2,3,0,1]: l ^ 2
+    const float r4 = dppf<0x124>(v), r12 = dppf<0x12C>(v);
+    v += (threadIdx.x & 4) ? r4 : r12;         // row_ror:N reads lane (l - N) mod 16: l ^ 4
+    v += dppf<0x128>(v);                       // row_ror 8: l ^ 8
     return v;
 }
 
