@@ -393,6 +393,28 @@ int vt_batchnorm_bwd_coef(const float* dy, const float* x, int64_t M, int C, con
  *           ref/model/inception_time.py:77,:139 (validation, frozen VAE, predict) */
 int vt_batchnorm_eval(const float* x, int64_t M, int C, const float* run_mean, const float* run_var, float eps,
                       const float* gamma, const float* beta, int act, float* y, void* stream);
+/* Synchronised train-mode BatchNorm, split at its cross-rank exchange points (the
+ * caller all-reduces `sums` (SUM) between the launches; no host synchronisation).
+ * replaces: torch.nn.SyncBatchNorm, which Lightning's sync_batchnorm=True substitutes for
+ *           the 17 BatchNorm1d on more than one GPU (ref/model/graph_model.py:517).
+ * vt_syncbn_sums: sums = [S0 | S1] (2 x C doubles) + the local row count at [2C];
+ *   which 0: S0 = sum x;  which 1: S0 = sum (x - mean)^2;  which 2 (backward, dy given):
+ *   S0 = sum dz, S1 = sum dz xhat, dz = dy act'(xhat gamma + beta).  ws: as vt_batchnorm_fwd.
+ * vt_syncbn_stats (on the all-reduced sums): which 0: mean;  which 1: rstd + running
+ *   statistics (unbiased with the global count);  which 2 (on the LOCAL sums, before the
+ *   all-reduce): dbeta / dgamma (+)= S0 / S1 (this rank's parameter gradients).
+ * vt_batchnorm_apply: y = act((x - mean) rstd gamma + beta).
+ * vt_syncbn_bwd_dx: dx from the all-reduced backward sums; ws: 2 x C floats.           */
+int vt_syncbn_sums(const float* x, const float* dy, int64_t M, int C, int which, const float* mean,
+                   const float* rstd, const float* gamma, const float* beta, int act, double* sums, float* ws,
+                   int64_t ws_floats, void* stream);
+int vt_syncbn_stats(const double* sums, int C, int which, float eps, float momentum, float* mean, float* rstd,
+                    float* run_mean, float* run_var, float* dgamma, float* dbeta, int accumulate, void* stream);
+int vt_batchnorm_apply(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
+                       const float* beta, int act, float* y, void* stream);
+int vt_syncbn_bwd_dx(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, int act, const double* sums, float* dx, float* ws,
+                     void* stream);
 int vt_act_fwd(const float* x, int64_t n, int act, float* y, void* stream);
 int vt_act_bwd(const float* dy, const float* x, int64_t n, int act, float* dx, void* stream);
 

@@ -92,9 +92,9 @@ def _wrap(m):
 
 
 class SourceEnc(nn.Module):
-    def __init__(self):
+    def __init__(self, cin=130):
         super().__init__()
-        self.mlp = ResMLP(130, geometric(130, 32, 5), final_act=False)
+        self.mlp = ResMLP(cin, geometric(130, 32, 5), final_act=False)
         self.conv = nn.Sequential(*[CausalBlock(32, k) for k in (3, 5, 7)])
         self.fused_norm = nn.LayerNorm(32)
         self.lstm_norm = nn.LayerNorm(64)
@@ -109,10 +109,10 @@ class SourceEnc(nn.Module):
 
 
 class TargetEnc(nn.Module):
-    def __init__(self):
+    def __init__(self, c_st=43, c_ph=44):
         super().__init__()
-        self.mlp_scattering = _wrap(ResMLP(43, geometric(43, 16, 4), final_act=False, act="gelu"))
-        self.mlp_phase = ResMLP(44, geometric(44, 16, 4), final_act=False)
+        self.mlp_scattering = _wrap(ResMLP(c_st, geometric(43, 16, 4), final_act=False, act="gelu"))
+        self.mlp_phase = ResMLP(c_ph, geometric(44, 16, 4), final_act=False)
         self.conv_scattering = nn.Sequential(*[CausalBlock(16, k) for k in (3, 5, 7)])
         self.conv_phase = nn.Sequential(*[CausalBlock(16, k) for k in (3, 5, 7)])
         self.scatter_fused_norm = nn.LayerNorm(16)
@@ -166,10 +166,14 @@ def kld(mp, lp, mq, lq):
 
 
 class SeqVaeTebRef(nn.Module):
-    def __init__(self, sequence_length=300):
+    """Encoder input widths are parameters (the reference hard-codes 43 / 44 / 130 at
+    ref/model/vae_teb_model.py:429,438,613; the hidden schedules keep those anchors, as
+    the HIP model does), so the literal J=6 Q=1 front-end (8 / 13 / 7) has an oracle."""
+
+    def __init__(self, sequence_length=300, scattering_channels=43, phase_channels=44, cross_phase_channels=130):
         super().__init__()
-        self.source_encoder = SourceEnc()
-        self.target_encoder = TargetEnc()
+        self.source_encoder = SourceEnc(cross_phase_channels)
+        self.target_encoder = TargetEnc(scattering_channels, phase_channels)
         self.conditional_encoder = CondEnc()
         self.decoder = Dec(16 * sequence_length)
 
@@ -183,6 +187,19 @@ class SeqVaeTebRef(nn.Module):
         lin, mu, lvr = self.decoder(z)
         return dict(z=z, linear_output=lin, mu_pr=mu, logvar_pr=lvr, mu_prior=my, logvar_prior=lvp,
                     mu_post=mq, logvar_post=lq)
+
+    def measure_transfer_entropy(self, y_st, y_ph, x_ph, reduce_mean=False):
+        """ref/model/vae_teb_model.py:1194-1226: eval mode (left set), no grad, KL(q || p)
+        elementwise (B, S, 32) or the mean of its latent sums."""
+        self.eval()
+        with torch.no_grad():
+            mx = self.source_encoder(x_ph)
+            my, lv = self.target_encoder(y_st, y_ph)
+            lvp, c = torch.split(lv, 32, -1)
+            mq, lq = self.conditional_encoder(mx, c)
+            mq = mq + my
+            k = 0.5 * (lvp - lq - 1 + (lq.exp() + (mq - my) ** 2) / lvp.exp())
+        return k.sum(-1).mean() if reduce_mean else k
 
     @staticmethod
     def compute_loss(fw, y_st, y_ph, y_raw, beta=1.0):

@@ -232,6 +232,32 @@ def test_model_step_vs_reference_golden(golden, name):
         assert rel(sd[k], torch.from_numpy(g[f"bn_{i}"])) < 1e-5, k
 
 
+@pytest.mark.parametrize("concurrent", [False, True])
+def test_measure_transfer_entropy_vs_reference_golden(golden, concurrent):
+    """SeqVaeTeb.measure_transfer_entropy (ref/model/vae_teb_model.py:1194-1226): after
+    one train-mode forward (running statistics updated), eval-mode BatchNorm, no
+    gradients; elementwise KL (B, S, 32) and its mean vs the reference, model left in
+    eval mode."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g, t = golden("model_s16_b4"), golden("te_s16_b4")
+    m = _load_model(16)
+    m.concurrent_encoders = concurrent
+    m.train()
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    with torch.no_grad():
+        m(T("y_st"), T("y_ph"), T("x_ph"), eps=T("eps"))
+    sd = m.state_dict()
+    for i, k in enumerate(list(t["bn_names"])):
+        if not k.startswith("decoder."):   # the decoder's statistics depend on the reference's random eps
+            assert rel(sd[k], torch.from_numpy(t[f"bn_{i}"])) < 1e-5, k
+    te = m.measure_transfer_entropy(T("y_st"), T("y_ph"), T("x_ph"))
+    assert not m.training and te.shape == (4, 16, 32) and not te.requires_grad
+    assert rel(te, torch.from_numpy(t["te"])) < 5e-5
+    te_mean = m.measure_transfer_entropy(T("y_st"), T("y_ph"), T("x_ph"), reduce_mean=True)
+    assert abs(te_mean.item() - float(t["te_mean"])) <= 5e-5 * abs(float(t["te_mean"]))
+
+
 def test_tiny_c1_vs_reference_golden(golden):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

@@ -113,12 +113,33 @@ def test_model_step(golden, name):
                                     T("eps"), float(g["beta"]))
     for k in ("total_loss", "nll_loss", "kld_loss", "mse_loss"):
         assert abs(L[k].item() - float(g["loss_" + k])) <= 1e-6 * abs(float(g["loss_" + k])) + 1e-7
-    gl2 = np.array([grads[k].norm().item() for k in names])
+    gl2 = np.array([grads[k].double().norm().item() for k in names])
     assert np.allclose(gl2, g["grad_l2"], rtol=1e-5, atol=1e-9)
+    for i, k in enumerate(names):
+        if f"grad_{i}" in g.files:
+            assert np.allclose(grads[k].numpy(), g[f"grad_{i}"], rtol=1e-5, atol=1e-7), k
+        elif f"gradrows_{i}" in g.files:
+            assert np.allclose(grads[k][:16].numpy(), g[f"gradrows_{i}"], rtol=1e-5, atol=1e-7), k
     if "after_0" in g.files:
         sd = m.state_dict()
         for i, k in enumerate(names):
             assert np.allclose(sd[k].numpy(), g[f"after_{i}"], rtol=1e-6, atol=1e-7), k
+
+
+def test_transfer_entropy(golden):
+    """measure_transfer_entropy (ref/model/vae_teb_model.py:1194-1226) after one
+    train-mode forward: eval-mode BatchNorm on the updated running statistics."""
+    g, t = golden("model_s16_b4"), golden("te_s16_b4")
+    m = det_fill_(M.SeqVaeTebRef(16))
+    m.train()
+    T = lambda k: torch.from_numpy(g[k])
+    with torch.no_grad():
+        m(T("y_st"), T("y_ph"), T("x_ph"), T("eps"))
+    te = m.measure_transfer_entropy(T("y_st"), T("y_ph"), T("x_ph"))
+    assert not m.training
+    assert np.allclose(te.numpy(), t["te"], rtol=1e-5, atol=1e-6)
+    assert abs(m.measure_transfer_entropy(T("y_st"), T("y_ph"), T("x_ph"), reduce_mean=True).item()
+               - float(t["te_mean"])) <= 1e-6 * abs(float(t["te_mean"]))
 
 
 def test_tiny_c1(golden):
@@ -173,5 +194,5 @@ def test_seqvae_classifier_loss(golden):
     params = [("vae_model." + k, p) for k, p in vae.named_parameters()] + \
              [("classifier." + k, p) for k, p in clf.named_parameters()]
     assert [k for k, _ in params] == list(g["param_names"])
-    gl2 = np.array([p.grad.norm().item() for _, p in params])
+    gl2 = np.array([p.grad.double().norm().item() for _, p in params])
     assert np.allclose(gl2, g["grad_l2"], rtol=2e-4, atol=1e-8)

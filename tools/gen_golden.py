@@ -263,6 +263,129 @@ def run_ref_step(model, y_st, y_ph, x_ph, y_raw, eps, beta, lr=1e-3, clip=1.0):
     return fw, losses, grads, gnorm
 
 
+BIG = 1 << 20   # parameters above this many elements (the R x R head weights) are stored by rows
+
+
+def _amp_inputs(S, B):
+    rng = np.random.Generator(np.random.PCG64(7 + S))
+    y_st = rng.standard_normal((B, S, 43)).astype(np.float32)
+    y_ph = rng.standard_normal((B, S, 44)).astype(np.float32)
+    x_ph = rng.standard_normal((B, S, 130)).astype(np.float32)
+    y_raw = rng.standard_normal((B, 16 * S)).astype(np.float32)
+    eps = rng.standard_normal((B, S, 32)).astype(np.float32)
+    return y_st, y_ph, x_ph, y_raw, eps
+
+
+class Emu16:
+    """CUDA-autocast emulation on the CPU (the reference's own training precision is
+    `torch.amp.autocast('cuda')` = fp16, ref/model/graph_model.py:709-711, and Lightning
+    `precision="16-mixed"`, :510): the operands and the output of every Linear, Conv1d
+    and LSTM GEMM are rounded to `dt` (fp32 accumulation, as MFMA / tensor cores), the
+    LSTM's h / c state is stored in `dt`, every other op (LayerNorm, BatchNorm, GELU,
+    exp, the losses) runs in fp32 on those rounded values, and the backward rounds the
+    gradients flowing through those casts to `dt` as the 16-bit backward GEMMs do.
+    fp16 adds GradScaler's loss scale (2^16) so small gradients do not flush to zero."""
+
+    def __init__(self, dt):
+        self.dt = dt
+
+    def r(self, t):
+        return None if t is None else t.to(self.dt).to(torch.float32)
+
+    def __enter__(self):
+        import torch.nn.functional as Fn
+        self._lin, self._conv = Fn.linear, Fn.conv1d
+        lin, conv, r = self._lin, self._conv, self.r
+        Fn.linear = lambda x, w, b=None: r(lin(r(x), r(w), r(b)))
+        Fn.conv1d = lambda x, w, b=None, *a, **k: r(conv(r(x), r(w), r(b), *a, **k))
+        return self
+
+    def __exit__(self, *exc):
+        import torch.nn.functional as Fn
+        Fn.linear, Fn.conv1d = self._lin, self._conv
+
+    def lstm_forward(self, mod):
+        r = self.r
+
+        def fwd(x, hx=None):
+            B, S, _ = x.shape
+            H = mod.hidden_size
+            inp = x
+            for l in range(mod.num_layers):
+                w_ih, w_hh = getattr(mod, f"weight_ih_l{l}"), getattr(mod, f"weight_hh_l{l}")
+                b = r(getattr(mod, f"bias_ih_l{l}")) + r(getattr(mod, f"bias_hh_l{l}"))
+                gx = r(torch.matmul(r(inp), r(w_ih).t()))
+                h = x.new_zeros(B, H)
+                c = x.new_zeros(B, H)
+                outs = []
+                for t in range(S):
+                    g = gx[:, t] + r(torch.matmul(r(h), r(w_hh).t())) + b
+                    i, f, gg, o = g.chunk(4, -1)
+                    c = r(torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg))
+                    h = r(torch.sigmoid(o) * torch.tanh(c))
+                    outs.append(h)
+                inp = torch.stack(outs, 1)
+            return inp, (None, None)
+        return fwd
+
+
+def run_ref_step_amp(model, inputs, beta, mode):
+    """The reference step (forward + compute_loss + backward) at 16-bit precision:
+    mode 'cpu_bf16' = torch.autocast('cpu', bfloat16) literally (CPU autocast also
+    keeps LayerNorm / the LSTM in bf16); 'emu_bf16' / 'emu_fp16' = Emu16 (the CUDA
+    autocast op split) in bf16 / fp16 (+ loss scale 2^16)."""
+    import contextlib
+    y_st, y_ph, x_ph, y_raw, eps = [torch.from_numpy(a) for a in inputs]
+    model.train()
+    model.reparameterize = lambda mu, lv: mu + eps * torch.exp(0.5 * lv)
+    scale = 1.0
+    if mode == "cpu_bf16":
+        ctx = torch.autocast("cpu", dtype=torch.bfloat16)
+    else:
+        emu = Emu16(torch.bfloat16 if mode == "emu_bf16" else torch.float16)
+        ctx = emu
+        scale = 65536.0 if mode == "emu_fp16" else 1.0
+        for m in model.modules():
+            if isinstance(m, torch.nn.LSTM):
+                m.forward = emu.lstm_forward(m)
+    with ctx:
+        fw = model(y_st, y_ph, x_ph)
+        losses = model.compute_loss(fw, y_st, y_ph, y_raw, compute_kld_loss=True, beta=beta)
+    (losses["total_loss"].float() * scale).backward()
+    grads = {k: p.grad.detach().float() / scale for k, p in model.named_parameters()}
+    return ({k: v.float() for k, v in fw.items()},
+            {k: v.float() for k, v in losses.items() if isinstance(v, torch.Tensor)}, grads)
+
+
+def gen_amp():
+    """The S=256 / B=2 training-geometry step of model_s256_b2.npz at 16-bit precision
+    (VERDICT r02 item 1b): losses, forward outputs and each gradient's rel-L2 distance
+    from the fp32 reference — the reference's own fp32-vs-16-bit spread, which bounds
+    the bf16 HIP step's distance from fp32 (tests/test_gpu_parity_s256.py)."""
+    S, B = 256, 2
+    inputs = _amp_inputs(S, B)
+    ref = build_ref_model(S)
+    fw32, l32, g32, _ = run_ref_step(ref, *inputs[:4], inputs[4], 1e-5)
+    d = dict(S=S, B=B)
+    names = list(g32.keys())
+    d["param_names"] = np.array(names)
+    for mode in ("cpu_bf16", "emu_bf16", "emu_fp16"):
+        t = time.time()
+        fw, losses, grads = run_ref_step_amp(build_ref_model(S), inputs, 1e-5, mode)
+        for k in ("mse_loss", "nll_loss", "kld_loss", "total_loss"):
+            d[f"{mode}_loss_{k}"] = losses[k].item()
+        for k, v in fw.items():
+            d[f"{mode}_fwrel_{k}"] = ((v - fw32[k]).norm() / fw32[k].norm()).item()
+        d[f"{mode}_fw_mu_pr"] = fw["mu_pr"].detach().numpy()
+        d[f"{mode}_fw_logvar_pr"] = fw["logvar_pr"].detach().numpy()
+        d[f"{mode}_grad_rel"] = np.array([((grads[k] - g32[k]).norm() / g32[k].norm().clamp_min(1e-30)).item()
+                                          for k in names])
+        print(f"amp {mode}: {time.time() - t:.1f}s total={losses['total_loss'].item():.6f} "
+              f"(fp32 {l32['total_loss'].item():.6f}) grad rel median "
+              f"{np.median(d[f'{mode}_grad_rel']):.2e} max {d[f'{mode}_grad_rel'].max():.2e}")
+    save("model_s256_b2_amp.npz", **d)
+
+
 def gen_model():
     for (S, B, full) in [(16, 4, True), (4, 3, True), (256, 2, False)]:
         rng = np.random.Generator(np.random.PCG64(7 + S))
@@ -284,8 +407,9 @@ def gen_model():
             d["fw_" + k] = v.detach().numpy()
         names = list(grads.keys())
         d["param_names"] = np.array(names)
-        d["grad_l2"] = np.array([grads[k].norm().item() for k in names])
-        d["grad_sum"] = np.array([grads[k].sum().item() for k in names])
+        # norms / sums in fp64 (an fp32 torch norm of a 16.7 M-element head gradient is off by ~1e-3)
+        d["grad_l2"] = np.array([grads[k].double().norm().item() for k in names])
+        d["grad_sum"] = np.array([grads[k].double().sum().item() for k in names])
         sd = model.state_dict()
         bn_keys = [k for k in sd if k.endswith("running_mean") or k.endswith("running_var")]
         d["bn_names"] = np.array(bn_keys)
@@ -296,13 +420,54 @@ def gen_model():
             for i, k in enumerate(bn_keys):
                 d[f"bn_{i}"] = sd[k].numpy()
         else:
-            d["after_l2"] = np.array([sd[k].norm().item() for k in names])
-            d["bn_sum"] = np.array([sd[k].sum().item() for k in bn_keys])
+            d["after_l2"] = np.array([sd[k].double().norm().item() for k in names])
+            d["bn_sum"] = np.array([sd[k].double().sum().item() for k in bn_keys])
+            # the reference's own fp32 error: the same step in fp64 (per-gradient rel-L2 of the
+            # fp32 step from it) — at S = 256 some encoder gradients are ~5e-3 off in fp32,
+            # so a second fp32 implementation is bounded by that, not by a fixed 2e-4
+            m64 = build_ref_model(S).double()
+            fw64, l64, g64, _ = run_ref_step(m64, *[a.astype(np.float64) for a in (y_st, y_ph, x_ph, y_raw, eps)],
+                                             beta)
+            d["grad_rel64"] = np.array([((grads[k].double() - g64[k]).norm() / g64[k].norm().clamp_min(1e-300)).item()
+                                        for k in names])
+            d["rel64_fw"] = np.array([((fw[k].double() - fw64[k]).norm() / fw64[k].norm()).item() for k in fw])
+            d["names_fw"] = np.array(list(fw))
+            for k in ("mse_loss", "nll_loss", "kld_loss", "total_loss"):
+                d["loss64_" + k] = l64[k].item()
+            # every gradient of the training geometry except the R x R head weights in
+            # full; those by their first 16 rows (plus grad_l2 / grad_sum above)
+            for i, k in enumerate(names):
+                if grads[k].numel() <= BIG:
+                    d[f"grad_{i}"] = grads[k].numpy()
+                else:
+                    d[f"gradrows_{i}"] = grads[k][:16].numpy()
+            for i, k in enumerate(bn_keys):
+                d[f"bn_{i}"] = sd[k].numpy()
             d["fw_mu_pr"] = fw["mu_pr"].detach().numpy()
             for k in list(d):
                 if k.startswith("fw_") and k not in ("fw_mu_pr", "fw_logvar_pr"):
                     d[k] = np.asarray(d[k])[:, :8]  # keep fixtures small
         save(f"model_s{S}_b{B}.npz", **d)
+
+
+def gen_te():
+    """SeqVaeTeb.measure_transfer_entropy (ref/model/vae_teb_model.py:1194-1226) at S=16,
+    B=4 on model_s16_b4's inputs, after one train-mode forward (so the eval-mode
+    BatchNorms run on non-trivial running statistics): the elementwise KL and its mean."""
+    S, B = 16, 4
+    g = np.load(os.path.join(OUT, "model_s16_b4.npz"))
+    model = build_ref_model(S)
+    model.train()
+    T = lambda k: torch.from_numpy(g[k])
+    with torch.no_grad():
+        model(T("y_st"), T("y_ph"), T("x_ph"))          # updates the BatchNorm running statistics
+    te = model.measure_transfer_entropy(T("y_st"), T("y_ph"), T("x_ph"), reduce_mean=False)
+    te_mean = model.measure_transfer_entropy(T("y_st"), T("y_ph"), T("x_ph"), reduce_mean=True)
+    sd = model.state_dict()
+    bn_keys = [k for k in sd if k.endswith("running_mean") or k.endswith("running_var")]
+    print(f"transfer entropy S={S} B={B}: mean {te_mean.item():.6f} training={model.training}")
+    save("te_s16_b4.npz", te=te.numpy(), te_mean=te_mean.item(), still_training=model.training,
+         bn_names=np.array(bn_keys), **{f"bn_{i}": sd[k].numpy() for i, k in enumerate(bn_keys)})
 
 
 def gen_tiny():
@@ -422,7 +587,7 @@ def gen_classifier():
 
 
 GENS = dict(kat=gen_kymatio_kat, filters=gen_filters, scattering=gen_scattering, frontend=gen_frontend,
-            stats=gen_stats_and_norm, model=gen_model, tiny=gen_tiny,
+            stats=gen_stats_and_norm, model=gen_model, amp=gen_amp, te=gen_te, tiny=gen_tiny,
             classifier=gen_classifier)
 
 if __name__ == "__main__":

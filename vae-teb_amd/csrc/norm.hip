@@ -717,6 +717,76 @@ static void col_partial_vec(int kind, const float* x, const float* dy, int64_t M
 
 static inline unsigned blocks_for(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
+// ----------------------------------------------------- synchronised BatchNorm
+// The per-rank halves of a cross-rank (SyncBatchNorm) train-mode BatchNorm: per-channel
+// sums in double from the same column partials (k_col_partial4) and the same
+// fixed-order combine as k_bn_finalize, written as [2][C] doubles + the row count at
+// [2C], so the caller can all-reduce them (SUM) between the launches.
+__global__ __launch_bounds__(NT) void k_sbn_sums(const float* __restrict__ part, int blocks, int C, int64_t M,
+                                                 double* __restrict__ sums) {
+    __shared__ double r0[NT], r1[NT];
+    const int c = blockIdx.x;
+    double a0 = 0.0, a1 = 0.0;
+    const float* p0 = part + (int64_t)c * blocks;
+    const float* p1 = part + (int64_t)(C + c) * blocks;
+    for (int b = threadIdx.x; b < blocks; b += NT) {
+        a0 += (double)p0[b];
+        a1 += (double)p1[b];
+    }
+    r0[threadIdx.x] = a0;
+    r1[threadIdx.x] = a1;
+    __syncthreads();
+    for (int o = NT / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            r0[threadIdx.x] += r0[threadIdx.x + o];
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        sums[c] = r0[0];
+        sums[C + c] = r1[0];
+        if (c == 0) sums[2 * C] = (double)M;
+    }
+}
+
+// which 0: mean = S0 / M_total.  which 1: var = S0 / M_total -> rstd, running statistics
+// (unbiased with the global count, as torch's SyncBatchNorm).  which 2: the LOCAL column
+// sums of the backward -> dbeta (+)= S0, dgamma (+)= S1 (this rank's parameter gradients,
+// averaged by the data-parallel all-reduce like any other gradient).
+__global__ void k_sbn_stats(const double* __restrict__ sums, int C, int which, float eps, float momentum,
+                            float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ run_mean,
+                            float* __restrict__ run_var, float* __restrict__ dgamma, float* __restrict__ dbeta,
+                            int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double M = sums[2 * C];
+    if (which == 0) {
+        mean[c] = (float)(sums[c] / M);
+    } else if (which == 1) {
+        const double var = sums[c] / M;
+        rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+        if (run_mean) {
+            const double unb = M > 1 ? var * M / (M - 1) : var;
+            run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean[c]);
+            run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+        }
+    } else {
+        dbeta[c] = accumulate ? dbeta[c] + (float)sums[c] : (float)sums[c];
+        dgamma[c] = accumulate ? dgamma[c] + (float)sums[C + c] : (float)sums[C + c];
+    }
+}
+
+// the global column sums of the backward, divided by the global row count (read on the
+// device: no host synchronisation), as the dgamma / dbeta arrays of k_bn_dx4 with M = 1
+__global__ void k_sbn_dsum(const double* __restrict__ sums, int C, float* __restrict__ dg, float* __restrict__ db) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double M = sums[2 * C];
+    db[c] = (float)(sums[c] / M);
+    dg[c] = (float)(sums[C + c] / M);
+}
+
 // y = act(BN(x)) for conv.hip's fused conv + BatchNorm forward
 int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
                     const float* beta, int act, float* y, hipStream_t st) {
@@ -894,6 +964,59 @@ int vt_batchnorm_eval(const float* x, int64_t M, int C, const float* run_mean, c
     hipLaunchKernelGGL(k_bn_eval, dim3(blocks_for(M * C)), dim3(256), 0, S(stream), x, M, C, run_mean, run_var, eps,
                        gamma, beta, act, y);
     VT_LAUNCH_CHECK("vt_batchnorm_eval");
+    return VT_OK;
+}
+
+int vt_syncbn_sums(const float* x, const float* dy, int64_t M, int C, int which, const float* mean,
+                   const float* rstd, const float* gamma, const float* beta, int act, double* sums, float* ws,
+                   int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0 && C <= 256 && which >= 0 && which <= 2 && sums, "vt_syncbn_sums: shape");
+    VT_CHECK_ARG(which == 0 || mean, "vt_syncbn_sums: mean needed");
+    VT_CHECK_ARG(which < 2 || (dy && rstd && gamma && beta), "vt_syncbn_sums: backward arguments");
+    int64_t rpb;
+    const int blocks = bn_blocks(M, ws_floats, C, &rpb);
+    VT_CHECK_ARG(blocks >= 1, "vt_syncbn_sums: workspace too small");
+    hipStream_t st = S(stream);
+    col_partial_vec(which, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st);
+    hipLaunchKernelGGL(k_sbn_sums, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, sums);
+    VT_LAUNCH_CHECK("vt_syncbn_sums");
+    return VT_OK;
+}
+
+int vt_syncbn_stats(const double* sums, int C, int which, float eps, float momentum, float* mean, float* rstd,
+                    float* run_mean, float* run_var, float* dgamma, float* dbeta, int accumulate, void* stream) {
+    VT_CHECK_ARG(sums && C > 0 && which >= 0 && which <= 2, "vt_syncbn_stats: arguments");
+    VT_CHECK_ARG((which == 0 && mean) || (which == 1 && mean && rstd) || (which == 2 && dgamma && dbeta),
+                 "vt_syncbn_stats: outputs");
+    hipLaunchKernelGGL(k_sbn_stats, dim3(blocks_for(C)), dim3(256), 0, S(stream), sums, C, which, eps, momentum, mean,
+                       rstd, run_mean, run_var, dgamma, dbeta, accumulate);
+    VT_LAUNCH_CHECK("vt_syncbn_stats");
+    return VT_OK;
+}
+
+int vt_batchnorm_apply(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
+                       const float* beta, int act, float* y, void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0 && C <= BNV_C, "vt_batchnorm_apply: shape");
+    bn_apply_vec(x, M, C, mean, rstd, gamma, beta, act, y, S(stream));
+    VT_LAUNCH_CHECK("vt_batchnorm_apply");
+    return VT_OK;
+}
+
+int vt_syncbn_bwd_dx(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, int act, const double* sums, float* dx, float* ws,
+                     void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0 && C <= BNV_C && sums && ws, "vt_syncbn_bwd_dx: arguments");
+    hipStream_t st = S(stream);
+    float* dg = ws;
+    float* db = ws + C;
+    hipLaunchKernelGGL(k_sbn_dsum, dim3(blocks_for(C)), dim3(256), 0, st, sums, C, dg, db);
+    const int64_t n = M * C;
+#define VT_F(A)                                                                                                   \
+    hipLaunchKernelGGL(k_bn_dx4<A>, dim3(bnv_blocks(n)), dim3(NT), 0, st, dy, x, n, (int64_t)1, C, mean, rstd, \
+                       gamma, beta, dg, db, dx)
+    VT_ACT_SWITCH(act, VT_F)
+#undef VT_F
+    VT_LAUNCH_CHECK("vt_syncbn_bwd_dx");
     return VT_OK;
 }
 

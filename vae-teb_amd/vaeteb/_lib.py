@@ -20,7 +20,7 @@ VT_ERR_ARG, VT_ERR_LAYOUT, VT_ERR_HIP = -1, -2, -3
 
 _CT = {
     "int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "double": ctypes.c_double,
-    "void*": ctypes.c_void_p, "float*": ctypes.c_void_p, "int*": ctypes.c_void_p, "int64_t*": ctypes.c_void_p,
+    "void*": ctypes.c_void_p, "float*": ctypes.c_void_p, "double*": ctypes.c_void_p, "int*": ctypes.c_void_p, "int64_t*": ctypes.c_void_p,
     "char*": ctypes.c_char_p,
 }
 

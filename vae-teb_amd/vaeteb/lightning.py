@@ -52,6 +52,7 @@ class FlatAdamW:
         dev = self.flat.p.device
         self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, initial_lr=lr)]
         self.max_norm = max_norm
+        self.pre_scale = 1.0      # 1 / world under data parallelism: the all-reduced SUM becomes the mean
         self.norm_out = torch.zeros(2, device=dev)
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.coef = torch.zeros(2, device=dev)
@@ -73,8 +74,10 @@ class FlatAdamW:
         g = self.param_groups[0]
         s = self.flat
         gscale = 0
-        if self.max_norm is not None:
-            _lib.call("vt_grad_norm_clip", s.g.data_ptr(), s.numel, 1.0, float(self.max_norm),
+        if self.max_norm is not None or self.pre_scale != 1.0:
+            # clip_grad_norm_ on the averaged gradient (max_norm <= 0: scale only)
+            _lib.call("vt_grad_norm_clip", s.g.data_ptr(), s.numel, float(self.pre_scale),
+                      float(self.max_norm) if self.max_norm is not None else 0.0,
                       self.norm_out.data_ptr(), self.norm_ws.data_ptr(), _lib.stream())
             gscale = self.norm_out.data_ptr() + 4
         b1, b2 = g["betas"]
@@ -239,13 +242,39 @@ def load_pytorch_checkpoint(model, path, map_location="cpu"):
     return ck.get("epoch")
 
 
-def fit(module, train_loader, max_epochs=1, gradient_clip_val=0.5, val_loader=None, to_device=None):
+def _join_side_streams():
+    """The HIP ops write some gradients in place on side streams (no AccumulateGrad, so
+    autograd does not join them): the optimizer's stream waits for them."""
+    if torch.cuda.is_available():
+        from . import ops
+        for st in ops.SIDE_STREAMS:
+            _lib.wait_for(_lib.stream(), st)
+
+
+def fit(module, train_loader, max_epochs=1, gradient_clip_val=0.5, val_loader=None, to_device=None,
+        sync_batchnorm=False, group=None):
     """Lightning Trainer.fit as configured at ref/model/graph_model.py:404-610
     (gradient_clip_val 0.5, step-interval scheduler).  Returns the module's
-    last logged values.  No host synchronisation inside an epoch."""
+    last logged values.  No host synchronisation inside an epoch.
+
+    Under torch.distributed with world size > 1 (one process per GPU, as Lightning's
+    DDPStrategy, :470-471): the gradients are all-reduced in buckets from the backward
+    (vaeteb.train.GradBuckets) and averaged (1 / world folded into the clip), and with
+    sync_batchnorm=True (Lightning's flag, :517) every conv block's BatchNorm takes its
+    statistics over all ranks (vaeteb.model.convert_sync_batchnorm)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if sync_batchnorm and world > 1:
+        from .model import convert_sync_batchnorm
+        convert_sync_batchnorm(module.model, group)
     conf = module.configure_optimizers()
     opt, sched = (conf["optimizer"], conf["lr_scheduler"]["scheduler"]) if isinstance(conf, dict) else (conf, None)
     opt.max_norm = gradient_clip_val
+    buckets = None
+    if world > 1:
+        from .train import GradBuckets
+        buckets = GradBuckets(opt.flat, group)
+        opt.pre_scale = 1.0 / world
     mv = lambda b: to_device(b) if to_device else b
     for epoch in range(module.current_epoch, max_epochs):
         module.current_epoch = epoch
@@ -253,8 +282,13 @@ def fit(module, train_loader, max_epochs=1, gradient_clip_val=0.5, val_loader=No
         module.on_train_epoch_start()
         for i, batch in enumerate(train_loader):
             opt.zero_grad()
+            if buckets is not None:
+                buckets.reset()
             loss = module.training_step(mv(batch), i)
             loss.backward()
+            _join_side_streams()
+            if buckets is not None:
+                buckets.finish()
             opt.step()
             if sched is not None:
                 sched.step()

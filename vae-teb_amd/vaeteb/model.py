@@ -314,6 +314,8 @@ class ConvBlock(nn.Module):
         self.bf16 = False  # bf16-MFMA conv (the reference's 16-bit autocast precision); BatchNorm stays fp32
         self.conv = _ConvWeight(cin, cout, k)
         self.bn_layer = _BatchNorm(cout)
+        self.sync_bn = False      # cross-rank BatchNorm statistics (convert_sync_batchnorm)
+        self.sync_group = None    # process group of the synchronised statistics (None: the default group)
 
     def forward(self, x):
         bn = self.bn_layer
@@ -321,12 +323,29 @@ class ConvBlock(nn.Module):
             return ops.conv_bn_eval(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                     mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
                                     eps=bn.eps, bf16=self.bf16)
-        y = ops.conv_bn_act(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                            mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
-                            momentum=bn.momentum, eps=bn.eps, bf16=self.bf16)
+        if self.sync_bn:
+            y = ops.sync_conv_bn_act(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                     mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
+                                     momentum=bn.momentum, eps=bn.eps, bf16=self.bf16, group=self.sync_group)
+        else:
+            y = ops.conv_bn_act(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
+                                momentum=bn.momentum, eps=bn.eps, bf16=self.bf16)
         if not getattr(bn, "_vt_batched", False):   # else counted by SeqVaeTeb in one launch
             bn.num_batches_tracked.add_(1)
         return y
+
+
+def convert_sync_batchnorm(module, process_group=None):
+    """torch.nn.SyncBatchNorm.convert_sync_batchnorm for the HIP conv blocks: every
+    ConvBlock's train-mode BatchNorm takes its statistics over all ranks of
+    `process_group` (Lightning's sync_batchnorm=True, ref/model/graph_model.py:517).
+    Same parameters / buffers / state_dict keys; returns the module."""
+    for m in module.modules():
+        if isinstance(m, ConvBlock):
+            m.sync_bn = True
+            m.sync_group = process_group
+    return module
 
 
 class LSTM(nn.Module):
@@ -650,6 +669,55 @@ class SeqVaeTeb(nn.Module):
         """_kld_loss(reduce_mean=False), ref/model/vae_teb_model.py:1071-1082."""
         return 0.5 * (logvar_prior - logvar_post - 1 + (logvar_post.exp() + (mu_post - mu_prior) ** 2)
                       / logvar_prior.exp())
+
+    def _kld_loss(self, mu_prior, logvar_prior, mu_post, logvar_post, reduce_mean=True):
+        """ref/model/vae_teb_model.py:1052-1082: KL(q || p) per (sample, step, latent);
+        reduce_mean: summed over the latent dimension, averaged over (sample, step)."""
+        kld = self.kld_elementwise(mu_prior, logvar_prior, mu_post, logvar_post)
+        return kld.sum(dim=-1).mean() if reduce_mean else kld
+
+    def encode(self, y_st, y_ph, x_ph):
+        """The posterior / prior half of forward() (encoders + conditional encoder,
+        ref/model/vae_teb_model.py:1097-1115): (mu_prior, logvar_prior, mu_post,
+        logvar_post).  The reparameterisation and the decoder do not influence these."""
+        prev = dict(_PAR)
+        _PAR["on"], _PAR["next"] = bool(self.concurrent_encoders and x_ph.is_cuda), 1
+        try:
+            (mu_y, logvar_y_full), mu_x = fork_lockstep(self.target_encoder.stages(y_st, y_ph),
+                                                        self.source_encoder.stages(x_ph))
+            logvar_y_prior, c_logvar = torch.split(logvar_y_full, self.latent_dim_target, dim=-1)
+            mu_c, logvar_post = self.conditional_encoder(mu_x, c_logvar)
+        finally:
+            _PAR.update(prev)
+        return mu_y, logvar_y_prior.contiguous(), mu_c + mu_y, logvar_post
+
+    def measure_transfer_entropy(self, y_st, y_ph, x_ph, reduce_mean=False):
+        """ref/model/vae_teb_model.py:1194-1226: transfer entropy x -> z as the KL
+        divergence between the posterior q(z | x, y) and the prior p(z | y), with the
+        model put in eval mode (BatchNorm on its running statistics; the model stays
+        in eval mode afterwards, as in the reference) and no gradients.  Same values
+        as the reference's full forward: the decoder it also runs there does not enter
+        the KL, so only the encoders and the conditional encoder run here.  Returns
+        (B, S, latent) (reduce_mean=False) or the scalar mean of the latent sums."""
+        self.eval()
+        with torch.no_grad():
+            mu_p, lv_p, mu_q, lv_q = self.encode(y_st, y_ph, x_ph)
+            return self._kld_loss(mu_p, lv_p, mu_q, lv_q, reduce_mean=reduce_mean)
+
+    @staticmethod
+    def get_predictions(x, stride=16, new_C=4800):
+        """ref/model/vae_teb_model.py:1228-1246: overlapping per-step windows x (B, N, C)
+        placed at offsets i * stride of a (B, N, new_C) canvas (NaN elsewhere) and their
+        NaN-mean over the steps (B, new_C)."""
+        B, N, C = x.shape
+        y = x.new_full((B, N, new_C), float("nan"))
+        for i in range(N):
+            start = i * stride
+            if start >= new_C:
+                break
+            end = min(start + C, new_C)
+            y[:, i, start:end] = x[:, i, :end - start]
+        return y, torch.nanmean(y, dim=1)
 
 
 class TinyVaeTeb(nn.Module):

@@ -555,6 +555,95 @@ class ConvBNActF(torch.autograd.Function):
         return gx, gw, gg, gb, None, None, None, None, None, None, None, None
 
 
+class SyncConvBNActF(torch.autograd.Function):
+    """ConvBNActF with cross-rank BatchNorm statistics (torch.nn.SyncBatchNorm semantics,
+    Lightning sync_batchnorm=True: ref/model/graph_model.py:517): the per-channel sums
+    are all-reduced over `group` twice in the forward (sum, then the centred sum of
+    squares: two-pass, as the single-rank path) and once in the backward (sum dz, sum
+    dz xhat, for dx); dgamma / dbeta are this rank's own sums (the data-parallel
+    gradient all-reduce averages them, as DDP does for SyncBatchNorm's grad_weight)."""
+
+    @staticmethod
+    def forward(ctx, x, w, g, b, run_mean, run_var, mode, up, act, momentum, eps, bf16, group):
+        import torch.distributed as dist
+        _check(x, w, g, b)
+        B, L, Cin = x.shape
+        Cout, _, K = w.shape
+        x = x.contiguous()
+        Lo = _lib.lib().fns["vt_conv1d_out_len"](L, K, mode, up)
+        conv = torch.empty((B, Lo, Cout), device=x.device)
+        if bf16:
+            w16, w16t = _conv_shadow(w)
+            call("vt_conv1d_fwd_bf16", ptr(x), B, L, Cin, ptr(w16), Cout, K, mode, up, ptr(conv), _st())
+        else:
+            w16t = None
+            call("vt_conv1d_direct_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(conv), _st())
+        M = B * Lo
+        mean = torch.empty(Cout, device=x.device)
+        rstd = torch.empty(Cout, device=x.device)
+        sums = torch.empty(2 * Cout + 1, dtype=torch.float64, device=x.device)
+        ws = WS.get(4096 * Cout * 2 + 2 * Cout, x.device, 2)
+        for which, outs in ((0, (ptr(mean), None, None, None)), (1, (ptr(mean), ptr(rstd), ptr(run_mean),
+                                                                     ptr(run_var)))):
+            call("vt_syncbn_sums", ptr(conv), None, M, Cout, which, ptr(mean), None, None, None, 0, ptr(sums),
+                 ptr(ws), ws.numel(), _st())
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)   # counts add up too (sums[2C])
+            call("vt_syncbn_stats", ptr(sums), Cout, which, eps, momentum, *outs, None, None, 0, _st())
+        y = torch.empty_like(conv)
+        call("vt_batchnorm_apply", ptr(conv), M, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT[act], ptr(y), _st())
+        ctx.save_for_backward(x, conv, mean, rstd, w16t)
+        ctx.params = (w, g, b)
+        ctx.cfg = (mode, up, act, bf16, group)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        import torch.distributed as dist
+        x, conv, mean, rstd, w16t = ctx.saved_tensors
+        w, g, b = ctx.params
+        mode, up, act, bf16, group = ctx.cfg
+        B, L, Cin = x.shape
+        Cout, _, K = w.shape
+        Lo = conv.shape[1]
+        M = B * Lo
+        gy = gy.contiguous()
+        pbn = _ParamGrads([g, b], [True, True])
+        sums = torch.empty(2 * Cout + 1, dtype=torch.float64, device=x.device)
+        ws = WS.get(4096 * Cout * 2 + 2 * Cout, x.device, 2)
+        call("vt_syncbn_sums", ptr(conv), ptr(gy), M, Cout, 2, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT[act],
+             ptr(sums), ptr(ws), ws.numel(), _st())
+        call("vt_syncbn_stats", ptr(sums), Cout, 2, 0.0, 0.0, None, None, None, None, ptr(pbn.out[0]),
+             ptr(pbn.out[1]), pbn.acc, _st())
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+        gconv = torch.empty_like(conv)
+        call("vt_syncbn_bwd_dx", ptr(gy), ptr(conv), M, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT[act],
+             ptr(sums), ptr(gconv), ptr(ws), _st())
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            gpad = WS.get(B * (Lo + K - 1) * Cin, x.device, 3)
+            if bf16:
+                call("vt_conv1d_bwd_gpad_bf16", ptr(gconv), B, L, Cin, ptr(w16t), Cout, K, mode, up, ptr(gpad), _st())
+            else:
+                call("vt_conv1d_direct_bwd_gpad", ptr(gconv), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(gpad), _st())
+            call("vt_conv1d_fold", ptr(gpad), B, L, Cin, Cout, K, mode, up, ptr(gx), 0, _st())
+        pw = _ParamGrads([w], [ctx.needs_input_grad[1]])
+        if pw.out[0] is not None:
+            ws1 = WS.get(WS_LINEAR, x.device, 1)
+            fn = "vt_conv1d_bwd_weight_bf16" if bf16 else "vt_conv1d_direct_bwd_weight"
+            call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1), ws1.numel(),
+                 _st())
+        gw, = pw.result()
+        gg, gb = pbn.result()
+        return gx, gw, gg, gb, None, None, None, None, None, None, None, None, None
+
+
+def sync_conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momentum=0.9, eps=1e-5, bf16=False,
+                     group=None):
+    return SyncConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps, bool(bf16),
+                                group)
+
+
 def conv_bn_eval(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", eps=1e-5, bf16=False):
     """Eval-mode ConvBlock: conv -> BatchNorm with the running statistics -> act
     (validation / frozen-VAE / predict path; not differentiable)."""

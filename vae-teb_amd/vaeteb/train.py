@@ -114,18 +114,26 @@ class GradBuckets:
             # reset(): the model creates them lazily during the first forward, and
             # a head weight gradient queued on one just before this hook must be
             # covered by the wait
-            if self.state.g.is_cuda:
-                from . import ops
-                cur = torch.cuda.current_stream()
-                for st in ops.SIDE_STREAMS:
-                    if st != cur:
-                        cur.wait_stream(st)
+            self._join_side_streams()
             s, e, _ = self.buckets[b]
             self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
                                               async_op=True))
 
+    def _join_side_streams(self):
+        """The collective's stream waits for every stream that may have written gradients
+        (the concurrent encoders, the side-stream weight gradients)."""
+        if self.state.g.is_cuda:
+            from . import ops
+            cur = torch.cuda.current_stream()
+            for st in ops.SIDE_STREAMS:
+                if st != cur:
+                    cur.wait_stream(st)
+
     def finish(self):
-        # parameters that received no gradient this step still have to be reduced
+        # parameters that received no gradient this step still have to be reduced (after
+        # every gradient writer: a caller's backward may leave side-stream work in flight)
+        if any(left > 0 for left in self.pending):
+            self._join_side_streams()
         for b, left in enumerate(self.pending):
             if left > 0:
                 s, e, _ = self.buckets[b]
@@ -182,6 +190,15 @@ class Trainer:
         fw = self.model(batch["fhr_st"], batch["fhr_ph"], batch["fhr_up_ph"], eps=eps)
         return self.model.compute_loss(fw, batch["fhr_st"], batch["fhr_ph"], batch["fhr"], compute_kld_loss=True,
                                        beta=self.beta_kld)
+
+    def eval_losses(self, batch, eps=None):
+        """Validation losses (ref/model/graph_model.py:769-815): the model in eval mode
+        (BatchNorm on its running statistics), no gradients, the training loss terms."""
+        if self.model.training:
+            self.model.eval()
+        with torch.no_grad():
+            out = self.loss(batch, eps)
+        return {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
 
     def step(self, batch, eps=None, before_update=None):
         """One optimisation step; returns the loss dict (device scalars, no sync).
