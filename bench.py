@@ -84,6 +84,36 @@ MFMA_CALLS = {
 MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 
 
+def profile_mfma(ROOT_=None):
+    """Decoder-head MFMA kernel time per step from the latest committed rocprofv3
+    kernel-stats summary of this bench (profiles/r*/kernel_stats_*.csv): the sum of
+    k_mfma_gemm + k_mfma_dw + k_mfma_reduce over the profiled steps (one k_adamw4 per
+    step).  Returns (ms per step, csv path) or (None, None)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_step*.csv")), key=os.path.getmtime)
+    for f in reversed(files):
+        rows = list(csv.DictReader(open(f)))
+        steps = sum(int(r["Calls"]) for r in rows if "k_adamw4" in r["Name"])
+        ns = sum(float(r["TotalDurationNs"]) for r in rows if "k_mfma_" in r["Name"])
+        if steps and ns:
+            return ns / steps / 1e6, os.path.relpath(f, ROOT)
+    return None, None
+
+
+# SURVEY.md §8(d): algorithmic HBM bytes per sample of the whole step (c2, S = 256):
+# front-end raw read + analytic-signal write and read + feature write, VAE activations
+# (4,161,024 leaf activation elements per sample x 2 B x 4 passes, measured with hooks on
+# the J11 model) and parameter / optimizer traffic 46 B x P per step over the batch.
+ACT_ELEMS_PER_SAMPLE = 4_161_024
+
+
+def step_bytes_per_sample(plan, fe, n_params, batch):
+    N, F = plan.N, plan.n_filters
+    front = 2 * N * 4 + 2 * (2 * F * N * 8) + (fe.C_st + fe.C_ph + fe.C_x) * plan.S * 4
+    return front + ACT_ELEMS_PER_SAMPLE * 2 * 4 + 46 * n_params / batch
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of the roofline kernel from the latest committed
     rocprofv3 PMC measurement (profiles/r*/pmc_traffic.json, written by
@@ -264,7 +294,8 @@ def main():
         # config 4: SeqVaeTebClassifier end to end (freeze_vae=False), the reference's default classifier
         # (filters 32, depth 6, dropout 0.2, attention), total = CE + 0.1 * ELBO(beta 1)
         from vaeteb.classifier import SeqVaeTebClassifier
-        assert not args.graph, "--graph is not wired for the classifier workload"
+        # the captured step would replay the classifier's dropout masks (host-side seeds at capture time)
+        assert not (args.graph or args.native), "--graph / --native are not wired for the classifier workload"
         model = SeqVaeTebClassifier(sequence_length=S, freeze_vae=False, **vae_kw).to(dev)
     else:
         model = SeqVaeTeb(sequence_length=S, **vae_kw).to(dev)
@@ -276,11 +307,18 @@ def main():
     labels = [torch.from_numpy(np.random.default_rng(rank + world * i).integers(0, 2, B)).to(dev) for i in range(2)]
     torch.cuda.synchronize()
 
-    # vt_fe_pairs work = algorithmic HBM bytes of the call: B x n_pairs x (read a_i, a_j: 2 N complex64; write
-    # pair_len fp32).  The phase and cross pair launches run concurrently on two streams; each call's events
-    # span its own launch, so achieved = bytes of all calls / summed call durations (a lower bound).
+    # vt_fe_pairs compulsory HBM bytes per launch: every analytic-signal slot the launch's pairs use, read
+    # once (N complex64), and the pair features written (pair_len fp32) — SURVEY.md §8(d)'s analytic-signal
+    # read + feature write for the pairs of that launch (phase: ch0 slots of the 44 phase pairs; cross: the
+    # ch0 i-slots and ch1 j-slots of the 130 cross pairs).  The phase and cross launches run concurrently
+    # on two streams; each call's events span its own launch.
+    p_ = plan
+    ph_slots = {(0, int(p_.i_idx[k])) for k in fe.phase_pairs} | {(0, int(p_.j_idx[k])) for k in fe.phase_pairs}
+    x_slots = {(0, int(p_.i_idx[k])) for k in fe.cross_pairs} | {(1, int(p_.j_idx[k])) for k in fe.cross_pairs}
+    slots_of = {fe.C_ph: len(ph_slots), fe.C_x: len(x_slots)}
     work = dict(MFMA_CALLS)
-    work["vt_fe_pairs"] = lambda an, B, n_slots, N, n_pad, pad_left, n_pairs, *a: B * n_pairs * (2 * N * 8 + a[7] * 4)
+    work["vt_fe_pairs"] = lambda an, B, n_slots, N, n_pad, pad_left, n_pairs, *a: \
+        B * (slots_of.get(n_pairs, n_slots) * N * 8 + n_pairs * a[7] * 4)
     timer = KernelTimer(["vt_fe_pairs", *MFMA_CALLS], flops=work)
     graph = args.graph or args.native
     if graph:
@@ -403,6 +441,8 @@ def main():
     elbo = {k: round(float(last[k].item()), 6) for k in keys}
     samples = args.steps * B * world
     value = samples / dt
+    n_params = sum(p.numel() for p in model.parameters())
+    step_bytes = step_bytes_per_sample(plan, fe, n_params, B)
     k_ms, k_n = timer.mean_ms("vt_fe_pairs")
     k_bytes = timer.total_flops["vt_fe_pairs"] / max(k_n, 1)   # mean algorithmic bytes per launch
     traffic, traffic_src = pmc_traffic("k_fe_pairs8k") if (J, Q, T, B) == (11, 4, 16, 256) else (None, None)
@@ -438,7 +478,16 @@ def main():
                      "traffic": traffic, "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src, "avg_launch_ms": round(k_ms, 4), "launches": k_n,
                      "algorithmic_bytes": round(k_bytes),
+                     "algorithmic_bytes_def": "compulsory: the launch's analytic-signal slots read once + pair "
+                                              "features written (SURVEY.md §8(d))",
+                     "limiter": "VALU / LDS latency, not HBM (DESIGN.md §5: 0.74k VALU per wave, 49 % SQ_WAIT_ANY)",
                      "launches_per_step": k_n / args.steps},
+        # SURVEY.md §8(d)'s step-level roofline: samples/s x algorithmic bytes per sample / (GPUs x 8 TB/s)
+        "roofline_step": {"bound": "hbm", "bytes_per_sample": round(step_bytes),
+                          "achieved": round(value * step_bytes / world / 1e9, 1), "peak": HBM_PEAK_GBS,
+                          "unit": "GB/s", "frac": round(value * step_bytes / world / (HBM_PEAK_GBS * 1e9), 4),
+                          "formula": "value x bytes_per_sample / (n_gpus x 8e12); bytes_per_sample = front-end "
+                                     "+ 4,161,024 activation elements x 2 B x 4 + 46 B x params / batch"},
     }
     mfma_steps = args.steps
     if graph:
@@ -452,10 +501,17 @@ def main():
         mfma_steps = 2
     mfma_ms = timer.total_ms(list(MFMA_CALLS))
     if mfma_ms > 0:
-        tf = sum(timer.total_flops[n] for n in MFMA_CALLS) / (mfma_ms * 1e-3) / 1e12
-        out["mfma"] = {"kernels": "vt_mfma_linear_{fwd,bwd_data,bwd_weight} (decoder heads)",
-                       "achieved": round(tf, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                       "frac": round(tf / MFMA_PEAK_TFLOPS, 4), "ms_per_step": round(mfma_ms / mfma_steps, 3),
+        # MFMA utilisation of the decoder heads from KERNEL time: the committed rocprofv3 summary of this
+        # bench (k_mfma_gemm + k_mfma_dw + k_mfma_reduce per step); the live HIP-event span around the
+        # C-ABI calls (which also covers the split-K reduces' launch gaps) is kept as call_span_ms
+        flops_step = sum(timer.total_flops[n] for n in MFMA_CALLS) / mfma_steps
+        k_mfma_ms, k_src = profile_mfma() if (J, Q, T, B) == (11, 4, 16, 256) else (None, None)
+        tf = flops_step / (k_mfma_ms * 1e-3) / 1e12 if k_mfma_ms else None
+        out["mfma"] = {"kernels": "k_mfma_gemm + k_mfma_dw + k_mfma_reduce (decoder heads, bf16)",
+                       "flop_per_step": flops_step, "kernel_ms_per_step": k_mfma_ms and round(k_mfma_ms, 4),
+                       "source": k_src, "achieved": tf and round(tf, 1), "peak": MFMA_PEAK_TFLOPS,
+                       "unit": "TFLOP/s", "frac": tf and round(tf / MFMA_PEAK_TFLOPS, 4),
+                       "call_span_ms_per_step": round(mfma_ms / mfma_steps, 3),
                        "timed_in": "eager steps after the timed region" if graph else "timed region"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline((J, Q, T), batch=args.cpu_batch, classifier=c4)

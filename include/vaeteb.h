@@ -317,6 +317,9 @@ int vt_conv1d_bn_fwd(const float* X, int B, int L_in, int Cin, const float* W, i
  * step: w16 [Cout][K][ceil32(Cin)] (forward), w16t [Cin][K][ceil32(Cout)]
  * = W[co][ci][K-1-k] (backward-data), zero-padded.                             */
 int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, void* w16t, void* stream);
+/* Operand-window staging of the bf16 conv kernels: 1 (default) lanes along channels
+ * (coalesced row segments), 0 the octet-per-lane staging; bit-identical results (A/B). */
+int vt_conv_bf16_set_staging(int channel_lanes);
 int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode,
                           int up, const float* gamma, const float* beta, int act, float eps, float momentum,
                           float* conv_out, float* Y, float* mean, float* rstd, float* run_mean, float* run_var,

@@ -258,3 +258,39 @@ def test_backward_data_direct_dx_bitwise(L, geo):
     torch.cuda.synchronize()
     assert torch.equal(dx0, dx1), ((dx0 != dx1).sum().item(), dx0.numel())
     assert torch.equal(d0, d1)
+
+
+@pytest.mark.parametrize("geo", GEOS)
+def test_window_staging_channel_lanes_bitwise(L, geo):
+    """vt_conv_bf16_set_staging: the channel-lane window staging (default) and the
+    octet staging give the same bits — forward, backward-data with the fused
+    BatchNorm backward, and its bf16 side output."""
+    B, Lin, Cin, Cout, K, mode, up = geo
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    M = B * Lo
+    torch.manual_seed(7 * sum(geo))
+    x = torch.randn(B, Lin, Cin, device="cuda")
+    w = torch.randn(Cout, Cin, K, device="cuda") / (Cin * K) ** 0.5
+    conv = torch.randn(B, Lo, Cout, device="cuda") * 2 + 0.3
+    gy = torch.randn(B, Lo, Cout, device="cuda")
+    bnp = torch.cat([conv.reshape(-1, Cout).mean(0), 1 / (conv.reshape(-1, Cout).var(0) + 1e-5).sqrt(),
+                     1 + 0.1 * torch.randn(Cout, device="cuda"), 0.1 * torch.randn(Cout, device="cuda"),
+                     torch.randn(Cout, device="cuda"), torch.randn(Cout, device="cuda")]).contiguous()
+    w16, w16t = _shadow(L, w)
+    cp = (Cout + 7) // 8 * 8
+    outs = []
+    try:
+        for cl in (0, 1):
+            L.call("vt_conv_bf16_set_staging", cl)
+            y = torch.full((B, Lo, Cout), float("nan"), device="cuda")
+            L.call("vt_conv1d_fwd_bf16", L.ptr(x), B, Lin, Cin, L.ptr(w16), Cout, K, mode, up, L.ptr(y), L.stream())
+            gp = torch.full((B, Lo + K - 1, Cin), float("nan"), device="cuda")
+            d = torch.full((M, cp), float("nan"), dtype=torch.bfloat16, device="cuda")
+            L.call("vt_conv1d_bwd_gpad_bf16_bn", L.ptr(gy), L.ptr(conv), L.ptr(bnp), 3, M, B, Lin, Cin, L.ptr(w16t),
+                   Cout, K, mode, up, L.ptr(gp), L.ptr(d), L.stream())
+            torch.cuda.synchronize()
+            outs.append((y, gp, d))
+    finally:
+        L.call("vt_conv_bf16_set_staging", 1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), ((a != b).sum().item(), a.numel())

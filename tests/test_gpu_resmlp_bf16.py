@@ -223,3 +223,29 @@ def test_seqvaeteb_mlp_bf16_step(golden):
         den = sum(v.norm() ** 2 for v in ref.values())
         return (num / den).sqrt().item()
     assert dev("bf16") <= 4 * dev("pert") + 1e-3, (dev("bf16"), dev("pert"))
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_resmlp_bf16_backward_accumulates_into_sinks(case):
+    """The training path's flat-buffer gradients (vaeteb.train.FlatState: every .grad a
+    sink, vt_resmlp_bf16_bwd with accumulate = 1) == the pre-filled value + the
+    accumulate = 0 gradient, bit for bit (one fp32 add per element in the fixed-order
+    partial sum)."""
+    m, x = _setup(case, 1000, 11)
+    gy = torch.randn(1000, m.body[m._plan[-1][0]].out_features, dtype=torch.float64)
+    _, g0 = _gpu(m, x, gy)
+    g0 = {n: g.clone() for n, g in g0.items()}
+    prefill = {n: torch.randn_like(p) for n, p in m.named_parameters()}
+    for n, p in m.named_parameters():
+        p.grad = prefill[n].clone()
+        p._vt_sink = True
+    try:
+        xd = x.float().cuda().requires_grad_(True)
+        (m(xd) * gy.float().cuda()).sum().backward()
+        torch.cuda.synchronize()
+        for n, p in m.named_parameters():
+            assert torch.equal(p.grad, prefill[n] + g0[n]), n
+        assert torch.equal(xd.grad, g0["x"])
+    finally:
+        for p in m.parameters():
+            p._vt_sink = False

@@ -7,7 +7,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
 import torch  # noqa: E402
+from vaeteb import _lib  # noqa: E402
 from vaeteb.model import ConvBlock, Decoder  # noqa: E402
+
+_lib.call("vt_conv_bf16_set_staging", int(os.environ.get("VAETEB_CONV_CL", "1")))   # window staging A/B
 
 B, L = 256, 256
 dev = "cuda"

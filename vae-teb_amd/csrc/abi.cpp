@@ -2,6 +2,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <atomic>
+
 #include "common.h"
 
 namespace vt {
@@ -29,32 +31,41 @@ int vt_abi_version(void) { return 1; }
 // re-recorded once its waits are enqueued; the ring is far larger than the forks
 // of one step.  Under hipGraph capture both calls become graph dependencies.
 namespace {
-constexpr int kForkEvents = 1024;
-hipEvent_t g_fork_ev[kForkEvents];
-int g_fork_next = 0;
+constexpr int kForkEvents = 1024, kMaxDevices = 16;
+// one ring per device (an event is created on, and may only be recorded on streams of,
+// the device current at its creation); the index advances atomically, so marks from
+// several host threads take distinct slots.  slot = device * kForkEvents + index.
+hipEvent_t g_fork_ev[kMaxDevices][kForkEvents];
+std::atomic<unsigned> g_fork_next[kMaxDevices];
 }  // namespace
 
 extern "C" int vt_stream_mark(void* stream, int* slot) {
-    const int i = g_fork_next;
-    g_fork_next = (i + 1) % kForkEvents;
-    if (!g_fork_ev[i] && hipEventCreateWithFlags(&g_fork_ev[i], hipEventDisableTiming) != hipSuccess) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+        vt::set_error("vt_stream_mark: device %d (at most %d devices)", dev, kMaxDevices);
+        return VT_ERR_ARG;
+    }
+    const int i = (int)(g_fork_next[dev].fetch_add(1, std::memory_order_relaxed) % kForkEvents);
+    hipEvent_t& ev = g_fork_ev[dev][i];
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
         vt::set_error("vt_stream_mark: hipEventCreateWithFlags failed");
         return VT_ERR_HIP;
     }
-    if (hipEventRecord(g_fork_ev[i], (hipStream_t)stream) != hipSuccess) {
+    if (hipEventRecord(ev, (hipStream_t)stream) != hipSuccess) {
         vt::set_error("vt_stream_mark: %s", hipGetErrorString(hipGetLastError()));
         return VT_ERR_HIP;
     }
-    *slot = i;
+    *slot = dev * kForkEvents + i;
     return VT_OK;
 }
 
 extern "C" int vt_stream_wait_mark(void* stream, int slot) {
-    if (slot < 0 || slot >= kForkEvents || !g_fork_ev[slot]) {
+    const int dev = slot / kForkEvents, i = slot % kForkEvents;
+    if (slot < 0 || dev >= kMaxDevices || !g_fork_ev[dev][i]) {
         vt::set_error("vt_stream_wait_mark: bad slot %d", slot);
         return VT_ERR_ARG;
     }
-    if (hipStreamWaitEvent((hipStream_t)stream, g_fork_ev[slot], 0) != hipSuccess) {
+    if (hipStreamWaitEvent((hipStream_t)stream, g_fork_ev[dev][i], 0) != hipSuccess) {
         vt::set_error("vt_stream_wait_mark: %s", hipGetErrorString(hipGetLastError()));
         return VT_ERR_HIP;
     }

@@ -53,6 +53,77 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
     return r;
 }
 
+// Window staging with lanes along channels (the default; g_conv_cl): thread t stages
+// channel c0 + (t & 31) of rows (t >> 5) + 8 i, so a wave-instruction reads two
+// 128-B row segments (2-4 cache lines) instead of 4 channels in each of 16 rows, and
+// the BatchNorm-backward parameters of its one channel sit in registers.  U rows per
+// round, all their loads issued before the first use.  Same values and the same bf16
+// roundings as the octet staging below (bit-identical results).
+template <int K, int WIN, bool BNB>
+__device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const float* __restrict__ xb,
+                                                const float* __restrict__ x2b, const Geo& g, int t0, int TP, int Lo,
+                                                int c0, const float* __restrict__ bp, int act, float invM,
+                                                __bf16* __restrict__ dbf, int b, bool write_dbf) {
+    constexpr int NR = (WIN + 7) / 8, U = K <= 3 ? 3 : 6;
+    const int tid = threadIdx.x, cl = tid & 31, rg = tid >> 5;
+    const int c = c0 + cl;
+    const bool cok = c < g.Cin;
+    const int cc = cok ? c : 0;
+    float pm = 0.f, prs = 0.f, pga = 0.f, pbe = 0.f, pdg = 0.f, pdb = 0.f;
+    if constexpr (BNB) {
+        pm = bp[cc];
+        prs = bp[g.Cin + cc];
+        pga = bp[2 * g.Cin + cc];
+        pbe = bp[3 * g.Cin + cc];
+        pdg = bp[4 * g.Cin + cc];
+        pdb = bp[5 * g.Cin + cc];
+    }
+    const int cpad = (g.Cin + 7) & ~7;
+#pragma unroll
+    for (int i0 = 0; i0 < NR; i0 += U) {
+        float a[U], q[U], l1[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = rg + 8 * (i0 + u);
+            const int tp = t0 + r;
+            const bool rin = i0 + u < NR && r < WIN && tp < Lo + K - 1 && cok;
+            if constexpr (BNB) {
+                const int t = tp - g.pad;   // causal geometry: zero outside [0, L_in)
+                ok[u] = rin && t >= 0 && t < g.L_in;
+                const int64_t off = ok[u] ? (int64_t)t * g.Cin + c : 0;
+                a[u] = xb[off];
+                q[u] = x2b[off];
+                l1[u] = 0.f;
+            } else {
+                int i0r = 0, i1r = 0;
+                float w1 = 0.f;
+                ok[u] = rin && src_row(g, tp, i0r, i1r, w1);
+                a[u] = xb[ok[u] ? (int64_t)i0r * g.Cin + c : 0];
+                q[u] = g.up ? xb[ok[u] ? (int64_t)i1r * g.Cin + c : 0] : 0.f;
+                l1[u] = w1;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = rg + 8 * (i0 + u);
+            if (i0 + u >= NR || r >= WIN) continue;
+            float v = 0.f;
+            if (ok[u]) {
+                if constexpr (BNB) v = bn_bwd_val_r(a[u], q[u], pm, prs, pga, pbe, pdg, pdb, act, invM);
+                else v = g.up ? (1.f - l1[u]) * a[u] + l1[u] * q[u] : a[u];
+            }
+            xs[r * RS + cl] = (__bf16)v;
+            if constexpr (BNB) {
+                const int t = t0 + r - g.pad;
+                if (write_dbf && ok[u] && t >= t0 && t < t0 + TP) dbf[((int64_t)b * g.L_in + t) * cpad + c] = (__bf16)v;
+            }
+        }
+    }
+}
+
+int g_conv_cl = 1;   // window staging: 1 lanes along channels (stage_window_cl), 0 octets (vt_conv_bf16_set_staging)
+
 // x: fp32 (B, L_in, g.Cin) activations; w16: [g.Cout][K][cin32] bf16 shadow.
 // BNB (backward-data only: causal geometry, no upsample): x is the block output
 // gradient dy and the staged operand is the BatchNorm input gradient computed on
@@ -60,7 +131,7 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
 // dbf (BNB, nullable): the staged BN input gradient, bf16, is also written to
 // dbf[(b L_in + t) cpad + c] (cpad = ceil8(Cin)) by the blockIdx.y == 0 workgroups
 // for their own rows t0 .. t0 + TP - 1 (each row once) — the weight gradient's operand.
-template <int K, int NT, bool BNB = false>
+template <int K, int NT, bool BNB = false, bool CL = true>
 __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, Geo g, const __bf16* __restrict__ w16,
                                                    int cin32, float* __restrict__ y, int Lo,
                                                    float* __restrict__ stats, const float* __restrict__ x2,
@@ -86,7 +157,34 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int c0 = 0; c0 < g.Cin; c0 += CB) {
-        if constexpr (K <= 3) {
+        if constexpr (CL) {
+            // taps (K x TC rows x 4 octets, 16 B each from the shadow): loads first, stores
+            // after the window
+            constexpr int NWI = (K * TC * 4 + 255) / 256;
+            bf16x8 wt[NWI];
+#pragma unroll
+            for (int it = 0; it < NWI; ++it) {
+                const int i = tid + 256 * it;
+                const int ic = i < K * TC * 4 ? i : K * TC * 4 - 1;
+                const int oct = ic & 3, r = ic >> 2, k = r / TC, co = r - k * TC;
+                const int coc = co0 + co < g.Cout ? co0 + co : g.Cout - 1;
+                wt[it] = *(const bf16x8*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
+            }
+            stage_window_cl<K, WIN, BNB>(xs, xb, x2b, g, t0, TP, Lo, c0, bp, act, invM, dbf, b,
+                                         BNB && dbf && blockIdx.y == 0);
+#pragma unroll
+            for (int it = 0; it < NWI; ++it) {
+                const int i = tid + 256 * it;
+                if (i >= K * TC * 4) continue;
+                const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
+                bf16x8 val = wt[it];
+                if (co0 + co >= g.Cout) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
+                }
+                *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = val;
+            }
+        } else if constexpr (K <= 3) {
             // small K (few taps, little MFMA work per staged row): the per-element staging
             // keeps the register count, and with it the occupancy, low (measured faster)
             for (int i = tid; i < WIN * 4; i += 256) {
@@ -488,12 +586,18 @@ int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, 
           hipStream_t st, const BnB* bn, FoldOut fo) {
     using C = BCfg<K, NT>;
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
-    if (x && bn)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
+    if (x && bn && g_conv_cl)
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, true, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
                            cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo);
+    else if (x && bn)
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, true, false>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g,
+                           w16, cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo);
+    else if (x && g_conv_cl)
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
+                           Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo);
     else if (x)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y, Lo, stats,
-                           nullptr, nullptr, 0, 0.f, nullptr, fo);
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, false>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
+                           Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo);
     return C::TP;
 }
 
@@ -556,6 +660,11 @@ constexpr int KMAXB = 11;
 using namespace vt;
 
 extern "C" {
+
+int vt_conv_bf16_set_staging(int channel_lanes) {
+    g_conv_cl = channel_lanes ? 1 : 0;
+    return VT_OK;
+}
 
 int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, void* w16t, void* stream) {
     VT_CHECK_ARG(Cout > 0 && Cin > 0 && K > 0 && K <= KMAXB, "vt_conv1d_bf16_shadow: shape");

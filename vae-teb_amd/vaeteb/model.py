@@ -572,6 +572,10 @@ class SeqVaeTeb(nn.Module):
         # makes ROCm 7's hipStreamEndCapture segfault, as the head-gradient branch below)
         if getattr(self, "_prepassed", False):
             self._prepassed = False            # done ahead of this forward (prepass())
+            if not self.training:
+                # the prepass counted a training step, but this forward runs in eval mode
+                # (e.g. a frozen VAE switched by its classifier wrapper): take it back
+                self._bn_counters().sub_(1)
         elif _PAR["on"] and self.training and PREPASS and not torch.cuda.is_current_stream_capturing():
             self._prepass()
         else:
@@ -614,6 +618,8 @@ class SeqVaeTeb(nn.Module):
         """Run the weight-only prepass now, ahead of the next training forward (the
         trainer calls it before the front-end, so it overlaps that); the forward
         then skips its own."""
+        if getattr(self, "_prepassed", False):
+            return   # already done for the coming forward (counted once)
         if (self.concurrent_encoders and self.training and PREPASS and torch.cuda.is_available()
                 and next(self.parameters()).is_cuda and not torch.cuda.is_current_stream_capturing()):
             self._prepass()
