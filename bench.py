@@ -267,12 +267,12 @@ def main():
     ap.add_argument("--serial-encoders", action="store_true",
                     help="run the source / target encoders on one stream (default: two HIP streams)")
     ap.add_argument("--heads", choices=["bf16", "fp32"], default="bf16",
-                    help="decoder R x R head GEMMs: bf16 MFMA (the reference trains under 16-bit autocast) or fp32")
+                    help="decoder R x R head GEMMs: bf16 MFMA (the reference trains in fp16 autocast; bf16 is the documented deviation, DESIGN.md §5) or fp32")
     ap.add_argument("--conv", choices=["bf16", "fp32"], default="bf16",
-                    help="conv blocks: bf16 MFMA with fp32 accumulation / BatchNorm (16-bit autocast) or exact fp32")
+                    help="conv blocks: bf16 MFMA with fp32 accumulation / BatchNorm (bf16 for the reference's fp16 autocast) or exact fp32")
     ap.add_argument("--mlp", choices=["bf16", "fp32"], default="bf16",
                     help="ResidualMLP stacks: Linear layers on bf16 MFMA with fp32 accumulation, LayerNorm fp32 "
-                         "(16-bit autocast) or exact fp32")
+                         "(bf16 for the reference's fp16 autocast) or exact fp32")
     args = ap.parse_args()
 
     rank, world, local, dev = init_distributed()

@@ -103,6 +103,12 @@ int vt_fe_set_pairs_stamps(void* buf);
  *           (C,S)->(S,C) transpose :758-759                                              */
 int vt_fe_normalize(const float* in, int64_t B, int C, int in_C, int S, const int* kind, const float* mean, const float* stdv,
                     float log_eps, float* out, int out_C, int out_off, void* stream);
+/* The same on the steps [s0, s0 + S_len) of input rows of in_S steps: the dataset's
+ * trim of trim_minutes at each end (ref/hdf5_dataset/hdf5_dataset.py:359-364, :733-741;
+ * 2 minutes = 30 decimated steps of a 5760-point window -> 300) fused into the pass.    */
+int vt_fe_normalize_window(const float* in, int64_t B, int C, int in_C, int in_S, int s0, int S_len,
+                           const int* kind, const float* mean, const float* stdv, float log_eps, float* out,
+                           int out_C, int out_off, void* stream);
 /* fhr / up: (x-mean)/(std+1e-8)  (hdf5_dataset.py:78-80)                                */
 int vt_normalize_raw(const float* x, int64_t rows, int64_t row_stride, int N, float mean, float stdv, float* out,
                      void* stream);
@@ -191,6 +197,9 @@ int vt_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, f
 int vt_adamw_set_vector(int on);
 /* bf16 (RNE) shadow copy of fp32 data, for MFMA operands.                         */
 int vt_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
+/* dst = float(src) for bf16 src (exact).  With vt_cast_bf16: the optional bf16 gradient
+ * all-reduce of the data-parallel step (vaeteb.train.GradBuckets(reduce_dtype=bfloat16)). */
+int vt_cast_bf16_to_f32(const void* src, float* dst, int64_t n, void* stream);
 
 /* --------------------------------------------------------------- dense layers
  * fp32 tiled GEMM engine (gemm.hip).  Activations are row-major (rows, C);
@@ -245,7 +254,7 @@ int vt_resmlp_bwd(int n_layers, const int* dims, const int* layer_ln, const int*
  * The same ResidualMLP (ref/model/vae_teb_model.py:336-403, same arguments and
  * parameter / gradient layout as vt_resmlp_*) with every Linear on bf16 MFMA
  * (v_mfma_f32_16x16x32_bf16, fp32 accumulation) — the reference trains under
- * 16-bit autocast (ref/model/graph_model.py:510, :709-711): Linear in 16 bit,
+ * fp16 autocast (ref/model/graph_model.py:510, :709-711; bf16 here): Linear in 16 bit,
  * LayerNorm, activations, the saved state and every reduction in fp32.  The
  * saved xhat / rstd (sizes[0], sizes[1] floats) use this family's own layout
  * (pass them only to vt_resmlp_bf16_bwd); the backward needs sizes[2] floats of
@@ -267,7 +276,7 @@ int vt_resmlp_bf16_set_stamps(void* buf);
 /* ------------------------------------------------------- bf16 MFMA (heads)
  * The decoder's R x R output heads (Decoder.output_mu / output_logvar,
  * ref/model/vae_teb_model.py:882-897,926-927, R = 16*S; the reference runs
- * them under 16-bit autocast, ref/model/graph_model.py:510,710) as bf16 MFMA GEMMs
+ * them in fp16 autocast, ref/model/graph_model.py:510,710; bf16 here) as bf16 MFMA GEMMs
  * (v_mfma_f32_16x16x32_bf16, fp32 accumulation).  Same meaning as vt_linear_*;
  * the weight operand is a bf16 shadow of the fp32 master weight W [N][K]:
  * W16 = bf16(W) [N][K] for the forward, W16t = bf16(W)^T [K][N] for the input
@@ -310,16 +319,17 @@ int vt_conv1d_bn_fwd(const float* X, int B, int L_in, int Cin, const float* W, i
                      const float* gamma, const float* beta, int act, float eps, float momentum, float* conv_out,
                      float* Y, float* mean, float* rstd, float* run_mean, float* run_var, float* ws,
                      int64_t ws_floats, void* stream);
-/* bf16-MFMA variants (conv_bf16.hip) — the reference trains under 16-bit
+/* bf16-MFMA variants (conv_bf16.hip) — the reference trains in fp16 (bf16 here) under
  * autocast (ref/model/graph_model.py:510, :709-711): bf16 operands, fp32
  * accumulation, fp32 activations and BatchNorm.  Weights come from a bf16
  * shadow refreshed from the fp32 master weight W [Cout][Cin][K] once per
  * step: w16 [Cout][K][ceil32(Cin)] (forward), w16t [Cin][K][ceil32(Cout)]
  * = W[co][ci][K-1-k] (backward-data), zero-padded.                             */
 int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, void* w16t, void* stream);
-/* Operand-window staging of the bf16 conv kernels: 1 (default) lanes along channels
- * (coalesced row segments), 0 the octet-per-lane staging; bit-identical results (A/B). */
-int vt_conv_bf16_set_staging(int channel_lanes);
+/* Operand-window staging of the bf16 conv kernels (A/B; bit-identical results):
+ * 0 octets per lane, 2 lanes along channels (coalesced row segments), 1 (default) lanes
+ * along channels for the fused-BN backward-data kernels with K >= 7, octets elsewhere. */
+int vt_conv_bf16_set_staging(int mode);
 int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode,
                           int up, const float* gamma, const float* beta, int act, float eps, float momentum,
                           float* conv_out, float* Y, float* mean, float* rstd, float* run_mean, float* run_var,

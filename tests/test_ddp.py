@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, bucket_mb, q):
+def _worker(rank, world, port, bucket_mb, q, reduce_dtype=torch.float32):
     sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -31,7 +31,7 @@ def _worker(rank, world, port, bucket_mb, q):
     model = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64), torch.nn.ReLU(),
                                 torch.nn.Linear(64, 3))
     st = FlatState(model)
-    gb = GradBuckets(st, None, bucket_mb=bucket_mb)
+    gb = GradBuckets(st, None, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype)
     results = []
     for step in range(2):
         st.zero_grad()
@@ -83,3 +83,37 @@ def test_bucketed_allreduce_matches_full_batch_average(bucket_mb):
         # backward hooks (overlapped), not at finish()
         assert all(f >= n_buckets - 1 for f in out[0][2])
     assert all(o[4] for o in out)
+
+
+def test_bucketed_allreduce_bf16():
+    """GradBuckets(reduce_dtype=bfloat16): each bucket rounded to bf16, reduced in bf16,
+    widened back into the fp32 gradient buffer == the sum of the ranks' bf16-rounded
+    gradients in bf16 arithmetic (2 ranks: one rounding of the sum), within bf16
+    rounding (rel-L2 2^-8) of the fp32 average."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 0.01, q, torch.bfloat16)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    ref_model = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64),
+                                    torch.nn.ReLU(), torch.nn.Linear(64, 3))
+    for step in range(2):
+        grads = []
+        for rank in range(world):
+            ref_model.zero_grad()
+            g = torch.Generator().manual_seed(100 * step + rank)
+            ref_model(torch.randn(8, 16, generator=g)).pow(2).mean().backward()
+            grads.append(torch.cat([p.grad.reshape(-1) for p in reversed(list(ref_model.parameters()))]))
+        exp = (grads[0].bfloat16() + grads[1].bfloat16()).float() / world
+        for rank in range(world):
+            assert torch.equal(out[rank][1][step], exp), (rank, step)
+        avg = (grads[0] + grads[1]) / world
+        # elementwise the sum can cancel; overall the bf16 reduce is within bf16 rounding
+        assert ((out[0][1][step] - avg).norm() / avg.norm()).item() < 2 ** -8

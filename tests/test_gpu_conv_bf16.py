@@ -280,7 +280,7 @@ def test_window_staging_channel_lanes_bitwise(L, geo):
     cp = (Cout + 7) // 8 * 8
     outs = []
     try:
-        for cl in (0, 1):
+        for cl in (0, 2):
             L.call("vt_conv_bf16_set_staging", cl)
             y = torch.full((B, Lo, Cout), float("nan"), device="cuda")
             L.call("vt_conv1d_fwd_bf16", L.ptr(x), B, Lin, Cin, L.ptr(w16), Cout, K, mode, up, L.ptr(y), L.stream())

@@ -100,24 +100,32 @@ def test_scattering_vs_oracle(request, cfg):
     assert_ref_precision(rel_rows(S, S64), rel_rows(S32, S64), what="scattering")
 
 
-@pytest.mark.parametrize("J,Q", [(11, 4), (6, 1)])
-def test_frontend_vs_reference_golden(golden, request, J, Q):
-    """Feed the reference's fixture windows; compare against the reference's own outputs."""
-    fe = request.getfixturevalue("fe11" if J == 11 else "fe6")
-    g = _golden_x(golden, J, Q)
+@pytest.fixture(scope="module")
+def fe11_5760():
+    dev = _dev()
+    from vaeteb.frontend import FrontEnd, FrontEndPlan, load_stats
+    return FrontEnd(FrontEndPlan(11, 4, 16, 5760, device=dev), load_stats(11, 4, 16, 4096))
+
+
+@pytest.mark.parametrize("J,Q,N", [(11, 4, 4096), (6, 1, 4096), (11, 4, 5760)])
+def test_frontend_vs_reference_golden(golden, request, J, Q, N):
+    """Feed the reference's fixture windows; compare against the reference's own outputs.
+    N = 5760 is the reference's own dataset window (create_hdf5_dataset.py:360: 360 steps)."""
+    fe = request.getfixturevalue({(11, 4096): "fe11", (6, 4096): "fe6", (11, 5760): "fe11_5760"}[(J, N)])
+    g = golden(f"frontend_j{J}q{Q}t16_n{N}")
     x = g["x"]
     r = fe.raw(torch.from_numpy(x).cuda())
     assert_ref_precision(rel_rows(r["fhr_st"].cpu().numpy(), g["fhr_st64"]), rel_rows(g["fhr_st"], g["fhr_st64"]),
                          what="fhr_st")
     pairs = r["pairs"].cpu().numpy()
     nph = fe.C_ph
-    fe64 = F.PhaseFrontEnd(J, Q, 16, 4096, dtype=np.float64)
+    fe64 = F.PhaseFrontEnd(J, Q, 16, N, dtype=np.float64)
     a64 = fe64.analytic(x[:, [0, 1]])
     pm, cm = g["phase_mask"], g["cross_mask"]
     for key, out, sel, ai, aj in (("fhr_ph", pairs[:, :nph], pm, a64[:, 0], a64[:, 0]),
                                   ("fhr_up_ph", pairs[:, nph:], cm, a64[:, 0], a64[:, 1])):
         ii, jj = fe64.i_idx[sel], fe64.j_idx[sel]
-        scale = np.sqrt((fe64._lowpass(np.abs(ai[:, ii]) * np.abs(aj[:, jj]) + 0j, 256) ** 2).sum(-1))
+        scale = np.sqrt((fe64._lowpass(np.abs(ai[:, ii]) * np.abs(aj[:, jj]) + 0j, fe.plan.S) ** 2).sum(-1))
         err = np.sqrt(((out - g[key + "64"]) ** 2).sum(-1)) / scale
         ref_err = np.sqrt(((g[key] - g[key + "64"]) ** 2).sum(-1)) / scale
         assert err.max() <= 2 * ref_err.max() + 1e-5, (key, err.max(), ref_err.max())

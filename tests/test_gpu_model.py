@@ -8,6 +8,8 @@ tests/golden/model_s*.npz (fp32 CPU reference vs fp32 HIP: different
 summation orders through a 4-layer LSTM and 17 train-mode BatchNorms, so
 per-tensor rel-L2 <= 2e-4 for gradients and 1e-5 for the losses).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -479,3 +481,52 @@ def test_prepass_and_deferred_lstm_grads_bitwise(golden, monkeypatch, defer):
     for r in res[1:]:
         assert res[0][0] == r[0]
         assert torch.equal(res[0][1], r[1]) and torch.equal(res[0][2], r[2])
+
+
+_HANDOFF_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [{pkg!r}]
+from vaeteb import ops
+d = np.load({inp!r})
+x = torch.from_numpy(d["x"]).cuda()
+params = [torch.from_numpy(d[f"p{{i}}"]).cuda() for i in range(4)]
+ops.LSTM_FUSED = 1
+y = ops.lstm(x, params)
+torch.cuda.synchronize()
+np.save({out!r}, y.cpu().numpy())
+"""
+
+
+@pytest.mark.parametrize("In,B,S", [(64, 4, 64), (20, 3, 48), (32, 2, 80)])
+def test_lstm_fused_chunk_handoff_bitwise_fresh_process(ops, tmp_path, In, B, S):
+    """The fused forward kernel (k_lstm_fwd_x) issues the NEXT chunk's input projection
+    behind each step's barrier and hands it to the lanes at the chunk boundary; round 2
+    found an operand read hoisted ahead of that barrier, which made the first steps of
+    a process intermittently wrong.  Pinned here: S a multiple of the 16-step chunk with
+    several chunks, the layer's outputs bitwise equal to the plain path (separate
+    projection GEMM + recurrence) on 8 back-to-back launches in this process AND on the
+    first launch of a fresh process."""
+    import subprocess
+    import sys
+    import numpy as np
+    torch.manual_seed(In * 10 + S)
+    ref = torch.nn.LSTM(In, 64, 1, batch_first=True)
+    x = torch.randn(B, S, In)
+    params = [p.detach().clone() for p in ref.parameters()]
+    ops.LSTM_FUSED = 0
+    try:
+        with torch.no_grad():
+            y0 = ops.lstm(x.cuda(), [p.cuda() for p in params])
+        ops.LSTM_FUSED = 1
+        with torch.no_grad():
+            for _ in range(8):
+                y1 = ops.lstm(x.cuda(), [p.cuda() for p in params])
+                assert torch.equal(y0, y1), (y0 != y1).nonzero()[:4]
+    finally:
+        ops.LSTM_FUSED = 1
+    inp, out = str(tmp_path / "in.npz"), str(tmp_path / "out.npy")
+    np.savez(inp, x=x.numpy(), **{f"p{i}": p.numpy() for i, p in enumerate(params)})
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "vae-teb_amd")
+    code = _HANDOFF_SCRIPT.format(pkg=pkg, inp=inp, out=out)
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=120)
+    assert np.array_equal(np.load(out), y0.cpu().numpy())

@@ -137,7 +137,9 @@ def _frontend_double(m):
 
 def gen_frontend():
     from kymatio_phase_scattering import KymatioPhaseScattering1D
-    for (J, Q, T, N, B) in [(11, 4, 16, 4096, 2), (6, 1, 16, 4096, 2)]:
+    # N = 5760: the reference's own dataset windows (create_hdf5_dataset.py:360, 360 steps -> 300 after
+    # the 30-step trim of hdf5_dataset.py:359-364)
+    for (J, Q, T, N, B) in [(11, 4, 16, 4096, 2), (6, 1, 16, 4096, 2), (11, 4, 16, 5760, 2)]:
         x = synthetic.batch(2000, B, N)
         outs = {}
         for tag, prec in (("", torch.float32), ("64", torch.float64)):
@@ -387,7 +389,7 @@ def gen_amp():
 
 
 def gen_model():
-    for (S, B, full) in [(16, 4, True), (4, 3, True), (256, 2, False)]:
+    for (S, B, full) in [(16, 4, True), (4, 3, True), (256, 2, False), (300, 2, False)]:
         rng = np.random.Generator(np.random.PCG64(7 + S))
         y_st = rng.standard_normal((B, S, 43)).astype(np.float32)
         y_ph = rng.standard_normal((B, S, 44)).astype(np.float32)

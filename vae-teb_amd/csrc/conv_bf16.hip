@@ -1,6 +1,6 @@
 // bf16-MFMA 1-D convolution for the conv blocks (SURVEY.md §8(a) a11, a15;
 // ref/model/vae_teb_model.py:128-253) in the reference's training precision:
-// the reference trains under 16-bit autocast (Lightning precision="16-mixed",
+// the reference trains in fp16 autocast (bf16 here: DESIGN.md §5; Lightning precision="16-mixed",
 // ref/model/graph_model.py:510; torch.amp.autocast, :709-711), i.e. conv
 // operands in 16 bits with fp32 accumulation.  Here: bf16 operands on
 // v_mfma_f32_16x16x32_bf16 (16x the fp32 MFMA rate), fp32 accumulation, fp32
@@ -82,7 +82,7 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
 #pragma unroll
     for (int i0 = 0; i0 < NR; i0 += U) {
         float a[U], q[U], l1[U];
-        bool ok[U];
+        bool ok[U], rok[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int r = rg + 8 * (i0 + u);
@@ -90,6 +90,7 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
             const bool rin = i0 + u < NR && r < WIN && tp < Lo + K - 1 && cok;
             if constexpr (BNB) {
                 const int t = tp - g.pad;   // causal geometry: zero outside [0, L_in)
+                rok[u] = i0 + u < NR && r < WIN && tp < Lo + K - 1 && t >= 0 && t < g.L_in;
                 ok[u] = rin && t >= 0 && t < g.L_in;
                 const int64_t off = ok[u] ? (int64_t)t * g.Cin + c : 0;
                 a[u] = xb[off];
@@ -98,6 +99,7 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
             } else {
                 int i0r = 0, i1r = 0;
                 float w1 = 0.f;
+                rok[u] = false;
                 ok[u] = rin && src_row(g, tp, i0r, i1r, w1);
                 a[u] = xb[ok[u] ? (int64_t)i0r * g.Cin + c : 0];
                 q[u] = g.up ? xb[ok[u] ? (int64_t)i1r * g.Cin + c : 0] : 0.f;
@@ -115,14 +117,21 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
             }
             xs[r * RS + cl] = (__bf16)v;
             if constexpr (BNB) {
+                // the bf16 side output: the row's channels and its zero channel padding up to cpad
                 const int t = t0 + r - g.pad;
-                if (write_dbf && ok[u] && t >= t0 && t < t0 + TP) dbf[((int64_t)b * g.L_in + t) * cpad + c] = (__bf16)v;
+                if (write_dbf && rok[u] && c < cpad && t >= t0 && t < t0 + TP)
+                    dbf[((int64_t)b * g.L_in + t) * cpad + c] = (__bf16)v;
             }
         }
     }
 }
 
-int g_conv_cl = 1;   // window staging: 1 lanes along channels (stage_window_cl), 0 octets (vt_conv_bf16_set_staging)
+// window staging (vt_conv_bf16_set_staging): 0 octets per lane, 2 lanes along channels everywhere,
+// 1 (default) lanes along channels for the fused-BN backward-data kernels with K >= 7 only —
+// measured in isolation (tools/conv_micro.py): K 11 / 9 / 7 BNB 98 / 91 / 105 -> 82 / 82 / 92 us,
+// but the forward and every K = 3 instance slower (K 3 BNB 32 -> 260 us: 11-33 channel rows
+// leave most of the 32 channel lanes idle)
+int g_conv_cl = 1;
 
 // x: fp32 (B, L_in, g.Cin) activations; w16: [g.Cout][K][cin32] bf16 shadow.
 // BNB (backward-data only: causal geometry, no upsample): x is the block output
@@ -586,13 +595,14 @@ int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, 
           hipStream_t st, const BnB* bn, FoldOut fo) {
     using C = BCfg<K, NT>;
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
-    if (x && bn && g_conv_cl)
+    const bool cl = g_conv_cl == 2 || (g_conv_cl == 1 && bn && K >= 7);
+    if (x && bn && cl)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, true, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
                            cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo);
     else if (x && bn)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, true, false>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g,
                            w16, cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo);
-    else if (x && g_conv_cl)
+    else if (x && cl)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
                            Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo);
     else if (x)
@@ -661,8 +671,9 @@ using namespace vt;
 
 extern "C" {
 
-int vt_conv_bf16_set_staging(int channel_lanes) {
-    g_conv_cl = channel_lanes ? 1 : 0;
+int vt_conv_bf16_set_staging(int mode) {
+    VT_CHECK_ARG(mode >= 0 && mode <= 2, "vt_conv_bf16_set_staging: mode %d not in 0..2", mode);
+    g_conv_cl = mode;
     return VT_OK;
 }
 

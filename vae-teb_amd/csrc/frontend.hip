@@ -481,14 +481,15 @@ __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
 // ---------------------------------------------------------------- normalise
 // in (B, C, S) raw -> out[b, s, off + c] with row width out_C.
 // kind: 0 = z-score only, 1 = log(max(x,0)+eps) then z, 2 = asinh then z.
-__global__ void k_fe_normalize(const float* __restrict__ in, int C, int in_C, int S, const int* __restrict__ kind,
-                               const float* __restrict__ mean, const float* __restrict__ stdv, float log_eps,
-                               float* __restrict__ out, int out_C, int out_off) {
+__global__ void k_fe_normalize(const float* __restrict__ in, int C, int in_C, int in_S, int s0, int S,
+                               const int* __restrict__ kind, const float* __restrict__ mean,
+                               const float* __restrict__ stdv, float log_eps, float* __restrict__ out, int out_C,
+                               int out_off) {
     const int64_t b = blockIdx.y;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= C * S) return;
     const int c = idx % C, s = idx / C;  // consecutive threads -> consecutive output channels
-    float v = in[(b * in_C + c) * S + s];
+    float v = in[(b * in_C + c) * in_S + s0 + s];
     const int k = kind[c];
     if (k == 1) v = logf(fmaxf(v, 0.f) + log_eps);
     else if (k == 2) v = asinhf(v);
@@ -777,14 +778,22 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
     return VT_OK;
 }
 
+int vt_fe_normalize_window(const float* in, int64_t B, int C, int in_C, int in_S, int s0, int S_len,
+                           const int* kind, const float* mean, const float* stdv, float log_eps, float* out,
+                           int out_C, int out_off, void* stream) {
+    VT_CHECK_ARG(B > 0 && C > 0 && S_len > 0 && out_off + C <= out_C && in_C >= C && s0 >= 0 && s0 + S_len <= in_S,
+                 "vt_fe_normalize_window: shape");
+    dim3 grid((C * S_len + 255) / 256, (unsigned)B);
+    hipLaunchKernelGGL(k_fe_normalize, grid, dim3(256), 0, S(stream), in, C, in_C, in_S, s0, S_len, kind, mean, stdv,
+                       log_eps, out, out_C, out_off);
+    VT_LAUNCH_CHECK("vt_fe_normalize_window");
+    return VT_OK;
+}
+
 int vt_fe_normalize(const float* in, int64_t B, int C, int in_C, int S_len, const int* kind, const float* mean,
                     const float* stdv, float log_eps, float* out, int out_C, int out_off, void* stream) {
-    VT_CHECK_ARG(B > 0 && C > 0 && S_len > 0 && out_off + C <= out_C && in_C >= C, "vt_fe_normalize: shape");
-    dim3 grid((C * S_len + 255) / 256, (unsigned)B);
-    hipLaunchKernelGGL(k_fe_normalize, grid, dim3(256), 0, S(stream), in, C, in_C, S_len, kind, mean, stdv, log_eps, out,
-                       out_C, out_off);
-    VT_LAUNCH_CHECK("vt_fe_normalize");
-    return VT_OK;
+    return vt_fe_normalize_window(in, B, C, in_C, S_len, 0, S_len, kind, mean, stdv, log_eps, out, out_C, out_off,
+                                  stream);
 }
 
 int vt_normalize_raw(const float* x, int64_t rows, int64_t row_stride, int N, float mean, float stdv, float* out,

@@ -11,58 +11,13 @@
 #include <math.h>
 
 #include "common.h"
+#include "lstm_cell.h"
 #include "skinny.h"
 
 namespace vt {
 
 static constexpr int H = 64;
 static constexpr int G4 = 4 * H;
-
-// Recurrence-latency transcendentals on the hardware v_exp_f32 / v_rcp_f32
-// (~1 ulp each) — the libm expf / tanhf / IEEE divide sequences are dozens of
-// dependent instructions on the per-step critical path:
-//   sigmoid(x) = 1 / (1 + 2^(-x log2 e))                (relative error ~2 ulp)
-//   tanh(x)    = odd Taylor polynomial to x^11 for |x| < 0.3 (truncation 2e-9),
-//                else sign(x) (1 - 2 / (e^{2|x|} + 1))   (relative error < 4e-7)
-// Relative (not just absolute) accuracy near 0 matters: h = o tanh(c) feeds
-// deep LayerNorm stacks whose gradients amplify relative input errors
-// (the 33-layer target mu_layer; tests/test_gpu_classifier.py).
-__device__ __forceinline__ float sigm(float x) {
-    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
-}
-__device__ __forceinline__ float ftanh(float x) {
-    const float ax = fabsf(x), x2 = x * x;
-    float p = -0.00886323552990220f;            // -1382/155925
-    p = fmaf(p, x2, 0.0218694885361552f);       //  62/2835
-    p = fmaf(p, x2, -0.0539682539682540f);      // -17/315
-    p = fmaf(p, x2, 0.133333333333333f);        //  2/15
-    p = fmaf(p, x2, -0.333333333333333f);       // -1/3
-    const float small = fmaf(x * x2, p, x);
-    const float e = __builtin_amdgcn_exp2f(2.88539008177792681f * ax);   // e^{2|x|}
-    const float big = copysignf(fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f), x);
-    return ax < 0.3f ? small : big;
-}
-
-// The cell arithmetic of one step, shared by the plain and the fused kernels so
-// both give the same bits wherever they are inlined: contraction is spelled out
-// (fmaf) and otherwise off, so the compiler's choice cannot depend on context.
-__device__ __forceinline__ float cell_fwd_c(float c, float gi, float gf, float gg) {
-#pragma clang fp contract(off)
-    return fmaf(gf, c, gi * gg);
-}
-__device__ __forceinline__ void cell_bwd(float dh, float gi, float gf, float gg, float go, float c, float cp, float& dc,
-                                         float& v0, float& v1, float& v2, float& v3) {
-#pragma clang fp contract(off)
-    const float tc = ftanh(c);
-    const float d_o = dh * tc;
-    dc = fmaf(dh * go, fmaf(-tc, tc, 1.f), dc);
-    const float di = dc * gg, dgg = dc * gi, df = dc * cp;
-    dc = dc * gf;
-    v0 = di * gi * (1.f - gi);
-    v1 = df * gf * (1.f - gf);
-    v2 = dgg * fmaf(-gg, gg, 1.f);
-    v3 = d_o * go * (1.f - go);
-}
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic,
 // not for its global stores / prefetch loads (__syncthreads() would drain

@@ -171,6 +171,11 @@ __global__ void k_cast_bf16(const float* __restrict__ src, uint16_t* __restrict_
     }
 }
 
+__global__ void k_bf16_to_f32(const uint16_t* __restrict__ src, float* __restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = __uint_as_float((uint32_t)src[i] << 16);
+}
+
 static inline int grid_for(int64_t n, int cap) {
     int64_t b = (n + OPT_THREADS - 1) / OPT_THREADS;
     return (int)(b < 1 ? 1 : (b > cap ? cap : b));
@@ -242,6 +247,14 @@ int vt_cast_bf16(const float* src, void* dst, int64_t n, void* stream) {
     VT_CHECK_ARG(n > 0, "vt_cast_bf16: empty");
     hipLaunchKernelGGL(k_cast_bf16, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, S(stream), src, (uint16_t*)dst, n);
     VT_LAUNCH_CHECK("vt_cast_bf16");
+    return VT_OK;
+}
+
+int vt_cast_bf16_to_f32(const void* src, float* dst, int64_t n, void* stream) {
+    VT_CHECK_ARG(n > 0, "vt_cast_bf16_to_f32: empty");
+    hipLaunchKernelGGL(k_bf16_to_f32, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, S(stream), (const uint16_t*)src,
+                       dst, n);
+    VT_LAUNCH_CHECK("vt_cast_bf16_to_f32");
     return VT_OK;
 }
 

@@ -64,6 +64,14 @@ class _Lib:
             f.restype = ctypes.c_char_p if ret == "constchar*" else ctypes.c_int
             f.argtypes = [_CT[a] for a in args]
             self.fns[name] = f
+        # DIAGNOSTIC ONLY (tools/ablate_step.sh): VAETEB_ABLATE=name[,name...] turns the named
+        # entry points into no-ops, so a timing run shows how much of the step a kernel
+        # family holds on the critical path.  Results are then wrong; never set in training.
+        ablate = [n for n in os.environ.get("VAETEB_ABLATE", "").split(",") if n]
+        for n in ablate:
+            if n not in self.fns:
+                raise KeyError(f"VAETEB_ABLATE: unknown entry point {n}")
+            self.fns[n] = lambda *a: 0
 
     def last_error(self):
         return self.fns["vt_last_error"]().decode()

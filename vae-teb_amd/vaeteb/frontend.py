@@ -166,8 +166,17 @@ def launch_pairs(p, analytic, B, tab, out, lowpass=True, pad_mode=0):
 class FrontEnd:
     """Fused training-step front-end: raw windows -> normalised model inputs."""
 
-    def __init__(self, plan: FrontEndPlan, stats=None):
+    def __init__(self, plan: FrontEndPlan, stats=None, trim=0):
+        """trim: decimated steps dropped at each end of the model inputs — the dataset's
+        trim_minutes (ref/hdf5_dataset/hdf5_dataset.py:359-364, :733-741: 2 minutes of a
+        4 Hz window = 480 raw samples = 30 steps), fused into the normalisation pass; the
+        raw fhr loses trim x 16 samples at each end.  S_out = S - 2 trim, N_out = N - 32 trim."""
         self.plan = p = plan
+        if trim < 0 or 2 * trim >= p.S:
+            raise ValueError(f"trim {trim} out of range for {p.S} steps")
+        self.trim = trim
+        self.S_out = p.S - 2 * trim
+        self.N_out = p.N - 2 * trim * p.step
         self.phase_pairs = np.nonzero(p.phase_mask)[0]
         self.cross_pairs = np.nonzero(p.cross_mask)[0]
         self.tab = p.tables(self.phase_pairs, self.cross_pairs, scattering=True)
@@ -237,35 +246,36 @@ class FrontEnd:
             raise RuntimeError("FrontEnd needs normalisation statistics (set_stats)")
         p = self.plan
         r = self.raw(x, side)
-        B, S = x.shape[0], p.S
+        B, S, S0, Sl = x.shape[0], p.S, self.trim, self.S_out
         st = _lib.stream()
         out = {} if out is None else out
         get = lambda k, shape: out[k] if k in out else torch.empty(shape, device=p.device)
-        y_st = get("fhr_st", (B, S, self.C_st))
-        y_ph = get("fhr_ph", (B, S, self.C_ph))
-        x_ph = get("fhr_up_ph", (B, S, self.C_x))
-        y_raw = get("fhr", (B, p.N))
+        y_st = get("fhr_st", (B, Sl, self.C_st))
+        y_ph = get("fhr_ph", (B, Sl, self.C_ph))
+        x_ph = get("fhr_up_ph", (B, Sl, self.C_x))
+        y_raw = get("fhr", (B, self.N_out))
         k, m, s = self.stats["fhr_st"]
-        _lib.call("vt_fe_normalize", _lib.ptr(r["fhr_st"]), B, self.C_st, self.C_st, S, _lib.ptr(k), _lib.ptr(m),
-                  _lib.ptr(s),
-                  1e-6, _lib.ptr(y_st), self.C_st, 0, st)
+        _lib.call("vt_fe_normalize_window", _lib.ptr(r["fhr_st"]), B, self.C_st, self.C_st, S, S0, Sl, _lib.ptr(k),
+                  _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(y_st), self.C_st, 0, st)
         pairs = r["pairs"]
         if self.C_ph:
             k, m, s = self.stats["fhr_ph"]
-            _lib.call("vt_fe_normalize", pairs.data_ptr(), B, self.C_ph, pairs.shape[1], S, _lib.ptr(k),
-                      _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(y_ph), self.C_ph, 0, st)
+            _lib.call("vt_fe_normalize_window", pairs.data_ptr(), B, self.C_ph, pairs.shape[1], S, S0, Sl,
+                      _lib.ptr(k), _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(y_ph), self.C_ph, 0, st)
         if self.C_x:
             k, m, s = self.stats["fhr_up_ph"]
             if "cross" in r:
                 with torch.cuda.stream(side):
-                    _lib.call("vt_fe_normalize", r["cross"].data_ptr(), B, self.C_x, self.C_x, S, _lib.ptr(k),
-                              _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(x_ph), self.C_x, 0, _lib.stream())
+                    _lib.call("vt_fe_normalize_window", r["cross"].data_ptr(), B, self.C_x, self.C_x, S, S0, Sl,
+                              _lib.ptr(k), _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(x_ph), self.C_x, 0,
+                              _lib.stream())
                 x_ph.record_stream(side)
             else:
-                _lib.call("vt_fe_normalize", pairs[:, self.C_ph:].data_ptr(), B, self.C_x, pairs.shape[1], S,
-                          _lib.ptr(k), _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(x_ph), self.C_x, 0, st)
+                _lib.call("vt_fe_normalize_window", pairs[:, self.C_ph:].data_ptr(), B, self.C_x, pairs.shape[1], S,
+                          S0, Sl, _lib.ptr(k), _lib.ptr(m), _lib.ptr(s), 1e-6, _lib.ptr(x_ph), self.C_x, 0, st)
         fm, fs = self.stats["fhr"]
-        _lib.call("vt_normalize_raw", _lib.ptr(x), B, 2 * p.N, p.N, fm, fs, _lib.ptr(y_raw), st)
+        _lib.call("vt_normalize_raw", _lib.ptr(x) + 4 * S0 * p.step, B, 2 * p.N, self.N_out, fm, fs, _lib.ptr(y_raw),
+                  st)
         return {"fhr_st": y_st, "fhr_ph": y_ph, "fhr_up_ph": x_ph, "fhr": y_raw}
 
 

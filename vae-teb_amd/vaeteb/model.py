@@ -208,7 +208,7 @@ class ResidualMLP(nn.Module):
             d = h
         self.body = nn.Sequential(*mods)
         self.fused = True   # whole-stack kernels (vt_resmlp_*); False: one launch sequence per layer
-        self.bf16 = False   # whole-stack kernels on bf16 MFMA (vt_resmlp_bf16_*, 16-bit autocast precision)
+        self.bf16 = False   # whole-stack kernels on bf16 MFMA (vt_resmlp_bf16_*; the reference's fp16 autocast in bf16)
         self.use_skip_connection = use_skip_connection
         if use_skip_connection:
             self.skip_proj = Linear(input_dim, hidden_dims[-1]) if input_dim != hidden_dims[-1] else nn.Identity()
@@ -311,7 +311,7 @@ class ConvBlock(nn.Module):
     def __init__(self, cin, cout, k, causal, up=False, tanh=False):
         super().__init__()
         self.causal, self.up, self.tanh = causal, up, tanh
-        self.bf16 = False  # bf16-MFMA conv (the reference's 16-bit autocast precision); BatchNorm stays fp32
+        self.bf16 = False  # bf16-MFMA conv (the reference's fp16 autocast, in bf16); BatchNorm stays fp32
         self.conv = _ConvWeight(cin, cout, k)
         self.bn_layer = _BatchNorm(cout)
         self.sync_bn = False      # cross-rank BatchNorm statistics (convert_sync_batchnorm)
@@ -489,7 +489,8 @@ class Decoder(nn.Module):
     def set_head_precision(self, precision):
         """"fp32": every GEMM on the fp32 kernels (parity mode); "bf16": the
         R x R head GEMMs on bf16 MFMA with fp32 accumulation (the reference
-        trains under 16-bit autocast, ref/model/graph_model.py:510,710)."""
+        trains in fp16 autocast, ref/model/graph_model.py:510,710; bf16 here is the
+        documented deviation)."""
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"head_precision must be 'fp32' or 'bf16', got {precision!r}")
         self.head_precision = precision
@@ -532,7 +533,7 @@ class SeqVaeTeb(nn.Module):
     def set_mlp_precision(self, precision):
         """"fp32": the ResidualMLP stacks on exact-fp32 MFMA (parity mode); "bf16":
         their Linear layers on bf16 MFMA with fp32 accumulation, LayerNorm and
-        reductions fp32 — the reference trains under 16-bit autocast
+        reductions fp32 — the reference trains in fp16 autocast (bf16 here: DESIGN.md §5)
         (ref/model/graph_model.py:510, :709-711)."""
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"mlp_precision must be 'fp32' or 'bf16', got {precision!r}")
@@ -543,7 +544,7 @@ class SeqVaeTeb(nn.Module):
 
     def set_conv_precision(self, precision):
         """"fp32": exact-fp32 MFMA convs (parity mode); "bf16": bf16-MFMA convs with
-        fp32 accumulation and fp32 BatchNorm — the reference trains under 16-bit
+        fp32 accumulation and fp32 BatchNorm — the reference trains in fp16 (bf16 here: DESIGN.md §5) under
         autocast (ref/model/graph_model.py:510, :709-711)."""
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"conv_precision must be 'fp32' or 'bf16', got {precision!r}")

@@ -66,8 +66,17 @@ class GradBuckets:
     >= bucket_mb of contiguous gradient memory (xGMI rings are per-link bound:
     fewer, larger collectives)."""
 
-    def __init__(self, state: FlatState, group=None, bucket_mb=64.0):
+    def __init__(self, state: FlatState, group=None, bucket_mb=64.0, reduce_dtype=torch.float32):
+        """reduce_dtype=torch.bfloat16: each bucket is rounded to bf16 (vt_cast_bf16), reduced
+        in bf16 (half the bytes over xGMI) and widened back into the fp32 gradient buffer
+        (vt_cast_bf16_to_f32) before clip + AdamW, which keep fp32 master gradients and
+        moments.  The default fp32 reduce is the reference's DDP semantics."""
         self.state, self.group = state, group
+        if reduce_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"reduce_dtype must be float32 or bfloat16, got {reduce_dtype}")
+        self.reduce_dtype = reduce_dtype
+        self.g16 = (torch.empty(state.numel, dtype=torch.bfloat16, device=state.g.device)
+                    if reduce_dtype == torch.bfloat16 else None)
         limit = int(bucket_mb * (1 << 20) / 4)
         self.buckets = []  # (start, end, n_params)
         self.param_bucket = {}
@@ -81,6 +90,7 @@ class GradBuckets:
                 start, count = cur, 0
         self.pending = [0] * len(self.buckets)
         self.works = []
+        self.launched = []
         self.ready = set()
         self.enabled = True   # False while a hipGraph is captured: no collective inside the graph
         # torch ops reach the flat gradient through AccumulateGrad (hook); the HIP
@@ -92,13 +102,13 @@ class GradBuckets:
     def reset(self):
         self.pending = [b[2] for b in self.buckets]
         self.works = []
+        self.launched = []
         self.ready = set()
 
     def reduce_all(self):
         """All buckets at once (after a graph replay of the backward)."""
         for b, (s, e, _) in enumerate(self.buckets):
-            self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                              async_op=True))
+            self._launch(s, e)
             self.pending[b] = 0
 
     def _hook(self, p):
@@ -116,8 +126,7 @@ class GradBuckets:
             # covered by the wait
             self._join_side_streams()
             s, e, _ = self.buckets[b]
-            self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                              async_op=True))
+            self._launch(s, e)
 
     def _join_side_streams(self):
         """The collective's stream waits for every stream that may have written gradients
@@ -137,12 +146,39 @@ class GradBuckets:
         for b, left in enumerate(self.pending):
             if left > 0:
                 s, e, _ = self.buckets[b]
-                self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                                  async_op=True))
+                self._launch(s, e)
                 self.pending[b] = 0
         for w in self.works:
             w.wait()  # orders the compute stream after the collective; no host wait for RCCL
+        if self.g16 is not None:
+            for s, e in self.launched:
+                self._cast(s, e, back=True)
         self.works = []
+        self.launched = []
+
+    def _cast(self, s, e, back=False):
+        g, h = self.state.g, self.g16
+        if not g.is_cuda:   # the CPU (gloo) path: torch casts, same rounding (round to nearest even)
+            if back:
+                g[s:e].copy_(h[s:e])
+            else:
+                h[s:e].copy_(g[s:e])
+            return
+        if back:
+            _lib.call("vt_cast_bf16_to_f32", h[s:].data_ptr(), g[s:].data_ptr(), e - s, _lib.stream())
+        else:
+            _lib.call("vt_cast_bf16", g[s:].data_ptr(), h[s:].data_ptr(), e - s, _lib.stream())
+
+    def _launch(self, s, e):
+        """all_reduce(SUM) of the flat gradient slice [s, e) (through its bf16 copy when
+        reduce_dtype is bfloat16)."""
+        if self.g16 is None:
+            self.works.append(dist.all_reduce(self.state.g[s:e], op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True))
+            return
+        self._cast(s, e)
+        self.works.append(dist.all_reduce(self.g16[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        self.launched.append((s, e))
 
 
 class Trainer:
@@ -150,7 +186,8 @@ class Trainer:
     over flat buffers (ref/model/graph_model.py:654-660, :724)."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=1e-4, max_norm=1.0, beta_kld=1e-5,
-                 frontend=None, world_size=1, group=None, bucket_mb=64.0, vae_loss_weight=0.1):
+                 frontend=None, world_size=1, group=None, bucket_mb=64.0, vae_loss_weight=0.1,
+                 reduce_dtype=torch.float32):
         self.model = model
         self.vae_loss_weight = vae_loss_weight
         self.frontend = frontend
@@ -165,7 +202,17 @@ class Trainer:
         self.adam_coef = torch.zeros(2, device=dev)
         self.graph = None
         self.norm_ws = torch.empty(_lib.lib().fns["vt_grad_norm_workspace_floats"](), device=dev)
-        self.buckets = GradBuckets(self.state, group, bucket_mb) if world_size > 1 else None
+        self.buckets = GradBuckets(self.state, group, bucket_mb, reduce_dtype) if world_size > 1 else None
+        if world_size > 1 and torch.cuda.is_available():
+            # hardware-queue budget: a process's streams map onto GPU_MAX_HW_QUEUES = 4 queues;
+            # the model uses main + 3 side streams on one GPU, and RCCL's stream would be a 5th
+            # sharing (and serialising behind) one of them — with several ranks the model keeps
+            # main + 2 side streams so RCCL owns a queue (VAETEB_* environment overrides)
+            from . import model as _model
+            if "VAETEB_MAX_SIDE_STREAMS" not in os.environ:
+                _model.MAX_SIDE = min(_model.MAX_SIDE, 2)
+            if "VAETEB_GRAD_SIDE_STREAM" not in os.environ:
+                _model.GRAD_SIDE = min(_model.GRAD_SIDE, 2)
 
     def loss(self, batch, eps=None):
         """Forward + loss for an AttributeDict-like batch with fields fhr_st,
@@ -375,35 +422,3 @@ def init_distributed():
         dist.init_process_group(backend=backend)
     dev = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device("cpu")
     return rank, world, local, dev
-
-
-def smoke_step():
-    """One small HIP training step checked against the oracle (used by
-    __graft_entry__.smoke())."""
-    import sys
-    import numpy as np
-    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    sys.path.insert(0, root)
-    sys.path.insert(0, os.path.join(root, "tests"))
-    from golden_util import det_fill_
-    from oracle import model_ref as M
-    from .model import SeqVaeTeb
-    S, B = 16, 2
-    rng = np.random.default_rng(0)
-    batch = {k: rng.standard_normal(s).astype(np.float32) for k, s in
-             (("fhr_st", (B, S, 43)), ("fhr_ph", (B, S, 44)), ("fhr_up_ph", (B, S, 130)), ("fhr", (B, 16 * S)))}
-    eps = rng.standard_normal((B, S, 32)).astype(np.float32)
-    ref = det_fill_(M.SeqVaeTebRef(S))
-    T = {k: torch.from_numpy(v) for k, v in batch.items()}
-    _, Lr, _, _ = M.train_step(ref, dict(y_st=T["fhr_st"], y_ph=T["fhr_ph"], x_ph=T["fhr_up_ph"], y_raw=T["fhr"]),
-                               torch.from_numpy(eps), 1e-5)
-    m = det_fill_(SeqVaeTeb(sequence_length=S)).cuda()
-    tr = Trainer(m, lr=1e-3)
-    L = tr.step({k: v.cuda() for k, v in T.items()}, eps=torch.from_numpy(eps).cuda())
-    got, exp = L["total_loss"].item(), Lr["total_loss"].item()
-    assert abs(got - exp) <= 1e-5 * abs(exp), (got, exp)
-    sd = m.state_dict()
-    worst = max(((sd[k].cpu() - v).norm() / v.norm().clamp_min(1e-12)).item() for k, v in ref.state_dict().items()
-                if v.dtype == torch.float32)
-    assert worst < 1e-3, worst
-    print(f"smoke: training step ok (loss {got:.6f} vs oracle {exp:.6f}, worst param rel err {worst:.2e})")
