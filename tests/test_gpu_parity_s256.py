@@ -118,7 +118,13 @@ def test_fp32_step_vs_reference_golden_training_geometry(golden, name):
     T = lambda k: torch.from_numpy(g[k]).cuda()
     Ls = tr.step({"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}, eps=T("eps"))
     assert abs(Ls["total_loss"].item() - float(g["loss_total_loss"])) <= 1e-5 * abs(float(g["loss_total_loss"]))
-    assert abs(Ls["grad_norm"].item() - float(g["grad_norm_total"])) <= 1e-4 * float(g["grad_norm_total"])
+    # global norm vs the reference's, within 1e-4 + 3 x the reference's own fp32 spread of it
+    # (each parameter's fp32-vs-fp64 gradient error weighted by its share of the squared norm:
+    # 2.4e-4 at S = 256, 3.3e-3 at S = 300, where the decoder convs' gradients carry 3.8e-3)
+    l2 = np.asarray(g["grad_l2"], np.float64)
+    spread = float((l2 ** 2 * np.asarray(g["grad_rel64"], np.float64)).sum() / (l2 ** 2).sum())
+    gn = float(g["grad_norm_total"])
+    assert abs(Ls["grad_norm"].item() - gn) <= (1e-4 + 3 * spread) * gn, (Ls["grad_norm"].item(), gn, spread)
     sd2 = m2.state_dict()
     for i, k in enumerate(list(g["param_names"])):
         a = sd2[k].double().norm().item()
