@@ -273,6 +273,9 @@ def main():
     ap.add_argument("--mlp", choices=["bf16", "fp32"], default="bf16",
                     help="ResidualMLP stacks: Linear layers on bf16 MFMA with fp32 accumulation, LayerNorm fp32 "
                          "(bf16 for the reference's fp16 autocast) or exact fp32")
+    ap.add_argument("--lstm", choices=["16-mixed", "fp32"], default="fp32",
+                    help="encoder LSTMs: 16-bit MFMA recurrences over 4-sample tiles (f16 forward / bf16 backward "
+                         "operands, fp32 state: the reference's own 16-mixed LSTM width) or exact fp32")
     args = ap.parse_args()
 
     rank, world, local, dev = init_distributed()
@@ -288,7 +291,7 @@ def main():
     torch.manual_seed(1234)  # same initial weights on every rank (DDP semantics)
     vae_kw = dict(scattering_channels=fe.C_st, phase_channels=fe.C_ph, cross_phase_channels=fe.C_x,
                   head_precision=args.heads, conv_precision=args.conv, mlp_precision=args.mlp,
-                  concurrent_encoders=not args.serial_encoders)
+                  lstm_precision=args.lstm, concurrent_encoders=not args.serial_encoders)
     c4 = args.workload == "c4"
     if c4:
         # config 4: SeqVaeTebClassifier end to end (freeze_vae=False), the reference's default classifier
@@ -452,10 +455,11 @@ def main():
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32" if (args.heads, args.conv, args.mlp) == ("fp32", "fp32", "fp32") else
+        "dtype": "fp32" if (args.heads, args.conv, args.mlp, args.lstm) == ("fp32", "fp32", "fp32", "fp32") else
                  "bf16 MFMA (" + " + ".join(n for n, v in (("decoder heads", args.heads), ("conv blocks", args.conv),
                                                          ("ResidualMLP linears", args.mlp)) if v == "bf16")
-                 + "), fp32 accumulation; fp32 LayerNorm / BatchNorm / LSTM / front-end / optimizer",
+                 + (", LSTM recurrences f16 fwd / bf16 bwd" if args.lstm == "16-mixed" else "")
+                 + "), fp32 accumulation; fp32 LayerNorm / BatchNorm / LSTM state / front-end / optimizer",
         "data": "synthetic",
         "config": {"workload": (f"c4: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTebClassifier("
                                 f"R={16 * S}, FHRInceptionTimeClassifier f32 d6 attention, dropout 0.2) end-to-end "

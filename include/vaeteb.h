@@ -454,6 +454,22 @@ int vt_lstm_layer_fwd_x(const float* x, int In, const float* w_ih, const float* 
  * no weight gradient is wanted); bitwise vt_lstm_layer_bwd + vt_linear_bwd_data.  */
 int vt_lstm_layer_bwd_x(const float* dh_out, const float* gates, const float* cst, const float* w_hh,
                         const float* w_ih, int In, int B, int S, int hidden, float* dgates, float* dx, void* stream);
+/* The same layer at the reference's 16-bit autocast width (its LSTM runs with fp16
+ * operands under torch.amp, ref/model/graph_model.py:510, :709-711): 4 samples per
+ * workgroup, the recurrent matvec and the input projection on
+ * v_mfma_f32_16x16x32_f16 (h, x, W rounded to f16; fp32 accumulation, cell state,
+ * activations and outputs).  In % 4 == 0, In <= 64.  Same outputs as
+ * vt_lstm_layer_fwd_x.
+ * replaces: one layer of nn.LSTM under torch.amp.autocast (vae_teb_model.py:474-480,
+ *           :647-653; graph_model.py:709-711)                                       */
+int vt_lstm16_layer_fwd(const float* x, int In, const float* w_ih, const float* b_ih, const float* w_hh,
+                        const float* b_hh, int B, int S, int hidden, float* out_h, float* out_hprev, float* out_c,
+                        float* gates, void* stream);
+/* Its backward: dh_rec = dg_{t+1} W_hh and dx = dgates W_ih on bf16 MFMA (bf16
+ * keeps fp32's exponent range, so no loss scale is needed where the reference uses
+ * GradScaler); cell derivatives and dgates fp32.  dgates / dx may be null.          */
+int vt_lstm16_layer_bwd(const float* dh_out, const float* gates, const float* cst, const float* w_hh,
+                        const float* w_ih, int In, int B, int S, int hidden, float* dgates, float* dx, void* stream);
 /* All of a layer's parameter gradients in one pass over dgates [B*S, 4H]:
  * dw_ih (+)= dgates^T x, dw_hh (+)= dgates^T h_{t-1}, db_ih and db_hh (may be
  * null) (+)= column sums of dgates.  In + hidden + 1 <= 144; ws: at least

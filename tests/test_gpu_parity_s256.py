@@ -114,6 +114,7 @@ def test_fp32_step_vs_reference_golden_training_geometry(golden, name):
     # one full Trainer step (clip 1.0 + AdamW as ref/model/graph_model.py:654-660,724)
     from vaeteb.train import Trainer
     m2 = _model(S)
+    p0 = {k: v.detach().double().cpu() for k, v in m2.state_dict().items()}
     tr = Trainer(m2, lr=1e-3)
     T = lambda k: torch.from_numpy(g[k]).cuda()
     Ls = tr.step({"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}, eps=T("eps"))
@@ -125,10 +126,24 @@ def test_fp32_step_vs_reference_golden_training_geometry(golden, name):
     spread = float((l2 ** 2 * np.asarray(g["grad_rel64"], np.float64)).sum() / (l2 ** 2).sum())
     gn = float(g["grad_norm_total"])
     assert abs(Ls["grad_norm"].item() - gn) <= (1e-4 + 3 * spread) * gn, (Ls["grad_norm"].item(), gn, spread)
+    # post-AdamW parameter norms: 1e-5 relative, plus what sign-ambiguous updates can move
+    # the norm.  A first AdamW step moves each element by lr g / (|g| + eps) ~ lr sign(g), so
+    # an element whose reference gradient lies within 3x the reference's own fp32 noise of
+    # zero (noise per element: rel64 ||g|| / sqrt(n)) can legitimately step the other way,
+    # a change of <= 2 lr that moves the norm by <= 2 lr (|p0_j| + 2 lr) / ||p||, summed over
+    # those elements (S = 300: the input LayerNorm's bias has 3).  Counted from the full
+    # reference gradients; the head weights (16 rows stored) keep the strict bound.
     sd2 = m2.state_dict()
     for i, k in enumerate(list(g["param_names"])):
         a = sd2[k].double().norm().item()
-        assert abs(a - float(g["after_l2"][i])) <= 1e-5 * float(g["after_l2"][i]) + 1e-7, k
+        amb = 0.0
+        if f"grad_{i}" in g.files:
+            gr = np.abs(np.asarray(g[f"grad_{i}"], np.float64)).reshape(-1)
+            noise = float(g["grad_rel64"][i]) * float(g["grad_l2"][i]) / np.sqrt(gr.size)
+            pj = p0[k].reshape(-1).abs().numpy()[gr <= 3 * noise]
+            amb = float((2 * tr.lr * (pj + 2 * tr.lr)).sum()) / max(float(g["after_l2"][i]), 1e-30)
+        tol = 1e-5 * float(g["after_l2"][i]) + 1e-7 + amb
+        assert abs(a - float(g["after_l2"][i])) <= tol, (k, a, float(g["after_l2"][i]), amb)
 
 
 def test_s256_bf16_step_within_reference_autocast_spread(golden):

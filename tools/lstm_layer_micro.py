@@ -10,7 +10,8 @@ sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
 import torch  # noqa: E402
 from vaeteb._lib import call, ptr, stream  # noqa: E402
 
-B, S, H, In = 256, 256, 64, int(os.environ.get("IN", "64"))
+B, S, H, In = int(os.environ.get("B", "256")), 256, 64, int(os.environ.get("IN", "64"))
+L16 = os.environ.get("L16", "0") == "1"   # the 16-bit MFMA recurrences (vt_lstm16_layer_*)
 dev = "cuda"
 
 
@@ -43,12 +44,12 @@ def layer():
 
 
 def fwd(t):
-    call("vt_lstm_layer_fwd_x", ptr(t["x"]), In, ptr(t["wih"]), ptr(t["bih"]), ptr(t["whh"]), ptr(t["bhh"]), B, S, H,
+    call("vt_lstm16_layer_fwd" if L16 else "vt_lstm_layer_fwd_x", ptr(t["x"]), In, ptr(t["wih"]), ptr(t["bih"]), ptr(t["whh"]), ptr(t["bhh"]), B, S, H,
          ptr(t["h"]), ptr(t["hp"]), ptr(t["c"]), ptr(t["gates"]), stream())
 
 
 def bwd(t):
-    call("vt_lstm_layer_bwd_x", ptr(t["dh"]), ptr(t["gates"]), ptr(t["c"]), ptr(t["whh"]), ptr(t["wih"]), In, B, S, H,
+    call("vt_lstm16_layer_bwd" if L16 else "vt_lstm_layer_bwd_x", ptr(t["dh"]), ptr(t["gates"]), ptr(t["c"]), ptr(t["whh"]), ptr(t["wih"]), In, B, S, H,
          ptr(t["dg"]), ptr(t["dx"]), stream())
 
 
@@ -78,7 +79,7 @@ fwd(a), fwd(b), bwd(a), bwd(b)
 for name, fn in (("fwd_x", fwd), ("bwd_x", bwd), ("bwd_weight", bww)):
     one = timed(lambda: fn(a))
     two = timed(pair(fn))
-    print(f"In={In} {name:11s}: alone {one:7.1f} us ({one / S * 1e3:6.1f} ns/step)   two streams {two:7.1f} us",
+    print(f"{'16' if L16 else '32'} In={In} {name:11s}: alone {one:7.1f} us ({one / S * 1e3:6.1f} ns/step)   two streams {two:7.1f} us",
           flush=True)
 
 

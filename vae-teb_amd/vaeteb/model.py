@@ -355,6 +355,7 @@ class LSTM(nn.Module):
     def __init__(self, input_size, hidden_size=64, num_layers=4):
         super().__init__()
         self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        self.half = False   # 16-bit MFMA recurrences (SeqVaeTeb.set_lstm_precision)
         for l in range(num_layers):
             din = input_size if l == 0 else hidden_size
             w_ih = nn.Parameter(torch.empty(4 * hidden_size, din))
@@ -378,7 +379,7 @@ class LSTM(nn.Module):
         return out
 
     def forward(self, x):
-        return ops.lstm(x, self.flat())
+        return ops.lstm(x, self.flat(), half=self.half)
 
 
 def _seq1(m):
@@ -514,7 +515,7 @@ class SeqVaeTeb(nn.Module):
     def __init__(self, input_channels=76, sequence_length=300, latent_dim_source=32, latent_dim_target=32,
                  latent_dim_z=32, decimation_factor=16, warmup_period=30, scattering_channels=43,
                  phase_channels=44, cross_phase_channels=130, head_precision="fp32", concurrent_encoders=False,
-                 conv_precision="fp32", mlp_precision="fp32"):
+                 conv_precision="fp32", mlp_precision="fp32", lstm_precision="fp32"):
         super().__init__()
         # the source and target encoders are independent until the conditional
         # encoder: on a GPU they can run on two HIP streams (their LSTM
@@ -529,6 +530,20 @@ class SeqVaeTeb(nn.Module):
         self.decoder = Decoder(latent_dim_z, sequence_length, head_precision)
         self.set_conv_precision(conv_precision)
         self.set_mlp_precision(mlp_precision)
+        self.set_lstm_precision(lstm_precision)
+
+    def set_lstm_precision(self, precision):
+        """"fp32": the exact-fp32 recurrences (parity mode); "16-mixed": the reference's
+        own LSTM width under Lightning precision="16-mixed" / torch.amp autocast
+        (ref/model/graph_model.py:510, :709-711) — f16 forward operands, bf16 backward
+        operands (no loss scale needed), fp32 accumulation, cell state and outputs, on
+        MFMA over 4-sample tiles (vt_lstm16_layer_*)."""
+        if precision not in ("fp32", "16-mixed"):
+            raise ValueError(f"lstm_precision must be 'fp32' or '16-mixed', got {precision!r}")
+        self.lstm_precision = precision
+        for m in self.modules():
+            if isinstance(m, LSTM):
+                m.half = precision == "16-mixed"
 
     def set_mlp_precision(self, precision):
         """"fp32": the ResidualMLP stacks on exact-fp32 MFMA (parity mode); "bf16":

@@ -671,7 +671,7 @@ class LSTMF(torch.autograd.Function):
     params: flat list [w_ih_l0, w_hh_l0, b_ih_l0, b_hh_l0, w_ih_l1, ...]."""
 
     @staticmethod
-    def forward(ctx, x, *params):
+    def forward(ctx, x, half, *params):
         _check(x, *params)
         B, S, _ = x.shape
         nl = len(params) // 4
@@ -685,7 +685,11 @@ class LSTMF(torch.autograd.Function):
             hp = torch.empty_like(h)
             c = torch.empty_like(h)
             gates = torch.empty((B, S, 4 * H), device=x.device)
-            if LSTM_FUSED and In <= 64:
+            if half and In <= 64 and In % 4 == 0:
+                # 16-bit MFMA recurrence over 4-sample tiles (f16 operands, fp32 state)
+                call("vt_lstm16_layer_fwd", ptr(inp), In, ptr(w_ih), ptr(b_ih), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h),
+                     ptr(hp), ptr(c), ptr(gates), _st())
+            elif LSTM_FUSED and In <= 64:
                 # input projection inside the recurrence kernel (bitwise the unfused result)
                 call("vt_lstm_layer_fwd_x", ptr(inp), In, ptr(w_ih), ptr(b_ih), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h),
                      ptr(hp), ptr(c), ptr(gates), _st())
@@ -699,6 +703,7 @@ class LSTMF(torch.autograd.Function):
         ctx.save_for_backward(*saved)
         ctx.params = params
         ctx.nl = nl
+        ctx.half = bool(half)
         return inp
 
     @staticmethod
@@ -720,7 +725,11 @@ class LSTMF(torch.autograd.Function):
             need_dx = l > 0 or ctx.needs_input_grad[0]
             fused = LSTM_FUSED and In <= 64
             gin = torch.empty((B, S, In), device=gy.device) if need_dx else None
-            if fused:
+            if ctx.half and In <= 64 and In % 4 == 0:
+                # bf16-MFMA recurrence, dX = dG W_ih inside; dG in fp32 for the weight gradients
+                call("vt_lstm16_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), ptr(w_ih), In, B, S, H, ptr(dg),
+                     ptr(gin) if need_dx else None, _st())
+            elif fused:
                 # dX = dG W_ih inside the recurrence kernel (bitwise the unfused result)
                 call("vt_lstm_layer_bwd_x", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), ptr(w_ih), In, B, S, H, ptr(dg),
                      ptr(gin) if need_dx else None, _st())
@@ -801,7 +810,7 @@ class LSTMF(torch.autograd.Function):
                     for t in (dg, inp, hp):
                         t.record_stream(side)
                 pg.result()
-        return (gx, *grads)
+        return (gx, None, *grads)
 
 
 # ---------------------------------------------------------------------- ELBO
@@ -889,8 +898,10 @@ def conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momen
     return ConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps, bool(bf16))
 
 
-def lstm(x, params):
-    return LSTMF.apply(x, *params)
+def lstm(x, params, half=False):
+    """half: the 16-bit MFMA recurrences (vt_lstm16_layer_*: f16 forward / bf16 backward
+    operands, fp32 accumulation and cell state), the reference's 16-bit autocast width."""
+    return LSTMF.apply(x, bool(half), *params)
 
 
 def latent(mu_c, lv_q, mu_y, lv_p, eps):
