@@ -459,7 +459,9 @@ int vt_lstm_layer_bwd_x(const float* dh_out, const float* gates, const float* cs
  * workgroup, the recurrent matvec and the input projection on
  * v_mfma_f32_16x16x32_f16 (h, x, W rounded to f16; fp32 accumulation, cell state,
  * activations and outputs).  In % 4 == 0, In <= 64.  Same outputs as
- * vt_lstm_layer_fwd_x.
+ * vt_lstm_layer_fwd_x, except: gates are [B, S, hidden, 4] (each unit's i, f, g~, o
+ * contiguous; consumed by vt_lstm16_layer_bwd only) and out_hprev may be null
+ * (vt_lstm16_layer_bwd_weight reads h_{t-1} from h).
  * replaces: one layer of nn.LSTM under torch.amp.autocast (vae_teb_model.py:474-480,
  *           :647-653; graph_model.py:709-711)                                       */
 int vt_lstm16_layer_fwd(const float* x, int In, const float* w_ih, const float* b_ih, const float* w_hh,
@@ -477,6 +479,11 @@ int vt_lstm16_layer_bwd(const float* dh_out, const float* gates, const float* cs
 int vt_lstm_layer_bwd_weight(const float* dgates, const float* x, int In, const float* hprev, int B, int S,
                              int hidden, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate,
                              float* ws, int64_t ws_floats, void* stream);
+/* The same with h_{t-1} read from the layer's outputs h [B, S, hidden] (row t - 1 of each
+ * sample, zero at t = 0): the 16-bit forward need not write h_{t-1} (out_hprev = null).  */
+int vt_lstm16_layer_bwd_weight(const float* dgates, const float* x, int In, const float* h, int B, int S,
+                               int hidden, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate,
+                               float* ws, int64_t ws_floats, void* stream);
 
 /* ---------------------------------------------------------- classifier (c4)
  * FHRInceptionTimeClassifier (ref/model/inception_time.py:185-333) on

@@ -3,7 +3,8 @@
 The kernels compute a definite 16-bit model of nn.LSTM (ref/model/vae_teb_model.py:
 474-480, :647-653 under the reference's 16-mixed autocast, graph_model.py:510,
 :709-711): forward operands x, h_{t-1} and the pre-scaled W_ih, W_hh (gate rows times
--log2 e, or -2 log2 e for g, in fp32) rounded to f16, backward operands
+-log2 e, or -2 log2 e for g, in fp32) rounded to f16, sigmoid = 1 / (1 + 2^p) and
+tanh = 2 sigmoid(2x) - 1 in the forward, backward operands
 dg and W_hh / W_ih rounded to bf16, everything else (accumulation, biases, cell state,
 activations, outputs, dgates, weight gradients) fp32.  The oracle here is that model
 restated in fp64 on the CPU (`_emu`), with torch's fp64 nn.LSTM as the exact model.
@@ -68,7 +69,9 @@ def _emu(x, params, gy, dt=torch.float64):
             g = 2 * g - 1
             hps.append(h)
             c = f * c + i * g
-            h = o * torch.tanh(c)
+            # the kernel's tanh(c) = 2 / (1 + 2^(-2 log2(e) c)) - 1 (absolute, not relative,
+            # accuracy near 0: the fp32 restatement carries the same cancellation)
+            h = o * (2 / (1 + torch.pow(2.0, float(2 * nl2e) * c)) - 1)
             hs.append(h), cs.append(c), gs.append(torch.cat([i, f, g, o], 1))
         saved.append((inp, torch.stack(hps, 1), torch.stack(cs, 1), torch.stack(gs, 1)))
         inp = torch.stack(hs, 1)
@@ -174,3 +177,28 @@ def test_lstm16_no_dx_and_outputs(ops):
     with pytest.raises(ValueError):
         _lib.call("vt_lstm16_layer_fwd", P(x), 30, P(w_ih), P(b_ih), P(w_hh), P(b_hh), B, S, H, P(h), P(hp), P(c),
                   P(gates), st)
+
+
+@pytest.mark.parametrize("In,B,S", [(20, 3, 37), (64, 4, 16)])
+def test_lstm16_weight_grad_reads_h_shifted(ops, In, B, S):
+    """vt_lstm16_layer_bwd_weight (h_{t-1} read from h, zero at t = 0) == vt_lstm_layer_bwd_weight
+    on an explicit h_{t-1} tensor, bit for bit (same kernel and summation order)."""
+    from vaeteb import _lib
+    torch.manual_seed(In + S)
+    H = 64
+    dg = torch.randn(B, S, 4 * H, device="cuda")
+    x = torch.randn(B, S, In, device="cuda")
+    h = torch.randn(B, S, H, device="cuda")
+    hp = torch.cat([torch.zeros_like(h[:, :1]), h[:, :-1]], 1).contiguous()
+    ws = torch.empty(32 << 20, device="cuda")
+    P = lambda t: t.data_ptr()
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for fn, hh in (("vt_lstm_layer_bwd_weight", hp), ("vt_lstm16_layer_bwd_weight", h)):
+        o = [torch.empty(4 * H, In, device="cuda"), torch.empty(4 * H, H, device="cuda"),
+             torch.empty(4 * H, device="cuda"), torch.empty(4 * H, device="cuda")]
+        _lib.call(fn, P(dg), P(x), In, P(hh), B, S, H, *[P(t) for t in o], 0, P(ws), ws.numel(), st)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

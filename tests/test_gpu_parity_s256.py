@@ -13,7 +13,7 @@ MFMA.  These tests pin that configuration to the reference and the oracle:
       S = 256: 256 LSTM steps and 17 train-mode BatchNorms amplify rounding), so a
       second fp32 implementation cannot be held to a fixed 2e-4 there.
   (b) the all-bf16 HIP step (decoder heads + conv blocks + ResidualMLP linears, the
-      bench default) at the same inputs, bounded by the reference's OWN spread at
+      bench default; with and without the 16-bit LSTM recurrences) at the same inputs, bounded by the reference's OWN spread at
       16-bit precision (tests/golden/model_s256_b2_amp.npz: the reference step under
       torch.autocast('cpu', bfloat16) and under an emulation of CUDA autocast in
       bf16, each compared with the reference fp32 step).  Tolerance:
@@ -146,11 +146,16 @@ def test_fp32_step_vs_reference_golden_training_geometry(golden, name):
         assert abs(a - float(g["after_l2"][i])) <= tol, (k, a, float(g["after_l2"][i]), amb)
 
 
-def test_s256_bf16_step_within_reference_autocast_spread(golden):
+@pytest.mark.parametrize("lstm", ["fp32", "16-mixed"])
+def test_s256_bf16_step_within_reference_autocast_spread(golden, lstm):
+    """lstm "16-mixed": the encoders' LSTMs on the 16-bit MFMA recurrences as well (the
+    reference's autocast runs its LSTM in 16 bits; the Emu16 spread rounds the LSTM operands
+    and stores h / c in 16 bits)."""
     _need_gpu()
     g = golden("model_s256_b2")
     ga = golden("model_s256_b2_amp")
-    m = _model(256, head_precision="bf16", conv_precision="bf16", mlp_precision="bf16", concurrent_encoders=True)
+    m = _model(256, head_precision="bf16", conv_precision="bf16", mlp_precision="bf16", lstm_precision=lstm,
+               concurrent_encoders=True)
     fw, L = _forward_backward(m, g)
     report = {}
     for k in FW_KEYS:

@@ -45,7 +45,7 @@ def layer():
 
 def fwd(t):
     call("vt_lstm16_layer_fwd" if L16 else "vt_lstm_layer_fwd_x", ptr(t["x"]), In, ptr(t["wih"]), ptr(t["bih"]), ptr(t["whh"]), ptr(t["bhh"]), B, S, H,
-         ptr(t["h"]), ptr(t["hp"]), ptr(t["c"]), ptr(t["gates"]), stream())
+         ptr(t["h"]), None if L16 else ptr(t["hp"]), ptr(t["c"]), ptr(t["gates"]), stream())
 
 
 def bwd(t):
@@ -54,7 +54,8 @@ def bwd(t):
 
 
 def bww(t):
-    call("vt_lstm_layer_bwd_weight", ptr(t["dg"]), ptr(t["x"]), In, ptr(t["hp"]), B, S, H, ptr(t["dwih"]),
+    call("vt_lstm16_layer_bwd_weight" if L16 else "vt_lstm_layer_bwd_weight", ptr(t["dg"]), ptr(t["x"]), In,
+         ptr(t["h"] if L16 else t["hp"]), B, S, H, ptr(t["dwih"]),
          ptr(t["dwhh"]), ptr(t["db1"]), ptr(t["db2"]), 0, ptr(t["ws"]), t["ws"].numel(), stream())
 
 

@@ -710,4 +710,19 @@ int vt_lstm_layer_bwd_weight(const float* dgates, const float* x, int In, const 
     return VT_OK;
 }
 
+int vt_lstm16_layer_bwd_weight(const float* dgates, const float* x, int In, const float* h, int B, int seq,
+                               int hidden, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate,
+                               float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(hidden == H, "vt_lstm16_layer_bwd_weight: hidden size %d (kernel built for %d)", hidden, H);
+    VT_CHECK_ARG(B > 0 && seq > 0 && In > 0 && In + H + 1 <= SK_MAX_K1 && (int64_t)B * seq < ((int64_t)1 << 31),
+                 "vt_lstm16_layer_bwd_weight: shape (In %d)", In);
+    VT_CHECK_ARG(dgates && x && h && dw_ih && dw_hh && db_ih, "vt_lstm16_layer_bwd_weight: null pointer");
+    const int64_t R = (int64_t)B * seq;
+    const int rc = sk_linear_bwd_weight2(dgates, R, G4, x, In, h, H, dw_ih, dw_hh, db_ih, db_hh, accumulate, ws,
+                                         ws_floats, S(stream), seq);
+    VT_CHECK_ARG(rc == VT_OK, "vt_lstm16_layer_bwd_weight: workspace too small");
+    VT_LAUNCH_CHECK("vt_lstm16_layer_bwd_weight");
+    return VT_OK;
+}
+
 }  // extern "C"

@@ -18,14 +18,13 @@
 //
 // Forward: f16 operands (h in [-1, 1], layer inputs O(1): the reference's own
 // fp16), fp32 accumulate, fp32 cell state, gates and h written in fp32.  The
-// input projection x W_ih^T + b of the NEXT 16-step chunk is a dense chunk GEMM
-// (rows (sample, step) = 4 x 4 per M-tile, laid out so that its accumulator
-// lands in the lanes that consume it: no LDS round trip), KX MFMAs per step
-// issued under the step's LDS latency.
+// input projection x W_ih^T + b of a 16-step chunk is a dense chunk GEMM (rows
+// (sample, step) = 4 x 4 per M-tile, laid out so that its accumulator lands in
+// the lanes that consume it: no LDS round trip), one burst per chunk.
 // Backward: bf16 operands (gradients need fp32's exponent range: the
 // reference scales fp16 gradients with GradScaler, bf16 needs no scale), dh_rec
-// = dg_{t+1} W_hh as 8 MFMAs per wave and step; dX = dG W_ih of the previous
-// chunk as a dense chunk GEMM (2 MFMAs per step) from the chunk's bf16 dg image.
+// = dg_{t+1} W_hh as 8 MFMAs per wave and step; dX = dG W_ih of a chunk as a
+// dense chunk GEMM from the chunk's bf16 dg image, one burst per chunk.
 // dgates are written in fp32 for the weight gradients (vt_lstm_layer_bwd_weight).
 #include <stdlib.h>
 
@@ -37,8 +36,7 @@ namespace l16 {
 
 static constexpr int H = 64;
 static constexpr int G4 = 4 * H;
-static constexpr int NS = 4;    // samples per workgroup
-static constexpr int TC = 16;   // steps per chunk (4 M-tiles of 4 steps x 4 samples)
+static constexpr int TC = 16;   // steps per chunk
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -84,9 +82,12 @@ __device__ __forceinline__ float th2(float p) { return fmaf(2.f, sg2(p), -1.f); 
 __device__ __forceinline__ float gate_scale(int g) { return g == 2 ? 2.f * NL2E : NL2E; }
 
 // x [B, S, In] (In % 4 == 0, In <= 32 KX), w_ih [4H][In], w_hh [4H][H];
-// out_h / out_hprev / out_c [B, S, H]; gates [B, S, H, 4]: post-activation (i, f, g~, o) of
-// each unit contiguous (one 16-B store per lane and step; private to vt_lstm16_layer_bwd).
-template <int KX, int DIAG = 0>
+// out_h / out_c [B, S, H], out_hprev [B, S, H] (HP only); gates [B, S, H, 4]: post-activation
+// (i, f, g~, o) of each unit contiguous (one 16-B store per lane and step; private to
+// vt_lstm16_layer_bwd).  NS samples per workgroup (4 or 2): the 4 row groups of the MFMA
+// tiles hold samples lg & (NS - 1) — with NS = 2 the lanes of groups 2, 3 repeat groups 0, 1
+// and only groups 0, 1 store (half the per-CU store traffic, twice the workgroups).
+template <int NS, int KX, bool HP, int DIAG = 0>
 __global__ __launch_bounds__(G4) void k_lstm16_fwd(const float* __restrict__ x, int In, const float* __restrict__ wih,
                                                    const float* __restrict__ bih, const float* __restrict__ whh,
                                                    const float* __restrict__ bhh, int B, int S,
@@ -94,11 +95,13 @@ __global__ __launch_bounds__(G4) void k_lstm16_fwd(const float* __restrict__ x, 
                                                    float* __restrict__ out_c, float* __restrict__ gates) {
     __shared__ __attribute__((aligned(16))) _Float16 hs[2][NS][HS];
     const int j = threadIdx.x, lane = j & 63, w = j >> 6, ln = lane & 15, lg = lane >> 4;
-    const int u = 16 * w + ln;                 // this lane's unit; its sample is lg
+    const int u = 16 * w + ln;                 // this lane's unit; its sample is sl
+    const int sl = lg & (NS - 1), sa = (ln >> 2) & (NS - 1);   // the A row's sample: sa
+    const bool wr = NS == 4 || lg < NS;        // the lanes that store
     const int b0 = blockIdx.x * NS;
-    // output row base of (sample lg); lanes of samples past B compute the clamped sample's
+    // output row base of (sample sl); lanes of samples past B compute the clamped sample's
     // values bit for bit (same inputs, same instructions) and store them unmasked
-    const int64_t ob = (int64_t)(b0 + lg < B ? b0 + lg : B - 1) * S;
+    const int64_t ob = (int64_t)(b0 + sl < B ? b0 + sl : B - 1) * S;
     // recurrence B fragments: B[k][n] = W_hh[g H + u][k], k = 32 ks + 8 lg + e
     f16x8 bh[4][2];
     // input-projection B fragments: W_ih[g H + u][k] (zero for k >= In)
@@ -125,10 +128,11 @@ __global__ __launch_bounds__(G4) void k_lstm16_fwd(const float* __restrict__ x, 
         }
         bias[g] = (bih[g * H + u] + bhh[g * H + u]) * sc;
     }
-    // chunk-GEMM A operand: M-tile m, row rho = ln -> (sample ln >> 2, step 4 m + (ln & 3)),
-    // k = 32 ks + 8 lg + e; its accumulator element r is (sample lg, step 4 m + r) of this
-    // lane's unit — exactly the value this lane consumes at that step
-    const int xs = b0 + (ln >> 2) < B ? b0 + (ln >> 2) : B - 1;
+    // chunk-GEMM A operand: M-tile m, row rho = ln -> (sample sa, step 4 m + (ln & 3)),
+    // k = 32 ks + 8 lg + e; its accumulator element r is (sample sl, step 4 m + r) of this
+    // lane's unit — exactly the value this lane consumes at that step.  Computed at the start of
+// each chunk (x converted a chunk ahead, loaded two ahead).
+    const int xs = b0 + sa < B ? b0 + sa : B - 1;
     const float* xb = x + (int64_t)xs * S * In;
     float4 xr[4][KX][2];
     f16x8 xa[4][KX];
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(G4) void k_lstm16_fwd(const float* __restrict__ x, 
 #pragma unroll
             for (int ks = 0; ks < KX; ++ks) xa[m][ks] = to_f16(xr[m][ks][0], xr[m][ks][1]);
     };
-    f32x4 gc[4][4], gn[4][4];   // [m][g]: x W_ih^T + b of the current / next chunk
+    f32x4 gc[4][4];   // [m][g]: x W_ih^T + b of the current chunk
     auto xtile = [&](int m, int g) {
         f32x4 acc = f32x4{bias[g], bias[g], bias[g], bias[g]};
 #pragma unroll
@@ -163,27 +167,28 @@ __global__ __launch_bounds__(G4) void k_lstm16_fwd(const float* __restrict__ x, 
     for (int i = j; i < 2 * NS * HS; i += G4) (&hs[0][0][0])[i] = (_Float16)0.f;
     xload(0);
     xcvt();
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) gc[m][g] = xtile(m, g);
     xload(TC);
-    xcvt();
-    xload(2 * TC);
     lds_barrier();
     float c = 0.f, hprev = 0.f;
     for (int t0 = 0; t0 < S; t0 += TC) {
         const int n = S - t0 < TC ? S - t0 : TC;
-        const bool more = t0 + TC < S;
+        // the chunk's input projection as one burst of 16 KX MFMAs (issued per step beside the
+        // recurrence's MFMAs it cost ~130 ns per step), then the next chunk's x converted and
+        // the one after it loaded
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) gc[m][g] = xtile(m, g);
+        xcvt();
+        xload(t0 + 2 * TC);
 #pragma unroll
         for (int i = 0; i < TC; ++i) {
             if (i >= n) continue;   // block-uniform
             const int t = t0 + i;
             if constexpr ((DIAG & 2) != 0) stamp(reinterpret_cast<unsigned long long*>(out_hprev), t, 0);
-            const _Float16* hp = &hs[i & 1][ln >> 2][8 * lg];
+            const _Float16* hp = &hs[i & 1][sa][8 * lg];
             const f16x8 a0 = *reinterpret_cast<const f16x8*>(hp);
             const f16x8 a1 = *reinterpret_cast<const f16x8*>(hp + 32);
-            if (more) gn[i >> 2][i & 3] = xtile(i >> 2, i & 3);   // next chunk, under the LDS latency
             // C operand = the chunk GEMM's whole accumulator: every row of this lane's
             // 4-row group is its sample, so element r is step 4 m + r's pre-activation
             f32x4 p[4];
@@ -193,34 +198,31 @@ __global__ __launch_bounds__(G4) void k_lstm16_fwd(const float* __restrict__ x, 
                 p[g] = mma16(a1, bh[g][1], p[g]);
             }
             const int r = i & 3;
-            const float gi = sg2(p[0][r]), gf = sg2(p[1][r]), gg = th2(p[2][r]), go = sg2(p[3][r]);
+            float gi, gf, gg, go;
+            if constexpr ((DIAG & 16) != 0) {   // probe: no activations
+                gi = p[0][r] * 0.1f, gf = p[1][r] * 0.1f, gg = p[2][r] * 0.1f, go = p[3][r] * 0.1f;
+            } else {
+                gi = sg2(p[0][r]), gf = sg2(p[1][r]), gg = th2(p[2][r]), go = sg2(p[3][r]);
+            }
             if constexpr ((DIAG & 2) != 0) {
                 asm volatile("" ::"v"(gi), "v"(gf), "v"(gg), "v"(go));
                 stamp(reinterpret_cast<unsigned long long*>(out_hprev), t, 1);
             }
             c = cell_fwd_c(c, gi, gf, gg);
-            const float hn = go * th2(2.f * NL2E * c);
-            hs[(i + 1) & 1][lg][u] = (_Float16)hn;
+            const float hn = (DIAG & 16) ? go * c : go * th2(2.f * NL2E * c);
+            hs[(i + 1) & 1][sl][u] = (_Float16)hn;
             if constexpr ((DIAG & 2) != 0) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 stamp(reinterpret_cast<unsigned long long*>(out_hprev), t, 2);
             }
-            if constexpr (!(DIAG & 3)) {
+            if (!(DIAG & 3) && wr) {
                 *reinterpret_cast<float4*>(gates + ((ob + t) * H + u) * 4) = make_float4(gi, gf, gg, go);
                 out_h[(ob + t) * H + u] = hn;
-                out_hprev[(ob + t) * H + u] = hprev;
+                if constexpr (HP) out_hprev[(ob + t) * H + u] = hprev;
                 out_c[(ob + t) * H + u] = c;
             }
             hprev = hn;
             lds_barrier();
-        }
-        if (more) {
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) gc[m][g] = gn[m][g];
-            xcvt();
-            xload(t0 + 3 * TC);
         }
     }
 }
@@ -229,9 +231,6 @@ static constexpr int DS = G4 + 8;   // bf16 row stride of the dg image (528 B)
 
 // gate row of dg-image column k' (k' = 4 u + g: a lane's 4 gate derivatives are one 8-B store)
 __device__ __forceinline__ int krow(int k) { return (k & 3) * H + (k >> 2); }
-
-// tanh with relative accuracy ~1e-7 only in absolute terms (see th2)
-__device__ __forceinline__ float tanh16(float x) { return th2(2.f * NL2E * x); }
 
 // dh_out [B, S, H] (gradient at the layer's outputs), gates [B, S, H, 4] / cst from the
 // forward; dgates [B, S, 4H] fp32 (may be null), dx [B, S, In] (may be null), In <= 16 NTX.
@@ -248,7 +247,9 @@ __device__ __forceinline__ void cell_bwd16(float dh, float gi, float gf, float g
     v3 = d_o * go * (1.f - go);
 }
 
-template <int NTX, bool WD, int DIAG = 0>
+// NS samples per workgroup as in the forward.  The dX chunk GEMM's M-tiles hold RPS = 16 / NS
+// steps of each sample (row rho = RPS s + tl), TC NS / 16 tiles per chunk.
+template <int NS, int NTX, bool WD, int DIAG = 0>
 __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_out, const float* __restrict__ gates,
                                                    const float* __restrict__ cst, const float* __restrict__ whh,
                                                    const float* __restrict__ wih, int In, int B, int S,
@@ -258,8 +259,11 @@ __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_
     __shared__ __attribute__((aligned(16))) __bf16 dgs[2][TC][NS][DS];
     const int j = threadIdx.x, lane = j & 63, w = j >> 6, ln = lane & 15, lg = lane >> 4;
     const int u = 16 * w + ln;
+    const int sl = lg & (NS - 1), sa = (ln >> 2) & (NS - 1);
+    const bool wr = NS == 4 || lg < NS;
+    constexpr int RPS = 16 / NS, MT = TC * NS / 16;
     const int b0 = blockIdx.x * NS;
-    const int64_t ob = (int64_t)(b0 + lg < B ? b0 + lg : B - 1) * S;
+    const int64_t ob = (int64_t)(b0 + sl < B ? b0 + sl : B - 1) * S;
     // recurrence B fragments: B[k'][n] = W_hh[krow(k')][u], k' = 32 ks + 8 lg + e
     bf16x8 bw[8];
 #pragma unroll
@@ -304,22 +308,22 @@ __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_
 #pragma unroll
         for (int k = 0; k < 9; ++k) cc[k] = nc[k];
     };
-    f32x4 ax[4];
-    float* dxb = dx ? dx + ob * In : nullptr;
-    // dX tile m of the chunk at p0 from image buffer pb: k-steps [ks0, ks0 + nk)
-    auto dx_mma = [&](int pb, int m, int ks0, int nk) {
-        const __bf16* ap = &dgs[pb][4 * m + (ln & 3)][ln >> 2][8 * lg];
+    f32x4 ax[MT];
+    // dX tile m of a chunk from image buffer pb: A row rho = ln -> (sample ln / RPS, step
+    // m RPS + ln % RPS); accumulator row 4 lg + r -> (sample (4 lg + r) / RPS, step ...)
+    auto dx_mma = [&](int pb, int m) {
+        const __bf16* ap = &dgs[pb][m * RPS + ln % RPS][ln / RPS][8 * lg];
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (q >= ks0 && q < ks0 + nk) ax[m] = mmab(*reinterpret_cast<const bf16x8*>(ap + 32 * q), bxw[q], ax[m]);
+        for (int q = 0; q < 8; ++q) ax[m] = mmab(*reinterpret_cast<const bf16x8*>(ap + 32 * q), bxw[q], ax[m]);
     };
     // rows of samples past B hold the clamped sample's values bit for bit: stored unmasked
     auto dx_store = [&](int p0, int m) {
-        if (col >= In) return;
+        if (col >= In || !dx) return;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int t = p0 + 4 * m + r;
-            if (t < S) dxb[(int64_t)t * In + col] = ax[m][r];
+            const int row = 4 * lg + r, sr = row / RPS, t = p0 + m * RPS + row % RPS;
+            const int64_t b = b0 + sr < B ? b0 + sr : B - 1;
+            if (t < S) dx[(b * S + t) * In + col] = ax[m][r];
         }
     };
     const int tl0 = ((S - 1) / TC) * TC;   // first chunk processed (the last in time)
@@ -327,12 +331,8 @@ __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_
     lds_barrier();
     float dc = 0.f;
     int cur = 0;
-    int p0 = -1;   // start step of the previous (time-later) chunk, whose dX is pending
     for (int t0 = tl0; t0 >= 0; t0 -= TC) {
         const int n = S - t0 < TC ? S - t0 : TC;
-        const bool pend = p0 >= 0 && dxw;   // block-uniform
-#pragma unroll
-        for (int m = 0; m < 4; ++m) ax[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = TC - 1; i >= 0; --i) {
             if (i == 15) {   // upper half in hand, the lower half in flight
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_
             if constexpr ((DIAG & 2) != 0) stamp(reinterpret_cast<unsigned long long*>(dx), t, 0);
             // dh_rec = dg_{t+1} W_hh: A rows are the 4 samples' dg at t + 1 (zero at t = S - 1);
             // all 8 A fragments read before the first MFMA
-            const __bf16* ap = (i + 1 < TC) ? &dgs[cur][i + 1][ln >> 2][8 * lg] : &dgs[cur ^ 1][0][ln >> 2][8 * lg];
+            const __bf16* ap = (i + 1 < TC) ? &dgs[cur][i + 1][sa][8 * lg] : &dgs[cur ^ 1][0][sa][8 * lg];
             bf16x8 af[8];
 #pragma unroll
             for (int ks = 0; ks < 8; ++ks) af[ks] = *reinterpret_cast<const bf16x8*>(ap + 32 * ks);
@@ -362,42 +362,42 @@ __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_
             // pairs them one read ahead: 4 LDS round trips per step)
             __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
             __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-            // the previous chunk's dX: tile q >> 2, k-steps 2 (q & 3) .. +1 (q = processing order)
-            const int q = TC - 1 - i;
-            if (pend) dx_mma(cur ^ 1, q >> 2, 2 * (q & 3), 2);
             const float dh = cd[k8] + (a0[0] + a1[0]);
             if constexpr ((DIAG & 2) != 0) {
                 asm volatile("" ::"v"(dh));
                 stamp(reinterpret_cast<unsigned long long*>(dx), t, 1);
             }
             float v0, v1, v2, v3;
-            cell_bwd16(dh, cg[k8].x, cg[k8].y, cg[k8].z, cg[k8].w, tanh16(cc[k8 + 1]), cc[k8], dc, v0, v1, v2, v3);
+            // tanh(c_t) with lstm_cell.h's relative accuracy near 0 (dg_o is proportional to it;
+            // it depends on loaded c only, off the recurrence chain)
+            cell_bwd16(dh, cg[k8].x, cg[k8].y, cg[k8].z, cg[k8].w, ftanh(cc[k8 + 1]), cc[k8], dc, v0, v1, v2, v3);
             typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<bf16x4*>(&dgs[cur][i][lg][4 * u]) = bf16x4{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3};
+            *reinterpret_cast<bf16x4*>(&dgs[cur][i][sl][4 * u]) = bf16x4{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3};
             if constexpr ((DIAG & 2) != 0) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 stamp(reinterpret_cast<unsigned long long*>(dx), t, 2);
             }
-            if constexpr (WD && !(DIAG & 3)) {
+            if (WD && !(DIAG & 3) && wr) {
                 float* o = dgates + (ob + t) * G4 + u;
                 o[0] = v0;
                 o[H] = v1;
                 o[2 * H] = v2;
                 o[3 * H] = v3;
             }
-            if (pend && (q & 3) == 3 && !(DIAG & 2)) dx_store(p0, q >> 2);
             lds_barrier();
         }
-        p0 = t0;
-        cur ^= 1;
-    }
-    if (dxw && !(DIAG & 2)) {   // chunk 0's dX (its image is in dgs[cur ^ 1])
+        // the chunk's dX = dG W_ih as one burst of 32 MFMAs per column tile from the complete
+        // image (spread over the steps beside the recurrence's MFMAs it cost more than it hid)
+        if (dxw && !(DIAG & 2)) {
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            ax[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-            dx_mma(cur ^ 1, m, 0, 8);
-            dx_store(0, m);
+            for (int m = 0; m < MT; ++m) {
+                ax[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+                dx_mma(cur, m);
+            }
+#pragma unroll
+            for (int m = 0; m < MT; ++m) dx_store(t0, m);
         }
+        cur ^= 1;
     }
 }
 
@@ -405,6 +405,54 @@ __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_
 }  // namespace vt
 
 using namespace vt::l16;
+
+namespace {
+
+// samples per workgroup: VAETEB_L16_NS (2 or 4; default 2)
+static int l16_ns() {
+    static const int ns = getenv("VAETEB_L16_NS") ? atoi(getenv("VAETEB_L16_NS")) : 2;
+    return ns == 4 ? 4 : 2;
+}
+// timing probes only (outputs not valid): 1 no stores, 2 in-kernel stamps
+static int l16_diag() {
+    static const int d = getenv("VAETEB_L16_DIAG") ? atoi(getenv("VAETEB_L16_DIAG")) : 0;
+    return d == 1 || d == 2 ? d : 0;
+}
+
+template <int NS, int KX>
+static void fwd_launch(dim3 grid, hipStream_t st, const float* x, int In, const float* w_ih, const float* b_ih,
+                       const float* w_hh, const float* b_hh, int B, int seq, float* h, float* hp, float* c,
+                       float* gates) {
+#define VT_L16F(HP_, D_) \
+    hipLaunchKernelGGL((k_lstm16_fwd<NS, KX, HP_, D_>), grid, dim3(G4), 0, st, x, In, w_ih, b_ih, w_hh, b_hh, B, seq, \
+                       h, hp, c, gates)
+    switch (l16_diag()) {
+        case 1: VT_L16F(false, 1); break;
+        case 2: VT_L16F(true, 2); break;
+        default:
+            if (hp) VT_L16F(true, 0);
+            else VT_L16F(false, 0);
+    }
+#undef VT_L16F
+}
+
+template <int NS, int NTX>
+static void bwd_launch(dim3 grid, hipStream_t st, const float* dh_out, const float* gates, const float* cst,
+                       const float* w_hh, const float* w_ih, int In, int B, int seq, float* dgates, float* dx) {
+#define VT_L16B(W_, D_)                                                                                            \
+    hipLaunchKernelGGL((k_lstm16_bwd<NS, NTX, W_, D_>), grid, dim3(G4), 0, st, dh_out, gates, cst, w_hh, w_ih, In, \
+                       B, seq, dgates, dx)
+    switch (l16_diag()) {
+        case 1: VT_L16B(true, 1); break;
+        case 2: VT_L16B(true, 2); break;
+        default:
+            if (dgates) VT_L16B(true, 0);
+            else VT_L16B(false, 0);
+    }
+#undef VT_L16B
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -414,21 +462,18 @@ int vt_lstm16_layer_fwd(const float* x, int In, const float* w_ih, const float* 
     VT_CHECK_ARG(hidden == H, "vt_lstm16_layer_fwd: hidden size %d (kernel built for %d)", hidden, H);
     VT_CHECK_ARG(B > 0 && seq > 0 && In > 0 && In <= 64 && In % 4 == 0,
                  "vt_lstm16_layer_fwd: shape (input size %d: a multiple of 4, at most 64)", In);
-    VT_CHECK_ARG(x && w_ih && b_ih && w_hh && b_hh && out_h && out_hprev && out_c && gates,
-                 "vt_lstm16_layer_fwd: null pointer");
-    const dim3 grid((B + NS - 1) / NS);
-    static const int diag = getenv("VAETEB_L16_DIAG") ? atoi(getenv("VAETEB_L16_DIAG")) : 0;   // timing probes only
-#define VT_L16F(K_, D_)                                                                                        \
-    hipLaunchKernelGGL((k_lstm16_fwd<K_, D_>), grid, dim3(G4), 0, vt::S(stream), x, In, w_ih, b_ih, w_hh, b_hh, B, \
-                       seq, out_h, out_hprev, out_c, gates)
-    if (diag == 1) {
-        if (In <= 32) VT_L16F(1, 1); else VT_L16F(2, 1);
-    } else if (diag == 2) {
-        if (In <= 32) VT_L16F(1, 2); else VT_L16F(2, 2);
+    VT_CHECK_ARG(x && w_ih && b_ih && w_hh && b_hh && out_h && out_c && gates, "vt_lstm16_layer_fwd: null pointer");
+    VT_CHECK_ARG(l16_diag() != 2 || out_hprev, "vt_lstm16_layer_fwd: the stamp probe writes into out_hprev");
+    const int ns = l16_ns();
+    const dim3 grid((B + ns - 1) / ns);
+    hipStream_t st = vt::S(stream);
+    if (ns == 4) {
+        if (In <= 32) fwd_launch<4, 1>(grid, st, x, In, w_ih, b_ih, w_hh, b_hh, B, seq, out_h, out_hprev, out_c, gates);
+        else fwd_launch<4, 2>(grid, st, x, In, w_ih, b_ih, w_hh, b_hh, B, seq, out_h, out_hprev, out_c, gates);
     } else {
-        if (In <= 32) VT_L16F(1, 0); else VT_L16F(2, 0);
+        if (In <= 32) fwd_launch<2, 1>(grid, st, x, In, w_ih, b_ih, w_hh, b_hh, B, seq, out_h, out_hprev, out_c, gates);
+        else fwd_launch<2, 2>(grid, st, x, In, w_ih, b_ih, w_hh, b_hh, B, seq, out_h, out_hprev, out_c, gates);
     }
-#undef VT_L16F
     VT_LAUNCH_CHECK("vt_lstm16_layer_fwd");
     return VT_OK;
 }
@@ -440,22 +485,18 @@ int vt_lstm16_layer_bwd(const float* dh_out, const float* gates, const float* cs
     VT_CHECK_ARG(B > 0 && seq > 0 && In > 0 && In <= 64, "vt_lstm16_layer_bwd: shape (input size %d, at most 64)",
                  In);
     VT_CHECK_ARG(dh_out && gates && cst && w_hh && (w_ih || !dx), "vt_lstm16_layer_bwd: null pointer");
-    const dim3 grid((B + NS - 1) / NS);
-    const int ntx = (In + 15) / 16;
-    static const int diag = getenv("VAETEB_L16_DIAG") ? atoi(getenv("VAETEB_L16_DIAG")) : 0;   // timing probes only
-#define VT_L16B_(N_, W_, D_)                                                                                    \
-    hipLaunchKernelGGL((k_lstm16_bwd<N_, W_, D_>), grid, dim3(G4), 0, vt::S(stream), dh_out, gates, cst, w_hh, w_ih, \
-                       In, B, seq, dgates, dx)
-#define VT_L16B(N_)                                 \
-    case N_:                                        \
-        if (diag == 1) VT_L16B_(N_, true, 1);       \
-        else if (diag == 2) VT_L16B_(N_, true, 2);  \
-        else if (dgates) VT_L16B_(N_, true, 0);     \
-        else VT_L16B_(N_, false, 0);                \
-        break;
-    switch (ntx) { VT_L16B(1) VT_L16B(2) VT_L16B(3) VT_L16B(4) }
-#undef VT_L16B_
-#undef VT_L16B
+    VT_CHECK_ARG(l16_diag() != 2 || dx, "vt_lstm16_layer_bwd: the stamp probe writes into dx");
+    const int ns = l16_ns();
+    const dim3 grid((B + ns - 1) / ns);
+    hipStream_t st = vt::S(stream);
+    // column tiles of dX: 2 cover In <= 32 (the encoders' first layers: 20 / 32), 4 the rest
+    if (ns == 4) {
+        if (In <= 32) bwd_launch<4, 2>(grid, st, dh_out, gates, cst, w_hh, w_ih, In, B, seq, dgates, dx);
+        else bwd_launch<4, 4>(grid, st, dh_out, gates, cst, w_hh, w_ih, In, B, seq, dgates, dx);
+    } else {
+        if (In <= 32) bwd_launch<2, 2>(grid, st, dh_out, gates, cst, w_hh, w_ih, In, B, seq, dgates, dx);
+        else bwd_launch<2, 4>(grid, st, dh_out, gates, cst, w_hh, w_ih, In, B, seq, dgates, dx);
+    }
     VT_LAUNCH_CHECK("vt_lstm16_layer_bwd");
     return VT_OK;
 }

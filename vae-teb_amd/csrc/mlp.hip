@@ -204,7 +204,8 @@ static constexpr int DW_THREADS = 512;
 
 // part[blk][n][k'] = sum over the workgroup's rows of dY[r][n] * X1[r][k'], where
 // X1 = [X | X2 | 1] (X2 [R, K2] optional, K2 = 0 without; k' = K + K2 is the
-// bias column when with_bias).  NTN x NTK tile pairs over 8 waves, PPW pairs
+// bias column when with_bias).  x2_shift > 0: X2's row r is the given matrix's row r - 1,
+// zero where r % x2_shift == 0 (an LSTM's h_{t-1} read from h, x2_shift = S).  NTN x NTK tile pairs over 8 waves, PPW pairs
 // per wave: when PPW is a multiple of NTK a wave owns PPW / NTK whole tile rows
 // (its A fragments are read once per k-step for all NTK pairs of a row), else
 // pairs are dealt round-robin.  The next 64-row chunk is loaded into registers
@@ -213,7 +214,7 @@ template <int NTN, int NTK>
 __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ dY, const float* __restrict__ X,
                                                       int64_t R, int N, int K, const float* __restrict__ X2, int K2,
                                                       int with_bias, int64_t rows_per_block,
-                                                      float* __restrict__ part) {
+                                                      float* __restrict__ part, int x2_shift) {
     constexpr int HS = 16 * NTN + ((NTN & 1) ? 0 : 16);  // == 16 mod 32
     constexpr int XS2 = 16 * NTK + ((NTK & 1) ? 0 : 16);
     constexpr int PAIRS = NTN * NTK, PPW = (PAIRS + 7) / 8;
@@ -234,6 +235,7 @@ __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ 
     float vh[UH], vx[UX];
     auto load = [&](int64_t c0) {  // dY rows [t][n] and X1 rows [t][k'] of the chunk at c0
         const int n = re - c0 < DW_ROWS ? (int)(re - c0) : DW_ROWS;
+        const int rm0 = x2_shift > 0 ? (int)(c0 % x2_shift) : 0;   // the chunk's first row within its sample
 #pragma unroll
         for (int u = 0; u < UH; ++u) {
             const int i = tid + DW_THREADS * u;
@@ -245,9 +247,22 @@ __global__ __launch_bounds__(DW_THREADS) void k_sk_dw(const float* __restrict__ 
             const int i = tid + DW_THREADS * u;
             const int t = i / (16 * NTK), c = i - t * (16 * NTK);
             float x = 0.f;
-            if (i < XT && t < n)
-                x = c < K ? X[(c0 + t) * K + c]
-                          : (c < KX ? X2[(c0 + t) * K2 + (c - K)] : (c == KX && with_bias ? 1.f : 0.f));
+            if (i < XT && t < n) {
+                if (c < K) {
+                    x = X[(c0 + t) * K + c];
+                } else if (c < KX) {
+                    if (x2_shift > 0) {   // R < 2^31 rows (checked by the caller)
+                        int rm = rm0 + t;   // (c0 + t) mod x2_shift: one subtraction when x2_shift >= DW_ROWS
+                        if (x2_shift >= DW_ROWS) rm = rm >= x2_shift ? rm - x2_shift : rm;
+                        else rm %= x2_shift;
+                        x = rm ? X2[(c0 + t - 1) * K2 + (c - K)] : 0.f;
+                    } else {
+                        x = X2[(c0 + t) * K2 + (c - K)];
+                    }
+                } else {
+                    x = c == KX && with_bias ? 1.f : 0.f;
+                }
+            }
             vx[u] = x;
         }
     };
@@ -382,11 +397,11 @@ int sk_linear_bwd_data(const float* dY, int64_t R, int N, const float* W, int K,
 
 template <int NTN>
 static void sk_dw_k(int NTK, dim3 grid, hipStream_t st, const float* dY, const float* X, int64_t R, int N, int K,
-                    const float* X2, int K2, int wb, int64_t rpb, float* part) {
+                    const float* X2, int K2, int wb, int64_t rpb, float* part, int x2_shift) {
 #define VT_DWK(K_)                                                                                                 \
     case K_:                                                                                                       \
         hipLaunchKernelGGL((k_sk_dw<NTN, K_>), grid, dim3(DW_THREADS), 0, st, dY, X, R, N, K, X2, K2, wb, rpb,     \
-                           part);                                                                                  \
+                           part, x2_shift);                                                                        \
         break;
     switch (NTK) {
         VT_DWK(1) VT_DWK(2) VT_DWK(3) VT_DWK(4) VT_DWK(5) VT_DWK(6) VT_DWK(7) VT_DWK(8) VT_DWK(9)
@@ -410,8 +425,9 @@ int64_t sk_dw_workspace(int64_t R, int N, int K) { return sk_dw_blocks(R) * N * 
 
 int sk_linear_bwd_weight2(const float* dY, int64_t R, int N, const float* X, int K, const float* X2, int K2,
                           float* dW, float* dW2, float* db, float* db2, int accumulate, float* ws, int64_t ws_floats,
-                          hipStream_t st) {
+                          hipStream_t st, int x2_shift) {
     const int K1 = K + K2 + (db ? 1 : 0);
+    if (x2_shift > 0 && R >= ((int64_t)1 << 31)) return VT_ERR_ARG;
     const int NTN = (N + 15) / 16, NTK = (K1 + 15) / 16;
     if (NTN > 16 || NTK > 9) return VT_ERR_ARG;
     int64_t blocks = sk_dw_blocks(R);
@@ -423,16 +439,16 @@ int sk_linear_bwd_weight2(const float* dY, int64_t R, int N, const float* X, int
     dim3 grid((unsigned)blocks);
     const int wb = db != nullptr;
     switch (NTN) {
-        case 1: sk_dw_k<1>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        case 2: sk_dw_k<2>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        case 3: sk_dw_k<3>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        case 4: sk_dw_k<4>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        case 5: sk_dw_k<5>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        case 6: sk_dw_k<6>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        case 7: sk_dw_k<7>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        case 8: sk_dw_k<8>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        case 9: sk_dw_k<9>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
-        default: sk_dw_k<16>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws); break;
+        case 1: sk_dw_k<1>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        case 2: sk_dw_k<2>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        case 3: sk_dw_k<3>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        case 4: sk_dw_k<4>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        case 5: sk_dw_k<5>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        case 6: sk_dw_k<6>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        case 7: sk_dw_k<7>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        case 8: sk_dw_k<8>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        case 9: sk_dw_k<9>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
+        default: sk_dw_k<16>(NTK, grid, st, dY, X, R, N, K, X2, K2, wb, rpb, ws, x2_shift); break;
     }
     const int64_t total = (int64_t)N * K1;
     hipLaunchKernelGGL(k_sk_sum, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, ws, (int)blocks, N, K, K2, K1,

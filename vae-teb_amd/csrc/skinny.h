@@ -22,6 +22,6 @@ int sk_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int 
 // dW (+)= dY^T X, dW2 (+)= dY^T X2, db (and db2) (+)= column sums of dY, in one pass over dY
 int sk_linear_bwd_weight2(const float* dY, int64_t R, int N, const float* X, int K, const float* X2, int K2,
                           float* dW, float* dW2, float* db, float* db2, int accumulate, float* ws, int64_t ws_floats,
-                          hipStream_t st);
+                          hipStream_t st, int x2_shift = 0);
 
 }  // namespace vt

@@ -682,14 +682,18 @@ class LSTMF(torch.autograd.Function):
             w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
             In = inp.shape[-1]
             h = torch.empty((B, S, H), device=x.device)
-            hp = torch.empty_like(h)
             c = torch.empty_like(h)
             gates = torch.empty((B, S, 4 * H), device=x.device)
             if half and In <= 64 and In % 4 == 0:
-                # 16-bit MFMA recurrence over 4-sample tiles (f16 operands, fp32 state)
+                # 16-bit MFMA recurrence over sample tiles (f16 operands, fp32 state); no h_{t-1}
+                # output: the weight gradient reads it from h (vt_lstm16_layer_bwd_weight)
                 call("vt_lstm16_layer_fwd", ptr(inp), In, ptr(w_ih), ptr(b_ih), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h),
-                     ptr(hp), ptr(c), ptr(gates), _st())
-            elif LSTM_FUSED and In <= 64:
+                     None, ptr(c), ptr(gates), _st())
+                saved += [inp, h, c, gates]
+                inp = h
+                continue
+            hp = torch.empty_like(h)
+            if LSTM_FUSED and In <= 64:
                 # input projection inside the recurrence kernel (bitwise the unfused result)
                 call("vt_lstm_layer_fwd_x", ptr(inp), In, ptr(w_ih), ptr(b_ih), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h),
                      ptr(hp), ptr(c), ptr(gates), _st())
@@ -721,11 +725,13 @@ class LSTMF(torch.autograd.Function):
             inp, hp, c, gates = saved[4 * l: 4 * l + 4]
             w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
             In = inp.shape[-1]
+            half = ctx.half and In <= 64 and In % 4 == 0   # hp is then h (read shifted by one step)
+            wfn = "vt_lstm16_layer_bwd_weight" if half else "vt_lstm_layer_bwd_weight"
             dg = torch.empty((B, S, 4 * H), device=gy.device)
             need_dx = l > 0 or ctx.needs_input_grad[0]
             fused = LSTM_FUSED and In <= 64
             gin = torch.empty((B, S, In), device=gy.device) if need_dx else None
-            if ctx.half and In <= 64 and In % 4 == 0:
+            if half:
                 # bf16-MFMA recurrence, dX = dG W_ih inside; dG in fp32 for the weight gradients
                 call("vt_lstm16_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), ptr(w_ih), In, B, S, H, ptr(dg),
                      ptr(gin) if need_dx else None, _st())
@@ -737,13 +743,13 @@ class LSTMF(torch.autograd.Function):
                 call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
                 if need_dx:
                     call("vt_linear_bwd_data", ptr(dg), B * S, 4 * H, ptr(w_ih), In, ptr(gin), 0, _st())
-            if LSTM_FUSED and In + H + 1 <= 144:
+            if (LSTM_FUSED or half) and In + H + 1 <= 144:
                 # every parameter gradient of the layer in one pass over dg
                 pg = _ParamGrads([w_ih, w_hh, b_ih, b_hh], [True] * 4)
                 if pg.direct and LSTM_GRAD_DEFER:
                     # in-place sinks: issued after the last layer's recurrence (below), so
                     # the layer-to-layer dh chain is not interrupted by them
-                    deferred.append((dg, inp, In, hp, pg))
+                    deferred.append((dg, inp, In, hp, pg, wfn))
                 else:
                     side = LSTM_GRAD_STREAM if (pg.direct and LSTM_GRAD_STREAM is not None) else None
                     if side is not None and side.cuda_stream != _lib.stream():
@@ -751,12 +757,12 @@ class LSTMF(torch.autograd.Function):
                         _lib.wait_for(side)
                         with torch.cuda.stream(side):
                             ws_s = WS.get(WS_LINEAR, gy.device, 1)
-                            call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                            call(wfn, ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
                                  *[ptr(t) for t in pg.out], pg.acc, ptr(ws_s), ws_s.numel(), _st())
                         for t in (dg, inp, hp):
                             t.record_stream(side)
                     else:
-                        call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                        call(wfn, ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
                              *[ptr(t) for t in pg.out], pg.acc, ptr(ws), ws.numel(), _st())
                     grads[4 * l: 4 * l + 4] = pg.result()
             else:
@@ -802,10 +808,10 @@ class LSTMF(torch.autograd.Function):
                 _lib.wait_for(side)
             with torch.cuda.stream(side if on_side else torch.cuda.current_stream()):
                 ws_d = WS.get(WS_LINEAR, gy.device, 1)
-                for dg, inp, In, hp, pg in deferred:
-                    call("vt_lstm_layer_bwd_weight", ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                for dg, inp, In, hp, pg, wfn in deferred:
+                    call(wfn, ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
                          *[ptr(t) for t in pg.out], pg.acc, ptr(ws_d), ws_d.numel(), _st())
-            for dg, inp, In, hp, pg in deferred:
+            for dg, inp, In, hp, pg, wfn in deferred:
                 if on_side:
                     for t in (dg, inp, hp):
                         t.record_stream(side)
