@@ -91,7 +91,14 @@ def profile_mfma(ROOT_=None):
     step).  Returns (ms per step, csv path) or (None, None)."""
     import csv
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_step*.csv")), key=os.path.getmtime)
+    # latest round first (profiles/rNN); within a round, the file named in profiles/rNN/LATEST
+    # when present, else the most recently written
+    def key(f):
+        d = os.path.dirname(f)
+        latest = os.path.join(d, "LATEST")
+        pinned = os.path.exists(latest) and open(latest).read().strip() == os.path.basename(f)
+        return (os.path.basename(d), pinned, os.path.getmtime(f))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_step*.csv")), key=key)
     for f in reversed(files):
         rows = list(csv.DictReader(open(f)))
         steps = sum(int(r["Calls"]) for r in rows if "k_adamw4" in r["Name"])
@@ -273,7 +280,7 @@ def main():
     ap.add_argument("--mlp", choices=["bf16", "fp32"], default="bf16",
                     help="ResidualMLP stacks: Linear layers on bf16 MFMA with fp32 accumulation, LayerNorm fp32 "
                          "(bf16 for the reference's fp16 autocast) or exact fp32")
-    ap.add_argument("--lstm", choices=["16-mixed", "fp32"], default="fp32",
+    ap.add_argument("--lstm", choices=["16-mixed", "fp32"], default="16-mixed",
                     help="encoder LSTMs: 16-bit MFMA recurrences over 4-sample tiles (f16 forward / bf16 backward "
                          "operands, fp32 state: the reference's own 16-mixed LSTM width) or exact fp32")
     args = ap.parse_args()
