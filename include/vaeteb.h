@@ -364,6 +364,27 @@ int vt_conv1d_bwd_dx_bf16_bn(const float* dY, const float* Xc, const float* bnp,
 int vt_conv1d_bwd_weight_bf16_dy16(const void* dY16, const float* X, int B, int L_in, int Cin, int Cout, int K,
                                    int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
                                    void* stream);
+/* The same with the bf16 rows of dY16 dys elements apart (a multiple of 8, >= ceil8(Cout);
+ * the rows of vt_batchnorm_bwd_x16 are ceil32(Cout)).                              */
+int vt_conv1d_bwd_weight_bf16_dy16s(const void* dY16, int dys, const float* X, int B, int L_in, int Cin, int Cout,
+                                    int K, int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
+                                    void* stream);
+/* Conv-block backward in two launches on a bf16 operand (conv_bwd16.hip):
+ * vt_batchnorm_bwd_x16: the BatchNorm input gradient of vt_conv1d_bwd_gpad_bf16_bn (the
+ *   same bits) written once, in bf16, rows of ceil32(C) channels (padding 0), from dY, the
+ *   pre-BN conv output Xc and bnp (vt_batchnorm_bwd_coef); M rows.
+ * vt_conv1d_bwd_dx16: dX (B, L_in, Cin) of the conv (W as in vt_conv1d_bwd_gpad_bf16: w16t
+ *   from vt_conv1d_bf16_shadow) from that operand (B, L_out, ceil32(Cout)) — the padded
+ *   gradient and vt_conv1d_fold in one launch (x2 upsample: the fold applied in LDS;
+ *   reflect without upsample: mirror rows through edge [B][2 pad][Cin]).  Geometries:
+ *   causal without upsample, reflect with L_in*(1+up) > pad.  Bit-identical to
+ *   vt_conv1d_bwd_gpad_bf16_bn + vt_conv1d_fold.
+ * replaces: the BatchNorm1d + Conv1d (+ F.interpolate x2) backward of the conv blocks
+ *           (ref/model/vae_teb_model.py:170-176, :225-232 under autograd)             */
+int vt_batchnorm_bwd_x16(const float* dY, const float* Xc, const float* bnp, int act, int64_t M, int C, void* d16,
+                         void* stream);
+int vt_conv1d_bwd_dx16(const void* d16, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode, int up,
+                       float* dX, float* edge, void* stream);
 /* Direct (LDS-windowed) conv kernels used on the training path (conv.hip), K <= 11:
  * forward; bwd-data as a full correlation into gpad (B, L_out+K-1, Cin) + fold;
  * bwd-weight with fixed-order split reduction.                                   */

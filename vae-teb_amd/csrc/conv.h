@@ -99,6 +99,8 @@ int bn_stats_finalize_launch(const float* stats, int tiles_per_sample, int B, in
                              float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
                              hipStream_t st);
 int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st);
+// conv_bf16.hip: the reflect mirror rows of a direct-dX backward-data conv added back (k_conv_fold_edges)
+void fold_edges_launch(float* dx, const float* edge, int B, int L, int pad, int C, hipStream_t st);
 int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,
                     const float* beta, int act, float* y, hipStream_t st);
 

@@ -665,6 +665,11 @@ __global__ void k_conv_fold_edges(float* __restrict__ dx, const float* __restric
 constexpr int KMAXB = 11;
 
 }  // namespace
+
+void fold_edges_launch(float* dx, const float* edge, int B, int L, int pad, int C, hipStream_t st) {
+    hipLaunchKernelGGL(k_conv_fold_edges, dim3((unsigned)((2 * pad * C + 255) / 256), (unsigned)B), dim3(256), 0, st,
+                       dx, edge, L, pad, C);
+}
 }  // namespace vt
 
 using namespace vt;
@@ -754,15 +759,15 @@ int vt_conv1d_bwd_dx_bf16_bn(const float* dY, const float* Xc, const float* bnp,
     if (rc) return rc;
     if (mode == 1 && f.pad > 0) {
         VT_CHECK_ARG(B <= 65535, "vt_conv1d_bwd_dx_bf16_bn: batch");
-        hipLaunchKernelGGL(k_conv_fold_edges, dim3((unsigned)((2 * f.pad * Cin + 255) / 256), (unsigned)B), dim3(256),
-                           0, S(stream), dX, edge, L_in, f.pad, Cin);
+        fold_edges_launch(dX, edge, B, L_in, f.pad, Cin, S(stream));
         VT_LAUNCH_CHECK("vt_conv1d_bwd_dx_bf16_bn");
     }
     return VT_OK;
 }
 
 static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode, int up,
-                      float* dW, int accumulate, float* ws, int64_t ws_floats, hipStream_t st, const __bf16* dy16) {
+                      float* dW, int accumulate, float* ws, int64_t ws_floats, hipStream_t st, const __bf16* dy16,
+                      int dys = 0) {
     VT_CHECK_ARG(B > 0 && L_in > 0 && K > 0 && K <= KMAXB && Cin > 0 && Cout > 0 && Cin <= 128 && Cout <= 128,
                  "vt_conv1d_bwd_weight_bf16: shape (K <= %d, channels <= 128)", KMAXB);
     Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
@@ -789,7 +794,7 @@ static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin,
     // row strides (bf16): channels rounded to 16, + 8 (rows start 16 B apart mod 64 banks)
     const int dstride = 16 * cdiv(Cout, 16) + 8, xstride = 16 * cdiv(Cin, 16) + 8;
     const size_t lds = (size_t)(DWR * dstride + (DWR + KMAXB + 8) * xstride) * 2;
-    const int dys = (Cout + 7) & ~7;
+    if (dys == 0) dys = (Cout + 7) & ~7;
     dim3 grid(bx, (unsigned)splits);
 #define VT_DWB(KK, PP)                                                                                         \
     if (K == KK && ppw == PP) {                                                                                \
@@ -831,6 +836,15 @@ int vt_conv1d_bwd_weight_bf16_dy16(const void* dY16, const float* X, int B, int 
     VT_CHECK_ARG(dY16 != nullptr, "vt_conv1d_bwd_weight_bf16_dy16: null dY16");
     return bwd_weight(nullptr, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream),
                       (const __bf16*)dY16);
+}
+
+int vt_conv1d_bwd_weight_bf16_dy16s(const void* dY16, int dys, const float* X, int B, int L_in, int Cin, int Cout,
+                                    int K, int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
+                                    void* stream) {
+    VT_CHECK_ARG(dY16 != nullptr && dys >= ((Cout + 7) & ~7) && dys % 8 == 0,
+                 "vt_conv1d_bwd_weight_bf16_dy16s: null dY16 or row stride %d (a multiple of 8 >= ceil8(Cout))", dys);
+    return bwd_weight(nullptr, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream),
+                      (const __bf16*)dY16, dys);
 }
 
 }  // extern "C"

@@ -69,6 +69,9 @@ LSTM_FUSED = int(os.environ.get("VAETEB_LSTM_FUSED", "1"))
 LSTM_GRAD_DEFER = int(os.environ.get("VAETEB_LSTM_GRAD_DEFER", "1"))
 # bf16 conv backward-data written straight into dX where the fold is a crop; 0: gpad + fold
 CONV_DIRECT_DX = int(os.environ.get("VAETEB_CONV_DIRECT_DX", "1"))
+# conv-block backward as vt_batchnorm_bwd_x16 + vt_conv1d_bwd_dx16 (bf16 operand written once,
+# upsample fold inside the conv); 0: the fused-staging kernels (vt_conv1d_bwd_*_bf16_bn)
+CONV_BWD16 = int(os.environ.get("VAETEB_CONV_BWD16", "1"))
 
 
 class _ParamGrads:
@@ -496,7 +499,22 @@ class ConvBNActF(torch.autograd.Function):
         ws = WS.get(4096 * Cout + 2 * Cout, x.device, 2)
         M = B * Lo
         fused = bf16 and ctx.needs_input_grad[0]
-        if fused:
+        pad = K - 1 if mode == 0 else (K - 1) // 2
+        # two-launch backward (vt_batchnorm_bwd_x16 + vt_conv1d_bwd_dx16): every geometry of the
+        # model's blocks (causal; reflect with L_up > pad, x2 upsample folded in the conv)
+        bwd16 = fused and CONV_BWD16 and (mode == 1 and L * (2 if up else 1) > pad or mode == 0 and not up)
+        if bwd16:
+            bnp = torch.empty(6 * Cout, device=x.device)
+            call("vt_batchnorm_bwd_coef", ptr(gy), ptr(conv), M, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b),
+                 ACT[act], ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(bnp), ptr(ws), ws.numel(), _st())
+            c32 = (Cout + 31) // 32 * 32
+            dxbn = torch.empty(M * c32, dtype=torch.bfloat16, device=x.device)
+            call("vt_batchnorm_bwd_x16", ptr(gy), ptr(conv), ptr(bnp), ACT[act], M, Cout, ptr(dxbn), _st())
+            srcs = (dxbn,)
+            dw_args = lambda wsx: (ptr(dxbn), c32, ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc,
+                                   ptr(wsx), wsx.numel(), _st())
+            fn = "vt_conv1d_bwd_weight_bf16_dy16s"
+        elif fused:
             # fused BatchNorm backward: only the column sums here; the bf16 backward-data
             # conv forms the BN input gradient while staging its operand from (gy, conv,
             # bnp) and leaves it in bf16 (dxbn) for the weight gradient
@@ -519,8 +537,11 @@ class ConvBNActF(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
-            pad = K - 1 if mode == 0 else (K - 1) // 2
-            if fused and CONV_DIRECT_DX and not up and (mode == 0 or L > pad):
+            if bwd16:
+                edge = WS.get(max(B * 2 * pad * Cin, 1), x.device, 3)
+                call("vt_conv1d_bwd_dx16", ptr(dxbn), B, L, Cin, ptr(w16t), Cout, K, mode, up, ptr(gx), ptr(edge),
+                     _st())
+            elif fused and CONV_DIRECT_DX and not up and (mode == 0 or L > pad):
                 # the fold is a crop: the conv writes gx itself (reflect: + the mirrored edge rows)
                 edge = WS.get(max(B * 2 * pad * Cin, 1), x.device, 3)
                 call("vt_conv1d_bwd_dx_bf16_bn", ptr(gy), ptr(conv), ptr(bnp), ACT[act], M, B, L, Cin, ptr(w16t),
