@@ -255,11 +255,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--graph", action="store_true",
-                    help="replay the model step as a captured hipGraph (double-buffered, front-end one step ahead) "
-                         "instead of dispatching every op from Python (default: eager, currently faster)")
-    ap.add_argument("--native", action="store_true",
-                    help="graph mode replayed by the library's multi-stream executor (vt_stepgraph_*) instead of "
-                         "hipGraphLaunch; the reparameterisation noise is drawn eagerly each step")
+                    help="= --mode graph: the model step replayed as a captured hipGraph (double-buffered, "
+                         "front-end one step ahead)")
+    ap.add_argument("--mode", choices=["auto", "eager", "native", "graph"], default="auto",
+                    help="auto (default): native on one GPU (the eager step's ~190 C-ABI calls from Python take "
+                         "about as long as the GPU work), eager with several GPUs (the bucketed all-reduce overlaps "
+                         "the backward there; a captured step reduces after it) and for c4 (host-side dropout "
+                         "seeds); native: the step captured once and replayed by the library's multi-stream "
+                         "executor (vt_stepgraph_*); graph: hipGraphLaunch; eager: every op from Python")
+    ap.add_argument("--native", action="store_true", help="= --mode native")
     ap.add_argument("--streams", type=int, default=4, help="--native: executor streams")
     ap.add_argument("--overlap-fe", action="store_true",
                     help="--native: run the next batch's front-end one step ahead on its own stream (as --graph) "
@@ -286,6 +290,11 @@ def main():
     args = ap.parse_args()
 
     rank, world, local, dev = init_distributed()
+    mode = "native" if args.native else ("graph" if args.graph else args.mode)
+    if mode == "auto":
+        mode = "native" if (world == 1 and args.workload == "c2" and not (args.prefetch or args.overlap_update)) \
+            else "eager"
+    args.native, args.graph = mode == "native", mode == "graph"
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     torch.cuda.set_device(dev)
     if args.workload == "c5":
@@ -342,7 +351,7 @@ def main():
         if args.native:
             eps_shape = (B, S, model.latent_dim_z)
             caps = [trainer.capture(fe(pool[j]), eps=torch.randn(eps_shape, device=dev), native=True,
-                                    n_streams=args.streams) for j in range(2)]
+                                    n_streams=args.streams) for j in range(2 if args.overlap_fe else 1)]
         else:
             caps = [trainer.capture(fe(pool[0])), trainer.capture(fe(pool[1]))]
         main = torch.cuda.current_stream()
