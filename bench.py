@@ -265,6 +265,9 @@ def main():
                          "executor (vt_stepgraph_*); graph: hipGraphLaunch; eager: every op from Python")
     ap.add_argument("--native", action="store_true", help="= --mode native")
     ap.add_argument("--streams", type=int, default=4, help="--native: executor streams")
+    ap.add_argument("--overlap-adam", type=int, default=0,
+                    help="native: 1 = the step captured without AdamW, which runs after each replay on a side "
+                         "stream, overlapping the next batch's front-end (independent of the weights)")
     ap.add_argument("--overlap-fe", action="store_true",
                     help="--native: run the next batch's front-end one step ahead on its own stream (as --graph) "
                          "instead of inline before each replay")
@@ -351,7 +354,11 @@ def main():
         if args.native:
             eps_shape = (B, S, model.latent_dim_z)
             caps = [trainer.capture(fe(pool[j]), eps=torch.randn(eps_shape, device=dev), native=True,
-                                    n_streams=args.streams) for j in range(2 if args.overlap_fe else 1)]
+                                    n_streams=args.streams, update=not args.overlap_adam)
+                    for j in range(2 if args.overlap_fe else 1)]
+            if args.overlap_adam:
+                from vaeteb.model import side_stream
+                adam_side = side_stream(dev.index or 0, 1)
         else:
             caps = [trainer.capture(fe(pool[0])), trainer.capture(fe(pool[1]))]
         main = torch.cuda.current_stream()
@@ -374,6 +381,10 @@ def main():
                 # this step's noise (drawn outside the graph) and the replay
                 fe(pool[i % 2], out=caps[0].static_in)
                 torch.randn(caps[0].static_eps.shape, out=caps[0].static_eps)
+                if args.overlap_adam:
+                    # the previous step's AdamW (side stream) ran beside this front-end: join it
+                    _lib.wait_for(torch.cuda.current_stream(), adam_side)
+                    return caps[0].replay(adam_stream=adam_side)
                 return caps[0].replay()
             if i == 0 or step.first:
                 frontend_into(i)

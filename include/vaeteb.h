@@ -330,6 +330,12 @@ int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, v
  * 0 octets per lane, 2 lanes along channels (coalesced row segments), 1 (default) lanes
  * along channels for the fused-BN backward-data kernels with K >= 7, octets elsewhere. */
 int vt_conv_bf16_set_staging(int mode);
+/* Kernel selection of the bf16 conv forward / weight gradient (A/B; bit-identical results):
+ * bit 0 = the flat-staged forward of conv_fwd16.hip (source rows copied with float4 loads,
+ * the whole bf16 window formed in LDS, next chunk's taps prefetched) for K <= 5, bit 1 = the
+ * flat-staged, prefetching weight gradient (k_cdw16) for K >= 7 — where each measured faster
+ * (default 3) — bit 2 = both at every K; 0 = k_conv_bf16 / k_conv_dw_bf16 everywhere.   */
+int vt_conv_bf16_set_kernels(int flags);
 int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode,
                           int up, const float* gamma, const float* beta, int act, float eps, float momentum,
                           float* conv_out, float* Y, float* mean, float* rstd, float* run_mean, float* run_var,

@@ -125,3 +125,70 @@ def test_bwd16_block_matches_fused_in_autograd(L):
                 ops.CONV_BWD16 = 1
         for t0, t1 in zip(*res):
             assert torch.equal(t0, t1)
+
+
+FWD_GEOS = GEOS + [(2, 5, 33, 22, 3, 1, 1), (2, 2, 20, 13, 9, 1, 0), (3, 1, 8, 8, 3, 1, 0), (2, 9, 16, 16, 11, 0, 0),
+                   (2, 300, 1, 16, 3, 0, 0), (2, 40, 130, 100, 5, 1, 1), (2, 257, 87, 77, 1, 1, 0)]
+
+
+@pytest.mark.parametrize("geo", FWD_GEOS)
+def test_flat_staged_forward_bitwise(L, geo):
+    """vt_conv_bf16_set_kernels: the flat-staged forward (conv_fwd16.hip, default) and
+    k_conv_bf16 give the same conv output, BatchNorm statistics and running statistics,
+    bit for bit (same tiles, accumulation order and interpolation arithmetic)."""
+    B, Lin, Cin, Cout, K, mode, up = geo
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    torch.manual_seed(5 * sum(geo))
+    x = torch.randn(B, Lin, Cin, device="cuda")
+    w = torch.randn(Cout, Cin, K, device="cuda") / (Cin * K) ** 0.5
+    w16, _ = _shadow(L, w)
+    gam = 1 + 0.1 * torch.randn(Cout, device="cuda")
+    bet = 0.1 * torch.randn(Cout, device="cuda")
+    ws = torch.empty(1 << 22, device="cuda")
+    outs = []
+    try:
+        for flags in (0, 7):
+            L.call("vt_conv_bf16_set_kernels", flags)
+            conv = torch.full((B, Lo, Cout), float("nan"), device="cuda")
+            y = torch.full_like(conv, float("nan"))
+            mean, rstd = torch.empty(Cout, device="cuda"), torch.empty(Cout, device="cuda")
+            rm, rv = torch.zeros(Cout, device="cuda"), torch.ones(Cout, device="cuda")
+            L.call("vt_conv1d_bn_fwd_bf16", L.ptr(x), B, Lin, Cin, L.ptr(w16), Cout, K, mode, up, L.ptr(gam),
+                   L.ptr(bet), 1, 1e-5, 0.9, L.ptr(conv), L.ptr(y), L.ptr(mean), L.ptr(rstd), L.ptr(rm), L.ptr(rv),
+                   L.ptr(ws), ws.numel(), L.stream())
+            y2 = torch.full_like(conv, float("nan"))
+            L.call("vt_conv1d_fwd_bf16", L.ptr(x), B, Lin, Cin, L.ptr(w16), Cout, K, mode, up, L.ptr(y2), L.stream())
+            torch.cuda.synchronize()
+            outs.append((conv, y, mean, rstd, rm, rv, y2))
+    finally:
+        L.call("vt_conv_bf16_set_kernels", 3)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), ((a != b).sum().item(), a.numel())
+
+
+@pytest.mark.parametrize("geo", [g for g in FWD_GEOS if g[2] <= 128 and g[3] <= 128])
+def test_flat_staged_weight_grad_bitwise(L, geo):
+    """vt_conv_bf16_set_kernels bit 1: the flat-staged, prefetching weight gradient
+    (k_cdw16, default) and k_conv_dw_bf16 on the same bf16 dY rows give the same dW bit for
+    bit (same splits, chunks, pairs and MFMA order; the window's values by up_lerp)."""
+    B, Lin, Cin, Cout, K, mode, up = geo
+    Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
+    M = B * Lo
+    torch.manual_seed(9 * sum(geo))
+    x = torch.randn(B, Lin, Cin, device="cuda")
+    c32 = (Cout + 31) // 32 * 32
+    d16 = torch.zeros(M, c32, dtype=torch.bfloat16, device="cuda")
+    d16[:, :Cout] = torch.randn(M, Cout, device="cuda").bfloat16()
+    wsw = torch.empty(8 << 20, device="cuda")
+    outs = []
+    try:
+        for flags in (0, 7):
+            L.call("vt_conv_bf16_set_kernels", flags)
+            dw = torch.full((Cout, Cin, K), float("nan"), device="cuda")
+            L.call("vt_conv1d_bwd_weight_bf16_dy16s", L.ptr(d16), c32, L.ptr(x), B, Lin, Cin, Cout, K, mode, up,
+                   L.ptr(dw), 0, L.ptr(wsw), wsw.numel(), L.stream())
+            torch.cuda.synchronize()
+            outs.append(dw)
+    finally:
+        L.call("vt_conv_bf16_set_kernels", 3)
+    assert torch.equal(outs[0], outs[1]), ((outs[0] != outs[1]).sum().item(), outs[0].numel())

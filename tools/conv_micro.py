@@ -25,3 +25,13 @@ for (a, b, k, u) in Decoder.SPEC:
     torch.cuda.synchronize()
     print(f"block {a}->{b} k{k} up{int(u)} L{L}", flush=True)
     L = L * (2 if u else 1)
+# encoder blocks (causal, L = S = 256)
+for (c, k) in [(32, 3), (32, 5), (32, 7), (16, 3), (16, 5), (16, 7)]:
+    blk = ConvBlock(c, c, k, causal=True).to(dev)
+    blk.bf16 = True
+    x = torch.randn(B, 256, c, device=dev, requires_grad=True)
+    for _ in range(3):
+        y = blk(x)
+        y.backward(torch.randn_like(y))
+    torch.cuda.synchronize()
+    print(f"encoder block {c} k{k}", flush=True)

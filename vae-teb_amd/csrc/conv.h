@@ -11,6 +11,14 @@ struct Geo {
     int B, L_in, Cin, Cout, K, up, mode, L_up, pad, L_out;
 };
 
+// the x2 linear upsample's value between source samples a, b (weight l1 on b): one
+// definition with contraction off, so every kernel that stages an upsampled window
+// (bf16 forward / weight gradient, the flat-staged forward) rounds it identically
+__device__ __forceinline__ float up_lerp(float a, float b, float l1) {
+#pragma clang fp contract(off)
+    return (1.f - l1) * a + l1 * b;
+}
+
 // input value at padded position tp (upsampled domain) — see gemm.hip conv_src
 __device__ __forceinline__ float src_val(const float* __restrict__ xb, const Geo& g, int tp, int ci) {
     int t = tp - g.pad;
@@ -28,7 +36,7 @@ __device__ __forceinline__ float src_val(const float* __restrict__ xb, const Geo
     const int i0 = (int)s;
     const int i1 = i0 + 1 < g.L_in ? i0 + 1 : g.L_in - 1;
     const float l1 = s - (float)i0;
-    return (1.f - l1) * xb[(int64_t)i0 * g.Cin + ci] + l1 * xb[(int64_t)i1 * g.Cin + ci];
+    return up_lerp(xb[(int64_t)i0 * g.Cin + ci], xb[(int64_t)i1 * g.Cin + ci], l1);
 }
 
 
@@ -58,6 +66,54 @@ __device__ __forceinline__ bool src_row(const Geo& g, int tp, int& i0, int& i1, 
     return true;
 }
 
+// source rows [lo, hi] of input x (B, L_in, Cin) that padded positions [t0, t0 + n) read
+// (conv.h src_row over the range): the up-domain rows t = tp - pad map monotonically in the
+// interior, reflect (mode 1, L_up > pad) folds t < 0 onto [1, pad] and t >= L_up onto
+// [L_up - 1 - pad, L_up - 2], replicate (L_up <= pad) stays within [0, L_up), zero padding
+// (mode 0) reads nothing outside; the x2 upsample reads rows i0(t) .. i1(t) around t / 2
+__device__ __forceinline__ void src_span(const Geo& g, int t0, int n, int& lo, int& hi) {
+    const int ta = t0 - g.pad, tz = t0 + n - 1 - g.pad;
+    int a = 0x7fffffff, z = -1;
+    if (g.mode == 0) {
+        a = ta > 0 ? ta : 0;
+        z = tz < g.L_up - 1 ? tz : g.L_up - 1;
+    } else if (g.L_up <= g.pad) {
+        a = 0;
+        z = g.L_up - 1;
+    } else {
+        if (tz >= 0 && ta <= g.L_up - 1) {
+            a = ta > 0 ? ta : 0;
+            z = tz < g.L_up - 1 ? tz : g.L_up - 1;
+        }
+        if (ta < 0) {
+            const int l = -tz > 1 ? -tz : 1;
+            a = l < a ? l : a;
+            z = -ta > z ? -ta : z;
+        }
+        if (tz >= g.L_up) {
+            const int l = 2 * (g.L_up - 1) - tz;
+            const int h = 2 * (g.L_up - 1) - (ta > g.L_up ? ta : g.L_up);
+            a = l < a ? l : a;
+            z = h > z ? h : z;
+        }
+    }
+    if (z < a) {
+        lo = 0;
+        hi = -1;
+        return;
+    }
+    if (!g.up) {
+        lo = a;
+        hi = z;
+        return;
+    }
+    float sa = (a + 0.5f) * 0.5f - 0.5f, sz = (z + 0.5f) * 0.5f - 0.5f;
+    sa = sa < 0.f ? 0.f : sa;
+    sz = sz < 0.f ? 0.f : sz;
+    lo = (int)sa;
+    hi = (int)sz + 1 < g.L_in ? (int)sz + 1 : g.L_in - 1;
+}
+
 // NC consecutive channels cb .. cb + NC - 1 of padded position tp (src_val for each,
 // 0 where !ok or past Cin) with every load issued before any use: the row mapping
 // is computed once, addresses are clamped into the sample and the values masked
@@ -80,7 +136,7 @@ __device__ __forceinline__ void src_vec(const float* __restrict__ xb, const Geo&
     }
 #pragma unroll
     for (int j = 0; j < NC; ++j)
-        v[j] = (in && cb + j < g.Cin) ? (g.up ? (1.f - l1) * a[j] + l1 * b[j] : a[j]) : 0.f;
+        v[j] = (in && cb + j < g.Cin) ? (g.up ? up_lerp(a[j], b[j], l1) : a[j]) : 0.f;
 }
 
 static inline Geo geo(int B, int L_in, int Cin, int Cout, int K, int mode, int up) {
@@ -99,6 +155,8 @@ int bn_stats_finalize_launch(const float* stats, int tiles_per_sample, int B, in
                              float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
                              hipStream_t st);
 int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st);
+// conv_fwd16.hip: the flat-staged bf16 forward (returns its position tile, or VT_ERR_ARG)
+int cfw16_launch(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st);
 // conv_bf16.hip: the reflect mirror rows of a direct-dX backward-data conv added back (k_conv_fold_edges)
 void fold_edges_launch(float* dx, const float* edge, int B, int L, int pad, int C, hipStream_t st);
 int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,

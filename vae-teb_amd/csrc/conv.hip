@@ -472,22 +472,30 @@ __global__ __launch_bounds__(256) void k_sum_splits_grp(float* __restrict__ part
     if (i >= n) return;
     const int s0 = blockIdx.y * SG_GRP;
     const int s1 = s0 + SG_GRP < splits ? s0 + SG_GRP : splits;
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    int s = s0;
-    for (; s + 4 <= s1; s += 4)
+    // every load of the group in flight at once, then a fixed pairwise tree
+    float a[SG_GRP];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) a[u] += part[(int64_t)(s + u) * n + i];
-    for (; s < s1; ++s) a[0] += part[(int64_t)s * n + i];
-    part[(int64_t)s0 * n + i] = (a[0] + a[1]) + (a[2] + a[3]);
+    for (int u = 0; u < SG_GRP; ++u) a[u] = s0 + u < s1 ? part[(int64_t)(s0 + u) * n + i] : 0.f;
+#pragma unroll
+    for (int w = SG_GRP / 2; w >= 1; w /= 2)
+#pragma unroll
+        for (int u = 0; u < w; ++u) a[u] += a[u + w];
+    part[(int64_t)s0 * n + i] = a[0];
 }
 
 __global__ __launch_bounds__(256) void k_sum_splits_fin(const float* __restrict__ part, int splits, int64_t n,
                                                         float* __restrict__ out, int accumulate) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    float a = 0.f;
-    for (int s0 = 0; s0 < splits; s0 += SG_GRP) a += part[(int64_t)s0 * n + i];
-    out[i] = accumulate ? out[i] + a : a;
+    // the group sums (<= SG_GRP of them: splits <= SG_GRP^2) in flight at once, fixed tree
+    float a[SG_GRP];
+#pragma unroll
+    for (int u = 0; u < SG_GRP; ++u) a[u] = u * SG_GRP < splits ? part[(int64_t)u * SG_GRP * n + i] : 0.f;
+#pragma unroll
+    for (int w = SG_GRP / 2; w >= 1; w /= 2)
+#pragma unroll
+        for (int u = 0; u < w; ++u) a[u] += a[u + w];
+    out[i] = accumulate ? out[i] + a[0] : a[0];
 }
 
 // part is scratch: the two-stage path overwrites it
@@ -497,6 +505,7 @@ int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int 
                            accumulate);
         return VT_OK;
     }
+    if (splits > SG_GRP * SG_GRP) return VT_ERR_ARG;
     float* p = const_cast<float*>(part);
     const unsigned bx = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_sum_splits_grp, dim3(bx, (unsigned)((splits + SG_GRP - 1) / SG_GRP)), dim3(256), 0, st, p,

@@ -113,7 +113,7 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
             float v = 0.f;
             if (ok[u]) {
                 if constexpr (BNB) v = bn_bwd_val_r(a[u], q[u], pm, prs, pga, pbe, pdg, pdb, act, invM);
-                else v = g.up ? (1.f - l1[u]) * a[u] + l1[u] * q[u] : a[u];
+                else v = g.up ? up_lerp(a[u], q[u], l1[u]) : a[u];
             }
             xs[r * RS + cl] = (__bf16)v;
             if constexpr (BNB) {
@@ -132,6 +132,8 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
 // but the forward and every K = 3 instance slower (K 3 BNB 32 -> 260 us: 11-33 channel rows
 // leave most of the 32 channel lanes idle)
 int g_conv_cl = 1;
+// kernel selection (vt_conv_bf16_set_kernels): bit 0 the flat-staged forward (conv_fwd16.hip)
+int g_conv_kern = 3;   // bit 1: the flat-staged weight gradient (k_cdw16); bit 2: both at every K
 
 // x: fp32 (B, L_in, g.Cin) activations; w16: [g.Cout][K][cin32] bf16 shadow.
 // BNB (backward-data only: causal geometry, no upsample): x is the block output
@@ -423,6 +425,7 @@ __global__ void k_conv_shadow(const float* __restrict__ W, int Cout, int Cin, in
 // k_sum_splits.
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 constexpr int DWR = 64;  // rows per staged chunk (2 MFMA k-steps)
+constexpr int KMAXB_DW = 11;
 
 __device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int row0, int col0, int stride) {
     // lane 4q+p of each 16-lane group addresses row (row0 + q), columns col0 + 4p .. +3; two reads
@@ -580,6 +583,168 @@ __global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restri
     }
 }
 
+// The weight gradient with flat staging and a register-prefetched next chunk (round 3;
+// vt_conv_bf16_set_kernels bit 1): the MFMA body, pair assignment, splits and 64-row
+// chunks of k_conv_dw_bf16<.., DYB = true> (bit-identical partial slabs), the operands
+// staged as in conv_fwd16.hip — dY from its bf16 rows by 16-byte loads, the input window's
+// source rows copied with float4 loads into LDS (F) and formed into the bf16 image there
+// (padding / x2 interpolation by up_lerp, the values of src_vec).  The next chunk's dY
+// segments and F rows are loaded into registers before the current chunk's MFMAs.
+constexpr int CDW_UD = 4;    // dY 16-byte segments per thread and chunk (256 threads)
+constexpr int CDW_UF = 8;    // F float4 per thread and chunk (256 threads)
+
+template <int K, int PPW, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ dyb16, int dys,
+                                                   const float* __restrict__ x, Geo g, int64_t rows_per_split,
+                                                   int NTc, int npairs, int dstride, int xstride,
+                                                   float* __restrict__ part, int64_t total) {
+    constexpr int NT = 64 * NWV;
+    constexpr int UD = CDW_UD * 256 / NT, UF = CDW_UF * 256 / NT;
+    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
+    __bf16* ds = lb;                          // [DWR][dstride]   dY rows
+    __bf16* xs = lb + DWR * dstride;          // [DWR + K - 1 (+pad)][xstride] input window
+    float* F = reinterpret_cast<float*>(lb + DWR * dstride + (DWR + KMAXB_DW + 8) * xstride);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int mt[PPW], nt[PPW];
+    bool act[PPW];
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+        const int p = blockIdx.x * (NWV * PPW) + wv + NWV * j;
+        act[j] = p < npairs;
+        mt[j] = act[j] ? p / NTc : 0;
+        nt[j] = act[j] ? p - mt[j] * NTc : 0;
+    }
+    const int64_t rows = (int64_t)g.B * g.L_out;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
+    const int64_t r1 = r0 + rows_per_split < rows ? r0 + rows_per_split : rows;
+    f32x4 acc[PPW][K];
+#pragma unroll
+    for (int j = 0; j < PPW; ++j)
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int cout16 = (g.Cout + 15) / 16 * 16, cin16 = (g.Cin + 15) / 16 * 16;
+    const int dsegs = cout16 / 8;
+    // one chunk's operands into registers: dY segments and the F rows (float4 from the
+    // boundary at or below the source run)
+    bf16x8 dv[UD];
+    float4 fv[UF];
+    struct Chunk {
+        int b, t0, n, lo, hi, off;
+    };
+    auto load = [&](int64_t r, Chunk& c) {
+        c.b = (int)(r / g.L_out);
+        c.t0 = (int)(r - (int64_t)c.b * g.L_out);
+        c.n = g.L_out - c.t0 < DWR ? g.L_out - c.t0 : DWR;
+        if (r + c.n > r1) c.n = (int)(r1 - r);
+        const __bf16* db = dyb16 + ((int64_t)c.b * g.L_out + c.t0) * dys;
+#pragma unroll
+        for (int u = 0; u < UD; ++u) {
+            const int i = tid + NT * u;
+            const int t = i / dsegs, sg = i - t * dsegs;
+            const bool ok = i < DWR * dsegs && t < c.n && 8 * sg < dys;
+            dv[u] = *(const bf16x8*)(db + (int64_t)(ok ? t : 0) * dys + (ok ? 8 * sg : 0));
+            if (!ok) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) dv[u][j] = (__bf16)0.f;
+            }
+        }
+        src_span(g, c.t0, c.n + K - 1, c.lo, c.hi);
+        const int64_t f0 = ((int64_t)c.b * g.L_in + c.lo) * g.Cin;
+        const int64_t fa = f0 & ~(int64_t)3;
+        c.off = (int)(f0 - fa);
+        const int nf = c.hi >= c.lo ? (int)(((int64_t)c.b * g.L_in + c.hi + 1) * g.Cin - fa) : 0;
+        const int nv = (nf + 3) >> 2;
+#pragma unroll
+        for (int u = 0; u < UF; ++u) {
+            const int i = tid + NT * u;
+            const int64_t e = fa + 4 * (int64_t)i;
+            if (i < nv && e + 3 < total) {
+                fv[u] = *reinterpret_cast<const float4*>(x + e);
+            } else {
+                fv[u].x = i < nv && e < total ? x[e] : 0.f;
+                fv[u].y = i < nv && e + 1 < total ? x[e + 1] : 0.f;
+                fv[u].z = i < nv && e + 2 < total ? x[e + 2] : 0.f;
+                fv[u].w = 0.f;
+            }
+        }
+    };
+    Chunk cur;
+    if (r0 < r1) load(r0, cur);
+    for (int64_t r = r0; r < r1;) {
+        // registers -> LDS: dY rows, F
+#pragma unroll
+        for (int u = 0; u < UD; ++u) {
+            const int i = tid + NT * u;
+            if (i < DWR * dsegs) {
+                const int t = i / dsegs, sg = i - t * dsegs;
+                *(bf16x8*)(ds + t * dstride + 8 * sg) = dv[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UF; ++u) reinterpret_cast<float4*>(F)[tid + NT * u] = fv[u];
+        __syncthreads();
+        // F -> the bf16 window image (rows t0 .. t0 + DWR + K - 2, zero past n + K - 1), 8 channels
+        // of one row per item
+        {
+            const int osegs = cin16 / 8;
+            for (int i = tid; i < (DWR + K - 1) * osegs; i += NT) {
+                const int t = i / osegs, o = i - t * osegs;
+                const int tp = cur.t0 + t, cb = 8 * o;
+                int i0 = 0, i1 = 0;
+                float l1 = 0.f;
+                const bool in = t < cur.n + K - 1 && src_row(g, tp, i0, i1, l1);
+                const float* p0 = F + cur.off + (in ? i0 - cur.lo : 0) * g.Cin;
+                const float* p1 = F + cur.off + (in ? i1 - cur.lo : 0) * g.Cin;
+                bf16x8 v;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
+                    const float a = p0[c];
+                    const float q = g.up ? p1[c] : 0.f;
+                    v[j] = (__bf16)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
+                }
+                *(bf16x8*)(xs + t * xstride + cb) = v;
+            }
+        }
+        __syncthreads();
+        const int64_t rn = r + cur.n;
+        Chunk nxt = cur;
+        if (rn < r1) load(rn, nxt);   // in flight during the MFMAs
+#pragma unroll
+        for (int s = 0; s < DWR / 32; ++s) {
+            if (!act[0]) break;  // wave-uniform: a wave without pairs only stages
+#pragma unroll
+            for (int j = 0; j < PPW; ++j) {
+                const bf16x8 a = tr_frag(ds, 32 * s, 16 * mt[j], dstride);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const bf16x8 bb = tr_frag(xs, 32 * s + k, 16 * nt[j], xstride);
+                    acc[j][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[j][k], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+        cur = nxt;
+        r = rn;
+    }
+    const int lr = lane & 15, lc = lane >> 4;
+    const int64_t slot = blockIdx.y;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+        if (!act[j]) continue;
+        const int ci = 16 * nt[j] + lr;
+        if (ci >= g.Cin) continue;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int co = 16 * mt[j] + 4 * lc + rr;
+            if (co >= g.Cout) continue;
+            float* pp = part + ((slot * g.Cout + co) * g.Cin + ci) * K;
+#pragma unroll
+            for (int k = 0; k < K; ++k) pp[k] = acc[j][k][rr];
+        }
+    }
+}
+
 // BatchNorm-backward staging (k_conv_bf16 / k_conv_dw_bf16 BNB): dy, the pre-BN
 // conv output, the packed per-channel parameters (6 x C), activation and 1/M
 struct BnB {
@@ -594,6 +759,12 @@ template <int K, int NT>
 int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
           hipStream_t st, const BnB* bn, FoldOut fo) {
     using C = BCfg<K, NT>;
+    // flat-staged forward where it measured faster than k_conv_bf16 (isolated, decoder
+    // geometry: K 5 / 3 layers 60 -> 52, 102 -> 60 us; K >= 7 slower: 30 -> 43 us at K 11)
+    if (x && !bn && (g_conv_kern & 1) && (K <= 5 || (g_conv_kern & 4)) && fo.pad < 0 && ((uintptr_t)x & 15) == 0) {
+        const int tp = cfw16_launch(x, g, w16, y, Lo, stats, st);
+        if (tp > 0) return tp;
+    }
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
     const bool cl = g_conv_cl == 2 || (g_conv_cl == 1 && bn && K >= 7);
     if (x && bn && cl)
@@ -679,6 +850,12 @@ extern "C" {
 int vt_conv_bf16_set_staging(int mode) {
     VT_CHECK_ARG(mode >= 0 && mode <= 2, "vt_conv_bf16_set_staging: mode %d not in 0..2", mode);
     g_conv_cl = mode;
+    return VT_OK;
+}
+
+int vt_conv_bf16_set_kernels(int flags) {
+    VT_CHECK_ARG(flags >= 0 && flags <= 7, "vt_conv_bf16_set_kernels: flags %d not in 0..7", flags);
+    g_conv_kern = flags;
     return VT_OK;
 }
 
@@ -796,9 +973,24 @@ static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin,
     const size_t lds = (size_t)(DWR * dstride + (DWR + KMAXB + 8) * xstride) * 2;
     if (dys == 0) dys = (Cout + 7) & ~7;
     dim3 grid(bx, (unsigned)splits);
+    // flat-staged kernel: F rows of a chunk fit the per-thread prefetch and LDS
+    const int f_rows = (up ? (DWR + K - 1) / 2 + 3 : DWR + K - 1);
+    const int64_t f_floats = (int64_t)f_rows * Cin + 8;
+    // flat-staged weight gradient where it measured faster (K 9 / 7: 176 -> 111, 184 -> 118 us;
+    // K <= 5 slower: 85 -> 108 us)
+    const bool flat = (g_conv_kern & 2) && (K >= 7 || (g_conv_kern & 4)) && dy16 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)dy16 & 15) == 0 &&
+                      dys % 8 == 0 && f_floats <= (int64_t)4 * CDW_UF * 256 && 16 * cdiv(Cout, 16) <= 8 * CDW_UD * 32;
+    const size_t lds_flat = lds + (size_t)4 * CDW_UF * 256 * 4;
+    const int64_t total_x = (int64_t)B * L_in * Cin;
 #define VT_DWB(KK, PP)                                                                                         \
     if (K == KK && ppw == PP) {                                                                                \
-        if (dy16 && nwv == 8)                                                                             \
+        if (flat && nwv == 8)                                                                                  \
+            hipLaunchKernelGGL((k_cdw16<KK, PP, 8>), grid, dim3(512), lds_flat, st, dy16, dys, X, g, rps, NTc,   \
+                               npairs, dstride, xstride, ws, total_x);                                        \
+        else if (flat)                                                                                         \
+            hipLaunchKernelGGL((k_cdw16<KK, PP, 4>), grid, dim3(256), lds_flat, st, dy16, dys, X, g, rps, NTc,   \
+                               npairs, dstride, xstride, ws, total_x);                                        \
+        else if (dy16 && nwv == 8)                                                                             \
             hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true, 8>), grid, dim3(512), lds, st, dY, X, g, rps, NTc,  \
                                npairs, dstride, xstride, ws, dy16, dys);                                      \
         else if (dy16)                                                                                         \

@@ -115,11 +115,14 @@ struct BdGeo {
     int L_up;     // upsampled length (UPF)
     int TS;       // UPF: input rows owned per workgroup
     float* edge;  // non-UPF reflect: mirrored rows [B][2 pad][Co] (nullable: crop only)
+    int p_first;  // non-UPF: first padded row computed (causal crop: pad; reflect: 0)
+    int p_end;    // non-UPF: one past the last padded row computed
 };
 
 template <int K, int NT>
 struct DCfg {
-    static constexpr int PM = NT <= 2 ? 4 : 2;
+    // position blocks per wave: taller tiles for the narrow layers (more MFMA work per staged window)
+    static constexpr int PM = NT <= 2 ? 8 : 2;
     static constexpr int TC = 16 * NT, TP = 64 * PM, WIN = TP + K - 1;
     static constexpr int WB = K * TC * RS;                       // bf16 elements of one tap chunk
     static constexpr int NWI = (K * TC * 4 + 255) / 256;         // 16-byte tap items per thread
@@ -192,15 +195,17 @@ __global__ __launch_bounds__(256) void k_cbd16(const __bf16* __restrict__ d16, B
         s1 = s0 + g.TS < g.L ? s0 + g.TS : g.L;
         p0 = s0 == 0 ? 0 : 2 * s0 - 1 + g.pad;
     } else {
-        p0 = blockIdx.x * TP;
+        p0 = g.p_first + blockIdx.x * TP;   // causal: only the rows the crop keeps (p_first = pad)
     }
+    bf16x8 wt[C::NWI];
+    load_taps<K, NT>(wt, w16t, co0, g.Co, c32, 0);   // in flight during the window staging
     // the operand window: d16 rows p0 - (K - 1) .. p0 - (K - 1) + WIN - 1 of sample b, all chunks
     // (one contiguous run of rows in HBM), 16-byte items, zero outside [0, Lf)
     {
         const int segs = 4 * nch;
         const __bf16* db = d16 + (int64_t)b * g.Lf * c32;
         const int rbase = p0 - (K - 1);
-        constexpr int U = 4;
+        constexpr int U = 8;
         for (int i0 = tid; i0 < WIN * segs; i0 += 256 * U) {
             bf16x8 v[U];
 #pragma unroll
@@ -224,8 +229,6 @@ __global__ __launch_bounds__(256) void k_cbd16(const __bf16* __restrict__ d16, B
             }
         }
     }
-    bf16x8 wt[C::NWI];
-    load_taps<K, NT>(wt, w16t, co0, g.Co, c32, 0);
     store_taps<K, NT>(wt, ws, co0, g.Co);
     __syncthreads();
     f32x4 acc[PM][NT];
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(256) void k_cbd16(const __bf16* __restrict__ d16, B
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int p = p0 + PM * 16 * wv + 16 * m + 4 * lc + r;
-                if (p >= g.Lp) continue;
+                if (p >= g.p_end) continue;
                 const int sx = p - g.pad;
                 float* yr;
                 if (sx >= 0 && sx < g.L) yr = dx + ((int64_t)b * g.L + sx) * g.Co;
@@ -338,7 +341,7 @@ int cbd_nt(const __bf16* d16, BdGeo g, int B, const __bf16* w16t, float* dx, boo
         dim3 grid(cdiv(g.L, g.TS), cdiv(g.Co, C::TC), B);
         hipLaunchKernelGGL((k_cbd16<K, NT, true>), grid, dim3(256), lds, st, d16, g, w16t, dx);
     } else {
-        dim3 grid(cdiv(g.Lp, C::TP), cdiv(g.Co, C::TC), B);
+        dim3 grid(cdiv(g.p_end - g.p_first, C::TP), cdiv(g.Co, C::TC), B);
         hipLaunchKernelGGL((k_cbd16<K, NT, false>), grid, dim3(256), lds, st, d16, g, w16t, dx);
     }
     return VT_OK;
@@ -406,6 +409,8 @@ int vt_conv1d_bwd_dx16(const void* d16, int B, int L_in, int Cin, const void* w1
     g.L_up = f.L_up;
     g.TS = 0;
     g.edge = mode == 0 ? nullptr : edge;
+    g.p_first = mode == 0 ? f.pad : 0;                 // causal: dX row s = padded row s + pad
+    g.p_end = mode == 0 ? f.pad + L_in : g.Lp;
     hipStream_t st = S(stream);
     int rc = VT_ERR_ARG;
     const __bf16* a = (const __bf16*)d16;

@@ -72,6 +72,9 @@ class _Lib:
             if n not in self.fns:
                 raise KeyError(f"VAETEB_ABLATE: unknown entry point {n}")
             self.fns[n] = lambda *a: 0
+        # A/B switch of the bf16 conv kernels (vt_conv_bf16_set_kernels; same bits either way)
+        if "VAETEB_CONV_KERNELS" in os.environ:
+            self.call("vt_conv_bf16_set_kernels", int(os.environ["VAETEB_CONV_KERNELS"]))
 
     def last_error(self):
         return self.fns["vt_last_error"]().decode()

@@ -294,18 +294,25 @@ class Trainer:
         # stream) alive into the next step or a hipGraph capture
         return {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in losses.items()}
 
-    def _update(self):
+    def _update(self, adam_stream=None):
+        """clip_grad_norm_ + AdamW over the flat buffers.  adam_stream: run the AdamW pass
+        (memory-bound) on that stream, forked after the norm, so the caller can overlap it
+        with work that does not read the parameters (the next batch's front-end); the
+        caller joins it before the next forward."""
         self.steps += 1
         st = _lib.stream()
         s = self.state
         _lib.call("vt_grad_norm_clip", s.g.data_ptr(), s.numel, 1.0 / self.world, float(self.max_norm),
                   self.norm_out.data_ptr(), self.norm_ws.data_ptr(), st)
+        if adam_stream is not None:
+            _lib.wait_for(adam_stream, st)
+            st = adam_stream.cuda_stream
         _lib.call("vt_adamw_step_dev", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(), s.numel,
                   float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
                   self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4, st)
 
     # ------------------------------------------------------------ hipGraph
-    def capture(self, batch, eps=None, warmup=2, pre_capture=None, native=False, n_streams=4):
+    def capture(self, batch, eps=None, warmup=2, pre_capture=None, native=False, n_streams=4, update=True):
         """Record the training step as a hipGraph over static input buffers and
         return it as a `CapturedStep` (also kept as the trainer's default for
         `replay`).  A replay is one launch instead of ~1200 host-side op
@@ -341,10 +348,11 @@ class Trainer:
         graph = torch.cuda.CUDAGraph(keep_graph=native)
         with torch.cuda.graph(graph):
             out = self._forward_backward(static_in, static_eps, overlap_comm=False)
-            if not self.buckets:
+            if not self.buckets and update:
                 self._update()
         out["grad_norm"] = self.norm_out[0]
         self.captured = CapturedStep(self, graph, static_in, static_eps, out, native=native, n_streams=n_streams)
+        self.captured.update = update
         return self.captured
 
     def replay(self, batch=None, eps=None):
@@ -384,7 +392,9 @@ class CapturedStep:
             self._destroy(self.handle)   # bound at build time: safe during interpreter shutdown
             self.handle = None
 
-    def replay(self, batch=None, eps=None):
+    def replay(self, batch=None, eps=None, adam_stream=None):
+        """One step.  A step captured with update=False issues clip + AdamW after the
+        replay (adam_stream: the AdamW pass on that stream, see Trainer._update)."""
         tr = self.trainer
         if batch is not None:
             for k, v in batch.items():
@@ -404,6 +414,8 @@ class CapturedStep:
             tr.buckets.reduce_all()
             tr.buckets.finish()
             tr._update()
+        elif not getattr(self, "update", True):
+            tr._update(adam_stream)
         else:
             tr.steps += 1
         return self.out
