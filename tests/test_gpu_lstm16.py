@@ -5,8 +5,9 @@ The kernels compute a definite 16-bit model of nn.LSTM (ref/model/vae_teb_model.
 :709-711): forward operands x, h_{t-1} and the pre-scaled W_ih, W_hh (gate rows times
 -log2 e, or -2 log2 e for g, in fp32) rounded to f16, sigmoid = 1 / (1 + 2^p) and
 tanh = 2 sigmoid(2x) - 1 in the forward, backward operands
-dg and W_hh / W_ih rounded to bf16, everything else (accumulation, biases, cell state,
-activations, outputs, dgates, weight gradients) fp32.  The oracle here is that model
+dg and W_hh / W_ih rounded to bf16, the parameter gradients from bf16-rounded dg, x and
+h_{t-1} (bf16 MFMA, skdw16.hip), everything else (accumulation, biases, cell state,
+activations, outputs, dgates) fp32.  The oracle here is that model
 restated in fp64 on the CPU (`_emu`), with torch's fp64 nn.LSTM as the exact model.
 
 Tolerance: two correct implementations of the same 16-bit model differ by
@@ -14,7 +15,10 @@ rounding-boundary flips (an h or dg within fp32 rounding of an f16 / bf16 bounda
 the other way, and the recurrence carries the difference), so the bound is the distance
 between the model computed in fp64 and the SAME model computed in fp32 (`_emu(dt=fp32)`):
 rel-L2(ours, emu64) <= 3 x rel-L2(emu32, emu64) + 2e-5 on outputs, dx and every
-parameter gradient — and that bound must stay inside the 16-bit model's own distance to
+parameter gradient (+ 2 % of the gradient's own bf16 operand-rounding effect: its x / h
+operands are the recurrence's fp32 outputs, whose ~1e-6 differences between two correct
+implementations flip ~1e-4 of their bf16 roundings by one ulp — a rounding the kernel
+did not apply would cost 100 % of that effect) — and that bound must stay inside the 16-bit model's own distance to
 the exact LSTM (asserted for 1-2 layers; through 4 layers x 48 steps the flips make the
 floor ~1/2 of that distance, and the 4-layer case bounds gross errors only).
 """
@@ -77,6 +81,7 @@ def _emu(x, params, gy, dt=torch.float64):
         inp = torch.stack(hs, 1)
     y = inp
     grads = [None] * len(params)
+    qround = [0.0] * len(params)
     dh_out = gy.to(dt)
     for l in reversed(range(nl)):
         xin, hp, cs, gs = saved[l]
@@ -96,11 +101,16 @@ def _emu(x, params, gy, dt=torch.float64):
             dg[:, t] = d
             dhr = b16(d) @ b16(w_hh)
         dx = b16(dg) @ b16(w_ih)
-        grads[4 * l] = torch.einsum("bsg,bsi->gi", dg, xin)
-        grads[4 * l + 1] = torch.einsum("bsg,bsi->gi", dg, hp)
-        grads[4 * l + 2] = dg.sum((0, 1))
-        grads[4 * l + 3] = dg.sum((0, 1))
+        grads[4 * l] = torch.einsum("bsg,bsi->gi", b16(dg), b16(xin))
+        grads[4 * l + 1] = torch.einsum("bsg,bsi->gi", b16(dg), b16(hp))
+        grads[4 * l + 2] = b16(dg).sum((0, 1))
+        grads[4 * l + 3] = b16(dg).sum((0, 1))
+        # the same gradients on the unrounded operands: the size of the bf16 operand rounding
+        qround[4 * l] = rel(grads[4 * l], torch.einsum("bsg,bsi->gi", dg, xin))
+        qround[4 * l + 1] = rel(grads[4 * l + 1], torch.einsum("bsg,bsi->gi", dg, hp))
+        qround[4 * l + 2] = qround[4 * l + 3] = rel(grads[4 * l + 2], dg.sum((0, 1)))
         dh_out = dx
+    _emu.qround = qround
     return y.double(), dh_out.double(), [g.double() for g in grads]
 
 
@@ -125,6 +135,7 @@ def test_lstm16_vs_16bit_model(ops, In, B, S, nl):
     x = torch.randn(B, S, In)
     gy = torch.randn(B, S, 64)
     ye, dxe, ge = _emu(x, params, gy)
+    q = [0.0, 0.0] + list(_emu.qround)
     y3, dx3, g3 = _emu(x, params, gy, torch.float32)
     yx, dxx, gx = _exact(x, params, gy, In)
     pd = [p.cuda().requires_grad_() for p in params]
@@ -133,13 +144,13 @@ def test_lstm16_vs_16bit_model(ops, In, B, S, nl):
     (y * gy.cuda()).sum().backward()
     torch.cuda.synchronize()
     names = ["y", "dx"] + [f"{n}_l{l}" for l in range(nl) for n in ("w_ih", "w_hh", "b_ih", "b_hh")]
-    for n, ours, e, e32, ex in zip(names, [y, xd.grad] + [p.grad for p in pd], [ye, dxe] + ge, [y3, dx3] + g3,
-                                  [yx, dxx] + gx):
+    for n, ours, e, e32, ex, qr in zip(names, [y, xd.grad] + [p.grad for p in pd], [ye, dxe] + ge, [y3, dx3] + g3,
+                                      [yx, dxx] + gx, q):
         d, floor, model = rel(ours, e), rel(e32, e), rel(e, ex)
-        assert d <= 3 * floor + 2e-5, (n, d, floor, model)
+        assert d <= 3 * floor + 2e-5 + 0.02 * qr, (n, d, floor, model, qr)
         if nl <= 2:   # shallow: the bound separates the 16-bit model from the exact one (4 layers
             # x 48 steps of bf16 flips make the model's own fp32/fp64 floor ~1/3 of its distance)
-            assert 3 * floor + 2e-5 < model, (n, floor, model)
+            assert 3 * floor + 2e-5 + 0.02 * qr < model, (n, floor, model, qr)
 
 
 def test_lstm16_no_dx_and_outputs(ops):
@@ -179,10 +190,12 @@ def test_lstm16_no_dx_and_outputs(ops):
                   P(gates), st)
 
 
-@pytest.mark.parametrize("In,B,S", [(20, 3, 37), (64, 4, 16)])
-def test_lstm16_weight_grad_reads_h_shifted(ops, In, B, S):
-    """vt_lstm16_layer_bwd_weight (h_{t-1} read from h, zero at t = 0) == vt_lstm_layer_bwd_weight
-    on an explicit h_{t-1} tensor, bit for bit (same kernel and summation order)."""
+@pytest.mark.parametrize("In,B,S", [(20, 3, 37), (64, 4, 16), (32, 5, 256), (64, 8, 300), (20, 2, 1)])
+def test_lstm16_weight_grad_bf16(ops, In, B, S):
+    """vt_lstm16_layer_bwd_weight (bf16 MFMA, h_{t-1} read from h, zero at t = 0) == the
+    parameter gradients of bf16-rounded dg, x, h_{t-1} summed in fp64 (rel-L2 <= 1e-5: fp32
+    accumulation order only); the exact-fp32 entry point on the same operands stays within
+    bf16 rounding of it."""
     from vaeteb import _lib
     torch.manual_seed(In + S)
     H = 64
@@ -195,10 +208,52 @@ def test_lstm16_weight_grad_reads_h_shifted(ops, In, B, S):
     st = torch.cuda.current_stream().cuda_stream
     outs = []
     for fn, hh in (("vt_lstm_layer_bwd_weight", hp), ("vt_lstm16_layer_bwd_weight", h)):
-        o = [torch.empty(4 * H, In, device="cuda"), torch.empty(4 * H, H, device="cuda"),
+        o = [torch.full((4 * H, In), float("nan"), device="cuda"), torch.full((4 * H, H), float("nan"), device="cuda"),
              torch.empty(4 * H, device="cuda"), torch.empty(4 * H, device="cuda")]
         _lib.call(fn, P(dg), P(x), In, P(hh), B, S, H, *[P(t) for t in o], 0, P(ws), ws.numel(), st)
         outs.append(o)
     torch.cuda.synchronize()
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    b16 = lambda t: t.cpu().bfloat16().double()
+    g16 = b16(dg)
+    ref = [torch.einsum("bsg,bsi->gi", g16, b16(x)), torch.einsum("bsg,bsi->gi", g16, b16(hp)), g16.sum((0, 1)),
+           g16.sum((0, 1))]
+    for ours, fp32, r in zip(outs[1], outs[0], ref):
+        assert rel(ours, r) <= 1e-5, (rel(ours, r), rel(fp32, r))
+        assert rel(fp32, r) <= 2e-2   # the exact gradient, within bf16 operand rounding
+
+
+@pytest.mark.parametrize("In,B,S", [(20, 3, 37), (64, 4, 16)])
+def test_lstm16_weight_grad_reads_h_shifted(ops, In, B, S):
+    """With the bf16 kernel off (VAETEB_L16_DW16=0, checked in a fresh process):
+    vt_lstm16_layer_bwd_weight (h_{t-1} read from h, zero at t = 0) == vt_lstm_layer_bwd_weight
+    on an explicit h_{t-1} tensor, bit for bit (same kernel and summation order)."""
+    import os
+    import subprocess
+    import sys
+    code = f"""
+import torch, sys
+sys.path.insert(0, {repr(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "vae-teb_amd"))})
+from vaeteb import _lib
+torch.manual_seed({In} + {S})
+B, S, In, H = {B}, {S}, {In}, 64
+dg = torch.randn(B, S, 4 * H, device="cuda")
+x = torch.randn(B, S, In, device="cuda")
+h = torch.randn(B, S, H, device="cuda")
+hp = torch.cat([torch.zeros_like(h[:, :1]), h[:, :-1]], 1).contiguous()
+ws = torch.empty(32 << 20, device="cuda")
+P = lambda t: t.data_ptr()
+st = torch.cuda.current_stream().cuda_stream
+outs = []
+for fn, hh in (("vt_lstm_layer_bwd_weight", hp), ("vt_lstm16_layer_bwd_weight", h)):
+    o = [torch.empty(4 * H, In, device="cuda"), torch.empty(4 * H, H, device="cuda"),
+         torch.empty(4 * H, device="cuda"), torch.empty(4 * H, device="cuda")]
+    _lib.call(fn, P(dg), P(x), In, P(hh), B, S, H, *[P(t) for t in o], 0, P(ws), ws.numel(), st)
+    outs.append(o)
+torch.cuda.synchronize()
+assert all(torch.equal(a, b) for a, b in zip(*outs))
+print("ok")
+"""
+    env = dict(os.environ, VAETEB_L16_DW16="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+

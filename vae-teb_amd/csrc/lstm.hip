@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // LSTM recurrence for the encoders' nn.LSTM(in, 64, 4 layers, batch_first)
 // (ref/model/vae_teb_model.py:474-480, :647-653).
 //
@@ -718,6 +719,14 @@ int vt_lstm16_layer_bwd_weight(const float* dgates, const float* x, int In, cons
                  "vt_lstm16_layer_bwd_weight: shape (In %d)", In);
     VT_CHECK_ARG(dgates && x && h && dw_ih && dw_hh && db_ih, "vt_lstm16_layer_bwd_weight: null pointer");
     const int64_t R = (int64_t)B * seq;
+    // bf16 operands on bf16 MFMA (skdw16.hip, the 16-bit model's precision: dG / x / h rounded to
+    // bf16, fp32 accumulation); VAETEB_L16_DW16=0 or an unsupported shape: the exact-fp32 kernel
+    static const int dw16 = getenv("VAETEB_L16_DW16") ? atoi(getenv("VAETEB_L16_DW16")) : 1;
+    if (dw16 && sk_lstm16_dw(dgates, x, In, h, seq, R, dw_ih, dw_hh, db_ih, db_hh, accumulate, ws, ws_floats,
+                             S(stream)) == VT_OK) {
+        VT_LAUNCH_CHECK("vt_lstm16_layer_bwd_weight");
+        return VT_OK;
+    }
     const int rc = sk_linear_bwd_weight2(dgates, R, G4, x, In, h, H, dw_ih, dw_hh, db_ih, db_hh, accumulate, ws,
                                          ws_floats, S(stream), seq);
     VT_CHECK_ARG(rc == VT_OK, "vt_lstm16_layer_bwd_weight: workspace too small");

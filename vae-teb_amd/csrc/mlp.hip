@@ -456,6 +456,13 @@ int sk_linear_bwd_weight2(const float* dY, int64_t R, int N, const float* X, int
     return VT_OK;
 }
 
+void sk_sum_launch(const float* part, int blocks, int N, int K, int K2, int K1, float* dW, float* dW2, float* db,
+                   float* db2, int accumulate, hipStream_t st) {
+    const int64_t total = (int64_t)N * K1;
+    hipLaunchKernelGGL(k_sk_sum, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, part, blocks, N, K, K2, K1,
+                       dW, dW2, db, db2, accumulate);
+}
+
 int sk_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int K, float* dW, float* db,
                          int accumulate, float* ws, int64_t ws_floats, hipStream_t st) {
     return sk_linear_bwd_weight2(dY, R, N, X, K, nullptr, 0, dW, nullptr, db, nullptr, accumulate, ws, ws_floats, st);

@@ -23,5 +23,13 @@ int sk_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X, int 
 int sk_linear_bwd_weight2(const float* dY, int64_t R, int N, const float* X, int K, const float* X2, int K2,
                           float* dW, float* dW2, float* db, float* db2, int accumulate, float* ws, int64_t ws_floats,
                           hipStream_t st, int x2_shift = 0);
+// the fixed-order sum of k_sk_dw's per-workgroup partial slabs part[blocks][N][K1] into dW / dW2 / db / db2
+void sk_sum_launch(const float* part, int blocks, int N, int K, int K2, int K1, float* dW, float* dW2, float* db,
+                   float* db2, int accumulate, hipStream_t st);
+// skdw16.hip: the 16-bit LSTM's parameter gradients on bf16 MFMA (dG, x, h_{t-1} rounded to bf16,
+// fp32 accumulation); VT_ERR_ARG when the shape / alignment is not supported
+int sk_lstm16_dw(const float* dG, const float* x, int In, const float* h, int S, int64_t R, float* dW_ih,
+                 float* dW_hh, float* db_ih, float* db_hh, int accumulate, float* ws, int64_t ws_floats,
+                 hipStream_t st);
 
 }  // namespace vt
