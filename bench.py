@@ -265,6 +265,10 @@ def main():
                          "executor (vt_stepgraph_*); graph: hipGraphLaunch; eager: every op from Python")
     ap.add_argument("--native", action="store_true", help="= --mode native")
     ap.add_argument("--streams", type=int, default=4, help="--native: executor streams")
+    ap.add_argument("--fe-in-graph", type=int, default=0,
+                    help="native: 1 = the front-end is captured into the step too (raw windows are the "
+                         "static input), so the executor runs the cross pairs beside the target encoder as the eager "
+                         "step does; the roofline kernel is then timed in eager steps after the timed region")
     ap.add_argument("--overlap-adam", type=int, default=0,
                     help="native: 1 = the step captured without AdamW, which runs after each replay on a side "
                          "stream, overlapping the next batch's front-end (independent of the weights)")
@@ -343,6 +347,7 @@ def main():
         B * (slots_of.get(n_pairs, n_slots) * N * 8 + n_pairs * a[7] * 4)
     timer = KernelTimer(["vt_fe_pairs", *MFMA_CALLS], flops=work)
     graph = args.graph or args.native
+    fe_in_graph = False
     if graph:
         # The model step (forward, backward, clip, AdamW) is replayed as a
         # hipGraph.  The front-end (~10 launches, independent of the weights)
@@ -353,7 +358,9 @@ def main():
         fe_stream = torch.cuda.Stream()
         if args.native:
             eps_shape = (B, S, model.latent_dim_z)
-            caps = [trainer.capture(fe(pool[j]), eps=torch.randn(eps_shape, device=dev), native=True,
+            fe_in_graph = bool(args.fe_in_graph) and not args.overlap_fe
+            caps = [trainer.capture({"x": pool[j]} if fe_in_graph else fe(pool[j]),
+                                    eps=torch.randn(eps_shape, device=dev), native=True,
                                     n_streams=args.streams, update=not args.overlap_adam)
                     for j in range(2 if args.overlap_fe else 1)]
             if args.overlap_adam:
@@ -376,6 +383,14 @@ def main():
 
         def step(i, last=False):
             slot = i % 2
+            if args.native and fe_in_graph:
+                # this step's windows into the graph's static input, its noise, the replay
+                # (front-end + model step)
+                torch.randn(caps[0].static_eps.shape, out=caps[0].static_eps)
+                if args.overlap_adam:
+                    _lib.wait_for(torch.cuda.current_stream(), adam_side)
+                    return caps[0].replay({"x": pool[i % 2]}, adam_stream=adam_side)
+                return caps[0].replay({"x": pool[i % 2]})
             if args.native and not args.overlap_fe:
                 # the step's own front-end first, on the same stream (as the eager step), then
                 # this step's noise (drawn outside the graph) and the replay
@@ -473,6 +488,16 @@ def main():
     value = samples / dt
     n_params = sum(p.numel() for p in model.parameters())
     step_bytes = step_bytes_per_sample(plan, fe, n_params, B)
+    fe_timed_in = "timed region"
+    if graph and args.native and fe_in_graph:
+        # the front-end runs inside the replay: time its kernel in two eager steps after the
+        # timed region (the same kernels and shapes; profiles/ holds the in-replay durations)
+        timer.reset(True)
+        for i in range(2):
+            trainer.step({"x": pool[i % 2]})
+        torch.cuda.synchronize()
+        timer.enabled = False
+        fe_timed_in = "eager steps after the timed region (front-end captured in the replayed step)"
     k_ms, k_n = timer.mean_ms("vt_fe_pairs")
     k_bytes = timer.total_flops["vt_fe_pairs"] / max(k_n, 1)   # mean algorithmic bytes per launch
     traffic, traffic_src = pmc_traffic("k_fe_pairs8k") if (J, Q, T, B) == (11, 4, 16, 256) else (None, None)
@@ -496,9 +521,10 @@ def main():
                    "parallelism": f"dp{world}"},
         "elbo": elbo,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
-        "mode": (f"model step captured once, replayed by the native {args.streams}-stream executor "
-                 "(vt_stepgraph); front-end eager " + ("one step ahead on its own stream" if args.overlap_fe else
-                                                      "before each replay on the same stream")) if args.native else
+        "mode": (f"step captured once, replayed by the native {args.streams}-stream executor (vt_stepgraph); "
+                 + ("front-end inside the captured step" if fe_in_graph else
+                    "front-end eager " + ("one step ahead on its own stream" if args.overlap_fe else
+                                          "before each replay on the same stream"))) if args.native else
                 "model step replayed as a hipGraph (double-buffered), front-end eager one step ahead on its own stream"
                 if graph else ("eager, next batch's front-end overlapped with clip + AdamW (own streams, "
                                "double-buffered features)" if args.overlap_update else
@@ -512,7 +538,8 @@ def main():
                      "algorithmic_bytes_def": "compulsory: the launch's analytic-signal slots read once + pair "
                                               "features written (SURVEY.md §8(d))",
                      "limiter": "VALU / LDS latency, not HBM (DESIGN.md §5: 0.74k VALU per wave, 49 % SQ_WAIT_ANY)",
-                     "launches_per_step": k_n / args.steps},
+                     "launches_per_step": k_n / (2 if fe_timed_in != "timed region" else args.steps),
+                     "timed_in": fe_timed_in},
         # SURVEY.md §8(d)'s step-level roofline: samples/s x algorithmic bytes per sample / (GPUs x 8 TB/s)
         "roofline_step": {"bound": "hbm", "bytes_per_sample": round(step_bytes),
                           "achieved": round(value * step_bytes / world / 1e9, 1), "peak": HBM_PEAK_GBS,

@@ -333,8 +333,9 @@ int vt_conv_bf16_set_staging(int mode);
 /* Kernel selection of the bf16 conv forward / weight gradient (A/B; bit-identical results):
  * bit 0 = the flat-staged forward of conv_fwd16.hip (source rows copied with float4 loads,
  * the whole bf16 window formed in LDS, next chunk's taps prefetched) for K <= 5, bit 1 = the
- * flat-staged, prefetching weight gradient (k_cdw16) for K >= 7 — where each measured faster
- * (default 3) — bit 2 = both at every K; 0 = k_conv_bf16 / k_conv_dw_bf16 everywhere.   */
+ * flat-staged, prefetching weight gradient (k_cdw16) for K >= 7 — where each measured faster —
+ * bit 2 = both at every K, bit 3 = the weight gradient in 256-row chunks for dY <= 32 channels
+ * (default 11); 0 = k_conv_bf16 / k_conv_dw_bf16 everywhere.                              */
 int vt_conv_bf16_set_kernels(int flags);
 int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode,
                           int up, const float* gamma, const float* beta, int act, float eps, float momentum,

@@ -161,12 +161,14 @@ def test_flat_staged_forward_bitwise(L, geo):
             torch.cuda.synchronize()
             outs.append((conv, y, mean, rstd, rm, rv, y2))
     finally:
-        L.call("vt_conv_bf16_set_kernels", 3)
+        L.call("vt_conv_bf16_set_kernels", 11)
     for a, b in zip(*outs):
         assert torch.equal(a, b), ((a != b).sum().item(), a.numel())
 
 
-@pytest.mark.parametrize("geo", [g for g in FWD_GEOS if g[2] <= 128 and g[3] <= 128])
+@pytest.mark.parametrize("geo", [g for g in FWD_GEOS if g[2] <= 128 and g[3] <= 128] +
+                         [(8, 2048, 33, 22, 3, 1, 1), (8, 4096, 22, 11, 3, 1, 0), (8, 4096, 11, 1, 3, 1, 0),
+                          (16, 256, 16, 16, 7, 0, 0), (16, 256, 32, 32, 3, 0, 0), (4, 1000, 20, 30, 5, 1, 1)])
 def test_flat_staged_weight_grad_bitwise(L, geo):
     """vt_conv_bf16_set_kernels bit 1: the flat-staged, prefetching weight gradient
     (k_cdw16, default) and k_conv_dw_bf16 on the same bf16 dY rows give the same dW bit for
@@ -182,7 +184,7 @@ def test_flat_staged_weight_grad_bitwise(L, geo):
     wsw = torch.empty(8 << 20, device="cuda")
     outs = []
     try:
-        for flags in (0, 7):
+        for flags in (0, 7, 11, 15):
             L.call("vt_conv_bf16_set_kernels", flags)
             dw = torch.full((Cout, Cin, K), float("nan"), device="cuda")
             L.call("vt_conv1d_bwd_weight_bf16_dy16s", L.ptr(d16), c32, L.ptr(x), B, Lin, Cin, Cout, K, mode, up,
@@ -190,5 +192,6 @@ def test_flat_staged_weight_grad_bitwise(L, geo):
             torch.cuda.synchronize()
             outs.append(dw)
     finally:
-        L.call("vt_conv_bf16_set_kernels", 3)
-    assert torch.equal(outs[0], outs[1]), ((outs[0] != outs[1]).sum().item(), outs[0].numel())
+        L.call("vt_conv_bf16_set_kernels", 11)
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o), ((outs[0] != o).sum().item(), o.numel())

@@ -433,6 +433,42 @@ def test_native_executor_bitwise_identical_to_eager(golden, n_streams):
         assert torch.equal(a, b)
 
 
+def test_native_executor_with_frontend_bitwise_identical_to_eager():
+    """The step captured from RAW windows (the front-end inside the graph, its cross pairs
+    on the source encoder's stream: bench.py's default native mode) replayed by the
+    executor == eager steps from the same windows, bit for bit (losses, parameters, Adam
+    moments), at the benchmarked front-end (J=11 Q=4 T=16, N=4096) on a small batch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb import synthetic
+    from vaeteb.frontend import FrontEnd, FrontEndPlan, load_stats
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    fe = FrontEnd(FrontEndPlan(11, 4, 16, 4096, device="cuda"), load_stats())
+    xs = [torch.from_numpy(synthetic.batch(100 * i, 4, 4096)).cuda() for i in range(2)]
+    S = fe.plan.S
+    epss = [torch.randn(4, S, 32, generator=torch.Generator().manual_seed(i)).cuda() for i in range(2)]
+    res = []
+    for native in (False, True):
+        m = det_fill_(SeqVaeTeb(sequence_length=S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,
+                                cross_phase_channels=fe.C_x, concurrent_encoders=True, head_precision="bf16",
+                                conv_precision="bf16", mlp_precision="bf16", lstm_precision="16-mixed")).cuda()
+        tr = Trainer(m, lr=1e-3, frontend=fe)
+        if native:
+            cap = tr.capture({"x": xs[0]}, eps=epss[0], warmup=2, native=True)
+            outs = [cap.replay({"x": xs[i % 2]}, eps=epss[i % 2])["total_loss"].item() for i in (1, 0, 1)]
+        else:
+            for _ in range(2):
+                tr.step({"x": xs[0]}, eps=epss[0])
+            outs = [tr.step({"x": xs[i % 2]}, eps=epss[i % 2])["total_loss"].item() for i in (1, 0, 1)]
+        torch.cuda.synchronize()
+        res.append((outs, tr.state.p.clone(), tr.state.m.clone(), tr.state.v.clone()))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, b)
+
+
 def test_native_executor_requires_eps(golden):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

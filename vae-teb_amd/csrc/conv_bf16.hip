@@ -17,6 +17,8 @@
 // row.  Rows are 40 bf16 (20 dwords) apart: 16 consecutive rows hit 16
 // distinct 4-bank groups.  Backward-data is the same kernel on dY with the
 // transposed / flipped shadow (causal padding K-1), as in conv.hip.
+#include <stdlib.h>
+
 #include "conv.h"
 
 namespace vt {
@@ -133,7 +135,7 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
 // leave most of the 32 channel lanes idle)
 int g_conv_cl = 1;
 // kernel selection (vt_conv_bf16_set_kernels): bit 0 the flat-staged forward (conv_fwd16.hip)
-int g_conv_kern = 3;   // bit 1: the flat-staged weight gradient (k_cdw16); bit 2: both at every K
+int g_conv_kern = 11;   // bit 3: 256-row chunks in the flat weight gradient for dY <= 32 channels   // bit 1: the flat-staged weight gradient (k_cdw16); bit 2: both at every K
 
 // x: fp32 (B, L_in, g.Cin) activations; w16: [g.Cout][K][cin32] bf16 shadow.
 // BNB (backward-data only: causal geometry, no upsample): x is the block output
@@ -592,18 +594,22 @@ __global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restri
 // segments and F rows are loaded into registers before the current chunk's MFMAs.
 constexpr int CDW_UD = 4;    // dY 16-byte segments per thread and chunk (256 threads)
 constexpr int CDW_UF = 8;    // F float4 per thread and chunk (256 threads)
+constexpr int CDW_UF_WIDE = 12;   // ... for the 256-row chunks
 
-template <int K, int PPW, int NWV>
+// CR: rows per chunk — 64 (DWR), or 256 for the narrow layers (dY <= 32 channels: four times
+// the MFMA work per staged chunk, the same k-step order, so the same bits)
+template <int K, int PPW, int NWV, int CR = DWR>
 __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ dyb16, int dys,
                                                    const float* __restrict__ x, Geo g, int64_t rows_per_split,
                                                    int NTc, int npairs, int dstride, int xstride,
                                                    float* __restrict__ part, int64_t total) {
     constexpr int NT = 64 * NWV;
-    constexpr int UD = CDW_UD * 256 / NT, UF = CDW_UF * 256 / NT;
+    constexpr int UD = CR == DWR ? CDW_UD * 256 / NT : CR * 4 / NT;   // CR 256: dY rows of <= 4 segments
+    constexpr int UF = CR == DWR ? CDW_UF * 256 / NT : CDW_UF_WIDE * 256 / NT;
     extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
-    __bf16* ds = lb;                          // [DWR][dstride]   dY rows
-    __bf16* xs = lb + DWR * dstride;          // [DWR + K - 1 (+pad)][xstride] input window
-    float* F = reinterpret_cast<float*>(lb + DWR * dstride + (DWR + KMAXB_DW + 8) * xstride);
+    __bf16* ds = lb;                          // [CR][dstride]   dY rows
+    __bf16* xs = lb + CR * dstride;           // [CR + K - 1 (+pad)][xstride] input window
+    float* F = reinterpret_cast<float*>(lb + CR * dstride + (CR + KMAXB_DW + 8) * xstride);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int mt[PPW], nt[PPW];
     bool act[PPW];
@@ -629,19 +635,19 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
     bf16x8 dv[UD];
     float4 fv[UF];
     struct Chunk {
-        int b, t0, n, lo, hi, off;
+        int b, t0, n, lo, hi, off, nv;
     };
     auto load = [&](int64_t r, Chunk& c) {
         c.b = (int)(r / g.L_out);
         c.t0 = (int)(r - (int64_t)c.b * g.L_out);
-        c.n = g.L_out - c.t0 < DWR ? g.L_out - c.t0 : DWR;
+        c.n = g.L_out - c.t0 < CR ? g.L_out - c.t0 : CR;
         if (r + c.n > r1) c.n = (int)(r1 - r);
         const __bf16* db = dyb16 + ((int64_t)c.b * g.L_out + c.t0) * dys;
 #pragma unroll
         for (int u = 0; u < UD; ++u) {
             const int i = tid + NT * u;
             const int t = i / dsegs, sg = i - t * dsegs;
-            const bool ok = i < DWR * dsegs && t < c.n && 8 * sg < dys;
+            const bool ok = i < CR * dsegs && t < c.n && 8 * sg < dys;
             dv[u] = *(const bf16x8*)(db + (int64_t)(ok ? t : 0) * dys + (ok ? 8 * sg : 0));
             if (!ok) {
 #pragma unroll
@@ -654,6 +660,7 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
         c.off = (int)(f0 - fa);
         const int nf = c.hi >= c.lo ? (int)(((int64_t)c.b * g.L_in + c.hi + 1) * g.Cin - fa) : 0;
         const int nv = (nf + 3) >> 2;
+        c.nv = nv;
 #pragma unroll
         for (int u = 0; u < UF; ++u) {
             const int i = tid + NT * u;
@@ -675,19 +682,20 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
 #pragma unroll
         for (int u = 0; u < UD; ++u) {
             const int i = tid + NT * u;
-            if (i < DWR * dsegs) {
+            if (i < CR * dsegs) {
                 const int t = i / dsegs, sg = i - t * dsegs;
                 *(bf16x8*)(ds + t * dstride + 8 * sg) = dv[u];
             }
         }
 #pragma unroll
-        for (int u = 0; u < UF; ++u) reinterpret_cast<float4*>(F)[tid + NT * u] = fv[u];
+        for (int u = 0; u < UF; ++u)
+            if (tid + NT * u < cur.nv) reinterpret_cast<float4*>(F)[tid + NT * u] = fv[u];
         __syncthreads();
-        // F -> the bf16 window image (rows t0 .. t0 + DWR + K - 2, zero past n + K - 1), 8 channels
+        // F -> the bf16 window image (rows t0 .. t0 + CR + K - 2, zero past n + K - 1), 8 channels
         // of one row per item
         {
             const int osegs = cin16 / 8;
-            for (int i = tid; i < (DWR + K - 1) * osegs; i += NT) {
+            for (int i = tid; i < (CR + K - 1) * osegs; i += NT) {
                 const int t = i / osegs, o = i - t * osegs;
                 const int tp = cur.t0 + t, cb = 8 * o;
                 int i0 = 0, i1 = 0;
@@ -711,7 +719,7 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
         Chunk nxt = cur;
         if (rn < r1) load(rn, nxt);   // in flight during the MFMAs
 #pragma unroll
-        for (int s = 0; s < DWR / 32; ++s) {
+        for (int s = 0; s < CR / 32; ++s) {
             if (!act[0]) break;  // wave-uniform: a wave without pairs only stages
 #pragma unroll
             for (int j = 0; j < PPW; ++j) {
@@ -854,7 +862,7 @@ int vt_conv_bf16_set_staging(int mode) {
 }
 
 int vt_conv_bf16_set_kernels(int flags) {
-    VT_CHECK_ARG(flags >= 0 && flags <= 7, "vt_conv_bf16_set_kernels: flags %d not in 0..7", flags);
+    VT_CHECK_ARG(flags >= 0 && flags <= 15, "vt_conv_bf16_set_kernels: flags %d not in 0..15", flags);
     g_conv_kern = flags;
     return VT_OK;
 }
@@ -960,7 +968,11 @@ static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin,
     const int bx = cdiv(npairs, nwv * ppw);
     const int64_t rows = (int64_t)B * g.L_out;
     const int64_t nout = (int64_t)Cout * Cin * K;
-    int64_t splits = 4096 / (nwv * bx);
+    // workgroup budget of the row splits (VAETEB_CONVDW_WG, default 8192; measured 4096 -> 8192:
+    // 8.80-8.85 -> 8.78-8.79 ms, 1024: 9.2 ms — the weight gradients join the step's end)
+    static const int wg_budget = getenv("VAETEB_CONVDW_WG") ? atoi(getenv("VAETEB_CONVDW_WG")) : 8192;
+    int64_t splits = (wg_budget > 0 ? wg_budget : 4096) / (nwv * bx);
+    if (splits > 1024) splits = 1024;   // the two-stage split sum handles <= 32^2
     if (splits * nout > (int64_t)8 << 20) splits = ((int64_t)8 << 20) / nout;
     if (splits > rows / (4 * DWR)) splits = rows / (4 * DWR);
     if (splits < 1) splits = 1;
@@ -978,13 +990,27 @@ static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin,
     const int64_t f_floats = (int64_t)f_rows * Cin + 8;
     // flat-staged weight gradient where it measured faster (K 9 / 7: 176 -> 111, 184 -> 118 us;
     // K <= 5 slower: 85 -> 108 us)
-    const bool flat = (g_conv_kern & 2) && (K >= 7 || (g_conv_kern & 4)) && dy16 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)dy16 & 15) == 0 &&
-                      dys % 8 == 0 && f_floats <= (int64_t)4 * CDW_UF * 256 && 16 * cdiv(Cout, 16) <= 8 * CDW_UD * 32;
-    const size_t lds_flat = lds + (size_t)4 * CDW_UF * 256 * 4;
+    const bool flat_ok = dy16 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)dy16 & 15) == 0 && dys % 8 == 0;
+    const bool flat = flat_ok && (g_conv_kern & 2) && (K >= 7 || (g_conv_kern & 4)) &&
+                      f_floats <= (int64_t)4 * CDW_UF * 256 && 16 * cdiv(Cout, 16) <= 8 * CDW_UD * 32;
+    const size_t lds_flat = lds + (size_t)f_floats * 4 + 64;
     const int64_t total_x = (int64_t)B * L_in * Cin;
+    // 256-row chunks for the narrow layers (dY <= 32 channels, the window's source rows in
+    // the wide prefetch): four times the MFMA work per staged chunk (measured: see DESIGN §9)
+    const int fw_rows = up ? (256 + K - 1) / 2 + 3 : 256 + K - 1;
+    const int64_t fw_floats = (int64_t)fw_rows * Cin + 8;
+    const bool wide = flat_ok && (g_conv_kern & 8) && cdiv(Cout, 16) <= 2 &&
+                      fw_floats <= (int64_t)4 * CDW_UF_WIDE * 256 && rps >= 256;
+    const size_t lds_wide = (size_t)(256 * dstride + (256 + KMAXB + 8) * xstride) * 2 + (size_t)fw_floats * 4 + 64;
 #define VT_DWB(KK, PP)                                                                                         \
     if (K == KK && ppw == PP) {                                                                                \
-        if (flat && nwv == 8)                                                                                  \
+        if (wide && nwv == 8)                                                                                  \
+            hipLaunchKernelGGL((k_cdw16<KK, PP, 8, 256>), grid, dim3(512), lds_wide, st, dy16, dys, X, g, rps,   \
+                               NTc, npairs, dstride, xstride, ws, total_x);                                   \
+        else if (wide)                                                                                         \
+            hipLaunchKernelGGL((k_cdw16<KK, PP, 4, 256>), grid, dim3(256), lds_wide, st, dy16, dys, X, g, rps,   \
+                               NTc, npairs, dstride, xstride, ws, total_x);                                   \
+        else if (flat && nwv == 8)                                                                             \
             hipLaunchKernelGGL((k_cdw16<KK, PP, 8>), grid, dim3(512), lds_flat, st, dy16, dys, X, g, rps, NTc,   \
                                npairs, dstride, xstride, ws, total_x);                                        \
         else if (flat)                                                                                         \

@@ -16,6 +16,8 @@
 // contiguous per fragment).  Each wave owns two whole 16-row tiles of dW (its A fragments read
 // once per k-step for all NTK column tiles).  Per-workgroup partial slabs, summed in fixed
 // order by mlp.hip's k_sk_sum (the fp32 path's reduction and output layout).
+#include <stdlib.h>
+
 #include "common.h"
 #include "skinny.h"
 
@@ -164,8 +166,9 @@ int sk_lstm16_dw(const float* dG, const float* x, int In, const float* h, int S,
     const int K1 = In + 64 + 1, NTK = (K1 + 15) / 16;
     if (In % 4 != 0 || In > 64 || NTK < 5 || NTK > 9 || (((uintptr_t)dG | (uintptr_t)x | (uintptr_t)h) & 15))
         return VT_ERR_ARG;
+    static const int cap = getenv("VAETEB_L16DW_BLOCKS") ? atoi(getenv("VAETEB_L16DW_BLOCKS")) : 128;
     int64_t blocks = (R + 255) / 256;
-    if (blocks > 128) blocks = 128;
+    if (blocks > cap) blocks = cap > 0 ? cap : 128;
     if (blocks * G * K1 > ws_floats) blocks = ws_floats / ((int64_t)G * K1);
     if (blocks < 1) return VT_ERR_ARG;
     int64_t rpb = (R + blocks - 1) / blocks;
