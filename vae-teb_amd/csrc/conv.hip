@@ -500,7 +500,10 @@ __global__ __launch_bounds__(256) void k_sum_splits_fin(const float* __restrict_
 
 // part is scratch: the two-stage path overwrites it
 int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st) {
-    if (splits <= 2 * SG_GRP || n >= (int64_t)64 * 1024) {
+    // one stage only for few splits: with many (e.g. 330 slabs of the 74k-weight K = 11 layer) a
+    // thread's serial loop over the slabs was latency-bound (80 us); the group stage keeps
+    // SG_GRP loads in flight per thread at any n
+    if (splits <= 2 * SG_GRP) {
         hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, splits, n, out,
                            accumulate);
         return VT_OK;
