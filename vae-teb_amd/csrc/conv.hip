@@ -234,12 +234,12 @@ __global__ __launch_bounds__(256) void k_bn_stats_finalize(const float* __restri
     const float* s1p = stats + (int64_t)(C + c) * ntile;
     double a = 0.0;
     int i = tid;
-    for (; i + 768 < ntile; i += 1024) {   // four coalesced loads in flight, same order
-        float u[4];
+    for (; i + 1792 < ntile; i += 2048) {   // eight coalesced loads in flight, same order
+        float u[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) u[k] = s0p[i + 256 * k];
+        for (int k = 0; k < 8; ++k) u[k] = s0p[i + 256 * k];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) a += (double)u[k];
+        for (int k = 0; k < 8; ++k) a += (double)u[k];
     }
     for (; i < ntile; i += 256) a += (double)s0p[i];
     red[tid] = a;
@@ -251,13 +251,25 @@ __global__ __launch_bounds__(256) void k_bn_stats_finalize(const float* __restri
     const double mu = red[0] / M;
     __syncthreads();
     double q = 0.0;
-    for (int i = tid; i < ntile; i += 256) {
+    auto m2 = [&](int i, float sv, float mv) {
         const int tx = i % tiles_per_sample;
         const int n = Lo - tx * TP < TP ? Lo - tx * TP : TP;
-        const double s1 = (double)s0p[i];
+        const double s1 = (double)sv;
         const double dm = s1 / n - mu;
-        q += (double)s1p[i] + n * dm * dm;
+        q += (double)mv + n * dm * dm;
+    };
+    i = tid;
+    for (; i + 1792 < ntile; i += 2048) {   // the same order, eight tiles' loads in flight
+        float u[8], v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            u[k] = s0p[i + 256 * k];
+            v[k] = s1p[i + 256 * k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m2(i + 256 * k, u[k], v[k]);
     }
+    for (; i < ntile; i += 256) m2(i, s0p[i], s1p[i]);
     red[tid] = q;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {

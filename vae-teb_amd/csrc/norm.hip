@@ -402,15 +402,15 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ pa
     const float* p0 = part + (int64_t)c * blocks;
     const float* p1 = part + (int64_t)(C + c) * blocks;
     int b = threadIdx.x;
-    for (; b + 3 * NT < blocks; b += 4 * NT) {
-        float u[4], v[4];
+    for (; b + 7 * NT < blocks; b += 8 * NT) {   // eight coalesced loads per array in flight, same order
+        float u[8], v[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 8; ++k) {
             u[k] = p0[b + k * NT];
             v[k] = p1[b + k * NT];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 8; ++k) {
             a0 += (double)u[k];
             a1 += (double)v[k];
         }
