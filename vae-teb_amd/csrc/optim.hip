@@ -9,6 +9,7 @@
 //   AdamW            : torch.optim.AdamW single-tensor update order, with the
 //                      hyper-parameters of ref/model/graph_model.py:654-660.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -111,6 +112,11 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw(float* __restrict__ p, co
 // The same update over 16-byte vectors (all four buffers 16-byte aligned):
 // 2 float4 of each stream in flight per thread and iteration (8 x 16 B loads
 // issued before the first use), the < 4 tail elements by the first threads.
+typedef float f32x4n __attribute__((ext_vector_type(4)));
+
+// U float4 of each stream in flight per thread and iteration; NT: the gradient read and the
+// three write-backs as non-temporal accesses (streamed once per step)
+template <int U, bool NT>
 __global__ __launch_bounds__(OPT_THREADS) void k_adamw4(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                         float lr, float beta1, float beta2, float eps, float wd,
@@ -129,23 +135,42 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw4(float* __restrict__ p, c
         adamw_elem(k, pp.z, gg.z, mm.z, vv.z);
         adamw_elem(k, pp.w, gg.w, mm.w, vv.w);
     };
+    auto ldg = [&](int64_t j) -> float4 {
+        if constexpr (NT) {
+            const f32x4n x = __builtin_nontemporal_load(reinterpret_cast<const f32x4n*>(g4 + j));
+            return make_float4(x[0], x[1], x[2], x[3]);
+        } else {
+            return g4[j];
+        }
+    };
+    auto st4 = [&](float4* a, int64_t j, const float4& x) {
+        if constexpr (NT) __builtin_nontemporal_store(f32x4n{x.x, x.y, x.z, x.w}, reinterpret_cast<f32x4n*>(a + j));
+        else a[j] = x;
+    };
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + stride < n4; i += 2 * stride) {
-        float4 pa = p4[i], pb = p4[i + stride];
-        const float4 ga = g4[i], gb = g4[i + stride];
-        float4 ma = m4[i], mb = m4[i + stride];
-        float4 va = v4[i], vb = v4[i + stride];
-        upd(pa, ga, ma, va);
-        upd(pb, gb, mb, vb);
-        p4[i] = pa; m4[i] = ma; v4[i] = va;
-        p4[i + stride] = pb; m4[i + stride] = mb; v4[i + stride] = vb;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        float4 pa[U], ga[U], ma[U], va[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            pa[u] = p4[i + u * stride];
+            ga[u] = ldg(i + u * stride);
+            ma[u] = m4[i + u * stride];
+            va[u] = v4[i + u * stride];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            upd(pa[u], ga[u], ma[u], va[u]);
+            st4(p4, i + u * stride, pa[u]);
+            st4(m4, i + u * stride, ma[u]);
+            st4(v4, i + u * stride, va[u]);
+        }
     }
-    if (i < n4) {
+    for (; i < n4; i += stride) {
         float4 pa = p4[i];
-        const float4 ga = g4[i];
+        const float4 ga = ldg(i);
         float4 ma = m4[i], va = v4[i];
         upd(pa, ga, ma, va);
-        p4[i] = pa; m4[i] = ma; v4[i] = va;
+        st4(p4, i, pa); st4(m4, i, ma); st4(v4, i, va);
     }
     const int64_t t = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) adamw_elem(k, p[t], g[t], m[t], v[t]);
@@ -191,9 +216,21 @@ static void adamw_launch(float* p, const float* g, float* m, float* v, int64_t n
         g_adamw_vec = (e && e[0] == '1') ? 0 : 1;
     }
     if (g_adamw_vec && aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v)) {
-        // ~2 float4 per thread and iteration, at most 2048 x 256 threads (8 per CU)
-        hipLaunchKernelGGL(k_adamw4, dim3(grid_for((n / 4 + 1) / 2, 2048)), dim3(OPT_THREADS), 0, st, p, g, m, v, n,
-                           lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
+        // U float4 per thread and iteration, at most cap x 256 threads (default 4, non-temporal, 2048:
+        // 8 per CU; same-box step 8.72-8.75 vs 8.78-9.0 ms with 2 and cached accesses)
+        static const int U = getenv("VAETEB_ADAMW_U") ? atoi(getenv("VAETEB_ADAMW_U")) : 4;
+        static const int cap = getenv("VAETEB_ADAMW_GRID") ? atoi(getenv("VAETEB_ADAMW_GRID")) : 2048;
+        static const bool nt = !(getenv("VAETEB_ADAMW_NT") && getenv("VAETEB_ADAMW_NT")[0] == '0');
+        const dim3 grid(grid_for((n / 4 + 1) / (U == 4 ? 4 : 2), cap > 0 ? cap : 2048));
+#define VT_ADAMW4(UU, NN)                                                                                          \
+    hipLaunchKernelGGL((k_adamw4<UU, NN>), grid, dim3(OPT_THREADS), 0, st, p, g, m, v, n, lr, beta1, beta2, eps, wd, \
+                       step_size, bc2_sqrt, gscale, coef)
+        if (U == 4) {
+            if (nt) VT_ADAMW4(4, true); else VT_ADAMW4(4, false);
+        } else {
+            if (nt) VT_ADAMW4(2, true); else VT_ADAMW4(2, false);
+        }
+#undef VT_ADAMW4
     } else {
         hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, st, p, g, m, v, n, lr, beta1,
                            beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
