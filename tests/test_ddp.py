@@ -117,3 +117,42 @@ def test_bucketed_allreduce_bf16():
         avg = (grads[0] + grads[1]) / world
         # elementwise the sum can cancel; overall the bf16 reduce is within bf16 rounding
         assert ((out[0][1][step] - avg).norm() / avg.norm()).item() < 2 ** -8
+
+
+def _bcast_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vaeteb.train import FlatState, broadcast_state
+    torch.manual_seed(10 + rank)  # a DIFFERENT initialisation on every rank
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.BatchNorm1d(32), torch.nn.Linear(32, 3))
+    model.train()
+    model(torch.randn(8, 16))     # rank-local BatchNorm running statistics / counter
+    before = [t.detach().numpy().copy() for t in list(model.parameters()) + list(model.buffers())]
+    st = FlatState(model)
+    broadcast_state(st, model)
+    after = [t.detach().numpy().copy() for t in list(model.parameters()) + list(model.buffers())]
+    q.put((rank, before, after, st.p.numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_broadcast_state_starts_every_rank_from_rank0():
+    """Trainer(world_size > 1) / lightning.fit: ranks initialised differently end up with
+    rank 0's parameters (through the flat buffer) and buffers (BatchNorm running stats and
+    counter), as DDP's construction-time sync (ref/model/graph_model.py:644)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, b0, a0, p0), (_, b1, a1, p1) = out
+    assert any(not (x == y).all() for x, y in zip(b0, b1))       # they did start apart
+    for x0, y0, y1 in zip(b0, a0, a1):
+        assert (x0 == y0).all() and (y0 == y1).all()             # rank 0 unchanged, rank 1 = rank 0
+    assert (p0 == p1).all()

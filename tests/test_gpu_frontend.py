@@ -150,11 +150,14 @@ def test_analytic_signals(fe11):
     assert_ref_precision(np.array(errs), np.array(ref_errs), what="analytic")
 
 
-def test_pairs_random_inputs_vs_oracle(fe11):
+@pytest.mark.parametrize("B", [3, 4, 8])
+def test_pairs_random_inputs_vs_oracle(fe11, B):
     """Bigger random batch: HIP fp32 vs oracle fp64, distribution-bounded by the
-    oracle's own fp32 error on the same inputs."""
+    oracle's own fp32 error on the same inputs.  B = 4 / 8: every launch's item count
+    (B x 44, B x 130, B x 174) is a multiple of 8, so the XCD-aware item order the bench
+    runs (xcd_item, csrc/frontend.hip) is active; B = 3 keeps the identity order."""
     from vaeteb import synthetic
-    x = synthetic.batch(900, 3, 4096)
+    x = synthetic.batch(900, B, 4096)
     r = fe11.raw(torch.from_numpy(x).cuda())
     pairs = r["pairs"].cpu().numpy()
     p = fe11.plan
@@ -220,3 +223,22 @@ def test_pairs_direct_columns_match_staged(fe11):
     torch.cuda.synchronize()
     diff = (staged - direct).abs().max().item()
     assert diff <= 1e-5 * staged.abs().max().item(), diff
+
+
+def test_frontend_bench_batch_rows_equal_small_batch(fe11):
+    """The front-end at the bench's batch (B = 256) vs a B = 4 run of its first four
+    windows, bit for bit (every output is per sample; the XCD-aware item order is active
+    in both, at different item counts, so this pins the remapped indexing at bench size)."""
+    from vaeteb import synthetic
+    x = torch.from_numpy(synthetic.batch(70_000, 256, 4096)).cuda()
+    big = {k: v.clone() for k, v in fe11(x).items()}
+    small = fe11(x[:4].contiguous())
+    torch.cuda.synchronize()
+    for k, v in small.items():
+        assert big[k].shape[0] == 256, k
+        assert torch.equal(big[k][:4], v), (k, (big[k][:4] - v).abs().max().item())
+    raw_big = {k: v.clone() for k, v in fe11.raw(x).items()}
+    raw_small = fe11.raw(x[252:].contiguous())     # the LAST four rows: the far end of the remap
+    torch.cuda.synchronize()
+    for k, v in raw_small.items():
+        assert torch.equal(raw_big[k][252:], v), k

@@ -433,11 +433,14 @@ def test_native_executor_bitwise_identical_to_eager(golden, n_streams):
         assert torch.equal(a, b)
 
 
-def test_native_executor_with_frontend_bitwise_identical_to_eager():
+@pytest.mark.parametrize("B", [4, 256])
+def test_native_executor_with_frontend_bitwise_identical_to_eager(B):
     """The step captured from RAW windows (the front-end inside the graph, its cross pairs
-    on the source encoder's stream: bench.py's default native mode) replayed by the
-    executor == eager steps from the same windows, bit for bit (losses, parameters, Adam
-    moments), at the benchmarked front-end (J=11 Q=4 T=16, N=4096) on a small batch."""
+    on the source encoder's stream) replayed by the executor == eager steps from the same
+    windows, bit for bit (losses, parameters, Adam moments), at the benchmarked front-end
+    (J=11 Q=4 T=16, N=4096) and bench precision; B = 256 is the bench's own batch (the
+    128-workgroup LSTM grids, the > 64-slab split sums and the XCD-remapped front-end at
+    their bench sizes)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from golden_util import det_fill_
@@ -446,9 +449,9 @@ def test_native_executor_with_frontend_bitwise_identical_to_eager():
     from vaeteb.model import SeqVaeTeb
     from vaeteb.train import Trainer
     fe = FrontEnd(FrontEndPlan(11, 4, 16, 4096, device="cuda"), load_stats())
-    xs = [torch.from_numpy(synthetic.batch(100 * i, 4, 4096)).cuda() for i in range(2)]
+    xs = [torch.from_numpy(synthetic.batch(1000 * i, B, 4096)).cuda() for i in range(2)]
     S = fe.plan.S
-    epss = [torch.randn(4, S, 32, generator=torch.Generator().manual_seed(i)).cuda() for i in range(2)]
+    epss = [torch.randn(B, S, 32, generator=torch.Generator().manual_seed(i)).cuda() for i in range(2)]
     res = []
     for native in (False, True):
         m = det_fill_(SeqVaeTeb(sequence_length=S, scattering_channels=fe.C_st, phase_channels=fe.C_ph,

@@ -103,8 +103,8 @@ def test_fp32_step_vs_reference_golden_training_geometry(golden, name):
         exp = float(g["loss_" + k])
         assert abs(L[k].item() - exp) <= 1e-5 * abs(exp) + 1e-7, (k, L[k].item(), exp)
     for k in FW_KEYS:
-        ours = fw[k] if k in ("mu_pr", "logvar_pr") else fw[k][:, :8]
-        assert rel(ours, g["fw_" + k]) < 5e-5, k
+        assert g["fw_" + k].shape == tuple(fw[k].shape), k    # every step (crosses the LSTM chunk hand-offs)
+        assert rel(fw[k], g["fw_" + k]) < 5e-5, k
     worst = max(_grad_rels(m, g, scaled=True))
     assert worst[0] <= 1.0, worst       # in units of the tolerance
     sd = m.state_dict()
@@ -159,8 +159,7 @@ def test_s256_bf16_step_within_reference_autocast_spread(golden, lstm):
     fw, L = _forward_backward(m, g)
     report = {}
     for k in FW_KEYS:
-        ours = fw[k] if k in ("mu_pr", "logvar_pr") else fw[k][:, :8]
-        r = rel(ours, g["fw_" + k])
+        r = rel(fw[k], g["fw_" + k])
         spread = max(float(ga[f"{mode}_fwrel_{k}"]) for mode in BF16_MODES)
         report[k] = (r, spread, float(ga[f"emu_fp16_fwrel_{k}"]))
         assert r <= 2 * spread, (k, r, spread)
@@ -182,6 +181,81 @@ def test_s256_bf16_step_within_reference_autocast_spread(golden, lstm):
           f"max {ref.max():.3e}; ref fp16 median {np.median(ga['emu_fp16_grad_rel']):.3e}")
     assert np.median(o) <= 2 * np.median(ref), (np.median(o), np.median(ref))
     assert o.max() <= 2 * ref.max(), (o.max(), ref.max())
+    # the binding part: every parameter whose gradient the reference's own 16-bit step keeps
+    # within 0.5 rel-L2 of fp32 (the decoder heads — 97 % of the gradient's squared norm —
+    # the decoder MLPs, ~1/4 of the parameters) is held to 2x that spread, a bound below the
+    # 1.0 a zero or unrelated gradient scores; the others are chaotic in the reference itself
+    # (their 16-bit gradients sit 0.5-2.5 rel-L2 from fp32) and keep the aggregate bounds
+    tight = [(o[i] / (2 * ref[i]), names[i]) for i in range(len(names)) if ref[i] < 0.5]
+    print(f"{len(tight)} parameters with a binding bound; worst (ours / 2 x ref spread): {max(tight)}")
+    assert len(tight) >= 100 and max(tight)[0] <= 1.0, max(tight)
+    # the whole gradient vector (squared-norm weighted): the reference's bf16 spread is 0.47
+    l2 = np.asarray(g["grad_l2"], np.float64)
+    w = l2 ** 2 / (l2 ** 2).sum()
+    assert float((w * o).sum()) <= 2 * float((w * ref).sum()), (float((w * o).sum()), float((w * ref).sum()))
+
+
+def _traj_run(precision):
+    """20 Trainer steps (clip 1.0 + AdamW, ref/model/graph_model.py:700-726) at S = 256,
+    B = 2 on the trajectory fixture's batches and noise; per-step losses and pre-clip
+    gradient norms, and the last step's mu_pr."""
+    from golden_util import traj_inputs
+    from vaeteb.train import Trainer
+    kw = dict(head_precision=precision, conv_precision=precision, mlp_precision=precision,
+              lstm_precision="16-mixed" if precision == "bf16" else "fp32", concurrent_encoders=True)
+    m = _model(256, **kw)
+    tr = Trainer(m, lr=1e-3)
+    rec = {k: [] for k in (*LOSSES, "grad_norm")}
+    last = None
+    for t in range(20):
+        y_st, y_ph, x_ph, y_raw, eps = [torch.from_numpy(a).cuda() for a in traj_inputs(256, 2, t)]
+        batch = {"fhr_st": y_st, "fhr_ph": y_ph, "fhr_up_ph": x_ph, "fhr": y_raw}
+        if t == 19:   # the last step's forward outputs: the model's forward before this step's update
+            with torch.no_grad():
+                m.train()
+                last = m(y_st, y_ph, x_ph, eps=eps)["mu_pr"].double().cpu()
+        L = tr.step(batch, eps=eps)
+        for k in rec:
+            rec[k].append(float(L[k]))
+    return {k: np.array(v) for k, v in rec.items()}, last
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_s256_training_trajectory_vs_reference(golden, precision):
+    """the ELBO over 20 training steps (a new batch per step, as the
+    reference's loop) vs the reference's own trajectory (tests/golden/traj_s256_b2.npz).
+    This model is chaotic under AdamW: the reference's fp32 trajectory leaves its own fp64
+    trajectory by 1e-3 at step 2 and by up to 24 % at step 17 (the first update moves every
+    head weight by ~lr, with a sign rounding noise decides wherever a gradient is near 0),
+    so every bound is an envelope env(t) = max over steps s <= t of the reference's own
+    spread at step s:
+      fp32 (exact kernels): |ours - ref fp32| <= 1e-4 |ref| + 3 env_fp64(t)
+          (steps 0-1, before the divergence: 1e-4 relative);
+      bf16 (the bench precision: bf16 heads / convs / MLP linears, 16-mixed LSTM):
+          |ours - ref fp32| <= 1e-4 |ref| + 2 env_bf16(t), env_bf16 = the larger of the
+          reference's emulated bf16 autocast and fp32-vs-fp64 deviations;
+    for each of the four losses and the pre-clip gradient norm, and the last step's mu_pr
+    within 2x the reference's deviation at that step."""
+    _need_gpu()
+    d = golden("traj_s256_b2")
+    ours, mu_pr = _traj_run(precision)
+    r32 = lambda k: np.asarray(d[f"fp32_{k}"], np.float64)
+    spread_modes = ["fp64"] + (["emu_bf16"] if precision == "bf16" else [])
+    factor = 3.0 if precision == "fp32" else 2.0
+    for k in (*LOSSES, "grad_norm"):
+        ref = r32(k)
+        dev = np.max([np.abs(np.asarray(d[f"{m}_{k}"], np.float64) - ref) for m in spread_modes], axis=0)
+        env = np.maximum.accumulate(dev)
+        err = np.abs(ours[k] - ref)
+        bound = 1e-4 * np.abs(ref) + factor * env + 1e-7
+        print(f"{precision} {k}: ours-ref {np.round(err / np.abs(ref), 5).tolist()}\n"
+              f"   bound/|ref| {np.round(bound / np.abs(ref), 5).tolist()}")
+        assert (err <= bound).all(), (k, int(np.argmax(err - bound)), ours[k].tolist(), ref.tolist())
+    ref_mu = np.asarray(d["fp32_mu_pr"], np.float64)
+    dev = max(rel(np.asarray(d[f"{m}_mu_pr"]), ref_mu) for m in spread_modes)
+    got = rel(mu_pr, ref_mu)
+    print(f"{precision} last-step mu_pr rel-L2 {got:.4f} (reference spread {dev:.4f})")
+    assert got <= 2 * dev + 1e-4, (got, dev)
 
 
 def _oracle_features(fe, x, st, dtype, engine):
@@ -261,8 +335,10 @@ def test_j6_config2_step_end_to_end_vs_oracle():
         e_ours, e_ref = rel(params[k].grad, gr), rel(g_o32[k], gr)
         ratios.append(e_ours / max(e_ref, 1e-12))
         worst.append((e_ours / (2e-5 + 10 * e_ref), k))
+    errs = np.array([rel(params[k].grad, gr) for k, gr in g_o.items() if gr.norm() > 0])
     print(f"J6 grads vs fp64 oracle: median ours/oracle-fp32 error ratio {np.median(ratios):.2f}, "
-          f"worst {max(worst)}")
+          f"worst {max(worst)}; ours rel-L2 median {np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} "
+          f"max {errs.max():.3e}")
     assert np.median(ratios) <= 2.0, np.median(ratios)
     worst = max(worst)
     assert worst[0] <= 1.0, worst
@@ -331,7 +407,10 @@ def test_production_geometry_end_to_end_vs_oracle():
         e_ours, e_ref = rel(params[k].grad, gr), rel(g_o32[k], gr)
         ratios.append(e_ours / max(e_ref, 1e-12))
         worst.append((e_ours / (2e-5 + 10 * e_ref), k))
+    errs = np.array([rel(params[k].grad, gr) for k, gr in g_o.items()])
+    e32 = np.array([rel(g_o32[k], gr) for k, gr in g_o.items()])
     print(f"S=300 grads vs fp64 oracle: median ours/oracle-fp32 error ratio {np.median(ratios):.2f}, "
-          f"worst {max(worst)}")
+          f"worst {max(worst)}; ours rel-L2 median {np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} "
+          f"max {errs.max():.3e}; oracle fp32 median {np.median(e32):.3e} max {e32.max():.3e}")
     assert np.median(ratios) <= 2.0, np.median(ratios)
     assert max(worst)[0] <= 1.0, max(worst)

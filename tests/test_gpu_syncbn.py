@@ -169,6 +169,16 @@ def _fit(rank, world):
     # rounding-level differences flip bf16 roundings that this model amplifies (one bf16
     # step's gradients sit ~50 % from fp32's, tests/test_gpu_parity_s256.py)
     m = det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=True)).cuda()
+    if rank > 0:
+        # every other rank starts from a different model: fit() must start all ranks from
+        # rank 0's parameters and buffers (DDP's construction-time broadcast)
+        with torch.no_grad():
+            gen = torch.Generator(device="cuda").manual_seed(rank)
+            for p_ in m.parameters():
+                p_.add_(0.1 * torch.randn(p_.shape, device="cuda", generator=gen))
+            for b_ in m.buffers():
+                if b_.is_floating_point():
+                    b_.add_(1.0)
     fwd = m.forward
     m.forward = lambda *a, **k: fwd(*a, eps=eps)        # the stored reparameterisation noise
     mod = LightSeqVaeTeb(m, lr=1e-3, beta_schedule="constant", beta_const_val=1e-5)

@@ -39,7 +39,7 @@ sys.path.insert(0, os.path.join(REF, "model"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
 
-from golden_util import det_fill_  # noqa: E402
+from golden_util import det_fill_, traj_inputs  # noqa: E402
 from vaeteb import synthetic  # noqa: E402  (data generator only)
 
 torch.set_num_threads(8)
@@ -388,8 +388,85 @@ def gen_amp():
     save("model_s256_b2_amp.npz", **d)
 
 
-def gen_model():
+TRAJ_STEPS = 20
+
+
+def run_ref_trajectory(S, B, mode, steps=TRAJ_STEPS, beta=1e-5, lr=1e-3, same_batch=False):
+    """`steps` training steps of the reference SeqVaeTeb (ref/model/graph_model.py:700-726:
+    zero_grad -> forward -> compute_loss -> backward -> clip 1.0 -> AdamW(lr 1e-3, wd 1e-4,
+    eps 1e-8, betas (0.9, 0.98)), one persistent optimizer) at `mode` precision:
+    'fp32' / 'fp64' plain; 'emu_bf16' / 'emu_fp16' under Emu16 (the CUDA-autocast op split,
+    fp32 master weights and optimizer), fp16 with GradScaler's dynamic loss scale (init
+    2^16, a step with non-finite gradients is skipped and the scale halved, :709-726).
+    Returns per-step losses / pre-clip gradient norms and the last step's mu_pr / logvar_pr."""
+    model = build_ref_model(S)
+    dt = torch.float64 if mode == "fp64" else torch.float32
+    if mode == "fp64":
+        model = model.double()
+    emu = None
+    if mode.startswith("emu_"):
+        emu = Emu16(torch.bfloat16 if mode == "emu_bf16" else torch.float16)
+        for m in model.modules():
+            if isinstance(m, torch.nn.LSTM):
+                m.forward = emu.lstm_forward(m)
+    opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=1e-4, eps=1e-8, betas=(0.9, 0.98))
+    scale = 65536.0 if mode == "emu_fp16" else 1.0
+    rec = {k: [] for k in ("mse_loss", "nll_loss", "kld_loss", "total_loss", "grad_norm", "skipped")}
+    fw = None
+    for t in range(steps):
+        y_st, y_ph, x_ph, y_raw, eps = [torch.from_numpy(a).to(dt) for a in traj_inputs(S, B, 0 if same_batch else t)]
+        model.train()
+        model.reparameterize = lambda mu, lv, _e=eps: mu + _e * torch.exp(0.5 * lv)
+        opt.zero_grad()
+        if emu is not None:
+            with emu:
+                fw = model(y_st, y_ph, x_ph)
+                L = model.compute_loss(fw, y_st, y_ph, y_raw, compute_kld_loss=True, beta=beta)
+        else:
+            fw = model(y_st, y_ph, x_ph)
+            L = model.compute_loss(fw, y_st, y_ph, y_raw, compute_kld_loss=True, beta=beta)
+        (L["total_loss"].float() * scale if scale != 1.0 else L["total_loss"]).backward()
+        skipped = False
+        if scale != 1.0:
+            grads = [p.grad for p in model.parameters() if p.grad is not None]
+            if not all(torch.isfinite(g).all() for g in grads):
+                skipped = True
+                scale *= 0.5
+            for g in grads:
+                g.div_(scale if not skipped else 2 * scale)
+        gn = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0) if not skipped else torch.tensor(0.0)
+        if not skipped:
+            opt.step()
+        for k in ("mse_loss", "nll_loss", "kld_loss", "total_loss"):
+            rec[k].append(float(L[k]))
+        rec["grad_norm"].append(float(gn))
+        rec["skipped"].append(skipped)
+    return ({k: np.array(v) for k, v in rec.items()}, fw["mu_pr"].detach().double().numpy(),
+            fw["logvar_pr"].detach().double().numpy())
+
+
+def gen_traj():
+    """a 20-step training trajectory of the reference at S = 256, B = 2
+    in fp32, fp64 (the fp32 trajectory's own rounding spread), and the 16-bit autocast
+    emulations in bf16 and fp16 (the reference's literal precision): per step the four
+    losses and the pre-clip gradient norm, and the last step's decoder outputs."""
+    S, B = 256, 2
+    d = dict(S=S, B=B, steps=TRAJ_STEPS, seed_base=5000)
+    for mode in ("fp32", "fp64", "emu_bf16", "emu_fp16"):
+        t = time.time()
+        rec, mu_pr, lv_pr = run_ref_trajectory(S, B, mode)
+        for k, v in rec.items():
+            d[f"{mode}_{k}"] = v
+        d[f"{mode}_mu_pr"] = mu_pr.astype(np.float32)
+        d[f"{mode}_logvar_pr"] = lv_pr.astype(np.float32)
+        print(f"trajectory {mode}: {time.time() - t:.1f}s total {np.round(rec['total_loss'], 5).tolist()}")
+    save("traj_s256_b2.npz", **d)
+
+
+def gen_model(only_s=None):
     for (S, B, full) in [(16, 4, True), (4, 3, True), (256, 2, False), (300, 2, False)]:
+        if only_s and S not in only_s:
+            continue
         rng = np.random.Generator(np.random.PCG64(7 + S))
         y_st = rng.standard_normal((B, S, 43)).astype(np.float32)
         y_ph = rng.standard_normal((B, S, 44)).astype(np.float32)
@@ -445,10 +522,8 @@ def gen_model():
                     d[f"gradrows_{i}"] = grads[k][:16].numpy()
             for i, k in enumerate(bn_keys):
                 d[f"bn_{i}"] = sd[k].numpy()
-            d["fw_mu_pr"] = fw["mu_pr"].detach().numpy()
-            for k in list(d):
-                if k.startswith("fw_") and k not in ("fw_mu_pr", "fw_logvar_pr"):
-                    d[k] = np.asarray(d[k])[:, :8]  # keep fixtures small
+            # every forward output over all S steps (the latent paths cross the LSTM kernels'
+            # 16-step chunk hand-offs; the decoder outputs in full)
         save(f"model_s{S}_b{B}.npz", **d)
 
 
@@ -590,7 +665,7 @@ def gen_classifier():
 
 GENS = dict(kat=gen_kymatio_kat, filters=gen_filters, scattering=gen_scattering, frontend=gen_frontend,
             stats=gen_stats_and_norm, model=gen_model, amp=gen_amp, te=gen_te, tiny=gen_tiny,
-            classifier=gen_classifier)
+            classifier=gen_classifier, traj=gen_traj, model_big=lambda: gen_model((256, 300)))
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()

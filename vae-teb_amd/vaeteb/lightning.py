@@ -272,7 +272,8 @@ def fit(module, train_loader, max_epochs=1, gradient_clip_val=0.5, val_loader=No
     opt.max_norm = gradient_clip_val
     buckets = None
     if world > 1:
-        from .train import GradBuckets
+        from .train import GradBuckets, broadcast_state
+        broadcast_state(opt.flat, module.model, group)   # DDP: every rank starts from rank 0's model
         buckets = GradBuckets(opt.flat, group)
         opt.pre_scale = 1.0 / world
     mv = lambda b: to_device(b) if to_device else b

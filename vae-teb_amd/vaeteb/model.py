@@ -720,10 +720,15 @@ class SeqVaeTeb(nn.Module):
         in eval mode afterwards, as in the reference) and no gradients.  Same values
         as the reference's full forward: the decoder it also runs there does not enter
         the KL, so only the encoders and the conditional encoder run here.  Returns
-        (B, S, latent) (reduce_mean=False) or the scalar mean of the latent sums."""
+        (B, S, latent) (reduce_mean=False) or the scalar mean of the latent sums.
+        The reference's forward also draws the reparameterisation noise (torch.randn_like,
+        :1046-1050); one draw of that shape is made and discarded here, so the device's
+        random stream advances exactly as in the reference and every later draw (noise,
+        dropout, sampling) stays aligned with it."""
         self.eval()
         with torch.no_grad():
             mu_p, lv_p, mu_q, lv_q = self.encode(y_st, y_ph, x_ph)
+            torch.randn_like(lv_q)
             return self._kld_loss(mu_p, lv_p, mu_q, lv_q, reduce_mean=reduce_mean)
 
     @staticmethod

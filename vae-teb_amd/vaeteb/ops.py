@@ -502,7 +502,10 @@ class ConvBNActF(torch.autograd.Function):
         pad = K - 1 if mode == 0 else (K - 1) // 2
         # two-launch backward (vt_batchnorm_bwd_x16 + vt_conv1d_bwd_dx16): every geometry of the
         # model's blocks (causal; reflect with L_up > pad, x2 upsample folded in the conv)
-        bwd16 = fused and CONV_BWD16 and (mode == 1 and L * (2 if up else 1) > pad or mode == 0 and not up)
+        # (and within the two kernels' limits: K <= 11, B <= 65535 workgroup rows, the BN-gradient
+        # row image of Cout <= 1024 channels in LDS; other shapes keep the fused-staging kernels)
+        bwd16 = fused and CONV_BWD16 and K <= 11 and B <= 65535 and Cout <= 1024 and \
+            (mode == 1 and L * (2 if up else 1) > pad or mode == 0 and not up)
         if bwd16:
             bnp = torch.empty(6 * Cout, device=x.device)
             call("vt_batchnorm_bwd_coef", ptr(gy), ptr(conv), M, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b),
@@ -587,6 +590,11 @@ class SyncConvBNActF(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, g, b, run_mean, run_var, mode, up, act, momentum, eps, bf16, group):
         import torch.distributed as dist
+        if x.is_cuda and torch.cuda.is_current_stream_capturing():
+            # the BatchNorm statistics are all-reduced inside the op: a collective cannot be
+            # captured into a hipGraph (Trainer.capture / the native executor)
+            raise RuntimeError("SyncBatchNorm conv blocks cannot be captured into a hipGraph "
+                               "(cross-rank statistics need a collective inside the step); train them eagerly")
         _check(x, w, g, b)
         B, L, Cin = x.shape
         Cout, _, K = w.shape

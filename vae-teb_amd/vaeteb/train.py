@@ -59,6 +59,17 @@ class FlatState:
                 p.grad = self.g[o:o + n].view_as(p)
 
 
+def broadcast_state(state, module, group=None, src=0):
+    """DistributedDataParallel's construction-time module-state sync (the reference wraps
+    the model in DDP: ref/model/graph_model.py:644, Lightning DDPStrategy :470-471): rank
+    `src`'s parameters (the flat buffer: one collective) and buffers (BatchNorm running
+    statistics and step counters) are copied to every rank, so all ranks start from the
+    same model whatever their local initialisation was."""
+    dist.broadcast(state.p, src=src, group=group)
+    for b in module.buffers():
+        dist.broadcast(b, src=src, group=group)
+
+
 class GradBuckets:
     """Bucketed all-reduce (SUM) of the flat gradient buffer, launched from
     post-accumulate-grad hooks as soon as every parameter of a bucket has its
@@ -203,6 +214,8 @@ class Trainer:
         self.graph = None
         self.norm_ws = torch.empty(_lib.lib().fns["vt_grad_norm_workspace_floats"](), device=dev)
         self.buckets = GradBuckets(self.state, group, bucket_mb, reduce_dtype) if world_size > 1 else None
+        if world_size > 1:
+            broadcast_state(self.state, model, group)   # every rank starts from rank 0's model (DDP)
         if world_size > 1 and torch.cuda.is_available():
             # hardware-queue budget: a process's streams map onto GPU_MAX_HW_QUEUES = 4 queues;
             # the model uses main + 3 side streams on one GPU, and RCCL's stream would be a 5th
@@ -335,6 +348,9 @@ class Trainer:
         noise into `CapturedStep.static_eps` before the replay."""
         if native and eps is None:
             raise ValueError("native replay needs an explicit eps buffer (in-graph RNG is not advanced)")
+        if any(getattr(m, "sync_bn", False) for m in self.model.modules()):
+            raise ValueError("a model with SyncBatchNorm blocks (convert_sync_batchnorm) cannot be captured: its "
+                             "BatchNorm statistics are all-reduced inside the step; use Trainer.step")
         static_in = {k: v.clone() for k, v in batch.items()}
         static_eps = None if eps is None else eps.clone()
         side = torch.cuda.Stream()
