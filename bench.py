@@ -258,11 +258,18 @@ def main():
                     help="= --mode graph: the model step replayed as a captured hipGraph (double-buffered, "
                          "front-end one step ahead)")
     ap.add_argument("--mode", choices=["auto", "eager", "native", "graph"], default="auto",
-                    help="auto (default): native on one GPU (the eager step's ~190 C-ABI calls from Python take "
-                         "about as long as the GPU work), eager with several GPUs (the bucketed all-reduce overlaps "
-                         "the backward there; a captured step reduces after it) and for c4 (host-side dropout "
-                         "seeds); native: the step captured once and replayed by the library's multi-stream "
-                         "executor (vt_stepgraph_*); graph: hipGraphLaunch; eager: every op from Python")
+                    help="auto (default): native for c2 at any GPU count (the eager step's ~190 C-ABI calls from "
+                         "Python take about as long as the GPU work; with several GPUs the replay is enqueued in "
+                         "ranges split at the gradient buckets' markers, each bucket's RCCL all-reduce issued as "
+                         "soon as its writers are enqueued, overlapping the rest of the backward), eager for c4 "
+                         "(host-side dropout seeds); native: the step captured once and replayed by the library's "
+                         "multi-stream executor (vt_stepgraph_*); graph: hipGraphLaunch; eager: every op from Python")
+    ap.add_argument("--ddp-probe", action="store_true",
+                    help="N = 1 with the data-parallel machinery: a single-rank RCCL process group, gradient "
+                         "buckets and their all-reduces, the world > 1 stream budget (main + 2 side streams) and "
+                         "the segmented replay -- the per-GPU cost of the DDP step without the exchange itself")
+    ap.add_argument("--reduce-bf16", action="store_true",
+                    help="reduce the gradient buckets in bf16 (fp32 master gradients; the reference reduces fp32)")
     ap.add_argument("--native", action="store_true", help="= --mode native")
     ap.add_argument("--streams", type=int, default=4, help="--native: executor streams")
     ap.add_argument("--fe-in-graph", type=int, default=0,
@@ -296,11 +303,21 @@ def main():
                          "operands, fp32 state: the reference's own 16-mixed LSTM width) or exact fp32")
     args = ap.parse_args()
 
+    if args.ddp_probe and "WORLD_SIZE" not in os.environ:
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]), WORLD_SIZE="1", RANK="0",
+                          LOCAL_RANK="0")
+        sk.close()
     rank, world, local, dev = init_distributed()
+    if args.ddp_probe and not dist.is_initialized():
+        torch.cuda.set_device(dev)
+        dist.init_process_group(backend="nccl")
+    ddp = world > 1 or args.ddp_probe
     mode = "native" if args.native else ("graph" if args.graph else args.mode)
     if mode == "auto":
-        mode = "native" if (world == 1 and args.workload == "c2" and not (args.prefetch or args.overlap_update)) \
-            else "eager"
+        mode = "native" if (args.workload == "c2" and not (args.prefetch or args.overlap_update)) else "eager"
     args.native, args.graph = mode == "native", mode == "graph"
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     torch.cuda.set_device(dev)
@@ -325,7 +342,8 @@ def main():
         model = SeqVaeTebClassifier(sequence_length=S, freeze_vae=False, **vae_kw).to(dev)
     else:
         model = SeqVaeTeb(sequence_length=S, **vae_kw).to(dev)
-    trainer = Trainer(model, lr=1e-3, frontend=fe, world_size=world)
+    trainer = Trainer(model, lr=1e-3, frontend=fe, world_size=world, ddp=ddp,
+                      reduce_dtype=torch.bfloat16 if args.reduce_bf16 else torch.float32)
 
     # synthetic windows resident in HBM before timing; global sample index ->
     # rank sharding as DistributedSampler (each rank its own B windows per step)
@@ -463,8 +481,12 @@ def main():
         step(i, last=i == args.warmup - 1)
     if hasattr(step, "first"):
         step.first = True
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
+    torch.cuda.synchronize()
+    # timed-region marker for profiles (tools/step_stats.py): a no-op kernel launched right
+    # before the timed loop and right after its synchronize, outside the timed interval
+    _lib.call("vt_bucket_marker", 0, _lib.stream())
     torch.cuda.synchronize()
     timer.reset(True)
     t0 = time.perf_counter()
@@ -473,9 +495,10 @@ def main():
         last = step(i, last=i == args.steps - 1)
     t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (launch-bound if ~= dt)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     dt = time.perf_counter() - t0
+    _lib.call("vt_bucket_marker", 0, _lib.stream())   # end of the timed region (profiles only)
     timer.enabled = False
     if world > 1:
         t = torch.tensor([dt], device=dev)
@@ -521,10 +544,16 @@ def main():
                    "parallelism": f"dp{world}"},
         "elbo": elbo,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
-        "mode": (f"step captured once, replayed by the native {args.streams}-stream executor (vt_stepgraph); "
+        "mode": (f"step captured once, replayed by the native "
+                 f"{len(caps[0].side) + 1 - bool(caps[0].markers)}-stream executor (vt_stepgraph); "
                  + ("front-end inside the captured step" if fe_in_graph else
                     "front-end eager " + ("one step ahead on its own stream" if args.overlap_fe else
-                                          "before each replay on the same stream"))) if args.native else
+                                          "before each replay on the same stream"))
+                 + (f"; {len(trainer.buckets.buckets)} gradient buckets "
+                    f"({'bf16' if args.reduce_bf16 else 'fp32'}), each all-reduced on a comm stream as soon as its "
+                    f"writers are enqueued ({len(caps[0].markers)} markers in the replay)"
+                    + (" [ddp probe: single-rank RCCL group]" if args.ddp_probe and world == 1 else "")
+                    if trainer.buckets else "")) if args.native else
                 "model step replayed as a hipGraph (double-buffered), front-end eager one step ahead on its own stream"
                 if graph else ("eager, next batch's front-end overlapped with clip + AdamW (own streams, "
                                "double-buffered features)" if args.overlap_update else
@@ -575,7 +604,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline((J, Q, T), batch=args.cpu_batch, classifier=c4)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

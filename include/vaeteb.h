@@ -588,6 +588,24 @@ int vt_stepgraph_build(void* graph, int n_streams, void** handle);
 int vt_stepgraph_launch(void* handle, void* const* streams);
 int vt_stepgraph_info(void* handle, int* n_kernel, int* n_memcpy, int* n_memset, int* n_waits);
 int vt_stepgraph_destroy(void* handle);
+/* Data-parallel replay with the gradient all-reduce overlapped (the reference's DDP
+ * reducer launches bucket all-reduces from the backward: ref/model/graph_model.py:644,
+ * Lightning DDPStrategy :470-471).  vt_bucket_marker enqueues a no-op marker kernel; a step
+ * captured with one marker per gradient bucket, each on a "comm" stream that has joined
+ * every stream that wrote the bucket, builds an executor whose markers are not launched but
+ * run on an extra stream streams[n_streams] (only their event waits): the launch list can
+ * then be enqueued in ranges, and after the range that ends with a bucket's marker the
+ * caller issues that bucket's collective on the comm stream (it waits only for the
+ * bucket's writers, not for the rest of the backward).
+ * vt_stepgraph_markers: n_ops (the length of the launch list), and for the first `cap`
+ *   markers in launch order the op index just past it (ends[i]) and its bucket id.
+ * vt_stepgraph_launch_range: ops [begin, end); flags bit 0 = fork every stream from
+ *   streams[0] first, bit 1 = join every stream into streams[0] after.  A full step is
+ *   ranges covering [0, n_ops) in order, the first with bit 0, the last with bit 1.
+ *   streams has n_streams + 1 entries when the graph holds markers.                      */
+int vt_bucket_marker(int bucket, void* stream);
+int vt_stepgraph_markers(void* handle, int* n_ops, int* n_markers, int* ends, int* buckets, int cap);
+int vt_stepgraph_launch_range(void* handle, void* const* streams, int begin, int end, int flags);
 
 #ifdef __cplusplus
 }

@@ -92,3 +92,63 @@ def test_bucketed_allreduce_waits_for_side_stream_gradients():
         assert torch.equal(out[rank][2], expect), rank
     assert out[0][4] > 1 and out[0][5] > 1                # buckets launched from the backward hooks
     assert torch.equal(out[0][3], out[1][3])
+
+
+def _seg_worker(rank, world, port, q):
+    """Eager DDP steps vs the captured step replayed by the native executor in ranges,
+    each bucket's all-reduce issued after the range that ends with its marker."""
+    sys.path[:0] = [os.path.join(ROOT, "vae-teb_amd"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vaeteb.train import Trainer
+    b0, e0 = _batch(rank)
+    b1 = {k: v.roll(1, 0).contiguous() for k, v in b0.items()}
+    e1 = e0.roll(1, 0).contiguous()
+    seq = ((b1, e1), (b0, e0), (b1, e1))
+    res, n_mark, n_buckets = [], 0, 0
+    for native in (False, True):
+        tr = Trainer(_model(), lr=1e-3, world_size=world, bucket_mb=0.5)
+        if native:
+            cap = tr.capture(b0, eps=e0, warmup=2, native=True)
+            n_mark, n_buckets = len(cap.markers), len(tr.buckets.buckets)
+            outs = [cap.replay(b, eps=e)["total_loss"].item() for b, e in seq]
+        else:
+            for _ in range(2):
+                tr.step(b0, eps=e0)
+            outs = [tr.step(b, eps=e)["total_loss"].item() for b, e in seq]
+        torch.cuda.synchronize()
+        res.append((outs, tr.state.p.cpu(), tr.state.m.cpu(), tr.state.v.cpu()))
+        del tr
+    q.put((rank, res, n_mark, n_buckets))
+    dist.destroy_process_group()
+
+
+def test_segmented_native_replay_equals_eager_ddp_step():
+    """the data-parallel step on the native executor.  The step is
+    captured with a marker where each gradient bucket completes (GradBuckets under
+    Trainer.capture), the executor enqueues the replay in ranges split at the markers,
+    and each bucket's all-reduce is issued on the comm stream right after its range —
+    overlapping the rest of the backward instead of following the whole replay.  Two
+    ranks on one GPU (gloo over CUDA tensors): losses, parameters and Adam moments after
+    2 + 3 steps equal the eager DDP step's (all-reduces from the backward hooks) bit for
+    bit, and the parameters are identical across ranks."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=200) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res, n_mark, n_buckets in out:
+        (o_e, p_e, m_e, v_e), (o_n, p_n, m_n, v_n) = res
+        assert n_buckets > 4 and n_mark >= n_buckets - 1, (n_mark, n_buckets)   # all but possibly the last
+        assert o_e == o_n, (rank, o_e, o_n)
+        assert torch.equal(p_e, p_n) and torch.equal(m_e, m_n) and torch.equal(v_e, v_n), rank
+    assert torch.equal(out[0][1][1][1], out[1][1][1][1])    # the same model on both ranks

@@ -6,9 +6,11 @@ CosineAnnealingLR — vs the same loop written out over the oracle model
 (oracle/model_ref.py) with torch's AdamW / clip_grad_norm_ / CosineAnnealingLR, at the
 golden S = 16 geometry in fp32.
 
-Tolerance per epoch and loss: |ours - oracle fp64| <= 3 x |oracle fp32 - oracle fp64|
-+ 1e-4 relative (four AdamW steps through a 4-layer LSTM and 17 train-mode BatchNorms
-carry each implementation's fp32 rounding into the later steps)."""
+Tolerance per epoch and loss: |ours - oracle fp64| <= 3 x the largest distance from the
+fp64 loop of three fp32 oracle loops (the base run and two from one-ulp perturbed initial
+weights) + 1e-4 relative.  AdamW makes this model's trajectory chaotic (rounding-level
+gradient differences near 0 become lr-sized steps), so one fp32 run's distance from fp64
+is luck: it measured 0.05 % on one host and 1.7 % on another for the same epoch."""
 import numpy as np
 import pytest
 import torch
@@ -31,11 +33,14 @@ def _batches(seed, n):
     return out
 
 
-def _oracle_history(train, val, dtype):
+def _oracle_history(train, val, dtype, perturb=None):
     """ref/model/graph_model.py:612-908 over the oracle model (per-epoch averages)."""
-    from golden_util import det_fill_
+    from golden_util import det_fill_, perturb_ulp_
     from oracle import model_ref as M
-    ref = det_fill_(M.SeqVaeTebRef(S)).to(dtype)
+    ref = det_fill_(M.SeqVaeTebRef(S))
+    if perturb is not None:
+        perturb_ulp_(ref, perturb)
+    ref = ref.to(dtype)
     opt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=1e-4, eps=1e-8, betas=(0.9, 0.98))
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=EPOCHS, eta_min=1e-3 * 0.01)
     T = lambda a: torch.from_numpy(a).to(dtype)
@@ -54,7 +59,7 @@ def _oracle_history(train, val, dtype):
             L["total_loss"].backward()
             torch.nn.utils.clip_grad_norm_(ref.parameters(), 1.0)
             opt.step()
-            sums += [float(L[k]) for k in KEYS]
+            sums += [float(L[k].detach()) for k in KEYS]
         ref.eval()
         vsums = np.zeros(len(KEYS))
         with torch.no_grad():
@@ -92,9 +97,10 @@ def test_epoch_driver_over_hip_trainer_vs_oracle_loop():
     hist = train_base_model_pytorch(tr, train, val, epochs=EPOCHS, to_device=to_dev)
     assert np.allclose(hist["lr"], [1e-3, 1e-3 * 0.01 + (1e-3 - 1e-3 * 0.01) * 0.5], rtol=1e-12, atol=0)
     h64 = _oracle_history(train, val, torch.float64)
-    h32 = _oracle_history(train, val, torch.float32)
+    h32 = [_oracle_history(train, val, torch.float32, perturb=p) for p in (None, 1, 2)]
     for key in h64:
         for e in range(EPOCHS):
-            a, x, r = hist[key][e], h64[key][e], h32[key][e]
-            print(f"{key} epoch {e}: ours {a:.8f} oracle64 {x:.8f} oracle32 {r:.8f}")
-            assert abs(a - x) <= 3 * abs(r - x) + 1e-4 * abs(x) + 1e-8, (key, e, a, x, r)
+            a, x = hist[key][e], h64[key][e]
+            spread = max(abs(h[key][e] - x) for h in h32)
+            print(f"{key} epoch {e}: ours {a:.8f} oracle64 {x:.8f} oracle32 spread {spread:.3e}")
+            assert abs(a - x) <= 3 * spread + 1e-4 * abs(x) + 1e-8, (key, e, a, x, spread)

@@ -224,27 +224,35 @@ def _traj_run(precision):
 def test_s256_training_trajectory_vs_reference(golden, precision):
     """the ELBO over 20 training steps (a new batch per step, as the
     reference's loop) vs the reference's own trajectory (tests/golden/traj_s256_b2.npz).
-    This model is chaotic under AdamW: the reference's fp32 trajectory leaves its own fp64
-    trajectory by 1e-3 at step 2 and by up to 24 % at step 17 (the first update moves every
-    head weight by ~lr, with a sign rounding noise decides wherever a gradient is near 0),
-    so every bound is an envelope env(t) = max over steps s <= t of the reference's own
-    spread at step s:
-      fp32 (exact kernels): |ours - ref fp32| <= 1e-4 |ref| + 3 env_fp64(t)
-          (steps 0-1, before the divergence: 1e-4 relative);
-      bf16 (the bench precision: bf16 heads / convs / MLP linears, 16-mixed LSTM):
-          |ours - ref fp32| <= 1e-4 |ref| + 2 env_bf16(t), env_bf16 = the larger of the
-          reference's emulated bf16 autocast and fp32-vs-fp64 deviations;
+    This model is chaotic under AdamW: the first update moves every head weight by ~lr,
+    with a sign that rounding noise decides wherever a gradient is near 0, so the
+    reference's fp32 trajectory leaves its own fp64 trajectory by 1e-3 at step 2 and by
+    tens of percent (NLL) later, and so do fp32 runs of it from one-ulp perturbed initial
+    weights.  The bound at step t is therefore an envelope: env(t) = the running maximum
+    over steps s <= t of the reference ensemble's deviation from its base fp32 run —
+      fp32 (exact kernels): the fp64 run and three one-ulp perturbed fp32 runs;
+          |ours - ref fp32| <= 1e-4 |ref| + 3 env(t)  (steps 0-1: the unperturbed members only,
+          1e-4 relative + 3x the fp64 distance);
+      bf16 (the bench precision: bf16 heads / convs / MLP linears, 16-mixed LSTM): those
+          and the emulated-bf16-autocast runs (base + two perturbed);
+          |ours - ref fp32| <= 1e-4 |ref| + 2 env(t);
     for each of the four losses and the pre-clip gradient norm, and the last step's mu_pr
-    within 2x the reference's deviation at that step."""
+    within 2x the ensemble's largest deviation at that step."""
     _need_gpu()
     d = golden("traj_s256_b2")
     ours, mu_pr = _traj_run(precision)
     r32 = lambda k: np.asarray(d[f"fp32_{k}"], np.float64)
-    spread_modes = ["fp64"] + (["emu_bf16"] if precision == "bf16" else [])
+    members = ["fp64", "fp32_p1", "fp32_p2", "fp32_p3"]
+    if precision == "bf16":
+        members += ["emu_bf16", "emu_bf16_p1", "emu_bf16_p2"]
     factor = 3.0 if precision == "fp32" else 2.0
     for k in (*LOSSES, "grad_norm"):
         ref = r32(k)
-        dev = np.max([np.abs(np.asarray(d[f"{m}_{k}"], np.float64) - ref) for m in spread_modes], axis=0)
+        devs = {m: np.abs(np.asarray(d[f"{m}_{k}"], np.float64) - ref) for m in members}
+        dev = np.max(list(devs.values()), axis=0)
+        # steps 0-1 (the first forward, and the forward after one update): only the unperturbed
+        # members (fp64 / emulated bf16), so those steps keep a strict pin
+        dev[:2] = np.max([v for m, v in devs.items() if "_p" not in m], axis=0)[:2]
         env = np.maximum.accumulate(dev)
         err = np.abs(ours[k] - ref)
         bound = 1e-4 * np.abs(ref) + factor * env + 1e-7
@@ -252,11 +260,10 @@ def test_s256_training_trajectory_vs_reference(golden, precision):
               f"   bound/|ref| {np.round(bound / np.abs(ref), 5).tolist()}")
         assert (err <= bound).all(), (k, int(np.argmax(err - bound)), ours[k].tolist(), ref.tolist())
     ref_mu = np.asarray(d["fp32_mu_pr"], np.float64)
-    dev = max(rel(np.asarray(d[f"{m}_mu_pr"]), ref_mu) for m in spread_modes)
+    dev = max(rel(np.asarray(d[f"{m}_mu_pr"]), ref_mu) for m in members)
     got = rel(mu_pr, ref_mu)
-    print(f"{precision} last-step mu_pr rel-L2 {got:.4f} (reference spread {dev:.4f})")
+    print(f"{precision} last-step mu_pr rel-L2 {got:.4f} (reference ensemble spread {dev:.4f})")
     assert got <= 2 * dev + 1e-4, (got, dev)
-
 
 def _oracle_features(fe, x, st, dtype, engine):
     """Oracle front-end (the reference's two calls, create_hdf5_dataset.py:418-441)
@@ -335,10 +342,16 @@ def test_j6_config2_step_end_to_end_vs_oracle():
         e_ours, e_ref = rel(params[k].grad, gr), rel(g_o32[k], gr)
         ratios.append(e_ours / max(e_ref, 1e-12))
         worst.append((e_ours / (2e-5 + 10 * e_ref), k))
-    errs = np.array([rel(params[k].grad, gr) for k, gr in g_o.items() if gr.norm() > 0])
+    # fixed bounds from the errors measured here (round 4: median 6.8e-6, p90 1.0e-5 over the
+    # gradients the oracle's own fp32 run gets within 1e-3 of fp64): the per-parameter bound
+    # above is relative to the oracle's fp32 error, which is large for the chaotic ones, so
+    # these aggregates are what a regression of the HIP gradients would fail
+    errs = np.array([rel(params[k].grad, gr) for k, gr in g_o.items()
+                     if gr.norm() > 0 and rel(g_o32[k], gr) < 1e-3])
     print(f"J6 grads vs fp64 oracle: median ours/oracle-fp32 error ratio {np.median(ratios):.2f}, "
-          f"worst {max(worst)}; ours rel-L2 median {np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} "
-          f"max {errs.max():.3e}")
+          f"worst {max(worst)}; ours rel-L2 over {len(errs)} well-conditioned gradients: median "
+          f"{np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} max {errs.max():.3e}")
+    assert len(errs) >= 100 and np.median(errs) <= 2e-5 and np.percentile(errs, 90) <= 5e-5, errs
     assert np.median(ratios) <= 2.0, np.median(ratios)
     worst = max(worst)
     assert worst[0] <= 1.0, worst
@@ -407,10 +420,14 @@ def test_production_geometry_end_to_end_vs_oracle():
         e_ours, e_ref = rel(params[k].grad, gr), rel(g_o32[k], gr)
         ratios.append(e_ours / max(e_ref, 1e-12))
         worst.append((e_ours / (2e-5 + 10 * e_ref), k))
+    # fixed bounds from the errors measured here (round 4: median 6.4e-6, p90 1.1e-5, max 2.7e-4
+    # over every gradient; the oracle's own fp32 step is 8e-3 off in median at S = 300, so the
+    # ratio bound above does not bind — these do)
     errs = np.array([rel(params[k].grad, gr) for k, gr in g_o.items()])
     e32 = np.array([rel(g_o32[k], gr) for k, gr in g_o.items()])
     print(f"S=300 grads vs fp64 oracle: median ours/oracle-fp32 error ratio {np.median(ratios):.2f}, "
           f"worst {max(worst)}; ours rel-L2 median {np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} "
           f"max {errs.max():.3e}; oracle fp32 median {np.median(e32):.3e} max {e32.max():.3e}")
+    assert np.median(errs) <= 2e-5 and np.percentile(errs, 90) <= 5e-5 and errs.max() <= 2e-3, errs
     assert np.median(ratios) <= 2.0, np.median(ratios)
     assert max(worst)[0] <= 1.0, max(worst)

@@ -39,7 +39,7 @@ sys.path.insert(0, os.path.join(REF, "model"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
 
-from golden_util import det_fill_, traj_inputs  # noqa: E402
+from golden_util import det_fill_, perturb_ulp_, traj_inputs  # noqa: E402
 from vaeteb import synthetic  # noqa: E402  (data generator only)
 
 torch.set_num_threads(8)
@@ -391,7 +391,7 @@ def gen_amp():
 TRAJ_STEPS = 20
 
 
-def run_ref_trajectory(S, B, mode, steps=TRAJ_STEPS, beta=1e-5, lr=1e-3, same_batch=False):
+def run_ref_trajectory(S, B, mode, steps=TRAJ_STEPS, beta=1e-5, lr=1e-3, same_batch=False, perturb=None):
     """`steps` training steps of the reference SeqVaeTeb (ref/model/graph_model.py:700-726:
     zero_grad -> forward -> compute_loss -> backward -> clip 1.0 -> AdamW(lr 1e-3, wd 1e-4,
     eps 1e-8, betas (0.9, 0.98)), one persistent optimizer) at `mode` precision:
@@ -400,6 +400,8 @@ def run_ref_trajectory(S, B, mode, steps=TRAJ_STEPS, beta=1e-5, lr=1e-3, same_ba
     2^16, a step with non-finite gradients is skipped and the scale halved, :709-726).
     Returns per-step losses / pre-clip gradient norms and the last step's mu_pr / logvar_pr."""
     model = build_ref_model(S)
+    if perturb is not None:
+        perturb_ulp_(model, perturb)
     dt = torch.float64 if mode == "fp64" else torch.float32
     if mode == "fp64":
         model = model.double()
@@ -452,14 +454,21 @@ def gen_traj():
     losses and the pre-clip gradient norm, and the last step's decoder outputs."""
     S, B = 256, 2
     d = dict(S=S, B=B, steps=TRAJ_STEPS, seed_base=5000)
-    for mode in ("fp32", "fp64", "emu_bf16", "emu_fp16"):
+    # the base runs, then ensemble members from one-ulp perturbed initial weights: the
+    # trajectory is chaotic (AdamW turns rounding-level gradient differences near 0 into
+    # lr-sized steps), so one fp32-vs-fp64 pair under-states the reference's own spread at
+    # some steps by luck; the tests bound by the ensemble's running maximum
+    runs = [("fp32", None), ("fp64", None), ("emu_bf16", None), ("emu_fp16", None),
+            ("fp32", 1), ("fp32", 2), ("fp32", 3), ("emu_bf16", 1), ("emu_bf16", 2)]
+    for mode, pert in runs:
         t = time.time()
-        rec, mu_pr, lv_pr = run_ref_trajectory(S, B, mode)
+        rec, mu_pr, lv_pr = run_ref_trajectory(S, B, mode, perturb=pert)
+        tag = mode if pert is None else f"{mode}_p{pert}"
         for k, v in rec.items():
-            d[f"{mode}_{k}"] = v
-        d[f"{mode}_mu_pr"] = mu_pr.astype(np.float32)
-        d[f"{mode}_logvar_pr"] = lv_pr.astype(np.float32)
-        print(f"trajectory {mode}: {time.time() - t:.1f}s total {np.round(rec['total_loss'], 5).tolist()}")
+            d[f"{tag}_{k}"] = v
+        d[f"{tag}_mu_pr"] = mu_pr.astype(np.float32)
+        d[f"{tag}_logvar_pr"] = lv_pr.astype(np.float32)
+        print(f"trajectory {tag}: {time.time() - t:.1f}s total {np.round(rec['total_loss'], 5).tolist()}", flush=True)
     save("traj_s256_b2.npz", **d)
 
 

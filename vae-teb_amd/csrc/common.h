@@ -11,6 +11,8 @@ namespace vt {
 // code; the message of the last failure on this thread is kept for
 // vt_last_error().  No C++ exception crosses the ABI.
 void set_error(const char* fmt, ...);
+// host stub of the gradient-bucket marker kernel (optim.hip), recognised by the executor
+const void* bucket_marker_kernel();
 
 #define VT_CHECK_ARG(cond, ...)                  \
     do {                                         \

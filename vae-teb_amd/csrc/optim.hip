@@ -296,3 +296,22 @@ int vt_cast_bf16_to_f32(const void* src, float* dst, int64_t n, void* stream) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ bucket markers
+// A no-op kernel captured into the step where a gradient bucket becomes complete
+// (vaeteb.train.GradBuckets under Trainer.capture with several ranks): the native
+// executor recognises it by its function pointer, does not launch it, and splits
+// its launch list there so the bucket's all-reduce is issued mid-backward
+// (csrc/stepgraph.cpp, vt_stepgraph_markers / vt_stepgraph_launch_range).
+__global__ void k_bucket_mark(int bucket) { (void)bucket; }
+
+namespace vt {
+const void* bucket_marker_kernel() { return reinterpret_cast<const void*>(&k_bucket_mark); }
+}  // namespace vt
+
+extern "C" int vt_bucket_marker(int bucket, void* stream) {
+    VT_CHECK_ARG(bucket >= 0, "vt_bucket_marker: bucket %d", bucket);
+    hipLaunchKernelGGL(k_bucket_mark, dim3(1), dim3(1), 0, S(stream), bucket);
+    VT_LAUNCH_CHECK("vt_bucket_marker");
+    return VT_OK;
+}

@@ -36,7 +36,7 @@
 namespace vt {
 namespace {
 
-enum OpKind { OP_KERNEL = 0, OP_MEMCPY = 1, OP_MEMSET = 2 };
+enum OpKind { OP_KERNEL = 0, OP_MEMCPY = 1, OP_MEMSET = 2, OP_MARK = 3 };
 
 struct Op {
     int kind = OP_KERNEL;
@@ -47,12 +47,14 @@ struct Op {
     hipMemcpyKind ckind = hipMemcpyDefault;
     hipMemsetParams sp{};
     int stream = 0;
+    int bucket = -1;          // OP_MARK: the gradient bucket whose writers it joins
     int record = -1;          // event recorded after this op (-1: none)
     std::vector<int> waits;   // events this op's stream waits on before it
 };
 
 struct StepGraph {
-    int n_streams = 0;
+    int n_streams = 0;        // compute streams; markers run on one more (index n_streams)
+    bool has_comm = false;
     std::vector<Op> ops;
     std::vector<hipEvent_t> events;
     hipEvent_t fork = nullptr;
@@ -156,9 +158,24 @@ int build(hipGraph_t g, int n_streams, StepGraph* sg) {
         r.erase(std::unique(r.begin(), r.end()), r.end());
         rdeps[i] = r;
     }
+    // gradient-bucket markers (vt_bucket_marker): not launched; they go to an extra
+    // stream (index n_streams) that only waits for the bucket's writers
+    const void* mark_fn = bucket_marker_kernel();
+    std::vector<int> mark_bucket(n, -1);
+    bool any_mark = false;
+    for (size_t i = 0; i < n; ++i) {
+        if (type[i] != hipGraphNodeTypeKernel) continue;
+        hipKernelNodeParams kp{};
+        SG_TRY(hipGraphKernelNodeGetParams(nodes[i], &kp), "hipGraphKernelNodeGetParams");
+        if (kp.func == mark_fn && kp.kernelParams && kp.kernelParams[0]) {
+            mark_bucket[i] = *(const int*)kp.kernelParams[0];
+            any_mark = true;
+        }
+    }
     // stream assignment with per-stream frontiers: seen[s][x] = number of ops of
     // stream x known complete before the next op of stream s (transitively)
-    const int S = n_streams;
+    const int S = n_streams + (any_mark ? 1 : 0);
+    const int SC = n_streams;   // streams a compute op may take
     std::vector<int> op_of(n, -1), pos(n, 0), cnt(S, 0), tail(S, -1), last_use(S, -1);
     std::vector<std::vector<int>> seen(S, std::vector<int>(S, 0));
     std::vector<std::vector<int>> snap(n);
@@ -169,16 +186,20 @@ int build(hipGraph_t g, int n_streams, StepGraph* sg) {
     for (int i : order) {
         if (type[i] == hipGraphNodeTypeEmpty) continue;
         int s = -1, best_d = -1;
-        for (int d : rdeps[i]) {  // follow the most recent dependency whose stream has not moved on
-            const int x = sg->ops[op_of[d]].stream;
-            if (tail[x] == d && d > best_d) {
-                best_d = d;
-                s = x;
+        if (mark_bucket[i] >= 0) {
+            s = SC;
+        } else {
+            for (int d : rdeps[i]) {  // follow the most recent dependency whose stream has not moved on
+                const int x = sg->ops[op_of[d]].stream;
+                if (x < SC && tail[x] == d && d > best_d) {
+                    best_d = d;
+                    s = x;
+                }
             }
         }
         if (s < 0) {  // the least recently used stream (an unused one first)
             s = 0;
-            for (int x = 1; x < S; ++x)
+            for (int x = 1; x < SC; ++x)
                 if (last_use[x] < last_use[s]) s = x;
         }
         Op op;
@@ -197,7 +218,10 @@ int build(hipGraph_t g, int n_streams, StepGraph* sg) {
             for (int y = 0; y < S; ++y) seen[s][y] = std::max(seen[s][y], snap[d][y]);
         }
         const hipGraphNode_t nd = nodes[i];
-        if (type[i] == hipGraphNodeTypeKernel) {
+        if (mark_bucket[i] >= 0) {
+            op.kind = OP_MARK;
+            op.bucket = mark_bucket[i];
+        } else if (type[i] == hipGraphNodeTypeKernel) {
             op.kind = OP_KERNEL;
             SG_TRY(hipGraphKernelNodeGetParams(nd, &op.kp), "hipGraphKernelNodeGetParams");
             if (op.kp.kernelParams == nullptr || op.kp.func == nullptr) {
@@ -243,11 +267,12 @@ int build(hipGraph_t g, int n_streams, StepGraph* sg) {
         op_of[i] = (int)sg->ops.size();
         sg->ops.push_back(op);
     }
-    sg->n_streams = S;
+    sg->n_streams = SC;
+    sg->has_comm = any_mark;
     sg->events.assign(n_events, nullptr);
     for (auto& e : sg->events) SG_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     SG_TRY(hipEventCreateWithFlags(&sg->fork, hipEventDisableTiming), "hipEventCreate");
-    sg->join.assign(S, nullptr);
+    sg->join.assign(S, nullptr);   // S includes the marker stream
     for (auto& e : sg->join) SG_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     return VT_OK;
 }
@@ -259,14 +284,20 @@ void destroy(StepGraph* sg) {
     delete sg;
 }
 
-int launch(StepGraph* sg, const hipStream_t* st) {
+int launch(StepGraph* sg, const hipStream_t* st, int begin, int end, int flags) {
     const hipStream_t caller = st[0];
-    SG_TRY(hipEventRecord(sg->fork, caller), "fork record");
-    for (int s = 1; s < sg->n_streams; ++s) SG_TRY(hipStreamWaitEvent(st[s], sg->fork, 0), "fork wait");
-    for (const Op& op : sg->ops) {
+    const int S = sg->n_streams + (sg->has_comm ? 1 : 0);
+    if (flags & 1) {
+        SG_TRY(hipEventRecord(sg->fork, caller), "fork record");
+        for (int s = 1; s < S; ++s) SG_TRY(hipStreamWaitEvent(st[s], sg->fork, 0), "fork wait");
+    }
+    for (int k = begin; k < end; ++k) {
+        const Op& op = sg->ops[k];
         hipStream_t q = st[op.stream];
         for (int e : op.waits) SG_TRY(hipStreamWaitEvent(q, sg->events[e], 0), "wait");
-        if (op.kind == OP_KERNEL) {
+        if (op.kind == OP_MARK) {
+            // not launched: the stream has now joined the bucket's writers
+        } else if (op.kind == OP_KERNEL) {
             SG_TRY(hipLaunchKernel(op.kp.func, op.kp.gridDim, op.kp.blockDim, op.kp.kernelParams,
                                    op.kp.sharedMemBytes, q),
                    "hipLaunchKernel");
@@ -283,9 +314,11 @@ int launch(StepGraph* sg, const hipStream_t* st) {
         }
         if (op.record >= 0) SG_TRY(hipEventRecord(sg->events[op.record], q), "record");
     }
-    for (int s = 1; s < sg->n_streams; ++s) {
-        SG_TRY(hipEventRecord(sg->join[s], st[s]), "join record");
-        SG_TRY(hipStreamWaitEvent(caller, sg->join[s], 0), "join wait");
+    if (flags & 2) {
+        for (int s = 1; s < S; ++s) {
+            SG_TRY(hipEventRecord(sg->join[s], st[s]), "join record");
+            SG_TRY(hipStreamWaitEvent(caller, sg->join[s], 0), "join wait");
+        }
     }
     return VT_OK;
 }
@@ -312,9 +345,40 @@ int vt_stepgraph_build(void* graph, int n_streams, void** handle) {
 int vt_stepgraph_launch(void* handle, void* const* streams) {
     VT_CHECK_ARG(handle != nullptr && streams != nullptr, "vt_stepgraph_launch: null handle / streams");
     const StepGraph* sg = (const StepGraph*)handle;
-    for (int s = 1; s < sg->n_streams; ++s)
+    const int S = sg->n_streams + (sg->has_comm ? 1 : 0);
+    for (int s = 1; s < S; ++s)
         VT_CHECK_ARG(streams[s] != streams[0], "vt_stepgraph_launch: stream %d is the caller's stream", s);
-    return launch((StepGraph*)handle, (const hipStream_t*)streams);
+    return launch((StepGraph*)handle, (const hipStream_t*)streams, 0, (int)sg->ops.size(), 3);
+}
+
+int vt_stepgraph_launch_range(void* handle, void* const* streams, int begin, int end, int flags) {
+    VT_CHECK_ARG(handle != nullptr && streams != nullptr, "vt_stepgraph_launch_range: null handle / streams");
+    const StepGraph* sg = (const StepGraph*)handle;
+    VT_CHECK_ARG(begin >= 0 && begin <= end && end <= (int)sg->ops.size() && flags >= 0 && flags <= 3,
+                 "vt_stepgraph_launch_range: range [%d, %d) of %d ops, flags %d", begin, end, (int)sg->ops.size(),
+                 flags);
+    const int S = sg->n_streams + (sg->has_comm ? 1 : 0);
+    for (int s = 1; s < S; ++s)
+        VT_CHECK_ARG(streams[s] != streams[0], "vt_stepgraph_launch_range: stream %d is the caller's stream", s);
+    return launch((StepGraph*)handle, (const hipStream_t*)streams, begin, end, flags);
+}
+
+int vt_stepgraph_markers(void* handle, int* n_ops, int* n_markers, int* ends, int* buckets, int cap) {
+    VT_CHECK_ARG(handle && n_ops && n_markers && cap >= 0 && (cap == 0 || (ends && buckets)),
+                 "vt_stepgraph_markers: args");
+    const StepGraph* sg = (const StepGraph*)handle;
+    *n_ops = (int)sg->ops.size();
+    int m = 0;
+    for (int k = 0; k < (int)sg->ops.size(); ++k) {
+        if (sg->ops[k].kind != OP_MARK) continue;
+        if (m < cap) {
+            ends[m] = k + 1;
+            buckets[m] = sg->ops[k].bucket;
+        }
+        ++m;
+    }
+    *n_markers = m;
+    return VT_OK;
 }
 
 int vt_stepgraph_info(void* handle, int* n_kernel, int* n_memcpy, int* n_memset, int* n_waits) {

@@ -104,6 +104,11 @@ class GradBuckets:
         self.launched = []
         self.ready = set()
         self.enabled = True   # False while a hipGraph is captured: no collective inside the graph
+        # while a step is captured for the native executor: a marker kernel on `comm` (joined
+        # with every gradient writer) where each bucket completes, so the replay can issue the
+        # bucket's all-reduce mid-backward (CapturedStep.replay, vt_stepgraph_launch_range)
+        self.mark_capture = False
+        self.comm = None
         # torch ops reach the flat gradient through AccumulateGrad (hook); the HIP
         # ops write it in place and report through vaeteb.ops.GRAD_READY
         self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in state.params]
@@ -116,6 +121,14 @@ class GradBuckets:
         self.launched = []
         self.ready = set()
 
+    def launch_bucket(self, b):
+        """Bucket b's all-reduce, issued on the current stream (the replay of a captured
+        step: the comm stream, after the executor range ending with b's marker)."""
+        if self.pending[b] > 0:
+            s, e, _ = self.buckets[b]
+            self._launch(s, e)
+            self.pending[b] = 0
+
     def reduce_all(self):
         """All buckets at once (after a graph replay of the backward)."""
         for b, (s, e, _) in enumerate(self.buckets):
@@ -123,12 +136,23 @@ class GradBuckets:
             self.pending[b] = 0
 
     def _hook(self, p):
-        if not self.enabled or id(p) in self.ready or id(p) not in self.param_bucket:
+        if not (self.enabled or self.mark_capture) or id(p) in self.ready or id(p) not in self.param_bucket:
             return  # each parameter counts once per step
         self.ready.add(id(p))
         b = self.param_bucket[id(p)]
         self.pending[b] -= 1
-        if self.pending[b] == 0:
+        if self.pending[b] == 0 and self.mark_capture:
+            # the comm stream joins every stream that may have written the bucket (the
+            # current one and the side streams), then the marker: a graph node that depends
+            # on exactly the bucket's writers and that nothing in the step waits for
+            cur = _lib.stream()
+            from . import ops
+            _lib.wait_for(self.comm, cur)
+            for st in ops.SIDE_STREAMS:
+                if st.cuda_stream != self.comm.cuda_stream:
+                    _lib.wait_for(self.comm, st)
+            _lib.call("vt_bucket_marker", b, self.comm.cuda_stream)
+        elif self.pending[b] == 0:
             # a bucket's gradients may have been written on several streams (the
             # concurrent encoders, the side-stream weight gradients): the collective
             # waits for all of them.  The side streams are read here, not at
@@ -198,7 +222,12 @@ class Trainer:
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=1e-4, max_norm=1.0, beta_kld=1e-5,
                  frontend=None, world_size=1, group=None, bucket_mb=64.0, vae_loss_weight=0.1,
-                 reduce_dtype=torch.float32):
+                 reduce_dtype=torch.float32, ddp=None):
+        """ddp: the bucketed gradient all-reduce (GradBuckets) on (True) / off (False);
+        default on exactly when world_size > 1.  ddp=True with one rank (an initialised
+        single-rank process group) runs the data-parallel step's whole machinery — buckets,
+        the world > 1 stream budget, the segmented native replay — at N = 1 (bench.py
+        --ddp-probe)."""
         self.model = model
         self.vae_loss_weight = vae_loss_weight
         self.frontend = frontend
@@ -213,10 +242,11 @@ class Trainer:
         self.adam_coef = torch.zeros(2, device=dev)
         self.graph = None
         self.norm_ws = torch.empty(_lib.lib().fns["vt_grad_norm_workspace_floats"](), device=dev)
-        self.buckets = GradBuckets(self.state, group, bucket_mb, reduce_dtype) if world_size > 1 else None
-        if world_size > 1:
+        ddp = world_size > 1 if ddp is None else bool(ddp)
+        self.buckets = GradBuckets(self.state, group, bucket_mb, reduce_dtype) if ddp else None
+        if ddp:
             broadcast_state(self.state, model, group)   # every rank starts from rank 0's model (DDP)
-        if world_size > 1 and torch.cuda.is_available():
+        if ddp and torch.cuda.is_available():
             # hardware-queue budget: a process's streams map onto GPU_MAX_HW_QUEUES = 4 queues;
             # the model uses main + 3 side streams on one GPU, and RCCL's stream would be a 5th
             # sharing (and serialising behind) one of them — with several ranks the model keeps
@@ -362,12 +392,27 @@ class Trainer:
         if pre_capture is not None:
             pre_capture()
         graph = torch.cuda.CUDAGraph(keep_graph=native)
-        with torch.cuda.graph(graph):
-            out = self._forward_backward(static_in, static_eps, overlap_comm=False)
-            if not self.buckets and update:
-                self._update()
+        comm = None
+        if self.buckets is not None and native:
+            # several ranks: the executor runs the model's streams (main + MAX_SIDE) plus a
+            # comm stream on which each bucket's marker joins that bucket's writers; the
+            # replay issues the bucket's all-reduce there as soon as its range is enqueued
+            from . import model as _model
+            n_streams = min(n_streams, 1 + _model.MAX_SIDE)
+            comm = _model.side_stream(torch.cuda.current_device(), n_streams)
+            self.buckets.comm = comm
+            self.buckets.mark_capture = True
+        try:
+            with torch.cuda.graph(graph):
+                out = self._forward_backward(static_in, static_eps, overlap_comm=False)
+                if not self.buckets and update:
+                    self._update()
+        finally:
+            if self.buckets is not None:
+                self.buckets.mark_capture = False
         out["grad_norm"] = self.norm_out[0]
-        self.captured = CapturedStep(self, graph, static_in, static_eps, out, native=native, n_streams=n_streams)
+        self.captured = CapturedStep(self, graph, static_in, static_eps, out, native=native, n_streams=n_streams,
+                                     comm=comm)
         self.captured.update = update
         return self.captured
 
@@ -379,9 +424,10 @@ class Trainer:
 class CapturedStep:
     """A training step recorded as a hipGraph (Trainer.capture)."""
 
-    def __init__(self, trainer, graph, static_in, static_eps, out, native=False, n_streams=4):
+    def __init__(self, trainer, graph, static_in, static_eps, out, native=False, n_streams=4, comm=None):
         self.trainer, self.graph, self.static_in, self.static_eps, self.out = trainer, graph, static_in, static_eps, out
         self.handle = None
+        self.markers, self.comm = [], comm
         if native:
             import ctypes
             from .model import side_stream
@@ -392,9 +438,24 @@ class CapturedStep:
             # (each bound to its own hardware queue)
             dev = torch.cuda.current_device()
             self.side = [side_stream(dev, i) for i in range(1, n_streams)]
-            self.streams = (ctypes.c_void_p * n_streams)()
+            n_ops, n_mark = ctypes.c_int(), ctypes.c_int()
+            _lib.call("vt_stepgraph_markers", self.handle, ctypes.addressof(n_ops), ctypes.addressof(n_mark), None,
+                      None, 0)
+            if n_mark.value:
+                ends, bks = (ctypes.c_int * n_mark.value)(), (ctypes.c_int * n_mark.value)()
+                _lib.call("vt_stepgraph_markers", self.handle, ctypes.addressof(n_ops), ctypes.addressof(n_mark),
+                          ctypes.addressof(ends), ctypes.addressof(bks), n_mark.value)
+                self.markers = list(zip(list(ends), list(bks)))
+                if comm is None:
+                    raise RuntimeError("captured step holds bucket markers but no comm stream")
+                self.side.append(comm)          # streams[n_streams]: the markers' stream
+            self.n_ops = n_ops.value
+            self.streams = (ctypes.c_void_p * len(self.side + [None]))()
             self._st_addr = ctypes.addressof(self.streams)
             self._destroy = _lib.lib().fns["vt_stepgraph_destroy"]
+
+    def _launch_range(self, begin, end, flags):
+        _lib.call("vt_stepgraph_launch_range", self.handle, self._st_addr, begin, end, flags)
 
     def info(self):
         """(kernels, memcpys, memsets, cross-stream waits) of the native executor's launch list."""
@@ -423,11 +484,26 @@ class CapturedStep:
             st[0] = _lib.stream()
             for i, sd in enumerate(self.side, 1):
                 st[i] = sd.cuda_stream
-            _lib.call("vt_stepgraph_launch", self.handle, self._st_addr)
+            if tr.buckets and self.markers:
+                # DDP overlap: the launch list in ranges; after the range that ends with a
+                # bucket's marker, that bucket's all-reduce on the comm stream, which has
+                # waited for exactly the bucket's gradient writers (the rest of the backward
+                # keeps running on the model's streams)
+                tr.buckets.reset()
+                pos = 0
+                for end, b in self.markers:
+                    self._launch_range(pos, end, 1 if pos == 0 else 0)
+                    with torch.cuda.stream(self.comm):
+                        tr.buckets.launch_bucket(b)
+                    pos = end
+                self._launch_range(pos, self.n_ops, (1 if pos == 0 else 0) | 2)
+            else:
+                _lib.call("vt_stepgraph_launch", self.handle, self._st_addr)
         else:
             self.graph.replay()
         if tr.buckets:
-            tr.buckets.reduce_all()
+            if not (self.handle is not None and self.markers):
+                tr.buckets.reduce_all()
             tr.buckets.finish()
             tr._update()
         elif not getattr(self, "update", True):
