@@ -89,6 +89,10 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
  * its padded column straight from HBM/L2 (faster alone, slower when the phase and cross
  * launches run concurrently).  Initial value from VAETEB_PAIRS_DIRECT; returns the
  * previous setting (not an error code).  Not thread-safe: set before launching. */
+/* pair kernel form on the training geometry: grid > 0 = the persistent kernel with that many
+ * workgroups (a multiple of 8; the default 2 per CU), 0 = one workgroup per item; returns the
+ * previous grid (same bits either way) */
+int vt_fe_set_pairs_persist(int grid);
 int vt_fe_set_pairs_direct(int on);
 
 /* Diagnostic (tools/pairs_phases.py): while buf != NULL, training-geometry vt_fe_pairs
@@ -191,6 +195,19 @@ int vt_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float
  * whole training step can be captured once in a hipGraph and replayed.          */
 int vt_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                       float eps, float weight_decay, int* step, float* coef, const float* gscale, void* stream);
+/* vt_adamw_step_dev + the bf16 shadows of up to 4 2-D weights written by the update itself:
+ * tiled weight h is W [N_h][K_h] at float offset off_h of the flat buffers (off_h a multiple of
+ * 64, N_h and K_h multiples of 64, sorted and disjoint; buffers 16-byte aligned); it is updated
+ * as 64 x 64 tiles that also write W16 [N][K] and W16t [K][N] in bf16 (round to nearest even:
+ * the vt_mfma_weight_shadow images) at the device addresses tiled_w16[h] / tiled_w16t[h]
+ * (host arrays of addresses); everything else as vt_adamw_step_dev.  The same element update
+ * (bits) as vt_adamw_step_dev.  The MFMA heads' forward then needs no shadow pass.
+ * replaces: torch.optim.AdamW.step (ref/model/graph_model.py:654-660, :726) + the 16-bit weight
+ *           casts of autocast in the next forward (:709-711)                                    */
+int vt_adamw_step_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                             float beta2, float eps, float weight_decay, int* step, float* coef, const float* gscale,
+                             int n_tiled, const int64_t* tiled_off, const int* tiled_N, const int* tiled_K,
+                             const int64_t* tiled_w16, const int64_t* tiled_w16t, void* stream);
 /* Tuning switch: 1 (default) = the float4 AdamW kernel when p, g, m, v are all
  * 16-byte aligned, 0 = the scalar kernel.  Same per-element expression: the
  * two give the same bits (tested).  Env override: VAETEB_ADAMW_SCALAR=1.         */
@@ -326,6 +343,10 @@ int vt_conv1d_bn_fwd(const float* X, int B, int L_in, int Cin, const float* W, i
  * step: w16 [Cout][K][ceil32(Cin)] (forward), w16t [Cin][K][ceil32(Cout)]
  * = W[co][ci][K-1-k] (backward-data), zero-padded.                             */
 int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, void* w16t, void* stream);
+/* the same shadows of n <= 24 conv weights in one launch (host arrays; device addresses as int64):
+ * issued by the trainer after its optimizer step, so the next forward needs no shadow launches */
+int vt_conv1d_bf16_shadow_batch(int n, const int64_t* W, const int* Cout, const int* Cin, const int* K,
+                                const int64_t* w16, const int64_t* w16t, void* stream);
 /* Operand-window staging of the bf16 conv kernels (A/B; bit-identical results):
  * 0 octets per lane, 2 lanes along channels (coalesced row segments), 1 (default) lanes
  * along channels for the fused-BN backward-data kernels with K >= 7, octets elsewhere. */

@@ -1,6 +1,8 @@
 """Fused ELBO kernels and the flat AdamW / grad-clip step vs torch fp32/fp64
 references of the same formulas (ref/model/vae_teb_model.py:932-1082,
 ref/model/graph_model.py:654-660,724).  Tolerances are written per assert."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -131,3 +133,49 @@ def test_adamw_vector_equals_scalar(L):
         L.call("vt_adamw_step", p.data_ptr() + 4, g.data_ptr() + 4, m.data_ptr() + 4, v.data_ptr() + 4, n, 1e-3, 0.9,
                0.999, 1e-8, 1e-4, 1, gscale.data_ptr(), L.stream())
         assert torch.equal(p[0], p0[0]) and not torch.equal(p[1:], p0[1:])
+
+
+def test_adamw_writes_bf16_shadows_same_bits():
+    """The optimizer step writing the bf16 weight shadows (tiled AdamW over the 4096^2
+    heads: vt_adamw_step_dev_shadow; the conv shadows in one batched launch) == the forward
+    rewriting them (VAETEB_SHADOW_UPDATE=0), bit for bit over 3 steps at the bench geometry
+    (S = 256, bf16 heads / convs / MLP, B = 2): losses, parameters, Adam moments; and a
+    load_state_dict between steps (the weights change behind the trainer's back) makes the
+    next forward rewrite the shadows (the torch version counter check)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb import ops
+    from vaeteb import train as T
+    from vaeteb.model import SeqVaeTeb
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "model_s256_b2.npz"), allow_pickle=False)
+    C = lambda k: torch.from_numpy(g[k]).cuda()
+    batch = {"fhr_st": C("y_st"), "fhr_ph": C("y_ph"), "fhr_up_ph": C("x_ph"), "fhr": C("y_raw")}
+    res = []
+    prev = T.SHADOW_UPDATE
+    try:
+        for mode in (0, 1):
+            T.SHADOW_UPDATE = mode
+            m = det_fill_(SeqVaeTeb(sequence_length=256, head_precision="bf16", conv_precision="bf16",
+                                    mlp_precision="bf16", concurrent_encoders=True)).cuda()
+            tr = T.Trainer(m, lr=1e-3)
+            losses = [tr.step(batch, eps=C("eps"))["total_loss"].item() for _ in range(3)]
+            if mode:
+                assert tr._shadow_plan()[0] == 4 and tr._shadow_plan()[1] == 17   # 4 heads, 17 convs
+                assert len(ops._FRESH) == 21
+            torch.cuda.synchronize()
+            res.append((losses, tr.state.p.clone(), tr.state.m.clone(), tr.state.v.clone(), m))
+    finally:
+        T.SHADOW_UPDATE = prev
+    assert res[0][0] == res[1][0], (res[0][0], res[1][0])
+    for a, b in zip(res[0][1:4], res[1][1:4]):
+        assert torch.equal(a, b)
+    # weights replaced behind the trainer's back: the fresh shadows must not be used
+    m_old, m_new = res[0][4], res[1][4]
+    with torch.no_grad():
+        m_new.load_state_dict(det_fill_(SeqVaeTeb(sequence_length=256)).state_dict())
+        m_old.load_state_dict(m_new.state_dict())
+        m_old.train(), m_new.train()
+        a = m_new(C("y_st"), C("y_ph"), C("x_ph"), eps=C("eps"))["mu_pr"]
+        b = m_old(C("y_st"), C("y_ph"), C("x_ph"), eps=C("eps"))["mu_pr"]
+    assert torch.equal(a, b)

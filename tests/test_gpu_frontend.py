@@ -242,3 +242,25 @@ def test_frontend_bench_batch_rows_equal_small_batch(fe11):
     torch.cuda.synchronize()
     for k, v in raw_small.items():
         assert torch.equal(raw_big[k][252:], v), k
+
+
+@pytest.mark.parametrize("B", [8, 64])
+def test_pairs_persistent_kernel_bitwise(fe11, B):
+    """k_fe_pairs8k_p (persistent workgroups, the one-wave inverse of item i overlapped with
+    item i+1's product on the other seven waves) == the one-item-per-workgroup kernel, bit for
+    bit; default grid and a small grid (many items per workgroup)."""
+    from vaeteb import _lib, synthetic
+    fns = _lib.lib().fns
+    x = torch.from_numpy(synthetic.batch(5150, B, 4096)).cuda()
+    prev = fns["vt_fe_set_pairs_persist"](0)
+    try:
+        ref = fe11.raw(x)["pairs"].clone()
+        fns["vt_fe_set_pairs_persist"](prev)
+        got = fe11.raw(x)["pairs"].clone()
+        fns["vt_fe_set_pairs_persist"](64)
+        got_small = fe11.raw(x)["pairs"].clone()
+    finally:
+        fns["vt_fe_set_pairs_persist"](prev)
+    torch.cuda.synchronize()
+    assert prev > 0
+    assert torch.equal(got, ref) and torch.equal(got_small, ref)

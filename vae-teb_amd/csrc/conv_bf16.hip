@@ -413,6 +413,40 @@ __global__ void k_conv_shadow(const float* __restrict__ W, int Cout, int Cin, in
     }
 }
 
+// Every bf16 conv weight's shadows in one launch (after the optimizer step, off the next
+// forward's chain): workgroup b -> (weight, 256-element block) by prefix sums; the same
+// element mapping as k_conv_shadow (the same bits).
+constexpr int CSB_MAX = 24;
+struct ConvShadowBatch {
+    int n;
+    const float* W[CSB_MAX];
+    int Cout[CSB_MAX], Cin[CSB_MAX], K[CSB_MAX];
+    __bf16* w16[CSB_MAX];
+    __bf16* w16t[CSB_MAX];
+    int prefix[CSB_MAX + 1];   // workgroups
+};
+__global__ __launch_bounds__(256) void k_conv_shadow_batch(ConvShadowBatch cb) {
+    int h = 0;
+    while (h + 1 < cb.n && (int)blockIdx.x >= cb.prefix[h + 1]) ++h;
+    const int Cout = cb.Cout[h], Cin = cb.Cin[h], K = cb.K[h];
+    const int cin32 = (Cin + 31) / 32 * 32, cout32 = (Cout + 31) / 32 * 32;
+    const int64_t i = (int64_t)(blockIdx.x - cb.prefix[h]) * 256 + threadIdx.x;
+    const float* W = cb.W[h];
+    const int64_t n1 = (int64_t)Cout * K * cin32;
+    if (i < n1) {
+        const int ci = (int)(i % cin32);
+        const int64_t r = i / cin32;
+        const int k = (int)(r % K), co = (int)(r / K);
+        cb.w16[h][i] = (__bf16)(ci < Cin ? W[((int64_t)co * Cin + ci) * K + k] : 0.f);
+    } else if (i < n1 + (int64_t)Cin * K * cout32) {
+        const int64_t j = i - n1;
+        const int co = (int)(j % cout32);
+        const int64_t r = j / cout32;
+        const int k = (int)(r % K), ci = (int)(r / K);
+        cb.w16t[h][j] = (__bf16)(co < Cout ? W[((int64_t)co * Cin + ci) * K + (K - 1 - k)] : 0.f);
+    }
+}
+
 // ------------------------------------------------------------ weight grad
 // dW[co][ci][k] = sum_rows dY[row][co] xpad[row + k][ci] on bf16 MFMA: rows
 // are the MFMA reduction (32 per k-step).  dY rows and the input window are
@@ -874,6 +908,30 @@ int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, v
     hipLaunchKernelGGL(k_conv_shadow, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(stream), W, Cout, Cin, K,
                        cin32, cout32, (__bf16*)w16, (__bf16*)w16t);
     VT_LAUNCH_CHECK("vt_conv1d_bf16_shadow");
+    return VT_OK;
+}
+
+int vt_conv1d_bf16_shadow_batch(int n, const int64_t* W, const int* Cout, const int* Cin, const int* K,
+                                const int64_t* w16, const int64_t* w16t, void* stream) {
+    VT_CHECK_ARG(n >= 0 && n <= CSB_MAX, "vt_conv1d_bf16_shadow_batch: %d weights (at most %d)", n, CSB_MAX);
+    if (n == 0) return VT_OK;
+    ConvShadowBatch cb{};
+    cb.n = n;
+    cb.prefix[0] = 0;
+    for (int h = 0; h < n; ++h) {
+        VT_CHECK_ARG(W[h] && w16[h] && w16t[h] && Cout[h] > 0 && Cin[h] > 0 && K[h] > 0 && K[h] <= KMAXB,
+                     "vt_conv1d_bf16_shadow_batch: weight %d", h);
+        cb.W[h] = reinterpret_cast<const float*>(W[h]);
+        cb.Cout[h] = Cout[h];
+        cb.Cin[h] = Cin[h];
+        cb.K[h] = K[h];
+        cb.w16[h] = reinterpret_cast<__bf16*>(w16[h]);
+        cb.w16t[h] = reinterpret_cast<__bf16*>(w16t[h]);
+        const int64_t e = (int64_t)Cout[h] * K[h] * (cdiv(Cin[h], 32) * 32) + (int64_t)Cin[h] * K[h] * (cdiv(Cout[h], 32) * 32);
+        cb.prefix[h + 1] = cb.prefix[h] + (int)((e + 255) / 256);
+    }
+    hipLaunchKernelGGL(k_conv_shadow_batch, dim3((unsigned)cb.prefix[n]), dim3(256), 0, S(stream), cb);
+    VT_LAUNCH_CHECK("vt_conv1d_bf16_shadow_batch");
     return VT_OK;
 }
 

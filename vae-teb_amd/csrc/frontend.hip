@@ -372,6 +372,137 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
 }
 #undef PR_STAMP
 
+// Persistent form of k_fe_pairs8k<true> (the training geometry): a grid of 2 workgroups per CU,
+// each walking the items L = blockIdx.x, + gridDim.x, ... (gridDim a multiple of 8, so every
+// workgroup stays on one XCD and the XCD-aware order keeps each XCD on consecutive items).
+// The one-wave 512-point inverse (phase 4) of item i runs on wave 0 while waves 1-7 form item
+// i+1's accelerated product (phase 0) in the image, which phase 3 has finished reading — the
+// seven other waves no longer idle through the inverse.  Phases 1-4 are k_fe_pairs8k's, the
+// product's elements are the same: bit-identical outputs.
+static constexpr int PRP_T7 = PR_T - 64;   // threads of waves 1-7
+__device__ __forceinline__ void pr_product_w17(float2* img, const float2* __restrict__ ai,
+                                               const float2* __restrict__ aj, float pw, int t7) {
+#pragma unroll
+    for (int bt = 0; bt < 2; ++bt) {
+        float2 xa[5], xb[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int u = t7 + PRP_T7 * (5 * bt + k);
+            if (bt == 0 || u < 4096) {
+                xa[k] = ai[u];
+                xb[k] = aj[u];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int u = t7 + PRP_T7 * (5 * bt + k);
+            if (bt == 0 || u < 4096) img[u] = F2(pmulc(C2(accel(xa[k], pw)), C2(xb[k])));
+        }
+    }
+}
+
+// (at most 128 VGPRs: two 8-wave workgroups per CU, as the per-item kernel; unconstrained, the
+// compiler hoists the twiddle tables out of the item loop and needs 228)
+__global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_fe_pairs8k_p(
+    const float2* __restrict__ analytic, int n_slots, int n_pairs, int B, const int* __restrict__ slot_i,
+    const int* __restrict__ slot_j, const float* __restrict__ power, const float2* __restrict__ tab,
+    const float* __restrict__ phi0, int start, int S, float* __restrict__ out) {
+    constexpr int N = 4096;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2* img = sm;               // PR_IMG
+    float2* Z = sm + PR_IMG;        // PR_ZP
+    const int t = threadIdx.x, total = n_pairs * B;
+    const int j3 = t & 255, ka = t >> 8, k2_3 = j3 >> 4, kb_3 = j3 & 15;
+    const int k3 = k2_3 + 16 * kb_3 + 256 * ka;
+    const float ph3 = phi0[k3];
+    auto item_of = [&](int L, int& pair, int64_t& b) {
+        const int item = xcd_item(L, total);
+        pair = item % n_pairs;
+        b = item / n_pairs;
+    };
+    int L = blockIdx.x;
+    int pair;
+    int64_t b;
+    item_of(L, pair, b);
+    if (t >= 64)   // the first item's product (wave 0 has no inverse to run yet)
+        pr_product_w17(img, analytic + (b * n_slots + slot_i[pair]) * (int64_t)N,
+                       analytic + (b * n_slots + slot_j[pair]) * (int64_t)N, power[pair], t - 64);
+    for (; L < total; L += gridDim.x) {
+        __syncthreads();   // the product of item L is in img; Z is free (previous inverse done)
+        // an opaque copy of the table pointer per item: the twiddle loads stay inside the loop
+        // (hoisted, they would hold ~60 VGPRs across it and spill)
+        const float2* tb = tab;
+        asm volatile("" : "+s"(tb));
+        c2 v[16];
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) {
+            const int i = t + 512 * n2 - 2048;
+            const int s = n2 < 4 ? -i : (n2 < 12 ? i : 2 * N - 2 - i);
+            v[n2] = C2(img[s]);
+        }
+        __syncthreads();
+        {
+            c2 w[15];
+#pragma unroll
+            for (int k2 = 1; k2 < 16; ++k2) w[k2 - 1] = C2(tb[TW8K_T1 + 512 * (k2 - 1) + t]);
+            pdft16(v);
+            img[pr_pos(t)] = F2(v[0]);
+#pragma unroll
+            for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(t + 512 * k2)] = F2(pmul(v[k2], w[k2 - 1]));
+        }
+        __syncthreads();
+        {
+            const int k2 = t >> 5, n1a = t & 31;
+            float2* base = img + k2 * 528 + n1a;
+            c2 w[15], x[16];
+#pragma unroll
+            for (int kb = 1; kb < 16; ++kb) w[kb - 1] = C2(tb[TW8K_T2 + 32 * (kb - 1) + n1a]);
+#pragma unroll
+            for (int n1b = 0; n1b < 16; ++n1b) x[n1b] = C2(base[33 * n1b]);
+            pdft16(x);
+            base[0] = F2(x[0]);
+#pragma unroll
+            for (int kb = 1; kb < 16; ++kb) base[33 * kb] = F2(pmul(x[kb], w[kb - 1]));
+        }
+        __syncthreads();
+        {
+            const float2* row = img + k2_3 * 528 + 33 * kb_3;
+            c2 x = C2(row[0]);
+            if (ka == 0) {
+#pragma unroll
+                for (int n1a = 1; n1a < 32; ++n1a) x += C2(row[n1a]);
+            } else {
+#pragma unroll
+                for (int n1a = 1; n1a < 32; ++n1a) x = pmac(x, C2(row[n1a]), w32(n1a));
+            }
+            Z[z512_pos(k3)] = make_float2(x.x * ph3, -x.y * ph3);
+        }
+        __syncthreads();   // img is free: waves 1-7 start the next item while wave 0 inverts this one
+        const int Ln = L + (int)gridDim.x;
+        if (t < 64) {   // wave 0 (wave-uniform branches: the register need is the larger, not the sum)
+            c2 r[8];
+            wave_fft512(Z, tb, r);
+            int st_ = start, S_ = S;
+            asm volatile("" : "+s"(st_), "+s"(S_));   // per-item output indices (not hoisted, spilled)
+            float* o = out + (b * n_pairs + pair) * (int64_t)S_;
+            const float inv = 1.0f / (float)PR_NB;
+            const int k0 = (t >> 3) + 8 * (t & 7);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int m = k0 + 64 * j - st_;
+                if (m >= 0 && m < S_) o[m] = r[j].x * inv;
+            }
+        } else if (Ln < total) {
+            int np;
+            int64_t nb;
+            item_of(Ln, np, nb);
+            pr_product_w17(img, analytic + (nb * n_slots + slot_i[np]) * (int64_t)N,
+                           analytic + (nb * n_slots + slot_j[np]) * (int64_t)N, power[np], t - 64);
+        }
+        if (Ln < total) item_of(Ln, pair, b);
+    }
+}
+
 // ------------------------------------------- wavelets, 8192-point register FFT
 // Inverse FFT of xhat * psi for the training geometry (n_pad = 8192) as the
 // forward 16 x 16 x 32 decomposition of the pair kernel on conj(input)
@@ -721,6 +852,23 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
 }
 
 static unsigned long long* g_pairs_stamps = nullptr;  // diagnostic phase stamps (nullptr: off)
+// persistent pair kernel grid (k_fe_pairs8k_p): VAETEB_PAIRS_PERSIST workgroups (a multiple of 8;
+// default 2 per CU; 0 = the one-item-per-workgroup kernel)
+static int g_pairs_persist = -1;
+static int pairs_persist_grid() {
+    if (g_pairs_persist < 0) {
+        const char* e = getenv("VAETEB_PAIRS_PERSIST");
+        int v = e ? atoi(e) : -1;
+        if (v < 0) {
+            int dev = 0, cus = 256;
+            if (hipGetDevice(&dev) == hipSuccess)
+                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            v = 2 * cus;
+        }
+        g_pairs_persist = v / 8 * 8;
+    }
+    return g_pairs_persist;
+}
 static int g_pairs_direct = -1;  // -1: not yet read from VAETEB_PAIRS_DIRECT
 static int pairs_direct() {
     if (g_pairs_direct < 0) {
@@ -732,6 +880,12 @@ static int pairs_direct() {
 
 // Select the pair kernel's product staging on the training geometry (0: LDS-staged
 // product, the default; 1: direct columns).  Returns the previous setting.
+int vt_fe_set_pairs_persist(int grid) {
+    const int prev = pairs_persist_grid();
+    g_pairs_persist = grid > 0 ? grid / 8 * 8 : 0;
+    return prev;
+}
+
 int vt_fe_set_pairs_direct(int on) {
     const int prev = pairs_direct();
     g_pairs_direct = on ? 1 : 0;
@@ -765,6 +919,15 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
         const float2* tab = tw8k_tables(S(stream));
         VT_CHECK_ARG(tab != nullptr, "vt_fe_pairs: twiddle tables unavailable (first call under stream capture?)");
         VT_CHECK_ARG((int64_t)n_pairs * B < (1ll << 31), "vt_fe_pairs: grid");
+        const int64_t total = (int64_t)n_pairs * B;
+        const int pgrid = pairs_persist_grid();
+        if (geo && !direct && g_pairs_stamps == nullptr && pgrid > 0 && total >= 2 * pgrid) {
+            hipLaunchKernelGGL(k_fe_pairs8k_p, dim3((unsigned)pgrid), dim3(PR_T), (PR_IMG + PR_ZP) * sizeof(float2),
+                               S(stream), (const float2*)analytic, n_slots, n_pairs, (int)B, slot_i, slot_j, power, tab,
+                               phi0, start, S_out, out);
+            VT_LAUNCH_CHECK("vt_fe_pairs");
+            return VT_OK;
+        }
         hipLaunchKernelGGL(kern, dim3((unsigned)(n_pairs * B)), dim3(PR_T), (PR_IMG + PR_ZP) * sizeof(float2),
                            S(stream), (const float2*)analytic, n_slots, N, pad_left, n_pairs, (int)B, slot_i, slot_j,
                            power, tab, phi0, start, S_out, pad_mode, out, g_pairs_stamps);

@@ -114,6 +114,20 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw(float* __restrict__ p, co
 // issued before the first use), the < 4 tail elements by the first threads.
 typedef float f32x4n __attribute__((ext_vector_type(4)));
 
+// Ranges of the flat buffers the float4 kernel leaves out (in float4 units, sorted, disjoint):
+// the 2-D weights k_adamw_tile16 updates (with their bf16 shadows).  Index c of the complement
+// maps to the flat float4 index c + the lengths of the ranges starting at or before it.
+constexpr int ADAMW_MAX_SKIP = 8;
+struct AdamwSkip {
+    int n;
+    int64_t start4[ADAMW_MAX_SKIP], len4[ADAMW_MAX_SKIP];
+};
+__device__ __forceinline__ int64_t skip_map(const AdamwSkip& sk, int64_t c) {
+    for (int r = 0; r < sk.n; ++r)
+        if (c >= sk.start4[r]) c += sk.len4[r];
+    return c;
+}
+
 // U float4 of each stream in flight per thread and iteration; NT: the gradient read and the
 // three write-backs as non-temporal accesses (streamed once per step)
 template <int U, bool NT>
@@ -122,13 +136,15 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw4(float* __restrict__ p, c
                                                         float lr, float beta1, float beta2, float eps, float wd,
                                                         float step_size, float bc2_sqrt,
                                                         const float* __restrict__ gscale,
-                                                        const float* __restrict__ coef) {
+                                                        const float* __restrict__ coef, AdamwSkip sk) {
     const AdamwK k = adamw_consts(lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
     float4* p4 = reinterpret_cast<float4*>(p);
     const float4* g4 = reinterpret_cast<const float4*>(g);
     float4* m4 = reinterpret_cast<float4*>(m);
     float4* v4 = reinterpret_cast<float4*>(v);
-    const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t skipped = 0;
+    for (int r = 0; r < sk.n; ++r) skipped += sk.len4[r];
+    const int64_t n4 = (n >> 2) - skipped, stride = (int64_t)gridDim.x * blockDim.x;
     auto upd = [&](float4& pp, const float4& gg, float4& mm, float4& vv) {
         adamw_elem(k, pp.x, gg.x, mm.x, vv.x);
         adamw_elem(k, pp.y, gg.y, mm.y, vv.y);
@@ -150,30 +166,100 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw4(float* __restrict__ p, c
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (; i + (U - 1) * stride < n4; i += U * stride) {
         float4 pa[U], ga[U], ma[U], va[U];
+        int64_t f[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            pa[u] = p4[i + u * stride];
-            ga[u] = ldg(i + u * stride);
-            ma[u] = m4[i + u * stride];
-            va[u] = v4[i + u * stride];
+            f[u] = skip_map(sk, i + u * stride);
+            pa[u] = p4[f[u]];
+            ga[u] = ldg(f[u]);
+            ma[u] = m4[f[u]];
+            va[u] = v4[f[u]];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             upd(pa[u], ga[u], ma[u], va[u]);
-            st4(p4, i + u * stride, pa[u]);
-            st4(m4, i + u * stride, ma[u]);
-            st4(v4, i + u * stride, va[u]);
+            st4(p4, f[u], pa[u]);
+            st4(m4, f[u], ma[u]);
+            st4(v4, f[u], va[u]);
         }
     }
     for (; i < n4; i += stride) {
-        float4 pa = p4[i];
-        const float4 ga = ldg(i);
-        float4 ma = m4[i], va = v4[i];
+        const int64_t f = skip_map(sk, i);
+        float4 pa = p4[f];
+        const float4 ga = ldg(f);
+        float4 ma = m4[f], va = v4[f];
         upd(pa, ga, ma, va);
-        st4(p4, i, pa); st4(m4, i, ma); st4(v4, i, va);
+        st4(p4, f, pa); st4(m4, f, ma); st4(v4, f, va);
     }
-    const int64_t t = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t t = ((n >> 2) << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) adamw_elem(k, p[t], g[t], m[t], v[t]);
+}
+
+// AdamW over 2-D weights W [N][K] (N, K multiples of 64; each 64-float aligned in the flat
+// buffers) as 64 x 64 tiles, writing the bf16 shadows the MFMA GEMMs read — W16 [N][K] and the
+// transposed W16t [K][N] (round to nearest even, as k_bf16_shadow) — from the updated values:
+// the forward then needs no shadow pass.  The same element function as the flat kernels (the
+// same bits); gradient reads and fp32 write-backs non-temporal, the shadows cached (read by the
+// next forward).  Up to 4 weights per launch, workgroup b -> (weight, tile) by prefix sums.
+struct TileHeads {
+    int n;
+    int64_t off[4];
+    int N[4], K[4];
+    int prefix[5];
+    __bf16* w16[4];
+    __bf16* w16t[4];
+};
+__global__ __launch_bounds__(256) void k_adamw_tile16(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, float* __restrict__ v, float lr,
+                                                      float beta1, float beta2, float eps, float wd, float step_size,
+                                                      float bc2_sqrt, const float* __restrict__ gscale,
+                                                      const float* __restrict__ coef, TileHeads th) {
+    __shared__ float tile[64][65];
+    const AdamwK k = adamw_consts(lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
+    int h = 0;
+    while (h + 1 < th.n && (int)blockIdx.x >= th.prefix[h + 1]) ++h;
+    const int t = (int)blockIdx.x - th.prefix[h], K = th.K[h], N = th.N[h], tk = K >> 6;
+    const int64_t n0 = (int64_t)(t / tk) * 64, k0 = (int64_t)(t % tk) * 64;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // float4 column, row within 16
+    const int64_t base = th.off[h] + n0 * K + k0 + 4 * tx;
+    float4 pa[4], ga[4], ma[4], va[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t e = base + (int64_t)(ty + 16 * j) * K;
+        pa[j] = *reinterpret_cast<const float4*>(p + e);
+        const f32x4n x = __builtin_nontemporal_load(reinterpret_cast<const f32x4n*>(g + e));
+        ga[j] = make_float4(x[0], x[1], x[2], x[3]);
+        ma[j] = *reinterpret_cast<const float4*>(m + e);
+        va[j] = *reinterpret_cast<const float4*>(v + e);
+    }
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        adamw_elem(k, pa[j].x, ga[j].x, ma[j].x, va[j].x);
+        adamw_elem(k, pa[j].y, ga[j].y, ma[j].y, va[j].y);
+        adamw_elem(k, pa[j].z, ga[j].z, ma[j].z, va[j].z);
+        adamw_elem(k, pa[j].w, ga[j].w, ma[j].w, va[j].w);
+        const int r = ty + 16 * j;
+        const int64_t e = base + (int64_t)r * K;
+        __builtin_nontemporal_store(f32x4n{pa[j].x, pa[j].y, pa[j].z, pa[j].w}, reinterpret_cast<f32x4n*>(p + e));
+        __builtin_nontemporal_store(f32x4n{ma[j].x, ma[j].y, ma[j].z, ma[j].w}, reinterpret_cast<f32x4n*>(m + e));
+        __builtin_nontemporal_store(f32x4n{va[j].x, va[j].y, va[j].z, va[j].w}, reinterpret_cast<f32x4n*>(v + e));
+        *reinterpret_cast<bf16x4*>(th.w16[h] + (n0 + r) * K + k0 + 4 * tx) =
+            bf16x4{(__bf16)pa[j].x, (__bf16)pa[j].y, (__bf16)pa[j].z, (__bf16)pa[j].w};
+        tile[r][4 * tx] = pa[j].x;
+        tile[r][4 * tx + 1] = pa[j].y;
+        tile[r][4 * tx + 2] = pa[j].z;
+        tile[r][4 * tx + 3] = pa[j].w;
+    }
+    __syncthreads();
+    // W16t row k0 + i, columns n0 + 4 tx .. +3: W[n0 + 4 tx + q][k0 + i]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = ty + 16 * j;
+        *reinterpret_cast<bf16x4*>(th.w16t[h] + (k0 + i) * N + n0 + 4 * tx) =
+            bf16x4{(__bf16)tile[4 * tx][i], (__bf16)tile[4 * tx + 1][i], (__bf16)tile[4 * tx + 2][i],
+                   (__bf16)tile[4 * tx + 3][i]};
+    }
 }
 
 static inline bool aligned16(const void* a) { return ((uintptr_t)a & 15u) == 0; }
@@ -210,21 +296,26 @@ static int g_adamw_vec = -1;  // -1: from VAETEB_ADAMW_SCALAR (unset: vector ker
 
 static void adamw_launch(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                          float eps, float wd, float step_size, float bc2_sqrt, const float* gscale, const float* coef,
-                         hipStream_t st) {
+                         hipStream_t st, const AdamwSkip* skip = nullptr) {
+    AdamwSkip sk{};
+    if (skip) sk = *skip;
+    int64_t skipped4 = 0;
+    for (int r = 0; r < sk.n; ++r) skipped4 += sk.len4[r];
     if (g_adamw_vec < 0) {
         const char* e = getenv("VAETEB_ADAMW_SCALAR");
         g_adamw_vec = (e && e[0] == '1') ? 0 : 1;
     }
-    if (g_adamw_vec && aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v)) {
+    // skipped ranges need the vector kernel (the caller checked the alignment)
+    if ((g_adamw_vec || sk.n > 0) && aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v)) {
         // U float4 per thread and iteration, at most cap x 256 threads (default 4, non-temporal, 2048:
         // 8 per CU; same-box step 8.72-8.75 vs 8.78-9.0 ms with 2 and cached accesses)
         static const int U = getenv("VAETEB_ADAMW_U") ? atoi(getenv("VAETEB_ADAMW_U")) : 4;
         static const int cap = getenv("VAETEB_ADAMW_GRID") ? atoi(getenv("VAETEB_ADAMW_GRID")) : 2048;
         static const bool nt = !(getenv("VAETEB_ADAMW_NT") && getenv("VAETEB_ADAMW_NT")[0] == '0');
-        const dim3 grid(grid_for((n / 4 + 1) / (U == 4 ? 4 : 2), cap > 0 ? cap : 2048));
+        const dim3 grid(grid_for((n / 4 - skipped4 + 1) / (U == 4 ? 4 : 2), cap > 0 ? cap : 2048));
 #define VT_ADAMW4(UU, NN)                                                                                          \
     hipLaunchKernelGGL((k_adamw4<UU, NN>), grid, dim3(OPT_THREADS), 0, st, p, g, m, v, n, lr, beta1, beta2, eps, wd, \
-                       step_size, bc2_sqrt, gscale, coef)
+                       step_size, bc2_sqrt, gscale, coef, sk)
         if (U == 4) {
             if (nt) VT_ADAMW4(4, true); else VT_ADAMW4(4, false);
         } else {
@@ -272,6 +363,46 @@ int vt_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, f
     hipLaunchKernelGGL(k_adamw_coef, dim3(1), dim3(1), 0, S(stream), step, lr, beta1, beta2, coef);
     adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, S(stream));
     VT_LAUNCH_CHECK("vt_adamw_step_dev");
+    return VT_OK;
+}
+
+int vt_adamw_step_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                             float beta2, float eps, float weight_decay, int* step, float* coef, const float* gscale,
+                             int n_tiled, const int64_t* tiled_off, const int* tiled_N, const int* tiled_K,
+                             const int64_t* tiled_w16, const int64_t* tiled_w16t, void* stream) {
+    VT_CHECK_ARG(n > 0 && step && coef && n_tiled >= 0 && n_tiled <= 4, "vt_adamw_step_dev_shadow: args (<= 4 tiled)");
+    VT_CHECK_ARG(aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v),
+                 "vt_adamw_step_dev_shadow: buffers must be 16-byte aligned");
+    AdamwSkip sk{};
+    TileHeads th{};
+    th.n = n_tiled;
+    th.prefix[0] = 0;
+    int64_t prev_end = -1;
+    for (int h = 0; h < n_tiled; ++h) {
+        const int64_t o = tiled_off[h];
+        const int N = tiled_N[h], K = tiled_K[h];
+        VT_CHECK_ARG(o % 64 == 0 && N > 0 && K > 0 && N % 64 == 0 && K % 64 == 0 && o + (int64_t)N * K <= n &&
+                         o >= prev_end && tiled_w16[h] && tiled_w16t[h],
+                     "vt_adamw_step_dev_shadow: tiled weight %d (offset %lld a multiple of 64, N %d / K %d multiples "
+                     "of 64, sorted, disjoint)", h, (long long)o, N, K);
+        prev_end = o + (int64_t)N * K;
+        sk.start4[h] = o / 4;
+        sk.len4[h] = (int64_t)N * K / 4;
+        th.off[h] = o;
+        th.N[h] = N;
+        th.K[h] = K;
+        th.prefix[h + 1] = th.prefix[h] + (N / 64) * (K / 64);
+        th.w16[h] = reinterpret_cast<__bf16*>(tiled_w16[h]);
+        th.w16t[h] = reinterpret_cast<__bf16*>(tiled_w16t[h]);
+    }
+    sk.n = n_tiled;
+    hipStream_t st = S(stream);
+    hipLaunchKernelGGL(k_adamw_coef, dim3(1), dim3(1), 0, st, step, lr, beta1, beta2, coef);
+    if (n_tiled > 0)
+        hipLaunchKernelGGL(k_adamw_tile16, dim3((unsigned)th.prefix[n_tiled]), dim3(256), 0, st, p, g, m, v, lr, beta1,
+                           beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, th);
+    adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, st, &sk);
+    VT_LAUNCH_CHECK("vt_adamw_step_dev_shadow");
     return VT_OK;
 }
 

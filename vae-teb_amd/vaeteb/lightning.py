@@ -84,6 +84,8 @@ class FlatAdamW:
         _lib.call("vt_adamw_step_dev", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(), s.numel,
                   float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
                   self.step_dev.data_ptr(), self.coef.data_ptr(), gscale, _lib.stream())
+        from . import ops
+        ops._FRESH.clear()   # the weights moved without their bf16 shadows: the next forward rewrites them
 
     def state_dict(self):
         return {"param_groups": [dict(g) for g in self.param_groups], "step": self.step_dev.clone(),

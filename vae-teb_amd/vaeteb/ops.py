@@ -113,6 +113,25 @@ _SHADOW = {}
 _PREPARED = {}
 
 
+# Shadows the trainer's optimizer step wrote together with the weights (Trainer._update:
+# vt_adamw_step_dev_shadow / vt_conv1d_bf16_shadow_batch): key -> the weight's torch version
+# counter at that time.  A forward finding its weight here at the same version uses the shadow
+# as it is; any torch-side in-place change of the weight (load_state_dict, copy_) bumps the
+# counter and the shadow is rewritten, and every other optimizer path clears the table.
+_FRESH = {}
+
+
+def mark_fresh(key, w):
+    import weakref
+    _FRESH[key] = (weakref.ref(w), w._version)
+
+
+def _fresh(key, w):
+    # the same tensor object (an address reused by a later model is not a match) at the same version
+    e = _FRESH.get(key)
+    return e is not None and e[0]() is w and e[1] == w._version
+
+
 def _take_prepared(key):
     slot = _PREPARED.pop(key, None)
     if slot is None:
@@ -131,7 +150,7 @@ def _weight_shadow(w, prepass=False):
         sh = (torch.empty((N, K), dtype=torch.bfloat16, device=w.device),
               torch.empty((K, N), dtype=torch.bfloat16, device=w.device))
         _SHADOW[key] = sh
-    if prepass or not _take_prepared(key):
+    if prepass or not (_take_prepared(key) or _fresh(key, w)):
         call("vt_mfma_weight_shadow", ptr(w), N, K, ptr(sh[0]), ptr(sh[1]), _st())
     return sh
 
@@ -440,7 +459,7 @@ def _conv_shadow(w, prepass=False):
         sh = (torch.empty(Cout * K * up32(Cin), dtype=torch.bfloat16, device=w.device),
               torch.empty(Cin * K * up32(Cout), dtype=torch.bfloat16, device=w.device))
         _CONV_SHADOW[key] = sh
-    if prepass or not _take_prepared(key):
+    if prepass or not (_take_prepared(key) or _fresh(key, w)):
         call("vt_conv1d_bf16_shadow", ptr(w), Cout, Cin, K, ptr(sh[0]), ptr(sh[1]), _st())
     return sh
 

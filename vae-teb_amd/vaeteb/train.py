@@ -22,33 +22,48 @@ from . import _lib
 # run the autograd backward on the calling thread instead of autograd's device worker thread
 # (measured: ~1 ms/step less host enqueue; 0 = torch default)
 BWD_SAME_THREAD = int(os.environ.get("VAETEB_BWD_SAME_THREAD", "1"))
+# the optimizer step writes the bf16 shadows of the MFMA heads (tiled AdamW) and of the bf16
+# convs (one batched launch) for the next forward, which then launches no shadow kernels
+# (0 = shadows rewritten by every forward, as before; same bits either way)
+SHADOW_UPDATE = int(os.environ.get("VAETEB_SHADOW_UPDATE", "1"))
+
+
+BIG_ALIGN = 64          # floats: start of every parameter with >= BIG_PARAM elements in the flat buffers
+BIG_PARAM = 1 << 20
 
 
 class FlatState:
     """Flat parameter / gradient / moment storage for a module's parameters.
     Layout is reverse registration order (≈ the order gradients become ready
-    in backward), so the all-reduce buckets fill front to back."""
+    in backward), so the all-reduce buckets fill front to back.  Parameters of
+    >= 2^20 elements (the decoder's R x R heads) start on a 64-float boundary (a few
+    zero padding elements before them: zero gradient, zero update), so the AdamW pass
+    can update them as 2-D tiles and write their bf16 shadows (vt_adamw_step_dev_shadow)
+    while the rest stays 16-byte aligned."""
 
     def __init__(self, module):
         params = [p for p in module.parameters() if p.requires_grad]
         self.params = list(reversed(params))
         dev = self.params[0].device
-        self.numel = sum(p.numel() for p in self.params)
-        self.p = torch.empty(self.numel, device=dev)
+        self.offsets = []
+        o = 0
+        for p in self.params:
+            n = p.numel()
+            if n >= BIG_PARAM:
+                o = (o + BIG_ALIGN - 1) // BIG_ALIGN * BIG_ALIGN
+            self.offsets.append((o, n))
+            o += n
+        self.numel = o
+        self.p = torch.zeros(self.numel, device=dev)
         self.g = torch.zeros(self.numel, device=dev)
         self.m = torch.zeros(self.numel, device=dev)
         self.v = torch.zeros(self.numel, device=dev)
-        self.offsets = []
-        o = 0
         with torch.no_grad():
-            for p in self.params:
-                n = p.numel()
+            for p, (o, n) in zip(self.params, self.offsets):
                 self.p[o:o + n].copy_(p.reshape(-1))
                 p.data = self.p[o:o + n].view_as(p)
                 p.grad = self.g[o:o + n].view_as(p)
                 p._vt_sink = True  # HIP ops accumulate this gradient in place (vaeteb.ops._ParamGrads)
-                self.offsets.append((o, n))
-                o += n
         self._grad_ptrs = [self.g.data_ptr() + 4 * o for o, _ in self.offsets]
 
     def zero_grad(self):
@@ -337,6 +352,41 @@ class Trainer:
         # stream) alive into the next step or a hipGraph capture
         return {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in losses.items()}
 
+    def _shadow_plan(self):
+        """The model's bf16 shadows the optimizer step can write: up to 4 2-D weights
+        (64-float aligned in the flat buffers, both dims multiples of 64: the MFMA heads) for
+        the tiled AdamW, up to 24 conv weights for the batched shadow launch — those whose
+        shadows a forward has created (ops._SHADOW / ops._CONV_SHADOW).  Cached until new
+        shadows appear."""
+        import ctypes
+        from . import ops
+        sig = (len(ops._SHADOW), len(ops._CONV_SHADOW))
+        if getattr(self, "_splan_sig", None) == sig:
+            return self._splan
+        heads, convs = [], []
+        for p, (o, n) in zip(self.state.params, self.state.offsets):
+            key = (p.data_ptr(), *p.shape)
+            if p.dim() == 2 and key in ops._SHADOW and len(heads) < 4:
+                N, K = p.shape
+                if o % 64 == 0 and N % 64 == 0 and K % 64 == 0:
+                    heads.append((o, N, K, ops._SHADOW[key], key, p))
+            elif p.dim() == 3 and key in ops._CONV_SHADOW and len(convs) < 24:
+                convs.append((p, ops._CONV_SHADOW[key], key))
+        I64, I32 = ctypes.c_int64, ctypes.c_int
+        arrs = {
+            "h_off": (I64 * 4)(*[h[0] for h in heads]), "h_N": (I32 * 4)(*[h[1] for h in heads]),
+            "h_K": (I32 * 4)(*[h[2] for h in heads]), "h_w16": (I64 * 4)(*[h[3][0].data_ptr() for h in heads]),
+            "h_w16t": (I64 * 4)(*[h[3][1].data_ptr() for h in heads]),
+            "c_w": (I64 * 24)(*[c[0].data_ptr() for c in convs]), "c_co": (I32 * 24)(*[c[0].shape[0] for c in convs]),
+            "c_ci": (I32 * 24)(*[c[0].shape[1] for c in convs]), "c_k": (I32 * 24)(*[c[0].shape[2] for c in convs]),
+            "c_w16": (I64 * 24)(*[c[1][0].data_ptr() for c in convs]),
+            "c_w16t": (I64 * 24)(*[c[1][1].data_ptr() for c in convs])}
+        addr = {k: ctypes.addressof(v) for k, v in arrs.items()}
+        keys = [(h[4], h[5]) for h in heads] + [(c[2], c[0]) for c in convs]
+        self._splan = (len(heads), len(convs), arrs, addr, keys) if (heads or convs) else None
+        self._splan_sig = sig
+        return self._splan
+
     def _update(self, adam_stream=None):
         """clip_grad_norm_ + AdamW over the flat buffers.  adam_stream: run the AdamW pass
         (memory-bound) on that stream, forked after the norm, so the caller can overlap it
@@ -350,9 +400,24 @@ class Trainer:
         if adam_stream is not None:
             _lib.wait_for(adam_stream, st)
             st = adam_stream.cuda_stream
-        _lib.call("vt_adamw_step_dev", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(), s.numel,
-                  float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
-                  self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4, st)
+        from . import ops
+        plan = self._shadow_plan() if (SHADOW_UPDATE and s.p.is_cuda) else None
+        ops._FRESH.clear()
+        if plan is None:
+            _lib.call("vt_adamw_step_dev", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(), s.numel,
+                      float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
+                      self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4, st)
+            return
+        n_heads, n_convs, _, a, keys = plan
+        _lib.call("vt_adamw_step_dev_shadow", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(),
+                  s.numel, float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps),
+                  float(self.wd), self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4,
+                  n_heads, a["h_off"], a["h_N"], a["h_K"], a["h_w16"], a["h_w16t"], st)
+        if n_convs:
+            _lib.call("vt_conv1d_bf16_shadow_batch", n_convs, a["c_w"], a["c_co"], a["c_ci"], a["c_k"], a["c_w16"],
+                      a["c_w16t"], st)
+        for key, w in keys:
+            ops.mark_fresh(key, w)           # the next forward uses these shadows as they are
 
     # ------------------------------------------------------------ hipGraph
     def capture(self, batch, eps=None, warmup=2, pre_capture=None, native=False, n_streams=4, update=True):
