@@ -135,6 +135,42 @@ def pmc_traffic(kernel):
     return None, None
 
 
+# kernel families of SURVEY.md §8(d)'s "rocprof-reported HBM GB/s for the scattering / conv kernels"
+PMC_FAMILIES = {"conv fwd (k_cfw16, k_conv_bf16)": ("k_cfw16", "k_conv_bf16<"),
+                "conv bwd-data (k_cbd16)": ("k_cbd16",),
+                "conv weight grad (k_cdw16, k_conv_dw_bf16, split sums)": ("k_cdw16", "k_conv_dw_bf16", "k_sum_splits"),
+                "BatchNorm (k_bn_*, k_col_partial4)": ("k_bn_", "k_col_partial4"),
+                "scattering / wavelets (k_fe_wavelet8k, k_fe_spectrum, k_fe_lowpass)": ("k_fe_wavelet8k", "k_fe_spectrum",
+                                                                                         "k_fe_lowpass"),
+                "phase pairs (k_fe_pairs8k*)": ("k_fe_pairs8k",)}
+
+
+def pmc_kernels():
+    """Per-family HBM GB/s of the step's kernels from the latest committed per-kernel PMC file
+    (profiles/r*/pmc_kernels.json: tools/pmc_traffic.py --kernels over separate FETCH_SIZE /
+    WRITE_SIZE passes of this bench; durations = average launches in the timed steps of a
+    kernel trace of the same command, tools/step_stats.py): bytes per step / kernel time per
+    step, and that as a fraction of 8 TB/s."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_kernels.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    out = {}
+    for fam, pats in PMC_FAMILIES.items():
+        byt = ns = 0.0
+        for name, e in d["kernels"].items():
+            if any(p in name for p in pats) and e.get("avg_launch_ns") and e.get("ms_per_step"):
+                launches = e["ms_per_step"] * 1e6 / e["avg_launch_ns"]
+                byt += e["traffic_bytes_per_launch"] * launches
+                ns += e["ms_per_step"] * 1e6
+        if ns:
+            out[fam] = {"hbm_bytes_per_step": round(byt), "kernel_ms_per_step": round(ns / 1e6, 4),
+                        "hbm_GBps": round(byt / ns, 1), "frac": round(byt / ns / HBM_PEAK_GBS, 4)}
+    return {"families": out, "source": os.path.relpath(files[-1], ROOT),
+            "method": "PMC FETCH_SIZE x2 + WRITE_SIZE per launch x launches per timed step / kernel time per step"}
+
+
 def cpu_baseline(frontend_cfg, batch=8, threads=None, classifier=False):
     """Faithful CPU restatement (oracle): front-end called twice per window with
     all 903 pairs then masked (create_hdf5_dataset.py:418-441), torch.fft as in
@@ -317,7 +353,7 @@ def main():
     ddp = world > 1 or args.ddp_probe
     mode = "native" if args.native else ("graph" if args.graph else args.mode)
     if mode == "auto":
-        mode = "native" if (args.workload == "c2" and not (args.prefetch or args.overlap_update)) else "eager"
+        mode = "native" if not (args.prefetch or args.overlap_update) else "eager"
     args.native, args.graph = mode == "native", mode == "graph"
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     torch.cuda.set_device(dev)
@@ -337,8 +373,9 @@ def main():
         # config 4: SeqVaeTebClassifier end to end (freeze_vae=False), the reference's default classifier
         # (filters 32, depth 6, dropout 0.2, attention), total = CE + 0.1 * ELBO(beta 1)
         from vaeteb.classifier import SeqVaeTebClassifier
-        # the captured step would replay the classifier's dropout masks (host-side seeds at capture time)
-        assert not (args.graph or args.native), "--graph / --native are not wired for the classifier workload"
+        # a captured step replays new dropout masks: the classifier advances a device-side seed
+        # offset every training forward (vt_dropout_seed_advance), added to the capture's host seeds
+        assert not args.graph, "--graph is not wired for the classifier workload (use --mode native)"
         model = SeqVaeTebClassifier(sequence_length=S, freeze_vae=False, **vae_kw).to(dev)
     else:
         model = SeqVaeTeb(sequence_length=S, **vae_kw).to(dev)
@@ -377,7 +414,8 @@ def main():
         if args.native:
             eps_shape = (B, S, model.latent_dim_z)
             fe_in_graph = bool(args.fe_in_graph) and not args.overlap_fe
-            caps = [trainer.capture({"x": pool[j]} if fe_in_graph else fe(pool[j]),
+            lab = (lambda j: {"labels": labels[j]}) if c4 else (lambda j: {})
+            caps = [trainer.capture({"x": pool[j], **lab(j)} if fe_in_graph else {**fe(pool[j]), **lab(j)},
                                     eps=torch.randn(eps_shape, device=dev), native=True,
                                     n_streams=args.streams, update=not args.overlap_adam)
                     for j in range(2 if args.overlap_fe else 1)]
@@ -523,7 +561,10 @@ def main():
         fe_timed_in = "eager steps after the timed region (front-end captured in the replayed step)"
     k_ms, k_n = timer.mean_ms("vt_fe_pairs")
     k_bytes = timer.total_flops["vt_fe_pairs"] / max(k_n, 1)   # mean algorithmic bytes per launch
-    traffic, traffic_src = pmc_traffic("k_fe_pairs8k") if (J, Q, T, B) == (11, 4, 16, 256) else (None, None)
+    # the PMC passes ran the default command (native replay, one launch of all pairs per step):
+    # only a run with that launch shape quotes their traffic
+    traffic, traffic_src = (pmc_traffic("k_fe_pairs8k") if (J, Q, T, B) == (11, 4, 16, 256) and args.native
+                            else (None, None))
     achieved = k_bytes / (k_ms * 1e-3) / 1e9
     out = {
         "metric": "train samples/sec + ELBO, 4096-pt windows, batch 256, 1/2/4/8 MI355X",
@@ -576,6 +617,9 @@ def main():
                           "formula": "value x bytes_per_sample / (n_gpus x 8e12); bytes_per_sample = front-end "
                                      "+ 4,161,024 activation elements x 2 B x 4 + 46 B x params / batch"},
     }
+    hbm = pmc_kernels() if (J, Q, T, B) == (11, 4, 16, 256) and not c4 else None
+    if hbm:
+        out["hbm_kernels"] = hbm
     mfma_steps = args.steps
     if graph:
         # the MFMA head GEMMs run inside the graph: time them with HIP events in

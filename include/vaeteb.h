@@ -571,6 +571,12 @@ int vt_add_act_fwd(const float* A, const float* Bm, int64_t n, int act, float* Y
  * channels).  The same call with the same seed is the backward (in place ok).
  * replaces: nn.Dropout / nn.Dropout1d in ref/model/inception_time.py:78,139,209,247,251 */
 int vt_dropout_apply(const float* X, int64_t n, int C, int L, float p, int64_t seed, float* Y, void* stream);
+/* a device uint64 added to every dropout / attention-dropout seed (nullptr: none), and its
+ * per-step advance: a captured step (host seeds frozen at capture) replayed by the native
+ * executor then draws new masks every replay; the forward and the backward of a step read the
+ * same offset (it advances once, at the step's start) */
+int vt_dropout_set_seed_offset(const void* offset);
+int vt_dropout_seed_advance(void* offset, void* stream);
 /* Mean over t of (B, L, C) -> (B, C); backward dX (+)= dY / L broadcast.
  * replaces: AdaptiveAvgPool1d(1) + squeeze (ref/model/inception_time.py:243,320-321) */
 int vt_time_mean_fwd(const float* X, int B, int L, int C, float* Y, void* stream);

@@ -316,8 +316,20 @@ __device__ __forceinline__ uint32_t drop_threshold(float p) {
     return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
+// Device-side seed offset (vt_dropout_set_seed_offset): added to every dropout seed, advanced
+// once per training step on the device (vt_dropout_seed_advance), so a captured step replayed
+// by the native executor draws new masks each replay (its host seeds are frozen at capture).
+__device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* __restrict__ soff) {
+    return soff ? seed + soff[0] : seed;
+}
+
+__global__ void k_seed_advance(uint64_t* off) {
+    if (threadIdx.x == 0) off[0] += 0xD1B54A32D192ED03ull;
+}
+
 __global__ void k_dropout(const float* __restrict__ X, int64_t n, int C, int L, float p, uint64_t seed,
-                          float* __restrict__ Y) {
+                          const uint64_t* __restrict__ soff, float* __restrict__ Y) {
+    seed = eff_seed(seed, soff);
     const uint32_t th = drop_threshold(p);
     const float sc = 1.f / (1.f - p);
     const int64_t LC = (int64_t)L * C;
@@ -388,7 +400,9 @@ constexpr int AKS = DH + 1;       // LDS row stride of K / V
 constexpr int AMAXKT = 16;        // S <= 256
 
 __global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ qkv, int S, int H, float scale, float p,
-                                                  uint64_t seed, float* __restrict__ out, float* __restrict__ lse) {
+                                                  uint64_t seed, const uint64_t* __restrict__ soff,
+                                                  float* __restrict__ out, float* __restrict__ lse) {
+    seed = eff_seed(seed, soff);
     __shared__ float Ks[256 * AKS];
     __shared__ float Vs[256 * AKS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
@@ -474,7 +488,8 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ qkv,
 __global__ __launch_bounds__(256) void k_attn_bwd(const float* __restrict__ qkv, const float* __restrict__ O,
                                                   const float* __restrict__ dO, const float* __restrict__ lse, int S,
                                                   int H, float scale, float p, uint64_t seed,
-                                                  float* __restrict__ dqkv) {
+                                                  const uint64_t* __restrict__ soff, float* __restrict__ dqkv) {
+    seed = eff_seed(seed, soff);
     __shared__ float Ks[256 * AKS];
     __shared__ float Qs[16 * AKS], dOs[16 * AKS];
     __shared__ float dSs[4][16 * 17];
@@ -671,9 +686,24 @@ int vt_add_act_fwd(const float* A, const float* Bm, int64_t n, int act, float* Y
     return VT_OK;
 }
 
+static const uint64_t* g_seed_off = nullptr;
+
+int vt_dropout_set_seed_offset(const void* offset) {
+    g_seed_off = reinterpret_cast<const uint64_t*>(offset);
+    return VT_OK;
+}
+
+int vt_dropout_seed_advance(void* offset, void* stream) {
+    VT_CHECK_ARG(offset != nullptr, "vt_dropout_seed_advance: null offset");
+    hipLaunchKernelGGL(k_seed_advance, dim3(1), dim3(64), 0, S(stream), reinterpret_cast<uint64_t*>(offset));
+    VT_LAUNCH_CHECK("vt_dropout_seed_advance");
+    return VT_OK;
+}
+
 int vt_dropout_apply(const float* X, int64_t n, int C, int L, float p, int64_t seed, float* Y, void* stream) {
     VT_CHECK_ARG(n > 0 && C > 0 && L >= 0 && p >= 0.f && p < 1.f, "vt_dropout_apply: args (0 <= p < 1)");
-    hipLaunchKernelGGL(k_dropout, dim3(ew_blocks(n)), dim3(256), 0, S(stream), X, n, C, L, p, (uint64_t)seed, Y);
+    hipLaunchKernelGGL(k_dropout, dim3(ew_blocks(n)), dim3(256), 0, S(stream), X, n, C, L, p, (uint64_t)seed,
+                       g_seed_off, Y);
     VT_LAUNCH_CHECK("vt_dropout_apply");
     return VT_OK;
 }
@@ -698,7 +728,7 @@ int vt_attn_fwd(const float* qkv, int B, int S_, int H, float scale, float p, in
     VT_CHECK_ARG(B > 0 && H > 0 && S_ > 0 && S_ % 16 == 0 && S_ <= 256 && p >= 0.f && p < 1.f,
                  "vt_attn_fwd: S multiple of 16 <= 256, 0 <= p < 1");
     hipLaunchKernelGGL(k_attn_fwd, dim3(cdiv(S_, 64), B * H), dim3(256), 0, S(stream), qkv, S_, H, scale, p,
-                       (uint64_t)seed, out, lse);
+                       (uint64_t)seed, g_seed_off, out, lse);
     VT_LAUNCH_CHECK("vt_attn_fwd");
     return VT_OK;
 }
@@ -708,7 +738,7 @@ int vt_attn_bwd(const float* qkv, const float* out, const float* dout, const flo
     VT_CHECK_ARG(B > 0 && H > 0 && S_ > 0 && S_ % 16 == 0 && S_ <= 256 && p >= 0.f && p < 1.f,
                  "vt_attn_bwd: S multiple of 16 <= 256, 0 <= p < 1");
     hipLaunchKernelGGL(k_attn_bwd, dim3(B * H), dim3(256), 0, S(stream), qkv, out, dout, lse, S_, H, scale, p,
-                       (uint64_t)seed, dqkv);
+                       (uint64_t)seed, g_seed_off, dqkv);
     VT_LAUNCH_CHECK("vt_attn_bwd");
     return VT_OK;
 }

@@ -23,7 +23,7 @@ import math
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 from ._lib import call, ptr
 from .model import Activation, LayerNorm, Linear, SeqVaeTeb, _BatchNorm, _ConvWeight
 from .ops import ACT, WS, _check, _ParamGrads, _st
@@ -464,6 +464,18 @@ class FHRInceptionTimeClassifier(nn.Module):
 
     def forward(self, x):
         tr = self.training
+        if tr and self.dropout > 0 and x.is_cuda:
+            # a device-side seed offset added to every host-drawn dropout seed.  Eager steps draw
+            # fresh host seeds (torch's CPU generator: torch.manual_seed makes runs repeatable);
+            # a captured step freezes them, so its forward advances the offset on the device
+            # once (a kernel in the graph): every replay draws new masks, and its backward reads
+            # the same offset as its forward
+            off = getattr(self, "_seed_off", None)
+            if off is None or off.device != x.device:
+                self._seed_off = off = torch.zeros(1, dtype=torch.int64, device=x.device)
+            _lib.lib().fns["vt_dropout_set_seed_offset"](off.data_ptr())
+            if torch.cuda.is_current_stream_capturing():
+                call("vt_dropout_seed_advance", off.data_ptr(), _st())
         ip = self.input_projection
         h = ip[0](x)
         h = _ActF.apply(ip[1](h), "gelu")
