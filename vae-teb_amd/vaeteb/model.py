@@ -33,6 +33,9 @@ HEAD_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_HEAD_GRAD_SIDE_STREAM"
 # stream; 0: in line after the chain (measured fastest: GPU-only step 10.22 vs 10.42 ms on stream 3
 # and 10.45 ms per layer in line)
 LSTM_GRAD_SIDE = int(__import__("os").environ.get("VAETEB_LSTM_GRAD_SIDE_STREAM", "0"))
+# DIAGNOSTIC (tools/capture_probe.py): keep the head / LSTM weight-gradient side-stream branches
+# under hipGraph capture too (they are dropped there: DESIGN.md §9, the capture segfault)
+CAPTURE_BRANCHES = __import__("os").environ.get("VAETEB_CAPTURE_BRANCHES", "0") == "1"
 # weight-only forward work (bf16 shadows, BatchNorm counters) on this side stream ahead of a
 # concurrent training forward; 0 (default): shadows in line, counters in one launch
 PREPASS = int(__import__("os").environ.get("VAETEB_PREPASS", "0"))   # measured: GPU-neutral, +1 ms host
@@ -578,12 +581,11 @@ class SeqVaeTeb(nn.Module):
         # until the encoders' backward, long after the heads')
         # (not under hipGraph capture: with that extra branch, ROCm 7's graph
         # instantiation segfaults in hipStreamEndCapture — measured)
+        cap_ok = CAPTURE_BRANCHES or not torch.cuda.is_current_stream_capturing()
         ops.HEAD_GRAD_STREAM = (side_stream(torch.cuda.current_device(), HEAD_GRAD_SIDE)
-                                if _PAR["on"] and HEAD_GRAD_SIDE > 0 and not torch.cuda.is_current_stream_capturing()
-                                else None)
+                                if _PAR["on"] and HEAD_GRAD_SIDE > 0 and cap_ok else None)
         ops.LSTM_GRAD_STREAM = (side_stream(torch.cuda.current_device(), LSTM_GRAD_SIDE)
-                                if _PAR["on"] and LSTM_GRAD_SIDE > 0 and not torch.cuda.is_current_stream_capturing()
-                                else None)
+                                if _PAR["on"] and LSTM_GRAD_SIDE > 0 and cap_ok else None)
         # (not under hipGraph capture: an extra side-stream branch at the start of the graph
         # makes ROCm 7's hipStreamEndCapture segfault, as the head-gradient branch below)
         if getattr(self, "_prepassed", False):
