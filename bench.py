@@ -216,6 +216,19 @@ def cpu_baseline(frontend_cfg, batch=8, threads=None, classifier=False):
                       f"torch threads={threads}, {dt:.1f} s"}
 
 
+OUT = sys.stdout
+
+
+def _json_stdout():
+    """The bench prints ONE JSON line on stdout (rank 0), but native libraries write there too
+    (RCCL's init banner on the first collective): fd 1 is pointed at stderr for the run and the
+    JSON line goes to a duplicate of the original stdout."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(saved, "w")
+
+
 def run_c5(args, rank, world, dev):
     """Config 5 (BASELINE.json configs[4]): long-sequence stress, front-end only —
     Scattering1D(J=8, Q=12, T=256, order 2) on 16384-point windows, batch 64 per
@@ -273,7 +286,7 @@ def run_c5(args, rank, world, dev):
         out["cpu_baseline"] = {"value": round(len(xs) / dtc, 4), "unit": "samples/s", "cores": 1, "kind": "port",
                                "sample": f"oracle numpy Scattering1D order 2 on {len(xs)} of the same windows, {dtc:.1f} s"}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=OUT, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -338,6 +351,8 @@ def main():
                     help="encoder LSTMs: 16-bit MFMA recurrences over 4-sample tiles (f16 forward / bf16 backward "
                          "operands, fp32 state: the reference's own 16-mixed LSTM width) or exact fp32")
     args = ap.parse_args()
+    global OUT
+    OUT = _json_stdout()
 
     if args.ddp_probe and "WORLD_SIZE" not in os.environ:
         import socket
@@ -647,7 +662,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline((J, Q, T), batch=args.cpu_batch, classifier=c4)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=OUT, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -90,8 +90,8 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
  * launches run concurrently).  Initial value from VAETEB_PAIRS_DIRECT; returns the
  * previous setting (not an error code).  Not thread-safe: set before launching. */
 /* pair kernel form on the training geometry: grid > 0 = the persistent kernel with that many
- * workgroups (a multiple of 8; the default 2 per CU), 0 = one workgroup per item; returns the
- * previous grid (same bits either way) */
+ * workgroups (a multiple of 8), -1 = persistent with 2 per CU, 0 = one workgroup per item (the
+ * default: measured faster in the step); returns the previous grid (same bits either way) */
 int vt_fe_set_pairs_persist(int grid);
 int vt_fe_set_pairs_direct(int on);
 

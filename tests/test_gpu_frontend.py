@@ -255,12 +255,11 @@ def test_pairs_persistent_kernel_bitwise(fe11, B):
     prev = fns["vt_fe_set_pairs_persist"](0)
     try:
         ref = fe11.raw(x)["pairs"].clone()
-        fns["vt_fe_set_pairs_persist"](prev)
+        fns["vt_fe_set_pairs_persist"](-1)
         got = fe11.raw(x)["pairs"].clone()
         fns["vt_fe_set_pairs_persist"](64)
         got_small = fe11.raw(x)["pairs"].clone()
     finally:
         fns["vt_fe_set_pairs_persist"](prev)
     torch.cuda.synchronize()
-    assert prev > 0
     assert torch.equal(got, ref) and torch.equal(got_small, ref)

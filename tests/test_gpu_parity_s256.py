@@ -231,8 +231,7 @@ def test_s256_training_trajectory_vs_reference(golden, precision):
     weights.  The bound at step t is therefore an envelope: env(t) = the running maximum
     over steps s <= t of the reference ensemble's deviation from its base fp32 run —
       fp32 (exact kernels): the fp64 run and three one-ulp perturbed fp32 runs;
-          |ours - ref fp32| <= 1e-4 |ref| + 3 env(t)  (steps 0-1: the unperturbed members only,
-          1e-4 relative + 3x the fp64 distance);
+          |ours - ref fp32| <= 1e-4 |ref| + 3 env(t)  (step 0: the fp64 distance only);
       bf16 (the bench precision: bf16 heads / convs / MLP linears, 16-mixed LSTM): those
           and the emulated-bf16-autocast runs (base + two perturbed);
           |ours - ref fp32| <= 1e-4 |ref| + 2 env(t);
@@ -250,9 +249,10 @@ def test_s256_training_trajectory_vs_reference(golden, precision):
         ref = r32(k)
         devs = {m: np.abs(np.asarray(d[f"{m}_{k}"], np.float64) - ref) for m in members}
         dev = np.max(list(devs.values()), axis=0)
-        # steps 0-1 (the first forward, and the forward after one update): only the unperturbed
-        # members (fp64 / emulated bf16), so those steps keep a strict pin
-        dev[:2] = np.max([v for m, v in devs.items() if "_p" not in m], axis=0)[:2]
+        # step 0 (the first forward / backward, at exactly the reference's weights): the fp32
+        # test is held to the fp64 distance only (the one-ulp perturbed fp32 members start from
+        # other weights); from step 1 on, one update's sign noise is in every member
+        dev[0] = max(v[0] for m, v in devs.items() if not m.startswith("fp32_p"))
         env = np.maximum.accumulate(dev)
         err = np.abs(ours[k] - ref)
         bound = 1e-4 * np.abs(ref) + factor * env + 1e-7

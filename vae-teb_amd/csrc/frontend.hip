@@ -853,12 +853,14 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
 
 static unsigned long long* g_pairs_stamps = nullptr;  // diagnostic phase stamps (nullptr: off)
 // persistent pair kernel grid (k_fe_pairs8k_p): VAETEB_PAIRS_PERSIST workgroups (a multiple of 8;
-// default 2 per CU; 0 = the one-item-per-workgroup kernel)
+// -1: 2 per CU).  Default 0 = the one-item-per-workgroup kernel: measured in the bench step,
+// the persistent form is slower (0.932 vs 0.844 ms per launch, round 4) — bit-identical, kept
+// as an option
 static int g_pairs_persist = -1;
 static int pairs_persist_grid() {
     if (g_pairs_persist < 0) {
         const char* e = getenv("VAETEB_PAIRS_PERSIST");
-        int v = e ? atoi(e) : -1;
+        int v = e ? atoi(e) : 0;
         if (v < 0) {
             int dev = 0, cus = 256;
             if (hipGetDevice(&dev) == hipSuccess)
@@ -882,7 +884,12 @@ static int pairs_direct() {
 // product, the default; 1: direct columns).  Returns the previous setting.
 int vt_fe_set_pairs_persist(int grid) {
     const int prev = pairs_persist_grid();
-    g_pairs_persist = grid > 0 ? grid / 8 * 8 : 0;
+    if (grid < 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        grid = 2 * cus;
+    }
+    g_pairs_persist = grid / 8 * 8;
     return prev;
 }
 

@@ -467,8 +467,13 @@ class Trainer:
             comm = _model.side_stream(torch.cuda.current_device(), n_streams)
             self.buckets.comm = comm
             self.buckets.mark_capture = True
+        # several ranks: torch's process-group watchdog thread queries the warmup steps'
+        # collective events while this thread captures; a global-mode capture forbids that
+        # (hipErrorStreamCaptureUnsupported, the watchdog aborts the process), a thread-local
+        # one restricts only this thread
+        mode = "thread_local" if self.buckets is not None else "global"
         try:
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph, capture_error_mode=mode):
                 out = self._forward_backward(static_in, static_eps, overlap_comm=False)
                 if not self.buckets and update:
                     self._update()
