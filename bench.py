@@ -570,7 +570,7 @@ def main():
         # timed region (the same kernels and shapes; profiles/ holds the in-replay durations)
         timer.reset(True)
         for i in range(2):
-            trainer.step({"x": pool[i % 2]})
+            trainer.step({"x": pool[i % 2], **({"labels": labels[i % 2]} if c4 else {})})
         torch.cuda.synchronize()
         timer.enabled = False
         fe_timed_in = "eager steps after the timed region (front-end captured in the replayed step)"
@@ -641,7 +641,7 @@ def main():
         # two extra eager steps after the timed region (same kernels, same shapes)
         timer.reset(True)
         for i in range(2):
-            trainer.step(fe(pool[i % 2]))   # eager, on the default stream
+            trainer.step({**fe(pool[i % 2]), **({"labels": labels[i % 2]} if c4 else {})})   # eager, default stream
         torch.cuda.synchronize()
         timer.enabled = False
         mfma_steps = 2

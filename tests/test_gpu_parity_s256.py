@@ -235,8 +235,9 @@ def test_s256_training_trajectory_vs_reference(golden, precision):
       bf16 (the bench precision: bf16 heads / convs / MLP linears, 16-mixed LSTM): those
           and the emulated-bf16-autocast runs (base + two perturbed);
           |ours - ref fp32| <= 1e-4 |ref| + 2 env(t);
-    for each of the four losses and the pre-clip gradient norm, and the last step's mu_pr
-    within 2x the ensemble's largest deviation at that step."""
+    for each of the four losses at every step, the pre-clip gradient norm while the ensemble
+    agrees within 50 % (the first steps), and the last step's mu_pr within 2x the ensemble's
+    largest deviation at that step."""
     _need_gpu()
     d = golden("traj_s256_b2")
     ours, mu_pr = _traj_run(precision)
@@ -256,9 +257,14 @@ def test_s256_training_trajectory_vs_reference(golden, precision):
         env = np.maximum.accumulate(dev)
         err = np.abs(ours[k] - ref)
         bound = 1e-4 * np.abs(ref) + factor * env + 1e-7
+        # the pre-clip gradient norm is held only while the reference ensemble itself agrees
+        # within 50 % (steps 0-3 or so): later the NLL head's exp(-logvar) makes it swing by
+        # 10-40x between members, and a bound of that size pins nothing
+        held = np.ones_like(err, dtype=bool) if k != "grad_norm" else env < 0.5 * np.abs(ref)
         print(f"{precision} {k}: ours-ref {np.round(err / np.abs(ref), 5).tolist()}\n"
-              f"   bound/|ref| {np.round(bound / np.abs(ref), 5).tolist()}")
-        assert (err <= bound).all(), (k, int(np.argmax(err - bound)), ours[k].tolist(), ref.tolist())
+              f"   bound/|ref| {np.round(bound / np.abs(ref), 5).tolist()}  (held at {int(held.sum())} steps)")
+        assert held[0] and (err <= bound)[held].all(), (k, int(np.argmax((err - bound) * held)), ours[k].tolist(),
+                                                        ref.tolist())
     ref_mu = np.asarray(d["fp32_mu_pr"], np.float64)
     dev = max(rel(np.asarray(d[f"{m}_mu_pr"]), ref_mu) for m in members)
     got = rel(mu_pr, ref_mu)
