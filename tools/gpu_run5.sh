@@ -1,0 +1,8 @@
+#!/bin/bash
+# the whole GPU suite at this tree, smoke, the default bench, then rocprofv3 (+ PMC passes)
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 ; rc=$? ; \
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ; \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err && \
+bash tools/gpu_prof.sh

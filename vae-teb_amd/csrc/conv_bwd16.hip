@@ -119,10 +119,11 @@ struct BdGeo {
     int p_end;    // non-UPF: one past the last padded row computed
 };
 
-template <int K, int NT>
+template <int K, int NT, int PMX = 0>
 struct DCfg {
-    // position blocks per wave: taller tiles for the narrow layers (more MFMA work per staged window)
-    static constexpr int PM = NT <= 2 ? 8 : 2;
+    // position blocks per wave: taller tiles for the narrow layers (more MFMA work per staged window);
+    // PMX overrides (short rows: the encoders' 256 positions fill only half of a 512-row tile)
+    static constexpr int PM = PMX ? PMX : (NT <= 2 ? 8 : 2);
     static constexpr int TC = 16 * NT, TP = 64 * PM, WIN = TP + K - 1;
     static constexpr int WB = K * TC * RS;                       // bf16 elements of one tap chunk
     static constexpr int NWI = (K * TC * 4 + 255) / 256;         // 16-byte tap items per thread
@@ -178,10 +179,10 @@ __device__ __forceinline__ float fold_gup(const float* __restrict__ gp, int gs, 
     return v;
 }
 
-template <int K, int NT, bool UPF>
+template <int K, int NT, bool UPF, int PMX = 0>
 __global__ __launch_bounds__(256) void k_cbd16(const __bf16* __restrict__ d16, BdGeo g,
                                                const __bf16* __restrict__ w16t, float* __restrict__ dx) {
-    using C = DCfg<K, NT>;
+    using C = DCfg<K, NT, PMX>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
     extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
     const int nch = g.nch, c32 = 32 * nch;
@@ -340,6 +341,14 @@ int cbd_nt(const __bf16* d16, BdGeo g, int B, const __bf16* w16t, float* dx, boo
         if (g.TS < 1) return VT_ERR_ARG;
         dim3 grid(cdiv(g.L, g.TS), cdiv(g.Co, C::TC), B);
         hipLaunchKernelGGL((k_cbd16<K, NT, true>), grid, dim3(256), lds, st, d16, g, w16t, dx);
+    } else if (NT <= 2 && g.p_end - g.p_first <= 256) {
+        // short rows (the encoders' L = 256): 128-position tiles, two per sample, every wave
+        // busy (a 512-position tile left half of its waves without rows).  Each output's sum
+        // over chunks and taps is one lane's, in the same order: the same bits
+        using C2 = DCfg<K, NT, 2>;
+        dim3 grid(cdiv(g.p_end - g.p_first, C2::TP), cdiv(g.Co, C2::TC), B);
+        hipLaunchKernelGGL((k_cbd16<K, NT, false, 2>), grid, dim3(256), C2::lds_bytes(g.nch, false), st, d16, g, w16t,
+                           dx);
     } else {
         dim3 grid(cdiv(g.p_end - g.p_first, C::TP), cdiv(g.Co, C::TC), B);
         hipLaunchKernelGGL((k_cbd16<K, NT, false>), grid, dim3(256), lds, st, d16, g, w16t, dx);

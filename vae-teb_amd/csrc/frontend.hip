@@ -58,6 +58,36 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_spectrum(const float* __restr
 }
 
 // ---------------------------------------------------------------- S0 lowpass
+// One workgroup per row (and 256 outputs): the padded row (reflect / zero / circular, as
+// reflect_idx over [0, n_pad)) is staged once in LDS, then each output's 2 radius + 1 taps
+// are read from LDS in the order of k_fe_lowpass (d = -radius .. radius: the same sums and
+// bits); the taps h0[|d|] are wave-uniform (scalar loads).  The per-tap modulo and
+// reflection of k_fe_lowpass made it latency-bound at ~67 us per launch.
+__global__ __launch_bounds__(256) void k_fe_lowpass_lds(const float* __restrict__ x, int64_t x_row_stride, int N,
+                                                        int n_pad, int pad_left, const float* __restrict__ h0,
+                                                        int radius, int step, int start, int S,
+                                                        float* __restrict__ out, int64_t out_row_stride) {
+    extern __shared__ float xp[];   // n_pad
+    const int64_t row = blockIdx.y;
+    const float* xr = x + row * x_row_stride;
+    for (int n = threadIdx.x; n < n_pad; n += 256) xp[n] = xr[reflect_idx(n - pad_left, N)];
+    __syncthreads();
+    const int m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= S) return;
+    const int c = step * (m + start);
+    float acc = 0.f;
+    if (c - radius >= 0 && c + radius < n_pad) {
+        for (int d = -radius; d <= radius; ++d) acc += xp[c - d] * h0[d < 0 ? -d : d];
+    } else {
+        for (int d = -radius; d <= radius; ++d) {
+            int n = (c - d) % n_pad;
+            if (n < 0) n += n_pad;
+            acc += xp[n] * h0[d < 0 ? -d : d];
+        }
+    }
+    out[row * out_row_stride + m] = acc;
+}
+
 __global__ void k_fe_lowpass(const float* __restrict__ x, int64_t x_row_stride, int N, int n_pad, int pad_left,
                              const float* __restrict__ h0, int radius, int step, int start, int S,
                              float* __restrict__ out, int64_t out_row_stride) {
@@ -821,8 +851,12 @@ int vt_fe_lowpass(const float* x, int64_t rows, int64_t x_row_stride, int N, int
                   void* stream) {
     VT_CHECK_ARG(rows > 0 && S_out > 0 && radius >= 0, "vt_fe_lowpass: shape");
     dim3 grid((S_out + 255) / 256, (unsigned)rows);
-    hipLaunchKernelGGL(k_fe_lowpass, grid, dim3(256), 0, S(stream), x, x_row_stride, N, n_pad, pad_left, h0, radius,
-                       step, start, S_out, out, out_row_stride);
+    if ((size_t)n_pad * sizeof(float) <= 64 * 1024)
+        hipLaunchKernelGGL(k_fe_lowpass_lds, grid, dim3(256), (size_t)n_pad * sizeof(float), S(stream), x, x_row_stride,
+                           N, n_pad, pad_left, h0, radius, step, start, S_out, out, out_row_stride);
+    else
+        hipLaunchKernelGGL(k_fe_lowpass, grid, dim3(256), 0, S(stream), x, x_row_stride, N, n_pad, pad_left, h0,
+                           radius, step, start, S_out, out, out_row_stride);
     VT_LAUNCH_CHECK("vt_fe_lowpass");
     return VT_OK;
 }
