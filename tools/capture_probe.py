@@ -13,6 +13,12 @@ first crash, as the GPU-box rules require).
     unjoined         s3 forked and never joined before capture_end
     model_branches   the S=16 model step with the head / LSTM weight-gradient branches kept
                      under capture (VAETEB_CAPTURE_BRANCHES=1, set by this script)
+    model_head       ... the head weight-gradient branch only (side stream 1)
+    model_lstm       ... the LSTM weight-gradient branch only (side stream 2)
+    model_head_norec ... the head branch with Tensor.record_stream disabled
+    model_head_join  ... the head branch joined back to the main stream right after its kernel
+    unjoined_refork  s1 forked, kernel, NOT joined, forked again, kernel, joined (the head
+                     branch's shape: side stream 1 is forked again by the encoders' backward)
 """
 import os
 import sys
@@ -20,13 +26,24 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "vae-teb_amd"), os.path.join(ROOT, "tests")]
 variant = sys.argv[1]
-if variant == "model_branches":
+if variant.startswith("model_"):
     os.environ["VAETEB_CAPTURE_BRANCHES"] = "1"
-    os.environ.setdefault("VAETEB_LSTM_GRAD_SIDE_STREAM", "2")
+    # model_branches: both branches; model_head: the head weight gradients on side stream 1 only
+    # (the production setting, dropped under capture); model_lstm: the LSTM weight gradients on
+    # side stream 2 only
+    os.environ["VAETEB_LSTM_GRAD_SIDE_STREAM"] = "0" if variant.startswith("model_head") else "2"
+    os.environ["VAETEB_HEAD_GRAD_SIDE_STREAM"] = "0" if variant == "model_lstm" else "1"
+    if variant == "model_head_join":
+        os.environ["VAETEB_HEAD_GRAD_JOIN"] = "1"
 
 import torch  # noqa: E402
 
 from vaeteb import _lib  # noqa: E402
+
+if variant == "model_head_norec":
+    # the head branch without Tensor.record_stream (the allocator's cross-stream use
+    # tracking under capture): isolates it as the trigger
+    torch.Tensor.record_stream = lambda self, stream: None
 
 
 def kern(t, s=None):
@@ -40,7 +57,7 @@ def run():
     a = torch.zeros(1 << 16, device=dev)
     b = torch.zeros(1 << 16, device=dev)
     s1, s3 = torch.cuda.Stream(), torch.cuda.Stream()
-    if variant == "model_branches":
+    if variant.startswith("model_"):
         import numpy as np
         from golden_util import det_fill_
         from vaeteb.model import SeqVaeTeb
@@ -80,6 +97,13 @@ def run():
                     kern(b, s1)
                     _lib.wait_for(torch.cuda.current_stream(), s1)
                     kern(a)
+            elif variant == "unjoined_refork":
+                _lib.wait_for(s1)
+                kern(b, s1)                              # left unjoined
+                kern(a)
+                _lib.wait_for(s1)                        # forked again
+                kern(b, s1)
+                _lib.wait_for(torch.cuda.current_stream(), s1)
             elif variant == "external_wait":
                 _lib.wait_mark(ext_slot)
                 kern(a)

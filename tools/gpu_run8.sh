@@ -1,0 +1,7 @@
+#!/bin/bash
+# bisect which library build changes the bf16 bits, then the capture-topology probes (last: may crash)
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
+timeout -k 10 120 python tools/bisect_bits.py > gpurun_out/bis_cur.log 2>&1 && \
+VAETEB_LIB=$GRAFT_REPO_ROOT/tools/probe/bis/lib_norm_old.so timeout -k 10 120 python tools/bisect_bits.py > gpurun_out/bis_norm.log 2>&1 && \
+VAETEB_LIB=$GRAFT_REPO_ROOT/tools/probe/bis/lib_cbd_old.so timeout -k 10 120 python tools/bisect_bits.py > gpurun_out/bis_cbd.log 2>&1 && \
+rm -f gpurun_out/capprobe/summary.txt && PROBE_VARIANTS="model_lstm model_head_norec model_head" bash tools/gpu_capture_probe.sh

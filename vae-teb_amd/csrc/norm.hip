@@ -626,25 +626,7 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
                 a1[e] += dz * h;
             }
         };
-        // four float4 of each stream in flight per thread (the same sequence of f, so the same
-        // accumulation order and bits as one at a time), then the tail one at a time
-        int64_t f = r0 * C + 4 * tid;
-        for (; f + 12 * (int64_t)Tp + 4 <= end; f += 16 * (int64_t)Tp) {
-            float4 xv[4], gv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                xv[u] = *(const float4*)(x + f + 4 * (int64_t)Tp * u);
-                gv[u] = KIND == 2 ? *(const float4*)(dy + f + 4 * (int64_t)Tp * u) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                acc(0, xv[u].x, gv[u].x);
-                acc(1, xv[u].y, gv[u].y);
-                acc(2, xv[u].z, gv[u].z);
-                acc(3, xv[u].w, gv[u].w);
-            }
-        }
-        for (; f < end; f += 4 * Tp) {
+        for (int64_t f = r0 * C + 4 * tid; f < end; f += 4 * Tp) {
             if (f + 4 <= end) {
                 const float4 xv = *(const float4*)(x + f);
                 float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
