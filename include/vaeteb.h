@@ -521,6 +521,25 @@ int vt_lstm16_layer_fwd(const float* x, int In, const float* w_ih, const float* 
  * GradScaler); cell derivatives and dgates fp32.  dgates / dx may be null.          */
 int vt_lstm16_layer_bwd(const float* dh_out, const float* gates, const float* cst, const float* w_hh,
                         const float* w_ih, int In, int B, int S, int hidden, float* dgates, float* dx, void* stream);
+/* Two stacked layers (l with input size In, l + 1 with input size hidden) in one launch:
+ * layer l + 1 runs one 16-step chunk behind layer l in the same workgroup (8 waves, the
+ * chunk's h handed over in LDS), S + 16 steps instead of 2 S.  Outputs are exactly two
+ * vt_lstm16_layer_fwd calls' (out_hprev omitted), bit for bit.  In % 4 == 0, In <= 64;
+ * layer l's input is staged in LDS: seq <= 416 (VAETEB_L16_PAIR_NS=4: <= 208).
+ * replaces: two layers of nn.LSTM(num_layers=4) under torch.amp.autocast
+ *           (vae_teb_model.py:474-480, :647-653)                                   */
+int vt_lstm16_pair_fwd(const float* x, int In, const float* w_ih0, const float* b_ih0, const float* w_hh0,
+                       const float* b_hh0, const float* w_ih1, const float* b_ih1, const float* w_hh1,
+                       const float* b_hh1, int B, int seq, int hidden, float* h0, float* c0, float* gates0, float* h1,
+                       float* c1, float* gates1, void* stream);
+/* Its backward: layer l + 1 (dh_out at its outputs, its forward's gates1 / c1) and layer l
+ * one chunk behind it, layer l + 1's dX handed to layer l in LDS.  dgates1 / dgates0 and
+ * dx (layer l's input gradient [B, S, In0], may be null) are exactly two
+ * vt_lstm16_layer_bwd calls', bit for bit.                                          */
+int vt_lstm16_pair_bwd(const float* dh_out, const float* gates1, const float* c1, const float* w_hh1,
+                       const float* w_ih1, const float* gates0, const float* c0, const float* w_hh0,
+                       const float* w_ih0, int In0, int B, int seq, int hidden, float* dgates1, float* dgates0,
+                       float* dx, void* stream);
 /* All of a layer's parameter gradients in one pass over dgates [B*S, 4H]:
  * dw_ih (+)= dgates^T x, dw_hh (+)= dgates^T h_{t-1}, db_ih and db_hh (may be
  * null) (+)= column sums of dgates.  In + hidden + 1 <= 144; ws: at least
@@ -630,6 +649,10 @@ int vt_stepgraph_destroy(void* handle);
  *   streams[0] first, bit 1 = join every stream into streams[0] after.  A full step is
  *   ranges covering [0, n_ops) in order, the first with bit 0, the last with bit 1.
  *   streams has n_streams + 1 entries when the graph holds markers.                      */
+/* One empty kernel: the last node of a captured step, enqueued on the capture stream after
+ * every side stream has been joined into it (vaeteb.train._join_side_streams), so that the
+ * capture ends on a single node (the capture-end crash).          */
+int vt_capture_tail(void* stream);
 int vt_bucket_marker(int bucket, void* stream);
 int vt_stepgraph_markers(void* handle, int* n_ops, int* n_markers, int* ends, int* buckets, int cap);
 int vt_stepgraph_launch_range(void* handle, void* const* streams, int begin, int end, int flags);

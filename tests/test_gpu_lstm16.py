@@ -257,3 +257,35 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
+
+
+@pytest.mark.parametrize("In,B,S,nl", [(20, 256, 256, 4), (32, 256, 256, 4), (32, 5, 37, 2), (64, 3, 16, 3),
+                                       (20, 2, 1, 2), (32, 7, 300, 4), (8, 4, 33, 2), (20, 3, 17, 2)])
+def test_lstm16_pair_bitwise_per_layer(ops, monkeypatch, In, B, S, nl):
+    """vt_lstm16_pair_fwd / _bwd (two layers per workgroup, the upper one chunk behind) ==
+    the per-layer kernels bit for bit: outputs, dx and every parameter gradient, at the bench
+    geometry (B = 256, S = 256, the encoders' input sizes 20 / 32, 4 layers = 2 pairs), a
+    ragged batch, S = 1, S not a multiple of the chunk, S = 300, and an odd layer count (a
+    pair + one single layer)."""
+    torch.manual_seed(11 + In + S + nl)
+    ref = torch.nn.LSTM(In, 64, nl, batch_first=True)
+    params = [p.detach().cuda() for p in ref.parameters()]
+    x = torch.randn(B, S, In, device="cuda")
+    gy = torch.randn(B, S, 64, device="cuda")
+    outs, names = [], []
+    real_call = ops.call
+    for pair in (0, 1):
+        monkeypatch.setattr(ops, "LSTM_PAIR", pair)
+        called = []
+        monkeypatch.setattr(ops, "call", lambda name, *a: (called.append(name), real_call(name, *a))[1])
+        pd = [p.clone().requires_grad_() for p in params]
+        xd = x.clone().requires_grad_()
+        y = ops.lstm(xd, pd, half=True)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        outs.append([y.detach(), xd.grad] + [p.grad for p in pd])
+        names.append(called)
+    assert "vt_lstm16_pair_fwd" not in names[0] and "vt_lstm16_pair_bwd" not in names[0]
+    assert names[1].count("vt_lstm16_pair_fwd") == nl // 2 and names[1].count("vt_lstm16_pair_bwd") == nl // 2
+    for k, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), (k, (a != b).sum().item(), (a - b).abs().max().item())

@@ -227,6 +227,186 @@ __global__ __launch_bounds__(G4) void k_lstm16_fwd(const float* __restrict__ x, 
     }
 }
 
+// ---------------------------------------------------------------- two layers per workgroup
+// Wavefront pipelining of a layer pair.  The recurrence is a latency
+// chain (~50 instructions per wave and step against ~900 cycles of dependent latency), so one
+// wave per SIMD leaves most issue slots idle.  Here one workgroup of 8 waves carries layers
+// l (role A, waves 0-3) and l + 1 (role B, waves 4-7) of the same NS samples: B runs one
+// 16-step chunk behind A, both step in lockstep under one barrier per step, and each SIMD
+// interleaves an A wave with a B wave.  A's h of a chunk goes to B through an LDS image
+// (16-bit, the A-operand layout of B's input-projection MFMAs) instead of HBM; A's whole
+// input sequence is staged into LDS once, at the start, by coalesced loads (no global loads
+// inside the step loop, so no wait there on the outstanding output stores).  The pair takes
+// S + 16 steps where two layer launches take 2 S; per role the arithmetic is k_lstm16_fwd's
+// (same operands, same MFMA chains, same activation code), so the outputs are bit-identical
+// to two vt_lstm16_layer_fwd calls.
+static constexpr int HX = H + 8;   // f16 row stride of the input images (144 B)
+static constexpr int64_t L16_PAIR_STAGE_MAX = 120 * 1024;   // + ~20 KB static: within 160 KB
+
+// LDS bytes of the staged input of one workgroup (dynamic shared memory)
+__host__ __device__ constexpr int64_t fwd2_stage_bytes(int ns, int S) {
+    return (int64_t)ns * ((S + TC - 1) / TC) * TC * HX * 2;
+}
+
+template <int NS, int KX, int ROLE>
+__device__ __forceinline__ void fwd2_role(int In, const float* __restrict__ wih, const float* __restrict__ bih,
+                                          const float* __restrict__ whh, const float* __restrict__ bhh, int B, int S,
+                                          float* __restrict__ out_h, float* __restrict__ out_c,
+                                          float* __restrict__ gates, _Float16 (*hs)[NS][HS], const _Float16* ximg,
+                                          _Float16 (*himg)[NS][TC][HX]) {
+    const int j = threadIdx.x & (G4 - 1), lane = j & 63, w = j >> 6, ln = lane & 15, lg = lane >> 4;
+    const int u = 16 * w + ln;
+    const int sl = lg & (NS - 1), sa = (ln >> 2) & (NS - 1);
+    const bool wr = NS == 4 || lg < NS;
+    const int b0 = blockIdx.x * NS;
+    const int64_t ob = (int64_t)(b0 + sl < B ? b0 + sl : B - 1) * S;
+    f16x8 bh[4][2];
+    f16x8 bx[4][KX];
+    float bias[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float sc = gate_scale(g);
+        const float* wr_ = whh + (int64_t)(g * H + u) * H;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const float4 p = *reinterpret_cast<const float4*>(wr_ + 32 * ks + 8 * lg);
+            const float4 q = *reinterpret_cast<const float4*>(wr_ + 32 * ks + 8 * lg + 4);
+            bh[g][ks] = to_f16(p * sc, q * sc);
+        }
+        const float* xr = wih + (int64_t)(g * H + u) * In;
+#pragma unroll
+        for (int ks = 0; ks < KX; ++ks) {
+            const int k = 32 * ks + 8 * lg;
+            float4 p = make_float4(0.f, 0.f, 0.f, 0.f), q = p;
+            if (k < In) p = *reinterpret_cast<const float4*>(xr + k);
+            if (k + 4 < In) q = *reinterpret_cast<const float4*>(xr + k + 4);
+            bx[g][ks] = to_f16(p * sc, q * sc);
+        }
+        bias[g] = (bih[g * H + u] + bhh[g * H + u]) * sc;
+    }
+    const int nch = (S + TC - 1) / TC;
+    f32x4 gc[4][4];
+    float c = 0.f;
+    for (int k = 0; k <= nch; ++k) {
+        const int ch = ROLE == 0 ? k : k - 1;   // this role's chunk in period k
+        const bool act = ch >= 0 && ch < nch;   // block-uniform per role
+        const int n = act ? (S - TC * ch < TC ? S - TC * ch : TC) : 0;
+        if (act) {
+            // the chunk's input projection from its 16-bit image: A rows (sample sa, step
+            // 4 m + (ln & 3)), k = 32 ks + 8 lg + e (zero columns past In)
+            const _Float16* im = ROLE == 0 ? ximg + ((int64_t)sa * nch * TC + TC * ch) * HX : &himg[ch & 1][sa][0][0];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                f16x8 xa[KX];
+#pragma unroll
+                for (int ks = 0; ks < KX; ++ks)
+                    xa[ks] = *reinterpret_cast<const f16x8*>(im + (4 * m + (ln & 3)) * HX + 32 * ks + 8 * lg);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    f32x4 acc = f32x4{bias[g], bias[g], bias[g], bias[g]};
+#pragma unroll
+                    for (int ks = 0; ks < KX; ++ks) acc = mma16(xa[ks], bx[g][ks], acc);
+                    gc[m][g] = acc;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+            if (i < n) {
+                const int t = TC * ch + i;
+                const _Float16* hp = &hs[i & 1][sa][8 * lg];
+                const f16x8 a0 = *reinterpret_cast<const f16x8*>(hp);
+                const f16x8 a1 = *reinterpret_cast<const f16x8*>(hp + 32);
+                f32x4 p[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    p[g] = mma16(a0, bh[g][0], gc[i >> 2][g]);
+                    p[g] = mma16(a1, bh[g][1], p[g]);
+                }
+                const int r = i & 3;
+                const float gi = sg2(p[0][r]), gf = sg2(p[1][r]), gg = th2(p[2][r]), go = sg2(p[3][r]);
+                c = cell_fwd_c(c, gi, gf, gg);
+                const float hn = go * th2(2.f * NL2E * c);
+                // (as in k_lstm16_fwd the compiler rounds go * tanh to f16 once, v_fma_mixlo_f16)
+                hs[(i + 1) & 1][sl][u] = (_Float16)hn;
+                if (ROLE == 0) {
+                    // the layer above reads h as the fp32 out_h rounded to f16 (twice rounded):
+                    // an opaque fp32 copy keeps the product from being fused into the conversion
+                    float hq = hn;
+                    asm volatile("" : "+v"(hq));
+                    himg[ch & 1][sl][i][u] = (_Float16)hq;
+                }
+                if (wr) {
+                    *reinterpret_cast<float4*>(gates + ((ob + t) * H + u) * 4) = make_float4(gi, gf, gg, go);
+                    out_h[(ob + t) * H + u] = hn;
+                    out_c[(ob + t) * H + u] = c;
+                }
+            }
+            lds_barrier();
+        }
+    }
+}
+
+// x [B, S, In] (In % 4 == 0, In <= 32 KXA); layer A's outputs hA / cA / gA, layer B's (input
+// size H) hB / cB / gB, as k_lstm16_fwd's (no h_{t-1} output).  Dynamic LDS:
+// fwd2_stage_bytes(NS, S), A's input [NS][ceil16(S)][HX] in f16.
+template <int NS, int KXA>
+__global__ __launch_bounds__(2 * G4) void k_lstm16_fwd2(const float* __restrict__ x, int In,
+                                                        const float* __restrict__ wihA, const float* __restrict__ bihA,
+                                                        const float* __restrict__ whhA, const float* __restrict__ bhhA,
+                                                        const float* __restrict__ wihB, const float* __restrict__ bihB,
+                                                        const float* __restrict__ whhB, const float* __restrict__ bhhB,
+                                                        int B, int S, float* __restrict__ hA, float* __restrict__ cA,
+                                                        float* __restrict__ gA, float* __restrict__ hB,
+                                                        float* __restrict__ cB, float* __restrict__ gB) {
+    __shared__ __attribute__((aligned(16))) _Float16 hsA[2][NS][HS];
+    __shared__ __attribute__((aligned(16))) _Float16 hsB[2][NS][HS];
+    __shared__ __attribute__((aligned(16))) _Float16 himg[2][NS][TC][HX];
+    extern __shared__ __attribute__((aligned(16))) _Float16 ximg[];
+    const int nch = (S + TC - 1) / TC, rows = NS * nch * TC;
+    // zero: the recurrence images (h_{-1} = 0), the staged input (columns past In, steps
+    // past S, samples past B), then the input itself in f16 (the same conversion as
+    // k_lstm16_fwd's operand)
+    for (int i = threadIdx.x; i < 2 * NS * HS; i += 2 * G4) {
+        (&hsA[0][0][0])[i] = (_Float16)0.f;
+        (&hsB[0][0][0])[i] = (_Float16)0.f;
+    }
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    for (int i = threadIdx.x; i < rows * HX / 4; i += 2 * G4)
+        reinterpret_cast<f16x4*>(ximg)[i] = f16x4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+    lds_barrier();
+    {
+        const int i4 = In >> 2, b0 = blockIdx.x * NS;
+        const int per = S * i4, total = NS * per;
+        constexpr int U = 8;
+        for (int q0 = threadIdx.x; q0 < total; q0 += U * 2 * G4) {
+            float4 v[U];
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const int q = q0 + r * 2 * G4;
+                const int s = q / per, rem = q - s * per, t = rem / i4, k4 = rem - t * i4;
+                const int bs = b0 + s < B ? b0 + s : B - 1;
+                v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (q < total) v[r] = *reinterpret_cast<const float4*>(x + ((int64_t)bs * S + t) * In + 4 * k4);
+            }
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const int q = q0 + r * 2 * G4;
+                const int s = q / per, rem = q - s * per, t = rem / i4, k4 = rem - t * i4;
+                if (q < total)
+                    *reinterpret_cast<f16x4*>(ximg + ((int64_t)s * nch * TC + t) * HX + 4 * k4) =
+                        f16x4{(_Float16)v[r].x, (_Float16)v[r].y, (_Float16)v[r].z, (_Float16)v[r].w};
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (threadIdx.x < G4)
+        fwd2_role<NS, KXA, 0>(In, wihA, bihA, whhA, bhhA, B, S, hA, cA, gA, hsA, ximg, himg);
+    else
+        fwd2_role<NS, 2, 1>(H, wihB, bihB, whhB, bhhB, B, S, hB, cB, gB, hsB, ximg, himg);
+}
+
 static constexpr int DS = G4 + 8;   // bf16 row stride of the dg image (528 B)
 
 // gate row of dg-image column k' (k' = 4 u + g: a lane's 4 gate derivatives are one 8-B store)
@@ -401,6 +581,174 @@ __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_
     }
 }
 
+// Backward of a layer pair: role U (waves 0-3) runs layer l + 1's backward recurrence,
+// role L (waves 4-7) layer l's one chunk behind it (both walk the chunks from the last in
+// time to the first).  U's dX = dG W_ih of a chunk — the gradient at layer l's outputs — goes
+// to L through an LDS image (fp32, [NS][TC][H]) instead of HBM; L reads it one step at a
+// time.  Per role the arithmetic is k_lstm16_bwd's instruction for instruction, so dgates of
+// both layers and L's dX are bit-identical to two vt_lstm16_layer_bwd calls.
+template <int NS, int NTX, int ROLE>
+__device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, const float* __restrict__ gates,
+                                          const float* __restrict__ cst, const float* __restrict__ whh,
+                                          const float* __restrict__ wih, int In, int B, int S,
+                                          float* __restrict__ dgates, float* __restrict__ dx,
+                                          __bf16 (*dgs)[TC][NS][DS], float (*dximg)[NS][TC][H],
+                                          __bf16 (*wT)[DS]) {
+    const int j = threadIdx.x & (G4 - 1), lane = j & 63, w = j >> 6, ln = lane & 15, lg = lane >> 4;
+    const int u = 16 * w + ln;
+    const int sl = lg & (NS - 1), sa = (ln >> 2) & (NS - 1);
+    const bool wr = NS == 4 || lg < NS;
+    constexpr int RPS = 16 / NS, MT = TC * NS / 16;
+    const int b0 = blockIdx.x * NS;
+    const int64_t ob = (int64_t)(b0 + sl < B ? b0 + sl : B - 1) * S;
+    bf16x8 bw[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bw[ks][e] = (__bf16)whh[(int64_t)krow(32 * ks + 8 * lg + e) * H + u];
+    // U's dX always (it is L's dh); L's only into a given dx.  The dX B operand (W_ih by
+    // column, bf16, rows k' of the dg image) lives in LDS, not in 32 registers per lane: it is
+    // read once per chunk, and two roles' registers must fit 256 per lane
+    const bool dxw = (ROLE == 0 || dx != nullptr) && w < NTX;   // wave-uniform
+    const int col = 16 * w + ln;
+    for (int e = j; e < H * G4; e += G4) {
+        const int cc_ = e / G4, kk = e - cc_ * G4;
+        wT[cc_][kk] = (__bf16)(cc_ < In && (ROLE == 0 || dx != nullptr) ? wih[(int64_t)krow(kk) * In + cc_] : 0.f);
+    }
+    float4 cg[8], ng[8];
+    float cc[9], nc[9], cd[8], nd[8];
+    auto load_half = [&](int tb) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            int t = tb + k;
+            t = t < S ? t : S - 1;
+            t = t > 0 ? t : 0;
+            ng[k] = *reinterpret_cast<const float4*>(gates + ((ob + t) * H + u) * 4);
+            if (ROLE == 0) nd[k] = dh_out[(ob + t) * H + u];
+            nc[k + 1] = cst[(ob + t) * H + u];
+        }
+        const int tp = tb > 0 ? (tb - 1 < S ? tb - 1 : S - 1) : 0;
+        nc[0] = cst[(ob + tp) * H + u];
+        if (tb <= 0) nc[0] = 0.f;
+    };
+    auto take = [&]() {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            cg[k] = ng[k];
+            if (ROLE == 0) cd[k] = nd[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) cc[k] = nc[k];
+    };
+    f32x4 ax[MT];
+    const int tl0 = ((S - 1) / TC) * TC;
+    const int nch = tl0 / TC + 1;
+    load_half(tl0 + 8);
+    float dc = 0.f;
+    int cur = 0;
+    for (int k = 0; k <= nch; ++k) {
+        const int t0 = ROLE == 0 ? tl0 - TC * k : tl0 - TC * (k - 1);
+        const bool act = t0 >= 0 && t0 <= tl0;   // block-uniform per role
+        const int n = act ? (S - t0 < TC ? S - t0 : TC) : 0;
+        const int xb = (t0 / TC) & 1;             // dX image of this chunk (U writes, L reads)
+#pragma unroll
+        for (int i = TC - 1; i >= 0; --i) {
+            // unconditional (indices clamped; an idle period's values are never used): a
+            // branch here would turn the register hand-over into copies behind a full wait
+            if (i == 15) {
+                take();
+                load_half(t0);
+            }
+            if (i == 7) {
+                take();
+                load_half(t0 - 8);
+            }
+            if (i < n) {
+                const int t = t0 + i, k8 = i & 7;
+                const float dho = ROLE == 0 ? cd[k8] : dximg[xb][sl][i][u];
+                const __bf16* ap = (i + 1 < TC) ? &dgs[cur][i + 1][sa][8 * lg] : &dgs[cur ^ 1][0][sa][8 * lg];
+                bf16x8 af[8];
+#pragma unroll
+                for (int ks = 0; ks < 8; ++ks) af[ks] = *reinterpret_cast<const bf16x8*>(ap + 32 * ks);
+                f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll
+                for (int ks = 0; ks < 8; ks += 2) {
+                    a0 = mmab(af[ks], bw[ks], a0);
+                    a1 = mmab(af[ks + 1], bw[ks + 1], a1);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                const float dh = dho + (a0[0] + a1[0]);
+                float v0, v1, v2, v3;
+                cell_bwd16(dh, cg[k8].x, cg[k8].y, cg[k8].z, cg[k8].w, ftanh(cc[k8 + 1]), cc[k8], dc, v0, v1, v2, v3);
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                *reinterpret_cast<bf16x4*>(&dgs[cur][i][sl][4 * u]) = bf16x4{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3};
+                if (wr) {
+                    float* o = dgates + (ob + t) * G4 + u;
+                    o[0] = v0;
+                    o[H] = v1;
+                    o[2 * H] = v2;
+                    o[3 * H] = v3;
+                }
+            }
+            lds_barrier();
+        }
+        if (dxw) {   // an idle period's burst stores nothing (t >= S) or into an unread image
+            bf16x8 bxw[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) bxw[q] = *reinterpret_cast<const bf16x8*>(&wT[col][32 * q + 8 * lg]);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                ax[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const __bf16* ap = &dgs[cur][m * RPS + ln % RPS][ln / RPS][8 * lg];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) ax[m] = mmab(*reinterpret_cast<const bf16x8*>(ap + 32 * q), bxw[q], ax[m]);
+            }
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 4 * lg + r, sr = row / RPS, tt = m * RPS + row % RPS, t = t0 + tt;
+                    if (ROLE == 0) {
+                        dximg[xb][sr][tt][col] = ax[m][r];
+                    } else if (col < In) {
+                        const int64_t b = b0 + sr < B ? b0 + sr : B - 1;
+                        if (t < S) dx[(b * S + t) * In + col] = ax[m][r];
+                    }
+                }
+        }
+        cur ^= 1;   // (both images start zero: L's first chunk may start on either)
+        lds_barrier();
+    }
+}
+
+// dh_out [B, S, H] at layer l + 1's outputs; gatesU / cU from layer l + 1's forward, gatesL /
+// cL from layer l's; W_hh / W_ih of both; dgU / dgL [B, S, 4H] fp32; dx [B, S, InL] (layer l's
+// input gradient; may be null)
+template <int NS, int NTXL>
+__global__ __launch_bounds__(2 * G4) void k_lstm16_bwd2(const float* __restrict__ dh_out,
+                                                        const float* __restrict__ gatesU, const float* __restrict__ cU,
+                                                        const float* __restrict__ whhU, const float* __restrict__ wihU,
+                                                        const float* __restrict__ gatesL, const float* __restrict__ cL,
+                                                        const float* __restrict__ whhL, const float* __restrict__ wihL,
+                                                        int InL, int B, int S, float* __restrict__ dgU,
+                                                        float* __restrict__ dgL, float* __restrict__ dx) {
+    __shared__ __attribute__((aligned(16))) __bf16 dgsU[2][TC][NS][DS];
+    __shared__ __attribute__((aligned(16))) __bf16 dgsL[2][TC][NS][DS];
+    __shared__ __attribute__((aligned(16))) float dximg[2][NS][TC][H];
+    __shared__ __attribute__((aligned(16))) __bf16 wTU[H][DS];   // W_ih by column (k' = 4 u + g)
+    __shared__ __attribute__((aligned(16))) __bf16 wTL[H][DS];
+    for (int i = threadIdx.x; i < 2 * TC * NS * DS; i += 2 * G4) {
+        (&dgsU[0][0][0][0])[i] = (__bf16)0.f;
+        (&dgsL[0][0][0][0])[i] = (__bf16)0.f;
+    }
+    lds_barrier();
+    if (threadIdx.x < G4)
+        bwd2_role<NS, 4, 0>(dh_out, gatesU, cU, whhU, wihU, H, B, S, dgU, nullptr, dgsU, dximg, wTU);
+    else
+        bwd2_role<NS, NTXL, 1>(nullptr, gatesL, cL, whhL, wihL, InL, B, S, dgL, dx, dgsL, dximg, wTL);
+}
+
 }  // namespace l16
 }  // namespace vt
 
@@ -411,6 +759,11 @@ namespace {
 // samples per workgroup: VAETEB_L16_NS (2 or 4; default 2)
 static int l16_ns() {
     static const int ns = getenv("VAETEB_L16_NS") ? atoi(getenv("VAETEB_L16_NS")) : 2;
+    return ns == 4 ? 4 : 2;
+}
+// samples per workgroup of the layer-pair kernels: VAETEB_L16_PAIR_NS (2 or 4; default 2)
+static int l16_pair_ns() {
+    static const int ns = getenv("VAETEB_L16_PAIR_NS") ? atoi(getenv("VAETEB_L16_PAIR_NS")) : 2;
     return ns == 4 ? 4 : 2;
 }
 // timing probes only (outputs not valid): 1 no stores, 2 in-kernel stamps
@@ -475,6 +828,58 @@ int vt_lstm16_layer_fwd(const float* x, int In, const float* w_ih, const float* 
         else fwd_launch<2, 2>(grid, st, x, In, w_ih, b_ih, w_hh, b_hh, B, seq, out_h, out_hprev, out_c, gates);
     }
     VT_LAUNCH_CHECK("vt_lstm16_layer_fwd");
+    return VT_OK;
+}
+
+int vt_lstm16_pair_fwd(const float* x, int In, const float* w_ih0, const float* b_ih0, const float* w_hh0,
+                       const float* b_hh0, const float* w_ih1, const float* b_ih1, const float* w_hh1,
+                       const float* b_hh1, int B, int seq, int hidden, float* h0, float* c0, float* gates0, float* h1,
+                       float* c1, float* gates1, void* stream) {
+    VT_CHECK_ARG(hidden == H, "vt_lstm16_pair_fwd: hidden size %d (kernel built for %d)", hidden, H);
+    VT_CHECK_ARG(B > 0 && seq > 0 && In > 0 && In <= 64 && In % 4 == 0,
+                 "vt_lstm16_pair_fwd: shape (input size %d: a multiple of 4, at most 64)", In);
+    VT_CHECK_ARG(x && w_ih0 && b_ih0 && w_hh0 && b_hh0 && w_ih1 && b_ih1 && w_hh1 && b_hh1 && h0 && c0 && gates0 &&
+                     h1 && c1 && gates1,
+                 "vt_lstm16_pair_fwd: null pointer");
+    const int ns = l16_pair_ns();
+    const int64_t lds = fwd2_stage_bytes(ns, seq);
+    VT_CHECK_ARG(lds <= L16_PAIR_STAGE_MAX, "vt_lstm16_pair_fwd: sequence length %d too long for the staged input", seq);
+    const dim3 grid((B + ns - 1) / ns);
+    hipStream_t st = vt::S(stream);
+#define VT_L16F2(NS_, KX_)                                                                                          \
+    hipLaunchKernelGGL((k_lstm16_fwd2<NS_, KX_>), grid, dim3(2 * G4), lds, st, x, In, w_ih0, b_ih0, w_hh0, b_hh0, \
+                       w_ih1, b_ih1, w_hh1, b_hh1, B, seq, h0, c0, gates0, h1, c1, gates1)
+    if (ns == 4) {
+        if (In <= 32) VT_L16F2(4, 1);
+        else VT_L16F2(4, 2);
+    } else {
+        if (In <= 32) VT_L16F2(2, 1);
+        else VT_L16F2(2, 2);
+    }
+#undef VT_L16F2
+    VT_LAUNCH_CHECK("vt_lstm16_pair_fwd");
+    return VT_OK;
+}
+
+int vt_lstm16_pair_bwd(const float* dh_out, const float* gates1, const float* c1, const float* w_hh1,
+                       const float* w_ih1, const float* gates0, const float* c0, const float* w_hh0,
+                       const float* w_ih0, int In0, int B, int seq, int hidden, float* dgates1, float* dgates0,
+                       float* dx, void* stream) {
+    VT_CHECK_ARG(hidden == H, "vt_lstm16_pair_bwd: hidden size %d (kernel built for %d)", hidden, H);
+    VT_CHECK_ARG(B > 0 && seq > 0 && In0 > 0 && In0 <= 64, "vt_lstm16_pair_bwd: shape (input size %d, at most 64)",
+                 In0);
+    VT_CHECK_ARG(dh_out && gates1 && c1 && w_hh1 && w_ih1 && gates0 && c0 && w_hh0 && (w_ih0 || !dx) && dgates1 &&
+                     dgates0,
+                 "vt_lstm16_pair_bwd: null pointer");
+    const dim3 grid((B + 1) / 2);
+    hipStream_t st = vt::S(stream);
+    if (In0 <= 32)
+        hipLaunchKernelGGL((k_lstm16_bwd2<2, 2>), grid, dim3(2 * G4), 0, st, dh_out, gates1, c1, w_hh1, w_ih1, gates0,
+                           c0, w_hh0, w_ih0, In0, B, seq, dgates1, dgates0, dx);
+    else
+        hipLaunchKernelGGL((k_lstm16_bwd2<2, 4>), grid, dim3(2 * G4), 0, st, dh_out, gates1, c1, w_hh1, w_ih1, gates0,
+                           c0, w_hh0, w_ih0, In0, B, seq, dgates1, dgates0, dx);
+    VT_LAUNCH_CHECK("vt_lstm16_pair_bwd");
     return VT_OK;
 }
 

@@ -60,6 +60,8 @@ GRAD_READY = None
 SIDE_STREAMS = []   # extra streams the model runs work on (see SeqVaeTeb.concurrent_encoders)
 GRAD_STREAM = None  # side stream for weight gradients off the data-gradient chain (set by SeqVaeTeb)
 HEAD_GRAD_STREAM = None  # ... for the bf16-MFMA decoder-head weight gradients (set by SeqVaeTeb)
+# diagnostic: join the head weight-gradient branch back right after its kernel (capture probe)
+HEAD_GRAD_JOIN = os.environ.get("VAETEB_HEAD_GRAD_JOIN", "0") == "1"
 LSTM_GRAD_STREAM = None  # ... for the LSTM weight gradients (set by SeqVaeTeb)
 # LSTM input projections inside the recurrence kernels (vt_lstm_layer_{fwd,bwd}_x) for
 # input sizes <= 64; 0: separate skinny GEMMs (the same results bit for bit)
@@ -67,6 +69,16 @@ LSTM_FUSED = int(os.environ.get("VAETEB_LSTM_FUSED", "1"))
 # LSTM parameter gradients (in-place sinks) issued after the whole backward recurrence
 # chain (on LSTM_GRAD_STREAM when set) instead of after each layer's recurrence
 LSTM_GRAD_DEFER = int(os.environ.get("VAETEB_LSTM_GRAD_DEFER", "1"))
+# 16-bit LSTM layers two at a time (vt_lstm16_pair_fwd / _bwd: the upper layer one chunk
+# behind the lower in the same workgroup, bit-identical to the per-layer kernels)
+LSTM_PAIR = int(os.environ.get("VAETEB_L16_PAIR", "1"))
+_L16_PAIR_NS = 4 if os.environ.get("VAETEB_L16_PAIR_NS") == "4" else 2
+
+
+def _l16_pair_fits(S):
+    """The pair forward stages its lower layer's input in LDS: NS x ceil16(S) rows of 144 B
+    within 120 KB (csrc/lstm16.hip fwd2_stage_bytes)."""
+    return _L16_PAIR_NS * ((S + 15) // 16) * 16 * 72 * 2 <= 120 * 1024
 # bf16 conv backward-data written straight into dX where the fold is a crop; 0: gpad + fold
 CONV_DIRECT_DX = int(os.environ.get("VAETEB_CONV_DIRECT_DX", "1"))
 # conv-block backward as vt_batchnorm_bwd_x16 + vt_conv1d_bwd_dx16 (bf16 operand written once,
@@ -237,6 +249,8 @@ class LinearF(torch.autograd.Function):
                          ptr(ws_s), ws_s.numel(), _st())
                 gy2.record_stream(side)
                 x2.record_stream(side)
+                if HEAD_GRAD_JOIN:   # diagnostic (tools/capture_probe.py model_head_join)
+                    _lib.wait_for(_lib.stream(), side)
             else:
                 call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(gw_t), ptr(gb_t), pg.acc, ptr(ws),
                      ws.numel(), _st())
@@ -725,20 +739,37 @@ class LSTMF(torch.autograd.Function):
         nl = len(params) // 4
         H = params[1].shape[1]
         saved = []
+        pairs = []   # lower layers of the layer pairs run by vt_lstm16_pair_fwd
         inp = x.contiguous()
-        for l in range(nl):
+        l = 0
+        while l < nl:
             w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
             In = inp.shape[-1]
             h = torch.empty((B, S, H), device=x.device)
             c = torch.empty_like(h)
             gates = torch.empty((B, S, 4 * H), device=x.device)
-            if half and In <= 64 and In % 4 == 0:
+            h16 = half and In <= 64 and In % 4 == 0
+            if h16 and LSTM_PAIR and l + 1 < nl and H <= 64 and _l16_pair_fits(S):
+                # layers l and l + 1 in one launch (the upper one chunk behind the lower)
+                w_ih1, w_hh1, b_ih1, b_hh1 = params[4 * l + 4: 4 * l + 8]
+                h1, c1 = torch.empty_like(h), torch.empty_like(h)
+                gates1 = torch.empty_like(gates)
+                call("vt_lstm16_pair_fwd", ptr(inp), In, ptr(w_ih), ptr(b_ih), ptr(w_hh), ptr(b_hh), ptr(w_ih1),
+                     ptr(b_ih1), ptr(w_hh1), ptr(b_hh1), B, S, H, ptr(h), ptr(c), ptr(gates), ptr(h1), ptr(c1),
+                     ptr(gates1), _st())
+                saved += [inp, h, c, gates, h, h1, c1, gates1]
+                pairs.append(l)
+                inp = h1
+                l += 2
+                continue
+            if h16:
                 # 16-bit MFMA recurrence over sample tiles (f16 operands, fp32 state); no h_{t-1}
                 # output: the weight gradient reads it from h (vt_lstm16_layer_bwd_weight)
                 call("vt_lstm16_layer_fwd", ptr(inp), In, ptr(w_ih), ptr(b_ih), ptr(w_hh), ptr(b_hh), B, S, H, ptr(h),
                      None, ptr(c), ptr(gates), _st())
                 saved += [inp, h, c, gates]
                 inp = h
+                l += 1
                 continue
             hp = torch.empty_like(h)
             if LSTM_FUSED and In <= 64:
@@ -752,10 +783,12 @@ class LSTMF(torch.autograd.Function):
                      ptr(gates), _st())
             saved += [inp, hp, c, gates]
             inp = h
+            l += 1
         ctx.save_for_backward(*saved)
         ctx.params = params
         ctx.nl = nl
         ctx.half = bool(half)
+        ctx.pairs = pairs
         return inp
 
     @staticmethod
@@ -769,12 +802,92 @@ class LSTMF(torch.autograd.Function):
         ws = WS.get(WS_LINEAR, gy.device, 1)
         gx = None
         deferred = []
-        for l in reversed(range(nl)):
-            inp, hp, c, gates = saved[4 * l: 4 * l + 4]
+
+        def wgrad(l, dg, half):
+            """every parameter gradient of layer l from its dgates (in place / deferred / on the
+            weight-gradient side stream, as configured)"""
+            inp, hp = saved[4 * l], saved[4 * l + 1]
             w_ih, w_hh, b_ih, b_hh = params[4 * l: 4 * l + 4]
             In = inp.shape[-1]
-            half = ctx.half and In <= 64 and In % 4 == 0   # hp is then h (read shifted by one step)
             wfn = "vt_lstm16_layer_bwd_weight" if half else "vt_lstm_layer_bwd_weight"
+            if (LSTM_FUSED or half) and In + H + 1 <= 144:
+                # every parameter gradient of the layer in one pass over dg
+                pg = _ParamGrads([w_ih, w_hh, b_ih, b_hh], [True] * 4)
+                if pg.direct and LSTM_GRAD_DEFER:
+                    # in-place sinks: issued after the last layer's recurrence (below), so
+                    # the layer-to-layer dh chain is not interrupted by them
+                    deferred.append((dg, inp, In, hp, pg, wfn))
+                    return
+                side = LSTM_GRAD_STREAM if (pg.direct and LSTM_GRAD_STREAM is not None) else None
+                if side is not None and side.cuda_stream != _lib.stream():
+                    # off the layer-to-layer chain (in-place sinks; same kernels, same bits)
+                    _lib.wait_for(side)
+                    with torch.cuda.stream(side):
+                        ws_s = WS.get(WS_LINEAR, gy.device, 1)
+                        call(wfn, ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                             *[ptr(t) for t in pg.out], pg.acc, ptr(ws_s), ws_s.numel(), _st())
+                    for t in (dg, inp, hp):
+                        t.record_stream(side)
+                else:
+                    call(wfn, ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
+                         *[ptr(t) for t in pg.out], pg.acc, ptr(ws), ws.numel(), _st())
+                grads[4 * l: 4 * l + 4] = pg.result()
+                return
+            pw = _ParamGrads([w_ih, w_hh], [True, True])
+            # b_ih and b_hh receive the same gradient (the sum of dg over rows), written
+            # by one column sum per bias straight into its gradient sink (no device copy:
+            # a memcpy node would not survive the native step executor, csrc/stepgraph.cpp)
+            pb = _ParamGrads([b_ih, b_hh], [True, True])
+            side = LSTM_GRAD_STREAM if (pw.direct and LSTM_GRAD_STREAM is not None) else None
+            if side is not None and side.cuda_stream != _lib.stream():
+                # weight gradients (in-place sinks) off the recurrence chain on a side
+                # stream; the returned bias gradient stays here (same kernels and
+                # summation orders as the serial branch below: bitwise equal)
+                _lib.wait_for(side)
+                with torch.cuda.stream(side):
+                    ws_s = WS.get(WS_LINEAR, gy.device, 1)
+                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
+                         ptr(ws_s), ws_s.numel(), _st())
+                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
+                         ptr(ws_s), ws_s.numel(), _st())
+                for t in (dg, inp, hp):
+                    t.record_stream(side)
+            else:
+                call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
+                     ptr(ws), ws.numel(), _st())
+                call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
+                     ptr(ws), ws.numel(), _st())
+            for gb in pb.out:
+                call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), pb.acc, ptr(ws), ws.numel(), _st())
+            gw_ih, gw_hh = pw.result()
+            grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, *pb.result()]
+
+        l = nl - 1
+        while l >= 0:
+            if l - 1 in ctx.pairs:
+                # layers l (upper) and l - 1 (lower) in one launch: the upper layer's dX goes
+                # to the lower layer through LDS (vt_lstm16_pair_bwd)
+                lo = l - 1
+                inpL, _, cL, gatesL = saved[4 * lo: 4 * lo + 4]
+                _, _, cU, gatesU = saved[4 * l: 4 * l + 4]
+                InL = inpL.shape[-1]
+                dgU = torch.empty((B, S, 4 * H), device=gy.device)
+                dgL = torch.empty_like(dgU)
+                need_dx = lo > 0 or ctx.needs_input_grad[0]
+                gin = torch.empty((B, S, InL), device=gy.device) if need_dx else None
+                call("vt_lstm16_pair_bwd", ptr(dh), ptr(gatesU), ptr(cU), ptr(params[4 * l + 1]), ptr(params[4 * l]),
+                     ptr(gatesL), ptr(cL), ptr(params[4 * lo + 1]), ptr(params[4 * lo]), InL, B, S, H, ptr(dgU),
+                     ptr(dgL), ptr(gin) if need_dx else None, _st())
+                wgrad(l, dgU, True)
+                wgrad(lo, dgL, True)
+                if need_dx:
+                    dh = gx = gin
+                l -= 2
+                continue
+            inp, hp, c, gates = saved[4 * l: 4 * l + 4]
+            w_ih, w_hh = params[4 * l], params[4 * l + 1]
+            In = inp.shape[-1]
+            half = ctx.half and In <= 64 and In % 4 == 0   # hp is then h (read shifted by one step)
             dg = torch.empty((B, S, 4 * H), device=gy.device)
             need_dx = l > 0 or ctx.needs_input_grad[0]
             fused = LSTM_FUSED and In <= 64
@@ -791,60 +904,11 @@ class LSTMF(torch.autograd.Function):
                 call("vt_lstm_layer_bwd", ptr(dh), ptr(gates), ptr(c), ptr(w_hh), B, S, H, ptr(dg), _st())
                 if need_dx:
                     call("vt_linear_bwd_data", ptr(dg), B * S, 4 * H, ptr(w_ih), In, ptr(gin), 0, _st())
-            if (LSTM_FUSED or half) and In + H + 1 <= 144:
-                # every parameter gradient of the layer in one pass over dg
-                pg = _ParamGrads([w_ih, w_hh, b_ih, b_hh], [True] * 4)
-                if pg.direct and LSTM_GRAD_DEFER:
-                    # in-place sinks: issued after the last layer's recurrence (below), so
-                    # the layer-to-layer dh chain is not interrupted by them
-                    deferred.append((dg, inp, In, hp, pg, wfn))
-                else:
-                    side = LSTM_GRAD_STREAM if (pg.direct and LSTM_GRAD_STREAM is not None) else None
-                    if side is not None and side.cuda_stream != _lib.stream():
-                        # off the layer-to-layer chain (in-place sinks; same kernels, same bits)
-                        _lib.wait_for(side)
-                        with torch.cuda.stream(side):
-                            ws_s = WS.get(WS_LINEAR, gy.device, 1)
-                            call(wfn, ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
-                                 *[ptr(t) for t in pg.out], pg.acc, ptr(ws_s), ws_s.numel(), _st())
-                        for t in (dg, inp, hp):
-                            t.record_stream(side)
-                    else:
-                        call(wfn, ptr(dg), ptr(inp), In, ptr(hp), B, S, H,
-                             *[ptr(t) for t in pg.out], pg.acc, ptr(ws), ws.numel(), _st())
-                    grads[4 * l: 4 * l + 4] = pg.result()
-            else:
-                pw = _ParamGrads([w_ih, w_hh], [True, True])
-                # b_ih and b_hh receive the same gradient (the sum of dg over rows), written
-                # by one column sum per bias straight into its gradient sink (no device copy:
-                # a memcpy node would not survive the native step executor, csrc/stepgraph.cpp)
-                pb = _ParamGrads([b_ih, b_hh], [True, True])
-                side = LSTM_GRAD_STREAM if (pw.direct and LSTM_GRAD_STREAM is not None) else None
-                if side is not None and side.cuda_stream != _lib.stream():
-                    # weight gradients (in-place sinks) off the recurrence chain on a side
-                    # stream; the returned bias gradient stays here (same kernels and
-                    # summation orders as the serial branch below: bitwise equal)
-                    _lib.wait_for(side)
-                    with torch.cuda.stream(side):
-                        ws_s = WS.get(WS_LINEAR, gy.device, 1)
-                        call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
-                             ptr(ws_s), ws_s.numel(), _st())
-                        call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
-                             ptr(ws_s), ws_s.numel(), _st())
-                    for t in (dg, inp, hp):
-                        t.record_stream(side)
-                else:
-                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(inp), In, ptr(pw.out[0]), None, pw.acc,
-                         ptr(ws), ws.numel(), _st())
-                    call("vt_linear_bwd_weight", ptr(dg), B * S, 4 * H, ptr(hp), H, ptr(pw.out[1]), None, pw.acc,
-                         ptr(ws), ws.numel(), _st())
-                for gb in pb.out:
-                    call("vt_colsum", ptr(dg), B * S, 4 * H, ptr(gb), pb.acc, ptr(ws), ws.numel(), _st())
-                gw_ih, gw_hh = pw.result()
-                grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, *pb.result()]
+            wgrad(l, dg, half)
             if need_dx:
                 dh = gin
                 gx = gin
+            l -= 1
         if deferred:
             # the layers' parameter gradients after the whole recurrence chain, on the
             # weight-gradient side stream when there is one (joined before the bucket
