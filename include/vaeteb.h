@@ -649,10 +649,6 @@ int vt_stepgraph_destroy(void* handle);
  *   streams[0] first, bit 1 = join every stream into streams[0] after.  A full step is
  *   ranges covering [0, n_ops) in order, the first with bit 0, the last with bit 1.
  *   streams has n_streams + 1 entries when the graph holds markers.                      */
-/* One empty kernel: the last node of a captured step, enqueued on the capture stream after
- * every side stream has been joined into it (vaeteb.train._join_side_streams), so that the
- * capture ends on a single node (the capture-end crash).          */
-int vt_capture_tail(void* stream);
 int vt_bucket_marker(int bucket, void* stream);
 int vt_stepgraph_markers(void* handle, int* n_ops, int* n_markers, int* ends, int* buckets, int cap);
 int vt_stepgraph_launch_range(void* handle, void* const* streams, int begin, int end, int flags);

@@ -477,6 +477,7 @@ class Trainer:
                 out = self._forward_backward(static_in, static_eps, overlap_comm=False)
                 if not self.buckets and update:
                     self._update()
+                _join_side_streams()
         finally:
             if self.buckets is not None:
                 self.buckets.mark_capture = False
@@ -489,6 +490,23 @@ class Trainer:
     def replay(self, batch=None, eps=None):
         """One step of the last captured graph on `batch` (copied into its static inputs)."""
         return self.captured.replay(batch, eps)
+
+
+def _join_side_streams():
+    """before a capture ends, the capture stream waits for every side
+    stream the model forked into it (ops.SIDE_STREAMS, the comm stream included), so no
+    branch can be left unjoined whatever a future fork does.  Streams not in the capture are
+    skipped (a wait on them would be an external dependency)."""
+    from . import ops
+    from ._lib import wait_for
+    cur = torch.cuda.current_stream()
+    for s in ops.SIDE_STREAMS:
+        if s.device != cur.device or s.cuda_stream == cur.cuda_stream:
+            continue
+        with torch.cuda.stream(s):
+            capturing = torch.cuda.is_current_stream_capturing()
+        if capturing:
+            wait_for(cur, s)
 
 
 class CapturedStep:
