@@ -569,3 +569,40 @@ def test_lstm_fused_chunk_handoff_bitwise_fresh_process(ops, tmp_path, In, B, S)
     code = _HANDOFF_SCRIPT.format(pkg=pkg, inp=inp, out=out)
     subprocess.run([sys.executable, "-c", code], check=True, timeout=120)
     assert np.array_equal(np.load(out), y0.cpu().numpy())
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_head_weight_grads_deferred_bitwise(golden, monkeypatch, native):
+    """VAETEB_HEAD_DW_DEFER: the bf16-MFMA heads' weight gradients enqueued at the end of the
+    backward (an autograd-engine callback) instead of between the decoder's data-gradient
+    kernels == in line, bit for bit (eager steps, and the captured step on the native
+    executor, where the heads have no side stream)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb import ops
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    g = golden("model_s16_b4")
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    b0 = {"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}
+    b1 = {k: v.flip(0).contiguous() for k, v in b0.items()}
+    eps0 = T("eps")
+    eps1 = eps0.flip(0).contiguous()
+    res = []
+    for defer in (False, True):
+        monkeypatch.setattr(ops, "HEAD_DW_DEFER", defer)
+        m = det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=True, head_precision="bf16",
+                                conv_precision="bf16", mlp_precision="bf16")).cuda()
+        tr = Trainer(m, lr=1e-3)
+        if native:
+            tr.capture(b0, eps=eps0, warmup=2, native=True)
+            outs = [tr.replay(b, eps=e)["total_loss"].item() for b, e in ((b1, eps1), (b0, eps0))]
+        else:
+            outs = [tr.step(b, eps=e)["total_loss"].item() for b, e in ((b0, eps0), (b1, eps1), (b0, eps0))]
+        torch.cuda.synchronize()
+        assert not ops._DEFERRED
+        res.append((outs, tr.state.p.clone(), tr.state.g.clone()))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, b)

@@ -15,11 +15,12 @@ from vaeteb.train import Trainer  # noqa: E402
 m = det_fill_(SeqVaeTeb(sequence_length=256, head_precision="bf16", conv_precision="bf16", mlp_precision="bf16",
                         lstm_precision="16-mixed", concurrent_encoders=True)).cuda()
 tr = Trainer(m, lr=1e-3)
+B = int(os.environ.get("BISECT_B", "2"))
 out = []
 for t in range(3):
-    y_st, y_ph, x_ph, y_raw, eps = [torch.from_numpy(a).cuda() for a in traj_inputs(256, 2, t)]
+    y_st, y_ph, x_ph, y_raw, eps = [torch.from_numpy(a).cuda() for a in traj_inputs(256, B, t)]
     L = tr.step({"fhr_st": y_st, "fhr_ph": y_ph, "fhr_up_ph": x_ph, "fhr": y_raw}, eps=eps)
     out.append(float(L["nll_loss"]))
 torch.cuda.synchronize()
 g = tr.state.g.double()
-print(os.environ.get("VAETEB_LIB", "in-tree"), out, float(tr.state.p.double().sum()), float(g.abs().sum()))
+print(os.environ.get("VAETEB_LIB", "in-tree"), B, out, float(tr.state.p.double().sum()), float(g.abs().sum()))

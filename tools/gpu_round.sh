@@ -1,5 +1,6 @@
 #!/bin/bash
-# the whole GPU suite at this tree, smoke, the default bench, then rocprofv3 (+ PMC passes)
+# round-end GPU pass at this tree: the whole GPU suite, smoke, the default bench, then
+# rocprofv3 (kernel trace + PMC passes, tools/gpu_prof.sh)
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 ; rc=$? ; \
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ; \
