@@ -25,6 +25,8 @@
 //         mirrors, then the adjoint of the linear upsample with its four fixed weights, in
 //         k_conv_fold's order: the same bits) is applied there; each workgroup owns TS input
 //         rows and computes the 2 TS + pad + 2 padded rows they read.
+#include <stdlib.h>
+
 #include "conv.h"
 
 namespace vt {
@@ -384,8 +386,12 @@ int vt_batchnorm_bwd_x16(const float* dY, const float* Xc, const float* bnp, int
     const int c32 = cdiv(C, 32) * 32;
     const size_t lds = (size_t)8 * ((C + 3) & ~3) * 4 + (size_t)XRB * c32 * 2;
     VT_CHECK_ARG(lds <= 160 * 1024, "vt_batchnorm_bwd_x16: C too large");
+    // at most 8 workgroups per CU of 64-row blocks, each walking several blocks: the per-workgroup
+    // parameter staging (6 C loads + a barrier) is paid once per workgroup, not per block
+    // (the same element computation: the same bits)
     const int64_t blocks = (M + XRB - 1) / XRB;
-    const dim3 grid((unsigned)(blocks < 65536 ? blocks : 65536));
+    static const int cap = getenv("VAETEB_BNX16_GRID") ? atoi(getenv("VAETEB_BNX16_GRID")) : 2048;
+    const dim3 grid((unsigned)(blocks < cap ? blocks : cap));
     const float invM = 1.f / (float)M;
     hipStream_t st = S(stream);
     switch (act) {

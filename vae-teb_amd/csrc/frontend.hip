@@ -70,7 +70,21 @@ __global__ __launch_bounds__(256) void k_fe_lowpass_lds(const float* __restrict_
     extern __shared__ float xp[];   // n_pad
     const int64_t row = blockIdx.y;
     const float* xr = x + row * x_row_stride;
-    for (int n = threadIdx.x; n < n_pad; n += 256) xp[n] = xr[reflect_idx(n - pad_left, N)];
+    // one reflection at most (the training geometry): no modulo; eight loads in flight
+    const bool single = pad_left <= N - 1 && n_pad - pad_left - N <= N - 1;
+    for (int n0 = threadIdx.x; n0 < n_pad; n0 += 256 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int n = n0 + 256 * u;
+            const int i = n - pad_left;
+            const int src = single ? (i < 0 ? -i : (i >= N ? 2 * N - 2 - i : i)) : reflect_idx(i, N);
+            v[u] = n < n_pad ? xr[src] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (n0 + 256 * u < n_pad) xp[n0 + 256 * u] = v[u];
+    }
     __syncthreads();
     const int m = blockIdx.x * 256 + threadIdx.x;
     if (m >= S) return;

@@ -615,35 +615,30 @@ __device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, cons
         const int cc_ = e / G4, kk = e - cc_ * G4;
         wT[cc_][kk] = (__bf16)(cc_ < In && (ROLE == 0 || dx != nullptr) ? wih[(int64_t)krow(kk) * In + cc_] : 0.f);
     }
-    float4 cg[8], ng[8];
-    float cc[9], nc[9], cd[8], nd[8];
-    auto load_half = [&](int tb) {
+    // step inputs of this lane's (sample, unit) by half chunks, in two fixed register sets:
+    // A holds a chunk's upper half (steps 15..8), B its lower half; each is reloaded right
+    // after its last use, 8 steps before its next one (no copies: a register hand-over across
+    // the chunk loop's back edge would wait for the loads in flight)
+    float4 gA[8], gB[8];
+    float cA[9], cB[9], dA[8], dB[8];
+    auto load_half = [&](int tb, float4(&g)[8], float(&c)[9], float(&d)[8]) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             int t = tb + k;
             t = t < S ? t : S - 1;
             t = t > 0 ? t : 0;
-            ng[k] = *reinterpret_cast<const float4*>(gates + ((ob + t) * H + u) * 4);
-            if (ROLE == 0) nd[k] = dh_out[(ob + t) * H + u];
-            nc[k + 1] = cst[(ob + t) * H + u];
+            g[k] = *reinterpret_cast<const float4*>(gates + ((ob + t) * H + u) * 4);
+            if (ROLE == 0) d[k] = dh_out[(ob + t) * H + u];
+            c[k + 1] = cst[(ob + t) * H + u];
         }
+        // c_{tb-1} (c_{-1} = 0 is applied at the use: a select here would wait for the load)
         const int tp = tb > 0 ? (tb - 1 < S ? tb - 1 : S - 1) : 0;
-        nc[0] = cst[(ob + tp) * H + u];
-        if (tb <= 0) nc[0] = 0.f;
-    };
-    auto take = [&]() {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            cg[k] = ng[k];
-            if (ROLE == 0) cd[k] = nd[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 9; ++k) cc[k] = nc[k];
+        c[0] = cst[(ob + tp) * H + u];
     };
     f32x4 ax[MT];
     const int tl0 = ((S - 1) / TC) * TC;
     const int nch = tl0 / TC + 1;
-    load_half(tl0 + 8);
+    load_half(tl0 + 8, gA, cA, dA);
     float dc = 0.f;
     int cur = 0;
     for (int k = 0; k <= nch; ++k) {
@@ -653,19 +648,14 @@ __device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, cons
         const int xb = (t0 / TC) & 1;             // dX image of this chunk (U writes, L reads)
 #pragma unroll
         for (int i = TC - 1; i >= 0; --i) {
-            // unconditional (indices clamped; an idle period's values are never used): a
-            // branch here would turn the register hand-over into copies behind a full wait
-            if (i == 15) {
-                take();
-                load_half(t0);
-            }
-            if (i == 7) {
-                take();
-                load_half(t0 - 8);
-            }
+            // unconditional (indices clamped; an idle period's values are never used)
+            if (i == 15) load_half(t0, gB, cB, dB);
+            if (i == 7) load_half(t0 - 8, gA, cA, dA);
             if (i < n) {
                 const int t = t0 + i, k8 = i & 7;
-                const float dho = ROLE == 0 ? cd[k8] : dximg[xb][sl][i][u];
+                const float4 gq = i >= 8 ? gA[k8] : gB[k8];
+                const float c1 = i >= 8 ? cA[k8 + 1] : cB[k8 + 1], c0 = t > 0 ? (i >= 8 ? cA[k8] : cB[k8]) : 0.f;
+                const float dho = ROLE == 0 ? (i >= 8 ? dA[k8] : dB[k8]) : dximg[xb][sl][i][u];
                 const __bf16* ap = (i + 1 < TC) ? &dgs[cur][i + 1][sa][8 * lg] : &dgs[cur ^ 1][0][sa][8 * lg];
                 bf16x8 af[8];
 #pragma unroll
@@ -680,7 +670,7 @@ __device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, cons
                 __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
                 const float dh = dho + (a0[0] + a1[0]);
                 float v0, v1, v2, v3;
-                cell_bwd16(dh, cg[k8].x, cg[k8].y, cg[k8].z, cg[k8].w, ftanh(cc[k8 + 1]), cc[k8], dc, v0, v1, v2, v3);
+                cell_bwd16(dh, gq.x, gq.y, gq.z, gq.w, ftanh(c1), c0, dc, v0, v1, v2, v3);
                 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
                 *reinterpret_cast<bf16x4*>(&dgs[cur][i][sl][4 * u]) = bf16x4{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3};
                 if (wr) {

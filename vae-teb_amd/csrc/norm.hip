@@ -626,17 +626,59 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
                 a1[e] += dz * h;
             }
         };
-        for (int64_t f = r0 * C + 4 * tid; f < end; f += 4 * Tp) {
+        // KIND < 2 or ACT <= 1: the arithmetic spelled out (contraction off, fmaf where the
+        // one-at-a-time loop compiled to an fma: KIND 1 d*d + a0; KIND 2 g act' + a0 and
+        // h (g act') + a1 — act' is 0 or 1 for ACT <= 1, so every product there is exact),
+        // four float4 of each stream in flight per thread over the same sequence of f: the
+        // sums and their bits do not depend on the unrolling or on the compiler's choices
+        constexpr bool PIN = KIND < 2 || ACT <= 1;
+        auto acc4 = [&](int e, float v, float g) {
+#pragma clang fp contract(off)
+            if (KIND == 0) {
+                a0[e] = a0[e] + v;
+            } else if (KIND == 1) {
+                const float d = v - mu[e];
+                a0[e] = fmaf(d, d, a0[e]);
+            } else {
+                const float h = (v - mu[e]) * rs[e];
+                const float ad = act_d(fmaf(h, ga[e], be[e]), ACT);
+                a0[e] = fmaf(g, ad, a0[e]);
+                a1[e] = fmaf(h, g * ad, a1[e]);
+            }
+        };
+        auto accx = [&](int e, float v, float g) {
+            if constexpr (PIN) acc4(e, v, g);
+            else acc(e, v, g);
+        };
+        int64_t f = r0 * C + 4 * tid;
+        if constexpr (PIN) {
+            for (; f + 12 * (int64_t)Tp + 4 <= end; f += 16 * (int64_t)Tp) {
+                float4 xv[4], gv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    xv[u] = *(const float4*)(x + f + 4 * (int64_t)Tp * u);
+                    gv[u] = KIND == 2 ? *(const float4*)(dy + f + 4 * (int64_t)Tp * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc4(0, xv[u].x, gv[u].x);
+                    acc4(1, xv[u].y, gv[u].y);
+                    acc4(2, xv[u].z, gv[u].z);
+                    acc4(3, xv[u].w, gv[u].w);
+                }
+            }
+        }
+        for (; f < end; f += 4 * Tp) {
             if (f + 4 <= end) {
                 const float4 xv = *(const float4*)(x + f);
                 float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (KIND == 2) gv = *(const float4*)(dy + f);
-                acc(0, xv.x, gv.x);
-                acc(1, xv.y, gv.y);
-                acc(2, xv.z, gv.z);
-                acc(3, xv.w, gv.w);
+                accx(0, xv.x, gv.x);
+                accx(1, xv.y, gv.y);
+                accx(2, xv.z, gv.z);
+                accx(3, xv.w, gv.w);
             } else {
-                for (int e = 0; e < (int)(end - f); ++e) acc(e, x[f + e], KIND == 2 ? dy[f + e] : 0.f);
+                for (int e = 0; e < (int)(end - f); ++e) accx(e, x[f + e], KIND == 2 ? dy[f + e] : 0.f);
             }
         }
     }

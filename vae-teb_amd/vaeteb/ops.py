@@ -60,6 +60,27 @@ GRAD_READY = None
 SIDE_STREAMS = []   # extra streams the model runs work on (see SeqVaeTeb.concurrent_encoders)
 GRAD_STREAM = None  # side stream for weight gradients off the data-gradient chain (set by SeqVaeTeb)
 HEAD_GRAD_STREAM = None  # ... for the bf16-MFMA decoder-head weight gradients (set by SeqVaeTeb)
+# decoder-head weight gradients (bf16 MFMA, in-place sinks) enqueued at the end of the backward
+# when they have no side stream (VAETEB_HEAD_DW_DEFER=1)
+HEAD_DW_DEFER = os.environ.get("VAETEB_HEAD_DW_DEFER", "0") == "1"
+_DEFERRED = []
+
+
+def _flush_deferred():
+    """Run the work deferred to the end of this backward pass, in the order it was deferred
+    (an autograd engine callback, queued by the first deferral of a pass)."""
+    work = list(_DEFERRED)
+    _DEFERRED.clear()
+    for fn in work:
+        fn()
+
+
+def _defer(fn):
+    if not _DEFERRED:
+        torch.autograd.Variable._execution_engine.queue_callback(_flush_deferred)
+    _DEFERRED.append(fn)
+
+
 # diagnostic: join the head weight-gradient branch back right after its kernel (capture probe)
 HEAD_GRAD_JOIN = os.environ.get("VAETEB_HEAD_GRAD_JOIN", "0") == "1"
 LSTM_GRAD_STREAM = None  # ... for the LSTM weight gradients (set by SeqVaeTeb)
@@ -239,6 +260,22 @@ class LinearF(torch.autograd.Function):
         if gw_t is not None:
             pre = "vt_mfma_" if ctx.mfma else "vt_"
             side = HEAD_GRAD_STREAM if (ctx.mfma and pg.direct and HEAD_GRAD_STREAM is not None) else None
+            if side is None and ctx.mfma and pg.direct and HEAD_DW_DEFER and GRAD_READY is None:
+                # no side stream for them (under capture the branch is dropped, model.py): the
+                # heads' weight gradients are enqueued at the end of this backward instead of
+                # between the decoder's data-gradient kernels, where the data chain waited for
+                # them; same kernels and operands, same bits (in-place sinks; single process
+                # only: with bucketed all-reduce hooks the heads' bucket must be ready early)
+                cs = torch.cuda.current_stream()
+
+                def run(gy2=gy2, x2=x2, pg=pg, cs=cs, R=R, N=N, K=K, pre=pre):
+                    with torch.cuda.stream(cs):
+                        ws_d = WS.get(WS_LINEAR, gy2.device, 1)
+                        call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(pg.out[0]), ptr(pg.out[1]),
+                             pg.acc, ptr(ws_d), ws_d.numel(), _st())
+                    pg.result()
+                _defer(run)
+                return gx, None, None, None
             if side is not None and side.cuda_stream != _lib.stream():
                 # the decoder heads' 4096 x 4096 weight gradients are off the data-gradient
                 # chain: a side stream idle during the decoder backward (in-place sinks)
