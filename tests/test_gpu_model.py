@@ -606,3 +606,39 @@ def test_head_weight_grads_deferred_bitwise(golden, monkeypatch, native):
     assert res[0][0] == res[1][0]
     for a, b in zip(res[0][1:], res[1][1:]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_first_writer_head_gradients_bitwise(monkeypatch, native):
+    """FlatState.first_writer (Trainer steps): the four R x R decoder-head weights (+ biases) are
+    not zeroed by zero_grad and their weight-gradient kernel overwrites instead of accumulating
+    == zeroing everything, bit for bit: losses, parameters, moments and the last step's
+    gradients (S = 256: R = 4096, the bench's heads; eager steps and the native replay)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_, traj_inputs
+    from vaeteb import ops, train
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    res = []
+    for fw in (False, True):
+        monkeypatch.setattr(train, "FIRST_WRITER", fw)
+        m = det_fill_(SeqVaeTeb(sequence_length=256, concurrent_encoders=True, head_precision="bf16",
+                                conv_precision="bf16", mlp_precision="bf16", lstm_precision="16-mixed")).cuda()
+        tr = Trainer(m, lr=1e-3)
+        assert len(tr.state.first_writer) == 4
+        batches = []
+        for t in range(3):
+            y_st, y_ph, x_ph, y_raw, eps = [torch.from_numpy(a).cuda() for a in traj_inputs(256, 2, t)]
+            batches.append(({"fhr_st": y_st, "fhr_ph": y_ph, "fhr_up_ph": x_ph, "fhr": y_raw}, eps))
+        if native:
+            tr.capture(batches[0][0], eps=batches[0][1], warmup=1, native=True)
+            outs = [tr.replay(b, eps=e)["total_loss"].item() for b, e in batches[1:]]
+        else:
+            outs = [tr.step(b, eps=e)["total_loss"].item() for b, e in batches]
+        torch.cuda.synchronize()
+        assert not ops.FIRST_WRITER
+        res.append((outs, tr.state.p.clone(), tr.state.m.clone(), tr.state.v.clone(), tr.state.g.clone()))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, b)

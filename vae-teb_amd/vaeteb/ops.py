@@ -60,6 +60,11 @@ GRAD_READY = None
 SIDE_STREAMS = []   # extra streams the model runs work on (see SeqVaeTeb.concurrent_encoders)
 GRAD_STREAM = None  # side stream for weight gradients off the data-gradient chain (set by SeqVaeTeb)
 HEAD_GRAD_STREAM = None  # ... for the bf16-MFMA decoder-head weight gradients (set by SeqVaeTeb)
+# first-writer gradient groups of the current Trainer step (vaeteb.train.FlatState.first_writer):
+# id(weight) -> [weight, bias]; LinearF's weight-gradient call writes the group's first gradient
+# with accumulate = 0 and removes it
+FIRST_WRITER = {}
+
 # decoder-head weight gradients (bf16 MFMA, in-place sinks) enqueued at the end of the backward
 # when they have no side stream (VAETEB_HEAD_DW_DEFER=1)
 HEAD_DW_DEFER = os.environ.get("VAETEB_HEAD_DW_DEFER", "0") == "1"
@@ -257,6 +262,12 @@ class LinearF(torch.autograd.Function):
         want_b = b is not None and ctx.needs_input_grad[2]
         pg = _ParamGrads([w, b], [ctx.needs_input_grad[1], want_b])
         gw_t, gb_t = pg.out
+        grp = FIRST_WRITER.pop(id(w), None)
+        if grp is not None:
+            if pg.direct and gw_t is not None and (b is None or gb_t is not None) and len(grp) == (1 if b is None else 2):
+                pg.acc = 0   # the first gradient of this step into an unzeroed range: overwrite
+            else:
+                FIRST_WRITER[id(w)] = grp   # not written here: zeroed after the backward
         if gw_t is not None:
             pre = "vt_mfma_" if ctx.mfma else "vt_"
             side = HEAD_GRAD_STREAM if (ctx.mfma and pg.direct and HEAD_GRAD_STREAM is not None) else None

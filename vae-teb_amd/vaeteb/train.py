@@ -30,6 +30,9 @@ SHADOW_UPDATE = int(os.environ.get("VAETEB_SHADOW_UPDATE", "1"))
 
 BIG_ALIGN = 64          # floats: start of every parameter with >= BIG_PARAM elements in the flat buffers
 BIG_PARAM = 1 << 20
+# Trainer steps leave the decoder heads' gradient ranges unzeroed and let their weight-gradient
+# kernel overwrite them (FlatState.first_writer; VAETEB_FIRST_WRITER=0: zero everything)
+FIRST_WRITER = os.environ.get("VAETEB_FIRST_WRITER", "1") == "1"
 
 
 class FlatState:
@@ -65,13 +68,59 @@ class FlatState:
                 p.grad = self.g[o:o + n].view_as(p)
                 p._vt_sink = True  # HIP ops accumulate this gradient in place (vaeteb.ops._ParamGrads)
         self._grad_ptrs = [self.g.data_ptr() + 4 * o for o, _ in self.offsets]
+        # first-writer gradients: the weight (>= BIG_PARAM elements, 2-D) and bias of each
+        # linear module whose backward writes them with one kernel call (the decoder heads):
+        # zero_grad(first_writer=True) leaves their ranges alone and that call overwrites
+        # instead of accumulating (ops.FIRST_WRITER), saving the fill and the kernel's read of
+        # the old gradient (2 x 268 MB per step at R = 4096)
+        ids = {id(p): i for i, p in enumerate(self.params)}
+        self.first_writer = []
+        for m in module.modules():
+            w, b = getattr(m, "weight", None), getattr(m, "bias", None)
+            if isinstance(w, torch.nn.Parameter) and id(w) in ids and w.dim() == 2 and w.numel() >= BIG_PARAM and \
+                    (b is None or id(b) in ids):
+                self.first_writer.append([w] + ([b] if b is not None else []))
+        skip = sorted(ids[id(q)] for grp in self.first_writer for q in grp)
+        self._zero_ranges = []   # the complement of the first-writer ranges
+        o0 = 0
+        for i in skip:
+            o, n = self.offsets[i]
+            if o > o0:
+                self._zero_ranges.append((o0, o))
+            o0 = max(o0, o + n)
+        if o0 < self.numel:
+            self._zero_ranges.append((o0, self.numel))
 
-    def zero_grad(self):
-        self.g.zero_()
+    def zero_grad(self, first_writer=False):
+        """first_writer (Trainer steps: one forward / backward per zero_grad): the first-writer
+        groups are not zeroed; their first gradient kernel of the backward overwrites them and
+        Trainer._forward_backward zeroes any group no kernel wrote."""
+        if first_writer and self.first_writer:
+            from . import ops
+            for a, b in self._zero_ranges:
+                self.g[a:b].zero_()
+            ops.FIRST_WRITER.clear()
+            for grp in self.first_writer:
+                ops.FIRST_WRITER[id(grp[0])] = grp
+        else:
+            self.g.zero_()
+            if self.first_writer:
+                from . import ops
+                ops.FIRST_WRITER.clear()
         for p, (o, n), gp in zip(self.params, self.offsets, self._grad_ptrs):
             g = p.grad
             if g is None or g.data_ptr() != gp:
                 p.grad = self.g[o:o + n].view_as(p)
+
+    def finish_first_writer(self):
+        """After the backward: a first-writer group no kernel wrote is zeroed now."""
+        if not self.first_writer:
+            return
+        from . import ops
+        for grp in ops.FIRST_WRITER.values():
+            for q in grp:
+                q.grad.zero_()
+        ops.FIRST_WRITER.clear()
 
 
 def broadcast_state(state, module, group=None, src=0):
@@ -135,6 +184,10 @@ class GradBuckets:
         self.works = []
         self.launched = []
         self.ready = set()
+        # the stream the step's forward / backward is issued on: a bucket's writers may be on it
+        # even when the hook that completes the bucket runs on a side stream (the encoders'
+        # backward runs on the streams their forward ran on)
+        self.base = torch.cuda.current_stream() if self.state.g.is_cuda else None
 
     def launch_bucket(self, b):
         """Bucket b's all-reduce, issued on the current stream (the replay of a captured
@@ -163,6 +216,8 @@ class GradBuckets:
             cur = _lib.stream()
             from . import ops
             _lib.wait_for(self.comm, cur)
+            if self.base is not None and self.base.cuda_stream != cur:
+                _lib.wait_for(self.comm, self.base)
             for st in ops.SIDE_STREAMS:
                 if st.cuda_stream != self.comm.cuda_stream:
                     _lib.wait_for(self.comm, st)
@@ -184,6 +239,9 @@ class GradBuckets:
         if self.state.g.is_cuda:
             from . import ops
             cur = torch.cuda.current_stream()
+            base = getattr(self, "base", None)
+            if base is not None and base != cur:
+                cur.wait_stream(base)
             for st in ops.SIDE_STREAMS:
                 if st != cur:
                     cur.wait_stream(st)
@@ -322,7 +380,7 @@ class Trainer:
     def _forward_backward(self, batch, eps, overlap_comm):
         if not self.model.training:
             self.model.train()
-        self.state.zero_grad()
+        self.state.zero_grad(first_writer=FIRST_WRITER)
         if self.state.g.is_cuda:
             # every side stream joins the step at its start: under hipGraph capture a
             # stream the step never forked to would otherwise be joined at the end
@@ -347,6 +405,7 @@ class Trainer:
             cur = _lib.stream()
             for st in ops.SIDE_STREAMS:
                 _lib.wait_for(cur, st)
+        self.state.finish_first_writer()
         # detached: a returned loss must not keep this step's autograd graph (and
         # with it the parameters' AccumulateGrad nodes, bound to this step's
         # stream) alive into the next step or a hipGraph capture
@@ -477,7 +536,8 @@ class Trainer:
                 out = self._forward_backward(static_in, static_eps, overlap_comm=False)
                 if not self.buckets and update:
                     self._update()
-                _join_side_streams()
+                if CAPTURE_JOIN:
+                    _join_side_streams()
         finally:
             if self.buckets is not None:
                 self.buckets.mark_capture = False
@@ -490,6 +550,10 @@ class Trainer:
     def replay(self, batch=None, eps=None):
         """One step of the last captured graph on `batch` (copied into its static inputs)."""
         return self.captured.replay(batch, eps)
+
+
+CAPTURE_JOIN = os.environ.get("VAETEB_CAPTURE_JOIN", "1") == "1"
+DDP_DIAG = int(os.environ.get("VAETEB_DDP_DIAG", "0"))   # segmented-replay diagnostics (tools/gpu_ddp_ab.sh)
 
 
 def _join_side_streams():
@@ -582,7 +646,14 @@ class CapturedStep:
                 for end, b in self.markers:
                     self._launch_range(pos, end, 1 if pos == 0 else 0)
                     with torch.cuda.stream(self.comm):
+                        if DDP_DIAG == 1:   # diagnostic: the comm stream waits for every executor stream
+                            _lib.wait_for(self.comm, st[0])
+                            for sd in self.side:
+                                if sd.cuda_stream != self.comm.cuda_stream:
+                                    _lib.wait_for(self.comm, sd)
                         tr.buckets.launch_bucket(b)
+                        if DDP_DIAG == 2 and tr.buckets.works:   # diagnostic: each collective completes here
+                            tr.buckets.works[-1].wait()
                     pos = end
                 self._launch_range(pos, self.n_ops, (1 if pos == 0 else 0) | 2)
             else:
