@@ -64,7 +64,8 @@ int vt_fe_lowpass(const float* x, int64_t rows, int64_t x_row_stride, int N, int
                   void* stream);
 
 /* One workgroup per (sample b, item): xhat[b,chan] * psi[filter] -> inverse FFT
- * in LDS -> analytic[b, slot, 0:N] = result[pad_left:pad_left+N] (if slot>=0)
+ * in LDS -> analytic[b, slot, 0:N] = result[pad_left:pad_left+N] (if slot>=0; in the
+ * polar form when vt_fe_set_analytic_polar(1) on the 8192-point geometry)
  * and s1[b, s1_channel, :] = lowpass(|result[::2^k1]|) (if s1_channel>=0).
  * items: int[n_items][5] = {chan, filter, slot, s1_channel, k1}.
  * replaces: first-order loop scattering1d.py:306-333 and
@@ -94,6 +95,13 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
  * default: measured faster in the step); returns the previous grid (same bits either way) */
 int vt_fe_set_pairs_persist(int grid);
 int vt_fe_set_pairs_direct(int on);
+/* Storage form of the analytic slots on the 8192-point geometry (n_pad 8192,
+ * pad_left + N <= 8192), shared by vt_fe_wavelet (writes) and vt_fe_pairs (reads):
+ * 1 = polar {arg(a) / 2 pi, |a|} (the pair product becomes |a_i| |a_j|
+ * e^{2 pi i (power arg_i - arg_j)}, no per-pair arctangent: pair kernel 0.837 -> 0.785 ms),
+ * 0 = complex {re, im} (the default; every other geometry is always complex).  Initial
+ * value from VAETEB_ANALYTIC_POLAR; returns the previous setting.  Not thread-safe.  */
+int vt_fe_set_analytic_polar(int on);
 
 /* Diagnostic (tools/pairs_phases.py): while buf != NULL, training-geometry vt_fe_pairs
  * launches stamp wave 0's wall clock (100 MHz) at each phase boundary into

@@ -133,11 +133,24 @@ def test_frontend_vs_reference_golden(golden, request, J, Q, N):
 
 
 def test_analytic_signals(fe11):
+    """The analytic slots in their complex form (vt_fe_set_analytic_polar(0)) vs the oracle;
+    the default polar form {arg / 2 pi, |a|} is the same signal to fp32 rounding."""
     p, t = fe11.plan, fe11.tab
-    from vaeteb import synthetic
+    from vaeteb import _lib, synthetic
+    fns = _lib.lib().fns
     x = synthetic.batch(700, 2, 4096)
-    fe11.raw(torch.from_numpy(x).cuda())
-    an = torch.view_as_complex(fe11._bufs["analytic"]).cpu().numpy()
+    prev = fns["vt_fe_set_analytic_polar"](1)
+    try:
+        fe11.raw(torch.from_numpy(x).cuda())
+        pol = fe11._bufs["analytic"].double().cpu().numpy().copy()
+        fns["vt_fe_set_analytic_polar"](0)
+        fe11.raw(torch.from_numpy(x).cuda())
+        an = torch.view_as_complex(fe11._bufs["analytic"]).cpu().numpy()
+    finally:
+        fns["vt_fe_set_analytic_polar"](prev)
+    from_polar = pol[..., 1] * np.exp(2j * np.pi * pol[..., 0])
+    used = sorted({int(s) for s in t["items"].cpu().numpy()[:, 2] if s >= 0})
+    assert rel_rows(from_polar[:, used].reshape(-1, p.N), an[:, used].reshape(-1, p.N)).max() < 1e-6
     a64 = F.PhaseFrontEnd(11, 4, 16, 4096, dtype=np.float64).analytic(x[:, [0, 1]])
     a32 = torch_engine(F.PhaseFrontEnd(11, 4, 16, 4096).analytic, x[:, [0, 1]])
     items = t["items"].cpu().numpy()
@@ -150,16 +163,20 @@ def test_analytic_signals(fe11):
     assert_ref_precision(np.array(errs), np.array(ref_errs), what="analytic")
 
 
-@pytest.mark.parametrize("B", [3, 4, 8])
-def test_pairs_random_inputs_vs_oracle(fe11, B):
+@pytest.mark.parametrize("B,polar", [(3, 0), (4, 0), (8, 0), (4, 1)])
+def test_pairs_random_inputs_vs_oracle(fe11, B, polar):
     """Bigger random batch: HIP fp32 vs oracle fp64, distribution-bounded by the
     oracle's own fp32 error on the same inputs.  B = 4 / 8: every launch's item count
     (B x 44, B x 130, B x 174) is a multiple of 8, so the XCD-aware item order the bench
     runs (xcd_item, csrc/frontend.hip) is active; B = 3 keeps the identity order."""
-    from vaeteb import synthetic
+    from vaeteb import _lib, synthetic
     x = synthetic.batch(900, B, 4096)
-    r = fe11.raw(torch.from_numpy(x).cuda())
-    pairs = r["pairs"].cpu().numpy()
+    prev = _lib.lib().fns["vt_fe_set_analytic_polar"](polar)   # polar = 1: the opt-in polar slots
+    try:
+        r = fe11.raw(torch.from_numpy(x).cuda())
+        pairs = r["pairs"].cpu().numpy()
+    finally:
+        _lib.lib().fns["vt_fe_set_analytic_polar"](prev)
     p = fe11.plan
     o32 = F.PhaseFrontEnd(11, 4, 16, 4096)
     o64 = F.PhaseFrontEnd(11, 4, 16, 4096, dtype=np.float64)
@@ -223,6 +240,26 @@ def test_pairs_direct_columns_match_staged(fe11):
     torch.cuda.synchronize()
     diff = (staged - direct).abs().max().item()
     assert diff <= 1e-5 * staged.abs().max().item(), diff
+
+
+def test_pairs_polar_slots_match_complex(fe11):
+    """The pair features from polar analytic slots (opt-in, vt_fe_set_analytic_polar(1):
+    |a_i| |a_j| and one fused angle per element) against the complex slots with the per-pair
+    accelerated product: the same quantity in fp32, to 1e-5 of the batch's largest
+    coefficient (and against the fp64 oracle: test_pairs_random_inputs_vs_oracle[polar])."""
+    from vaeteb import _lib, synthetic
+    fns = _lib.lib().fns
+    x = torch.from_numpy(synthetic.batch(902, 4, 4096)).cuda()
+    prev = fns["vt_fe_set_analytic_polar"](1)
+    try:
+        polar = fe11.raw(x)["pairs"].clone()
+        fns["vt_fe_set_analytic_polar"](0)
+        cplx = fe11.raw(x)["pairs"].clone()
+    finally:
+        fns["vt_fe_set_analytic_polar"](prev)
+    torch.cuda.synchronize()
+    diff = (polar - cplx).abs().max().item()
+    assert diff <= 1e-5 * cplx.abs().max().item(), diff
 
 
 def test_frontend_bench_batch_rows_equal_small_batch(fe11):

@@ -10,6 +10,4 @@ timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/
 timeout -k 10 300 python bench.py --workload c4 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err && \
 timeout -k 10 300 python bench.py --workload c5 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err && \
 timeout -k 10 300 python bench.py --ddp-probe --no-cpu-baseline > gpurun_out/bench_ddp_probe.json 2> gpurun_out/bench_ddp_probe.err && \
-mkdir -p gpurun_out/ab && VAETEB_FIRST_WRITER=0 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/ab/fw0.json 2> gpurun_out/ab/fw0.err && \
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/ab/fw1.json 2> gpurun_out/ab/fw1.err && \
 bash tools/gpu_prof.sh

@@ -171,6 +171,39 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_wavelet(
 }
 
 // ---------------------------------------------------------------- phase pairs
+// Polar analytic slots (round 4): the wavelet kernel stores each analytic
+// sample of the 8192-point geometry as {arg(a) / 2 pi, |a|} — accel()'s angle and magnitude,
+// computed once per slot sample instead of once per pair — and a pair's accelerated product
+// accel(a_i, p) conj(a_j) = |a_i| |a_j| e^{2 pi i (p arg_i - arg_j)} is then one fused angle,
+// one range reduction, one cos / sin and a product of magnitudes (no atan polynomial, no
+// square root in the pair kernel).
+__device__ __forceinline__ float2 polar_rev(float2 a) {
+    const float ax = fabsf(a.x), ay = fabsf(a.y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float t = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+    const float s = t * t;
+    float r = 0.000390918023f;
+    r = fmaf(r, s, -0.00229176274f);
+    r = fmaf(r, s, 0.00633099675f);
+    r = fmaf(r, s, -0.0115143927f);
+    r = fmaf(r, s, 0.016709527f);
+    r = fmaf(r, s, -0.0225382969f);
+    r = fmaf(r, s, 0.0318085626f);
+    r = fmaf(r, s, -0.0530504771f);
+    r = fmaf(r, s, 0.159154922f);
+    r *= t;
+    if (ay > ax) r = 0.25f - r;
+    if (a.x < 0.f) r = 0.5f - r;
+    r = copysignf(r, a.y);
+    return make_float2(r, __builtin_amdgcn_sqrtf(a.x * a.x + a.y * a.y));
+}
+__device__ __forceinline__ float2 pair_polar(float2 pi, float2 pj, float p) {
+    float v = fmaf(pi.x, p, -pj.x);   // revolutions
+    v -= rintf(v);
+    const float m = pi.y * pj.y;
+    return make_float2(m * __builtin_amdgcn_cosf(v), m * __builtin_amdgcn_sinf(v));
+}
+template <bool POLAR>
 __global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
     const float2* __restrict__ analytic, int n_slots, int N, int n_pad, int pad_left, int n_pairs,
     const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
@@ -188,12 +221,16 @@ __global__ __launch_bounds__(FE_THREADS) void k_fe_pairs(
     // accelerated product (kymatio_phase_scattering.py:211-218, :282-283)
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
         const float2 u = ai[i], v = aj[i];
-        const float mag = sqrtf(u.x * u.x + u.y * u.y);
-        const float ph = atan2f(u.y, u.x) * pw;
-        float sn, cs;
-        sincosf(ph, &sn, &cs);
-        const float2 acc = make_float2(mag * cs, mag * sn);
-        Y[i] = cmul(acc, cconj(v));
+        if constexpr (POLAR) {
+            Y[i] = pair_polar(u, v, pw);
+        } else {
+            const float mag = sqrtf(u.x * u.x + u.y * u.y);
+            const float ph = atan2f(u.y, u.x) * pw;
+            float sn, cs;
+            sincosf(ph, &sn, &cs);
+            const float2 acc = make_float2(mag * cs, mag * sn);
+            Y[i] = cmul(acc, cconj(v));
+        }
         if (dec == 0) o[i] = Y[i].x;  // cross_phase_low_pass=False (:356-360): raw real part
     }
     if (dec == 0) return;
@@ -262,6 +299,13 @@ __device__ __forceinline__ float2 accel(float2 a, float p) {
     return make_float2(mag * __builtin_amdgcn_cosf(v), mag * __builtin_amdgcn_sinf(v));
 }
 
+// the product of a pair's two analytic samples in either storage form
+template <bool POLAR>
+__device__ __forceinline__ float2 pair_prod(float2 ai, float2 aj, float p) {
+    if constexpr (POLAR) return pair_polar(ai, aj, p);
+    else return F2(pmulc(C2(accel(ai, p)), C2(aj)));
+}
+
 // XCD-aware workgroup order: the hardware deals consecutive workgroups round-robin
 // to the 8 XCDs, so the linear id is remapped to give each XCD a contiguous run of
 // (sample, pair) items — the pairs of one sample then share that XCD's L2 copy of
@@ -284,7 +328,7 @@ __device__ __forceinline__ int xcd_item(int L, int total) {
         }                                                                                     \
     } while (0)
 static constexpr int PR_ZP = PR_NB + PR_NB / 8;  // padded 512-point buffer (z512_pos)
-template <bool G, bool D = false, bool P = false>
+template <bool G, bool D = false, bool P = false, bool POLAR = true>
 __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
     const float2* __restrict__ analytic, int n_slots, int N_, int pad_left_, int n_pairs, int B,
     const int* __restrict__ slot_i, const int* __restrict__ slot_j, const float* __restrict__ power,
@@ -322,7 +366,7 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
             xb[n2] = aj[s];
         }
 #pragma unroll
-        for (int n2 = 0; n2 < 16; ++n2) v[n2] = pmulc(C2(accel(xa[n2], pw)), C2(xb[n2]));
+        for (int n2 = 0; n2 < 16; ++n2) v[n2] = C2(pair_prod<POLAR>(xa[n2], xb[n2], pw));
     } else {
         // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283), compact;
         // loads in batches of 8 per thread (all in flight before the first use)
@@ -337,7 +381,7 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int u = u0 + PR_T * k;
-                if (G || u < N) img[u] = F2(pmulc(C2(accel(xa[k], pw)), C2(xb[k])));
+                if (G || u < N) img[u] = pair_prod<POLAR>(xa[k], xb[k], pw);
             }
         }
         PR_STAMP(1);
@@ -424,6 +468,7 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
 // seven other waves no longer idle through the inverse.  Phases 1-4 are k_fe_pairs8k's, the
 // product's elements are the same: bit-identical outputs.
 static constexpr int PRP_T7 = PR_T - 64;   // threads of waves 1-7
+template <bool POLAR>
 __device__ __forceinline__ void pr_product_w17(float2* img, const float2* __restrict__ ai,
                                                const float2* __restrict__ aj, float pw, int t7) {
 #pragma unroll
@@ -440,13 +485,14 @@ __device__ __forceinline__ void pr_product_w17(float2* img, const float2* __rest
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             const int u = t7 + PRP_T7 * (5 * bt + k);
-            if (bt == 0 || u < 4096) img[u] = F2(pmulc(C2(accel(xa[k], pw)), C2(xb[k])));
+            if (bt == 0 || u < 4096) img[u] = pair_prod<POLAR>(xa[k], xb[k], pw);
         }
     }
 }
 
 // (at most 128 VGPRs: two 8-wave workgroups per CU, as the per-item kernel; unconstrained, the
 // compiler hoists the twiddle tables out of the item loop and needs 228)
+template <bool POLAR>
 __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_fe_pairs8k_p(
     const float2* __restrict__ analytic, int n_slots, int n_pairs, int B, const int* __restrict__ slot_i,
     const int* __restrict__ slot_j, const float* __restrict__ power, const float2* __restrict__ tab,
@@ -469,7 +515,7 @@ __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     int64_t b;
     item_of(L, pair, b);
     if (t >= 64)   // the first item's product (wave 0 has no inverse to run yet)
-        pr_product_w17(img, analytic + (b * n_slots + slot_i[pair]) * (int64_t)N,
+        pr_product_w17<POLAR>(img, analytic + (b * n_slots + slot_i[pair]) * (int64_t)N,
                        analytic + (b * n_slots + slot_j[pair]) * (int64_t)N, power[pair], t - 64);
     for (; L < total; L += gridDim.x) {
         __syncthreads();   // the product of item L is in img; Z is free (previous inverse done)
@@ -540,7 +586,7 @@ __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
             int np;
             int64_t nb;
             item_of(Ln, np, nb);
-            pr_product_w17(img, analytic + (nb * n_slots + slot_i[np]) * (int64_t)N,
+            pr_product_w17<POLAR>(img, analytic + (nb * n_slots + slot_i[np]) * (int64_t)N,
                            analytic + (nb * n_slots + slot_j[np]) * (int64_t)N, power[np], t - 64);
         }
         if (Ln < total) item_of(Ln, pair, b);
@@ -558,6 +604,7 @@ __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
 // path ping-pongs two 64 KB buffers: one).
 __device__ __forceinline__ int nat_pos(int k) { return k + (k >> 5); }  // natural order, padded every 32
 
+template <bool POLAR>
 __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
     const float2* __restrict__ xhat, int C, const float* __restrict__ psi, const int* __restrict__ items, int n_items,
     int B, const float2* __restrict__ tab, int N, int pad_left, float2* __restrict__ analytic, int n_slots,
@@ -628,7 +675,10 @@ __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
     __syncthreads();
     if (slot >= 0) {
         float2* a = analytic + (b * n_slots + slot) * (int64_t)N;
-        for (int i = t; i < N; i += PR_T) a[i] = img[nat_pos(pad_left + i)];
+        for (int i = t; i < N; i += PR_T) {
+            const float2 v = img[nat_pos(pad_left + i)];
+            a[i] = POLAR ? polar_rev(v) : v;
+        }
     }
     if (s1ch >= 0) {
         const int M = PR_N >> k1;
@@ -875,6 +925,26 @@ int vt_fe_lowpass(const float* x, int64_t rows, int64_t x_row_stride, int N, int
     return VT_OK;
 }
 
+// polar analytic slots on the 8192-point geometry (opt-in: VAETEB_ANALYTIC_POLAR=1 /
+// vt_fe_set_analytic_polar(1); default complex, as every other geometry — DESIGN.md §9); the
+// wavelet and the pair entry points decide the form from the same predicate, so a pair launch
+// always reads what the wavelet launch wrote
+static int g_polar = -1;
+static bool analytic_polar(int n_pad, int N, int pad_left) {
+    if (g_polar < 0) {
+        const char* e = getenv("VAETEB_ANALYTIC_POLAR");
+        g_polar = e && e[0] == '1' ? 1 : 0;
+    }
+    return g_polar && n_pad == PR_N && pad_left + N <= PR_N;
+}
+
+int vt_fe_set_analytic_polar(int on) {
+    (void)analytic_polar(PR_N, 0, 0);
+    const int prev = g_polar;
+    g_polar = on ? 1 : 0;
+    return prev;
+}
+
 int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* psi, int n_items, const int* items,
                   const void* tw, int N, int pad_left, void* analytic, int n_slots, const float* h0, int radius,
                   int step, int start, int S_out, float* s1, int s1_channels, void* stream) {
@@ -887,7 +957,8 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
         const float2* tab = tw8k_tables(S(stream));
         VT_CHECK_ARG(tab != nullptr, "vt_fe_wavelet: twiddle tables unavailable (first call under stream capture?)");
         VT_CHECK_ARG((int64_t)n_items * B < (1ll << 31), "vt_fe_wavelet: grid");
-        hipLaunchKernelGGL(k_fe_wavelet8k, dim3((unsigned)(n_items * B)), dim3(PR_T), PR_IMG * sizeof(float2),
+        auto kern = analytic_polar(n_pad, N, pad_left) ? k_fe_wavelet8k<true> : k_fe_wavelet8k<false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(n_items * B)), dim3(PR_T), PR_IMG * sizeof(float2),
                            S(stream), (const float2*)xhat, C, psi, items, n_items, (int)B, tab, N, pad_left,
                            (float2*)analytic, n_slots, h0, radius, step, start, S_out, s1, s1_channels, nowrap);
     } else {
@@ -969,15 +1040,21 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
         // slower in the training step, where the phase and cross launches run concurrently
         // and the doubled L2 reads compete (1.19 -> 1.32 ms per launch): opt-in
         const bool direct = pairs_direct() != 0;
-        auto kern = geo ? (direct ? k_fe_pairs8k<true, true> : k_fe_pairs8k<true, false>) : k_fe_pairs8k<false>;
-        if (g_pairs_stamps != nullptr) kern = geo && !direct ? k_fe_pairs8k<true, false, true> : kern;
+        const bool pol = analytic_polar(n_pad, N, pad_left);
+        auto kern = pol ? (geo ? (direct ? k_fe_pairs8k<true, true, false, true> : k_fe_pairs8k<true, false, false, true>)
+                               : k_fe_pairs8k<false, false, false, true>)
+                        : (geo ? (direct ? k_fe_pairs8k<true, true, false, false> : k_fe_pairs8k<true, false, false, false>)
+                               : k_fe_pairs8k<false, false, false, false>);
+        if (g_pairs_stamps != nullptr && geo && !direct)
+            kern = pol ? k_fe_pairs8k<true, false, true, true> : k_fe_pairs8k<true, false, true, false>;
         const float2* tab = tw8k_tables(S(stream));
         VT_CHECK_ARG(tab != nullptr, "vt_fe_pairs: twiddle tables unavailable (first call under stream capture?)");
         VT_CHECK_ARG((int64_t)n_pairs * B < (1ll << 31), "vt_fe_pairs: grid");
         const int64_t total = (int64_t)n_pairs * B;
         const int pgrid = pairs_persist_grid();
         if (geo && !direct && g_pairs_stamps == nullptr && pgrid > 0 && total >= 2 * pgrid) {
-            hipLaunchKernelGGL(k_fe_pairs8k_p, dim3((unsigned)pgrid), dim3(PR_T), (PR_IMG + PR_ZP) * sizeof(float2),
+            hipLaunchKernelGGL(pol ? k_fe_pairs8k_p<true> : k_fe_pairs8k_p<false>, dim3((unsigned)pgrid), dim3(PR_T),
+                               (PR_IMG + PR_ZP) * sizeof(float2),
                                S(stream), (const float2*)analytic, n_slots, n_pairs, (int)B, slot_i, slot_j, power, tab,
                                phi0, start, S_out, out);
             VT_LAUNCH_CHECK("vt_fe_pairs");
@@ -988,7 +1065,8 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
                            power, tab, phi0, start, S_out, pad_mode, out, g_pairs_stamps);
         if (g_pairs_stamps != nullptr && geo && !direct) g_pairs_stamps += (size_t)B * n_pairs * 8;  // next launch after
     } else {
-        hipLaunchKernelGGL(k_fe_pairs, dim3(n_pairs, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
+        hipLaunchKernelGGL(analytic_polar(n_pad, N, pad_left) ? k_fe_pairs<true> : k_fe_pairs<false>,
+                           dim3(n_pairs, (unsigned)B), dim3(FE_THREADS), fft_lds_bytes(n_pad), S(stream),
                            (const float2*)analytic, n_slots, N, n_pad, pad_left, n_pairs, slot_i, slot_j, power,
                            (const float2*)tw, phi0, dec, start, S_out, pad_mode, out);
     }

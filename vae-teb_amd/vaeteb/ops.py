@@ -64,6 +64,7 @@ HEAD_GRAD_STREAM = None  # ... for the bf16-MFMA decoder-head weight gradients (
 # id(weight) -> [weight, bias]; LinearF's weight-gradient call writes the group's first gradient
 # with accumulate = 0 and removes it
 FIRST_WRITER = {}
+FIRST_WRITER_HIT = []   # group indices LinearF wrote this step (FlatState.finish_first_writer)
 
 # decoder-head weight gradients (bf16 MFMA, in-place sinks) enqueued at the end of the backward
 # when they have no side stream (VAETEB_HEAD_DW_DEFER=1)
@@ -262,12 +263,15 @@ class LinearF(torch.autograd.Function):
         want_b = b is not None and ctx.needs_input_grad[2]
         pg = _ParamGrads([w, b], [ctx.needs_input_grad[1], want_b])
         gw_t, gb_t = pg.out
-        grp = FIRST_WRITER.pop(id(w), None)
-        if grp is not None:
+        ent = FIRST_WRITER.pop(id(w), None)
+        if ent is not None:
+            grp, overwrite, gi = ent
             if pg.direct and gw_t is not None and (b is None or gb_t is not None) and len(grp) == (1 if b is None else 2):
-                pg.acc = 0   # the first gradient of this step into an unzeroed range: overwrite
+                FIRST_WRITER_HIT.append(gi)
+                if overwrite:
+                    pg.acc = 0   # the first gradient of this step into an unzeroed range: overwrite
             else:
-                FIRST_WRITER[id(w)] = grp   # not written here: zeroed after the backward
+                FIRST_WRITER[id(w)] = ent   # not written here: handled after the backward
         if gw_t is not None:
             pre = "vt_mfma_" if ctx.mfma else "vt_"
             side = HEAD_GRAD_STREAM if (ctx.mfma and pg.direct and HEAD_GRAD_STREAM is not None) else None

@@ -90,37 +90,55 @@ class FlatState:
             o0 = max(o0, o + n)
         if o0 < self.numel:
             self._zero_ranges.append((o0, self.numel))
+        self._fw_ok, self._fw_bad = set(), set()   # groups confirmed / seen written by another op
 
     def zero_grad(self, first_writer=False):
-        """first_writer (Trainer steps: one forward / backward per zero_grad): the first-writer
-        groups are not zeroed; their first gradient kernel of the backward overwrites them and
-        Trainer._forward_backward zeroes any group no kernel wrote."""
+        """first_writer (Trainer steps: one forward / backward per zero_grad): a first-writer
+        group is left unzeroed once a step has shown that its weight gradient comes from one
+        first-writer-aware kernel call (vaeteb.ops.LinearF); until then it is zeroed like the
+        rest (and any group the step does not write is zeroed after the backward,
+        finish_first_writer), so an op that accumulates into it never sees stale values."""
         if first_writer and self.first_writer:
             from . import ops
-            for a, b in self._zero_ranges:
-                self.g[a:b].zero_()
+            ranges = self._zero_ranges if len(self._fw_ok) == len(self.first_writer) else None
+            if ranges is None:
+                self.g.zero_()
+            else:
+                for a, b in ranges:
+                    self.g[a:b].zero_()
             ops.FIRST_WRITER.clear()
-            for grp in self.first_writer:
-                ops.FIRST_WRITER[id(grp[0])] = grp
+            ops.FIRST_WRITER_HIT.clear()
+            for gi, grp in enumerate(self.first_writer):
+                # [group, overwrite?]: overwrite only when the whole buffer was not zeroed
+                ops.FIRST_WRITER[id(grp[0])] = [grp, ranges is not None, gi]
         else:
             self.g.zero_()
             if self.first_writer:
                 from . import ops
                 ops.FIRST_WRITER.clear()
+                ops.FIRST_WRITER_HIT.clear()
         for p, (o, n), gp in zip(self.params, self.offsets, self._grad_ptrs):
             g = p.grad
             if g is None or g.data_ptr() != gp:
                 p.grad = self.g[o:o + n].view_as(p)
 
     def finish_first_writer(self):
-        """After the backward: a first-writer group no kernel wrote is zeroed now."""
+        """After the backward: a group its first-writer kernel handled is confirmed; a group no
+        such kernel wrote is zeroed if it was left unzeroed, and never confirmed."""
         if not self.first_writer:
             return
         from . import ops
-        for grp in ops.FIRST_WRITER.values():
-            for q in grp:
-                q.grad.zero_()
+        for gi in ops.FIRST_WRITER_HIT:
+            self._fw_ok.add(gi)
+        for grp, overwrite, gi in ops.FIRST_WRITER.values():
+            self._fw_bad.add(gi)
+            self._fw_ok.discard(gi)
+            if overwrite:
+                for q in grp:
+                    q.grad.zero_()
+        self._fw_ok -= self._fw_bad
         ops.FIRST_WRITER.clear()
+        ops.FIRST_WRITER_HIT.clear()
 
 
 def broadcast_state(state, module, group=None, src=0):
