@@ -98,7 +98,8 @@ def profile_mfma(ROOT_=None):
         latest = os.path.join(d, "LATEST")
         pinned = os.path.exists(latest) and open(latest).read().strip() == os.path.basename(f)
         return (os.path.basename(d), pinned, os.path.getmtime(f))
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_step*.csv")), key=key)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_step*.csv")) +
+                   glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_timed.csv")), key=key)
     for f in reversed(files):
         rows = list(csv.DictReader(open(f)))
         steps = sum(int(r["Calls"]) for r in rows if "k_adamw4" in r["Name"])
@@ -658,7 +659,8 @@ def main():
                        "source": k_src, "achieved": tf and round(tf, 1), "peak": MFMA_PEAK_TFLOPS,
                        "unit": "TFLOP/s", "frac": tf and round(tf / MFMA_PEAK_TFLOPS, 4),
                        "call_span_ms_per_step": round(mfma_ms / mfma_steps, 3),
-                       "timed_in": "eager steps after the timed region" if graph else "timed region"}
+                       "timed_in": ("call span: eager steps after the timed region" if graph else "timed region")
+                                   + "; kernel time: the source's rocprofv3 trace"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline((J, Q, T), batch=args.cpu_batch, classifier=c4)
     if rank == 0:

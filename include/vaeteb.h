@@ -99,8 +99,8 @@ int vt_fe_set_pairs_direct(int on);
  * pad_left + N <= 8192), shared by vt_fe_wavelet (writes) and vt_fe_pairs (reads):
  * 1 = polar {arg(a) / 2 pi, |a|} (the pair product becomes |a_i| |a_j|
  * e^{2 pi i (power arg_i - arg_j)}, no per-pair arctangent: pair kernel 0.837 -> 0.785 ms),
- * 0 = complex {re, im} (the default; every other geometry is always complex).  Initial
- * value from VAETEB_ANALYTIC_POLAR; returns the previous setting.  Not thread-safe.  */
+ * 0 = complex {re, im} (every other geometry is always complex).  Default 1;
+ * VAETEB_ANALYTIC_POLAR=0 sets 0 initially; returns the previous setting.  Not thread-safe.  */
 int vt_fe_set_analytic_polar(int on);
 
 /* Diagnostic (tools/pairs_phases.py): while buf != NULL, training-geometry vt_fe_pairs

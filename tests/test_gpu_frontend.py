@@ -163,7 +163,7 @@ def test_analytic_signals(fe11):
     assert_ref_precision(np.array(errs), np.array(ref_errs), what="analytic")
 
 
-@pytest.mark.parametrize("B,polar", [(3, 0), (4, 0), (8, 0), (4, 1)])
+@pytest.mark.parametrize("B,polar", [(3, 0), (4, 0), (8, 0), (4, 1), (8, 1)])
 def test_pairs_random_inputs_vs_oracle(fe11, B, polar):
     """Bigger random batch: HIP fp32 vs oracle fp64, distribution-bounded by the
     oracle's own fp32 error on the same inputs.  B = 4 / 8: every launch's item count
@@ -171,7 +171,7 @@ def test_pairs_random_inputs_vs_oracle(fe11, B, polar):
     runs (xcd_item, csrc/frontend.hip) is active; B = 3 keeps the identity order."""
     from vaeteb import _lib, synthetic
     x = synthetic.batch(900, B, 4096)
-    prev = _lib.lib().fns["vt_fe_set_analytic_polar"](polar)   # polar = 1: the opt-in polar slots
+    prev = _lib.lib().fns["vt_fe_set_analytic_polar"](polar)   # polar = 1: the default polar slots
     try:
         r = fe11.raw(torch.from_numpy(x).cuda())
         pairs = r["pairs"].cpu().numpy()
@@ -243,7 +243,7 @@ def test_pairs_direct_columns_match_staged(fe11):
 
 
 def test_pairs_polar_slots_match_complex(fe11):
-    """The pair features from polar analytic slots (opt-in, vt_fe_set_analytic_polar(1):
+    """The pair features from polar analytic slots (the default, vt_fe_set_analytic_polar(1):
     |a_i| |a_j| and one fused angle per element) against the complex slots with the per-pair
     accelerated product: the same quantity in fp32, to 1e-5 of the batch's largest
     coefficient (and against the fp64 oracle: test_pairs_random_inputs_vs_oracle[polar])."""

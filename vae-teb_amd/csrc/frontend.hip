@@ -925,15 +925,15 @@ int vt_fe_lowpass(const float* x, int64_t rows, int64_t x_row_stride, int N, int
     return VT_OK;
 }
 
-// polar analytic slots on the 8192-point geometry (opt-in: VAETEB_ANALYTIC_POLAR=1 /
-// vt_fe_set_analytic_polar(1); default complex, as every other geometry — DESIGN.md §9); the
+// polar analytic slots on the 8192-point geometry (default on; VAETEB_ANALYTIC_POLAR=0 /
+// vt_fe_set_analytic_polar(0) keeps the complex form, as every other geometry — DESIGN.md §9); the
 // wavelet and the pair entry points decide the form from the same predicate, so a pair launch
 // always reads what the wavelet launch wrote
 static int g_polar = -1;
 static bool analytic_polar(int n_pad, int N, int pad_left) {
     if (g_polar < 0) {
         const char* e = getenv("VAETEB_ANALYTIC_POLAR");
-        g_polar = e && e[0] == '1' ? 1 : 0;
+        g_polar = e && e[0] == '0' ? 0 : 1;
     }
     return g_polar && n_pad == PR_N && pad_left + N <= PR_N;
 }
