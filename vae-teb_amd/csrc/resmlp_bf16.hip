@@ -746,8 +746,8 @@ __device__ __forceinline__ void dw_img(const __bf16* zi, const __bf16* hi, int N
     do {                                                                                     \
         if (stamps && threadIdx.x == 0) stamps[(int64_t)blockIdx.x * 256 + (k)] = wall_clock64(); \
     } while (0)
-template <int NT, int TPW>
-__global__ __launch_bounds__(BT, 1) void k_mlpb_bwd(const BDesc* __restrict__ dp, const float* __restrict__ dout,
+template <int NT, int TPW, int OCC = 1>
+__global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restrict__ dp, const float* __restrict__ dout,
                                                     const float* __restrict__ xh, const float* __restrict__ rs,
                                                     int64_t R, int64_t Rp, float* __restrict__ dx,
                                                     float* __restrict__ part, unsigned long long* __restrict__ stamps) {
@@ -998,6 +998,7 @@ inline int h32(int n) { return (n + 31) & ~31; }
 struct BPlan {
     BDesc d;
     int nt, tpw;
+    int occ;                     // backward workgroups per CU the launch is built for (1, or 2: 128-row blocks)
     int64_t Rp, xh_floats, rs_floats, nblk;
     int gbytes;                  // global image bytes
     int prep_x, prep_y;          // k_mlpb_prep grid
@@ -1094,14 +1095,33 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
         const char* e = getenv("VAETEB_MLPB_TPW");
         tpw_env = e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
     }
-    p.tpw = p.nt >= 6 ? 1 : (tpw_env ? tpw_env : 2);
-    const int ims = IMR * p.tpw + 16;
-    const int rest = 2 * (bz + bh) * ims + 4 * (bprm + NW * 48 * p.nt);
-    d.bres = 2 * bwtot + rest <= 160 * 1024;  // all W^T images resident when they fit
-    if (!d.bres)
-        for (int g = 0; g < d.nG; ++g) d.G[g].bw = 0;
-    d.bwimg = d.bres ? bwtot : bw;
-    d.bbytes = 2 * d.bwimg + rest;
+    // VAETEB_MLPB_OCC=2 (tuning option, off by default): two 128-row workgroups per CU
+    // (<= 128 VGPRs and <= 80 KB of LDS each, W^T images streamed per GEMM when they do not
+    // fit beside the images) instead of one 256-row workgroup, for widths <= 32 (isolated
+    // kernel span 213 -> 174 us on the 33-GEMM stacks, but the replayed step 8.19-8.22 vs
+    // 8.16-8.18 ms: DESIGN.md §9); =3 also at width 64, where the 128-VGPR cap spills
+    // (74 -> 104 us)
+    static int occ_env = -1;
+    if (occ_env < 0) {
+        const char* e = getenv("VAETEB_MLPB_OCC");
+        occ_env = e && (e[0] == '2' || e[0] == '3') ? e[0] - '0' : 1;
+    }
+    const bool occ2 = !tpw_env && (occ_env == 3 ? p.nt <= 4 : occ_env == 2 && p.nt == 2);
+    for (int occ = occ2 ? 2 : 1;; --occ) {
+        const int cap = 160 * 1024 / occ;
+        p.occ = occ;
+        p.tpw = occ == 2 ? 1 : p.nt >= 6 ? 1 : (tpw_env ? tpw_env : 2);
+        const int ims = IMR * p.tpw + 16;
+        const int rest = 2 * (bz + bh) * ims + 4 * (bprm + NW * 48 * p.nt);
+        d.bres = 2 * bwtot + rest <= cap;  // all W^T images resident when they fit
+        for (int g = 0, o = 0; g < d.nG; ++g) {
+            d.G[g].bw = d.bres ? o : 0;
+            o += (h16(d.G[g].K) * d.G[g].bs + 7) & ~7;
+        }
+        d.bwimg = d.bres ? bwtot : bw;
+        d.bbytes = 2 * d.bwimg + rest;
+        if (d.bbytes <= cap || occ == 1) break;
+    }
     // global image (k_mlpb_prep): forward LDS image | W^T images | backward params
     d.gbo = (d.fbytes + 15) & ~15;
     d.gpo = d.gbo + ((2 * bwtot + 15) & ~15);
@@ -1323,13 +1343,14 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
         if (p.d.l[l].ln) add(2 * p.d.G[l].N, p.d.G[l].N, 0, p.d.l[l].lpo, grads[4 + 4 * l], grads[5 + 4 * l]);
     add(2 * dims[0], dims[0], 0, p.d.lpo0, grads[0], grads[1]);
     const dim3 grid((unsigned)p.nblk);
-#define VT_MBB(NTV, TPWV)                                                                                        \
-    if (p.nt == NTV && p.tpw == TPWV) {                                                                    \
-        set_lds(k_mlpb_bwd<NTV, TPWV>, p.d.bbytes);                                                        \
-        hipLaunchKernelGGL((k_mlpb_bwd<NTV, TPWV>), grid, dim3(BT), p.d.bbytes, st, ddev, dout, xhat, rstd, rows, \
-                           p.Rp, dx, ws, g_mlpb_stamps);                                                   \
+#define VT_MBB(NTV, TPWV, OCCV)                                                                                  \
+    if (p.nt == NTV && p.tpw == TPWV && p.occ == OCCV) {                                                           \
+        set_lds(k_mlpb_bwd<NTV, TPWV, OCCV>, p.d.bbytes);                                                          \
+        hipLaunchKernelGGL((k_mlpb_bwd<NTV, TPWV, OCCV>), grid, dim3(BT), p.d.bbytes, st, ddev, dout, xhat, rstd, rows, \
+                           p.Rp, dx, ws, g_mlpb_stamps);                                                           \
     }
-    VT_MBB(2, 2) VT_MBB(4, 2) VT_MBB(2, 1) VT_MBB(4, 1) VT_MBB(6, 1) VT_MBB(9, 1)
+    VT_MBB(2, 2, 1) VT_MBB(4, 2, 1) VT_MBB(2, 1, 1) VT_MBB(4, 1, 1) VT_MBB(6, 1, 1) VT_MBB(9, 1, 1)
+    VT_MBB(2, 1, 2) VT_MBB(4, 1, 2)
 #undef VT_MBB
     if (sa.nseg) {
         const dim3 gs((unsigned)((emax + 63) / 64), (unsigned)sa.nseg);
