@@ -218,6 +218,28 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ x, G
     }
 }
 
+// The fixed pairwise tree over a 256-thread workgroup's values (level o: v[t] += v[t + o],
+// o = 128 .. 1) with the levels below 64 as wave-0 shuffles instead of LDS round trips and
+// barriers: the same additions in the same order (the same bits); every thread gets the sum.
+// red: 256 doubles of LDS, reusable on return.
+__device__ __forceinline__ double tree256(double v, double* red) {
+    const int tid = threadIdx.x;
+    red[tid] = v;
+    __syncthreads();
+    if (tid < 128) red[tid] += red[tid + 128];
+    __syncthreads();
+    if (tid < 64) {
+        double x = red[tid] + red[tid + 64];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
+        if (tid == 0) red[0] = x;
+    }
+    __syncthreads();
+    const double r = red[0];
+    __syncthreads();
+    return r;
+}
+
 // BatchNorm batch statistics from the conv tiles' (sum, M2) partials (Chan's
 // parallel combination in double, fixed order): mean, rstd and the running
 // statistics (torch momentum semantics, unbiased running variance).
@@ -242,14 +264,7 @@ __global__ __launch_bounds__(256) void k_bn_stats_finalize(const float* __restri
         for (int k = 0; k < 8; ++k) a += (double)u[k];
     }
     for (; i < ntile; i += 256) a += (double)s0p[i];
-    red[tid] = a;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) red[tid] += red[tid + o];
-        __syncthreads();
-    }
-    const double mu = red[0] / M;
-    __syncthreads();
+    const double mu = tree256(a, red) / M;
     double q = 0.0;
     auto m2 = [&](int i, float sv, float mv) {
         const int tx = i % tiles_per_sample;
@@ -270,14 +285,8 @@ __global__ __launch_bounds__(256) void k_bn_stats_finalize(const float* __restri
         for (int k = 0; k < 8; ++k) m2(i + 256 * k, u[k], v[k]);
     }
     for (; i < ntile; i += 256) m2(i, s0p[i], s1p[i]);
-    red[tid] = q;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) red[tid] += red[tid + o];
-        __syncthreads();
-    }
+    const double var = tree256(q, red) / M;
     if (tid != 0) return;
-    const double var = red[0] / M;
     mean[c] = (float)mu;
     rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
     if (run_mean) {

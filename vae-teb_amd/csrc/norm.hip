@@ -419,18 +419,27 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ pa
         a0 += (double)p0[b];
         a1 += (double)p1[b];
     }
-    r0[threadIdx.x] = a0;
-    r1[threadIdx.x] = a1;
+    // the fixed pairwise tree (level o: r[t] += r[t + o], o = 128 .. 1), the levels below 64
+    // as wave-0 shuffles (the same additions in the same order: the same bits)
+    static_assert(NT == 256, "k_bn_finalize: 256-thread tree");
+    const int t = threadIdx.x;
+    r0[t] = a0;
+    r1[t] = a1;
     __syncthreads();
-    for (int o = NT / 2; o > 0; o >>= 1) {
-        if (threadIdx.x < o) {
-            r0[threadIdx.x] += r0[threadIdx.x + o];
-            r1[threadIdx.x] += r1[threadIdx.x + o];
-        }
-        __syncthreads();
+    if (t < 128) {
+        r0[t] += r0[t + 128];
+        r1[t] += r1[t + 128];
     }
-    if (threadIdx.x != 0) return;
-    const double s0 = r0[0], s1 = r1[0];
+    __syncthreads();
+    if (t >= 64) return;
+    double x0 = r0[t] + r0[t + 64], x1 = r1[t] + r1[t + 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        x0 += __shfl_down(x0, o);
+        x1 += __shfl_down(x1, o);
+    }
+    if (t != 0) return;
+    const double s0 = x0, s1 = x1;
     if (mode == 0) {
         mean[c] = (float)(s0 / (double)M);
     } else if (mode == 1) {
@@ -689,6 +698,30 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
     }
     __syncthreads();
     const int groups = 4 * Tp / C;
+    if (groups >= 256) {
+        // very narrow rows (C <= 4: 256 to 1024 thread groups per channel): one wave per
+        // channel, lane l sums groups l, l + 64, ... in order, then a fixed shuffle tree — the
+        // one-thread loop over 1024 LDS values was the kernel's tail (C = 1, M = 1M rows:
+        // 46 -> 8.5 us; at C = 11 / 16 the one-thread loop is not slower, and keeps its bits)
+        const int lane = tid & 63;
+        for (int cc = tid >> 6; cc < C; cc += NT / 64) {
+            float s0 = 0.f, s1 = 0.f;
+            for (int q = lane; q < groups; q += 64) {
+                s0 += red0[q * C + cc];
+                s1 += red1[q * C + cc];
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                s0 += __shfl_down(s0, o);
+                s1 += __shfl_down(s1, o);
+            }
+            if (lane == 0) {
+                part[(int64_t)cc * gridDim.x + blockIdx.x] = s0;
+                part[(int64_t)(C + cc) * gridDim.x + blockIdx.x] = s1;
+            }
+        }
+        return;
+    }
     for (int cc = tid; cc < C; cc += NT) {
         float s0 = 0.f, s1 = 0.f;
         for (int q = 0; q < groups; ++q) {
