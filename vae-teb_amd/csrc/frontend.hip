@@ -604,7 +604,7 @@ __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
 // path ping-pongs two 64 KB buffers: one).
 __device__ __forceinline__ int nat_pos(int k) { return k + (k >> 5); }  // natural order, padded every 32
 
-template <bool POLAR>
+template <bool POLAR, bool LP = true>
 __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
     const float2* __restrict__ xhat, int C, const float* __restrict__ psi, const int* __restrict__ items, int n_items,
     int B, const float2* __restrict__ tab, int N, int pad_left, float2* __restrict__ analytic, int n_slots,
@@ -680,7 +680,43 @@ __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
             a[i] = POLAR ? polar_rev(v) : v;
         }
     }
-    if (s1ch >= 0) {
+    if (LP && s1ch >= 0) {
+        // the S1 low-pass with h0 staged in LDS and |u| of every sample the taps read formed
+        // once, in place (the .x of its image entry), instead of a global h0 load and a square
+        // root per tap (313 taps at k1 = 0, each sample read by ~20 outputs): the same
+        // products summed in the same order as the else branch (the same bits).  Measured
+        // 539 -> 419 us per launch; a residue-major copy of |u| for conflict-free lane reads
+        // was slower (431 us: its extra pass and barrier cost more than the conflicts)
+        const int M = PR_N >> k1;
+        float* hl = reinterpret_cast<float*>(img + PR_IMG);
+        for (int i = t; i <= radius; i += PR_T) hl[i] = h0[i];
+        __syncthreads();   // the analytic copy above is done with the complex values
+        for (int n = t; n < M; n += PR_T) {
+            const float2 u = img[nat_pos(n << k1)];
+            img[nat_pos(n << k1)].x = sqrtf(u.x * u.x + u.y * u.y);
+        }
+        __syncthreads();
+        auto taps = [&](int c, int n0, int n1) {
+            float acc = 0.f;
+            for (int n = n0; n <= n1; ++n) {
+                int d = c - (n << k1);
+                d = d < 0 ? -d : d;
+                int nn = n;
+                if (!nowrap) {
+                    nn %= M;
+                    if (nn < 0) nn += M;
+                }
+                acc += img[nat_pos(nn << k1)].x * hl[d];
+            }
+            return acc;
+        };
+        for (int m = t; m < S; m += PR_T) {
+            const int c = step * (m + start);
+            const int lo = (c - radius + (1 << k1) - 1) >> k1;
+            const int hi = (c + radius) >> k1;
+            s1[(b * s1_channels + s1ch) * S + m] = taps(c, lo, hi);
+        }
+    } else if (s1ch >= 0) {
         const int M = PR_N >> k1;
         for (int m = t; m < S; m += PR_T) {
             const int c = step * (m + start);
@@ -957,8 +993,16 @@ int vt_fe_wavelet(const void* xhat, int64_t B, int C, int n_pad, const float* ps
         const float2* tab = tw8k_tables(S(stream));
         VT_CHECK_ARG(tab != nullptr, "vt_fe_wavelet: twiddle tables unavailable (first call under stream capture?)");
         VT_CHECK_ARG((int64_t)n_items * B < (1ll << 31), "vt_fe_wavelet: grid");
-        auto kern = analytic_polar(n_pad, N, pad_left) ? k_fe_wavelet8k<true> : k_fe_wavelet8k<false>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)(n_items * B)), dim3(PR_T), PR_IMG * sizeof(float2),
+        // VAETEB_WAVELET_LP=0: the S1 low-pass with a global h0 load and a square root per tap (A/B)
+        // (two threads per output with the taps summed in two halves: 411 -> 380 us, but other
+        // bits, and the J = 6 end-to-end gradient bound failed on them: not kept)
+        static const bool lp_env = !(getenv("VAETEB_WAVELET_LP") && getenv("VAETEB_WAVELET_LP")[0] == '0');
+        const bool lp = lp_env && radius < 2048;
+        const bool pol = analytic_polar(n_pad, N, pad_left);
+        auto kern = pol ? (lp ? k_fe_wavelet8k<true, true> : k_fe_wavelet8k<true, false>)
+                        : (lp ? k_fe_wavelet8k<false, true> : k_fe_wavelet8k<false, false>);
+        const size_t lds = PR_IMG * sizeof(float2) + (lp ? (size_t)((radius + 4) / 4 * 4) * 4 : 0);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(n_items * B)), dim3(PR_T), lds,
                            S(stream), (const float2*)xhat, C, psi, items, n_items, (int)B, tab, N, pad_left,
                            (float2*)analytic, n_slots, h0, radius, step, start, S_out, s1, s1_channels, nowrap);
     } else {
