@@ -685,8 +685,9 @@ __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
         // once, in place (the .x of its image entry), instead of a global h0 load and a square
         // root per tap (313 taps at k1 = 0, each sample read by ~20 outputs): the same
         // products summed in the same order as the else branch (the same bits).  Measured
-        // 539 -> 419 us per launch; a residue-major copy of |u| for conflict-free lane reads
-        // was slower (431 us: its extra pass and barrier cost more than the conflicts)
+        // 539 -> 419 us per launch, 372 us with the uniform-offset loop below; a residue-major
+        // copy of |u| for conflict-free lane reads was slower (431 vs 419 us: its extra pass and
+        // barrier cost more than the conflicts)
         const int M = PR_N >> k1;
         float* hl = reinterpret_cast<float*>(img + PR_IMG);
         for (int i = t; i <= radius; i += PR_T) hl[i] = h0[i];
@@ -710,11 +711,30 @@ __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
             }
             return acc;
         };
-        for (int m = t; m < S; m += PR_T) {
-            const int c = step * (m + start);
-            const int lo = (c - radius + (1 << k1) - 1) >> k1;
-            const int hi = (c + radius) >> k1;
-            s1[(b * s1_channels + s1ch) * S + m] = taps(c, lo, hi);
+        if (nowrap && (step >> k1 << k1) == step) {
+            // every output's centre c is a multiple of 2^k1: tap n = c / 2^k1 + j, j = -jr .. jr,
+            // weight h0[|j| 2^k1] the same for every lane (a scalar load) — the same n order and
+            // products as taps() (lo = c / 2^k1 - jr, hi = c / 2^k1 + jr)
+            const int jr = radius >> k1;
+            for (int m = t; m < S; m += PR_T) {
+                const int c0 = (step >> k1) * (m + start);
+                float acc = 0.f;
+#pragma unroll 8
+                for (int j = -jr; j <= jr; ++j) {
+                    const int nn = c0 + j;
+                    // fmaf spelled out: the unrolled body would otherwise be vectorised into
+                    // packed multiplies + adds (two roundings, other bits than taps()'s fma)
+                    acc = fmaf(img[nat_pos(nn << k1)].x, h0[(j < 0 ? -j : j) << k1], acc);
+                }
+                s1[(b * s1_channels + s1ch) * S + m] = acc;
+            }
+        } else {
+            for (int m = t; m < S; m += PR_T) {
+                const int c = step * (m + start);
+                const int lo = (c - radius + (1 << k1) - 1) >> k1;
+                const int hi = (c + radius) >> k1;
+                s1[(b * s1_channels + s1ch) * S + m] = taps(c, lo, hi);
+            }
         }
     } else if (s1ch >= 0) {
         const int M = PR_N >> k1;
