@@ -160,14 +160,18 @@ static constexpr int TW8K_T1 = 0, TW8K_T2 = 15 * 512, TW8K_TA = TW8K_T2 + 15 * 3
 // k = (lane >> 3) + 8 (lane & 7) + 64 j.  Only lanes of the calling wave touch z:
 // the passes are ordered by wave-scope fences, no workgroup barrier.
 __device__ __forceinline__ int z512_pos(int i) { return i + (i >> 3); }
-__device__ __forceinline__ void wave_fft512(float2* z, const float2* __restrict__ tab, c2 r[8]) {
-    const int l = threadIdx.x & 63, q = l >> 3, l0 = l & 7;
-    c2 u[8], w[7], wb[7];
+// the lane's twiddles of wave_fft512 (passes A and B), loadable ahead of the call
+__device__ __forceinline__ void fft512_twiddles(const float2* __restrict__ tab, c2 w[7], c2 wb[7]) {
+    const int l = threadIdx.x & 63, l0 = l & 7;
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
         w[j] = C2(tab[TW8K_TA + 64 * j + l]);
         wb[j] = C2(tab[TW8K_TB + 8 * j + l0]);
     }
+}
+__device__ __forceinline__ void wave_fft512(float2* z, const c2 w[7], const c2 wb[7], c2 r[8]) {
+    const int l = threadIdx.x & 63, q = l >> 3, l0 = l & 7;
+    c2 u[8];
     // A: n = l + 64 j -> y[l][q'] = W_512^{l q'} DFT8_j
 #pragma unroll
     for (int j = 0; j < 8; ++j) u[j] = C2(z[z512_pos(l + 64 * j)]);
@@ -194,6 +198,11 @@ __device__ __forceinline__ void wave_fft512(float2* z, const float2* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] = C2(z[z512_pos(j + 8 * l0 + 64 * q)]);
     pdft8(r);
+}
+__device__ __forceinline__ void wave_fft512(float2* z, const float2* __restrict__ tab, c2 r[8]) {
+    c2 w[7], wb[7];
+    fft512_twiddles(tab, w, wb);
+    wave_fft512(z, w, wb, r);
 }
 
 }  // namespace vt

@@ -351,8 +351,15 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
     const int k3 = k2_3 + 16 * kb_3 + 256 * ka;
     const float ph3 = phi0[k3];
     PR_STAMP(0);
-    c2 v[16];
+    c2 v[16], w[15];
+    // the pass-1 twiddles W_8192^{t k2}: issued before the barriers of the column formation
+    // (no dependence on it), so their L2 latency overlaps the waits instead of following them
+    auto load_w1 = [&]() {
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) w[k2 - 1] = C2(tab[TW8K_T1 + 512 * (k2 - 1) + t]);
+    };
     if constexpr (D) {
+        load_w1();
         // 0+1 fused (training geometry only): column n1 = t of the reflect-padded product
         // straight from HBM / L2, the product formed in registers (each sample of the
         // signal is visited twice, once per reflection), first radix-16 pass, no staging
@@ -385,6 +392,7 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
             }
         }
         PR_STAMP(1);
+        load_w1();
         __syncthreads();
         // 1: column n1 = t of the padded signal (reflect / zero / circular); one
         // reflection at most on the training geometry (no modulo)
@@ -399,23 +407,21 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
         __syncthreads();
     }
     {
-        c2 w[15];
-#pragma unroll
-        for (int k2 = 1; k2 < 16; ++k2) w[k2 - 1] = C2(tab[TW8K_T1 + 512 * (k2 - 1) + t]);
         pdft16(v);
         img[pr_pos(t)] = F2(v[0]);
 #pragma unroll
         for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(t + 512 * k2)] = F2(pmul(v[k2], w[k2 - 1]));
     }
     PR_STAMP(2);
+    // the pass-2 twiddles W_512^{n1a kb}, likewise in flight across the barrier
+#pragma unroll
+    for (int kb = 1; kb < 16; ++kb) w[kb - 1] = C2(tab[TW8K_T2 + 32 * (kb - 1) + (t & 31)]);
     __syncthreads();
     // 2: job (k2, n1a) = (t >> 5, t & 31): radix-16 over n1b inside block k2, in place
     {
         const int k2 = t >> 5, n1a = t & 31;
         float2* base = img + k2 * 528 + n1a;
-        c2 w[15], x[16];
-#pragma unroll
-        for (int kb = 1; kb < 16; ++kb) w[kb - 1] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
+        c2 x[16];
 #pragma unroll
         for (int n1b = 0; n1b < 16; ++n1b) x[n1b] = C2(base[33 * n1b]);
         pdft16(x);
@@ -441,11 +447,14 @@ __global__ __launch_bounds__(PR_T) void k_fe_pairs8k(
         Z[z512_pos(k3)] = make_float2(x.x * ph3, -x.y * ph3);
     }
     PR_STAMP(4);
+    // wave 0's 512-point twiddles in flight across the barrier
+    c2 w5[7], wb5[7];
+    if (t < 64) fft512_twiddles(tab, w5, wb5);
     __syncthreads();
     // 4: inverse FFT of length 512 by wave 0, keep the real part of [start, start + S)
     if (t < 64) {
         c2 r[8];
-        wave_fft512(Z, tab, r);
+        wave_fft512(Z, w5, wb5, r);
         PR_STAMP(5);
         float* o = out + (b * n_pairs + pair) * (int64_t)S;
         const float inv = 1.0f / (float)PR_NB;
@@ -638,14 +647,17 @@ __global__ __launch_bounds__(PR_T) void k_fe_wavelet8k(
 #pragma unroll
         for (int k2 = 1; k2 < 16; ++k2) img[pr_pos(t + 512 * k2)] = F2(pmul(v[k2], w[k2 - 1]));
     }
+    // the pass-2 twiddles in flight across the barrier (as k_fe_pairs8k)
+    c2 w2[15];
+#pragma unroll
+    for (int kb = 1; kb < 16; ++kb) w2[kb - 1] = C2(tab[TW8K_T2 + 32 * (kb - 1) + (t & 31)]);
     __syncthreads();
     // pass 2: radix-16 over n1b inside block k2 (as k_fe_pairs8k)
     {
         const int k2 = t >> 5, n1a = t & 31;
         float2* base = img + k2 * 528 + n1a;
-        c2 w[15], x[16];
-#pragma unroll
-        for (int kb = 1; kb < 16; ++kb) w[kb - 1] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
+        c2 x[16];
+        const c2* w = w2;
 #pragma unroll
         for (int n1b = 0; n1b < 16; ++n1b) x[n1b] = C2(base[33 * n1b]);
         pdft16(x);
