@@ -91,7 +91,10 @@ __global__ __launch_bounds__(256) void k_fe_lowpass_lds(const float* __restrict_
     const int c = step * (m + start);
     float acc = 0.f;
     if (c - radius >= 0 && c + radius < n_pad) {
-        for (int d = -radius; d <= radius; ++d) acc += xp[c - d] * h0[d < 0 ? -d : d];
+        // unrolled (eight LDS reads and scalar weight loads in flight, not one round trip per
+        // tap) with the fma spelled out, as the one-at-a-time loop compiled it: the same bits
+#pragma unroll 8
+        for (int d = -radius; d <= radius; ++d) acc = fmaf(xp[c - d], h0[d < 0 ? -d : d], acc);
     } else {
         for (int d = -radius; d <= radius; ++d) {
             int n = (c - d) % n_pad;
