@@ -358,7 +358,8 @@ __global__ __launch_bounds__(NT) void k_colred16(const float* __restrict__ part,
     const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
     if (c >= n) return;
     float a = 0.f;
-    for (int b = lane; b < blocks; b += 64) a += part[(int64_t)b * n + c];
+#pragma unroll 8
+    for (int b = lane; b < blocks; b += 64) a += part[(int64_t)b * n + c];   // 8 loads in flight, same order
     a = wave_sum(a);
     if (lane != 0) return;
     float* dst = c < split ? out0 + c : out1 + (c - split);
@@ -373,7 +374,8 @@ __global__ __launch_bounds__(NT) void k_reduce_parts(const float* __restrict__ p
     __shared__ float red[16];
     const int c = blockIdx.x;
     float a = 0.f;
-    for (int b = threadIdx.x; b < blocks; b += NT) a += part[(int64_t)b * n + c];
+#pragma unroll 8
+    for (int b = threadIdx.x; b < blocks; b += NT) a += part[(int64_t)b * n + c];   // 8 loads in flight, same order
     a = block_sum(a, red);
     if (threadIdx.x == 0) {
         float* o = c < split ? out0 + c : out1 + (c - split);
