@@ -429,8 +429,10 @@ __global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ pa
     const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * 64 + o;
     float a = 0.f;
-    if (i < n)
-        for (int s = sl; s < splits; s += 4) a += part[(int64_t)s * n + i];
+    if (i < n) {
+#pragma unroll 8
+        for (int s = sl; s < splits; s += 4) a += part[(int64_t)s * n + i];   // 8 loads in flight, same order
+    }
     red[sl][o] = a;
     __syncthreads();
     if (sl == 0 && i < n) {

@@ -268,7 +268,8 @@ __global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ 
     __shared__ float red[16];
     const int n = blockIdx.x;
     float a = 0.f;
-    for (int b = threadIdx.x; b < blocks; b += 256) a += partial[(int64_t)b * N + n];
+#pragma unroll 8
+    for (int b = threadIdx.x; b < blocks; b += 256) a += partial[(int64_t)b * N + n];   // 8 loads in flight, same order
     a = block_sum(a, red);
     if (threadIdx.x == 0) out[n] = accumulate ? out[n] + a : a;
 }
