@@ -10,7 +10,10 @@ fetal-monitoring windows (vaeteb.synthetic; the clinical HDF5 records are not
 available), weights are the reference architecture's random init.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--frontend j11|j6] [--batch B] [--workload c2|c4|c5]
-  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+  N > 1: either form works —
+    python bench.py --gpus N          (starts N rank processes itself, vaeteb.train.spawn_local_ranks)
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+  VAETEB_DIST_BACKEND=gloo: gloo instead of RCCL, ranks share the visible GPUs (one-GPU rehearsal)
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel, timed
 live with HIP events on its own stream inside the timed region; `cpu_baseline`
@@ -32,7 +35,7 @@ import torch.distributed as dist  # noqa: E402
 from vaeteb import _lib, synthetic  # noqa: E402
 from vaeteb.frontend import FrontEnd, FrontEndPlan, load_stats  # noqa: E402
 from vaeteb.model import SeqVaeTeb  # noqa: E402
-from vaeteb.train import Trainer, init_distributed  # noqa: E402
+from vaeteb.train import Trainer, init_distributed, spawn_local_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 FRONTENDS = {"j11": (11, 4, 16), "j6": (6, 1, 16)}
@@ -352,6 +355,10 @@ def main():
                     help="encoder LSTMs: 16-bit MFMA recurrences over 4-sample tiles (f16 forward / bf16 backward "
                          "operands, fp32 state: the reference's own 16-mixed LSTM width) or exact fp32")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without torchrun: N fresh rank processes (before this
+        # process touches the GPU), rank 0's JSON line relayed, the first failure's exit code
+        sys.exit(spawn_local_ranks([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], args.gpus))
     global OUT
     OUT = _json_stdout()
 
@@ -633,6 +640,8 @@ def main():
                           "formula": "value x bytes_per_sample / (n_gpus x 8e12); bytes_per_sample = front-end "
                                      "+ 4,161,024 activation elements x 2 B x 4 + 46 B x params / batch"},
     }
+    if dist.is_initialized():
+        out["dist_backend"] = dist.get_backend()   # "nccl" = RCCL on ROCm
     hbm = pmc_kernels() if (J, Q, T, B) == (11, 4, 16, 256) and not c4 else None
     if hbm:
         out["hbm_kernels"] = hbm

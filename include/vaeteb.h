@@ -597,12 +597,13 @@ int vt_add_act_fwd(const float* A, const float* Bm, int64_t n, int act, float* Y
  * L > 0 on (B, L, C) data, the (sample, channel) pair (nn.Dropout1d drops whole
  * channels).  The same call with the same seed is the backward (in place ok).
  * replaces: nn.Dropout / nn.Dropout1d in ref/model/inception_time.py:78,139,209,247,251 */
-int vt_dropout_apply(const float* X, int64_t n, int C, int L, float p, int64_t seed, float* Y, void* stream);
-/* a device uint64 added to every dropout / attention-dropout seed (nullptr: none), and its
- * per-step advance: a captured step (host seeds frozen at capture) replayed by the native
- * executor then draws new masks every replay; the forward and the backward of a step read the
- * same offset (it advances once, at the step's start) */
-int vt_dropout_set_seed_offset(const void* offset);
+int vt_dropout_apply(const float* X, int64_t n, int C, int L, float p, int64_t seed, const void* seed_offset, float* Y,
+                     void* stream);
+/* seed_offset (vt_dropout_apply, vt_attn_fwd / _bwd): a device uint64 the caller owns, added to
+ * the host seed (nullptr: none; read only when p > 0), and its per-step advance: a captured step
+ * (host seeds frozen at capture) replayed by the native executor then draws new masks every
+ * replay; the forward and the backward of a step pass the same offset (it advances once, at the
+ * step's start).  Passed per call: no process-wide state, so two models never share an offset. */
 int vt_dropout_seed_advance(void* offset, void* stream);
 /* Mean over t of (B, L, C) -> (B, C); backward dX (+)= dY / L broadcast.
  * replaces: AdaptiveAvgPool1d(1) + squeeze (ref/model/inception_time.py:243,320-321) */
@@ -615,10 +616,10 @@ int vt_time_mean_bwd(const float* dY, int B, int L, int C, float* dX, int accumu
  * vt_dropout_apply hash over (b, h, query, key).
  * replaces: nn.MultiheadAttention(128, 4, dropout, batch_first=True) core
  *           (ref/model/inception_time.py:236-242, :306-309)                     */
-int vt_attn_fwd(const float* qkv, int B, int S, int H, float scale, float p, int64_t seed, float* out, float* lse,
-                void* stream);
+int vt_attn_fwd(const float* qkv, int B, int S, int H, float scale, float p, int64_t seed, const void* seed_offset,
+                float* out, float* lse, void* stream);
 int vt_attn_bwd(const float* qkv, const float* out, const float* dout, const float* lse, int B, int S, int H,
-                float scale, float p, int64_t seed, float* dqkv, void* stream);
+                float scale, float p, int64_t seed, const void* seed_offset, float* dqkv, void* stream);
 /* nn.CrossEntropyLoss (mean) over logits (B, C), int64 labels: loss[0] and the
  * softmax probabilities; backward dlogits = g[0] * (probs - onehot) / B with
  * g a device scalar (the upstream gradient).

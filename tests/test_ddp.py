@@ -156,3 +156,59 @@ def test_broadcast_state_starts_every_rank_from_rank0():
     for x0, y0, y1 in zip(b0, a0, a1):
         assert (x0 == y0).all() and (y0 == y1).all()             # rank 0 unchanged, rank 1 = rank 0
     assert (p0 == p1).all()
+
+
+def _bufsync_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "vae-teb_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vaeteb.train import BufferBroadcast
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.BatchNorm1d(16), torch.nn.ReLU(),
+                                torch.nn.Linear(16, 4), torch.nn.BatchNorm1d(4)).train()
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    bs = BufferBroadcast(model)
+    same_values = all(torch.equal(sd0[k], v) for k, v in model.state_dict().items())
+    res = []
+    for step in range(3):
+        bs()                                   # rank 0's statistics before the forward (DDP)
+        before = [b.numpy().copy() for b in model.buffers() if b.is_floating_point()]
+        g = torch.Generator().manual_seed(10 * step + rank)
+        model(torch.randn(32, 8, generator=g) * (rank + 1)).sum().backward()   # rank-local statistics
+        res.append((before, [b.detach().numpy().copy() for b in model.buffers() if b.is_floating_point()]))
+    # a replaced buffer (load_state_dict(assign=True)) is rebound on the next call
+    model.load_state_dict({k: v.clone() for k, v in model.state_dict().items()}, assign=True)
+    bs()
+    rebound = bs.bound()
+    # numpy, not tensors: shared-memory tensor handles can outlive a worker that exits first
+    q.put((rank, same_values, res, rebound, [b.numpy().copy() for b in model.buffers() if b.is_floating_point()]))
+    dist.destroy_process_group()
+
+
+def test_buffer_broadcast_every_step():
+    """DDP broadcast_buffers=True (the reference's DDP wrap, graph_model.py:644, and Lightning's
+    DDPStrategy): before every step every rank holds rank 0's BatchNorm running statistics, though
+    each rank's forward updated them from its own shard; one flat collective per step; state_dict
+    values unchanged by the flattening; a replaced buffer is rebound."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bufsync_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, s0, r0, b0, f0), (_, s1, r1, b1, f1) = out
+    assert s0 and s1 and b0 and b1
+    for step in range(3):
+        for a, b in zip(r0[step][0], r1[step][0]):
+            assert (a == b).all()                        # synced before the forward
+        assert any((a != b).any() for a, b in zip(r0[step][1], r1[step][1]))   # local updates differ
+        if step:
+            for a, b in zip(r0[step][0], r0[step - 1][1]):
+                assert (a == b).all()                    # rank 0 keeps its own statistics
+    for a, b in zip(f0, f1):
+        assert (a == b).all()

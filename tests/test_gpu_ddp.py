@@ -153,3 +153,28 @@ def test_segmented_native_replay_equals_eager_ddp_step():
         assert o_e == o_n, (rank, o_e, o_n)
         assert (p_e == p_n).all() and (m_e == m_n).all() and (v_e == v_n).all(), rank
     assert (out[0][1][1][1] == out[1][1][1][1]).all()        # the same model on both ranks
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` starts its own two ranks (no torchrun),
+    here with VAETEB_DIST_BACKEND=gloo so both share this box's one GPU.  Exactly one JSON line
+    reaches stdout (rank 0's), it reports the whole job (2 GPUs, global batch 512), the mode
+    names the gradient buckets all-reduced from the segmented native replay, and the ELBO of the
+    last step is finite; every rank ran the barrier / max-over-ranks timing (else rank 0 hangs)."""
+    import json
+    import math
+    import subprocess
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, VAETEB_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup",
+                        "1", "--no-cpu-baseline"], env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 512 and out["config"]["parallelism"] == "dp2"
+    assert "gradient buckets" in out["mode"] and out.get("dist_backend") == "gloo", out["mode"]
+    assert out["value"] > 0 and all(math.isfinite(v) for v in out["elbo"].values()), out["elbo"]
+    assert "cpu_baseline" not in out

@@ -433,6 +433,78 @@ def test_native_executor_bitwise_identical_to_eager(golden, n_streams):
         assert torch.equal(a, b)
 
 
+def test_first_writer_group_reached_through_autograd():
+    """Advisor r04 (low): once a first-writer group (a >= 2^20-element linear weight + bias)
+    is confirmed, zero_grad leaves its range unzeroed for LinearF to overwrite.  A later step
+    whose gradient for that weight arrives through autograd (AccumulateGrad, here F.linear)
+    must see a zeroed range (not last step's values) and keep its gradient (not be zeroed
+    after the backward)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vaeteb import ops
+    from vaeteb.train import FlatState
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(1024, 1024).cuda()
+    st = FlatState(lin)
+    assert len(st.first_writer) == 1
+    x = torch.randn(64, 1024, device="cuda")
+    for i in range(3):                                # LinearF steps: the group gets confirmed
+        st.zero_grad(first_writer=True)
+        ops.LinearF.apply(x * (i + 1), lin.weight, lin.bias, False).square().sum().backward()
+        st.finish_first_writer()
+    assert st._fw_ok == {0}
+    st.zero_grad(first_writer=True)                   # group left unzeroed (holds step 3's gradient)
+    torch.nn.functional.linear(x, lin.weight, lin.bias).square().sum().backward()
+    st.finish_first_writer()
+    torch.cuda.synchronize()
+    ref = torch.nn.Linear(1024, 1024).cuda()
+    ref.load_state_dict(lin.state_dict())
+    torch.nn.functional.linear(x, ref.weight, ref.bias).square().sum().backward()
+    torch.testing.assert_close(lin.weight.grad, ref.weight.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(lin.bias.grad, ref.bias.grad, rtol=1e-5, atol=1e-5)
+    assert st._fw_ok == set() and 0 in st._fw_bad     # demoted: zeroed with the rest from now on
+
+
+def test_native_replay_after_load_state_dict(golden):
+    """Advisor r04 (medium): the captured forward trusts the bf16 head / conv shadows the
+    optimizer pass wrote.  After a load_state_dict between replays the replay must compute with
+    the LOADED weights (CapturedStep re-checks the weights' version counters and rewrites the
+    shadows), exactly as an eager step from the same loaded state does — bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from golden_util import det_fill_
+    from vaeteb.model import SeqVaeTeb
+    from vaeteb.train import Trainer
+    g = golden("model_s16_b4")
+    T = lambda k: torch.from_numpy(g[k]).cuda()
+    b0 = {"fhr_st": T("y_st"), "fhr_ph": T("y_ph"), "fhr_up_ph": T("x_ph"), "fhr": T("y_raw")}
+    b1 = {k: v.flip(0).contiguous() for k, v in b0.items()}
+    eps0 = T("eps")
+    torch.manual_seed(7)
+    src = SeqVaeTeb(sequence_length=16)   # another model's weights (default init, not det_fill_)
+    loaded = {k: v.cuda() for k, v in src.state_dict().items()}
+    res = []
+    for native in (False, True):
+        m = det_fill_(SeqVaeTeb(sequence_length=16, concurrent_encoders=True, head_precision="bf16",
+                                conv_precision="bf16", mlp_precision="bf16")).cuda()
+        tr = Trainer(m, lr=1e-3)
+        if native:
+            tr.capture(b0, eps=eps0, warmup=2, native=True)
+            outs = [tr.replay(b1, eps=eps0)["total_loss"].item()]
+        else:
+            for _ in range(2):
+                tr.step(b0, eps=eps0)
+            outs = [tr.step(b1, eps=eps0)["total_loss"].item()]
+        torch.cuda.synchronize()
+        m.load_state_dict(loaded)
+        step = tr.replay if native else tr.step
+        outs += [step(b, eps=eps0)["total_loss"].item() for b in (b0, b1)]
+        torch.cuda.synchronize()
+        res.append((outs, tr.state.p.clone()))
+    assert res[0][0] == res[1][0], (res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("B", [4, 256])
 def test_native_executor_with_frontend_bitwise_identical_to_eager(B):
     """The step captured from RAW windows (the front-end inside the graph, its cross pairs

@@ -81,3 +81,31 @@ def test_reference_oracle_state_dict_loads_into_hip_model():
     m.load_state_dict(ref.state_dict(), strict=True)
     assert len(ref.state_dict()) == len(m.state_dict())
     assert "torch" in sys.modules
+
+
+def test_flat_adamw_loads_unpadded_moments():
+    """Advisor r04: optimizer checkpoints written before the 64-float alignment of the >= 2^20
+    element parameters (flat moments back to back) still load, remapped per parameter; the
+    current layout round-trips; any other length raises."""
+    from vaeteb.lightning import FlatAdamW
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(1024, 1024), torch.nn.Linear(1024, 3))
+    opt = FlatAdamW(net)
+    s = opt.flat
+    n_par = sum(n for _, n in s.offsets)
+    assert s.numel > n_par                     # the 2^20-element weight was padded to 64 floats
+    old_m, old_v = torch.randn(n_par), torch.randn(n_par)
+    sd = {"param_groups": opt.param_groups, "step": torch.tensor([5], dtype=torch.int32), "exp_avg": old_m,
+          "exp_avg_sq": old_v}
+    opt.load_state_dict(sd)
+    o_old = 0
+    for (o, n), p in zip(s.offsets, s.params):
+        assert torch.equal(s.m[o:o + n], old_m[o_old:o_old + n]) and torch.equal(s.v[o:o + n], old_v[o_old:o_old + n])
+        o_old += n
+    assert int(opt.step_dev.item()) == 5
+    cur = opt.state_dict()
+    opt2 = FlatAdamW(net)
+    opt2.load_state_dict(cur)
+    assert torch.equal(opt2.flat.m, s.m) and torch.equal(opt2.flat.v, s.v)
+    with pytest.raises(ValueError, match="moments"):
+        opt2.load_state_dict(dict(sd, exp_avg=torch.zeros(7), exp_avg_sq=torch.zeros(7)))

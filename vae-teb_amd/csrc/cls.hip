@@ -316,7 +316,7 @@ __device__ __forceinline__ uint32_t drop_threshold(float p) {
     return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
-// Device-side seed offset (vt_dropout_set_seed_offset): added to every dropout seed, advanced
+// Device-side seed offset (the seed_offset argument of the dropout / attention calls): added to every dropout seed, advanced
 // once per training step on the device (vt_dropout_seed_advance), so a captured step replayed
 // by the native executor draws new masks each replay (its host seeds are frozen at capture).
 __device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* __restrict__ soff) {
@@ -686,11 +686,10 @@ int vt_add_act_fwd(const float* A, const float* Bm, int64_t n, int act, float* Y
     return VT_OK;
 }
 
-static const uint64_t* g_seed_off = nullptr;
-
-int vt_dropout_set_seed_offset(const void* offset) {
-    g_seed_off = reinterpret_cast<const uint64_t*>(offset);
-    return VT_OK;
+// the seed offset is read only when something is dropped (p > 0): a caller without one, or an
+// eval / p = 0 call, passes nothing the kernels would dereference
+static inline const uint64_t* seed_off(const void* off, float p) {
+    return p > 0.f ? reinterpret_cast<const uint64_t*>(off) : nullptr;
 }
 
 int vt_dropout_seed_advance(void* offset, void* stream) {
@@ -700,10 +699,11 @@ int vt_dropout_seed_advance(void* offset, void* stream) {
     return VT_OK;
 }
 
-int vt_dropout_apply(const float* X, int64_t n, int C, int L, float p, int64_t seed, float* Y, void* stream) {
+int vt_dropout_apply(const float* X, int64_t n, int C, int L, float p, int64_t seed, const void* seed_offset, float* Y,
+                     void* stream) {
     VT_CHECK_ARG(n > 0 && C > 0 && L >= 0 && p >= 0.f && p < 1.f, "vt_dropout_apply: args (0 <= p < 1)");
     hipLaunchKernelGGL(k_dropout, dim3(ew_blocks(n)), dim3(256), 0, S(stream), X, n, C, L, p, (uint64_t)seed,
-                       g_seed_off, Y);
+                       seed_off(seed_offset, p), Y);
     VT_LAUNCH_CHECK("vt_dropout_apply");
     return VT_OK;
 }
@@ -723,22 +723,22 @@ int vt_time_mean_bwd(const float* dY, int B, int L, int C, float* dX, int accumu
     return VT_OK;
 }
 
-int vt_attn_fwd(const float* qkv, int B, int S_, int H, float scale, float p, int64_t seed, float* out, float* lse,
-                void* stream) {
+int vt_attn_fwd(const float* qkv, int B, int S_, int H, float scale, float p, int64_t seed, const void* seed_offset,
+                float* out, float* lse, void* stream) {
     VT_CHECK_ARG(B > 0 && H > 0 && S_ > 0 && S_ % 16 == 0 && S_ <= 256 && p >= 0.f && p < 1.f,
                  "vt_attn_fwd: S multiple of 16 <= 256, 0 <= p < 1");
     hipLaunchKernelGGL(k_attn_fwd, dim3(cdiv(S_, 64), B * H), dim3(256), 0, S(stream), qkv, S_, H, scale, p,
-                       (uint64_t)seed, g_seed_off, out, lse);
+                       (uint64_t)seed, seed_off(seed_offset, p), out, lse);
     VT_LAUNCH_CHECK("vt_attn_fwd");
     return VT_OK;
 }
 
 int vt_attn_bwd(const float* qkv, const float* out, const float* dout, const float* lse, int B, int S_, int H,
-                float scale, float p, int64_t seed, float* dqkv, void* stream) {
+                float scale, float p, int64_t seed, const void* seed_offset, float* dqkv, void* stream) {
     VT_CHECK_ARG(B > 0 && H > 0 && S_ > 0 && S_ % 16 == 0 && S_ <= 256 && p >= 0.f && p < 1.f,
                  "vt_attn_bwd: S multiple of 16 <= 256, 0 <= p < 1");
     hipLaunchKernelGGL(k_attn_bwd, dim3(B * H), dim3(256), 0, S(stream), qkv, out, dout, lse, S_, H, scale, p,
-                       (uint64_t)seed, g_seed_off, dqkv);
+                       (uint64_t)seed, seed_off(seed_offset, p), dqkv);
     VT_LAUNCH_CHECK("vt_attn_bwd");
     return VT_OK;
 }

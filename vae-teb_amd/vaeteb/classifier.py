@@ -31,8 +31,20 @@ from .ops import ACT, WS, _check, _ParamGrads, _st
 _BN_WS = 4096 * 128 + 256
 
 
+# the device seed offset of the classifier whose training forward is running (set for the
+# duration of FHRInceptionTimeClassifier.forward): each dropout op keeps it with its host seed
+_SEED_OFF = None
+
+
 def _seed():
-    return int(torch.randint(0, 2 ** 62, (1,)).item())
+    """(host seed, device seed offset or None) of one dropout / attention-dropout op; the op
+    keeps the pair for its backward (the same masks)."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item()), _SEED_OFF
+
+
+def _sarg(seed):
+    """The (seed, seed_offset pointer) call arguments of a _seed() pair (0 / NULL: no dropout)."""
+    return (seed[0], ptr(seed[1])) if isinstance(seed, tuple) else (int(seed), None)
 
 
 def _col(t, c0):
@@ -75,7 +87,7 @@ class _InceptionF(torch.autograd.Function):
         call("vt_batchnorm_fwd", ptr(cat), B * L, C4, ptr(g), ptr(b), ACT["relu"], eps, momentum, ptr(y), ptr(mean),
              ptr(rstd), ptr(run_mean), ptr(run_var), ptr(bws), bws.numel(), st)
         if p > 0:
-            call("vt_dropout_apply", ptr(y), y.numel(), C4, L, float(p), seed, ptr(y), st)
+            call("vt_dropout_apply", ptr(y), y.numel(), C4, L, float(p), *_sarg(seed), ptr(y), st)
         ctx.save_for_backward(x, x0, mp, cat, mean, rstd)
         ctx.params = (wb1, ws, wm, wl, wb2, g, b)
         ctx.cfg = (p, seed)
@@ -93,7 +105,7 @@ class _InceptionF(torch.autograd.Function):
         gy = gy.contiguous()
         if p > 0:
             gd = torch.empty_like(gy)
-            call("vt_dropout_apply", ptr(gy), gy.numel(), C4, L, float(p), seed, ptr(gd), st)
+            call("vt_dropout_apply", ptr(gy), gy.numel(), C4, L, float(p), *_sarg(seed), ptr(gd), st)
             gy = gd
         gcat = torch.empty_like(cat)
         pbn = _ParamGrads([g, b], [True, True])
@@ -148,7 +160,7 @@ class _ResidualF(torch.autograd.Function):
         out = s
         if p > 0:
             out = torch.empty_like(s)
-            call("vt_dropout_apply", ptr(s), s.numel(), C4, L, float(p), seed, ptr(out), st)
+            call("vt_dropout_apply", ptr(s), s.numel(), C4, L, float(p), *_sarg(seed), ptr(out), st)
         ctx.save_for_backward(x, r, s, mean, rstd)
         ctx.params = (w, g, b)
         ctx.cfg = (p, seed)
@@ -166,7 +178,7 @@ class _ResidualF(torch.autograd.Function):
         gs = torch.empty_like(s)
         src = gout
         if p > 0:
-            call("vt_dropout_apply", ptr(gout), gout.numel(), C4, L, float(p), seed, ptr(gs), st)
+            call("vt_dropout_apply", ptr(gout), gout.numel(), C4, L, float(p), *_sarg(seed), ptr(gs), st)
             src = gs
         call("vt_act_bwd", ptr(src), ptr(s), s.numel(), ACT["relu"], ptr(gs), st)
         gr = torch.empty_like(r)
@@ -199,7 +211,7 @@ class _AttnCoreF(torch.autograd.Function):
         scale = 1.0 / math.sqrt(E // H)
         out = torch.empty((B, S, E), device=qkv.device)
         lse = torch.empty((B, H, S), device=qkv.device)
-        call("vt_attn_fwd", ptr(qkv), B, S, H, scale, float(p), seed, ptr(out), ptr(lse), _st())
+        call("vt_attn_fwd", ptr(qkv), B, S, H, scale, float(p), *_sarg(seed), ptr(out), ptr(lse), _st())
         ctx.save_for_backward(qkv, out, lse)
         ctx.cfg = (H, scale, p, seed)
         return out
@@ -210,7 +222,7 @@ class _AttnCoreF(torch.autograd.Function):
         H, scale, p, seed = ctx.cfg
         B, S, _ = qkv.shape
         dqkv = torch.empty_like(qkv)
-        call("vt_attn_bwd", ptr(qkv), ptr(out), ptr(gout.contiguous()), ptr(lse), B, S, H, scale, float(p), seed,
+        call("vt_attn_bwd", ptr(qkv), ptr(out), ptr(gout.contiguous()), ptr(lse), B, S, H, scale, float(p), *_sarg(seed),
              ptr(dqkv), _st())
         return dqkv, None, None, None
 
@@ -253,7 +265,7 @@ class _DropoutF(torch.autograd.Function):
         _check(x)
         x = x.contiguous()
         y = torch.empty_like(x)
-        call("vt_dropout_apply", ptr(x), x.numel(), x.shape[-1], 0, float(p), seed, ptr(y), _st())
+        call("vt_dropout_apply", ptr(x), x.numel(), x.shape[-1], 0, float(p), *_sarg(seed), ptr(y), _st())
         ctx.cfg = (p, seed)
         return y
 
@@ -262,7 +274,7 @@ class _DropoutF(torch.autograd.Function):
         p, seed = ctx.cfg
         gy = gy.contiguous()
         gx = torch.empty_like(gy)
-        call("vt_dropout_apply", ptr(gy), gy.numel(), gy.shape[-1], 0, float(p), seed, ptr(gx), _st())
+        call("vt_dropout_apply", ptr(gy), gy.numel(), gy.shape[-1], 0, float(p), *_sarg(seed), ptr(gx), _st())
         return gx, None, None
 
 
@@ -463,19 +475,27 @@ class FHRInceptionTimeClassifier(nn.Module):
                                         Activation("dropout"), Linear(f, num_classes))
 
     def forward(self, x):
-        tr = self.training
-        if tr and self.dropout > 0 and x.is_cuda:
+        global _SEED_OFF
+        if self.training and self.dropout > 0 and x.is_cuda:
             # a device-side seed offset added to every host-drawn dropout seed.  Eager steps draw
             # fresh host seeds (torch's CPU generator: torch.manual_seed makes runs repeatable);
             # a captured step freezes them, so its forward advances the offset on the device
             # once (a kernel in the graph): every replay draws new masks, and its backward reads
-            # the same offset as its forward
+            # the same offset as its forward (each op keeps this model's offset tensor, _seed())
             off = getattr(self, "_seed_off", None)
             if off is None or off.device != x.device:
                 self._seed_off = off = torch.zeros(1, dtype=torch.int64, device=x.device)
-            _lib.lib().fns["vt_dropout_set_seed_offset"](off.data_ptr())
             if torch.cuda.is_current_stream_capturing():
                 call("vt_dropout_seed_advance", off.data_ptr(), _st())
+            prev, _SEED_OFF = _SEED_OFF, off
+            try:
+                return self._forward(x)
+            finally:
+                _SEED_OFF = prev
+        return self._forward(x)
+
+    def _forward(self, x):
+        tr = self.training
         ip = self.input_projection
         h = ip[0](x)
         h = _ActF.apply(ip[1](h), "gelu")

@@ -92,10 +92,30 @@ class FlatAdamW:
                 "exp_avg": self.flat.m.clone(), "exp_avg_sq": self.flat.v.clone()}
 
     def load_state_dict(self, sd):
+        """The flat moments as saved, or as saved before round 4 added the 64-float alignment of
+        the >= 2^20-element parameters (the same parameters back to back, no padding): those are
+        remapped parameter by parameter.  Any other length raises."""
+        s = self.flat
+        n_old = sd["exp_avg"].numel()
+        if n_old == s.numel:
+            remap = None
+        elif n_old == sum(n for _, n in s.offsets):
+            remap = s.offsets
+        else:
+            raise ValueError(f"FlatAdamW.load_state_dict: {n_old} moments for {s.numel} flat elements "
+                             f"({sum(n for _, n in s.offsets)} parameters)")
         self.param_groups = [dict(g) for g in sd["param_groups"]]
         self.step_dev.copy_(sd["step"])
-        self.flat.m.copy_(sd["exp_avg"])
-        self.flat.v.copy_(sd["exp_avg_sq"])
+        for dst, src in ((s.m, sd["exp_avg"]), (s.v, sd["exp_avg_sq"])):
+            src = src.to(dst.device)
+            if remap is None:
+                dst.copy_(src)
+                continue
+            dst.zero_()   # the padding elements hold zero moments (zero gradient, zero update)
+            o_old = 0
+            for o, n in remap:
+                dst[o:o + n].copy_(src[o_old:o_old + n])
+                o_old += n
 
 
 class CosineAnnealingWarmRestarts:
@@ -274,9 +294,12 @@ def fit(module, train_loader, max_epochs=1, gradient_clip_val=0.5, val_loader=No
     opt.max_norm = gradient_clip_val
     buckets = None
     if world > 1:
-        from .train import GradBuckets, broadcast_state
+        from .train import BufferBroadcast, GradBuckets, broadcast_state
         broadcast_state(opt.flat, module.model, group)   # DDP: every rank starts from rank 0's model
         buckets = GradBuckets(opt.flat, group)
+        # DDPStrategy's broadcast_buffers=True: rank 0's BatchNorm statistics before every step
+        # (SyncBatchNorm keeps them identical already)
+        bsync = None if sync_batchnorm else BufferBroadcast(module.model, group)
         opt.pre_scale = 1.0 / world
     mv = lambda b: to_device(b) if to_device else b
     for epoch in range(module.current_epoch, max_epochs):
@@ -287,6 +310,8 @@ def fit(module, train_loader, max_epochs=1, gradient_clip_val=0.5, val_loader=No
             opt.zero_grad()
             if buckets is not None:
                 buckets.reset()
+                if bsync is not None:
+                    bsync()
             loss = module.training_step(mv(batch), i)
             loss.backward()
             _join_side_streams()

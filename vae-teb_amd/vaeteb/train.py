@@ -91,13 +91,32 @@ class FlatState:
         if o0 < self.numel:
             self._zero_ranges.append((o0, self.numel))
         self._fw_ok, self._fw_bad = set(), set()   # groups confirmed / seen written by another op
+        # a gradient of a first-writer weight that reaches it through autograd (AccumulateGrad:
+        # LinearF without its in-place path, or another op using the weight) while the group's
+        # range is still unzeroed: the group is zeroed right before that accumulation
+        for grp in self.first_writer:
+            for q in grp:
+                q.register_hook(lambda grad, key=id(grp[0]): FlatState._fw_before_accumulate(key, grad))
+
+    @staticmethod
+    def _fw_before_accumulate(key, grad):
+        from . import ops
+        ent = ops.FIRST_WRITER.get(key)
+        if ent is not None and ent[1]:
+            with torch.no_grad():
+                for q in ent[0]:
+                    q.grad.zero_()
+            ent[1] = False   # now zeroed: later writers of this step accumulate, nothing is dropped
+        return grad
 
     def zero_grad(self, first_writer=False):
         """first_writer (Trainer steps: one forward / backward per zero_grad): a first-writer
         group is left unzeroed once a step has shown that its weight gradient comes from one
         first-writer-aware kernel call (vaeteb.ops.LinearF); until then it is zeroed like the
         rest (and any group the step does not write is zeroed after the backward,
-        finish_first_writer), so an op that accumulates into it never sees stale values."""
+        finish_first_writer).  A gradient that reaches an unzeroed group through autograd
+        instead zeroes the group first (_fw_before_accumulate) and demotes it, so an op that
+        accumulates into it never sees stale values and no gradient is dropped."""
         if first_writer and self.first_writer:
             from . import ops
             ranges = self._zero_ranges if len(self._fw_ok) == len(self.first_writer) else None
@@ -150,6 +169,52 @@ def broadcast_state(state, module, group=None, src=0):
     dist.broadcast(state.p, src=src, group=group)
     for b in module.buffers():
         dist.broadcast(b, src=src, group=group)
+
+
+class BufferBroadcast:
+    """DistributedDataParallel's `broadcast_buffers=True` — the default of the reference's DDP
+    wrap (ref/model/graph_model.py:644) and of Lightning's DDPStrategy (:470-471): before every
+    training forward, rank `src`'s floating buffers (BatchNorm running mean / variance) overwrite
+    every other rank's, so ranks never drift apart and checkpoints / eval-mode validation see
+    rank 0's statistics on every rank.  One collective per step: the buffers are rebound as views
+    of one flat tensor (state_dict keys and values unchanged; rebound again if a buffer is
+    replaced, e.g. by .to() or load_state_dict(assign=True)).  The step counters
+    (num_batches_tracked) advance identically on every rank and are not sent."""
+
+    def __init__(self, module, group=None, src=0):
+        self.module, self.group, self.src = module, group, src
+        self.flat, self.views = None, []
+        self._bind()
+
+    def _bind(self):
+        ents = [(m, n, b) for m in self.module.modules() for n, b in m._buffers.items()
+                if b is not None and b.is_floating_point()]
+        self.views = []
+        if not ents:
+            self.flat = None
+            return
+        with torch.no_grad():
+            self.flat = torch.cat([b.detach().reshape(-1).float() for _, _, b in ents])
+            o = 0
+            for m, n, b in ents:
+                v = self.flat[o:o + b.numel()].view(b.shape)
+                o += b.numel()
+                if b.dtype != torch.float32:
+                    raise ValueError(f"BufferBroadcast: buffer {n} is {b.dtype}, only float32 buffers are flattened")
+                m._buffers[n] = v
+                self.views.append((m, n, v))
+
+    def bound(self):
+        return all(m._buffers.get(n) is v for m, n, v in self.views)
+
+    def __call__(self):
+        if self.flat is None:
+            return
+        if not self.bound():
+            if self.flat.is_cuda and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("BufferBroadcast: buffers were replaced after a step was captured")
+            self._bind()
+        dist.broadcast(self.flat, src=self.src, group=self.group)
 
 
 class GradBuckets:
@@ -313,12 +378,14 @@ class Trainer:
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=1e-4, max_norm=1.0, beta_kld=1e-5,
                  frontend=None, world_size=1, group=None, bucket_mb=64.0, vae_loss_weight=0.1,
-                 reduce_dtype=torch.float32, ddp=None):
+                 reduce_dtype=torch.float32, ddp=None, broadcast_buffers=True):
         """ddp: the bucketed gradient all-reduce (GradBuckets) on (True) / off (False);
         default on exactly when world_size > 1.  ddp=True with one rank (an initialised
         single-rank process group) runs the data-parallel step's whole machinery — buckets,
         the world > 1 stream budget, the segmented native replay — at N = 1 (bench.py
-        --ddp-probe)."""
+        --ddp-probe).  broadcast_buffers (DDP's flag, default True as in the reference):
+        with several ranks, rank 0's BatchNorm running statistics are broadcast before every
+        step (BufferBroadcast)."""
         self.model = model
         self.vae_loss_weight = vae_loss_weight
         self.frontend = frontend
@@ -337,6 +404,7 @@ class Trainer:
         self.buckets = GradBuckets(self.state, group, bucket_mb, reduce_dtype) if ddp else None
         if ddp:
             broadcast_state(self.state, model, group)   # every rank starts from rank 0's model (DDP)
+        self.buffer_sync = BufferBroadcast(model, group) if (ddp and world_size > 1 and broadcast_buffers) else None
         if ddp and torch.cuda.is_available():
             # hardware-queue budget: a process's streams map onto GPU_MAX_HW_QUEUES = 4 queues;
             # the model uses main + 3 side streams on one GPU, and RCCL's stream would be a 5th
@@ -409,6 +477,8 @@ class Trainer:
         if self.buckets:
             self.buckets.reset()
             self.buckets.enabled = overlap_comm
+        if self.buffer_sync is not None and not (self.state.p.is_cuda and torch.cuda.is_current_stream_capturing()):
+            self.buffer_sync()   # DDP broadcast_buffers (under capture: CapturedStep.replay issues it)
         losses = self.loss(batch, eps)
         if BWD_SAME_THREAD:
             # the backward on this thread instead of autograd's device worker thread
@@ -533,6 +603,12 @@ class Trainer:
         torch.cuda.current_stream().wait_stream(side)
         if pre_capture is not None:
             pre_capture()
+        # the bf16 shadows the captured forward will trust instead of rewriting (written by the
+        # warmup steps' optimizer pass, ops._FRESH): CapturedStep.replay re-checks their weights'
+        # version counters, so a load_state_dict / copy_ between replays cannot leave the heads and
+        # convs computing with stale bf16 copies (advisor r04)
+        from . import ops
+        shadow_watch = [[ref, ver] for ref, ver in ops._FRESH.values()]
         graph = torch.cuda.CUDAGraph(keep_graph=native)
         comm = None
         if self.buckets is not None and native:
@@ -563,6 +639,7 @@ class Trainer:
         self.captured = CapturedStep(self, graph, static_in, static_eps, out, native=native, n_streams=n_streams,
                                      comm=comm)
         self.captured.update = update
+        self.captured.shadow_watch = shadow_watch
         return self.captured
 
     def replay(self, batch=None, eps=None):
@@ -624,6 +701,21 @@ class CapturedStep:
             self._st_addr = ctypes.addressof(self.streams)
             self._destroy = _lib.lib().fns["vt_stepgraph_destroy"]
 
+    shadow_watch = ()
+
+    def _refresh_shadows(self):
+        """The captured forward reads the bf16 shadows of the heads / convs as the optimizer
+        pass left them (the replay's own AdamW rewrites them, which does not touch torch's
+        version counters).  A weight changed from torch since (load_state_dict, copy_, another
+        optimizer) has a new version: its shadows are rewritten here, on the current stream,
+        before the launch."""
+        from . import ops
+        for e in self.shadow_watch:
+            w = e[0]()
+            if w is not None and w._version != e[1]:
+                (ops._weight_shadow if w.dim() == 2 else ops._conv_shadow)(w, prepass=True)
+                e[1] = w._version
+
     def _launch_range(self, begin, end, flags):
         _lib.call("vt_stepgraph_launch_range", self.handle, self._st_addr, begin, end, flags)
 
@@ -643,6 +735,9 @@ class CapturedStep:
         """One step.  A step captured with update=False issues clip + AdamW after the
         replay (adam_stream: the AdamW pass on that stream, see Trainer._update)."""
         tr = self.trainer
+        self._refresh_shadows()
+        if tr.buffer_sync is not None:
+            tr.buffer_sync()     # DDP broadcast_buffers: rank 0's BatchNorm statistics before the step
         if batch is not None:
             for k, v in batch.items():
                 if v.data_ptr() != self.static_in[k].data_ptr():
@@ -692,14 +787,83 @@ class CapturedStep:
 
 def init_distributed():
     """torchrun environment -> (rank, world, local_rank, device); RCCL on GPUs,
-    gloo on CPU-only hosts (the multi-process CPU tests)."""
+    gloo on CPU-only hosts (the multi-process CPU tests).
+
+    VAETEB_DIST_BACKEND=gloo|nccl overrides the backend.  With gloo on a GPU host the
+    ranks may outnumber the GPUs: rank r runs on cuda:(local_rank mod device_count),
+    so several ranks can share one GPU (RCCL refuses two ranks on one device) — the
+    one-GPU rehearsal of the multi-rank bench (tests/test_gpu_ddp.py)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    override = os.environ.get("VAETEB_DIST_BACKEND", "")
+    if override not in ("", "gloo", "nccl"):
+        raise ValueError(f"VAETEB_DIST_BACKEND must be gloo or nccl, got {override!r}")
+    cuda = torch.cuda.is_available()
+    if cuda and override == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1 and not dist.is_initialized():
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if torch.cuda.is_available():
+        backend = override or ("nccl" if cuda else "gloo")
+        if cuda:
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
-    dev = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device("cpu")
+    dev = torch.device(f"cuda:{local}") if cuda else torch.device("cpu")
     return rank, world, local, dev
+
+
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_local_ranks(cmd, n, env=None, poll_s=0.2, stdout=None):
+    """Start `n` ranks of `cmd` on this node, one process per GPU, and wait for them — the
+    reference's own launcher for its DDP loop (`mp.spawn(main_pytorch, nprocs=world_size)`,
+    ref/model/graph_model.py:2152-2157; torchrun in ref/run_train_ddp.sh:11-17) as fresh
+    processes, so the caller never touches the GPU itself (a process that has initialised
+    HIP must not fork / exec GPU workers).
+
+    Each rank gets RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = n and a free
+    MASTER_PORT on MASTER_ADDR 127.0.0.1.  Rank 0's stdout is relayed line by line to
+    `stdout` (default sys.stdout) after it exits; the other ranks' stdout goes to this
+    process's stderr.  When one rank fails, the others are terminated (they would wait in a
+    collective forever).  Returns the exit code of the rank that failed first (the ones
+    terminated because of it are not counted), else 0."""
+    import subprocess
+    import sys
+    import threading
+    import time
+    port = free_port()
+    procs, out0, failed, reader = [], [], None, None
+    try:
+        for r in range(n):
+            e = dict(os.environ if env is None else env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                     LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+            if r == 0:   # rank 0's pipe drained while it runs (never blocks on a full pipe)
+                reader = threading.Thread(target=lambda p=procs[0]: out0.extend(p.stdout), daemon=True)
+                reader.start()
+        while failed is None and None in [p.poll() for p in procs]:   # every rank polled
+            time.sleep(poll_s)
+            failed = next((p.returncode for p in procs if p.returncode not in (None, 0)), None)
+        if failed is None:
+            failed = next((p.returncode for p in procs if p.returncode != 0), None)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if reader is not None:
+        reader.join(timeout=10)
+    sink = stdout or sys.stdout
+    for line in out0:
+        sink.write(line.decode())
+    sink.flush()
+    return failed or 0
