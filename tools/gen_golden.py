@@ -483,6 +483,39 @@ def gen_traj():
     save("traj_s256_b2.npz", **d)
 
 
+TRAJ_LOW_LR = 1e-5
+
+
+def gen_traj_lowlr():
+    """the same 20-step trajectory (S = 256, B = 2, a new batch per step)
+    at lr = 1e-5, where the reference's own fp32 ensemble (fp64 + one-ulp perturbed members)
+    stays within ~1e-3 over all 20 steps — so a bound of 2x that envelope binds at EVERY step
+    (at lr 1e-3 the first AdamW step is chaotic and the envelope grows to O(1)).  Same runs as
+    gen_traj: fp32, fp64, the bf16 / fp16 autocast emulations, and perturbed members."""
+    S, B = 256, 2
+    name = "traj_s256_b2_lr1e-5.npz"
+    d = dict(S=S, B=B, steps=TRAJ_STEPS, seed_base=5000, lr=TRAJ_LOW_LR)
+    runs = [("fp32", None), ("fp64", None), ("emu_bf16", None), ("emu_fp16", None),
+            ("fp32", 1), ("fp32", 2), ("fp32", 3), ("emu_bf16", 1), ("emu_bf16", 2), ("emu_fp16", 1)]
+    path = os.path.join(OUT, name)
+    if os.path.exists(path):
+        with np.load(path) as f:
+            d.update({k: f[k] for k in f.files})
+    for mode, pert in runs:
+        t = time.time()
+        tag = mode if pert is None else f"{mode}_p{pert}"
+        if f"{tag}_total_loss" in d:
+            continue
+        rec, mu_pr, lv_pr = run_ref_trajectory(S, B, mode, perturb=pert, lr=TRAJ_LOW_LR)
+        for k, v in rec.items():
+            d[f"{tag}_{k}"] = v
+        d[f"{tag}_mu_pr"] = mu_pr.astype(np.float32)
+        d[f"{tag}_logvar_pr"] = lv_pr.astype(np.float32)
+        print(f"trajectory lr {TRAJ_LOW_LR} {tag}: {time.time() - t:.1f}s total "
+              f"{np.round(rec['total_loss'], 6).tolist()} gn {np.round(rec['grad_norm'], 5).tolist()}", flush=True)
+        save(name, **d)   # after every run: a long generation can be resumed
+
+
 def gen_model(only_s=None):
     for (S, B, full) in [(16, 4, True), (4, 3, True), (256, 2, False), (300, 2, False)]:
         if only_s and S not in only_s:
@@ -685,7 +718,7 @@ def gen_classifier():
 
 GENS = dict(kat=gen_kymatio_kat, filters=gen_filters, scattering=gen_scattering, frontend=gen_frontend,
             stats=gen_stats_and_norm, model=gen_model, amp=gen_amp, te=gen_te, tiny=gen_tiny,
-            classifier=gen_classifier, traj=gen_traj, model_big=lambda: gen_model((256, 300)))
+            classifier=gen_classifier, traj=gen_traj, traj_lowlr=gen_traj_lowlr, model_big=lambda: gen_model((256, 300)))
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()

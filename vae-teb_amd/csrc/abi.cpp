@@ -1,6 +1,7 @@
 // Error channel and version of the VAE-TEB C ABI (include/vaeteb.h).
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <atomic>
 
@@ -37,6 +38,38 @@ constexpr int kForkEvents = 1024, kMaxDevices = 16;
 // several host threads take distinct slots.  slot = device * kForkEvents + index.
 hipEvent_t g_fork_ev[kMaxDevices][kForkEvents];
 std::atomic<unsigned> g_fork_next[kMaxDevices];
+
+// Capture bookkeeping of every slot: the capture sequence id of the
+// stream that last recorded the slot (0: recorded outside any capture) and that stream.  A
+// wait is legal only inside the capture that recorded the slot (or, outside captures, on a
+// slot recorded outside one); anything else is reported as VT_ERR_HIP with the slot's
+// history instead of reaching the runtime.  VAETEB_EVENT_TRACE=1 also prints every mark /
+// wait to stderr.
+struct SlotRec {
+    unsigned long long cap;
+    void* stream;
+};
+SlotRec g_slot[kMaxDevices][kForkEvents];
+int g_trace = -1;
+
+unsigned long long capture_id(void* stream, bool* capturing) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (hipStreamGetCaptureInfo((hipStream_t)stream, &st, &id) != hipSuccess) {
+        (void)hipGetLastError();
+        st = hipStreamCaptureStatusNone;
+    }
+    *capturing = st == hipStreamCaptureStatusActive;
+    return *capturing ? id : 0ull;
+}
+
+bool trace() {
+    if (g_trace < 0) {
+        const char* e = getenv("VAETEB_EVENT_TRACE");
+        g_trace = e && e[0] == '1';
+    }
+    return g_trace;
+}
 }  // namespace
 
 extern "C" int vt_stream_mark(void* stream, int* slot) {
@@ -51,10 +84,15 @@ extern "C" int vt_stream_mark(void* stream, int* slot) {
         vt::set_error("vt_stream_mark: hipEventCreateWithFlags failed");
         return VT_ERR_HIP;
     }
+    bool capturing = false;
+    const unsigned long long cap = capture_id(stream, &capturing);
     if (hipEventRecord(ev, (hipStream_t)stream) != hipSuccess) {
         vt::set_error("vt_stream_mark: %s", hipGetErrorString(hipGetLastError()));
         return VT_ERR_HIP;
     }
+    g_slot[dev][i] = SlotRec{cap, stream};
+    if (trace()) fprintf(stderr, "[vt_event] mark slot %d event %p stream %p capture %llu\n", dev * kForkEvents + i,
+                         (void*)ev, stream, cap);
     *slot = dev * kForkEvents + i;
     return VT_OK;
 }
@@ -64,6 +102,26 @@ extern "C" int vt_stream_wait_mark(void* stream, int slot) {
     if (slot < 0 || dev >= kMaxDevices || !g_fork_ev[dev][i]) {
         vt::set_error("vt_stream_wait_mark: bad slot %d", slot);
         return VT_ERR_ARG;
+    }
+    bool capturing = false;
+    const unsigned long long cap = capture_id(stream, &capturing);
+    const SlotRec& r = g_slot[dev][i];
+    if (trace()) fprintf(stderr, "[vt_event] wait slot %d event %p stream %p capture %llu (recorded on %p capture %llu)\n",
+                         slot, (void*)g_fork_ev[dev][i], stream, cap, r.stream, r.cap);
+    // legal: the same capture; a non-capturing stream joining the capture the slot was recorded
+    // in (while that capture is active); a capturing stream waiting on a slot recorded outside
+    // any capture (an external dependency).  Not: a slot recorded in ANOTHER capture, or in a
+    // capture that has ended.
+    bool bad = cap != 0 && r.cap != 0 && r.cap != cap;
+    if (cap == 0 && r.cap != 0) {
+        bool rec_capturing = false;
+        bad = capture_id(r.stream, &rec_capturing) != r.cap;
+    }
+    if (bad) {
+        vt::set_error("vt_stream_wait_mark: slot %d was recorded on stream %p in capture %llu; the wait on stream %p "
+                      "is in capture %llu (0 = none): not the recording capture, or that capture has ended",
+                      slot, r.stream, r.cap, stream, cap);
+        return VT_ERR_HIP;
     }
     if (hipStreamWaitEvent((hipStream_t)stream, g_fork_ev[dev][i], 0) != hipSuccess) {
         vt::set_error("vt_stream_wait_mark: %s", hipGetErrorString(hipGetLastError()));

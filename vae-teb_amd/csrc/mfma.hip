@@ -25,10 +25,15 @@ namespace vt {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int QM = 256, QN = 64, QK = 64, QT = 512, NSTAGE = 3;
+constexpr int QM = 256, QN = 64, QK = 64, QT = 512;
 constexpr int ROWB = QK * 2;                      // 128 B per operand row in LDS
-constexpr int A_BYTES = QM * ROWB;                // 32 KB
-constexpr int STAGE_BYTES = A_BYTES + QN * ROWB;  // + 8 KB of B
+constexpr int A_BYTES = QM * ROWB;                // 32 KB per A stage (the activations: L2-resident)
+constexpr int B_BYTES = QN * ROWB;                // 8 KB per B stage (the weights: streamed from HBM)
+// A (shared by every workgroup of the launch, L2 hits) two tiles ahead; B (each weight tile read
+// by the launch's only M-tile, i.e. once: HBM misses, ~3 us under load) NB - 1 tiles ahead.  With
+// both operands two tiles ahead the loop ran at the HBM-miss latency / 2 per tile (~1.6 us).
+constexpr int NA = 3, NB = 8;
+constexpr int GEMM_LDS = NA * A_BYTES + NB * B_BYTES;   // 160 KB
 
 // 16-B chunk position of chunk c in LDS row r (involution)
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
@@ -43,7 +48,9 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
                                                   const __bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                   float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
                                                   int accumulate, float* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE_BYTES];
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sa = smem;                     // NA stages of A
+    char* sb = smem + NA * A_BYTES;      // NB stages of B
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n0 = blockIdx.x * QN, m0 = blockIdx.y * QM;
     const int64_t kbeg = (int64_t)blockIdx.z * K;
@@ -51,16 +58,20 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
 
     // LDS-DMA of one k-tile: lane l writes LDS byte (base + 16 l) = row l>>3, position l&7
     const int rsub = lane >> 3, pos = lane & 7;
-    auto issue = [&](int t, int s) {
-        const int64_t k0 = kbeg + (int64_t)(t < T ? t : T - 1) * QK;  // past the end: re-read, never used
-        char* st = smem + s * STAGE_BYTES;
+    auto kof = [&](int t) { return kbeg + (int64_t)(t < T ? t : T - 1) * QK; };  // past the end: re-read, unused
+    auto issue_a = [&](int t) {          // 4 DMAs per wave
+        const int64_t k0 = kof(t);
+        char* st = sa + (t % NA) * A_BYTES;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // A rows 32w + 8i .. +7
             const int r = 32 * w + 8 * i + rsub;
             glds16(A + (int64_t)(m0 + r) * lda + k0 + 8 * swz(r, pos), st + (32 * w + 8 * i) * ROWB);
         }
+    };
+    auto issue_b = [&](int t) {          // 1 DMA per wave
+        const int64_t k0 = kof(t);
         const int r = 8 * w + rsub;  // B rows 8w .. 8w+7
-        glds16(B + (int64_t)(n0 + r) * ldb + k0 + 8 * swz(r, pos), st + A_BYTES + 8 * w * ROWB);
+        glds16(B + (int64_t)(n0 + r) * ldb + k0 + 8 * swz(r, pos), sb + (t % NB) * B_BYTES + 8 * w * ROWB);
     };
 
     f32x4 acc[2][4];
@@ -70,8 +81,9 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int lr = lane & 15, lc = lane >> 4;
-    auto compute = [&](int s) {
-        const char* st = smem + s * STAGE_BYTES;
+    auto compute = [&](int t) {
+        const char* ta = sa + (t % NA) * A_BYTES;
+        const char* tb = sb + (t % NB) * B_BYTES;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // k 0..31, 32..63: chunks 4h + lc
             const int c = 4 * h + lc;
@@ -79,12 +91,12 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int r = 32 * w + 16 * i + lr;
-                af[i] = *(const bf16x8*)(st + r * ROWB + 16 * swz(r, c));
+                af[i] = *(const bf16x8*)(ta + r * ROWB + 16 * swz(r, c));
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int r = 16 * j + lr;
-                bfr[j] = *(const bf16x8*)(st + A_BYTES + r * ROWB + 16 * swz(r, c));
+                bfr[j] = *(const bf16x8*)(tb + r * ROWB + 16 * swz(r, c));
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -94,15 +106,22 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
         }
     };
 
-    issue(0, 0);
-    issue(1, 1);
+    // prologue: B tiles 0 .. NB-2, then A tiles 0, 1.  Loop t issues A(t+2), B(t+NB-1) after its
+    // barrier, so the DMAs younger than A(t) when tile t is needed are: t = 0: A(1) (4);
+    // t = 1: A(2), B(NB) (5); t >= 2: B(t+NB-3), A(t+1), B(t+NB-2) (6).  B(t) is older than A(t).
+#pragma unroll
+    for (int t = 0; t < NB - 1; ++t) issue_b(t);
+    issue_a(0);
+    issue_a(1);
     for (int t = 0; t < T; ++t) {
-        // 5 DMAs per wave per tile: tile t has landed once at most tile t+1's 5 are outstanding
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        if (t == 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (t == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // tile t complete for all waves; all waves done with tile t-1
-        issue(t + 2, (t + 2) % NSTAGE);
-        compute(t % NSTAGE);
+        issue_a(t + 2);                // overwrites A stage (t-1) % NA, B stage (t-1) % NB: both consumed
+        issue_b(t + NB - 1);
+        compute(t);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the re-read DMAs before the block exits
 
@@ -130,17 +149,52 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
 }
 
 // fixed-order sum of the split slabs (+ bias, + C when accumulating)
+// one output per thread (any alignment)
 __global__ void k_mfma_reduce(const float* __restrict__ part, int splits, int64_t MN, int N, const float* bias,
-                              float* __restrict__ C, int64_t ldc, int accumulate) {
+                              float* __restrict__ C, int accumulate) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= MN) return;
     float s = 0.f;
     for (int p = 0; p < splits; ++p) s += part[p * MN + i];
-    const int64_t row = i / N;
-    const int col = (int)(i - row * N);
-    if (bias) s += bias[col];
-    float* c = C + row * ldc + col;
-    *c = accumulate ? *c + s : s;
+    if (bias) s += bias[i % N];
+    C[i] = accumulate ? C[i] + s : s;
+}
+
+// Four consecutive outputs per thread (N a multiple of 64, ldc == N, C and bias 16-B aligned), every split's float4 in
+// flight before the first add; the same sum order as one element at a time:
+// (((0 + p_0) + p_1) + ...) + bias, then + C.
+template <int SPL>
+__global__ __launch_bounds__(256) void k_mfma_reduce4(const float* __restrict__ part, int splits, int64_t MN, int N,
+                                                      const float* bias, float* __restrict__ C, int accumulate) {
+    const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= MN) return;
+    const int ns = SPL ? SPL : splits;
+    float4 v[SPL ? SPL : 1];
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (SPL > 0) {
+#pragma unroll
+        for (int p = 0; p < SPL; ++p) v[p] = *(const float4*)(part + p * MN + i);
+#pragma unroll
+        for (int p = 0; p < SPL; ++p) {
+            s.x += v[p].x; s.y += v[p].y; s.z += v[p].z; s.w += v[p].w;
+        }
+    } else {
+        for (int p = 0; p < ns; ++p) {
+            const float4 q = *(const float4*)(part + p * MN + i);
+            s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
+        }
+    }
+    const int col = (int)(i % N);
+    if (bias) {
+        const float4 b = *(const float4*)(bias + col);
+        s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+    }
+    float4* c = (float4*)(C + i);
+    if (accumulate) {
+        const float4 o = *c;
+        s.x = o.x + s.x; s.y = o.y + s.y; s.z = o.z + s.z; s.w = o.w + s.w;
+    }
+    *c = s;
 }
 
 // out[m][k] = bf16(X[m][k]) for m < M, k < K; zero in the padding (Mpad x Kpad)
@@ -323,14 +377,31 @@ static MfmaPlan plan(int64_t M, int N, int64_t K) {
 
 static int run(const char* who, const __bf16* A, const __bf16* B, int64_t ldb, int64_t M, int N, const MfmaPlan& p,
                float* C, const float* bias, int accumulate, float* part, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {   // 160 KB of dynamic LDS (above the 64 KB default cap)
+        if (hipFuncSetAttribute((const void*)k_mfma_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, GEMM_LDS) !=
+            hipSuccess) {
+            set_error("%s: cannot allow %d B of LDS for k_mfma_gemm", who, GEMM_LDS);
+            return VT_ERR_HIP;
+        }
+        attr = true;
+    }
     const int kper = (int)(p.Kpad / p.splits);
     dim3 grid(N / QN, (unsigned)(p.Mpad / QM), p.splits);
-    hipLaunchKernelGGL(k_mfma_gemm, grid, dim3(QT), 0, st, A, p.Kpad, B, ldb, (int)M, N, kper, C, (int64_t)N, bias,
-                       accumulate, p.splits > 1 ? part : nullptr);
+    hipLaunchKernelGGL(k_mfma_gemm, grid, dim3(QT), GEMM_LDS, st, A, p.Kpad, B, ldb, (int)M, N, kper, C, (int64_t)N,
+                       bias, accumulate, p.splits > 1 ? part : nullptr);
     if (p.splits > 1) {
         const int64_t MN = M * N;
-        hipLaunchKernelGGL(k_mfma_reduce, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, part, p.splits, MN, N,
-                           bias, C, (int64_t)N, accumulate);
+        const dim3 g((unsigned)((MN / 4 + 255) / 256));
+        if ((reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(bias)) & 15)
+            hipLaunchKernelGGL(k_mfma_reduce, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, part, p.splits, MN,
+                               N, bias, C, accumulate);
+        else if (p.splits == 4)
+            hipLaunchKernelGGL(k_mfma_reduce4<4>, g, dim3(256), 0, st, part, p.splits, MN, N, bias, C, accumulate);
+        else if (p.splits == 2)
+            hipLaunchKernelGGL(k_mfma_reduce4<2>, g, dim3(256), 0, st, part, p.splits, MN, N, bias, C, accumulate);
+        else
+            hipLaunchKernelGGL(k_mfma_reduce4<0>, g, dim3(256), 0, st, part, p.splits, MN, N, bias, C, accumulate);
     }
     VT_LAUNCH_CHECK(who);
     return VT_OK;
