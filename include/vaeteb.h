@@ -294,6 +294,27 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
                        const float* const* params, const float* dout, const float* xhat, const float* rstd,
                        int64_t rows, float* dx, float* const* grads, int accumulate, float* ws, int64_t ws_floats,
                        void* stream);
+/* The same backward split in two (round 5), so the weight gradients leave the data-gradient
+ * chain (ref/model/vae_teb_model.py:336-403 backward, the reference's autograd of Linear /
+ * LayerNorm under fp16 autocast):
+ *   vt_resmlp_bf16_bwd_data   dx, the LayerNorm gamma / beta and bias gradients (grads as in
+ *                             vt_resmlp_bf16_bwd; the weight entries are not touched), and every
+ *                             GEMM's dZ as bf16 rows in dz16 (sizes[0] bf16 elements);
+ *                             workspace sizes[1] floats;
+ *   vt_resmlp_bf16_bwd_weight the weight gradients from dz16 and the saved xhat, on any stream
+ *                             ordered after bwd_data (e.g. a side stream); workspace sizes[2].
+ * vt_resmlp_bf16_split_sizes: sizes[0..2] as above, sizes[3] = 1 when the stack's W^T images fit
+ * the LDS budget of the split kernel (else use vt_resmlp_bf16_bwd).                        */
+int vt_resmlp_bf16_split_sizes(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                               int64_t rows, int64_t* sizes);
+int vt_resmlp_bf16_bwd_data(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                            float eps, const float* const* params, const float* dout, const float* xhat,
+                            const float* rstd, int64_t rows, float* dx, float* const* grads, int accumulate,
+                            void* dz16, float* ws, int64_t ws_floats, void* stream);
+int vt_resmlp_bf16_bwd_weight(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                              float eps, const float* const* params, const float* xhat, const void* dz16,
+                              int64_t rows, float* const* grads, int accumulate, float* ws, int64_t ws_floats,
+                              void* stream);
 /* Diagnostic (tools/mlpb_phases.py): while buf != NULL, vt_resmlp_bf16_bwd launches stamp
  * wave 0's wall clock at the kernel's phase boundaries, 256 uint64 per workgroup. */
 int vt_resmlp_bf16_set_stamps(void* buf);

@@ -543,19 +543,25 @@ def test_bench_batch_fp32_step_vs_fp64_oracle():
     params = dict(m.named_parameters())
     heads = {k for k, p in params.items() if p.numel() >= 1 << 20}
     assert len(heads) == 4, heads
-    # the norms (97 % of the squared gradient norm is in the heads: their NLL gradient through
-    # exp(-logvar) carries the fp32 rounding of every layer before it): within 2x the oracle's own
-    # fp32-vs-fp64 distance, at least 1e-5
+    # everything is printed first (the assertions follow): the norms (97 % of the squared gradient
+    # norm is in the heads) and every gradient's rel-L2 to the fp64 oracle beside the oracle's own
+    # fp32 distance
     print(f"grad norm: ours {gn:.7f}, oracle fp64 {gn_o:.7f}, oracle fp32 {gn_o32:.7f}")
-    assert abs(gn - gn_o) <= max(1e-5 * gn_o, 2 * abs(gn_o32 - gn_o)), (gn, gn_o, gn_o32)
-    for k in heads:   # the 4096^2 head weights: norms
-        a, e, e32 = params[k].grad.double().norm().item(), g_o[k].double().norm().item(), g_o32[k].double().norm().item()
-        print(f"{k}: |grad| ours {a:.7f}, oracle fp64 {e:.7f}, fp32 {e32:.7f}")
-        assert abs(a - e) <= max(1e-5 * e, 2 * abs(e32 - e)), (k, a, e, e32)
-    errs = np.array([rel(params[k].grad, gr) for k, gr in g_o.items()
-                     if k not in heads and gr.norm() > 0 and rel(g_o32[k], gr) < 1e-3])
-    e32 = np.array([rel(g_o32[k], gr) for k, gr in g_o.items() if k not in heads and gr.norm() > 0])
+    hn = {}
+    for k in sorted(heads):
+        hn[k] = (params[k].grad.double().norm().item(), g_o[k].double().norm().item(), g_o32[k].double().norm().item())
+        print(f"{k}: |grad| ours {hn[k][0]:.7f}, oracle fp64 {hn[k][1]:.7f}, fp32 {hn[k][2]:.7f}; rel-L2 ours "
+              f"{rel(params[k].grad, g_o[k]):.3e}, oracle fp32 {rel(g_o32[k], g_o[k]):.3e}")
+    table = sorted(((rel(params[k].grad, gr), rel(g_o32[k], gr), k) for k, gr in g_o.items()
+                    if k not in heads and gr.norm() > 0), reverse=True)
+    for e, e32, k in table[:15]:
+        print(f"  worst: {k}: ours {e:.3e}, oracle fp32 {e32:.3e}")
+    errs = np.array([e for e, e32, k in table if e32 < 1e-3])
+    e32 = np.array([e32 for e, e32, k in table])
     print(f"B=256 grads vs fp64 oracle over {len(errs)} well-conditioned non-head gradients: median "
           f"{np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} max {errs.max():.3e}; the oracle's own fp32 "
           f"step: median {np.median(e32):.3e} max {e32.max():.3e}")
+    assert abs(gn - gn_o) <= max(1e-5 * gn_o, 2 * abs(gn_o32 - gn_o)), (gn, gn_o, gn_o32)
+    for k, (a, e, e32_) in hn.items():
+        assert abs(a - e) <= max(1e-5 * e, 2 * abs(e32_ - e)), (k, a, e, e32_)
     assert len(errs) >= 300 and np.median(errs) <= 2e-5 and np.percentile(errs, 90) <= 5e-5, errs

@@ -249,3 +249,31 @@ def test_resmlp_bf16_backward_accumulates_into_sinks(case):
     finally:
         for p in m.parameters():
             p._vt_sink = False
+
+
+@pytest.mark.parametrize("case", list(CASES))
+@pytest.mark.parametrize("rows", [1000, 65536])
+def test_resmlp_bf16_split_backward_matches_one_kernel(case, rows, monkeypatch):
+    """Round 5: the backward split in two (vt_resmlp_bf16_bwd_data: the dx chain, LayerNorm /
+    bias gradients and the dZ rows; vt_resmlp_bf16_bwd_weight: dW from the dZ rows and the saved
+    xhat) == the one-kernel backward: dx bit for bit (the same per-row arithmetic), every
+    parameter gradient within 2e-6 rel-L2 (the same bf16 products and fp32 sums, grouped over
+    other row blocks)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vaeteb import ops
+    m, x = _setup(case, rows, 21 + rows)
+    spec = m._fused_spec()[0]
+    if not spec.split_sizes(rows)[3]:
+        pytest.skip("stack has no split plan")
+    gy = torch.randn(rows, m.body[m._plan[-1][0]].out_features, dtype=torch.float64)
+    res = {}
+    for split in (0, 1):
+        monkeypatch.setattr(ops, "MLPB_SPLIT", split)
+        y, G = _gpu(m, x, gy)
+        torch.cuda.synchronize()
+        res[split] = (y.detach().clone(), {k: v.detach().clone() for k, v in G.items()})
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1]["x"], res[1][1]["x"])
+    for k, v in res[0][1].items():
+        assert rel(res[1][1][k], v) < 2e-6, (k, rel(res[1][1][k], v))

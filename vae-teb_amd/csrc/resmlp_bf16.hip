@@ -55,11 +55,17 @@ struct BG {                      // one GEMM: z = h W^T + b, W [N][K]
     int po;                      // fp32 params in LDS: bias[pad16 N], gamma, beta
     int wo;                      // dW|db partial offset (floats), N x (K + 1)
     int gbw;                     // W^T image offset (bf16) in the global image's backward region
+    // split backward (k_mlpb_bwdx + k_mlpb_dw): dZ rows (bf16) of this GEMM at dz16 + zo, row stride
+    // zs = pad16(N); the bias-gradient partial at xdb of a k_mlpb_bwdx workgroup's partial; the dW
+    // partial (N x K) at dwo of a k_mlpb_dw row chunk's partial
+    int64_t zo;
+    int zs, xdb, dwo;
     const float* W;
     const float* b;
 };
 struct BL {                      // LayerNorm (+ act) after GEMM l
     int ln, act, xo, ri, lpo, bpo;   // xo: saved-xhat region (x Rp floats); bpo: backward LDS params
+    int xlpo;                        // split backward: gamma | beta partial offset (k_mlpb_bwdx)
     const float* g;
     const float* be;
 };
@@ -80,6 +86,9 @@ struct BDesc {
     int bpin;                    // backward LDS float offset of the input LN gamma / beta
     int gbo, gpo;                // global image: byte offsets of the W^T region and of the backward params
     char* gimg;                  // global image (k_mlpb_prep): [forward LDS image | W^T images | backward params]
+    int xP, xlpo0;               // split backward: k_mlpb_bwdx partial floats per workgroup, input-LN offset
+    int xbytes;                  // ... k_mlpb_bwdx LDS bytes (every W^T image resident), 0: no split plan
+    int dP;                      // ... k_mlpb_dw partial floats per row chunk (every GEMM's N x K)
     const float* g0;
     const float* be0;
     BG G[MAXG];
@@ -940,6 +949,240 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
 }
 #undef MB_STAMP
 
+// ----------------------------------------------------------- split backward
+// The same backward in two kernels, so the weight gradients leave the data-gradient chain
+// (tools/mlpb_phases.py, round 5: of a 64-wide step's ~10.5 us, the H image, its barrier and the
+// dW MFMAs took ~3.5 us on the chain the encoders' backward waits for):
+//   k_mlpb_bwdx  per GEMM step: LayerNorm backward in registers -> dZ; dZ stored as bf16 rows
+//                (dz16) for k_mlpb_dw; dH = W^T dZ; bias / gamma / beta column sums of the fp32 dZ
+//                (as k_mlpb_bwd).  Every W^T image resident, no dZ / H images: one barrier per
+//                step (the column-sum flush, double-buffered).
+//   k_mlpb_dw    per (row chunk, GEMM): dW partial = dZ^T H over the chunk, H = act(xhat gamma +
+//                beta) of the GEMM's input recomputed from the saved xhat, both staged as bf16
+//                row images and read as MFMA fragments with ds_read_b64_tr_b16 (rows as the
+//                contraction); fixed-order sum of the chunk partials afterwards.
+// dW = sum over rows of bf16(dZ) bf16(H) with fp32 accumulation, as k_mlpb_bwd (another row
+// grouping: other rounding, same precision).
+// (the second launch bound is waves per SIMD: two 512-thread workgroups per CU for the narrow
+// stacks with 128-row blocks, whose W^T images fit 80 KB; one otherwise)
+template <int NT, int TPW>
+__global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx(const BDesc* __restrict__ dp, const float* __restrict__ dout,
+                                                     const float* __restrict__ xh, const float* __restrict__ rs,
+                                                     int64_t R, int64_t Rp, float* __restrict__ dx,
+                                                     float* __restrict__ part, __bf16* __restrict__ dz16) {
+    const BDesc& d = *dp;
+    constexpr int KS = (NT + 1) / 2;
+    constexpr int ROWS = IMR * TPW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // every W^T image at its global-image offset G.gbw, then the LN parameters
+    __bf16* wimg = reinterpret_cast<__bf16*>(smem);
+    float* prm = reinterpret_cast<float*>(smem + (d.gpo - d.gbo));   // [LN params per LN layer][input LN]
+    float* red = prm + d.bprm;                                         // [2][NW][48 NT]: flushes double-buffered
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4;
+    const int L = d.L, d0 = d.d0, DL = d.G[L - 1].N;
+    const int64_t rbase = (int64_t)blockIdx.x * ROWS + 16 * wv + (lane & 15);
+    float* pb = part + (int64_t)blockIdx.x * d.xP;
+
+    lds_copy(reinterpret_cast<char*>(wimg), d.gimg + d.gbo, d.gpo - d.gbo);
+    lds_copy(reinterpret_cast<char*>(prm), d.gimg + d.gpo, 4 * d.bprm);
+    lds_copy_wait();
+    const float* prm_in = prm + d.bpin;
+
+    f32x4 dh[TPW][NT], xc[TPW][NT];
+    float rsc[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int64_t row = rbase + IMR * u;
+        load_rows<NT>(dh[u], dout, DL, R, row);
+        rsc[u] = 0.f;
+        if (d.l[L - 1].ln) {
+            load_sv<NT>(xc[u], xh + (int64_t)d.l[L - 1].xo * Rp, DL, Rp, row, row < R);
+            rsc[u] = bld(brs(rs + (int64_t)d.l[L - 1].ri * Rp, Rp * 4), row < R ? (unsigned)(row * 4) : OOB);
+        }
+    }
+
+    const int nsteps = L + (d.skip == 2 ? 1 : 0);
+    for (int step = 0; step < nsteps; ++step) {
+        const bool skp = step == L;
+        const int l = skp ? -1 : L - 1 - step;
+        const BG& G = d.G[skp ? L : l];
+        const int N = G.N, K = G.K, bs = G.bs;
+        const bool ln = !skp && d.l[l].ln;
+        const int hsrc = skp ? -1 : l - 1;
+        const int CH = hsrc >= 0 ? d.G[hsrc].N : d0;
+        const float* xH = xh + (hsrc >= 0 ? (int64_t)d.l[hsrc].xo * Rp : 0);
+        const rsrc_t rH = brs(rs + (hsrc >= 0 ? (int64_t)d.l[hsrc].ri * Rp : 0), Rp * 4);
+        float la[NT], lb[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
+        const int ntz = (N + 15) >> 4;
+        __bf16* zrow = dz16 + G.zo;
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int64_t row = rbase + IMR * u;
+            f32x4 dz[NT];
+            if (skp) {
+                load_rows<NT>(dz, dout, DL, R, row);
+            } else {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) dz[t] = dh[u][t];
+                if (ln) {
+                    const float* gl = prm + d.l[l].bpo;
+                    ln_bwd<NT>(dz, xc[u], rsc[u], N, gl, gl + p16(N), d.l[l].act, la);
+                }
+            }
+            // the next step's LayerNorm input (this GEMM's input's xhat) into the registers just
+            // consumed: in flight during this step's GEMM and flush
+            rsc[u] = bld(rH, row < R ? (unsigned)(row * 4) : OOB);
+            load_sv<NT>(xc[u], xH, CH, Rp, row, row < R);
+            colsum<NT>(dz, N, lb);
+            // dZ row (bf16, 0 past N and for rows past R) for the weight-gradient kernel
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            __bf16* zp = zrow + row * G.zs + 4 * g4;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                if (t < ntz)
+                    *(bf16x4*)(zp + 16 * t) = bf16x4{(__bf16)dz[t][0], (__bf16)dz[t][1], (__bf16)dz[t][2],
+                                                      (__bf16)dz[t][3]};
+            bf16x8 b[KS];
+            frags<NT>(dz, b);
+            f32x4 nh[NT];
+            tile_gemm<NT, KS>(wimg + G.gbw, bs, (K + 15) >> 4, (N + 31) >> 5, b, nh);
+            if (skp) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) dh[u][t] += nh[t];
+            } else {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) dh[u][t] = nh[t];
+            }
+        }
+        flush_cols<NT>(red + (step & 1) * (NW * 48 * NT), la, lb, N, ln, ln ? pb + d.l[l].xlpo : nullptr,
+                       pb + G.xdb, 1);
+    }
+    if (d.skip == 1) {
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int64_t row = rbase + IMR * u;
+            f32x4 t2[NT];
+            load_rows<NT>(t2, dout, DL, R, row);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) dh[u][t] += t2[t];
+        }
+    }
+    float la[NT], lb[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int64_t row = rbase + IMR * u;
+        ln_bwd<NT>(dh[u], xc[u], rsc[u], d0, prm_in, prm_in + p16(d0), 0, la);
+        store_rows<NT>(dx, dh[u], d0, R, row);
+    }
+    flush_cols<NT>(red + (nsteps & 1) * (NW * 48 * NT), la, lb, d0, true, pb + d.xlpo0, nullptr, 0);
+}
+
+// weight gradient of one GEMM over a chunk of rows: images of 64 rows (bf16 [r][col], row
+// stride DZS plus 64 every 8 rows: the transposed fragment reads of mfma.hip's k_mfma_dw)
+constexpr int DWROWS = 64, DZS = 160;
+constexpr int DZIMG = DWROWS * DZS + (DWROWS / 8) * 64;
+__device__ __forceinline__ int dz_pos(int r, int c) { return r * DZS + (r >> 3) * 64 + c; }
+
+// 16 columns col0.. x 32 rows row0.. of a [r][col] image as an MFMA operand (rows = the
+// contraction): lane 4q + p of 16-lane group g reads rows row0 + 8g + q (+4), columns col0 + 4p ..
+__device__ __forceinline__ bf16x8 dz_frag(const __bf16* img, int row0, int col0) {
+    typedef short v4i16 __attribute__((ext_vector_type(4)));
+    typedef short v8i16 __attribute__((ext_vector_type(8)));
+    const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const __bf16* a0 = img + dz_pos(row0 + 8 * g + q, col0 + 4 * p);
+    const __bf16* a1 = img + dz_pos(row0 + 8 * g + q + 4, col0 + 4 * p);
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a1);
+    const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+// grid (row chunks, GEMMs), 256 threads; MT >= output tiles per wave (4 waves share the
+// ceil(N/16) x ceil(K/16) tiles round-robin).  part: [chunk][dP], this GEMM's N x K at G.dwo.
+template <int MT>
+__global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, const __bf16* __restrict__ dz16,
+                                                 const float* __restrict__ xh, int64_t R, int64_t Rp, int chunk_rows,
+                                                 float* __restrict__ part) {
+    const BDesc& d = *dp;
+    __shared__ __attribute__((aligned(16))) __bf16 zimg[DZIMG];
+    __shared__ __attribute__((aligned(16))) __bf16 himg[DZIMG];
+    const int gi = blockIdx.y;
+    const BG& G = d.G[gi];
+    const int N = G.N, K = G.K;
+    const bool skp = gi == d.L;
+    const int hsrc = skp ? -1 : gi - 1;   // this GEMM's input: layer hsrc's output, or x0 (input LN)
+    const float* gam = hsrc >= 0 ? d.l[hsrc].g : d.g0;
+    const float* bet = hsrc >= 0 ? d.l[hsrc].be : d.be0;
+    const int actH = hsrc >= 0 ? d.l[hsrc].act : 0;
+    const int kp = p16(K);                // saved-xhat row stride (floats)
+    const float* xH = xh + (hsrc >= 0 ? (int64_t)d.l[hsrc].xo * Rp : 0);
+    const __bf16* zsrc = dz16 + G.zo;
+    const int zs = G.zs;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lc = lane >> 4;
+    const int ntn = (N + 15) >> 4, ntk = (K + 15) >> 4, ntiles = ntn * ntk;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int64_t r0 = (int64_t)blockIdx.x * chunk_rows;
+    const int64_t r1 = r0 + chunk_rows < Rp ? r0 + chunk_rows : Rp;
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    for (int64_t rb = r0; rb < r1; rb += DWROWS) {
+        // dZ rows: 16-B pieces (8 bf16), zs / 8 per row
+        const int zq = zs >> 3;
+        for (int e = tid; e < DWROWS * zq; e += 256) {
+            const int r = e / zq, q = e - r * zq;
+            const uint4 v = *(const uint4*)(zsrc + (rb + r) * zs + 8 * q);
+            *(uint4*)(zimg + dz_pos(r, 8 * q)) = v;
+        }
+        // H rows: act(xhat gamma + beta), 0 past K and for rows past R
+        const int hq = kp >> 2;
+        for (int e = tid; e < DWROWS * hq; e += 256) {
+            const int r = e / hq, q = e - r * hq;
+            const int64_t row = rb + r;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < R) v = *(const float4*)(xH + row * kp + 4 * q);
+            float h[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = 4 * q + i;
+                h[i] = (row < R && k < K) ? bact(fmaf(h[i], gam[k], bet[k]), actH) : 0.f;
+            }
+            *(bf16x4*)(himg + dz_pos(r, 4 * q)) = bf16x4{(__bf16)h[0], (__bf16)h[1], (__bf16)h[2], (__bf16)h[3]};
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < DWROWS / 32; ++s) {
+#pragma unroll
+            for (int j = 0; j < MT; ++j) {
+                const int tile = w + 4 * j;
+                if (tile < ntiles) {
+                    const int tn = tile / ntk, tk = tile - tn * ntk;
+                    acc[j] = mfma(dz_frag(zimg, 32 * s, 16 * tn), dz_frag(himg, 32 * s, 16 * tk), acc[j]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // D: col (k) = lane & 15, row (n) = 4 (lane >> 4) + rr
+    float* pd = part + (int64_t)blockIdx.x * d.dP + G.dwo;
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+        const int tile = w + 4 * j;
+        if (tile >= ntiles) continue;
+        const int tn = tile / ntk, tk = tile - tn * ntk;
+        const int k = 16 * tk + lr;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int n = 16 * tn + 4 * lc + rr;
+            if (n < N && k < K) pd[n * K + k] = acc[j][rr];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- final sum
 // one segment per dW|db slab (E = N (K + 1), K1 = K + 1) or gamma|beta pair
 // (E = 2N, K1 = 0), summed over the nblk workgroup partials in fixed order
@@ -982,7 +1225,9 @@ __global__ __launch_bounds__(256) void k_mlpb_sum(SumArgs sa, const float* __res
     if (w != 0 || i >= E) return;
     const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
     float* dst;
-    if (sg.K1) {
+    if (sg.K1 < 0) {                     // a plain vector (split backward: dW N x K, or a bias)
+        dst = sg.da ? sg.da + i : nullptr;
+    } else if (sg.K1) {
         const int n = i / sg.K1, k = i - n * sg.K1;
         dst = k < sg.K1 - 1 ? (sg.da ? sg.da + (int64_t)n * (sg.K1 - 1) + k : nullptr) : (sg.db ? sg.db + n : nullptr);
     } else {
@@ -998,6 +1243,9 @@ inline int h32(int n) { return (n + 31) & ~31; }
 struct BPlan {
     BDesc d;
     int nt, tpw;
+    int xtpw, mt;                // split backward: k_mlpb_bwdx tiles per wave; k_mlpb_dw tiles per wave bound
+    int64_t xnblk, dz_elems;     // ... k_mlpb_bwdx workgroups; bf16 elements of the dZ rows
+    int dw_rows, dw_chunks;      // ... k_mlpb_dw rows per chunk and chunks
     int occ;                     // backward workgroups per CU the launch is built for (1, or 2: 128-row blocks)
     int64_t Rp, xh_floats, rs_floats, nblk;
     int gbytes;                  // global image bytes
@@ -1145,6 +1393,40 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
     p.nblk = (R + blk - 1) / blk;
     p.xh_floats = (int64_t)xo * p.Rp;
     p.rs_floats = (int64_t)(1 + n_ln) * p.Rp;
+    // split backward (k_mlpb_bwdx + k_mlpb_dw)
+    int xP = 0;
+    for (int g = 0; g < d.nG; ++g) {
+        d.G[g].xdb = xP;
+        xP += d.G[g].N;
+    }
+    for (int l = 0; l < n_layers; ++l) {
+        d.l[l].xlpo = d.l[l].ln ? xP : -1;
+        if (d.l[l].ln) xP += 2 * d.G[l].N;
+    }
+    d.xlpo0 = xP;
+    xP += 2 * dims[0];
+    d.xP = xP;
+    int dP = 0;
+    int64_t zo = 0;
+    for (int g = 0; g < d.nG; ++g) {
+        BG& G = d.G[g];
+        G.dwo = dP;
+        dP += G.N * G.K;
+        G.zs = h16(G.N);
+        G.zo = zo;
+        zo += (int64_t)G.zs * p.Rp;
+    }
+    d.dP = dP;
+    p.dz_elems = zo;
+    const int xbytes = (d.gpo - d.gbo) + 4 * (bprm + 2 * NW * 48 * p.nt);
+    d.xbytes = xbytes <= 160 * 1024 ? xbytes : 0;
+    // 128-row blocks, two workgroups per CU, when they fit 80 KB; else 256-row blocks (one per CU);
+    // the wide stacks keep 128 rows (their registers)
+    p.xtpw = (xbytes <= 80 * 1024 || p.nt >= 6) ? 1 : 2;
+    p.xnblk = (R + IMR * p.xtpw - 1) / (IMR * p.xtpw);
+    p.mt = p.nt == 2 ? 1 : p.nt == 4 ? 4 : p.nt == 6 ? 9 : 21;
+    p.dw_rows = 1024;
+    p.dw_chunks = (int)((p.Rp + p.dw_rows - 1) / p.dw_rows);
     VT_CHECK_ARG(d.fbytes <= 160 * 1024, "%s: weights need %d bytes of LDS (> 160 KiB)", who, d.fbytes);
     VT_CHECK_ARG(d.bbytes <= 160 * 1024, "%s: backward needs %d bytes of LDS (> 160 KiB)", who, d.bbytes);
     return VT_OK;
@@ -1357,6 +1639,111 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
         hipLaunchKernelGGL(k_mlpb_sum, gs, dim3(256), 0, st, sa, ws, (int)p.nblk, accumulate);
     }
     VT_LAUNCH_CHECK("vt_resmlp_bf16_bwd");
+    return VT_OK;
+}
+
+int vt_resmlp_bf16_split_sizes(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                               int64_t rows, int64_t* sizes) {
+    const float* dummy[4 * MAXL + 4];
+    for (int i = 0; i < 4 * MAXL + 4; ++i) dummy[i] = reinterpret_cast<const float*>(16);
+    BPlan p;
+    const int rc = make_bplan(p, n_layers, dims, layer_ln, layer_act, skip, 1e-5f, dummy, rows,
+                              "vt_resmlp_bf16_split_sizes");
+    if (rc) return rc;
+    sizes[0] = p.dz_elems;
+    sizes[1] = p.xnblk * p.d.xP;
+    sizes[2] = (int64_t)p.dw_chunks * p.d.dP;
+    sizes[3] = p.d.xbytes > 0 ? 1 : 0;
+    return VT_OK;
+}
+
+static void sum_launch(const SumArgs& sa, int emax, const float* part, int nblk, int accumulate, hipStream_t st) {
+    if (!sa.nseg) return;
+    const dim3 gs((unsigned)((emax + 63) / 64), (unsigned)sa.nseg);
+    hipLaunchKernelGGL(k_mlpb_sum, gs, dim3(256), 0, st, sa, part, nblk, accumulate);
+}
+
+int vt_resmlp_bf16_bwd_data(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                            float eps, const float* const* params, const float* dout, const float* xhat,
+                            const float* rstd, int64_t rows, float* dx, float* const* grads, int accumulate,
+                            void* dz16, float* ws, int64_t ws_floats, void* stream) {
+    hipStream_t st = S(stream);
+    const BPlan* pp;
+    const BDesc* ddev;
+    const int rc = get_plan(pp, ddev, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, st,
+                            "vt_resmlp_bf16_bwd_data");
+    if (rc) return rc;
+    const BPlan& p = *pp;
+    VT_CHECK_ARG(p.d.xbytes > 0, "vt_resmlp_bf16_bwd_data: the W^T images do not fit in LDS (use vt_resmlp_bf16_bwd)");
+    VT_CHECK_ARG(dout && xhat && rstd && dx && grads && dz16, "vt_resmlp_bf16_bwd_data: null buffer");
+    VT_CHECK_ARG(ws && ws_floats >= p.xnblk * p.d.xP, "vt_resmlp_bf16_bwd_data: workspace %lld floats < %lld",
+                 (long long)ws_floats, (long long)(p.xnblk * p.d.xP));
+    SumArgs sa{};
+    sa.P = p.d.xP;
+    int emax = 0;
+    auto add = [&](int E, int N, int K1, int src, float* da, float* db) {
+        if (!da && !db) return;
+        sa.s[sa.nseg++] = SumSeg{E, N, K1, src, da, db};
+        emax = E > emax ? E : emax;
+    };
+    for (int q = 0; q < p.d.nG; ++q) {   // biases
+        const int gi = q < n_layers ? 2 + 4 * q : 2 + 4 * n_layers;
+        add(p.d.G[q].N, p.d.G[q].N, -1, p.d.G[q].xdb, grads[gi + 1], nullptr);
+    }
+    for (int l = 0; l < n_layers; ++l)
+        if (p.d.l[l].ln) add(2 * p.d.G[l].N, p.d.G[l].N, 0, p.d.l[l].xlpo, grads[4 + 4 * l], grads[5 + 4 * l]);
+    add(2 * dims[0], dims[0], 0, p.d.xlpo0, grads[0], grads[1]);
+    const dim3 grid((unsigned)p.xnblk);
+    __bf16* z = reinterpret_cast<__bf16*>(dz16);
+#define VT_MBX(NTV, TPWV)                                                                                       \
+    if (p.nt == NTV && p.xtpw == TPWV) {                                                                          \
+        set_lds(k_mlpb_bwdx<NTV, TPWV>, p.d.xbytes);                                                              \
+        hipLaunchKernelGGL((k_mlpb_bwdx<NTV, TPWV>), grid, dim3(BT), p.d.xbytes, st, ddev, dout, xhat, rstd, rows, \
+                           p.Rp, dx, ws, z);                                                                      \
+    }
+    VT_MBX(2, 1) VT_MBX(2, 2) VT_MBX(4, 1) VT_MBX(4, 2) VT_MBX(6, 1) VT_MBX(9, 1)
+#undef VT_MBX
+    sum_launch(sa, emax, ws, (int)p.xnblk, accumulate, st);
+    VT_LAUNCH_CHECK("vt_resmlp_bf16_bwd_data");
+    return VT_OK;
+}
+
+int vt_resmlp_bf16_bwd_weight(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                              float eps, const float* const* params, const float* xhat, const void* dz16,
+                              int64_t rows, float* const* grads, int accumulate, float* ws, int64_t ws_floats,
+                              void* stream) {
+    hipStream_t st = S(stream);
+    const BPlan* pp;
+    const BDesc* ddev;
+    const int rc = get_plan(pp, ddev, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, st,
+                            "vt_resmlp_bf16_bwd_weight");
+    if (rc) return rc;
+    const BPlan& p = *pp;
+    VT_CHECK_ARG(p.d.xbytes > 0, "vt_resmlp_bf16_bwd_weight: no split plan for this stack");
+    VT_CHECK_ARG(xhat && dz16 && grads, "vt_resmlp_bf16_bwd_weight: null buffer");
+    VT_CHECK_ARG(ws && ws_floats >= (int64_t)p.dw_chunks * p.d.dP,
+                 "vt_resmlp_bf16_bwd_weight: workspace %lld floats < %lld", (long long)ws_floats,
+                 (long long)p.dw_chunks * p.d.dP);
+    SumArgs sa{};
+    sa.P = p.d.dP;
+    int emax = 0;
+    for (int q = 0; q < p.d.nG; ++q) {
+        const int gi = q < n_layers ? 2 + 4 * q : 2 + 4 * n_layers;
+        if (!grads[gi]) continue;
+        const int E = p.d.G[q].N * p.d.G[q].K;
+        sa.s[sa.nseg++] = SumSeg{E, p.d.G[q].N, -1, p.d.G[q].dwo, grads[gi], nullptr};
+        emax = E > emax ? E : emax;
+    }
+    const dim3 grid((unsigned)p.dw_chunks, (unsigned)p.d.nG);
+    const __bf16* z = reinterpret_cast<const __bf16*>(dz16);
+    switch (p.mt) {
+        case 1: hipLaunchKernelGGL(k_mlpb_dw<1>, grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
+        case 4: hipLaunchKernelGGL(k_mlpb_dw<4>, grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
+        case 9: hipLaunchKernelGGL(k_mlpb_dw<9>, grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
+        default: hipLaunchKernelGGL(k_mlpb_dw<21>, grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
+    }
+    sum_launch(sa, emax, ws, p.dw_chunks, accumulate, st);
+    VT_LAUNCH_CHECK("vt_resmlp_bf16_bwd_weight");
     return VT_OK;
 }
 

@@ -106,6 +106,9 @@ def _l16_pair_fits(S):
     """The pair forward stages its lower layer's input in LDS: NS x ceil16(S) rows of 144 B
     within 120 KB (csrc/lstm16.hip fwd2_stage_bytes)."""
     return _L16_PAIR_NS * ((S + 15) // 16) * 16 * 72 * 2 <= 120 * 1024
+# bf16 ResidualMLP backward split in two (vt_resmlp_bf16_bwd_data on the chain, the weight gradients
+# from the saved dZ rows on the weight-gradient side stream); 0: the one-kernel backward
+MLPB_SPLIT = int(os.environ.get("VAETEB_MLPB_SPLIT", "1"))
 # bf16 conv backward-data written straight into dX where the fold is a crop; 0: gpad + fold
 CONV_DIRECT_DX = int(os.environ.get("VAETEB_CONV_DIRECT_DX", "1"))
 # conv-block backward as vt_batchnorm_bwd_x16 + vt_conv1d_bwd_dx16 (bf16 operand written once,
@@ -394,6 +397,17 @@ class MlpSpec:
     def supported(cls, dims):
         return len(dims) - 1 <= cls.MAX_LAYERS and max(dims) <= cls.MAX_WIDTH
 
+    def split_sizes(self, rows):
+        """(dZ bf16 elements, bwd_data workspace floats, bwd_weight workspace floats, supported) of
+        the split bf16 backward (vt_resmlp_bf16_bwd_data / _bwd_weight)."""
+        s = self._sizes.get((rows, "split"))
+        if s is None:
+            import ctypes
+            arr = (ctypes.c_int64 * 4)()
+            call("vt_resmlp_bf16_split_sizes", self.L, self.dims, self.ln, self.act, self.skip, rows, arr)
+            s = self._sizes[(rows, "split")] = tuple(arr)
+        return s
+
     def sizes(self, rows, bf16=False):
         s = self._sizes.get((rows, bf16))
         if s is None:
@@ -457,13 +471,37 @@ class ResMLPF(torch.autograd.Function):
         grads = [None] * len(params)
         for i, gt in zip(present, pg.out):
             grads[i] = gt
-        ws_floats = spec.sizes(R, bf16)[2]
-        ws = WS.get(ws_floats, xh.device, 5)
         dx = torch.empty((R, d0), device=xh.device)
         pp = spec.param_ptrs if spec.param_ptrs is not None else spec.pointers(params)
-        call("vt_resmlp_bf16_bwd" if bf16 else "vt_resmlp_bwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip,
-             spec.eps, pp, ptr(g2), ptr(xh), ptr(rs), R, ptr(dx), spec.grad_pointers(grads), pg.acc, ptr(ws),
-             ws.numel(), _st())
+        split = bf16 and MLPB_SPLIT and spec.split_sizes(R)[3]
+        if split:
+            # the data-gradient chain here; the weight gradients from the saved dZ rows on the
+            # weight-gradient side stream when they are written in place (off the critical chain)
+            n_dz, n_wx, n_ww, _ = spec.split_sizes(R)
+            dz16 = torch.empty(n_dz, dtype=torch.bfloat16, device=xh.device)
+            wsx = WS.get(n_wx, xh.device, 5)
+            gp = spec.grad_pointers(grads)
+            call("vt_resmlp_bf16_bwd_data", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp, ptr(g2),
+                 ptr(xh), ptr(rs), R, ptr(dx), gp, pg.acc, ptr(dz16), ptr(wsx), wsx.numel(), _st())
+            side = GRAD_STREAM if (pg.direct and GRAD_STREAM is not None) else None
+            if side is not None and side.cuda_stream != _lib.stream():
+                _lib.wait_for(side)
+                with torch.cuda.stream(side):
+                    wsw = torch.empty(n_ww, device=xh.device)
+                    call("vt_resmlp_bf16_bwd_weight", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp,
+                         ptr(xh), ptr(dz16), R, gp, pg.acc, ptr(wsw), wsw.numel(), _st())
+                dz16.record_stream(side)
+                xh.record_stream(side)
+            else:
+                wsw = torch.empty(n_ww, device=xh.device)
+                call("vt_resmlp_bf16_bwd_weight", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp,
+                     ptr(xh), ptr(dz16), R, gp, pg.acc, ptr(wsw), wsw.numel(), _st())
+        else:
+            ws_floats = spec.sizes(R, bf16)[2]
+            ws = WS.get(ws_floats, xh.device, 5)
+            call("vt_resmlp_bf16_bwd" if bf16 else "vt_resmlp_bwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip,
+                 spec.eps, pp, ptr(g2), ptr(xh), ptr(rs), R, ptr(dx), spec.grad_pointers(grads), pg.acc, ptr(ws),
+                 ws.numel(), _st())
         res = pg.result()
         out = [None] * len(params)
         for i, gt in zip(present, res):
