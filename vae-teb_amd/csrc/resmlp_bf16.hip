@@ -1127,15 +1127,18 @@ __global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, c
     f32x4 acc[MT];
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int64_t Rz = (R + DWROWS - 1) / DWROWS * DWROWS;   // rows past it are all 0: skipped
     const int64_t r0 = (int64_t)blockIdx.x * chunk_rows;
-    const int64_t r1 = r0 + chunk_rows < Rp ? r0 + chunk_rows : Rp;
+    const int64_t r1 = r0 + chunk_rows < Rz ? r0 + chunk_rows : Rz;
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     for (int64_t rb = r0; rb < r1; rb += DWROWS) {
-        // dZ rows: 16-B pieces (8 bf16), zs / 8 per row
+        // dZ rows: 16-B pieces (8 bf16), zs / 8 per row; rows past R are 0 (k_mlpb_bwdx writes
+        // the rows of its blocks only, not up to the padded Rp)
         const int zq = zs >> 3;
         for (int e = tid; e < DWROWS * zq; e += 256) {
             const int r = e / zq, q = e - r * zq;
-            const uint4 v = *(const uint4*)(zsrc + (rb + r) * zs + 8 * q);
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (rb + r < R) v = *(const uint4*)(zsrc + (rb + r) * zs + 8 * q);
             *(uint4*)(zimg + dz_pos(r, 8 * q)) = v;
         }
         // H rows: act(xhat gamma + beta), 0 past K and for rows past R
