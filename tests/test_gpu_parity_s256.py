@@ -556,6 +556,10 @@ def test_bench_batch_fp32_step_vs_fp64_oracle():
                     if k not in heads and gr.norm() > 0), reverse=True)
     for e, e32, k in table[:15]:
         print(f"  worst: {k}: ours {e:.3e}, oracle fp32 {e32:.3e}")
+    big = sorted(((g_o[k].double().norm().item(), k) for k in g_o), reverse=True)[:10]
+    for nrm, k in big:
+        print(f"  largest: {k}: |grad| {nrm:.5f}; rel-L2 ours {rel(params[k].grad, g_o[k]):.3e}, oracle fp32 "
+              f"{rel(g_o32[k], g_o[k]):.3e}")
     errs = np.array([e for e, e32, k in table if e32 < 1e-3])
     e32 = np.array([e32 for e, e32, k in table])
     print(f"B=256 grads vs fp64 oracle over {len(errs)} well-conditioned non-head gradients: median "
@@ -564,4 +568,14 @@ def test_bench_batch_fp32_step_vs_fp64_oracle():
     assert abs(gn - gn_o) <= max(1e-5 * gn_o, 2 * abs(gn_o32 - gn_o)), (gn, gn_o, gn_o32)
     for k, (a, e, e32_) in hn.items():
         assert abs(a - e) <= max(1e-5 * e, 2 * abs(e32_ - e)), (k, a, e, e32_)
-    assert len(errs) >= 300 and np.median(errs) <= 2e-5 and np.percentile(errs, 90) <= 5e-5, errs
+    # at B = 256 an fp32 step is itself ~6e-4 (median) from fp64 — 17 BatchNorms reducing over up
+    # to 1M rows, 256-step LSTMs (measured: the oracle's own fp32 median 6.2e-4, max 5.3e-3) — so
+    # the fixed J=6 bounds (median 2e-5) do not apply; the HIP step is held to the oracle's own
+    # fp32 error: median and p90 within 2x of it, and every gradient within 10x + 2e-5
+    e32w = np.array([e32 for e, e32, k in table if e32 < 1e-3])
+    assert len(errs) >= 300, len(errs)
+    assert np.median(errs) <= max(2e-5, 2 * np.median(e32w)), (np.median(errs), np.median(e32w))
+    assert np.percentile(errs, 90) <= max(5e-5, 2 * np.percentile(e32w, 90)), (np.percentile(errs, 90),
+                                                                                 np.percentile(e32w, 90))
+    worst = max((e / (2e-5 + 10 * e32), k) for e, e32, k in table)
+    assert worst[0] <= 1.0, worst

@@ -47,3 +47,7 @@ while 7 + 6 * step < 255 and (st[:, 7 + 6 * step] > 0).all():
     prev = cols[5]
     step += 1
 print(f"  input LN + dx    {us((st[:, 255] - prev).mean()):7.2f} us")
+if (st[:, 243] > 0).all():   # step 1, first tile of the dZ pass: LN backward | colsum | dZ image | fragments
+    c = [st[:, 2 + 6], st[:, 240], st[:, 241], st[:, 242], st[:, 243]]
+    print("  step 1 dZ pass, tile 0: " + "  ".join(f"{n} {us((c[i + 1] - c[i]).mean()):5.2f}" for i, n in
+                                                  enumerate(("LN bwd", "colsum", "dZ image", "frags"))))

@@ -18,30 +18,41 @@ namespace vt {
 static constexpr int OPT_THREADS = 256;
 static constexpr int NORM_BLOCKS = 1024;
 
+// Sum of squares in double: each thread squares in fp32 (exact products of fp32 values need
+// 48 bits; the fp32 rounding of one square is 6e-8 relative) and accumulates in double, the
+// workgroup and the final reduction in double — an fp32 running sum over ~260 positive squares
+// per thread and a 256-way fp32 tree drifted by ~4e-5 of the 67.8 M-parameter norm (the B = 256
+// fp32 step vs the fp64 oracle: tests/test_gpu_parity_s256.py), 16x the reference's own fp32
+// clip_grad_norm_ error.
 __global__ __launch_bounds__(OPT_THREADS) void k_sumsq(const float* __restrict__ g, int64_t n,
-                                                       float* __restrict__ partial) {
-    __shared__ float red[16];
-    float a = 0.f;
+                                                       double* __restrict__ partial) {
+    __shared__ double red[OPT_THREADS];
+    double a = 0.0;
     const int64_t n4 = n >> 2;
     const float4* g4 = reinterpret_cast<const float4*>(g);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const float4 v = g4[i];
-        a += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        a += (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z) + (double)(v.w * v.w);
     }
     for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
-        a += g[i] * g[i];
-    const float t = block_sum(a, red);
-    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+        a += (double)(g[i] * g[i]);
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int o = OPT_THREADS / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
 // out[0] = ||pre_scale * g||, out[1] = pre_scale * clip_coef (the factor the
 // optimiser applies to the raw gradient buffer).
-__global__ void k_norm_finalize(const float* __restrict__ partial, int count, float pre_scale, float max_norm,
+__global__ void k_norm_finalize(const double* __restrict__ partial, int count, float pre_scale, float max_norm,
                                 float* __restrict__ out) {
     __shared__ double red[256];
     double a = 0.0;
-    for (int i = threadIdx.x; i < count; i += blockDim.x) a += (double)partial[i];
+    for (int i = threadIdx.x; i < count; i += blockDim.x) a += partial[i];
     red[threadIdx.x] = a;
     __syncthreads();
     for (int o = blockDim.x / 2; o > 0; o >>= 1) {
@@ -334,14 +345,15 @@ using namespace vt;
 
 extern "C" {
 
-int vt_grad_norm_workspace_floats(void) { return NORM_BLOCKS; }
+int vt_grad_norm_workspace_floats(void) { return 2 * NORM_BLOCKS; }   // NORM_BLOCKS doubles
 
 int vt_grad_norm_clip(const float* g, int64_t n, float pre_scale, float max_norm, float* out2, float* ws,
                       void* stream) {
     VT_CHECK_ARG(n > 0, "vt_grad_norm_clip: empty");
     const int blocks = grid_for(n / 4 + 1, NORM_BLOCKS);
-    hipLaunchKernelGGL(k_sumsq, dim3(blocks), dim3(OPT_THREADS), 0, S(stream), g, n, ws);
-    hipLaunchKernelGGL(k_norm_finalize, dim3(1), dim3(256), 0, S(stream), ws, blocks, pre_scale, max_norm, out2);
+    double* wd = reinterpret_cast<double*>(ws);
+    hipLaunchKernelGGL(k_sumsq, dim3(blocks), dim3(OPT_THREADS), 0, S(stream), g, n, wd);
+    hipLaunchKernelGGL(k_norm_finalize, dim3(1), dim3(256), 0, S(stream), wd, blocks, pre_scale, max_norm, out2);
     VT_LAUNCH_CHECK("vt_grad_norm_clip");
     return VT_OK;
 }

@@ -869,9 +869,13 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
                     ln_bwd<NT>(dz, xc[u], rsc[u], N, gl, gl + p16(N), d.l[l].act, la);
                 }
             }
+            if (step == 1 && u == 0) MB_STAMP(240);   // diagnostic sub-phases of step 1, first tile
             colsum<NT>(dz, N, lb);            // the bias gradient: fp32 sum of dZ (not of its bf16 image)
+            if (step == 1 && u == 0) MB_STAMP(241);
             put_img<NT, IS>(zimg, dz, N, 128 * u + 16 * wv);
+            if (step == 1 && u == 0) MB_STAMP(242);
             frags<NT>(dz, b[u]);
+            if (step == 1 && u == 0) MB_STAMP(243);
         }
         MB_STAMP(3 + 6 * step);
         if constexpr (!PF) {

@@ -108,7 +108,7 @@ def _l16_pair_fits(S):
     return _L16_PAIR_NS * ((S + 15) // 16) * 16 * 72 * 2 <= 120 * 1024
 # bf16 ResidualMLP backward split in two (vt_resmlp_bf16_bwd_data on the chain, the weight gradients
 # from the saved dZ rows on the weight-gradient side stream); 0: the one-kernel backward
-MLPB_SPLIT = int(os.environ.get("VAETEB_MLPB_SPLIT", "1"))
+MLPB_SPLIT = int(os.environ.get("VAETEB_MLPB_SPLIT", "0"))
 # bf16 conv backward-data written straight into dX where the fold is a crop; 0: gpad + fold
 CONV_DIRECT_DX = int(os.environ.get("VAETEB_CONV_DIRECT_DX", "1"))
 # conv-block backward as vt_batchnorm_bwd_x16 + vt_conv1d_bwd_dx16 (bf16 operand written once,
