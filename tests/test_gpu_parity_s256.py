@@ -546,7 +546,14 @@ def test_bench_batch_fp32_step_vs_fp64_oracle():
     # everything is printed first (the assertions follow): the norms (97 % of the squared gradient
     # norm is in the heads) and every gradient's rel-L2 to the fp64 oracle beside the oracle's own
     # fp32 distance
-    print(f"grad norm: ours {gn:.7f}, oracle fp64 {gn_o:.7f}, oracle fp32 {gn_o32:.7f}")
+    gn_d = norm(p.grad for p in params.values())
+    print(f"grad norm: ours {gn:.7f} (fp64 norm of our gradients {gn_d:.7f}), oracle fp64 {gn_o:.7f}, "
+          f"oracle fp32 {gn_o32:.7f}")
+    contrib = sorted(((params[k].grad.double().norm().item() ** 2 - g.double().norm().item() ** 2, k)
+                      for k, g in g_o.items()), key=lambda t: -abs(t[0]))[:8]
+    for dsq, k in contrib:
+        print(f"  |grad|^2 ours - oracle: {k}: {dsq:+.3e} (oracle fp32 "
+              f"{g_o32[k].double().norm().item() ** 2 - g_o[k].double().norm().item() ** 2:+.3e})")
     hn = {}
     for k in sorted(heads):
         hn[k] = (params[k].grad.double().norm().item(), g_o[k].double().norm().item(), g_o32[k].double().norm().item())
