@@ -52,27 +52,35 @@ def _ln_bwd(du, xhat, rstd, g):
 
 def ref_step(m, x, gy, rounding=True, margins=None):
     """fp64 forward + explicit backward of a ResidualMLP; GEMM operands rounded
-    to bf16 where the kernels round them (rounding=True). Returns (y, grads)."""
+    to bf16 where the kernels round them (rounding=True). Returns (y, grads).
+
+    With rounding the backward also sees the saved LayerNorm state xhat rounded to fp16,
+    as the bf16 kernels store it (resmlp_bf16.hip load_sv): the LayerNorm gradients and
+    the recomputed activations (GEMM inputs of the weight gradients) derive from it."""
     r = bf if rounding else (lambda t: t)
+    q = (lambda t: t.half().double()) if rounding else (lambda t: t)
     P = {n: p.detach().double().cpu() for n, p in m.named_parameters()}
     G = {}
     x0h, rs0 = _ln(x)
-    x0 = x0h * P["input_norm.weight"] + P["input_norm.bias"]
-    h, saved = x0, []
+    x0h = q(x0h)
+    x0 = _ln(x)[0] * P["input_norm.weight"] + P["input_norm.bias"]
+    x0b = x0h * P["input_norm.weight"] + P["input_norm.bias"]     # backward's recomputed x0
+    h, hb, saved = x0, x0b, []
     for idx, has_ln, a in m._plan:
         W, b = P[f"body.{idx}.weight"], P[f"body.{idx}.bias"]
         z = r(h) @ r(W).T + b
-        rec = {"idx": idx, "hin": h, "ln": has_ln, "act": a}
+        rec = {"idx": idx, "hin": hb, "ln": has_ln, "act": a}
         if has_ln:
             g, be = P[f"body.{idx + 1}.weight"], P[f"body.{idx + 1}.bias"]
             xh, rs = _ln(z)
             u = xh * g + be
+            ub = q(xh) * g + be
             if margins is not None and a == "relu":
-                margins.append(u.abs().min(dim=-1).values)
-            rec.update(xh=xh, rs=rs, u=u)
-            h = ACT[a][0](u)
+                margins.append(torch.minimum(u.abs(), ub.abs()).min(dim=-1).values)
+            rec.update(xh=q(xh), rs=rs, u=ub)
+            h, hb = ACT[a][0](u), ACT[a][0](ub)
         else:
-            h = z
+            h = hb = z
         saved.append(rec)
     skip = None
     if m.use_skip_connection:
@@ -96,7 +104,7 @@ def ref_step(m, x, gy, rounding=True, margins=None):
         G[f"body.{idx}.bias"] = dz.sum(0)
         dh = r(dz) @ r(P[f"body.{idx}.weight"])
     if skip == "proj":
-        G["skip_proj.weight"] = r(gy).T @ r(x0)
+        G["skip_proj.weight"] = r(gy).T @ r(x0b)
         G["skip_proj.bias"] = gy.sum(0)
         dh = dh + r(gy) @ r(P["skip_proj.weight"])
     elif skip == "id":

@@ -284,15 +284,37 @@ __device__ __forceinline__ void store_rows(float* dst, const f32x4 (&a)[NT], int
     }
 }
 
-// saved state: row-major [Rp][pad16(C)] (float4 per lane and tile), rows past R read 0
+// Saved LayerNorm state xhat: fp16, row-major [Rp][pad16(C)] per LN layer (4 halves = 8 bytes per
+// lane and tile), rows past R read 0.  xhat is normalised (|xhat| <= sqrt(C) <= 12), so fp16 keeps
+// 11 significant bits over its whole range: the backward's LayerNorm gradient and its recomputed
+// GEMM input (rounded to bf16 anyway) see it at the precision the reference's autocast gives the
+// LayerNorm input (the 16-bit Linear output), at half the bytes of fp32 (round 5).
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+// the region of LN layer xo (feature offset, x Rp rows) in the saved-state buffer
+__device__ __forceinline__ const _Float16* xh_region(const float* xh, int64_t xo, int64_t Rp) {
+    return reinterpret_cast<const _Float16*>(xh) + xo * Rp;
+}
+// raw halves (2 VGPRs per tile, converted where used: a prefetch stays in flight across barriers)
 template <int NT>
-__device__ __forceinline__ void load_sv(f32x4 (&a)[NT], const float* src, int C, int64_t Rp, int64_t row, bool rok) {
+__device__ __forceinline__ void load_sv(u32x2 (&a)[NT], const _Float16* src, int C, int64_t Rp, int64_t row,
+                                        bool rok) {
     const int g4 = (threadIdx.x & 63) >> 4;
     const int nt = (C + 15) >> 4;
-    const rsrc_t r = brs(src, Rp * 64 * nt);
-    const unsigned base = rok ? (unsigned)((row * 16 * nt + 4 * g4) * 4) : OOB;
+    const rsrc_t r = brs(src, Rp * 32 * nt);
+    const unsigned base = rok ? (unsigned)((row * 16 * nt + 4 * g4) * 2) : OOB;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) a[t] = t < nt ? bld4(r, base + 64 * t) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NT; ++t)
+        a[t] = t < nt ? __builtin_amdgcn_raw_buffer_load_b64(r, (int)(base + 32 * t), 0, 0) : u32x2{0u, 0u};
+}
+__device__ __forceinline__ f32x4 sv_f32(u32x2 v) {
+    const h16x4 h = __builtin_bit_cast(h16x4, v);
+    return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+}
+template <int NT>
+__device__ __forceinline__ void sv_f32(const u32x2 (&a)[NT], f32x4 (&o)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) o[t] = sv_f32(a[t]);
 }
 
 __device__ __forceinline__ float sum_groups(float v) {  // over the 4 lane groups (same row)
@@ -306,7 +328,7 @@ __device__ __forceinline__ float sum_groups(float v) {  // over the 4 lane group
 // leaves h (0 past C).
 template <int NT>
 __device__ __forceinline__ void ln_fwd(f32x4 (&z)[NT], int C, const float* gl, const float* bl, int act, float eps,
-                                       float* xh, float* rs, int64_t Rp, int64_t row, bool rok) {
+                                       _Float16* xh, float* rs, int64_t Rp, int64_t row, bool rok) {
     const int lane = threadIdx.x & 63, g4 = lane >> 4;
     const int nt = (C + 15) >> 4;
     const float invC = 1.f / (float)C;
@@ -330,13 +352,14 @@ __device__ __forceinline__ void ln_fwd(f32x4 (&z)[NT], int C, const float* gl, c
     }
     const float rstd = rsqrtf(sum_groups(v) * invC + eps);
     bst(brs(rs, Rp * 4), (rok && g4 == 0) ? (unsigned)(row * 4) : OOB, rstd);
-    const rsrc_t rx = brs(xh, Rp * 64 * nt);
-    const unsigned bx = rok ? (unsigned)((row * 16 * nt + 4 * g4) * 4) : OOB;
+    const rsrc_t rx = brs(xh, Rp * 32 * nt);     // fp16 saved state (load_sv)
+    const unsigned bx = rok ? (unsigned)((row * 16 * nt + 4 * g4) * 2) : OOB;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         if (t < nt) {
             z[t] *= rstd;                               // xhat (0 past C)
-            bst4(rx, bx + 64 * t, z[t]);
+            const h16x4 hv = {(_Float16)z[t][0], (_Float16)z[t][1], (_Float16)z[t][2], (_Float16)z[t][3]};
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hv), rx, (int)(bx + 32 * t), 0, 0);
             const f32x4 gv = *(const f32x4*)(gl + 16 * t + 4 * g4);
             const f32x4 bv = *(const f32x4*)(bl + 16 * t + 4 * g4);
             z[t] = z[t] * gv + bv;                      // gamma / beta are 0 past C
@@ -489,7 +512,8 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
         const bool rok = row < R;
         f32x4 a[NT];
         load_rows<NT>(a, X, d0, R, row);
-        ln_fwd<NT>(a, d0, prm + d.pin, prm + d.pin + p16(d0), 0, d.eps, xh, rs, Rp, row, rok);
+        _Float16* xh16 = reinterpret_cast<_Float16*>(xh);
+        ln_fwd<NT>(a, d0, prm + d.pin, prm + d.pin + p16(d0), 0, d.eps, xh16, rs, Rp, row, rok);
         f32x4 x0[ID ? NT : 1];
         if constexpr (ID) {
 #pragma unroll
@@ -506,7 +530,7 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
             for (int t = 0; t < NT; ++t) a[t] += *(const f32x4*)(prm + po + 16 * t + 4 * g4);   // bias (0 past N)
             if (d.l[l].ln)
                 ln_fwd<NT>(a, N, prm + po + p16(N), prm + po + 2 * p16(N), d.l[l].act, d.eps,
-                           xh + (int64_t)d.l[l].xo * Rp, rs + (int64_t)d.l[l].ri * Rp, Rp, row, rok);
+                           xh16 + (int64_t)d.l[l].xo * Rp, rs + (int64_t)d.l[l].ri * Rp, Rp, row, rok);
             if (l < L - 1) frags<NT>(a, b);
         }
         if constexpr (ID) {
@@ -801,7 +825,8 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
     const float* prm_in = prm + d.bpin;
     MB_STAMP(1);
 
-    f32x4 dh[TPW][NT], xc[TPW][NT];            // output gradient / raw xhat of the current layer
+    f32x4 dh[TPW][NT];                         // output gradient
+    u32x2 xc[TPW][NT];                         // fp16 xhat of the current layer
     float rsc[TPW];                            // rstd of the current layer's LayerNorm (prefetched with xc)
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
@@ -809,7 +834,7 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
         load_rows<NT>(dh[u], dout, DL, R, row);
         rsc[u] = 0.f;
         if (d.l[L - 1].ln) {
-            load_sv<NT>(xc[u], xh + (int64_t)d.l[L - 1].xo * Rp, DL, Rp, row, row < R);
+            load_sv<NT>(xc[u], xh_region(xh, d.l[L - 1].xo, Rp), DL, Rp, row, row < R);
             rsc[u] = bld(brs(rs + (int64_t)d.l[L - 1].ri * Rp, Rp * 4), row < R ? (unsigned)(row * 4) : OOB);
         }
     }
@@ -824,12 +849,12 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
         const int hsrc = skp ? -1 : l - 1;    // H = output of layer hsrc (-1: x0, the input LN output)
         const float* gH = hsrc >= 0 ? prm + d.l[hsrc].bpo : prm_in;
         const int CH = hsrc >= 0 ? d.G[hsrc].N : d0, actH = hsrc >= 0 ? d.l[hsrc].act : 0;
-        const float* xH = xh + (hsrc >= 0 ? (int64_t)d.l[hsrc].xo * Rp : 0);
+        const _Float16* xH = xh_region(xh, hsrc >= 0 ? d.l[hsrc].xo : 0, Rp);
         const rsrc_t rH = brs(rs + (hsrc >= 0 ? (int64_t)d.l[hsrc].ri * Rp : 0), Rp * 4);   // its rstd
         // the H source rows: in flight during the LayerNorm backward below (the
         // widest stacks load them after it, for registers)
         constexpr bool PF = NT <= 6;
-        f32x4 xn[TPW][NT];
+        u32x2 xn[TPW][NT];
         float rsn[TPW];
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
@@ -866,7 +891,9 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
                 for (int t = 0; t < NT; ++t) dz[t] = dh[u][t];
                 if (ln) {
                     const float* gl = prm + d.l[l].bpo;
-                    ln_bwd<NT>(dz, xc[u], rsc[u], N, gl, gl + p16(N), d.l[l].act, la);
+                    f32x4 xf[NT];
+                    sv_f32<NT>(xc[u], xf);
+                    ln_bwd<NT>(dz, xf, rsc[u], N, gl, gl + p16(N), d.l[l].act, la);
                 }
             }
             if (step == 1 && u == 0) MB_STAMP(240);   // diagnostic sub-phases of step 1, first tile
@@ -892,7 +919,8 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
             f32x4 hv[NT];
 #pragma unroll
             for (int t = 0; t < NT; ++t)
-                hv[t] = xn[u][t] * *(const f32x4*)(gH + 16 * t + 4 * g4) + *(const f32x4*)(gH + p16(CH) + 16 * t + 4 * g4);
+                hv[t] = sv_f32(xn[u][t]) * *(const f32x4*)(gH + 16 * t + 4 * g4) +
+                        *(const f32x4*)(gH + p16(CH) + 16 * t + 4 * g4);
             act_tile<NT>(hv, actH);
             if (!rok) {
 #pragma unroll
@@ -944,7 +972,9 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
         const int64_t row = rbase + IMR * u;
-        ln_bwd<NT>(dh[u], xc[u], rsc[u], d0, prm_in, prm_in + p16(d0), 0, la);   // rsc: the input LN's rstd
+        f32x4 xf[NT];
+        sv_f32<NT>(xc[u], xf);
+        ln_bwd<NT>(dh[u], xf, rsc[u], d0, prm_in, prm_in + p16(d0), 0, la);   // rsc: the input LN's rstd
         store_rows<NT>(dx, dh[u], d0, R, row);
     }
     __syncthreads();
@@ -992,7 +1022,8 @@ __global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx
     lds_copy_wait();
     const float* prm_in = prm + d.bpin;
 
-    f32x4 dh[TPW][NT], xc[TPW][NT];
+    f32x4 dh[TPW][NT];
+    u32x2 xc[TPW][NT];
     float rsc[TPW];
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
@@ -1000,7 +1031,7 @@ __global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx
         load_rows<NT>(dh[u], dout, DL, R, row);
         rsc[u] = 0.f;
         if (d.l[L - 1].ln) {
-            load_sv<NT>(xc[u], xh + (int64_t)d.l[L - 1].xo * Rp, DL, Rp, row, row < R);
+            load_sv<NT>(xc[u], xh_region(xh, d.l[L - 1].xo, Rp), DL, Rp, row, row < R);
             rsc[u] = bld(brs(rs + (int64_t)d.l[L - 1].ri * Rp, Rp * 4), row < R ? (unsigned)(row * 4) : OOB);
         }
     }
@@ -1014,7 +1045,7 @@ __global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx
         const bool ln = !skp && d.l[l].ln;
         const int hsrc = skp ? -1 : l - 1;
         const int CH = hsrc >= 0 ? d.G[hsrc].N : d0;
-        const float* xH = xh + (hsrc >= 0 ? (int64_t)d.l[hsrc].xo * Rp : 0);
+        const _Float16* xH = xh_region(xh, hsrc >= 0 ? d.l[hsrc].xo : 0, Rp);
         const rsrc_t rH = brs(rs + (hsrc >= 0 ? (int64_t)d.l[hsrc].ri * Rp : 0), Rp * 4);
         float la[NT], lb[NT];
 #pragma unroll
@@ -1032,7 +1063,9 @@ __global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx
                 for (int t = 0; t < NT; ++t) dz[t] = dh[u][t];
                 if (ln) {
                     const float* gl = prm + d.l[l].bpo;
-                    ln_bwd<NT>(dz, xc[u], rsc[u], N, gl, gl + p16(N), d.l[l].act, la);
+                    f32x4 xf[NT];
+                    sv_f32<NT>(xc[u], xf);
+                    ln_bwd<NT>(dz, xf, rsc[u], N, gl, gl + p16(N), d.l[l].act, la);
                 }
             }
             // the next step's LayerNorm input (this GEMM's input's xhat) into the registers just
@@ -1079,7 +1112,9 @@ __global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
         const int64_t row = rbase + IMR * u;
-        ln_bwd<NT>(dh[u], xc[u], rsc[u], d0, prm_in, prm_in + p16(d0), 0, la);
+        f32x4 xf[NT];
+        sv_f32<NT>(xc[u], xf);
+        ln_bwd<NT>(dh[u], xf, rsc[u], d0, prm_in, prm_in + p16(d0), 0, la);
         store_rows<NT>(dx, dh[u], d0, R, row);
     }
     flush_cols<NT>(red + (nsteps & 1) * (NW * 48 * NT), la, lb, d0, true, pb + d.xlpo0, nullptr, 0);
@@ -1123,7 +1158,7 @@ __global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, c
     const float* bet = hsrc >= 0 ? d.l[hsrc].be : d.be0;
     const int actH = hsrc >= 0 ? d.l[hsrc].act : 0;
     const int kp = p16(K);                // saved-xhat row stride (floats)
-    const float* xH = xh + (hsrc >= 0 ? (int64_t)d.l[hsrc].xo * Rp : 0);
+    const _Float16* xH = xh_region(xh, hsrc >= 0 ? d.l[hsrc].xo : 0, Rp);
     const __bf16* zsrc = dz16 + G.zo;
     const int zs = G.zs;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lc = lane >> 4;
@@ -1150,9 +1185,9 @@ __global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, c
         for (int e = tid; e < DWROWS * hq; e += 256) {
             const int r = e / hq, q = e - r * hq;
             const int64_t row = rb + r;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (row < R) v = *(const float4*)(xH + row * kp + 4 * q);
-            float h[4] = {v.x, v.y, v.z, v.w};
+            h16x4 v = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+            if (row < R) v = *(const h16x4*)(xH + row * kp + 4 * q);
+            float h[4] = {(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int k = 4 * q + i;
@@ -1398,7 +1433,7 @@ int make_bplan(BPlan& p, int n_layers, const int* dims, const int* layer_ln, con
     const int blk = IMR * p.tpw;
     p.Rp = (R + 2 * IMR - 1) / (2 * IMR) * (2 * IMR);   // the saved state is padded for either block size
     p.nblk = (R + blk - 1) / blk;
-    p.xh_floats = (int64_t)xo * p.Rp;
+    p.xh_floats = ((int64_t)xo * p.Rp + 1) / 2;   // fp16 saved state
     p.rs_floats = (int64_t)(1 + n_ln) * p.Rp;
     // split backward (k_mlpb_bwdx + k_mlpb_dw)
     int xP = 0;
