@@ -16,6 +16,14 @@ void set_error(const char* fmt, ...) {
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
 }
+
+unsigned arrive_slots(unsigned n) {
+    static std::atomic<unsigned> next{0};
+    for (;;) {
+        const unsigned b = next.fetch_add(n) % ARRIVE_POOL;
+        if (b + n <= ARRIVE_POOL) return b;
+    }
+}
 }  // namespace vt
 
 extern "C" {

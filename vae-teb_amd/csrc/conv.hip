@@ -489,31 +489,32 @@ static int launch_fwd(const float* x, const Geo& g, const float* w, float* y, in
 // leaves each group's sum in place in the group's first slab; stage 2 sums the
 // groups in order.
 static constexpr int SG_GRP = 32;
+VT_ARRIVE_POOL(g_arrive_splits);
 
-__global__ __launch_bounds__(256) void k_sum_splits_grp(float* __restrict__ part, int splits, int64_t n) {
+// stage 1 per workgroup; the workgroup that arrives last among a column block's groups runs
+// stage 2 for that block (the same fixed tree over the group sums as a separate pass would:
+// the same bits, one launch)
+__global__ __launch_bounds__(256) void k_sum_splits_grp(float* __restrict__ part, int splits, int64_t n,
+                                                        float* __restrict__ out, int accumulate, unsigned slot0) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
     const int s0 = blockIdx.y * SG_GRP;
     const int s1 = s0 + SG_GRP < splits ? s0 + SG_GRP : splits;
-    // every load of the group in flight at once, then a fixed pairwise tree
     float a[SG_GRP];
+    const __amdgpu_buffer_rsrc_t pr = agent_rsrc(part, (int64_t)splits * n * 4);   // splits * n < 2^29 (bwd_weight)
+    if (i < n) {
+        // every load of the group in flight at once, then a fixed pairwise tree
 #pragma unroll
-    for (int u = 0; u < SG_GRP; ++u) a[u] = s0 + u < s1 ? part[(int64_t)(s0 + u) * n + i] : 0.f;
+        for (int u = 0; u < SG_GRP; ++u) a[u] = s0 + u < s1 ? part[(int64_t)(s0 + u) * n + i] : 0.f;
 #pragma unroll
-    for (int w = SG_GRP / 2; w >= 1; w /= 2)
+        for (int w = SG_GRP / 2; w >= 1; w /= 2)
 #pragma unroll
-        for (int u = 0; u < w; ++u) a[u] += a[u + w];
-    part[(int64_t)s0 * n + i] = a[0];
-}
-
-__global__ __launch_bounds__(256) void k_sum_splits_fin(const float* __restrict__ part, int splits, int64_t n,
-                                                        float* __restrict__ out, int accumulate) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+            for (int u = 0; u < w; ++u) a[u] += a[u + w];
+        st_agent(pr, (unsigned)(((int64_t)s0 * n + i) * 4), a[0]);
+    }
+    if (!last_arrival(&g_arrive_splits[slot0 + blockIdx.x], gridDim.y) || i >= n) return;
     // the group sums (<= SG_GRP of them: splits <= SG_GRP^2) in flight at once, fixed tree
-    float a[SG_GRP];
 #pragma unroll
-    for (int u = 0; u < SG_GRP; ++u) a[u] = u * SG_GRP < splits ? part[(int64_t)u * SG_GRP * n + i] : 0.f;
+    for (int u = 0; u < SG_GRP; ++u) a[u] = ld_agent(pr, u * SG_GRP < splits ? (unsigned)(((int64_t)u * SG_GRP * n + i) * 4) : 0x80000000u);   // past the array: 0
 #pragma unroll
     for (int w = SG_GRP / 2; w >= 1; w /= 2)
 #pragma unroll
@@ -535,8 +536,7 @@ int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int 
     float* p = const_cast<float*>(part);
     const unsigned bx = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_sum_splits_grp, dim3(bx, (unsigned)((splits + SG_GRP - 1) / SG_GRP)), dim3(256), 0, st, p,
-                       splits, n);
-    hipLaunchKernelGGL(k_sum_splits_fin, dim3(bx), dim3(256), 0, st, p, splits, n, out, accumulate);
+                       splits, n, out, accumulate, arrive_slots(bx));
     return VT_OK;
 }
 
