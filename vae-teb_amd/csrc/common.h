@@ -75,6 +75,14 @@ __device__ __forceinline__ float ld_agent(__amdgpu_buffer_rsrc_t r, unsigned off
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, CPOL_SC1));
 }
 
+__device__ __forceinline__ void st_agent(__amdgpu_buffer_rsrc_t r, unsigned off, double v) {
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0, CPOL_SC1);
+}
+__device__ __forceinline__ double ld_agent_d(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, CPOL_SC1));
+}
+
 // true in every thread of the workgroup that arrives last of `total` on *ctr; the caller's
 // partial stores (st_agent) are complete before the arrival
 __device__ __forceinline__ bool last_arrival(unsigned* ctr, unsigned total) {

@@ -11,6 +11,7 @@
 // momentum 0.9, eps 1e-5) + ReLU/tanh for the conv blocks
 // (ref/model/vae_teb_model.py:175, :206-210, :230, :252-253).
 #include <math.h>
+#include <stdlib.h>
 
 #include "bnbwd.h"
 #include "common.h"
@@ -385,26 +386,59 @@ __global__ __launch_bounds__(NT) void k_reduce_parts(const float* __restrict__ p
 
 // ------------------------------------------------------------- BatchNorm
 // mode 0: mean[c] = S/M.  mode 1: var = S/M -> rstd, running stats update.
-// mode 2: dbeta = S0, dgamma = S1.
-// one workgroup per channel; double accumulation, fixed-order tree.  part is
-// channel-major ([2][C][blocks], k_col_partial4): thread t sums blocks t, t + NT, ...
-// in that order with four coalesced loads in flight.
-__global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ part, int blocks, int C, int64_t M,
-                                                    int mode, float eps, float momentum, float* __restrict__ mean,
-                                                    float* __restrict__ rstd, float* __restrict__ run_mean,
-                                                    float* __restrict__ run_var, float* __restrict__ dgamma,
-                                                    float* __restrict__ dbeta, int accumulate,
-                                                    float* __restrict__ bnp = nullptr, const float* __restrict__ gamma = nullptr,
-                                                    const float* __restrict__ beta = nullptr,
-                                                    float* __restrict__ pg = nullptr, float* __restrict__ pb = nullptr,
-                                                    int pacc = 0) {
+// mode 2: dbeta = S0, dgamma = S1 (+ the packed coefficients of vt_batchnorm_bwd_coef).
+struct BnFin {
+    int mode;   // < 0: the column-partial kernel only writes its partials (a separate finaliser)
+    int64_t M;
+    float eps, momentum;
+    float *mean, *rstd, *run_mean, *run_var, *dgamma, *dbeta;
+    int accumulate;
+    float* bnp;
+    const float *gamma, *beta;
+    float *pg, *pb;
+    int pacc;
+    double* gpart;    // in-kernel finalize: the group sums ([2C][groups] doubles)
+    unsigned slot0;   // its arrival counters (groups + 1)
+};
+
+__device__ __forceinline__ void bn_fin_channel(int c, int C, double s0, double s1, const BnFin& f) {
+    const int64_t M = f.M;
+    if (f.mode == 0) {
+        f.mean[c] = (float)(s0 / (double)M);
+    } else if (f.mode == 1) {
+        const double var = s0 / (double)M;
+        f.rstd[c] = (float)(1.0 / sqrt(var + (double)f.eps));
+        if (f.run_mean) {
+            const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+            f.run_mean[c] = (float)((1.0 - f.momentum) * f.run_mean[c] + f.momentum * f.mean[c]);
+            f.run_var[c] = (float)((1.0 - f.momentum) * f.run_var[c] + f.momentum * unb);
+        }
+    } else {
+        f.dbeta[c] = f.accumulate ? f.dbeta[c] + (float)s0 : (float)s0;
+        f.dgamma[c] = f.accumulate ? f.dgamma[c] + (float)s1 : (float)s1;
+        if (f.bnp) {   // vt_batchnorm_bwd_coef: the packed parameters and the parameter gradients
+            f.bnp[c] = f.mean[c];
+            f.bnp[C + c] = f.rstd[c];
+            f.bnp[2 * C + c] = f.gamma[c];
+            f.bnp[3 * C + c] = f.beta[c];
+            f.pb[c] = f.pacc ? f.pb[c] + (float)s0 : (float)s0;
+            f.pg[c] = f.pacc ? f.pg[c] + (float)s1 : (float)s1;
+        }
+    }
+}
+
+// The separate finaliser (channels > 128: past the in-kernel finalize's one thread per sum):
+// one workgroup per channel; double accumulation, fixed-order tree.  part is channel-major
+// ([2][C][blocks], k_col_partial4): thread t sums blocks t, t + NT, ... in that order with
+// eight coalesced loads in flight.
+__global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ part, int blocks, int C, BnFin f) {
     __shared__ double r0[NT], r1[NT];
     const int c = blockIdx.x;
     double a0 = 0.0, a1 = 0.0;
     const float* p0 = part + (int64_t)c * blocks;
     const float* p1 = part + (int64_t)(C + c) * blocks;
     int b = threadIdx.x;
-    for (; b + 7 * NT < blocks; b += 8 * NT) {   // eight coalesced loads per array in flight, same order
+    for (; b + 7 * NT < blocks; b += 8 * NT) {
         float u[8], v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -421,8 +455,6 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ pa
         a0 += (double)p0[b];
         a1 += (double)p1[b];
     }
-    // the fixed pairwise tree (level o: r[t] += r[t + o], o = 128 .. 1), the levels below 64
-    // as wave-0 shuffles (the same additions in the same order: the same bits)
     static_assert(NT == 256, "k_bn_finalize: 256-thread tree");
     const int t = threadIdx.x;
     r0[t] = a0;
@@ -440,30 +472,54 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const float* __restrict__ pa
         x0 += __shfl_down(x0, o);
         x1 += __shfl_down(x1, o);
     }
-    if (t != 0) return;
-    const double s0 = x0, s1 = x1;
-    if (mode == 0) {
-        mean[c] = (float)(s0 / (double)M);
-    } else if (mode == 1) {
-        const double var = s0 / (double)M;
-        rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-        if (run_mean) {
-            const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-            run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean[c]);
-            run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
-        }
-    } else {
-        dbeta[c] = accumulate ? dbeta[c] + (float)s0 : (float)s0;
-        dgamma[c] = accumulate ? dgamma[c] + (float)s1 : (float)s1;
-        if (bnp) {   // vt_batchnorm_bwd_coef: the packed parameters and the parameter gradients
-            bnp[c] = mean[c];
-            bnp[C + c] = rstd[c];
-            bnp[2 * C + c] = gamma[c];
-            bnp[3 * C + c] = beta[c];
-            pb[c] = pacc ? pb[c] + (float)s0 : (float)s0;
-            pg[c] = pacc ? pg[c] + (float)s1 : (float)s1;
-        }
+    if (t == 0) bn_fin_channel(c, C, x0, x1, f);
+}
+
+// In-kernel finalize of the column partials (round 5; replaces the k_bn_finalize launch for
+// C <= 128): blocks form groups of BN_GB; the last-arriving block of a group sums its
+// group's partials per (kind, channel) in block order, in double; the last group to finish
+// sums the group sums in group order and applies bn_fin_channel.  Fixed order throughout.
+constexpr int BN_GB = 64;
+VT_ARRIVE_POOL(g_arrive_bn);
+static int g_bn_fold = getenv("VAETEB_BN_FOLD") ? atoi(getenv("VAETEB_BN_FOLD")) : 1;
+static int g_bn_fold_blocks = getenv("VAETEB_BN_BLOCKS") ? atoi(getenv("VAETEB_BN_BLOCKS")) : 512;
+#define BN_FOLD_BLOCKS ((int64_t)(g_bn_fold_blocks > 0 && g_bn_fold_blocks <= 2048 ? g_bn_fold_blocks : 512))
+
+__device__ __forceinline__ int bn_groups(int blocks) { return (blocks + BN_GB - 1) / BN_GB; }
+
+__device__ void bn_fold_finalize(const float* part, int C, const BnFin& f) {
+    __shared__ double fin[2 * 128];
+    const int blocks = gridDim.x, ng = bn_groups(blocks), g = blockIdx.x / BN_GB;
+    const int members = blocks - g * BN_GB < BN_GB ? blocks - g * BN_GB : BN_GB;
+    if (!last_arrival(&g_arrive_bn[f.slot0 + g], (unsigned)members)) return;
+    const int tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t pr = agent_rsrc(part, (int64_t)2 * C * blocks * 4);
+    const __amdgpu_buffer_rsrc_t gr = agent_rsrc(f.gpart, (int64_t)2 * C * ng * 8);
+    if (tid < 2 * C) {
+        const int b0 = g * BN_GB;
+        float v[BN_GB];
+#pragma unroll
+        for (int u = 0; u < BN_GB; ++u)
+            v[u] = ld_agent(pr, u < members ? (unsigned)(((int64_t)tid * blocks + b0 + u) * 4) : 0x80000000u);
+        double a = 0.0;
+#pragma unroll
+        for (int u = 0; u < BN_GB; ++u) a += (double)v[u];
+        st_agent(gr, (unsigned)(((int64_t)tid * ng + g) * 8), a);
     }
+    if (!last_arrival(&g_arrive_bn[f.slot0 + ng], (unsigned)ng)) return;
+    if (tid < 2 * C) {
+        constexpr int GMAX = 2048 / BN_GB;
+        double v[GMAX];
+#pragma unroll
+        for (int q = 0; q < GMAX; ++q)
+            v[q] = ld_agent_d(gr, q < ng ? (unsigned)(((int64_t)tid * ng + q) * 8) : 0x80000000u);
+        double a = 0.0;
+#pragma unroll
+        for (int q = 0; q < GMAX; ++q) a += v[q];
+        fin[tid] = a;
+    }
+    __syncthreads();
+    if (tid < C) bn_fin_channel(tid, C, fin[tid], fin[C + tid], f);
 }
 
 __global__ void k_bn_apply(const float* __restrict__ x, int64_t M, int C, const float* __restrict__ mean,
@@ -606,8 +662,20 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
                                                      int64_t M, int C, int64_t rows_per_block, int Tp,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, BnFin fin) {
     __shared__ float red0[4 * NT], red1[4 * NT];
+    // partials: plain stores for a separate finaliser, agent-coherent for the in-kernel one
+    const __amdgpu_buffer_rsrc_t pr = agent_rsrc(part, (int64_t)2 * C * gridDim.x * 4);
+    auto put = [&](int cc, float s0, float s1) {
+        const int64_t o0 = (int64_t)cc * gridDim.x + blockIdx.x, o1 = (int64_t)(C + cc) * gridDim.x + blockIdx.x;
+        if (fin.mode < 0) {
+            part[o0] = s0;
+            part[o1] = s1;
+        } else {
+            st_agent(pr, (unsigned)(o0 * 4), s0);
+            st_agent(pr, (unsigned)(o1 * 4), s1);
+        }
+    };
     const int tid = threadIdx.x;
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
@@ -717,24 +785,20 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
                 s0 += __shfl_down(s0, o);
                 s1 += __shfl_down(s1, o);
             }
-            if (lane == 0) {
-                part[(int64_t)cc * gridDim.x + blockIdx.x] = s0;
-                part[(int64_t)(C + cc) * gridDim.x + blockIdx.x] = s1;
+            if (lane == 0) put(cc, s0, s1);
+        }
+    } else {
+        for (int cc = tid; cc < C; cc += NT) {
+            float s0 = 0.f, s1 = 0.f;
+            for (int q = 0; q < groups; ++q) {
+                s0 += red0[q * C + cc];
+                s1 += red1[q * C + cc];
             }
+            // channel-major (part[k][c][block]): a channel's partials are one contiguous run
+            put(cc, s0, s1);
         }
-        return;
     }
-    for (int cc = tid; cc < C; cc += NT) {
-        float s0 = 0.f, s1 = 0.f;
-        for (int q = 0; q < groups; ++q) {
-            s0 += red0[q * C + cc];
-            s1 += red1[q * C + cc];
-        }
-        // channel-major (part[k][c][block]): k_bn_finalize reads a channel's partials
-        // as one contiguous run
-        part[(int64_t)cc * gridDim.x + blockIdx.x] = s0;
-        part[(int64_t)(C + cc) * gridDim.x + blockIdx.x] = s1;
-    }
+    if (fin.mode >= 0) bn_fold_finalize(part, C, fin);
 }
 
 // active threads of k_col_partial4: the largest multiple of C / gcd(C, 4) within NT
@@ -775,20 +839,43 @@ static void bn_dx_vec(const float* dy, const float* x, int64_t M, int C, const f
 
 static void col_partial_vec(int kind, const float* x, const float* dy, int64_t M, int C, int64_t rpb, int blocks,
                             const float* mean, const float* rstd, const float* gamma, const float* beta, int act,
-                            float* part, hipStream_t st) {
+                            float* part, hipStream_t st, BnFin fin) {
     const int Tp = colp_threads(C);
     if (kind == 0) {
         hipLaunchKernelGGL((k_col_partial4<0, ACT_NONE>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean,
-                           rstd, gamma, beta, part);
+                           rstd, gamma, beta, part, fin);
     } else if (kind == 1) {
         hipLaunchKernelGGL((k_col_partial4<1, ACT_NONE>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean,
-                           rstd, gamma, beta, part);
+                           rstd, gamma, beta, part, fin);
     } else {
 #define VT_F(A)                                                                                                       \
     hipLaunchKernelGGL((k_col_partial4<2, A>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean, rstd, gamma, \
-                       beta, part)
+                       beta, part, fin)
         VT_ACT_SWITCH(act, VT_F)
 #undef VT_F
+    }
+}
+
+static BnFin no_fin() {
+    BnFin f{};
+    f.mode = -1;
+    return f;
+}
+
+// column partials + their finalize: in the partial kernel's last-arriving workgroups when the
+// channels allow one thread per sum (C <= 128; the group sums after the block partials in
+// ws), else the separate k_bn_finalize launch
+static void col_partial_fin(int kind, const float* x, const float* dy, int64_t M, int C, int64_t rpb, int blocks,
+                            const float* mean, const float* rstd, const float* gamma, const float* beta, int act,
+                            float* ws, hipStream_t st, BnFin f) {
+    if (C <= 128 && g_bn_fold) {
+        const int ng = (blocks + BN_GB - 1) / BN_GB;
+        f.gpart = reinterpret_cast<double*>(ws + (((int64_t)2 * C * blocks + 1) & ~(int64_t)1));
+        f.slot0 = arrive_slots((unsigned)ng + 1);
+        col_partial_vec(kind, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f);
+    } else {
+        col_partial_vec(kind, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, no_fin());
+        hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, f);
     }
 }
 
@@ -961,13 +1048,26 @@ int vt_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, int6
     return VT_OK;
 }
 
+// column-partial blocks of an M-row BatchNorm within ws_floats: the block partials [2][C][blocks]
+// + (in-kernel finalize) the group sums [2C][ceil(blocks / BN_GB)] doubles after them
 static int bn_blocks(int64_t M, int64_t ws_floats, int C, int64_t* rpb) {
+    auto need = [&](int64_t b) { return ((2 * C * b + 1) & ~(int64_t)1) + 4 * C * ((b + BN_GB - 1) / BN_GB); };
     int64_t blocks = (M + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    if (blocks * 2 * C > ws_floats) blocks = ws_floats / (2 * C);
-    if (blocks < 1) return 0;
+    // in-kernel finalize (C <= 128): fewer, longer blocks — every block's arrival (an atomic round
+    // trip) lengthens it, and at 2048 blocks those waits stacked up over the block rounds
+    const int64_t cap = C <= 128 && g_bn_fold ? BN_FOLD_BLOCKS : 2048;
+    if (blocks > cap) blocks = cap;
+    while (blocks > 1 && need(blocks) > ws_floats) blocks = blocks * 15 / 16 < blocks - 1 ? blocks * 15 / 16 : blocks - 1;
+    if (need(blocks) > ws_floats) return 0;
     *rpb = ((M + blocks - 1) / blocks + 3) / 4 * 4;  // a multiple of 4 (k_col_partial4's float4 rows)
     return (int)((M + *rpb - 1) / *rpb);
+}
+
+static BnFin fin_of(int mode, int64_t M) {
+    BnFin f{};
+    f.mode = mode;
+    f.M = M;
+    return f;
 }
 
 // Train-mode BatchNorm1d over x (M = B*L rows, C channels) + activation.
@@ -981,12 +1081,17 @@ int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const
     const int blocks = bn_blocks(M, ws_floats, C, &rpb);
     VT_CHECK_ARG(blocks >= 1, "vt_batchnorm_fwd: workspace too small");
     hipStream_t st = S(stream);
-    col_partial_vec(0, x, nullptr, M, C, rpb, blocks, nullptr, nullptr, nullptr, nullptr, 0, ws, st);
-    hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 0, eps, momentum, mean,
-                       rstd, nullptr, nullptr, nullptr, nullptr, 0);
-    col_partial_vec(1, x, nullptr, M, C, rpb, blocks, mean, nullptr, nullptr, nullptr, 0, ws, st);
-    hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 1, eps, momentum, mean,
-                       rstd, run_mean, run_var, nullptr, nullptr, 0);
+    BnFin f0 = fin_of(0, M);
+    f0.mean = mean;
+    col_partial_fin(0, x, nullptr, M, C, rpb, blocks, nullptr, nullptr, nullptr, nullptr, 0, ws, st, f0);
+    BnFin f1 = fin_of(1, M);
+    f1.eps = eps;
+    f1.momentum = momentum;
+    f1.mean = mean;
+    f1.rstd = rstd;
+    f1.run_mean = run_mean;
+    f1.run_var = run_var;
+    col_partial_fin(1, x, nullptr, M, C, rpb, blocks, mean, nullptr, nullptr, nullptr, 0, ws, st, f1);
     bn_apply_vec(x, M, C, mean, rstd, gamma, beta, act, y, st);
     VT_LAUNCH_CHECK("vt_batchnorm_fwd");
     return VT_OK;
@@ -1003,9 +1108,10 @@ int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const fl
     // fresh sums for the dx formula live at the end of ws; params may accumulate
     float* dg_now = ws + (ws_floats - 2 * C);
     float* db_now = dg_now + C;
-    col_partial_vec(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st);
-    hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 2, 0.f, 0.f, nullptr,
-                       nullptr, nullptr, nullptr, dg_now, db_now, 0);
+    BnFin f = fin_of(2, M);
+    f.dgamma = dg_now;
+    f.dbeta = db_now;
+    col_partial_fin(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f);
     bn_dx_vec(dy, x, M, C, mean, rstd, gamma, beta, act, dg_now, db_now, dx, st);
     hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
                        accumulate_params);
@@ -1027,10 +1133,18 @@ int vt_batchnorm_bwd_coef(const float* dy, const float* x, int64_t M, int C, con
     hipStream_t st = S(stream);
     float* dg_now = bnp + 4 * C;
     float* db_now = bnp + 5 * C;
-    col_partial_vec(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st);
-    hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, 2, 0.f, 0.f,
-                       const_cast<float*>(mean), const_cast<float*>(rstd), nullptr, nullptr, dg_now, db_now, 0, bnp,
-                       gamma, beta, dgamma, dbeta, accumulate_params);
+    BnFin f = fin_of(2, M);
+    f.mean = const_cast<float*>(mean);
+    f.rstd = const_cast<float*>(rstd);
+    f.dgamma = dg_now;
+    f.dbeta = db_now;
+    f.bnp = bnp;
+    f.gamma = gamma;
+    f.beta = beta;
+    f.pg = dgamma;
+    f.pb = dbeta;
+    f.pacc = accumulate_params;
+    col_partial_fin(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f);
     VT_LAUNCH_CHECK("vt_batchnorm_bwd_coef");
     return VT_OK;
 }
@@ -1054,7 +1168,7 @@ int vt_syncbn_sums(const float* x, const float* dy, int64_t M, int C, int which,
     const int blocks = bn_blocks(M, ws_floats, C, &rpb);
     VT_CHECK_ARG(blocks >= 1, "vt_syncbn_sums: workspace too small");
     hipStream_t st = S(stream);
-    col_partial_vec(which, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st);
+    col_partial_vec(which, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, no_fin());
     hipLaunchKernelGGL(k_sbn_sums, dim3(C), dim3(NT), 0, st, ws, blocks, C, M, sums);
     VT_LAUNCH_CHECK("vt_syncbn_sums");
     return VT_OK;
