@@ -391,6 +391,20 @@ int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* 
                           int up, const float* gamma, const float* beta, int act, float eps, float momentum,
                           float* conv_out, float* Y, float* mean, float* rstd, float* run_mean, float* run_var,
                           float* ws, int64_t ws_floats, void* stream);
+/* The same block when its input is the PREVIOUS block's pre-BN conv output X: that block's
+ * BatchNorm + ReLU (in_act must be 1: the stacks' inner blocks), max(0, X scale + shift) with
+ * scale = in_rstd in_gamma, shift = in_beta - in_mean scale, applied to each source sample as
+ * the window is staged, before padding / the x2
+ * interpolation — the values vt_batchnorm_apply would have written, so a conv stack's inner
+ * block outputs are never materialised (round 5).  Y nullable: no BatchNorm apply of this
+ * block's own output either (the next block of the stack stages it from conv_out).
+ * replaces: ConvBlock -> ConvBlock in a Sequential (ref/model/vae_teb_model.py:175-212,
+ *           :230-253, the BatchNorm1d + activation output feeding the next Conv1d)         */
+int vt_conv1d_bn_fwd_bf16_in(const float* X, const float* in_mean, const float* in_rstd, const float* in_gamma,
+                             const float* in_beta, int in_act, int B, int L_in, int Cin, const void* w16, int Cout,
+                             int K, int mode, int up, const float* gamma, const float* beta, int act, float eps,
+                             float momentum, float* conv_out, float* Y, float* mean, float* rstd, float* run_mean,
+                             float* run_var, float* ws, int64_t ws_floats, void* stream);
 int vt_conv1d_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode, int up,
                        float* Y, void* stream);
 int vt_conv1d_bwd_gpad_bf16(const float* dY, int B, int L_in, int Cin, const void* w16t, int Cout, int K, int mode,
@@ -426,6 +440,13 @@ int vt_conv1d_bwd_weight_bf16_dy16(const void* dY16, const float* X, int B, int 
 int vt_conv1d_bwd_weight_bf16_dy16s(const void* dY16, int dys, const float* X, int B, int L_in, int Cin, int Cout,
                                     int K, int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
                                     void* stream);
+/* The weight gradient of a block fed by the previous block's pre-BN output X (as
+ * vt_conv1d_bn_fwd_bf16_in: its BatchNorm + activation applied while the window is staged)
+ * from dY16 (bf16 rows dys apart, as vt_conv1d_bwd_weight_bf16_dy16s); dY unused (NULL).   */
+int vt_conv1d_bwd_weight_bf16_in(const float* dY, const void* dY16, int dys, const float* X, const float* in_mean,
+                                 const float* in_rstd, const float* in_gamma, const float* in_beta, int in_act, int B,
+                                 int L_in, int Cin, int Cout, int K, int mode, int up, float* dW, int accumulate,
+                                 float* ws, int64_t ws_floats, void* stream);
 /* Conv-block backward in two launches on a bf16 operand (conv_bwd16.hip):
  * vt_batchnorm_bwd_x16: the BatchNorm input gradient of vt_conv1d_bwd_gpad_bf16_bn (the
  *   same bits) written once, in bf16, rows of ceil32(C) channels (padding 0), from dY, the

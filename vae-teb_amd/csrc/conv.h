@@ -19,8 +19,12 @@ __device__ __forceinline__ float up_lerp(float a, float b, float l1) {
     return (1.f - l1) * a + l1 * b;
 }
 
-// input value at padded position tp (upsampled domain) — see gemm.hip conv_src
-__device__ __forceinline__ float src_val(const float* __restrict__ xb, const Geo& g, int tp, int ci) {
+// input value at padded position tp (upsampled domain) — see gemm.hip conv_src.  IBN: x holds
+// the previous block's pre-BN conv output, its BatchNorm + activation (LDS parameters ip, channel
+// stride cs) applied to each source sample before the interpolation (zero padding stays 0)
+template <bool IBN = false>
+__device__ __forceinline__ float src_val(const float* __restrict__ xb, const Geo& g, int tp, int ci,
+                                         const float* ip = nullptr, int cs = 0, int iact = 0) {
     int t = tp - g.pad;
     if (g.mode == 0) {
         if (t < 0 || t >= g.L_up) return 0.f;
@@ -30,13 +34,21 @@ __device__ __forceinline__ float src_val(const float* __restrict__ xb, const Geo
         t = t < 0 ? -t : t;
         t = t >= g.L_up ? 2 * (g.L_up - 1) - t : t;
     }
-    if (!g.up) return xb[(int64_t)t * g.Cin + ci];
+    if (!g.up) {
+        const float v = xb[(int64_t)t * g.Cin + ci];
+        return IBN ? bn_relu_at(ip, cs, ci, v) : v;
+    }
     float s = (t + 0.5f) * 0.5f - 0.5f;
     s = s < 0.f ? 0.f : s;
     const int i0 = (int)s;
     const int i1 = i0 + 1 < g.L_in ? i0 + 1 : g.L_in - 1;
     const float l1 = s - (float)i0;
-    return up_lerp(xb[(int64_t)i0 * g.Cin + ci], xb[(int64_t)i1 * g.Cin + ci], l1);
+    float a = xb[(int64_t)i0 * g.Cin + ci], b = xb[(int64_t)i1 * g.Cin + ci];
+    if constexpr (IBN) {
+        a = bn_relu_at(ip, cs, ci, a);
+        b = bn_relu_at(ip, cs, ci, b);
+    }
+    return up_lerp(a, b, l1);
 }
 
 
@@ -119,9 +131,9 @@ __device__ __forceinline__ void src_span(const Geo& g, int t0, int n, int& lo, i
 // is computed once, addresses are clamped into the sample and the values masked
 // afterwards, so a staging loop keeps all its loads in flight instead of waiting
 // on each element.
-template <int NC>
+template <int NC, bool IBN = false>
 __device__ __forceinline__ void src_vec(const float* __restrict__ xb, const Geo& g, int tp, int cb, bool ok,
-                                        float (&v)[NC]) {
+                                        float (&v)[NC], const float* ip = nullptr, int cs = 0, int iact = 0) {
     int i0 = 0, i1 = 0;
     float l1 = 0.f;
     const bool in = ok && src_row(g, tp, i0, i1, l1);
@@ -133,6 +145,15 @@ __device__ __forceinline__ void src_vec(const float* __restrict__ xb, const Geo&
         const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
         a[j] = p0[c];
         b[j] = g.up ? p1[c] : 0.f;
+    }
+    if constexpr (IBN) {   // channels past Cin: padding parameters, masked below
+        float sc[NC], sh[NC];
+        bn_in_n<NC>(ip, cs, cb, sc, sh);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            a[j] = bn_relu_val(a[j], sc[j], sh[j]);
+            b[j] = g.up ? bn_relu_val(b[j], sc[j], sh[j]) : 0.f;
+        }
     }
 #pragma unroll
     for (int j = 0; j < NC; ++j)
@@ -155,8 +176,10 @@ int bn_stats_finalize_launch(const float* stats, int tiles_per_sample, int B, in
                              float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
                              hipStream_t st);
 int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st);
-// conv_fwd16.hip: the flat-staged bf16 forward (returns its position tile, or VT_ERR_ARG)
-int cfw16_launch(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st);
+// conv_fwd16.hip: the flat-staged bf16 forward (returns its position tile, or VT_ERR_ARG);
+// ibn (nullable): x is the previous block's pre-BN output, its BatchNorm + act applied in staging
+int cfw16_launch(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,
+                 const BnIn* ibn = nullptr);
 // conv_bf16.hip: the reflect mirror rows of a direct-dX backward-data conv added back (k_conv_fold_edges)
 void fold_edges_launch(float* dx, const float* edge, int B, int L, int pad, int C, hipStream_t st);
 int bn_apply_launch(const float* x, int64_t M, int C, const float* mean, const float* rstd, const float* gamma,

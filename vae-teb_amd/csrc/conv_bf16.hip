@@ -23,6 +23,11 @@
 
 namespace vt {
 
+// kernel selection (vt_conv_bf16_set_kernels): bit 0 the flat-staged forward (conv_fwd16.hip),
+// bit 1 the flat-staged weight gradient (k_cdw16, conv_dw16.hip), bit 2 both at every K, bit 3
+// 256-row chunks in the flat weight gradient for dY <= 32 channels
+int g_conv_kern = 11;
+
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -61,11 +66,12 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
 // the BatchNorm-backward parameters of its one channel sit in registers.  U rows per
 // round, all their loads issued before the first use.  Same values and the same bf16
 // roundings as the octet staging below (bit-identical results).
-template <int K, int WIN, bool BNB>
+template <int K, int WIN, bool BNB, bool IBN = false>
 __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const float* __restrict__ xb,
                                                 const float* __restrict__ x2b, const Geo& g, int t0, int TP, int Lo,
                                                 int c0, const float* __restrict__ bp, int act, float invM,
-                                                __bf16* __restrict__ dbf, int b, bool write_dbf) {
+                                                __bf16* __restrict__ dbf, int b, bool write_dbf,
+                                                const float* ip = nullptr, int ics = 0, int iact = 0) {
     constexpr int NR = (WIN + 7) / 8, U = K <= 3 ? 3 : 6;
     const int tid = threadIdx.x, cl = tid & 31, rg = tid >> 5;
     const int c = c0 + cl;
@@ -114,8 +120,14 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
             if (i0 + u >= NR || r >= WIN) continue;
             float v = 0.f;
             if (ok[u]) {
-                if constexpr (BNB) v = bn_bwd_val_r(a[u], q[u], pm, prs, pga, pbe, pdg, pdb, act, invM);
-                else v = g.up ? up_lerp(a[u], q[u], l1[u]) : a[u];
+                if constexpr (BNB) {
+                    v = bn_bwd_val_r(a[u], q[u], pm, prs, pga, pbe, pdg, pdb, act, invM);
+                } else if constexpr (IBN) {
+                    const float av = bn_relu_at(ip, ics, cc, a[u]);
+                    v = g.up ? up_lerp(av, bn_relu_at(ip, ics, cc, q[u]), l1[u]) : av;
+                } else {
+                    v = g.up ? up_lerp(a[u], q[u], l1[u]) : a[u];
+                }
             }
             xs[r * RS + cl] = (__bf16)v;
             if constexpr (BNB) {
@@ -134,8 +146,6 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
 // but the forward and every K = 3 instance slower (K 3 BNB 32 -> 260 us: 11-33 channel rows
 // leave most of the 32 channel lanes idle)
 int g_conv_cl = 1;
-// kernel selection (vt_conv_bf16_set_kernels): bit 0 the flat-staged forward (conv_fwd16.hip)
-int g_conv_kern = 11;   // bit 3: 256-row chunks in the flat weight gradient for dY <= 32 channels   // bit 1: the flat-staged weight gradient (k_cdw16); bit 2: both at every K
 
 // x: fp32 (B, L_in, g.Cin) activations; w16: [g.Cout][K][cin32] bf16 shadow.
 // BNB (backward-data only: causal geometry, no upsample): x is the block output
@@ -144,12 +154,15 @@ int g_conv_kern = 11;   // bit 3: 256-row chunks in the flat weight gradient for
 // dbf (BNB, nullable): the staged BN input gradient, bf16, is also written to
 // dbf[(b L_in + t) cpad + c] (cpad = ceil8(Cin)) by the blockIdx.y == 0 workgroups
 // for their own rows t0 .. t0 + TP - 1 (each row once) — the weight gradient's operand.
-template <int K, int NT, bool BNB = false, bool CL = true>
+// IBN (not with BNB): x is the previous block's pre-BN conv output, its BatchNorm + activation
+// (bi, staged into LDS at byte ipo) applied to the source samples while the window is staged.
+template <int K, int NT, bool BNB = false, bool CL = true, bool IBN = false>
 __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, Geo g, const __bf16* __restrict__ w16,
                                                    int cin32, float* __restrict__ y, int Lo,
                                                    float* __restrict__ stats, const float* __restrict__ x2,
                                                    const float* __restrict__ bnp, int act, float invM,
-                                                   __bf16* __restrict__ dbf, FoldOut fo) {
+                                                   __bf16* __restrict__ dbf, FoldOut fo, BnIn bi, int ipo) {
+    static_assert(!(BNB && IBN), "k_conv_bf16: BNB and IBN exclusive");
     using C = BCfg<K, NT>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
     extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
@@ -161,6 +174,11 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
     float* bp = reinterpret_cast<float*>(reinterpret_cast<char*>(lb) + C::LDS_BYTES);  // BNB: 6 x Cin params
     if constexpr (BNB) {
         for (int i = tid; i < 6 * g.Cin; i += 256) bp[i] = bnp[i];
+        __syncthreads();
+    }
+    float* ip = reinterpret_cast<float*>(reinterpret_cast<char*>(lb) + ipo);
+    if constexpr (IBN) {
+        stage_bn_in(bi, g.Cin, ip, cin32);
         __syncthreads();
     }
     const float* x2b = BNB ? x2 + (int64_t)b * g.L_in * g.Cin : nullptr;
@@ -183,8 +201,8 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
                 const int coc = co0 + co < g.Cout ? co0 + co : g.Cout - 1;
                 wt[it] = *(const bf16x8*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
             }
-            stage_window_cl<K, WIN, BNB>(xs, xb, x2b, g, t0, TP, Lo, c0, bp, act, invM, dbf, b,
-                                         BNB && dbf && blockIdx.y == 0);
+            stage_window_cl<K, WIN, BNB, IBN>(xs, xb, x2b, g, t0, TP, Lo, c0, bp, act, invM, dbf, b,
+                                              BNB && dbf && blockIdx.y == 0, ip, cin32, bi.act);
 #pragma unroll
             for (int it = 0; it < NWI; ++it) {
                 const int i = tid + 256 * it;
@@ -221,7 +239,8 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
                     }
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = (ok && cb + j < g.Cin) ? src_val(xb, g, tp, cb + j) : 0.f;
+                    for (int j = 0; j < 8; ++j)
+                        v[j] = (ok && cb + j < g.Cin) ? src_val<IBN>(xb, g, tp, cb + j, ip, cin32, bi.act) : 0.f;
                 }
                 *(bf16x8*)(xs + row * RS + 8 * oct) = pack8(v);
             }
@@ -282,7 +301,7 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
                         *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v[it]);
                     }
                 } else {
-                    src_vec<8>(xb, g, tp, cb, ok, v[it]);
+                    src_vec<8, IBN>(xb, g, tp, cb, ok, v[it], ip, cin32, bi.act);
                 }
             }
     #pragma unroll
@@ -447,346 +466,6 @@ __global__ __launch_bounds__(256) void k_conv_shadow_batch(ConvShadowBatch cb) {
     }
 }
 
-// ------------------------------------------------------------ weight grad
-// dW[co][ci][k] = sum_rows dY[row][co] xpad[row + k][ci] on bf16 MFMA: rows
-// are the MFMA reduction (32 per k-step).  dY rows and the input window are
-// staged row-major in bf16 (fp32 -> bf16 while staging; padding / upsample as
-// in the forward) and both operands are read with the gfx950 transposed read
-// ds_read_b64_tr_b16 (4 rows x 16 channels per 16-lane group, delivered
-// column-major), so the tap shift k is a plain row offset of the window.
-// Each wave owns PPW (16 co x 16 ci) tile pairs with K accumulators; NWV waves
-// per workgroup (4 or 8: 8 halves the workgroups that stage the same rows when 4
-// waves do not cover every pair); rows are split over workgroups
-// (blockIdx.y), per-split partial slabs are summed in fixed order by conv.hip's
-// k_sum_splits.
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-constexpr int DWR = 64;  // rows per staged chunk (2 MFMA k-steps)
-constexpr int KMAXB_DW = 11;
-
-__device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int row0, int col0, int stride) {
-    // lane 4q+p of each 16-lane group addresses row (row0 + q), columns col0 + 4p .. +3; two reads
-    // (rows +0..3 and +4..7 of the lane group's 8-row block)
-    const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const __bf16* a0 = img + (row0 + 8 * g + q) * stride + col0 + 4 * p;
-    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
-    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) v4i16*)(a0 + 4 * stride));
-    // whole-vector concatenation + bit_cast: element-wise bit_casts of the v4i16 results are
-    // miscompiled (each lane's element 0 replicated by v_perm_b32)
-    typedef short v8i16 __attribute__((ext_vector_type(8)));
-    const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, r);
-}
-
-// DYB: dY given in bf16 (dyb16, row stride dys = ceil8(Cout)), e.g. the BN input
-// gradient written by the fused backward-data kernel (k_conv_bf16 BNB + dbf).
-template <int K, int PPW, bool DYB = false, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restrict__ dy, const float* __restrict__ x, Geo g,
-                                                      int64_t rows_per_split, int NTc, int npairs, int dstride,
-                                                      int xstride, float* __restrict__ part,
-                                                      const __bf16* __restrict__ dyb16, int dys) {
-    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
-    __bf16* ds = lb;                          // [DWR][dstride]   dY rows
-    __bf16* xs = lb + DWR * dstride;          // [DWR + K - 1 (+pad)][xstride] input window
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
-    int mt[PPW], nt[PPW];
-    bool act[PPW];
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-        const int p = blockIdx.x * (NWV * PPW) + wv + NWV * j;
-        act[j] = p < npairs;
-        mt[j] = act[j] ? p / NTc : 0;
-        nt[j] = act[j] ? p - mt[j] * NTc : 0;
-    }
-    const int64_t rows = (int64_t)g.B * g.L_out;
-    const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
-    const int64_t r1 = r0 + rows_per_split < rows ? r0 + rows_per_split : rows;
-    f32x4 acc[PPW][K];
-#pragma unroll
-    for (int j = 0; j < PPW; ++j)
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc[j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int cout16 = (g.Cout + 15) / 16 * 16, cin16 = (g.Cin + 15) / 16 * 16;
-    for (int64_t r = r0; r < r1;) {
-        const int b = (int)(r / g.L_out);
-        const int t0 = (int)(r - (int64_t)b * g.L_out);
-        int n = g.L_out - t0;
-        if (n > DWR) n = DWR;
-        if (r + n > r1) n = (int)(r1 - r);
-        const float* xb = x + (int64_t)b * g.L_in * g.Cin;
-        const float* dyb = DYB ? nullptr : dy + ((int64_t)b * g.L_out + t0) * g.Cout;
-        // dY rows (zero rows past n, zero channels past Cout), 4 channels per thread-item,
-        // and the input window rows t0 .. t0 + DWR + K - 2 (padding / upsample applied,
-        // zero past n + K - 1): items in rounds of 4 per thread, every load of a round
-        // issued before its stores (clamped addresses, masked values)
-        constexpr int UR = K <= 3 ? 1 : 4;   // small K: registers (occupancy) first
-        const int nd = DWR * (cout16 / 4), nx = (DWR + K - 1) * (cin16 / 4);
-        if constexpr (DYB) {
-            const __bf16* db16 = dyb16 + ((int64_t)b * g.L_out + t0) * dys;
-            typedef short v4s __attribute__((ext_vector_type(4)));
-            for (int i0 = tid; i0 < nd; i0 += 64 * NWV * UR) {
-                v4s v[UR];
-#pragma unroll
-                for (int u = 0; u < UR; ++u) {
-                    const int i = i0 + 64 * NWV * u;
-                    const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
-                    const bool ok = i < nd && t < n && c < dys;   // pad channels are 0
-                    v[u] = *(const v4s*)(db16 + (int64_t)(ok ? t : 0) * dys + (ok ? c : 0));
-                    if (!ok) v[u] = v4s{0, 0, 0, 0};
-                }
-#pragma unroll
-                for (int u = 0; u < UR; ++u) {
-                    const int i = i0 + 64 * NWV * u;
-                    const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
-                    if (i < nd) *(v4s*)(ds + t * dstride + c) = v[u];
-                }
-            }
-        } else {
-            for (int i0 = tid; i0 < nd; i0 += 64 * NWV * UR) {
-                float v[UR][4];
-#pragma unroll
-                for (int u = 0; u < UR; ++u) {
-                    const int i = i0 + 64 * NWV * u;
-                    const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
-                    const bool ok = i < nd && t < n;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int cc = c + j < g.Cout ? c + j : g.Cout - 1;
-                        v[u][j] = dyb[(int64_t)(ok ? t : 0) * g.Cout + cc];
-                        v[u][j] = (ok && c + j < g.Cout) ? v[u][j] : 0.f;
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < UR; ++u) {
-                    const int i = i0 + 64 * NWV * u;
-                    const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
-                    if (i < nd)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) ds[t * dstride + c + j] = (__bf16)v[u][j];
-                }
-            }
-        }
-        for (int i0 = tid; i0 < nx; i0 += 64 * NWV * UR) {
-            float v[UR][4];
-#pragma unroll
-            for (int u = 0; u < UR; ++u) {
-                const int i = i0 + 64 * NWV * u;
-                const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
-                src_vec<4>(xb, g, t0 + t, c, i < nx && t < n + K - 1, v[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < UR; ++u) {
-                const int i = i0 + 64 * NWV * u;
-                const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
-                if (i < nx)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) xs[t * xstride + c + j] = (__bf16)v[u][j];
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int s = 0; s < DWR / 32; ++s) {
-            if (!act[0]) break;  // wave-uniform: a wave without pairs only stages
-#pragma unroll
-            for (int j = 0; j < PPW; ++j) {
-                // no early-out on inactive pairs: the transposed read needs all 64 lanes (EXEC all ones)
-                const bf16x8 a = tr_frag(ds, 32 * s, 16 * mt[j], dstride);
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const bf16x8 bb = tr_frag(xs, 32 * s + k, 16 * nt[j], xstride);
-                    acc[j][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[j][k], 0, 0, 0);
-                }
-            }
-        }
-        __syncthreads();
-        r += n;
-    }
-    // D: col (ci) = lane & 15, row (co) = 4 * (lane >> 4) + rr
-    const int64_t slot = blockIdx.y;
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-        if (!act[j]) continue;
-        const int ci = 16 * nt[j] + lr;
-        if (ci >= g.Cin) continue;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int co = 16 * mt[j] + 4 * lc + rr;
-            if (co >= g.Cout) continue;
-            float* pp = part + ((slot * g.Cout + co) * g.Cin + ci) * K;
-#pragma unroll
-            for (int k = 0; k < K; ++k) pp[k] = acc[j][k][rr];
-        }
-    }
-}
-
-// The weight gradient with flat staging and a register-prefetched next chunk (round 3;
-// vt_conv_bf16_set_kernels bit 1): the MFMA body, pair assignment, splits and 64-row
-// chunks of k_conv_dw_bf16<.., DYB = true> (bit-identical partial slabs), the operands
-// staged as in conv_fwd16.hip — dY from its bf16 rows by 16-byte loads, the input window's
-// source rows copied with float4 loads into LDS (F) and formed into the bf16 image there
-// (padding / x2 interpolation by up_lerp, the values of src_vec).  The next chunk's dY
-// segments and F rows are loaded into registers before the current chunk's MFMAs.
-constexpr int CDW_UD = 4;    // dY 16-byte segments per thread and chunk (256 threads)
-constexpr int CDW_UF = 8;    // F float4 per thread and chunk (256 threads)
-constexpr int CDW_UF_WIDE = 12;   // ... for the 256-row chunks
-
-// CR: rows per chunk — 64 (DWR), or 256 for the narrow layers (dY <= 32 channels: four times
-// the MFMA work per staged chunk, the same k-step order, so the same bits)
-template <int K, int PPW, int NWV, int CR = DWR>
-__global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ dyb16, int dys,
-                                                   const float* __restrict__ x, Geo g, int64_t rows_per_split,
-                                                   int NTc, int npairs, int dstride, int xstride,
-                                                   float* __restrict__ part, int64_t total) {
-    constexpr int NT = 64 * NWV;
-    constexpr int UD = CR == DWR ? CDW_UD * 256 / NT : CR * 4 / NT;   // CR 256: dY rows of <= 4 segments
-    constexpr int UF = CR == DWR ? CDW_UF * 256 / NT : CDW_UF_WIDE * 256 / NT;
-    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
-    __bf16* ds = lb;                          // [CR][dstride]   dY rows
-    __bf16* xs = lb + CR * dstride;           // [CR + K - 1 (+pad)][xstride] input window
-    float* F = reinterpret_cast<float*>(lb + CR * dstride + (CR + KMAXB_DW + 8) * xstride);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    int mt[PPW], nt[PPW];
-    bool act[PPW];
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-        const int p = blockIdx.x * (NWV * PPW) + wv + NWV * j;
-        act[j] = p < npairs;
-        mt[j] = act[j] ? p / NTc : 0;
-        nt[j] = act[j] ? p - mt[j] * NTc : 0;
-    }
-    const int64_t rows = (int64_t)g.B * g.L_out;
-    const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
-    const int64_t r1 = r0 + rows_per_split < rows ? r0 + rows_per_split : rows;
-    f32x4 acc[PPW][K];
-#pragma unroll
-    for (int j = 0; j < PPW; ++j)
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc[j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int cout16 = (g.Cout + 15) / 16 * 16, cin16 = (g.Cin + 15) / 16 * 16;
-    const int dsegs = cout16 / 8;
-    // one chunk's operands into registers: dY segments and the F rows (float4 from the
-    // boundary at or below the source run)
-    bf16x8 dv[UD];
-    float4 fv[UF];
-    struct Chunk {
-        int b, t0, n, lo, hi, off, nv;
-    };
-    auto load = [&](int64_t r, Chunk& c) {
-        c.b = (int)(r / g.L_out);
-        c.t0 = (int)(r - (int64_t)c.b * g.L_out);
-        c.n = g.L_out - c.t0 < CR ? g.L_out - c.t0 : CR;
-        if (r + c.n > r1) c.n = (int)(r1 - r);
-        const __bf16* db = dyb16 + ((int64_t)c.b * g.L_out + c.t0) * dys;
-#pragma unroll
-        for (int u = 0; u < UD; ++u) {
-            const int i = tid + NT * u;
-            const int t = i / dsegs, sg = i - t * dsegs;
-            const bool ok = i < CR * dsegs && t < c.n && 8 * sg < dys;
-            dv[u] = *(const bf16x8*)(db + (int64_t)(ok ? t : 0) * dys + (ok ? 8 * sg : 0));
-            if (!ok) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) dv[u][j] = (__bf16)0.f;
-            }
-        }
-        src_span(g, c.t0, c.n + K - 1, c.lo, c.hi);
-        const int64_t f0 = ((int64_t)c.b * g.L_in + c.lo) * g.Cin;
-        const int64_t fa = f0 & ~(int64_t)3;
-        c.off = (int)(f0 - fa);
-        const int nf = c.hi >= c.lo ? (int)(((int64_t)c.b * g.L_in + c.hi + 1) * g.Cin - fa) : 0;
-        const int nv = (nf + 3) >> 2;
-        c.nv = nv;
-#pragma unroll
-        for (int u = 0; u < UF; ++u) {
-            const int i = tid + NT * u;
-            const int64_t e = fa + 4 * (int64_t)i;
-            if (i < nv && e + 3 < total) {
-                fv[u] = *reinterpret_cast<const float4*>(x + e);
-            } else {
-                fv[u].x = i < nv && e < total ? x[e] : 0.f;
-                fv[u].y = i < nv && e + 1 < total ? x[e + 1] : 0.f;
-                fv[u].z = i < nv && e + 2 < total ? x[e + 2] : 0.f;
-                fv[u].w = 0.f;
-            }
-        }
-    };
-    Chunk cur;
-    if (r0 < r1) load(r0, cur);
-    for (int64_t r = r0; r < r1;) {
-        // registers -> LDS: dY rows, F
-#pragma unroll
-        for (int u = 0; u < UD; ++u) {
-            const int i = tid + NT * u;
-            if (i < CR * dsegs) {
-                const int t = i / dsegs, sg = i - t * dsegs;
-                *(bf16x8*)(ds + t * dstride + 8 * sg) = dv[u];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UF; ++u)
-            if (tid + NT * u < cur.nv) reinterpret_cast<float4*>(F)[tid + NT * u] = fv[u];
-        __syncthreads();
-        // F -> the bf16 window image (rows t0 .. t0 + CR + K - 2, zero past n + K - 1), 8 channels
-        // of one row per item
-        {
-            const int osegs = cin16 / 8;
-            for (int i = tid; i < (CR + K - 1) * osegs; i += NT) {
-                const int t = i / osegs, o = i - t * osegs;
-                const int tp = cur.t0 + t, cb = 8 * o;
-                int i0 = 0, i1 = 0;
-                float l1 = 0.f;
-                const bool in = t < cur.n + K - 1 && src_row(g, tp, i0, i1, l1);
-                const float* p0 = F + cur.off + (in ? i0 - cur.lo : 0) * g.Cin;
-                const float* p1 = F + cur.off + (in ? i1 - cur.lo : 0) * g.Cin;
-                bf16x8 v;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
-                    const float a = p0[c];
-                    const float q = g.up ? p1[c] : 0.f;
-                    v[j] = (__bf16)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
-                }
-                *(bf16x8*)(xs + t * xstride + cb) = v;
-            }
-        }
-        __syncthreads();
-        const int64_t rn = r + cur.n;
-        Chunk nxt = cur;
-        if (rn < r1) load(rn, nxt);   // in flight during the MFMAs
-#pragma unroll
-        for (int s = 0; s < CR / 32; ++s) {
-            if (!act[0]) break;  // wave-uniform: a wave without pairs only stages
-#pragma unroll
-            for (int j = 0; j < PPW; ++j) {
-                const bf16x8 a = tr_frag(ds, 32 * s, 16 * mt[j], dstride);
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const bf16x8 bb = tr_frag(xs, 32 * s + k, 16 * nt[j], xstride);
-                    acc[j][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[j][k], 0, 0, 0);
-                }
-            }
-        }
-        __syncthreads();
-        cur = nxt;
-        r = rn;
-    }
-    const int lr = lane & 15, lc = lane >> 4;
-    const int64_t slot = blockIdx.y;
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-        if (!act[j]) continue;
-        const int ci = 16 * nt[j] + lr;
-        if (ci >= g.Cin) continue;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int co = 16 * mt[j] + 4 * lc + rr;
-            if (co >= g.Cout) continue;
-            float* pp = part + ((slot * g.Cout + co) * g.Cin + ci) * K;
-#pragma unroll
-            for (int k = 0; k < K; ++k) pp[k] = acc[j][k][rr];
-        }
-    }
-}
-
 // BatchNorm-backward staging (k_conv_bf16 / k_conv_dw_bf16 BNB): dy, the pre-BN
 // conv output, the packed per-channel parameters (6 x C), activation and 1/M
 struct BnB {
@@ -799,59 +478,68 @@ struct BnB {
 
 template <int K, int NT>
 int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
-          hipStream_t st, const BnB* bn, FoldOut fo) {
+          hipStream_t st, const BnB* bn, FoldOut fo, const BnIn* ibn) {
     using C = BCfg<K, NT>;
     // flat-staged forward where it measured faster than k_conv_bf16 (isolated, decoder
     // geometry: K 5 / 3 layers 60 -> 52, 102 -> 60 us; K >= 7 slower: 30 -> 43 us at K 11)
     if (x && !bn && (g_conv_kern & 1) && (K <= 5 || (g_conv_kern & 4)) && fo.pad < 0 && ((uintptr_t)x & 15) == 0) {
-        const int tp = cfw16_launch(x, g, w16, y, Lo, stats, st);
+        const int tp = cfw16_launch(x, g, w16, y, Lo, stats, st, ibn);
         if (tp > 0) return tp;
     }
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
     const bool cl = g_conv_cl == 2 || (g_conv_cl == 1 && bn && K >= 7);
+    const BnIn bi = ibn ? *ibn : BnIn{};
+    const int ipo = C::LDS_BYTES, ilds = C::LDS_BYTES + 8 * cin32;   // IBN: [2][cin32] affine map
     if (x && bn && cl)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, true, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
-                           cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo);
+                           cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo, bi, 0);
     else if (x && bn)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, true, false>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g,
-                           w16, cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo);
+                           w16, cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo, bi, 0);
+    else if (x && cl && ibn)
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true, true>), grid, dim3(256), ilds, st, x, g, w16, cin32, y,
+                           Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, bi, ipo);
     else if (x && cl)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
-                           Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo);
+                           Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, bi, 0);
+    else if (x && ibn)
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, false, true>), grid, dim3(256), ilds, st, x, g, w16, cin32, y,
+                           Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, bi, ipo);
     else if (x)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, false, false>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
-                           Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo);
+                           Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, bi, 0);
     return C::TP;
 }
 
 template <int K>
 int bf_k(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats, hipStream_t st,
-         const BnB* bn, FoldOut fo) {
+         const BnB* bn, FoldOut fo, const BnIn* ibn) {
     switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
-        case 1: return bf_nt<K, 1>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 2: return bf_nt<K, 2>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 3: return bf_nt<K, 3>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 4: return bf_nt<K, 4>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 5: return bf_nt<K, 5>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        default: return bf_nt<K, 6>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 1: return bf_nt<K, 1>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 2: return bf_nt<K, 2>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 3: return bf_nt<K, 3>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 4: return bf_nt<K, 4>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 5: return bf_nt<K, 5>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        default: return bf_nt<K, 6>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
     }
 }
 
 // x == nullptr: no launch, only the position tile of this geometry
 int bf_launch(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
-              hipStream_t st, const BnB* bn = nullptr, FoldOut fo = FoldOut{-1, 0, nullptr}) {
+              hipStream_t st, const BnB* bn = nullptr, FoldOut fo = FoldOut{-1, 0, nullptr},
+              const BnIn* ibn = nullptr) {
     switch (g.K) {
-        case 1: return bf_k<1>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 2: return bf_k<2>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 3: return bf_k<3>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 4: return bf_k<4>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 5: return bf_k<5>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 6: return bf_k<6>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 7: return bf_k<7>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 8: return bf_k<8>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 9: return bf_k<9>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        case 10: return bf_k<10>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
-        default: return bf_k<11>(x, g, w16, cin32, y, Lo, stats, st, bn, fo);
+        case 1: return bf_k<1>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 2: return bf_k<2>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 3: return bf_k<3>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 4: return bf_k<4>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 5: return bf_k<5>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 6: return bf_k<6>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 7: return bf_k<7>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 8: return bf_k<8>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 9: return bf_k<9>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        case 10: return bf_k<10>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
+        default: return bf_k<11>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
     }
 }
 
@@ -935,23 +623,42 @@ int vt_conv1d_bf16_shadow_batch(int n, const int64_t* W, const int* Cout, const 
     return VT_OK;
 }
 
-int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode,
-                          int up, const float* gamma, const float* beta, int act, float eps, float momentum,
-                          float* conv_out, float* Y, float* mean, float* rstd, float* run_mean, float* run_var,
-                          float* ws, int64_t ws_floats, void* stream) {
+static int bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode, int up,
+                       const float* gamma, const float* beta, int act, float eps, float momentum, float* conv_out,
+                       float* Y, float* mean, float* rstd, float* run_mean, float* run_var, float* ws,
+                       int64_t ws_floats, hipStream_t st, const BnIn* ibn, const char* who) {
     VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB && (mode == 0 || mode == 1),
-                 "vt_conv1d_bn_fwd_bf16: shape (K <= %d)", KMAXB);
+                 "%s: shape (K <= %d)", who, KMAXB);
     Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
     const int cin32 = cdiv(Cin, 32) * 32;
     const int TP = bf_launch(nullptr, g, nullptr, cin32, nullptr, g.L_out, nullptr, nullptr);
     const int tps = cdiv(g.L_out, TP);
-    VT_CHECK_ARG(ws && ws_floats >= (int64_t)B * tps * 2 * Cout, "vt_conv1d_bn_fwd_bf16: workspace too small");
-    hipStream_t st = S(stream);
-    bf_launch(X, g, (const __bf16*)w16, cin32, conv_out, g.L_out, ws, st);
+    VT_CHECK_ARG(ws && ws_floats >= (int64_t)B * tps * 2 * Cout, "%s: workspace too small", who);
+    bf_launch(X, g, (const __bf16*)w16, cin32, conv_out, g.L_out, ws, st, nullptr, FoldOut{-1, 0, nullptr}, ibn);
     bn_stats_finalize_launch(ws, tps, B, TP, g.L_out, Cout, eps, momentum, mean, rstd, run_mean, run_var, st);
-    bn_apply_launch(conv_out, (int64_t)B * g.L_out, Cout, mean, rstd, gamma, beta, act, Y, st);
-    VT_LAUNCH_CHECK("vt_conv1d_bn_fwd_bf16");
+    if (Y) bn_apply_launch(conv_out, (int64_t)B * g.L_out, Cout, mean, rstd, gamma, beta, act, Y, st);
+    VT_LAUNCH_CHECK(who);
     return VT_OK;
+}
+
+int vt_conv1d_bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode,
+                          int up, const float* gamma, const float* beta, int act, float eps, float momentum,
+                          float* conv_out, float* Y, float* mean, float* rstd, float* run_mean, float* run_var,
+                          float* ws, int64_t ws_floats, void* stream) {
+    return bn_fwd_bf16(X, B, L_in, Cin, w16, Cout, K, mode, up, gamma, beta, act, eps, momentum, conv_out, Y, mean,
+                       rstd, run_mean, run_var, ws, ws_floats, S(stream), nullptr, "vt_conv1d_bn_fwd_bf16");
+}
+
+int vt_conv1d_bn_fwd_bf16_in(const float* X, const float* in_mean, const float* in_rstd, const float* in_gamma,
+                             const float* in_beta, int in_act, int B, int L_in, int Cin, const void* w16, int Cout,
+                             int K, int mode, int up, const float* gamma, const float* beta, int act, float eps,
+                             float momentum, float* conv_out, float* Y, float* mean, float* rstd, float* run_mean,
+                             float* run_var, float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(in_mean && in_rstd && in_gamma && in_beta && in_act == 1,
+                 "vt_conv1d_bn_fwd_bf16_in: input BatchNorm parameters (ReLU blocks only)");
+    const BnIn bi{in_mean, in_rstd, in_gamma, in_beta, in_act};
+    return bn_fwd_bf16(X, B, L_in, Cin, w16, Cout, K, mode, up, gamma, beta, act, eps, momentum, conv_out, Y, mean,
+                       rstd, run_mean, run_var, ws, ws_floats, S(stream), &bi, "vt_conv1d_bn_fwd_bf16_in");
 }
 
 int vt_conv1d_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16, int Cout, int K, int mode, int up,
@@ -1006,121 +713,6 @@ int vt_conv1d_bwd_dx_bf16_bn(const float* dY, const float* Xc, const float* bnp,
         VT_LAUNCH_CHECK("vt_conv1d_bwd_dx_bf16_bn");
     }
     return VT_OK;
-}
-
-static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode, int up,
-                      float* dW, int accumulate, float* ws, int64_t ws_floats, hipStream_t st, const __bf16* dy16,
-                      int dys = 0) {
-    VT_CHECK_ARG(B > 0 && L_in > 0 && K > 0 && K <= KMAXB && Cin > 0 && Cout > 0 && Cin <= 128 && Cout <= 128,
-                 "vt_conv1d_bwd_weight_bf16: shape (K <= %d, channels <= 128)", KMAXB);
-    Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
-    const int NTc = cdiv(Cin, 16), npairs = cdiv(Cout, 16) * NTc;
-    // pairs per wave: at most what the accumulators allow, and no more than the
-    // 4 waves of one workgroup need (small layers: no MFMAs on empty pairs)
-    const int ppw_max = K <= 3 ? 6 : (K <= 5 ? 4 : (K <= 7 ? 3 : 2));
-    const int ppw = cdiv(npairs, 4) < ppw_max ? cdiv(npairs, 4) : ppw_max;
-    // waves per workgroup (dy16 path): 8 when 4 do not own every pair, so each row is
-    // staged by half as many workgroups (16 waves would cap the accumulators at 128 VGPRs)
-    const int need = cdiv(npairs, ppw);
-    const int nwv = !dy16 || need <= 4 ? 4 : 8;
-    const int bx = cdiv(npairs, nwv * ppw);
-    const int64_t rows = (int64_t)B * g.L_out;
-    const int64_t nout = (int64_t)Cout * Cin * K;
-    // workgroup budget of the row splits (VAETEB_CONVDW_WG, default 8192; measured 4096 -> 8192:
-    // 8.80-8.85 -> 8.78-8.79 ms, 1024: 9.2 ms — the weight gradients join the step's end)
-    static const int wg_budget = getenv("VAETEB_CONVDW_WG") ? atoi(getenv("VAETEB_CONVDW_WG")) : 8192;
-    int64_t splits = (wg_budget > 0 ? wg_budget : 4096) / (nwv * bx);
-    if (splits > 1024) splits = 1024;   // the two-stage split sum handles <= 32^2
-    if (splits * nout > (int64_t)8 << 20) splits = ((int64_t)8 << 20) / nout;
-    if (splits > rows / (4 * DWR)) splits = rows / (4 * DWR);
-    if (splits < 1) splits = 1;
-    if (splits * nout > ws_floats) splits = ws_floats / nout;
-    VT_CHECK_ARG(splits >= 1, "vt_conv1d_bwd_weight_bf16: workspace too small");
-    int64_t rps = (rows + splits - 1) / splits;
-    splits = (rows + rps - 1) / rps;
-    // row strides (bf16): channels rounded to 16, + 8 (rows start 16 B apart mod 64 banks)
-    const int dstride = 16 * cdiv(Cout, 16) + 8, xstride = 16 * cdiv(Cin, 16) + 8;
-    const size_t lds = (size_t)(DWR * dstride + (DWR + KMAXB + 8) * xstride) * 2;
-    if (dys == 0) dys = (Cout + 7) & ~7;
-    dim3 grid(bx, (unsigned)splits);
-    // flat-staged kernel: F rows of a chunk fit the per-thread prefetch and LDS
-    const int f_rows = (up ? (DWR + K - 1) / 2 + 3 : DWR + K - 1);
-    const int64_t f_floats = (int64_t)f_rows * Cin + 8;
-    // flat-staged weight gradient where it measured faster (K 9 / 7: 176 -> 111, 184 -> 118 us;
-    // K <= 5 slower: 85 -> 108 us)
-    const bool flat_ok = dy16 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)dy16 & 15) == 0 && dys % 8 == 0;
-    const bool flat = flat_ok && (g_conv_kern & 2) && (K >= 7 || (g_conv_kern & 4)) &&
-                      f_floats <= (int64_t)4 * CDW_UF * 256 && 16 * cdiv(Cout, 16) <= 8 * CDW_UD * 32;
-    const size_t lds_flat = lds + (size_t)f_floats * 4 + 64;
-    const int64_t total_x = (int64_t)B * L_in * Cin;
-    // 256-row chunks for the narrow layers (dY <= 32 channels, the window's source rows in
-    // the wide prefetch): four times the MFMA work per staged chunk (measured: see DESIGN §9)
-    const int fw_rows = up ? (256 + K - 1) / 2 + 3 : 256 + K - 1;
-    const int64_t fw_floats = (int64_t)fw_rows * Cin + 8;
-    const bool wide = flat_ok && (g_conv_kern & 8) && cdiv(Cout, 16) <= 2 &&
-                      fw_floats <= (int64_t)4 * CDW_UF_WIDE * 256 && rps >= 256;
-    const size_t lds_wide = (size_t)(256 * dstride + (256 + KMAXB + 8) * xstride) * 2 + (size_t)fw_floats * 4 + 64;
-#define VT_DWB(KK, PP)                                                                                         \
-    if (K == KK && ppw == PP) {                                                                                \
-        if (wide && nwv == 8)                                                                                  \
-            hipLaunchKernelGGL((k_cdw16<KK, PP, 8, 256>), grid, dim3(512), lds_wide, st, dy16, dys, X, g, rps,   \
-                               NTc, npairs, dstride, xstride, ws, total_x);                                   \
-        else if (wide)                                                                                         \
-            hipLaunchKernelGGL((k_cdw16<KK, PP, 4, 256>), grid, dim3(256), lds_wide, st, dy16, dys, X, g, rps,   \
-                               NTc, npairs, dstride, xstride, ws, total_x);                                   \
-        else if (flat && nwv == 8)                                                                             \
-            hipLaunchKernelGGL((k_cdw16<KK, PP, 8>), grid, dim3(512), lds_flat, st, dy16, dys, X, g, rps, NTc,   \
-                               npairs, dstride, xstride, ws, total_x);                                        \
-        else if (flat)                                                                                         \
-            hipLaunchKernelGGL((k_cdw16<KK, PP, 4>), grid, dim3(256), lds_flat, st, dy16, dys, X, g, rps, NTc,   \
-                               npairs, dstride, xstride, ws, total_x);                                        \
-        else if (dy16 && nwv == 8)                                                                             \
-            hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true, 8>), grid, dim3(512), lds, st, dY, X, g, rps, NTc,  \
-                               npairs, dstride, xstride, ws, dy16, dys);                                      \
-        else if (dy16)                                                                                         \
-            hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true>), grid, dim3(256), lds, st, dY, X, g, rps, NTc, npairs, \
-                               dstride, xstride, ws, dy16, dys);                                              \
-        else                                                                                                   \
-            hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP>), grid, dim3(256), lds, st, dY, X, g, rps, NTc, npairs, \
-                               dstride, xstride, ws, nullptr, 0);                                             \
-    }
-#define VT_DWB6(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3) VT_DWB(KK, 4) VT_DWB(KK, 5) VT_DWB(KK, 6)
-#define VT_DWB4(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3) VT_DWB(KK, 4)
-#define VT_DWB3(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3)
-#define VT_DWB2(KK) VT_DWB(KK, 1) VT_DWB(KK, 2)
-    VT_DWB6(1) VT_DWB6(2) VT_DWB6(3) VT_DWB4(4) VT_DWB4(5) VT_DWB3(6) VT_DWB3(7)
-    VT_DWB2(8) VT_DWB2(9) VT_DWB2(10) VT_DWB2(11)
-#undef VT_DWB6
-#undef VT_DWB4
-#undef VT_DWB3
-#undef VT_DWB2
-#undef VT_DWB
-    const int rc = sum_splits_launch(ws, (int)splits, nout, dW, accumulate, st);
-    if (rc) return rc;
-    VT_LAUNCH_CHECK("vt_conv1d_bwd_weight_bf16");
-    return VT_OK;
-}
-
-int vt_conv1d_bwd_weight_bf16(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode,
-                              int up, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream) {
-    return bwd_weight(dY, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream), nullptr);
-}
-
-int vt_conv1d_bwd_weight_bf16_dy16(const void* dY16, const float* X, int B, int L_in, int Cin, int Cout, int K,
-                                   int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
-                                   void* stream) {
-    VT_CHECK_ARG(dY16 != nullptr, "vt_conv1d_bwd_weight_bf16_dy16: null dY16");
-    return bwd_weight(nullptr, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream),
-                      (const __bf16*)dY16);
-}
-
-int vt_conv1d_bwd_weight_bf16_dy16s(const void* dY16, int dys, const float* X, int B, int L_in, int Cin, int Cout,
-                                    int K, int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
-                                    void* stream) {
-    VT_CHECK_ARG(dY16 != nullptr && dys >= ((Cout + 7) & ~7) && dys % 8 == 0,
-                 "vt_conv1d_bwd_weight_bf16_dy16s: null dY16 or row stride %d (a multiple of 8 >= ceil8(Cout))", dys);
-    return bwd_weight(nullptr, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream),
-                      (const __bf16*)dY16, dys);
 }
 
 }  // extern "C"

@@ -34,10 +34,12 @@ struct FCfg {
     static constexpr int WBYTES = K * TC * RS * 2;
 };
 
-template <int K, int NT>
+// IBN: x is the previous block's pre-BN conv output; its BatchNorm + activation (bi, staged
+// into LDS at byte ipo) are applied to the source samples as the window is formed
+template <int K, int NT, bool IBN = false>
 __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo g, int nch,
                                                const __bf16* __restrict__ w16, float* __restrict__ y, int Lo,
-                                               float* __restrict__ stats, int64_t total) {
+                                               float* __restrict__ stats, int64_t total, BnIn bi, int ipo) {
     using C = FCfg<K, NT>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
     extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
@@ -60,6 +62,8 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
         }
     };
     load_taps(0);   // in flight during the window staging
+    float* ip = reinterpret_cast<float*>(reinterpret_cast<char*>(lb) + ipo);
+    if constexpr (IBN) stage_bn_in(bi, g.Cin, ip, cin32);   // visible after stage 1's barrier
     int lo, hi;
     src_span(g, t0, WIN < Lo + K - 1 - t0 ? WIN : Lo + K - 1 - t0, lo, hi);
     // 1. source rows lo .. hi: flat float4 copy (from the float4 boundary at or below the run)
@@ -106,11 +110,17 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
             const float* p0 = F + off + (in ? i0 - lo : 0) * g.Cin;
             const float* p1 = F + off + (in ? i1 - lo : 0) * g.Cin;
             bf16x8 v;
+            float sc[8], sh[8];
+            if constexpr (IBN) bn_in_n<8>(ip, cin32, cb, sc, sh);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
-                const float a = p0[c];
-                const float q = g.up ? p1[c] : 0.f;
+                float a = p0[c];
+                float q = g.up ? p1[c] : 0.f;
+                if constexpr (IBN) {
+                    a = bn_relu_val(a, sc[j], sh[j]);
+                    q = g.up ? bn_relu_val(q, sc[j], sh[j]) : 0.f;
+                }
                 // conv.h src_vec's values
                 v[j] = (__bf16)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
             }
@@ -229,7 +239,8 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
 
 // source rows a window of WIN padded positions can read: WIN + 2 (x2 upsample: half, + 2)
 template <int K, int NT>
-int cfw_nt(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st) {
+int cfw_nt(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,
+           const BnIn* ibn) {
     using C = FCfg<K, NT>;
     const int nch = cdiv(g.Cin, 32);
     const int src_rows = g.up ? C::WIN / 2 + 3 : C::WIN;
@@ -237,22 +248,30 @@ int cfw_nt(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, fl
     const int rest = fbytes > C::WBYTES ? fbytes : C::WBYTES;
     int lds = nch * C::WIN * RS * 2 + rest;
     if (lds < 8 * C::TC * 4) lds = 8 * C::TC * 4;
+    const int ipo = (lds + 15) & ~15;   // the input BatchNorm's affine map (IBN): [2][32 nch] floats
+    if (ibn) lds = ipo + 2 * 32 * nch * 4;
     if (lds > 160 * 1024) return VT_ERR_ARG;
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
     const int64_t total = (int64_t)g.B * g.L_in * g.Cin;
-    hipLaunchKernelGGL((k_cfw16<K, NT>), grid, dim3(256), lds, st, x, g, nch, w16, y, Lo, stats, total);
+    const BnIn bi = ibn ? *ibn : BnIn{};
+    if (ibn)
+        hipLaunchKernelGGL((k_cfw16<K, NT, true>), grid, dim3(256), lds, st, x, g, nch, w16, y, Lo, stats, total, bi,
+                           ipo);
+    else
+        hipLaunchKernelGGL((k_cfw16<K, NT>), grid, dim3(256), lds, st, x, g, nch, w16, y, Lo, stats, total, bi, ipo);
     return C::TP;
 }
 
 template <int K>
-int cfw_k(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st) {
+int cfw_k(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,
+          const BnIn* ibn) {
     switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
-        case 1: return cfw_nt<K, 1>(x, g, w16, y, Lo, stats, st);
-        case 2: return cfw_nt<K, 2>(x, g, w16, y, Lo, stats, st);
-        case 3: return cfw_nt<K, 3>(x, g, w16, y, Lo, stats, st);
-        case 4: return cfw_nt<K, 4>(x, g, w16, y, Lo, stats, st);
-        case 5: return cfw_nt<K, 5>(x, g, w16, y, Lo, stats, st);
-        default: return cfw_nt<K, 6>(x, g, w16, y, Lo, stats, st);
+        case 1: return cfw_nt<K, 1>(x, g, w16, y, Lo, stats, st, ibn);
+        case 2: return cfw_nt<K, 2>(x, g, w16, y, Lo, stats, st, ibn);
+        case 3: return cfw_nt<K, 3>(x, g, w16, y, Lo, stats, st, ibn);
+        case 4: return cfw_nt<K, 4>(x, g, w16, y, Lo, stats, st, ibn);
+        case 5: return cfw_nt<K, 5>(x, g, w16, y, Lo, stats, st, ibn);
+        default: return cfw_nt<K, 6>(x, g, w16, y, Lo, stats, st, ibn);
     }
 }
 
@@ -261,19 +280,20 @@ int cfw_k(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, flo
 // the flat-staged forward for geometry g (conv_bf16.hip dispatches here when enabled):
 // returns the position tile (> 0, the statistics' tile height), or VT_ERR_ARG when the
 // window's source rows do not fit in LDS (the caller uses k_conv_bf16)
-int cfw16_launch(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st) {
+int cfw16_launch(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,
+                 const BnIn* ibn) {
     switch (g.K) {
-        case 1: return cfw_k<1>(x, g, w16, y, Lo, stats, st);
-        case 2: return cfw_k<2>(x, g, w16, y, Lo, stats, st);
-        case 3: return cfw_k<3>(x, g, w16, y, Lo, stats, st);
-        case 4: return cfw_k<4>(x, g, w16, y, Lo, stats, st);
-        case 5: return cfw_k<5>(x, g, w16, y, Lo, stats, st);
-        case 6: return cfw_k<6>(x, g, w16, y, Lo, stats, st);
-        case 7: return cfw_k<7>(x, g, w16, y, Lo, stats, st);
-        case 8: return cfw_k<8>(x, g, w16, y, Lo, stats, st);
-        case 9: return cfw_k<9>(x, g, w16, y, Lo, stats, st);
-        case 10: return cfw_k<10>(x, g, w16, y, Lo, stats, st);
-        default: return cfw_k<11>(x, g, w16, y, Lo, stats, st);
+        case 1: return cfw_k<1>(x, g, w16, y, Lo, stats, st, ibn);
+        case 2: return cfw_k<2>(x, g, w16, y, Lo, stats, st, ibn);
+        case 3: return cfw_k<3>(x, g, w16, y, Lo, stats, st, ibn);
+        case 4: return cfw_k<4>(x, g, w16, y, Lo, stats, st, ibn);
+        case 5: return cfw_k<5>(x, g, w16, y, Lo, stats, st, ibn);
+        case 6: return cfw_k<6>(x, g, w16, y, Lo, stats, st, ibn);
+        case 7: return cfw_k<7>(x, g, w16, y, Lo, stats, st, ibn);
+        case 8: return cfw_k<8>(x, g, w16, y, Lo, stats, st, ibn);
+        case 9: return cfw_k<9>(x, g, w16, y, Lo, stats, st, ibn);
+        case 10: return cfw_k<10>(x, g, w16, y, Lo, stats, st, ibn);
+        default: return cfw_k<11>(x, g, w16, y, Lo, stats, st, ibn);
     }
 }
 

@@ -320,8 +320,17 @@ class ConvBlock(nn.Module):
         self.sync_bn = False      # cross-rank BatchNorm statistics (convert_sync_batchnorm)
         self.sync_group = None    # process group of the synchronised statistics (None: the default group)
 
-    def forward(self, x):
+    def forward(self, x, xin=None, vout=False):
+        """xin / vout: ConvStack's BatchNorm fold (ops.ConvBNActF) — x is the previous block's
+        pre-BN output with its BatchNorm xin, and vout returns (pre-BN output, its BatchNorm)."""
         bn = self.bn_layer
+        if xin is not None or vout:
+            out = ops.conv_bn_act(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                  mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
+                                  momentum=bn.momentum, eps=bn.eps, bf16=self.bf16, xin=xin, vout=vout)
+            if not getattr(bn, "_vt_batched", False):
+                bn.num_batches_tracked.add_(1)
+            return out
         if not self.training:   # model.eval(): running statistics (validation, frozen VAE, predict)
             return ops.conv_bn_eval(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                     mode=0 if self.causal else 1, up=self.up, act="tanh" if self.tanh else "relu",
@@ -337,6 +346,31 @@ class ConvBlock(nn.Module):
         if not getattr(bn, "_vt_batched", False):   # else counted by SeqVaeTeb in one launch
             bn.num_batches_tracked.add_(1)
         return y
+
+
+# the conv-stack BatchNorm fold (ConvStack): 0 runs every block on its own (y materialised)
+CONV_FOLD = int(os.environ.get("VAETEB_CONV_FOLD", "1"))
+
+
+class ConvStack(nn.Sequential):
+    """nn.Sequential of ConvBlocks (same children / state_dict keys).  Training with the bf16
+    conv kernels: each inner block hands the next its pre-BN output and BatchNorm instead of
+    y = act(BN(conv)) — the next block applies them while staging its windows, forward and
+    weight gradient (ops.ConvBNActF) — so the inner outputs never round-trip through HBM and
+    the separate BatchNorm-apply pass of every inner block is gone.  Same values as the
+    unfolded stack (the staged operand is the y the apply pass would have written)."""
+
+    def forward(self, x):
+        blocks = list(self)
+        if not (CONV_FOLD and len(blocks) > 1 and x.is_cuda and
+                all(isinstance(b, ConvBlock) and b.training and b.bf16 and not b.sync_bn for b in blocks) and
+                not any(b.tanh for b in blocks[:-1])):   # the staging applies the inner blocks' ReLU
+            return super().forward(x)
+        xin = None
+        for i, blk in enumerate(blocks):
+            if i == len(blocks) - 1:
+                return blk(x, xin=xin)
+            x, xin = blk(x, xin=xin, vout=True)
 
 
 def convert_sync_batchnorm(module, process_group=None):
@@ -398,7 +432,7 @@ class SourceEncoder(nn.Module):
     def __init__(self, input_channels=130):
         super().__init__()
         self.mlp = ResidualMLP(input_channels, geometric_schedule(130, 32, 5), final_activation=False)
-        self.conv = nn.Sequential(*[ConvBlock(32, 32, k, causal=True) for k in (3, 5, 7)])
+        self.conv = ConvStack(*[ConvBlock(32, 32, k, causal=True) for k in (3, 5, 7)])
         self.fused_norm = LayerNorm(32)
         self.lstm_norm = LayerNorm(64)
         self.lstm = LSTM(32, 64, 4)
@@ -429,8 +463,8 @@ class TargetEncoder(nn.Module):
         self.mlp_scattering = _seq1(ResidualMLP(scattering_channels, geometric_schedule(43, 16, 4),
                                                 final_activation=False, activation="gelu"))
         self.mlp_phase = ResidualMLP(phase_channels, geometric_schedule(44, 16, 4), final_activation=False)
-        self.conv_scattering = nn.Sequential(*[ConvBlock(16, 16, k, causal=True) for k in (3, 5, 7)])
-        self.conv_phase = nn.Sequential(*[ConvBlock(16, 16, k, causal=True) for k in (3, 5, 7)])
+        self.conv_scattering = ConvStack(*[ConvBlock(16, 16, k, causal=True) for k in (3, 5, 7)])
+        self.conv_phase = ConvStack(*[ConvBlock(16, 16, k, causal=True) for k in (3, 5, 7)])
         self.scatter_fused_norm = LayerNorm(16)
         self.phase_fused_norm = LayerNorm(16)
         self.lstm_norm = LayerNorm(64)
@@ -485,7 +519,7 @@ class Decoder(nn.Module):
         R = 16 * sequence_length
         self.linear = nn.Sequential(ResidualMLP(latent_dim, geometric_schedule(latent_dim, 50, 5)),
                                     ResidualMLP(50, geometric_schedule(50, 87, 5)))
-        self.conv = nn.Sequential(*[ConvBlock(a, b, k, causal=False, up=u) for a, b, k, u in self.SPEC])
+        self.conv = ConvStack(*[ConvBlock(a, b, k, causal=False, up=u) for a, b, k, u in self.SPEC])
         self.output_mu = ResidualMLP(R, (R, R), final_activation=False, use_skip_connection=False)
         self.output_logvar = ResidualMLP(R, (R, R), final_activation=False, use_skip_connection=False)
         self.set_head_precision(head_precision)
@@ -755,10 +789,10 @@ class TinyVaeTeb(nn.Module):
 
     def __init__(self):
         super().__init__()
-        self.enc = nn.Sequential(ConvBlock(1, 16, 3, causal=True), ConvBlock(16, 16, 5, causal=True))
+        self.enc = ConvStack(ConvBlock(1, 16, 3, causal=True), ConvBlock(16, 16, 5, causal=True))
         self.mu = ResidualMLP(16, (8,), final_activation=False)
         self.logvar = ResidualMLP(16, (8,), final_activation=False)
-        self.dec = nn.Sequential(ConvBlock(8, 16, 3, causal=False), ConvBlock(16, 2, 3, causal=False, tanh=True))
+        self.dec = ConvStack(ConvBlock(8, 16, 3, causal=False), ConvBlock(16, 2, 3, causal=False, tanh=True))
 
     def forward(self, x, eps):
         """x (B, 1, L) (reference layout) -> losses dict (NLL + KL with a

@@ -580,40 +580,64 @@ def _conv_bn_ws(*shape):
 
 class ConvBNActF(torch.autograd.Function):
     """(B, L, Cin) -> (B, L_out, Cout): conv (implicit GEMM with fused
-    padding/upsampling) -> train-mode BatchNorm (running stats updated) -> act."""
+    padding/upsampling) -> train-mode BatchNorm (running stats updated) -> act.
+
+    Conv-stack fold (bf16 only, round 5; ConvStack): xin = (mean, rstd, gamma, beta, act code)
+    of the PREVIOUS block means x is that block's pre-BN conv output and its BatchNorm +
+    activation are applied while this block stages its windows (forward and weight gradient:
+    vt_conv1d_bn_fwd_bf16_in / vt_conv1d_bwd_weight_bf16_in); vout returns this block's pre-BN
+    output in place of y (with its mean / rstd, non-differentiable) for the next block to stage
+    the same way — the inner blocks' y is never written or read.  The gradient autograd passes
+    back for that output is dL/dy (the next block's backward-data conv output), as for y."""
 
     @staticmethod
-    def forward(ctx, x, w, g, b, run_mean, run_var, mode, up, act, momentum, eps, bf16=False):
+    def forward(ctx, x, w, g, b, run_mean, run_var, mode, up, act, momentum, eps, bf16=False, xin=None, vout=False):
         _check(x, w, g, b)
+        if (xin is not None or vout) and not bf16:
+            raise ValueError("the conv-stack BatchNorm fold needs the bf16 conv kernels")
         B, L, Cin = x.shape
         Cout, _, K = w.shape
         x = x.contiguous()
         Lo = _lib.lib().fns["vt_conv1d_out_len"](L, K, mode, up)
         conv = torch.empty((B, Lo, Cout), device=x.device)
-        y = torch.empty_like(conv)
+        y = None if vout else torch.empty_like(conv)
         mean = torch.empty(Cout, device=x.device)
         rstd = torch.empty(Cout, device=x.device)
         ws = WS.get(_conv_bn_ws(B, L, Cin, Cout, K, mode, up), x.device, 2)
         w16t = None
         if bf16:
             w16, w16t = _conv_shadow(w)
-            call("vt_conv1d_bn_fwd_bf16", ptr(x), B, L, Cin, ptr(w16), Cout, K, mode, up, ptr(g), ptr(b), ACT[act],
-                 eps, momentum, ptr(conv), ptr(y), ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws),
-                 ws.numel(), _st())
+            tail = (B, L, Cin, ptr(w16), Cout, K, mode, up, ptr(g), ptr(b), ACT[act], eps, momentum, ptr(conv),
+                    None if vout else ptr(y), ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws), ws.numel(),
+                    _st())
+            if xin is not None:
+                call("vt_conv1d_bn_fwd_bf16_in", ptr(x), *(ptr(t) for t in xin[:4]), xin[4], *tail)
+            else:
+                call("vt_conv1d_bn_fwd_bf16", ptr(x), *tail)
         else:
             call("vt_conv1d_bn_fwd", ptr(x), B, L, Cin, ptr(w), Cout, K, mode, up, ptr(g), ptr(b), ACT[act], eps,
                  momentum, ptr(conv), ptr(y), ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), ptr(ws), ws.numel(),
                  _st())
-        ctx.save_for_backward(x, conv, mean, rstd, w16t)
+        ctx.save_for_backward(x, conv, mean, rstd, w16t, *(xin[:4] if xin is not None else ()))
         ctx.params = (w, g, b)
         ctx.cfg = (mode, up, act, bf16)
+        ctx.in_act = None if xin is None else xin[4]
+        if vout:
+            ctx.mark_non_differentiable(mean, rstd)
+            ctx.set_materialize_grads(False)   # no zero-filled gradients for mean / rstd
+            return conv, mean, rstd
         return y
 
     @staticmethod
-    def backward(ctx, gy):
-        x, conv, mean, rstd, w16t = ctx.saved_tensors
+    def backward(ctx, gy, *_):
+        x, conv, mean, rstd, w16t, *xin = ctx.saved_tensors
+        if gy is None:   # vout with its output unused (set_materialize_grads(False))
+            gy = torch.zeros_like(conv)
         w, g, b = ctx.params
         mode, up, act, bf16 = ctx.cfg
+        # the input is the previous block's pre-BN output: its BatchNorm + act in the weight
+        # gradient's staging (the backward-data output below is dL/d(that block's y), as always)
+        inb = (*(ptr(t) for t in xin), ctx.in_act) if xin else None
         B, L, Cin = x.shape
         Cout, _, K = w.shape
         Lo = conv.shape[1]
@@ -640,6 +664,10 @@ class ConvBNActF(torch.autograd.Function):
             dw_args = lambda wsx: (ptr(dxbn), c32, ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc,
                                    ptr(wsx), wsx.numel(), _st())
             fn = "vt_conv1d_bwd_weight_bf16_dy16s"
+            if inb:
+                dw_args = lambda wsx: (None, ptr(dxbn), c32, ptr(x), *inb, B, L, Cin, Cout, K, mode, up,
+                                       ptr(pw.out[0]), pw.acc, ptr(wsx), wsx.numel(), _st())
+                fn = "vt_conv1d_bwd_weight_bf16_in"
         elif fused:
             # fused BatchNorm backward: only the column sums here; the bf16 backward-data
             # conv forms the BN input gradient while staging its operand from (gy, conv,
@@ -652,6 +680,10 @@ class ConvBNActF(torch.autograd.Function):
             dw_args = lambda wsx: (ptr(dxbn), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc,
                                    ptr(wsx), wsx.numel(), _st())
             fn = "vt_conv1d_bwd_weight_bf16_dy16"
+            if inb:
+                dw_args = lambda wsx: (None, ptr(dxbn), (Cout + 7) // 8 * 8, ptr(x), *inb, B, L, Cin, Cout, K, mode,
+                                       up, ptr(pw.out[0]), pw.acc, ptr(wsx), wsx.numel(), _st())
+                fn = "vt_conv1d_bwd_weight_bf16_in"
         else:
             gconv = torch.empty_like(conv)
             call("vt_batchnorm_bwd", ptr(gy), ptr(conv), M, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT[act],
@@ -660,6 +692,8 @@ class ConvBNActF(torch.autograd.Function):
             dw_args = lambda wsx: (ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc,
                                    ptr(wsx), wsx.numel(), _st())
             fn = "vt_conv1d_bwd_weight_bf16" if bf16 else "vt_conv1d_direct_bwd_weight"
+            if inb:   # a folded input is the previous block's output: it always needs its gradient
+                raise RuntimeError("conv-stack fold: the block input's gradient is required")
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
@@ -692,14 +726,14 @@ class ConvBNActF(torch.autograd.Function):
                 with torch.cuda.stream(side):
                     ws1 = WS.get(WS_LINEAR, x.device, 1)
                     call(fn, *dw_args(ws1))
-                for t in (*srcs, x):
+                for t in (*srcs, x, *xin):   # xin: the folded input's BatchNorm, read by the staging
                     t.record_stream(side)
             else:
                 ws1 = WS.get(WS_LINEAR, x.device, 1)
                 call(fn, *dw_args(ws1))
         gw, = pw.result()
         gg, gb = pbn.result()
-        return gx, gw, gg, gb, None, None, None, None, None, None, None, None
+        return gx, gw, gg, gb, None, None, None, None, None, None, None, None, None, None
 
 
 class SyncConvBNActF(torch.autograd.Function):
@@ -783,11 +817,13 @@ class SyncConvBNActF(torch.autograd.Function):
         if pw.out[0] is not None:
             ws1 = WS.get(WS_LINEAR, x.device, 1)
             fn = "vt_conv1d_bwd_weight_bf16" if bf16 else "vt_conv1d_direct_bwd_weight"
+            if inb:   # a folded input is the previous block's output: it always needs its gradient
+                raise RuntimeError("conv-stack fold: the block input's gradient is required")
             call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1), ws1.numel(),
                  _st())
         gw, = pw.result()
         gg, gb = pbn.result()
-        return gx, gw, gg, gb, None, None, None, None, None, None, None, None, None
+        return gx, gw, gg, gb, None, None, None, None, None, None, None, None, None, None, None
 
 
 def sync_conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momentum=0.9, eps=1e-5, bf16=False,
@@ -1102,8 +1138,16 @@ def layer_norm_act(x, g, b, act="none", eps=1e-5):
     return LayerNormActF.apply(x, g, b, act, eps)
 
 
-def conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momentum=0.9, eps=1e-5, bf16=False):
-    return ConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps, bool(bf16))
+def conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momentum=0.9, eps=1e-5, bf16=False,
+                xin=None, vout=False):
+    """xin / vout: the conv-stack BatchNorm fold (ConvBNActF); vout returns (pre-BN output, its
+    BatchNorm as the next block's xin)."""
+    out = ConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps, bool(bf16), xin,
+                           bool(vout))
+    if not vout:
+        return out
+    conv, mean, rstd = out
+    return conv, (mean, rstd, g, b, ACT[act])
 
 
 def lstm(x, params, half=False):
