@@ -622,6 +622,30 @@ int vt_zconv_bwd_data(const float* dY, int ldy, int B, int L, int Cin, const flo
                       float* dX, int ldx, int accumulate, void* stream);
 /* dW (+)= sum_{b,t} dY[b,t,o] X[b,t+k-pad_left,i]: per-workgroup slabs summed in
  * fixed order; ws >= vt_zconv_bwd_weight_ws_floats(...) floats.                */
+/* The same convolution (forward / backward-data) on bf16 MFMA: operands rounded to bf16 as
+ * they are staged, fp32 accumulation (the reference's 16-bit autocast; the fp32 entry points
+ * above are the exact parity path).  X / dY 16-byte aligned with a row stride that is a
+ * multiple of 4 floats.                                                                  */
+int vt_zconv16_ws_floats(int Cin, int Cout, int K, int64_t* floats);   /* ws of the two below: the bf16 tap image */
+int vt_zconv16_fwd(const float* X, int ldx, int B, int L, int Cin, const float* W, int Cout, int K, int pad_left,
+                   float* Y, int ldy, int accumulate, float* ws, int64_t ws_floats, void* stream);
+int vt_zconv16_bwd_data(const float* dY, int ldy, int B, int L, int Cin, const float* W, int Cout, int K, int pad_left,
+                        float* dX, int ldx, int accumulate, float* ws, int64_t ws_floats, void* stream);
+/* The tap images of up to 8 weights W[h] [Cout][Cin][K] in one launch (flip = 0: for
+ * vt_zconv16_fwd_t; 1: the flipped, transposed taps of vt_zconv16_bwd_data_t), each into T[h]
+ * (16-B aligned, vt_zconv16_taps_elems(Cin, Cout, K) bf16 elements for the forward image,
+ * (Cout, Cin, K) for the flipped one) — then the convolutions read them without converting. */
+int vt_zconv16_taps_elems(int Cin, int Cout, int K, int64_t* elems);
+int vt_zconv16_taps(int n, const int64_t* W, const int* Cin, const int* Cout, const int* K, int flip,
+                    const int64_t* T, void* stream);
+int vt_zconv16_fwd_t(const float* X, int ldx, int B, int L, int Cin, const void* T, int Cout, int K, int pad_left,
+                     float* Y, int ldy, int accumulate, void* stream);
+int vt_zconv16_bwd_data_t(const float* dY, int ldy, int B, int L, int Cin, const void* T, int Cout, int K,
+                          int pad_left, float* dX, int ldx, int accumulate, void* stream);
+/* ... and the weight gradient on bf16 MFMA (transposed LDS reads of the bf16 dY / window row
+ * images), fp32 accumulation and fixed-order slab sum; ws as vt_zconv_bwd_weight.      */
+int vt_zconv16_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int B, int L, int Cin, int Cout, int K,
+                          int pad_left, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);
 int vt_zconv_bwd_weight_ws_floats(int B, int Cin, int Cout, int K, int64_t* floats);
 int vt_zconv_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int B, int L, int Cin, int Cout, int K,
                         int pad_left, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream);

@@ -168,6 +168,203 @@ int zconv_launch(const float* X, int ldx, int B, int L, int Cin, const float* W,
     }
 }
 
+// ------------------------------------------------------- zero-pad conv, bf16 MFMA
+// The same implicit GEMM on v_mfma_f32_16x16x32_bf16 (round 5; the
+// reference trains the classifier in 16-bit autocast as well, ref/model/graph_model.py:510):
+// operands rounded to bf16 while they are staged, fp32 accumulation.  Per chunk of 32 input
+// channels the zero-padded window is staged as bf16 rows of 32 channels (RS16-element stride:
+// 16 consecutive rows hit distinct 4-bank groups) and the taps as [tap][out][32 in] rows, in
+// groups of KG taps (the 40-tap conv: 4 groups, 39 KB of LDS instead of 115); one MFMA k-step
+// per (tap, position tile, output tile) contracts the chunk's 32 channels (16-channel inputs
+// padded with zeros), lane group lc taking channels 8 lc .. 8 lc + 7 — so a fragment is one
+// 16-byte LDS read of a window row shifted by the tap, or of a tap row.
+constexpr int RS16 = 40;
+
+template <int K, int NT>
+struct Z16Cfg {
+    static constexpr int TC = 16 * NT;
+    static constexpr int WIN = ZTP + K - 1;
+    static constexpr int KG = K <= 15 ? K : 10;
+    static constexpr int XB = WIN * RS16, WB = KG * TC * RS16;   // bf16 elements
+    static constexpr int LDS_BYTES = (XB + WB) * 2;
+};
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// the bf16 tap image of one call: T[k][o][c] = W[o][c][k] (FLIP: W[c][o][K-1-k], the
+// backward-data taps of a weight stored [Cin][Cout][K] in kernel terms), o < TC, c < cin32,
+// zero padded — written once per call instead of every workgroup gathering fp32 taps
+__global__ void k_zconv16_taps(const float* __restrict__ W, int Cin, int Cout, int K, int TC, int cin32, int flip,
+                               __bf16* __restrict__ T) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)K * TC * cin32) return;
+    const int c = (int)(e % cin32), ko = (int)(e / cin32), o = ko % TC, k = ko / TC;
+    float v = 0.f;
+    if (o < Cout && c < Cin)
+        v = flip ? W[((int64_t)c * Cout + o) * K + (K - 1 - k)] : W[((int64_t)o * Cin + c) * K + k];
+    T[e] = (__bf16)v;
+}
+
+// the tap images of up to ZTB_MAX weights in one launch (an inception block's five convolutions)
+constexpr int ZTB_MAX = 8;
+struct ZTapBatch {
+    int n, flip;
+    const float* W[ZTB_MAX];
+    __bf16* T[ZTB_MAX];
+    int Cin[ZTB_MAX], Cout[ZTB_MAX], K[ZTB_MAX], TC[ZTB_MAX], cin32[ZTB_MAX];
+    int prefix[ZTB_MAX + 1];   // workgroups before weight h
+};
+__global__ void k_zconv16_taps_batch(ZTapBatch tb) {
+    int h = 0;
+    while (h + 1 < tb.n && (int)blockIdx.x >= tb.prefix[h + 1]) ++h;
+    const int64_t e = (int64_t)(blockIdx.x - tb.prefix[h]) * blockDim.x + threadIdx.x;
+    const int K = tb.K[h], TC = tb.TC[h], cin32 = tb.cin32[h], Cin = tb.Cin[h], Cout = tb.Cout[h];
+    if (e >= (int64_t)K * TC * cin32) return;
+    const int c = (int)(e % cin32), ko = (int)(e / cin32), o = ko % TC, k = ko / TC;
+    const float* W = tb.W[h];
+    float v = 0.f;
+    if (o < Cout && c < Cin)
+        v = tb.flip ? W[((int64_t)c * Cout + o) * K + (K - 1 - k)] : W[((int64_t)o * Cin + c) * K + k];
+    tb.T[h][e] = (__bf16)v;
+}
+
+template <int K, int NT, bool FLIP>
+__global__ __launch_bounds__(ZT) void k_zconv16_fwd(const float* __restrict__ X, int ldx, int L, int Cin,
+                                                    const __bf16* __restrict__ T, int Cout, int pad,
+                                                    float* __restrict__ Y, int ldy, int accumulate) {
+    using C = Z16Cfg<K, NT>;
+    constexpr int TC = C::TC, WIN = C::WIN, KG = C::KG;
+    const int cin32 = (Cin + 31) & ~31;
+    extern __shared__ __attribute__((aligned(16))) __bf16 lb16[];
+    __bf16* xs = lb16;            // [WIN][RS16]
+    __bf16* ws = lb16 + C::XB;    // [KG][TC][RS16]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
+    const int t0 = blockIdx.x * ZTP, b = blockIdx.y;
+    const float* xb = X + (int64_t)b * L * ldx;
+    f32x4 acc[ZPM][NT];
+#pragma unroll
+    for (int m = 0; m < ZPM; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < Cin; c0 += 32) {
+        const int cn = Cin - c0 < 32 ? Cin - c0 : 32;
+        __syncthreads();   // the previous chunk's MFMAs are done with xs
+        // window: WIN rows x 4 octets of 8 channels (zero outside [0, L) and past cn)
+        for (int i = tid; i < WIN * 4; i += ZT) {
+            const int r = i >> 2, oct = i & 3;
+            const int t = t0 + r - pad;
+            const bool ok = t >= 0 && t < L && 8 * oct < cn;
+            float v[8];
+            if (ok) {
+                const float4 a = *reinterpret_cast<const float4*>(xb + (int64_t)t * ldx + c0 + 8 * oct);
+                const float4 q = *reinterpret_cast<const float4*>(xb + (int64_t)t * ldx + c0 + 8 * oct + 4);
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = 0.f;
+            }
+            bf16x8 h;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[j] = (__bf16)v[j];
+            *reinterpret_cast<bf16x8*>(xs + r * RS16 + 8 * oct) = h;
+        }
+        for (int kg0 = 0; kg0 < K; kg0 += KG) {
+            if (kg0) __syncthreads();   // the previous tap group's MFMAs are done with ws
+            // taps kg0 .. kg0 + KG - 1: rows (tap, out) x 4 octets of 8 input channels, 16-byte
+            // copies from the call's bf16 tap image (k_zconv16_taps: [K][TC][cin32], zero padded)
+            for (int i = tid; i < KG * TC * 4; i += ZT) {
+                const int oct = i & 3, r = i >> 2, kk = r / TC, o = r - kk * TC;
+                const int k = kg0 + kk;
+                bf16x8 h;
+                if (k < K) {
+                    h = *reinterpret_cast<const bf16x8*>(T + ((int64_t)k * TC + o) * cin32 + c0 + 8 * oct);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) h[j] = (__bf16)0.f;
+                }
+                *reinterpret_cast<bf16x8*>(ws + (kk * TC + o) * RS16 + 8 * oct) = h;
+            }
+            __syncthreads();
+            const __bf16* xq = xs + (ZPM * 16 * wv + lr + kg0) * RS16 + 8 * lc;
+            const __bf16* wq = ws + lr * RS16 + 8 * lc;
+            const int kn = K - kg0 < KG ? K - kg0 : KG;
+#pragma unroll 2
+            for (int kk = 0; kk < kn; ++kk) {
+                bf16x8 af[ZPM], bfr[NT];
+#pragma unroll
+                for (int m = 0; m < ZPM; ++m) af[m] = *reinterpret_cast<const bf16x8*>(xq + (16 * m + kk) * RS16);
+#pragma unroll
+                for (int n = 0; n < NT; ++n) bfr[n] = *reinterpret_cast<const bf16x8*>(wq + (kk * TC + 16 * n) * RS16);
+#pragma unroll
+                for (int m = 0; m < ZPM; ++m)
+#pragma unroll
+                    for (int n = 0; n < NT; ++n)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+            }
+        }
+    }
+    // D layout: channel = 16 n + lr, position = 4 lc + r (as k_zconv_fwd)
+#pragma unroll
+    for (int m = 0; m < ZPM; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int t = t0 + ZPM * 16 * wv + 16 * m + 4 * lc + r;
+            if (t >= L) continue;
+            float* yr = Y + ((int64_t)b * L + t) * ldy;
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int o = 16 * n + lr;
+                if (o < Cout) yr[o] = accumulate ? yr[o] + acc[m][n][r] : acc[m][n][r];
+            }
+        }
+}
+
+// bf16 elements of the tap image of a call (the workspace of vt_zconv16_fwd / _bwd_data)
+int64_t zconv16_taps_elems(int Cin, int Cout, int K) {
+    const int TC = Cout <= 32 ? 32 : 128;
+    return (int64_t)K * TC * ((Cin + 31) & ~31);
+}
+
+// W == nullptr: T already holds the call's tap image (vt_zconv16_taps)
+template <int K, bool FLIP>
+int zconv16_launch_k(const float* X, int ldx, int B, int L, int Cin, const float* W, int Cout, int pad, float* Y,
+                     int ldy, int acc, __bf16* T, hipStream_t st) {
+    if ((ldx & 3) || (reinterpret_cast<uintptr_t>(X) & 15)) return VT_ERR_ARG;   // float4 row segments
+    dim3 grid(cdiv(L, ZTP), B);
+    const int cin32 = (Cin + 31) & ~31;
+    auto taps = [&](int TC) {
+        if (!W) return;
+        const int64_t n = (int64_t)K * TC * cin32;
+        // FLIP: the kernel's (Cin, Cout) are the weight's (Cout, Cin)
+        hipLaunchKernelGGL(k_zconv16_taps, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, Cin, Cout, K, TC,
+                           cin32, FLIP ? 1 : 0, T);
+    };
+    if (Cout <= 32) {
+        taps(32);
+        hipLaunchKernelGGL((k_zconv16_fwd<K, 2, FLIP>), grid, dim3(ZT), (Z16Cfg<K, 2>::LDS_BYTES), st, X, ldx, L, Cin,
+                           T, Cout, pad, Y, ldy, acc);
+        return VT_OK;
+    }
+    if constexpr (K == 1) {
+        taps(128);
+        hipLaunchKernelGGL((k_zconv16_fwd<K, 8, FLIP>), grid, dim3(ZT), (Z16Cfg<K, 8>::LDS_BYTES), st, X, ldx, L, Cin,
+                           T, Cout, pad, Y, ldy, acc);
+        return VT_OK;
+    }
+    return VT_ERR_ARG;
+}
+
+template <bool FLIP>
+int zconv16_launch(const float* X, int ldx, int B, int L, int Cin, const float* W, int Cout, int K, int pad, float* Y,
+                   int ldy, int acc, __bf16* T, hipStream_t st) {
+    switch (K) {
+        case 1: return zconv16_launch_k<1, FLIP>(X, ldx, B, L, Cin, W, Cout, pad, Y, ldy, acc, T, st);
+        case 5: return zconv16_launch_k<5, FLIP>(X, ldx, B, L, Cin, W, Cout, pad, Y, ldy, acc, T, st);
+        case 15: return zconv16_launch_k<15, FLIP>(X, ldx, B, L, Cin, W, Cout, pad, Y, ldy, acc, T, st);
+        default: return zconv16_launch_k<40, FLIP>(X, ldx, B, L, Cin, W, Cout, pad, Y, ldy, acc, T, st);
+    }
+}
+
 // Cin / Cout multiples of 16 up to 128; channels > 32 on either side only for 1x1 convs
 bool zconv_shape_ok(int B, int L, int Cin, int Cout, int K, int pad) {
     return B > 0 && L > 0 && Cin > 0 && Cin % 16 == 0 && Cin <= 128 && Cout > 0 && Cout % 16 == 0 &&
@@ -247,6 +444,126 @@ __global__ __launch_bounds__(DT) void k_zconv_dw(const float* __restrict__ dY, i
         }
     }
 }
+
+// ------------------------------------------------------ conv weight grad, bf16 MFMA
+// dW[o][i][k] = sum_rows dY[row][o] X[row + k - pad][i] on v_mfma_f32_16x16x32_bf16 (round 5):
+// the 64-row chunk of dY and its input window are staged as bf16 row images (rows the
+// contraction), both operands read with the gfx950 transposed LDS read (ds_read_b64_tr_b16:
+// 8 rows x 16 channels per lane group), so one MFMA contracts 32 rows of one (16 o x 16 i x
+// tap) tile — the fp32 kernel above needs 8 MFMAs and 16 scalar LDS reads for the same rows.
+// Tiles (o, i, tap) with the tap fastest, 8 waves x <= D16MAXT tiles; per-workgroup slabs
+// summed in fixed order (k_sum_splits).
+typedef short zv4i16 __attribute__((ext_vector_type(4)));
+constexpr int D16T = 512, D16R = 64, D16MAXT = 20;
+constexpr int D16_DS = 136 * D16R;                  // dY image: 64 rows x (<= 128 + 8) channels
+constexpr int D16_XS = (D16R + 40 + 8) * 40;        // window image, K <= 40 at <= 32 channels ...
+constexpr int D16_XS1 = D16R * 136;                 // ... or K 1 at <= 128 channels
+
+__device__ __forceinline__ bf16x8 ztr_frag(const __bf16* img, int row0, int col0, int stride) {
+    // lane 4q + p of each 16-lane group: row row0 + 8 g + q (+ 4), columns col0 + 4p .. +3
+    const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const __bf16* a0 = img + (row0 + 8 * g + q) * stride + col0 + 4 * p;
+    const zv4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) zv4i16*)a0);
+    const zv4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) zv4i16*)(a0 + 4 * stride));
+    typedef short v8i16 __attribute__((ext_vector_type(8)));
+    const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+__global__ __launch_bounds__(D16T) void k_zconv16_dw(const float* __restrict__ dY, int ldy, const float* __restrict__ X,
+                                                     int ldx, int B, int L, int Cin, int Cout, int K, int pad,
+                                                     float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) __bf16 dys[D16_DS];
+    __shared__ __attribute__((aligned(16))) __bf16 xs[D16_XS > D16_XS1 ? D16_XS : D16_XS1];
+    const int DS = Cout + 8, XS = Cin + 8;   // Cin / Cout multiples of 16: rows 16 B apart mod 64 banks
+    const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lc = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the tile indices in SGPRs
+    const int nIt = Cin >> 4, nT = (Cout >> 4) * nIt * K;
+    const int tpw = (nT + 7) >> 3;
+    const int j0 = wv * tpw;
+    int tot[D16MAXT], tit[D16MAXT], tk[D16MAXT];
+#pragma unroll
+    for (int j = 0; j < D16MAXT; ++j) {
+        const int jj = j0 + j;
+        tk[j] = jj % K;
+        const int rest = jj / K;
+        tit[j] = rest % nIt;
+        tot[j] = rest / nIt;
+    }
+    f32x4 acc[D16MAXT];
+#pragma unroll
+    for (int j = 0; j < D16MAXT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int win = D16R + K - 1;
+    for (int b = blockIdx.x; b < B; b += gridDim.x) {
+        const float* dyb = dY + (int64_t)b * L * ldy;
+        const float* xb = X + (int64_t)b * L * ldx;
+        for (int t0 = 0; t0 < L; t0 += D16R) {
+            __syncthreads();   // the previous chunk's MFMAs are done with both images
+            // dY rows t0 .. t0 + 63 (zero past L), 8 channels per item
+            const int og = Cout >> 3;
+            for (int i = tid; i < D16R * og; i += D16T) {
+                const int r = i / og, o8 = i - r * og;
+                const bool ok = t0 + r < L;
+                const float* src = dyb + (int64_t)(ok ? t0 + r : 0) * ldy + 8 * o8;
+                const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
+                const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+                bf16x8 h;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) h[j] = (__bf16)(ok ? v[j] : 0.f);
+                *reinterpret_cast<bf16x8*>(dys + r * DS + 8 * o8) = h;
+            }
+            // the window: rows t0 - pad .. t0 - pad + win - 1 (zero outside [0, L))
+            const int ig = Cin >> 3;
+            for (int i = tid; i < win * ig; i += D16T) {
+                const int r = i / ig, i8 = i - r * ig;
+                const int t = t0 + r - pad;
+                const bool ok = t >= 0 && t < L;
+                const float* src = xb + (int64_t)(ok ? t : 0) * ldx + 8 * i8;
+                const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
+                const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+                bf16x8 h;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) h[j] = (__bf16)(ok ? v[j] : 0.f);
+                *reinterpret_cast<bf16x8*>(xs + r * XS + 8 * i8) = h;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < D16R / 32; ++s) {
+                if (j0 >= nT) break;   // wave-uniform: a wave without tiles only stages
+                int ot_prev = -1;
+                bf16x8 a;
+#pragma unroll
+                for (int j = 0; j < D16MAXT; ++j) {
+                    // no per-lane early-out: the transposed reads need all 64 lanes
+                    if (j < tpw && j0 + j < nT) {
+                        if (tot[j] != ot_prev) {
+                            a = ztr_frag(dys, 32 * s, 16 * tot[j], DS);
+                            ot_prev = tot[j];
+                        }
+                        const bf16x8 bb = ztr_frag(xs, 32 * s + tk[j], 16 * tit[j], XS);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[j], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+    // D: col (i) = lane & 15, row (o) = 4 (lane >> 4) + r.  Slab layout [tap][o][i] (i fastest:
+    // 64-byte row segments per store instead of a K-float stride between lanes); the [o][i][tap]
+    // weight layout is restored by the slab sum's output permutation (conv.hip sum_splits_launch)
+    float* slab = part + (int64_t)blockIdx.x * Cout * Cin * K;
+#pragma unroll
+    for (int j = 0; j < D16MAXT; ++j) {
+        if (j < tpw && j0 + j < nT) {
+            const int i = 16 * tit[j] + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = 16 * tot[j] + 4 * lc + r;
+                slab[((int64_t)tk[j] * Cout + o) * Cin + i] = acc[j][r];
+            }
+        }
+    }
+}
+
 
 // ------------------------------------------------------------- elementwise
 __global__ void k_maxpool3_fwd(const float* __restrict__ X, int B, int L, int C, float* __restrict__ Y) {
@@ -641,9 +958,120 @@ int vt_zconv_bwd_data(const float* dY, int ldy, int B, int L, int Cin, const flo
     return VT_OK;
 }
 
+int vt_zconv16_ws_floats(int Cin, int Cout, int K, int64_t* floats) {
+    VT_CHECK_ARG(floats && Cin > 0 && Cout > 0 && K > 0, "vt_zconv16_ws_floats: args");
+    const int64_t a = zconv16_taps_elems(Cin, Cout, K), b = zconv16_taps_elems(Cout, Cin, K);   // fwd / bwd-data
+    *floats = ((a > b ? a : b) + 1) / 2;
+    return VT_OK;
+}
+
+int vt_zconv16_taps_elems(int Cin, int Cout, int K, int64_t* elems) {
+    VT_CHECK_ARG(elems && Cin > 0 && Cout > 0 && K > 0, "vt_zconv16_taps_elems: args");
+    *elems = zconv16_taps_elems(Cin, Cout, K);
+    return VT_OK;
+}
+
+int vt_zconv16_taps(int n, const int64_t* W, const int* Cin, const int* Cout, const int* K, int flip,
+                    const int64_t* T, void* stream) {
+    VT_CHECK_ARG(n >= 1 && n <= ZTB_MAX && W && Cin && Cout && K && T, "vt_zconv16_taps: %d weights (1..%d)", n,
+                 ZTB_MAX);
+    ZTapBatch tb{};
+    tb.n = n;
+    tb.flip = flip ? 1 : 0;
+    tb.prefix[0] = 0;
+    for (int h = 0; h < n; ++h) {
+        VT_CHECK_ARG(W[h] && T[h] && !(T[h] & 15) && Cin[h] > 0 && Cout[h] > 0 && K[h] > 0,
+                     "vt_zconv16_taps: weight %d", h);
+        // the image of the convolution that reads it: forward (Cin -> Cout) or, flip, the
+        // backward-data conv (Cout -> Cin) of the same weight
+        const int ci = flip ? Cout[h] : Cin[h], co = flip ? Cin[h] : Cout[h];
+        tb.W[h] = reinterpret_cast<const float*>(W[h]);
+        tb.T[h] = reinterpret_cast<__bf16*>(T[h]);
+        tb.Cin[h] = ci;
+        tb.Cout[h] = co;
+        tb.K[h] = K[h];
+        tb.TC[h] = co <= 32 ? 32 : 128;
+        tb.cin32[h] = (ci + 31) & ~31;
+        const int64_t e = (int64_t)K[h] * tb.TC[h] * tb.cin32[h];
+        tb.prefix[h + 1] = tb.prefix[h] + (int)((e + 255) / 256);
+    }
+    hipLaunchKernelGGL(k_zconv16_taps_batch, dim3((unsigned)tb.prefix[n]), dim3(256), 0, S(stream), tb);
+    VT_LAUNCH_CHECK("vt_zconv16_taps");
+    return VT_OK;
+}
+
+int vt_zconv16_fwd_t(const float* X, int ldx, int B, int L, int Cin, const void* T, int Cout, int K, int pad_left,
+                     float* Y, int ldy, int accumulate, void* stream) {
+    VT_CHECK_ARG(zconv_shape_ok(B, L, Cin, Cout, K, pad_left) && ldx >= Cin && ldy >= Cout && T &&
+                     !(reinterpret_cast<uintptr_t>(T) & 15),
+                 "vt_zconv16_fwd_t: shape / tap image");
+    VT_CHECK_ARG(zconv16_launch<false>(X, ldx, B, L, Cin, nullptr, Cout, K, pad_left, Y, ldy, accumulate,
+                                       reinterpret_cast<__bf16*>(const_cast<void*>(T)), S(stream)) == VT_OK,
+                 "vt_zconv16_fwd_t: unsupported configuration (X 16-B aligned, ldx a multiple of 4)");
+    VT_LAUNCH_CHECK("vt_zconv16_fwd_t");
+    return VT_OK;
+}
+
+int vt_zconv16_bwd_data_t(const float* dY, int ldy, int B, int L, int Cin, const void* T, int Cout, int K,
+                          int pad_left, float* dX, int ldx, int accumulate, void* stream) {
+    VT_CHECK_ARG(zconv_shape_ok(B, L, Cin, Cout, K, pad_left) && ldx >= Cin && ldy >= Cout && T &&
+                     !(reinterpret_cast<uintptr_t>(T) & 15),
+                 "vt_zconv16_bwd_data_t: shape / tap image");
+    VT_CHECK_ARG(zconv16_launch<true>(dY, ldy, B, L, Cout, nullptr, Cin, K, K - 1 - pad_left, dX, ldx, accumulate,
+                                      reinterpret_cast<__bf16*>(const_cast<void*>(T)), S(stream)) == VT_OK,
+                 "vt_zconv16_bwd_data_t: unsupported configuration (dY 16-B aligned, ldy a multiple of 4)");
+    VT_LAUNCH_CHECK("vt_zconv16_bwd_data_t");
+    return VT_OK;
+}
+
+int vt_zconv16_fwd(const float* X, int ldx, int B, int L, int Cin, const float* W, int Cout, int K, int pad_left,
+                   float* Y, int ldy, int accumulate, float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(zconv_shape_ok(B, L, Cin, Cout, K, pad_left) && ldx >= Cin && ldy >= Cout,
+                 "vt_zconv16_fwd: shape (Cin/Cout multiples of 16 <= 128, K in {1,5,15,40}, 0 <= pad < K)");
+    VT_CHECK_ARG(ws && 2 * ws_floats >= zconv16_taps_elems(Cin, Cout, K) && !(reinterpret_cast<uintptr_t>(ws) & 15),
+                 "vt_zconv16_fwd: workspace (vt_zconv16_ws_floats, 16-B aligned)");
+    VT_CHECK_ARG(zconv16_launch<false>(X, ldx, B, L, Cin, W, Cout, K, pad_left, Y, ldy, accumulate,
+                                       reinterpret_cast<__bf16*>(ws), S(stream)) == VT_OK,
+                 "vt_zconv16_fwd: unsupported configuration (X 16-B aligned, ldx a multiple of 4)");
+    VT_LAUNCH_CHECK("vt_zconv16_fwd");
+    return VT_OK;
+}
+
+int vt_zconv16_bwd_data(const float* dY, int ldy, int B, int L, int Cin, const float* W, int Cout, int K, int pad_left,
+                        float* dX, int ldx, int accumulate, float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(zconv_shape_ok(B, L, Cin, Cout, K, pad_left) && ldx >= Cin && ldy >= Cout,
+                 "vt_zconv16_bwd_data: shape");
+    VT_CHECK_ARG(ws && 2 * ws_floats >= zconv16_taps_elems(Cout, Cin, K) && !(reinterpret_cast<uintptr_t>(ws) & 15),
+                 "vt_zconv16_bwd_data: workspace (vt_zconv16_ws_floats, 16-B aligned)");
+    VT_CHECK_ARG(zconv16_launch<true>(dY, ldy, B, L, Cout, W, Cin, K, K - 1 - pad_left, dX, ldx, accumulate,
+                                      reinterpret_cast<__bf16*>(ws), S(stream)) == VT_OK,
+                 "vt_zconv16_bwd_data: unsupported configuration (dY 16-B aligned, ldy a multiple of 4)");
+    VT_LAUNCH_CHECK("vt_zconv16_bwd_data");
+    return VT_OK;
+}
+
+int vt_zconv16_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int B, int L, int Cin, int Cout, int K,
+                          int pad_left, float* dW, int accumulate, float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(zconv_shape_ok(B, L, Cin, Cout, K, pad_left) && ldx >= Cin && ldy >= Cout && !(ldx & 3) &&
+                     !(ldy & 3) && !(reinterpret_cast<uintptr_t>(dY) & 15) && !(reinterpret_cast<uintptr_t>(X) & 15),
+                 "vt_zconv16_bwd_weight: shape / alignment (16-B rows)");
+    VT_CHECK_ARG(((Cout / 16) * (Cin / 16) * K + 7) / 8 <= D16MAXT, "vt_zconv16_bwd_weight: too many tiles");
+    // fewer, longer workgroups than the fp32 kernel (its slabs dominated: one sample of MFMA work
+    // per workgroup is ~1 us on bf16 MFMA): <= 128 slabs
+    const int G = B < 128 ? B : 128;
+    const int64_t n = (int64_t)Cout * Cin * K;
+    VT_CHECK_ARG(ws_floats >= G * n, "vt_zconv16_bwd_weight: workspace too small");
+    hipStream_t st = S(stream);
+    hipLaunchKernelGGL(k_zconv16_dw, dim3(G), dim3(D16T), 0, st, dY, ldy, X, ldx, B, L, Cin, Cout, K, pad_left, ws);
+    sum_splits_launch(ws, G, n, dW, accumulate, st, K, Cout, Cin);   // slab order [k][o][i] -> dW [o][i][k]
+    VT_LAUNCH_CHECK("vt_zconv16_bwd_weight");
+    return VT_OK;
+}
+
 int vt_zconv_bwd_weight_ws_floats(int B, int Cin, int Cout, int K, int64_t* floats) {
     VT_CHECK_ARG(B > 0 && floats, "vt_zconv_bwd_weight_ws_floats: args");
-    *floats = (int64_t)zdw_groups(B) * Cout * Cin * K;
+    const int g16 = B < 128 ? B : 128;   // vt_zconv16_bwd_weight's slabs
+    *floats = (int64_t)(zdw_groups(B) > g16 ? zdw_groups(B) : g16) * Cout * Cin * K;
     return VT_OK;
 }
 

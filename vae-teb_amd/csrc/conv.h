@@ -175,7 +175,10 @@ static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 int bn_stats_finalize_launch(const float* stats, int tiles_per_sample, int B, int TP, int Lo, int C, float eps,
                              float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
                              hipStream_t st);
-int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st);
+// out (+)= the fixed-order sum of `splits` slabs of n floats; (pK, pCo, pCi) != 0: the slabs are
+// in [k][o][i] order and out in [o][i][k] (the classifier's bf16 weight gradient)
+int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st,
+                      int pK = 0, int pCo = 0, int pCi = 0);
 // conv_fwd16.hip: the flat-staged bf16 forward (returns its position tile, or VT_ERR_ARG);
 // ibn (nullable): x is the previous block's pre-BN output, its BatchNorm + act applied in staging
 int cfw16_launch(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,

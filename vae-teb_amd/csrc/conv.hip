@@ -422,9 +422,19 @@ __global__ __launch_bounds__(512) void k_conv_dw(const float* __restrict__ dy, c
     }
 }
 
+// output position of slab element i: identity, or (SumPerm) slab order [k][o][i] -> [o][i][k]
+struct SumPerm {
+    int K, Co, Ci;   // K == 0: identity
+};
+__device__ __forceinline__ int64_t perm_out(int64_t i, SumPerm p) {
+    if (p.K == 0) return i;
+    const int64_t ci = i % p.Ci, r = i / p.Ci, o = r % p.Co, k = r / p.Co;
+    return (o * p.Ci + ci) * p.K + k;
+}
+
 // out[i] (+)= sum_s part[s][i] (fixed order): 64 outputs x 4 split lanes per workgroup
 __global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ part, int splits, int64_t n,
-                                                    float* __restrict__ out, int accumulate) {
+                                                    float* __restrict__ out, int accumulate, SumPerm pm) {
     __shared__ float red[4][64];
     const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * 64 + o;
@@ -437,7 +447,8 @@ __global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ pa
     __syncthreads();
     if (sl == 0 && i < n) {
         const float s = (red[0][o] + red[1][o]) + (red[2][o] + red[3][o]);
-        out[i] = accumulate ? out[i] + s : s;
+        const int64_t q = perm_out(i, pm);
+        out[q] = accumulate ? out[q] + s : s;
     }
 }
 
@@ -495,7 +506,8 @@ VT_ARRIVE_POOL(g_arrive_splits);
 // stage 2 for that block (the same fixed tree over the group sums as a separate pass would:
 // the same bits, one launch)
 __global__ __launch_bounds__(256) void k_sum_splits_grp(float* __restrict__ part, int splits, int64_t n,
-                                                        float* __restrict__ out, int accumulate, unsigned slot0) {
+                                                        float* __restrict__ out, int accumulate, unsigned slot0,
+                                                        SumPerm pm) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int s0 = blockIdx.y * SG_GRP;
     const int s1 = s0 + SG_GRP < splits ? s0 + SG_GRP : splits;
@@ -519,24 +531,27 @@ __global__ __launch_bounds__(256) void k_sum_splits_grp(float* __restrict__ part
     for (int w = SG_GRP / 2; w >= 1; w /= 2)
 #pragma unroll
         for (int u = 0; u < w; ++u) a[u] += a[u + w];
-    out[i] = accumulate ? out[i] + a[0] : a[0];
+    const int64_t q = perm_out(i, pm);
+    out[q] = accumulate ? out[q] + a[0] : a[0];
 }
 
 // part is scratch: the two-stage path overwrites it
-int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st) {
+int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int accumulate, hipStream_t st,
+                      int pK, int pCo, int pCi) {
+    const SumPerm pm{pK, pCo, pCi};
     // one stage only for few splits: with many (e.g. 330 slabs of the 74k-weight K = 11 layer) a
     // thread's serial loop over the slabs was latency-bound (80 us); the group stage keeps
     // SG_GRP loads in flight per thread at any n
     if (splits <= 2 * SG_GRP) {
         hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, splits, n, out,
-                           accumulate);
+                           accumulate, pm);
         return VT_OK;
     }
     if (splits > SG_GRP * SG_GRP) return VT_ERR_ARG;
     float* p = const_cast<float*>(part);
     const unsigned bx = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_sum_splits_grp, dim3(bx, (unsigned)((splits + SG_GRP - 1) / SG_GRP)), dim3(256), 0, st, p,
-                       splits, n, out, accumulate, arrive_slots(bx));
+                       splits, n, out, accumulate, arrive_slots(bx), pm);
     return VT_OK;
 }
 

@@ -52,6 +52,59 @@ def _col(t, c0):
     return t.data_ptr() + 4 * c0
 
 
+def _zc(name, bf16):
+    """The zero-pad conv entry point: exact fp32 (the parity path) or bf16 MFMA operands with fp32
+    accumulation (vt_zconv16_*: the reference's 16-bit autocast, set_conv_precision("bf16"))."""
+    assert name != "vt_zconv_bwd_weight_ws_floats"
+    return name.replace("vt_zconv_", "vt_zconv16_") if bf16 else name
+
+
+def _zcall(name, bf16, *args):
+    """One zero-pad conv call (vt_zconv_fwd / _bwd_data / _bwd_weight arguments); bf16: the
+    vt_zconv16_* kernel, whose forward / backward-data also take the workspace of the call's
+    bf16 tap image (WS slot 6: the classifier's convolutions run in stream order)."""
+    if bf16 and name in ("vt_zconv_fwd", "vt_zconv_bwd_data"):
+        Cin, Cout, K = args[4], args[6], args[7]
+        f = ctypes.c_int64()
+        call("vt_zconv16_ws_floats", Cin, Cout, K, ctypes.byref(f))
+        ws = WS.get(int(f.value), torch.device("cuda", torch.cuda.current_device()), 6)
+        call(_zc(name, True), *args[:-1], ptr(ws), ws.numel(), args[-1])
+    else:
+        call(_zc(name, bf16), *args)
+
+
+_TAPS_ELEMS = {}
+
+
+def _tap_images(ws, flip, slot):
+    """bf16 tap images of the block's weights ws = [(W, Cin, Cout, K), ...] in one launch
+    (vt_zconv16_taps; flip: the backward-data images) -> one device pointer per weight, valid
+    until the next use of WS slot `slot` (the block's convolutions run right after, in stream order)."""
+    sizes = []
+    for w, ci, co, k in ws:
+        key = (co, ci, k) if flip else (ci, co, k)
+        n = _TAPS_ELEMS.get(key)
+        if n is None:
+            e = ctypes.c_int64()
+            call("vt_zconv16_taps_elems", *key, ctypes.byref(e))
+            n = _TAPS_ELEMS[key] = (int(e.value) + 7) // 8 * 8   # 16-byte aligned images
+        sizes.append(n)
+    buf = WS.get((sum(sizes) + 1) // 2, ws[0][0].device, slot)
+    base, ptrs = buf.data_ptr(), []
+    for n in sizes:
+        ptrs.append(base)
+        base += 2 * n
+    m = len(ws)
+    W = (ctypes.c_int64 * m)(*[w.data_ptr() for w, _, _, _ in ws])
+    Ci = (ctypes.c_int * m)(*[ci for _, ci, _, _ in ws])
+    Co = (ctypes.c_int * m)(*[co for _, _, co, _ in ws])
+    Ks = (ctypes.c_int * m)(*[k for _, _, _, k in ws])
+    T = (ctypes.c_int64 * m)(*ptrs)
+    call("vt_zconv16_taps", m, ctypes.addressof(W), ctypes.addressof(Ci), ctypes.addressof(Co), ctypes.addressof(Ks),
+         int(flip), ctypes.addressof(T), _st())
+    return ptrs
+
+
 def _dw_ws(B, Cin, Cout, K, device):
     f = ctypes.c_int64()
     call("vt_zconv_bwd_weight_ws_floats", B, Cin, Cout, K, ctypes.byref(f))
@@ -65,7 +118,7 @@ class _InceptionF(torch.autograd.Function):
     column slices of the concatenation, train-mode BatchNorm + ReLU, Dropout1d."""
 
     @staticmethod
-    def forward(ctx, x, wb1, ws, wm, wl, wb2, g, b, run_mean, run_var, momentum, eps, p, seed):
+    def forward(ctx, x, wb1, ws, wm, wl, wb2, g, b, run_mean, run_var, momentum, eps, p, seed, bf16=False):
         _check(x, wb1, ws, wm, wl, wb2, g, b)
         x = x.contiguous()
         B, L, Cin = x.shape
@@ -73,13 +126,22 @@ class _InceptionF(torch.autograd.Function):
         C4 = 4 * f
         st = _st()
         x0 = torch.empty((B, L, f), device=x.device)
-        call("vt_zconv_fwd", ptr(x), Cin, B, L, Cin, ptr(wb1), f, 1, 0, ptr(x0), f, 0, st)
         cat = torch.empty((B, L, C4), device=x.device)
-        for j, (w, K, P) in enumerate(((ws, 5, 2), (wm, 15, 7), (wl, 40, 20))):
-            call("vt_zconv_fwd", ptr(x0), f, B, L, f, ptr(w), f, K, P, _col(cat, j * f), C4, 0, st)
         mp = torch.empty_like(x)
-        call("vt_maxpool3_fwd", ptr(x), B, L, Cin, ptr(mp), st)
-        call("vt_zconv_fwd", ptr(mp), Cin, B, L, Cin, ptr(wb2), f, 1, 0, _col(cat, 3 * f), C4, 0, st)
+        if bf16:   # the five tap images in one launch, then the convolutions read them
+            T = _tap_images([(wb1, Cin, f, 1), (ws, f, f, 5), (wm, f, f, 15), (wl, f, f, 40), (wb2, Cin, f, 1)],
+                            False, 7)
+            call("vt_zconv16_fwd_t", ptr(x), Cin, B, L, Cin, T[0], f, 1, 0, ptr(x0), f, 0, st)
+            for j, (K, P) in enumerate(((5, 2), (15, 7), (40, 20))):
+                call("vt_zconv16_fwd_t", ptr(x0), f, B, L, f, T[1 + j], f, K, P, _col(cat, j * f), C4, 0, st)
+            call("vt_maxpool3_fwd", ptr(x), B, L, Cin, ptr(mp), st)
+            call("vt_zconv16_fwd_t", ptr(mp), Cin, B, L, Cin, T[4], f, 1, 0, _col(cat, 3 * f), C4, 0, st)
+        else:
+            call("vt_zconv_fwd", ptr(x), Cin, B, L, Cin, ptr(wb1), f, 1, 0, ptr(x0), f, 0, st)
+            for j, (w, K, P) in enumerate(((ws, 5, 2), (wm, 15, 7), (wl, 40, 20))):
+                call("vt_zconv_fwd", ptr(x0), f, B, L, f, ptr(w), f, K, P, _col(cat, j * f), C4, 0, st)
+            call("vt_maxpool3_fwd", ptr(x), B, L, Cin, ptr(mp), st)
+            call("vt_zconv_fwd", ptr(mp), Cin, B, L, Cin, ptr(wb2), f, 1, 0, _col(cat, 3 * f), C4, 0, st)
         y = torch.empty_like(cat)
         mean = torch.empty(C4, device=x.device)
         rstd = torch.empty(C4, device=x.device)
@@ -90,14 +152,14 @@ class _InceptionF(torch.autograd.Function):
             call("vt_dropout_apply", ptr(y), y.numel(), C4, L, float(p), *_sarg(seed), ptr(y), st)
         ctx.save_for_backward(x, x0, mp, cat, mean, rstd)
         ctx.params = (wb1, ws, wm, wl, wb2, g, b)
-        ctx.cfg = (p, seed)
+        ctx.cfg = (p, seed, bf16)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, x0, mp, cat, mean, rstd = ctx.saved_tensors
         wb1, ws, wm, wl, wb2, g, b = ctx.params
-        p, seed = ctx.cfg
+        p, seed, bf16 = ctx.cfg
         B, L, Cin = x.shape
         f = wb1.shape[0]
         C4 = 4 * f
@@ -114,26 +176,31 @@ class _InceptionF(torch.autograd.Function):
              ptr(gcat), ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(bws), bws.numel(), st)
         pw = _ParamGrads([wb1, ws, wm, wl, wb2], [True] * 5)
         gx0 = torch.empty_like(x0)
+        # backward-data taps: one launch for the block's five flipped images (bf16)
+        T = _tap_images([(wb1, Cin, f, 1), (ws, f, f, 5), (wm, f, f, 15), (wl, f, f, 40), (wb2, Cin, f, 1)],
+                        True, 7) if bf16 else None
+        bd = (lambda j, w: T[j]) if bf16 else (lambda j, w: ptr(w))
+        zbd = "vt_zconv16_bwd_data_t" if bf16 else "vt_zconv_bwd_data"
         for j, (w, K, P) in enumerate(((ws, 5, 2), (wm, 15, 7), (wl, 40, 20))):
-            call("vt_zconv_bwd_data", _col(gcat, j * f), C4, B, L, f, ptr(w), f, K, P, ptr(gx0), f, int(j > 0), st)
+            call(zbd, _col(gcat, j * f), C4, B, L, f, bd(1 + j, w), f, K, P, ptr(gx0), f, int(j > 0), st)
             dws = _dw_ws(B, f, f, K, x.device)
-            call("vt_zconv_bwd_weight", _col(gcat, j * f), C4, ptr(x0), f, B, L, f, f, K, P, ptr(pw.out[1 + j]),
-                 pw.acc, ptr(dws), dws.numel(), st)
+            _zcall("vt_zconv_bwd_weight", bf16, _col(gcat, j * f), C4, ptr(x0), f, B, L, f, f, K, P,
+                   ptr(pw.out[1 + j]), pw.acc, ptr(dws), dws.numel(), st)
         gmp = torch.empty_like(mp)
-        call("vt_zconv_bwd_data", _col(gcat, 3 * f), C4, B, L, Cin, ptr(wb2), f, 1, 0, ptr(gmp), Cin, 0, st)
+        call(zbd, _col(gcat, 3 * f), C4, B, L, Cin, bd(4, wb2), f, 1, 0, ptr(gmp), Cin, 0, st)
         dws = _dw_ws(B, Cin, f, 1, x.device)
-        call("vt_zconv_bwd_weight", _col(gcat, 3 * f), C4, ptr(mp), Cin, B, L, Cin, f, 1, 0, ptr(pw.out[4]), pw.acc,
-             ptr(dws), dws.numel(), st)
+        _zcall("vt_zconv_bwd_weight", bf16, _col(gcat, 3 * f), C4, ptr(mp), Cin, B, L, Cin, f, 1, 0, ptr(pw.out[4]),
+               pw.acc, ptr(dws), dws.numel(), st)
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             call("vt_maxpool3_bwd", ptr(gmp), ptr(x), B, L, Cin, ptr(gx), 0, st)
-            call("vt_zconv_bwd_data", ptr(gx0), f, B, L, Cin, ptr(wb1), f, 1, 0, ptr(gx), Cin, 1, st)
-        call("vt_zconv_bwd_weight", ptr(gx0), f, ptr(x), Cin, B, L, Cin, f, 1, 0, ptr(pw.out[0]), pw.acc, ptr(dws),
-             dws.numel(), st)
+            call(zbd, ptr(gx0), f, B, L, Cin, bd(0, wb1), f, 1, 0, ptr(gx), Cin, 1, st)
+        _zcall("vt_zconv_bwd_weight", bf16, ptr(gx0), f, ptr(x), Cin, B, L, Cin, f, 1, 0, ptr(pw.out[0]), pw.acc,
+               ptr(dws), dws.numel(), st)
         gws = pw.result()
         gg, gb = pbn.result()
-        return (gx, *gws, gg, gb) + (None,) * 6
+        return (gx, *gws, gg, gb) + (None,) * 7
 
 
 class _ResidualF(torch.autograd.Function):
@@ -141,14 +208,14 @@ class _ResidualF(torch.autograd.Function):
     relu(y + BN(bottleneck(x))) then Dropout1d."""
 
     @staticmethod
-    def forward(ctx, x, y, w, g, b, run_mean, run_var, momentum, eps, p, seed):
+    def forward(ctx, x, y, w, g, b, run_mean, run_var, momentum, eps, p, seed, bf16=False):
         _check(x, y, w, g, b)
         x, y = x.contiguous(), y.contiguous()
         B, L, Cin = x.shape
         C4 = w.shape[0]
         st = _st()
         r = torch.empty((B, L, C4), device=x.device)
-        call("vt_zconv_fwd", ptr(x), Cin, B, L, Cin, ptr(w), C4, 1, 0, ptr(r), C4, 0, st)
+        _zcall("vt_zconv_fwd", bf16, ptr(x), Cin, B, L, Cin, ptr(w), C4, 1, 0, ptr(r), C4, 0, st)
         rb = torch.empty_like(r)
         mean = torch.empty(C4, device=x.device)
         rstd = torch.empty(C4, device=x.device)
@@ -163,14 +230,14 @@ class _ResidualF(torch.autograd.Function):
             call("vt_dropout_apply", ptr(s), s.numel(), C4, L, float(p), *_sarg(seed), ptr(out), st)
         ctx.save_for_backward(x, r, s, mean, rstd)
         ctx.params = (w, g, b)
-        ctx.cfg = (p, seed)
+        ctx.cfg = (p, seed, bf16)
         return out
 
     @staticmethod
     def backward(ctx, gout):
         x, r, s, mean, rstd = ctx.saved_tensors
         w, g, b = ctx.params
-        p, seed = ctx.cfg
+        p, seed, bf16 = ctx.cfg
         B, L, Cin = x.shape
         C4 = w.shape[0]
         st = _st()
@@ -188,15 +255,15 @@ class _ResidualF(torch.autograd.Function):
              ptr(gr), ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(bws), bws.numel(), st)
         pw = _ParamGrads([w], [True])
         dws = _dw_ws(B, Cin, C4, 1, x.device)
-        call("vt_zconv_bwd_weight", ptr(gr), C4, ptr(x), Cin, B, L, Cin, C4, 1, 0, ptr(pw.out[0]), pw.acc, ptr(dws),
-             dws.numel(), st)
+        _zcall("vt_zconv_bwd_weight", bf16, ptr(gr), C4, ptr(x), Cin, B, L, Cin, C4, 1, 0, ptr(pw.out[0]), pw.acc,
+               ptr(dws), dws.numel(), st)
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
-            call("vt_zconv_bwd_data", ptr(gr), C4, B, L, Cin, ptr(w), C4, 1, 0, ptr(gx), Cin, 0, st)
+            _zcall("vt_zconv_bwd_data", bf16, ptr(gr), C4, B, L, Cin, ptr(w), C4, 1, 0, ptr(gx), Cin, 0, st)
         gw, = pw.result()
         gg, gb = pbn.result()
-        return gx, gs, gw, gg, gb, None, None, None, None, None, None
+        return gx, gs, gw, gg, gb, None, None, None, None, None, None, None
 
 
 class _AttnCoreF(torch.autograd.Function):
@@ -345,14 +412,16 @@ def _inception_eval(m, x):
     C4 = 4 * f
     st = _st()
     x0 = torch.empty((B, L, f), device=x.device)
-    call("vt_zconv_fwd", ptr(x), Cin, B, L, Cin, ptr(m.bottleneck1.weight), f, 1, 0, ptr(x0), f, 0, st)
+    bf16 = m.bf16
+    _zcall("vt_zconv_fwd", bf16, ptr(x), Cin, B, L, Cin, ptr(m.bottleneck1.weight), f, 1, 0, ptr(x0), f, 0, st)
     cat = torch.empty((B, L, C4), device=x.device)
     for j, (w, K, P) in enumerate(((m.conv_short.weight, 5, 2), (m.conv_medium.weight, 15, 7),
                                    (m.conv_long.weight, 40, 20))):
-        call("vt_zconv_fwd", ptr(x0), f, B, L, f, ptr(w), f, K, P, _col(cat, j * f), C4, 0, st)
+        _zcall("vt_zconv_fwd", bf16, ptr(x0), f, B, L, f, ptr(w), f, K, P, _col(cat, j * f), C4, 0, st)
     mp = torch.empty_like(x)
     call("vt_maxpool3_fwd", ptr(x), B, L, Cin, ptr(mp), st)
-    call("vt_zconv_fwd", ptr(mp), Cin, B, L, Cin, ptr(m.bottleneck2.weight), f, 1, 0, _col(cat, 3 * f), C4, 0, st)
+    _zcall("vt_zconv_fwd", bf16, ptr(mp), Cin, B, L, Cin, ptr(m.bottleneck2.weight), f, 1, 0, _col(cat, 3 * f), C4,
+           0, st)
     bn = m.batch_norm
     call("vt_batchnorm_eval", ptr(cat), B * L, C4, ptr(bn.running_mean), ptr(bn.running_var), bn.eps, ptr(bn.weight),
          ptr(bn.bias), ACT["relu"], ptr(cat), st)
@@ -366,7 +435,7 @@ def _residual_eval(m, x, y):
     C4 = m.bottleneck.weight.shape[0]
     st = _st()
     r = torch.empty((B, L, C4), device=x.device)
-    call("vt_zconv_fwd", ptr(x), Cin, B, L, Cin, ptr(m.bottleneck.weight), C4, 1, 0, ptr(r), C4, 0, st)
+    _zcall("vt_zconv_fwd", m.bf16, ptr(x), Cin, B, L, Cin, ptr(m.bottleneck.weight), C4, 1, 0, ptr(r), C4, 0, st)
     bn = m.batch_norm
     call("vt_batchnorm_eval", ptr(r), B * L, C4, ptr(bn.running_mean), ptr(bn.running_var), bn.eps, ptr(bn.weight),
          ptr(bn.bias), ACT["none"], ptr(r), st)
@@ -387,6 +456,7 @@ class FHRInception(nn.Module):
         self.bottleneck2 = _ConvWeight(input_size, filters, 1)
         self.batch_norm = _BatchNorm(4 * filters, momentum=0.1)
         self.dropout = dropout
+        self.bf16 = False   # bf16-MFMA convolutions (FHRInceptionTimeClassifier.set_conv_precision)
         for m in (self.bottleneck1, self.conv_short, self.conv_medium, self.conv_long, self.bottleneck2):
             nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
 
@@ -397,7 +467,7 @@ class FHRInception(nn.Module):
         p = self.dropout
         y = _InceptionF.apply(x, self.bottleneck1.weight, self.conv_short.weight, self.conv_medium.weight,
                               self.conv_long.weight, self.bottleneck2.weight, bn.weight, bn.bias, bn.running_mean,
-                              bn.running_var, bn.momentum, bn.eps, p, _seed() if p > 0 else 0)
+                              bn.running_var, bn.momentum, bn.eps, p, _seed() if p > 0 else 0, self.bf16)
         bn.num_batches_tracked.add_(1)
         return y
 
@@ -410,6 +480,7 @@ class FHRResidual(nn.Module):
         self.bottleneck = _ConvWeight(input_size, 4 * filters, 1)
         self.batch_norm = _BatchNorm(4 * filters, momentum=0.1)
         self.dropout = dropout
+        self.bf16 = False
         nn.init.kaiming_normal_(self.bottleneck.weight, mode="fan_out", nonlinearity="relu")
 
     def forward(self, x, y):
@@ -418,7 +489,7 @@ class FHRResidual(nn.Module):
             return _residual_eval(self, x, y)
         p = self.dropout
         out = _ResidualF.apply(x, y, self.bottleneck.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                               bn.momentum, bn.eps, p, _seed() if p > 0 else 0)
+                               bn.momentum, bn.eps, p, _seed() if p > 0 else 0, self.bf16)
         bn.num_batches_tracked.add_(1)
         return out
 
@@ -473,6 +544,18 @@ class FHRInceptionTimeClassifier(nn.Module):
         self.classifier = nn.Sequential(Linear(4 * f, 2 * f), LayerNorm(2 * f), Activation("gelu"),
                                         Activation("dropout"), Linear(2 * f, f), LayerNorm(f), Activation("gelu"),
                                         Activation("dropout"), Linear(f, num_classes))
+
+    def set_conv_precision(self, precision):
+        """"fp32": the inception / residual convolutions on the exact-fp32 kernels (parity mode);
+        "bf16": on bf16 MFMA with fp32 accumulation (vt_zconv16_*), the reference's 16-bit
+        autocast training precision (ref/model/graph_model.py:510) in bf16: forward,
+        backward-data and weight gradient."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"conv precision must be 'fp32' or 'bf16', got {precision!r}")
+        for m in self.modules():
+            if isinstance(m, (FHRInception, FHRResidual)):
+                m.bf16 = precision == "bf16"
+        return self
 
     def forward(self, x):
         global _SEED_OFF
@@ -542,6 +625,9 @@ class SeqVaeTebClassifier(nn.Module):
         self.classifier = FHRInceptionTimeClassifier(input_size=latent_dim_z, num_classes=num_classes,
                                                      filters=classifier_filters, depth=classifier_depth,
                                                      dropout=classifier_dropout, use_attention=use_attention)
+        # the VAE's conv precision (SeqVaeTeb(conv_precision=...)) applies to the classifier's convs too
+        if vae_kwargs.get("conv_precision") == "bf16":
+            self.classifier.set_conv_precision("bf16")
 
     def load_pretrained_vae(self, path):
         """ref :1322-1348 (weights-only load; keys model_state_dict / state_dict / bare)."""
