@@ -454,8 +454,8 @@ __global__ __launch_bounds__(DT) void k_zconv_dw(const float* __restrict__ dY, i
 // Tiles (o, i, tap) with the tap fastest, 8 waves x <= D16MAXT tiles; per-workgroup slabs
 // summed in fixed order (k_sum_splits).
 typedef short zv4i16 __attribute__((ext_vector_type(4)));
-constexpr int D16T = 512, D16R = 64, D16MAXT = 20;
-constexpr int D16_DS = 136 * D16R;                  // dY image: 64 rows x (<= 128 + 8) channels
+constexpr int D16T = 512, D16R = 128, D16MAXT = 20;   // 128-row chunks: half the staging round trips of 64
+constexpr int D16_DS = 136 * D16R;                  // dY image: 128 rows x (<= 128 + 8) channels
 constexpr int D16_XS = (D16R + 40 + 8) * 40;        // window image, K <= 40 at <= 32 channels ...
 constexpr int D16_XS1 = D16R * 136;                 // ... or K 1 at <= 128 channels
 
@@ -1056,9 +1056,9 @@ int vt_zconv16_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int
                      !(ldy & 3) && !(reinterpret_cast<uintptr_t>(dY) & 15) && !(reinterpret_cast<uintptr_t>(X) & 15),
                  "vt_zconv16_bwd_weight: shape / alignment (16-B rows)");
     VT_CHECK_ARG(((Cout / 16) * (Cin / 16) * K + 7) / 8 <= D16MAXT, "vt_zconv16_bwd_weight: too many tiles");
-    // fewer, longer workgroups than the fp32 kernel (its slabs dominated: one sample of MFMA work
-    // per workgroup is ~1 us on bf16 MFMA): <= 128 slabs
-    const int G = B < 128 ? B : 128;
+    // one sample per workgroup up to 256 (the chunks' staging round trips, not the MFMAs, bound
+    // a workgroup: 128 slabs took 25-44 us per launch whatever K)
+    const int G = zdw_groups(B);
     const int64_t n = (int64_t)Cout * Cin * K;
     VT_CHECK_ARG(ws_floats >= G * n, "vt_zconv16_bwd_weight: workspace too small");
     hipStream_t st = S(stream);
@@ -1070,8 +1070,7 @@ int vt_zconv16_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int
 
 int vt_zconv_bwd_weight_ws_floats(int B, int Cin, int Cout, int K, int64_t* floats) {
     VT_CHECK_ARG(B > 0 && floats, "vt_zconv_bwd_weight_ws_floats: args");
-    const int g16 = B < 128 ? B : 128;   // vt_zconv16_bwd_weight's slabs
-    *floats = (int64_t)(zdw_groups(B) > g16 ? zdw_groups(B) : g16) * Cout * Cin * K;
+    *floats = (int64_t)zdw_groups(B) * Cout * Cin * K;   // both weight-gradient kernels: one slab per group
     return VT_OK;
 }
 
