@@ -71,12 +71,13 @@ def test_conv_stack_fold_bitwise(name):
     x = torch.randn(B, L, spec[0][0], device="cuda")
     gy = torch.randn(B, Lo, spec[-1][1], device="cuda")
     res = []
+    saved = model.CONV_FOLD
     for fold in (0, 1):
         model.CONV_FOLD = fold
         try:
             res.append(_run(_stack(spec, 11), x, gy))
         finally:
-            model.CONV_FOLD = 1
+            model.CONV_FOLD = saved
     ref, got = res
     assert ref.keys() == got.keys()
     bad = [k for k in ref if not torch.equal(ref[k], got[k])]

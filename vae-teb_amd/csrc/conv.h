@@ -147,12 +147,10 @@ __device__ __forceinline__ void src_vec(const float* __restrict__ xb, const Geo&
         b[j] = g.up ? p1[c] : 0.f;
     }
     if constexpr (IBN) {   // channels past Cin: padding parameters, masked below
-        float sc[NC], sh[NC];
-        bn_in_n<NC>(ip, cs, cb, sc, sh);
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-            a[j] = bn_relu_val(a[j], sc[j], sh[j]);
-            b[j] = g.up ? bn_relu_val(b[j], sc[j], sh[j]) : 0.f;
+            a[j] = bn_relu_at(ip, cs, cb + j, a[j]);
+            b[j] = g.up ? bn_relu_at(ip, cs, cb + j, b[j]) : 0.f;
         }
     }
 #pragma unroll

@@ -489,7 +489,7 @@ int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, 
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
     const bool cl = g_conv_cl == 2 || (g_conv_cl == 1 && bn && K >= 7);
     const BnIn bi = ibn ? *ibn : BnIn{};
-    const int ipo = C::LDS_BYTES, ilds = C::LDS_BYTES + 8 * cin32;   // IBN: [2][cin32] affine map
+    const int ipo = C::LDS_BYTES, ilds = C::LDS_BYTES + 16 * cin32;   // IBN: [4][cin32] parameters
     if (x && bn && cl)
         hipLaunchKernelGGL((k_conv_bf16<K, NT, true, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
                            cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo, bi, 0);

@@ -319,16 +319,14 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
                 const float* p0 = F + cur.off + (in ? i0 - cur.lo : 0) * g.Cin;
                 const float* p1 = F + cur.off + (in ? i1 - cur.lo : 0) * g.Cin;
                 bf16x8 v;
-                float sc[8], sh[8];
-                if constexpr (IBN) bn_in_n<8>(ip, cin16, cb, sc, sh);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
                     float a = p0[c];
                     float q = g.up ? p1[c] : 0.f;
                     if constexpr (IBN) {
-                        a = bn_relu_val(a, sc[j], sh[j]);
-                        q = g.up ? bn_relu_val(q, sc[j], sh[j]) : 0.f;
+                        a = bn_relu_at(ip, cin16, cb + j, a);
+                        q = g.up ? bn_relu_at(ip, cin16, cb + j, q) : 0.f;
                     }
                     v[j] = (__bf16)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
                 }
@@ -433,9 +431,9 @@ static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin,
     const bool wide = flat_ok && (g_conv_kern & 8) && cdiv(Cout, 16) <= 2 &&
                       fw_floats <= (int64_t)4 * CDW_UF_WIDE * 256 && rps >= 256;
     const size_t lds_wide = (size_t)(256 * dstride + (256 + KMAXB + 8) * xstride) * 2 + (size_t)fw_floats * 4 + 64;
-    // IBN: the input BatchNorm's affine map after each kernel's LDS ([2][ceil16(Cin)] floats)
+    // IBN: the input BatchNorm's parameters after each kernel's LDS ([4][ceil16(Cin)] floats)
     const BnIn bi = ibn ? *ibn : BnIn{};
-    const int ib = ibn ? 8 * (16 * cdiv(Cin, 16)) : 0;
+    const int ib = ibn ? 16 * (16 * cdiv(Cin, 16)) : 0;
     const int ipo_w = ((int)lds_wide + 15) & ~15, ipo_f = ((int)lds_flat + 15) & ~15, ipo_d = ((int)lds + 15) & ~15;
 #define VT_DWB_ONE(IB)                                                                                          \
     if (wide && nwv == 8)                                                                                       \

@@ -110,16 +110,14 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
             const float* p0 = F + off + (in ? i0 - lo : 0) * g.Cin;
             const float* p1 = F + off + (in ? i1 - lo : 0) * g.Cin;
             bf16x8 v;
-            float sc[8], sh[8];
-            if constexpr (IBN) bn_in_n<8>(ip, cin32, cb, sc, sh);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
                 float a = p0[c];
                 float q = g.up ? p1[c] : 0.f;
                 if constexpr (IBN) {
-                    a = bn_relu_val(a, sc[j], sh[j]);
-                    q = g.up ? bn_relu_val(q, sc[j], sh[j]) : 0.f;
+                    a = bn_relu_at(ip, cin32, cb + j, a);
+                    q = g.up ? bn_relu_at(ip, cin32, cb + j, q) : 0.f;
                 }
                 // conv.h src_vec's values
                 v[j] = (__bf16)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
@@ -248,8 +246,8 @@ int cfw_nt(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, fl
     const int rest = fbytes > C::WBYTES ? fbytes : C::WBYTES;
     int lds = nch * C::WIN * RS * 2 + rest;
     if (lds < 8 * C::TC * 4) lds = 8 * C::TC * 4;
-    const int ipo = (lds + 15) & ~15;   // the input BatchNorm's affine map (IBN): [2][32 nch] floats
-    if (ibn) lds = ipo + 2 * 32 * nch * 4;
+    const int ipo = (lds + 15) & ~15;   // the input BatchNorm's parameters (IBN): [4][32 nch] floats
+    if (ibn) lds = ipo + 4 * 32 * nch * 4;
     if (lds > 160 * 1024) return VT_ERR_ARG;
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
     const int64_t total = (int64_t)g.B * g.L_in * g.Cin;

@@ -528,8 +528,7 @@ __global__ void k_bn_apply(const float* __restrict__ x, int64_t M, int C, const 
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= M * C) return;
     const int c = (int)(i % C);
-    const float2 a = bn_affine(mean[c], rstd[c], gamma[c], beta[c]);
-    y[i] = bn_fwd_val(x[i], a.x, a.y, act);
+    y[i] = bn_fwd_val(x[i], mean[c], rstd[c], gamma[c], beta[c], act);
 }
 
 // eval-mode BatchNorm: running statistics
@@ -585,8 +584,8 @@ __global__ __launch_bounds__(NT) void k_bn_apply4(const float* __restrict__ x, i
                                                   const float* __restrict__ mean, const float* __restrict__ rstd,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
                                                   float* __restrict__ y) {
-    __shared__ float2 p[BNV_C];   // bnbwd.h bn_affine: (scale, shift)
-    for (int c = threadIdx.x; c < C; c += NT) p[c] = bn_affine(mean[c], rstd[c], gamma[c], beta[c]);
+    __shared__ float4 p[BNV_C];   // (mean, rstd, gamma, beta) per channel
+    for (int c = threadIdx.x; c < C; c += NT) p[c] = make_float4(mean[c], rstd[c], gamma[c], beta[c]);
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * (NT * 4 * BNV_V);
     const int step = (NT * 4) % C;
@@ -602,10 +601,16 @@ __global__ __launch_bounds__(NT) void k_bn_apply4(const float* __restrict__ x, i
             const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
             float o[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = bn_fwd_val(xs[e], p[ce[e]].x, p[ce[e]].y, ACT);
+            for (int e = 0; e < 4; ++e) {
+                const float4 q = p[ce[e]];
+                o[e] = bn_fwd_val(xs[e], q.x, q.y, q.z, q.w, ACT);
+            }
             *(float4*)(y + j) = make_float4(o[0], o[1], o[2], o[3]);
         } else {
-            for (int e = 0; e < (int)(n - j); ++e) y[j + e] = bn_fwd_val(x[j + e], p[ce[e]].x, p[ce[e]].y, ACT);
+            for (int e = 0; e < (int)(n - j); ++e) {
+                const float4 q = p[ce[e]];
+                y[j + e] = bn_fwd_val(x[j + e], q.x, q.y, q.z, q.w, ACT);
+            }
         }
     }
 }

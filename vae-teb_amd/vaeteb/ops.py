@@ -817,8 +817,6 @@ class SyncConvBNActF(torch.autograd.Function):
         if pw.out[0] is not None:
             ws1 = WS.get(WS_LINEAR, x.device, 1)
             fn = "vt_conv1d_bwd_weight_bf16" if bf16 else "vt_conv1d_direct_bwd_weight"
-            if inb:   # a folded input is the previous block's output: it always needs its gradient
-                raise RuntimeError("conv-stack fold: the block input's gradient is required")
             call(fn, ptr(gconv), ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc, ptr(ws1), ws1.numel(),
                  _st())
         gw, = pw.result()
