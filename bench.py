@@ -637,7 +637,8 @@ def main():
                      "algorithmic_bytes": round(k_bytes),
                      "algorithmic_bytes_def": "compulsory: the launch's analytic-signal slots read once + pair "
                                               "features written (SURVEY.md §8(d))",
-                     "limiter": "VALU / LDS latency, not HBM (DESIGN.md §5: 0.74k VALU per wave, 49 % SQ_WAIT_ANY)",
+                     "limiter": "issue stalls and waits, not HBM (profiles/r05/pmc_sq.json: of the wave cycles "
+                                "0.46 issue-stall, 0.33 waitcnt / barrier, 0.22 issuing, 0.13 VALU; DESIGN.md §5)",
                      "launches_per_step": k_n / (2 if fe_timed_in != "timed region" else args.steps),
                      "timed_in": fe_timed_in},
         # SURVEY.md §8(d)'s step-level roofline: samples/s x algorithmic bytes per sample / (GPUs x 8 TB/s)

@@ -68,7 +68,8 @@ def _worker(rank, world, port, q):
     tr._update()
     tr.step(batch, eps=eps)
     torch.cuda.synchronize()
-    q.put((rank, g_local, g_red, tr.state.p.cpu(), fired, len(tr.buckets.buckets)))
+    # numpy, not tensors: shared-memory tensor handles can outlive a worker that exits first
+    q.put((rank, g_local.numpy(), g_red.numpy(), tr.state.p.cpu().numpy(), fired, len(tr.buckets.buckets)))
     dist.destroy_process_group()
 
 
@@ -86,6 +87,7 @@ def test_bucketed_allreduce_waits_for_side_stream_gradients():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    out = [(o[0], torch.from_numpy(o[1]), torch.from_numpy(o[2]), torch.from_numpy(o[3]), o[4], o[5]) for o in out]
     expect = out[0][1] + out[1][1]
     assert not torch.equal(out[0][1], out[1][1])          # the ranks' local gradients differ
     for rank in range(world):
