@@ -18,8 +18,8 @@
 //                workgroup per group of samples, 8 waves each owning up to 20
 //                (16 o x 16 i x tap) tiles, rows 4 at a time from LDS; slabs
 //                summed in fixed order (k_sum_splits).
-//  k_attn_fwd    softmax(Q K^T) V per (sample, head, 64 queries): K / V of the
-//                head in LDS, S^T = K Q^T in registers (so the column softmax
+//  k_attn_fwd    softmax(Q K^T) V per (sample, head), 8 waves over the 16-query
+//                tiles: K / V of the head staged in LDS once, S^T = K Q^T in registers (so the column softmax
 //                is lane-local plus two shuffles and P^T is already the B
 //                operand of O^T = V^T P^T: no LDS round trip for P).
 //  k_attn_bwd    one workgroup per (sample, head), a wave per 64 keys, query
@@ -612,6 +612,123 @@ __global__ void k_maxpool3_bwd(const float* __restrict__ dY, const float* __rest
     }
 }
 
+// channel-vectorised forms (C % 4 == 0): a thread owns 4 channels of MP_TR consecutive steps of
+// one sequence, so each X / dY row is read once per run instead of three (fwd) / nine (bwd)
+// times, with 32-bit index math.  Same comparisons and the same s-1, s, s+1 summation order as
+// the scalar kernels above, hence bit-identical results.
+constexpr int MP_TR = 4;
+
+__device__ __forceinline__ float mp_max3(float a, float b, float c, bool ha, bool hc) {
+    float m = ha ? a : -INFINITY;
+    m = (b > m || !ha) ? b : m;
+    if (hc) m = c > m ? c : m;
+    return m;
+}
+
+__device__ __forceinline__ int mp_arg3(float a, float b, float c, bool ha, bool hc) {
+    int best = 0;
+    float m;
+    if (ha) {
+        m = a;
+        best = -1;
+        if (b > m) { m = b; best = 0; }
+    } else {
+        m = b;
+    }
+    if (hc && c > m) best = 1;
+    return best;
+}
+
+__global__ __launch_bounds__(256) void k_maxpool3_fwd4(const float4* __restrict__ X, int B, int L, int C4,
+                                                       float4* __restrict__ Y) {
+    const int nrun = (L + MP_TR - 1) / MP_TR;
+    const int n = B * nrun * C4;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int c = i % C4, r = i / C4;
+        const int t0 = (r % nrun) * MP_TR, b = r / nrun;
+        const float4* xb = X + (int64_t)b * L * C4 + c;
+        float4* yb = Y + (int64_t)b * L * C4 + c;
+        float4 v[MP_TR + 2];
+#pragma unroll
+        for (int j = 0; j < MP_TR + 2; ++j) {
+            const int t = t0 - 1 + j;
+            v[j] = (t >= 0 && t < L) ? xb[(int64_t)t * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < MP_TR; ++j) {
+            const int t = t0 + j;
+            if (t >= L) break;
+            const bool ha = t > 0, hc = t + 1 < L;
+            float4 m;
+            m.x = mp_max3(v[j].x, v[j + 1].x, v[j + 2].x, ha, hc);
+            m.y = mp_max3(v[j].y, v[j + 1].y, v[j + 2].y, ha, hc);
+            m.z = mp_max3(v[j].z, v[j + 1].z, v[j + 2].z, ha, hc);
+            m.w = mp_max3(v[j].w, v[j + 1].w, v[j + 2].w, ha, hc);
+            yb[(int64_t)t * C4] = m;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_maxpool3_bwd4(const float4* __restrict__ dY, const float4* __restrict__ X,
+                                                       int B, int L, int C4, float4* __restrict__ dX,
+                                                       int accumulate) {
+    const int nrun = (L + MP_TR - 1) / MP_TR;
+    const int n = B * nrun * C4;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int c = i % C4, r = i / C4;
+        const int t0 = (r % nrun) * MP_TR, b = r / nrun;
+        const int64_t base = (int64_t)b * L * C4 + c;
+        // X rows t0-2 .. t0+MP_TR+1, dY rows t0-1 .. t0+MP_TR
+        float4 v[MP_TR + 4], g[MP_TR + 2];
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < MP_TR + 4; ++j) {
+            const int t = t0 - 2 + j;
+            v[j] = (t >= 0 && t < L) ? X[base + (int64_t)t * C4] : z;
+        }
+#pragma unroll
+        for (int j = 0; j < MP_TR + 2; ++j) {
+            const int t = t0 - 1 + j;
+            g[j] = (t >= 0 && t < L) ? dY[base + (int64_t)t * C4] : z;
+        }
+        // first-maximum position of the windows centred at t0-1 .. t0+MP_TR, 4 channels packed
+        int a[MP_TR + 2][4];
+#pragma unroll
+        for (int j = 0; j < MP_TR + 2; ++j) {
+            const int w = t0 - 1 + j;
+            const bool ha = w > 0, hc = w + 1 < L;
+            a[j][0] = mp_arg3(v[j].x, v[j + 1].x, v[j + 2].x, ha, hc);
+            a[j][1] = mp_arg3(v[j].y, v[j + 1].y, v[j + 2].y, ha, hc);
+            a[j][2] = mp_arg3(v[j].z, v[j + 1].z, v[j + 2].z, ha, hc);
+            a[j][3] = mp_arg3(v[j].w, v[j + 1].w, v[j + 2].w, ha, hc);
+        }
+#pragma unroll
+        for (int j = 1; j <= MP_TR; ++j) {
+            const int s = t0 - 1 + j;
+            if (s >= L) break;
+            const float* gp = reinterpret_cast<const float*>(&g[j - 1]);
+            const float* g0 = reinterpret_cast<const float*>(&g[j]);
+            const float* gn = reinterpret_cast<const float*>(&g[j + 1]);
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float acc = 0.f;
+                if (s > 0 && a[j - 1][q] == 1) acc += gp[q];
+                if (a[j][q] == 0) acc += g0[q];
+                if (s + 1 < L && a[j + 1][q] == -1) acc += gn[q];
+                o[q] = acc;
+            }
+            float4* dp = dX + base + (int64_t)s * C4;
+            float4 r4 = make_float4(o[0], o[1], o[2], o[3]);
+            if (accumulate) {
+                const float4 d = *dp;
+                r4 = make_float4(d.x + r4.x, d.y + r4.y, d.z + r4.z, d.w + r4.w);
+            }
+            *dp = r4;
+        }
+    }
+}
+
 __global__ void k_add_act(const float* __restrict__ A, const float* __restrict__ Bm, int64_t n, int act,
                           float* __restrict__ Y) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -653,6 +770,28 @@ __global__ void k_dropout(const float* __restrict__ X, int64_t n, int C, int L, 
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t m = L > 0 ? (uint64_t)((i / LC) * C + i % C) : (uint64_t)i;
         Y[i] = mix_hash(seed, m) >= th ? X[i] * sc : 0.f;
+    }
+}
+
+// C % 4 == 0: four channels of one row per thread (one index split per float4, 16-byte accesses);
+// the same per-element mask index and hash as k_dropout.
+__global__ void k_dropout4(const float4* __restrict__ X, int64_t n4, int C, int L, float p, uint64_t seed,
+                           const uint64_t* __restrict__ soff, float4* __restrict__ Y) {
+    seed = eff_seed(seed, soff);
+    const uint32_t th = drop_threshold(p);
+    const float sc = 1.f / (1.f - p);
+    const int64_t LC = (int64_t)L * C;
+    for (int64_t i4 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i4 < n4;
+         i4 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = 4 * i4;
+        const uint64_t m = L > 0 ? (uint64_t)((i / LC) * C + i % C) : (uint64_t)i;
+        const float4 x = X[i4];
+        float4 y;
+        y.x = mix_hash(seed, m) >= th ? x.x * sc : 0.f;
+        y.y = mix_hash(seed, m + 1) >= th ? x.y * sc : 0.f;
+        y.z = mix_hash(seed, m + 2) >= th ? x.z * sc : 0.f;
+        y.w = mix_hash(seed, m + 3) >= th ? x.w * sc : 0.f;
+        Y[i4] = y;
     }
 }
 
@@ -716,93 +855,96 @@ constexpr int DH = 32;            // head dim (embed 128 / 4 heads)
 constexpr int AKS = DH + 1;       // LDS row stride of K / V
 constexpr int AMAXKT = 16;        // S <= 256
 
-__global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ qkv, int S, int H, float scale, float p,
-                                                  uint64_t seed, const uint64_t* __restrict__ soff,
-                                                  float* __restrict__ out, float* __restrict__ lse) {
+constexpr int AFW = 8;            // waves per forward workgroup (query tiles wv, wv + AFW)
+
+__global__ __launch_bounds__(64 * AFW, 4) void k_attn_fwd(const float* __restrict__ qkv, int S, int H, float scale,
+                                                       float p, uint64_t seed, const uint64_t* __restrict__ soff,
+                                                       float* __restrict__ out, float* __restrict__ lse) {
     seed = eff_seed(seed, soff);
     __shared__ float Ks[256 * AKS];
     __shared__ float Vs[256 * AKS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
-    const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int E = H * DH, E3 = 3 * E;
     const float* base = qkv + (int64_t)b * S * E3 + h * DH;
-    for (int i = tid; i < S * DH; i += 256) {
+    for (int i = tid; i < S * DH; i += 64 * AFW) {
         const int r = i / DH, d = i - r * DH;
         Ks[r * AKS + d] = base[(int64_t)r * E3 + E + d];
         Vs[r * AKS + d] = base[(int64_t)r * E3 + 2 * E + d];
     }
     __syncthreads();
-    const int q0 = blockIdx.x * 64 + 16 * wv;
-    if (q0 >= S) return;
     const int nkt = S >> 4;
-    // B operand Q^T[dim = 4 s + lc][query = lr]
-    float qf[8];
+    for (int qt = wv; qt < nkt; qt += AFW) {
+        const int q0 = 16 * qt;
+        // B operand Q^T[dim = 4 s + lc][query = lr]
+        float qf[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) qf[s] = base[(int64_t)(q0 + lr) * E3 + 4 * s + lc];
-    f32x4 st[AMAXKT];
+        for (int s = 0; s < 8; ++s) qf[s] = base[(int64_t)(q0 + lr) * E3 + 4 * s + lc];
+        f32x4 st[AMAXKT];
 #pragma unroll
-    for (int kt = 0; kt < AMAXKT; ++kt) {
-        st[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (kt < nkt) {
+        for (int kt = 0; kt < AMAXKT; ++kt) {
+            st[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (kt < nkt) {
 #pragma unroll
-            for (int s = 0; s < 8; ++s) st[kt] = mma(Ks[(16 * kt + lr) * AKS + 4 * s + lc], qf[s], st[kt]);
+                for (int s = 0; s < 8; ++s) st[kt] = mma(Ks[(16 * kt + lr) * AKS + 4 * s + lc], qf[s], st[kt]);
+            }
         }
-    }
-    // column softmax: S^T[key = 16 kt + 4 lc + r][query = lr]
-    float m = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < AMAXKT; ++kt)
-        if (kt < nkt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) m = fmaxf(m, st[kt][r] * scale);
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < AMAXKT; ++kt)
-        if (kt < nkt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float e = expf(st[kt][r] * scale - m);
-                st[kt][r] = e;
-                l += e;
-            }
-    l += __shfl_xor(l, 16);
-    l += __shfl_xor(l, 32);
-    const float inv = 1.f / l;
-    const int q = q0 + lr;
-    if (lc == 0) lse[(int64_t)bh * S + q] = m + logf(l);
-    const uint32_t th = drop_threshold(p);
-    const float dsc = p > 0.f ? 1.f / (1.f - p) : 1.f;
-#pragma unroll
-    for (int kt = 0; kt < AMAXKT; ++kt)
-        if (kt < nkt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float pv = st[kt][r] * inv;
-                if (p > 0.f) {
-                    const uint64_t id = ((uint64_t)bh * S + q) * S + 16 * kt + 4 * lc + r;
-                    pv = mix_hash(seed, id) >= th ? pv * dsc : 0.f;
-                }
-                st[kt][r] = pv;
-            }
-    // O^T[dim][query] = sum_key V^T[dim][key] P^T[key][query]; step (kt, j) covers keys 16 kt + 4 g + j
-    float* ob = out + ((int64_t)b * S + q) * E + h * DH;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-        f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+        // column softmax: S^T[key = 16 kt + 4 lc + r][query = lr]
+        float m = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < AMAXKT; ++kt)
             if (kt < nkt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) o = mma(Vs[(16 * kt + 4 * lc + j) * AKS + 16 * dt + lr], st[kt][j], o);
-        // D: O^T[dim = 16 dt + 4 lc + r][query = lr]
+                for (int r = 0; r < 4; ++r) m = fmaxf(m, st[kt][r] * scale);
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        float l = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ob[16 * dt + 4 * lc + r] = o[r];
+        for (int kt = 0; kt < AMAXKT; ++kt)
+            if (kt < nkt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float e = expf(st[kt][r] * scale - m);
+                    st[kt][r] = e;
+                    l += e;
+                }
+        l += __shfl_xor(l, 16);
+        l += __shfl_xor(l, 32);
+        const float inv = 1.f / l;
+        const int q = q0 + lr;
+        if (lc == 0) lse[(int64_t)bh * S + q] = m + logf(l);
+        const uint32_t th = drop_threshold(p);
+        const float dsc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+#pragma unroll
+        for (int kt = 0; kt < AMAXKT; ++kt)
+            if (kt < nkt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float pv = st[kt][r] * inv;
+                    if (p > 0.f) {
+                        const uint64_t id = ((uint64_t)bh * S + q) * S + 16 * kt + 4 * lc + r;
+                        pv = mix_hash(seed, id) >= th ? pv * dsc : 0.f;
+                    }
+                    st[kt][r] = pv;
+                }
+        // O^T[dim][query] = sum_key V^T[dim][key] P^T[key][query]; step (kt, j) covers keys 16 kt + 4 g + j
+        float* ob = out + ((int64_t)b * S + q) * E + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kt = 0; kt < AMAXKT; ++kt)
+                if (kt < nkt)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) o = mma(Vs[(16 * kt + 4 * lc + j) * AKS + 16 * dt + lr], st[kt][j], o);
+            // D: O^T[dim = 16 dt + 4 lc + r][query = lr]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ob[16 * dt + 4 * lc + r] = o[r];
+        }
     }
 }
 
-__global__ __launch_bounds__(256) void k_attn_bwd(const float* __restrict__ qkv, const float* __restrict__ O,
+__global__ __launch_bounds__(256, 2) void k_attn_bwd(const float* __restrict__ qkv, const float* __restrict__ O,
                                                   const float* __restrict__ dO, const float* __restrict__ lse, int S,
                                                   int H, float scale, float p, uint64_t seed,
                                                   const uint64_t* __restrict__ soff, float* __restrict__ dqkv) {
@@ -1093,7 +1235,13 @@ int vt_zconv_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int B
 int vt_maxpool3_fwd(const float* X, int B, int L, int C, float* Y, void* stream) {
     VT_CHECK_ARG(B > 0 && L > 0 && C > 0, "vt_maxpool3_fwd: shape");
     const int64_t n = (int64_t)B * L * C;
-    hipLaunchKernelGGL(k_maxpool3_fwd, dim3(ew_blocks(n)), dim3(256), 0, S(stream), X, B, L, C, Y);
+    if (C % 4 == 0 && n < (int64_t)1 << 31) {
+        const int64_t nv = (int64_t)B * ((L + MP_TR - 1) / MP_TR) * (C / 4);
+        hipLaunchKernelGGL(k_maxpool3_fwd4, dim3(ew_blocks(nv)), dim3(256), 0, S(stream),
+                           reinterpret_cast<const float4*>(X), B, L, C / 4, reinterpret_cast<float4*>(Y));
+    } else {
+        hipLaunchKernelGGL(k_maxpool3_fwd, dim3(ew_blocks(n)), dim3(256), 0, S(stream), X, B, L, C, Y);
+    }
     VT_LAUNCH_CHECK("vt_maxpool3_fwd");
     return VT_OK;
 }
@@ -1101,7 +1249,15 @@ int vt_maxpool3_fwd(const float* X, int B, int L, int C, float* Y, void* stream)
 int vt_maxpool3_bwd(const float* dY, const float* X, int B, int L, int C, float* dX, int accumulate, void* stream) {
     VT_CHECK_ARG(B > 0 && L > 0 && C > 0, "vt_maxpool3_bwd: shape");
     const int64_t n = (int64_t)B * L * C;
-    hipLaunchKernelGGL(k_maxpool3_bwd, dim3(ew_blocks(n)), dim3(256), 0, S(stream), dY, X, B, L, C, dX, accumulate);
+    if (C % 4 == 0 && n < (int64_t)1 << 31) {
+        const int64_t nv = (int64_t)B * ((L + MP_TR - 1) / MP_TR) * (C / 4);
+        hipLaunchKernelGGL(k_maxpool3_bwd4, dim3(ew_blocks(nv)), dim3(256), 0, S(stream),
+                           reinterpret_cast<const float4*>(dY), reinterpret_cast<const float4*>(X), B, L, C / 4,
+                           reinterpret_cast<float4*>(dX), accumulate);
+    } else {
+        hipLaunchKernelGGL(k_maxpool3_bwd, dim3(ew_blocks(n)), dim3(256), 0, S(stream), dY, X, B, L, C, dX,
+                           accumulate);
+    }
     VT_LAUNCH_CHECK("vt_maxpool3_bwd");
     return VT_OK;
 }
@@ -1129,8 +1285,14 @@ int vt_dropout_seed_advance(void* offset, void* stream) {
 int vt_dropout_apply(const float* X, int64_t n, int C, int L, float p, int64_t seed, const void* seed_offset, float* Y,
                      void* stream) {
     VT_CHECK_ARG(n > 0 && C > 0 && L >= 0 && p >= 0.f && p < 1.f, "vt_dropout_apply: args (0 <= p < 1)");
-    hipLaunchKernelGGL(k_dropout, dim3(ew_blocks(n)), dim3(256), 0, S(stream), X, n, C, L, p, (uint64_t)seed,
-                       seed_off(seed_offset, p), Y);
+    if (C % 4 == 0 && n % 4 == 0 && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15) == 0) {
+        hipLaunchKernelGGL(k_dropout4, dim3(ew_blocks(n / 4)), dim3(256), 0, S(stream),
+                           reinterpret_cast<const float4*>(X), n / 4, C, L, p, (uint64_t)seed,
+                           seed_off(seed_offset, p), reinterpret_cast<float4*>(Y));
+    } else {
+        hipLaunchKernelGGL(k_dropout, dim3(ew_blocks(n)), dim3(256), 0, S(stream), X, n, C, L, p, (uint64_t)seed,
+                           seed_off(seed_offset, p), Y);
+    }
     VT_LAUNCH_CHECK("vt_dropout_apply");
     return VT_OK;
 }
@@ -1154,7 +1316,7 @@ int vt_attn_fwd(const float* qkv, int B, int S_, int H, float scale, float p, in
                 float* out, float* lse, void* stream) {
     VT_CHECK_ARG(B > 0 && H > 0 && S_ > 0 && S_ % 16 == 0 && S_ <= 256 && p >= 0.f && p < 1.f,
                  "vt_attn_fwd: S multiple of 16 <= 256, 0 <= p < 1");
-    hipLaunchKernelGGL(k_attn_fwd, dim3(cdiv(S_, 64), B * H), dim3(256), 0, S(stream), qkv, S_, H, scale, p,
+    hipLaunchKernelGGL(k_attn_fwd, dim3(B * H), dim3(64 * AFW), 0, S(stream), qkv, S_, H, scale, p,
                        (uint64_t)seed, seed_off(seed_offset, p), out, lse);
     VT_LAUNCH_CHECK("vt_attn_fwd");
     return VT_OK;
