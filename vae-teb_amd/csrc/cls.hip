@@ -657,7 +657,7 @@ __global__ __launch_bounds__(256) void k_maxpool3_fwd4(const float4* __restrict_
 #pragma unroll
         for (int j = 0; j < MP_TR; ++j) {
             const int t = t0 + j;
-            if (t >= L) break;
+            if (t >= L) continue;
             const bool ha = t > 0, hc = t + 1 < L;
             float4 m;
             m.x = mp_max3(v[j].x, v[j + 1].x, v[j + 2].x, ha, hc);
@@ -667,6 +667,10 @@ __global__ __launch_bounds__(256) void k_maxpool3_fwd4(const float4* __restrict_
             yb[(int64_t)t * C4] = m;
         }
     }
+}
+
+__device__ __forceinline__ float f4c(const float4& v, int q) {   // q: a compile-time constant
+    return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
 }
 
 __global__ __launch_bounds__(256) void k_maxpool3_bwd4(const float4* __restrict__ dY, const float4* __restrict__ X,
@@ -684,12 +688,14 @@ __global__ __launch_bounds__(256) void k_maxpool3_bwd4(const float4* __restrict_
 #pragma unroll
         for (int j = 0; j < MP_TR + 4; ++j) {
             const int t = t0 - 2 + j;
-            v[j] = (t >= 0 && t < L) ? X[base + (int64_t)t * C4] : z;
+            v[j] = z;
+            if (t >= 0 && t < L) v[j] = X[base + (int64_t)t * C4];
         }
 #pragma unroll
         for (int j = 0; j < MP_TR + 2; ++j) {
             const int t = t0 - 1 + j;
-            g[j] = (t >= 0 && t < L) ? dY[base + (int64_t)t * C4] : z;
+            g[j] = z;
+            if (t >= 0 && t < L) g[j] = dY[base + (int64_t)t * C4];
         }
         // first-maximum position of the windows centred at t0-1 .. t0+MP_TR, 4 channels packed
         int a[MP_TR + 2][4];
@@ -705,17 +711,14 @@ __global__ __launch_bounds__(256) void k_maxpool3_bwd4(const float4* __restrict_
 #pragma unroll
         for (int j = 1; j <= MP_TR; ++j) {
             const int s = t0 - 1 + j;
-            if (s >= L) break;
-            const float* gp = reinterpret_cast<const float*>(&g[j - 1]);
-            const float* g0 = reinterpret_cast<const float*>(&g[j]);
-            const float* gn = reinterpret_cast<const float*>(&g[j + 1]);
+            if (s >= L) continue;
             float o[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float acc = 0.f;
-                if (s > 0 && a[j - 1][q] == 1) acc += gp[q];
-                if (a[j][q] == 0) acc += g0[q];
-                if (s + 1 < L && a[j + 1][q] == -1) acc += gn[q];
+                if (s > 0 && a[j - 1][q] == 1) acc += f4c(g[j - 1], q);
+                if (a[j][q] == 0) acc += f4c(g[j], q);
+                if (s + 1 < L && a[j + 1][q] == -1) acc += f4c(g[j + 1], q);
                 o[q] = acc;
             }
             float4* dp = dX + base + (int64_t)s * C4;
