@@ -350,21 +350,53 @@ __global__ __launch_bounds__(NT) void k_ln_bwd16(const float* __restrict__ dy, c
     }
 }
 
-// out0[c] / out1[c - split] (+)= sum_b part[b][c], c < n: a wave per column
-// (lanes stride over the partial rows, then a fixed shuffle tree), 4 per workgroup
+// out0[c] / out1[c - split] (+)= sum_b part[b][c], c < n.  A workgroup owns 16 columns; thread
+// (l0, cc) forms the lane partials s_l = sum_k part[l + 64 k][c0 + cc], l = l0 + 16 q, k in order
+// (16 adjacent columns of a partial row are one 64-B segment — a wave per column striding the
+// rows with its lanes read 4 B per row, up to 132 us per launch at 2 C = 512), then a wave per
+// column applies wave_sum's shuffle tree to the 64 s_l (round 5: the same bits as before)
+constexpr int CR_C = 16;
 __global__ __launch_bounds__(NT) void k_colred16(const float* __restrict__ part, int blocks, int n,
-                                                 float* __restrict__ out0, float* __restrict__ out1, int split,
-                                                 int accumulate) {
-    const int lane = threadIdx.x & 63;
-    const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
-    if (c >= n) return;
-    float a = 0.f;
-#pragma unroll 8
-    for (int b = lane; b < blocks; b += 64) a += part[(int64_t)b * n + c];   // 8 loads in flight, same order
-    a = wave_sum(a);
-    if (lane != 0) return;
-    float* dst = c < split ? out0 + c : out1 + (c - split);
-    *dst = accumulate ? *dst + a : a;
+                                                  float* __restrict__ out0, float* __restrict__ out1, int split,
+                                                  int accumulate) {
+    static_assert(NT == 256, "16 columns x 16 lane groups");
+    __shared__ float sl[CR_C][64 + 1];
+    const int c0 = blockIdx.x * CR_C, cc = threadIdx.x & (CR_C - 1), l0 = threadIdx.x >> 4;
+    const int c = c0 + cc;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < n) {
+        int k = 0;
+        for (; 64 * (k + 4) <= blocks; k += 4) {   // 16 loads in flight, each a[q] in row order
+            float v[4][4];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[kk][q] = part[(int64_t)(l0 + 16 * q + 64 * (k + kk)) * n + c];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] += v[kk][q];
+        }
+        for (; 64 * k < blocks; ++k) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int b = l0 + 16 * q + 64 * k;
+                if (b < blocks) a[q] += part[(int64_t)b * n + c];
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sl[cc][l0 + 16 * q] = a[q];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int j = w; j < CR_C; j += NT / 64) {
+        if (c0 + j >= n) break;
+        const float v = wave_sum(sl[j][lane]);
+        if (lane == 0) {
+            float* dst = c0 + j < split ? out0 + c0 + j : out1 + (c0 + j - split);
+            *dst = accumulate ? *dst + v : v;
+        }
+    }
 }
 
 // out[c] (+)= sum_b part[b][c] for c < n: one workgroup per column, threads
@@ -1023,8 +1055,8 @@ int vt_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, int6
         else if (C <= 128) VT_LNB(8);
         else VT_LNB(16);
 #undef VT_LNB
-        hipLaunchKernelGGL(k_colred16, dim3((unsigned)((2 * C + 3) / 4)), dim3(NT), 0, st, ws, (int)blocks, 2 * C,
-                           dgamma, dbeta, C, accumulate_params);
+        hipLaunchKernelGGL(k_colred16, dim3((unsigned)((2 * C + CR_C - 1) / CR_C)), dim3(NT), 0, st, ws, (int)blocks,
+                           2 * C, dgamma, dbeta, C, accumulate_params);
     } else if (C <= 512) {
         int64_t blocks = (R + 63) / 64;
         if (blocks > 1024) blocks = 1024;
