@@ -451,10 +451,11 @@ __global__ __launch_bounds__(DT) void k_zconv_dw(const float* __restrict__ dY, i
 // contraction), both operands read with the gfx950 transposed LDS read (ds_read_b64_tr_b16:
 // 8 rows x 16 channels per lane group), so one MFMA contracts 32 rows of one (16 o x 16 i x
 // tap) tile — the fp32 kernel above needs 8 MFMAs and 16 scalar LDS reads for the same rows.
-// Tiles (o, i, tap) with the tap fastest, 8 waves x <= D16MAXT tiles; per-workgroup slabs
-// summed in fixed order (k_sum_splits).
+// Tiles (o, i, tap) with the tap fastest, D16W waves x <= D16MAXT tiles; per-workgroup slabs
+// summed in fixed order (k_sum_splits).  16 waves of <= 10 tiles (round 5; was 8 x 20 at 256
+// VGPRs + spills, one wave per SIMD pair-issuing): the same tiles and per-tile accumulation order.
 typedef short zv4i16 __attribute__((ext_vector_type(4)));
-constexpr int D16T = 512, D16R = 128, D16MAXT = 20;   // 128-row chunks: half the staging round trips of 64
+constexpr int D16W = 16, D16T = 64 * D16W, D16R = 128, D16MAXT = 10;   // 128-row chunks: half the staging round trips of 64
 constexpr int D16_DS = 136 * D16R;                  // dY image: 128 rows x (<= 128 + 8) channels
 constexpr int D16_XS = (D16R + 40 + 8) * 40;        // window image, K <= 40 at <= 32 channels ...
 constexpr int D16_XS1 = D16R * 136;                 // ... or K 1 at <= 128 channels
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(D16T) void k_zconv16_dw(const float* __restrict__ d
     const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lc = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the tile indices in SGPRs
     const int nIt = Cin >> 4, nT = (Cout >> 4) * nIt * K;
-    const int tpw = (nT + 7) >> 3;
+    const int tpw = (nT + D16W - 1) / D16W;
     const int j0 = wv * tpw;
     int tot[D16MAXT], tit[D16MAXT], tk[D16MAXT];
 #pragma unroll
@@ -1200,7 +1201,7 @@ int vt_zconv16_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int
     VT_CHECK_ARG(zconv_shape_ok(B, L, Cin, Cout, K, pad_left) && ldx >= Cin && ldy >= Cout && !(ldx & 3) &&
                      !(ldy & 3) && !(reinterpret_cast<uintptr_t>(dY) & 15) && !(reinterpret_cast<uintptr_t>(X) & 15),
                  "vt_zconv16_bwd_weight: shape / alignment (16-B rows)");
-    VT_CHECK_ARG(((Cout / 16) * (Cin / 16) * K + 7) / 8 <= D16MAXT, "vt_zconv16_bwd_weight: too many tiles");
+    VT_CHECK_ARG(((Cout / 16) * (Cin / 16) * K + D16W - 1) / D16W <= D16MAXT, "vt_zconv16_bwd_weight: too many tiles");
     // one sample per workgroup up to 256 (the chunks' staging round trips, not the MFMAs, bound
     // a workgroup: 128 slabs took 25-44 us per launch whatever K)
     const int G = zdw_groups(B);
