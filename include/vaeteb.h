@@ -494,6 +494,20 @@ int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const
 int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, int act, float* dx, float* dgamma, float* dbeta,
                      int accumulate_params, float* ws, int64_t ws_floats, void* stream);
+/* vt_batchnorm_fwd / vt_batchnorm_bwd with the Dropout1d that follows the BatchNorm fused in:
+ * the forward writes y = vt_dropout_apply(BN(x)) (same mask index b C + c over L-row samples,
+ * same hash and scale: the values of the two calls), the backward reads dy through the mask
+ * (the values of vt_dropout_apply on dy followed by vt_batchnorm_bwd).  L = 0: element-wise.
+ * replaces: BatchNorm1d + ReLU + Dropout1d of FHRInception / FHRResidual
+ *           (ref/model/inception_time.py:89-117, :152-170) in one pass each way */
+int vt_batchnorm_fwd_dropout(const float* x, int64_t M, int C, const float* gamma, const float* beta, int act,
+                             float eps, float momentum, float* y, float* mean, float* rstd, float* run_mean,
+                             float* run_var, int L, float p, int64_t seed, const void* seed_offset, float* ws,
+                             int64_t ws_floats, void* stream);
+int vt_batchnorm_bwd_dropout(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                             const float* gamma, const float* beta, int act, int L, float p, int64_t seed,
+                             const void* seed_offset, float* dx, float* dgamma, float* dbeta, int accumulate_params,
+                             float* ws, int64_t ws_floats, void* stream);
 /* The column-sum half of vt_batchnorm_bwd (dgamma / dbeta (+)= their sums) with no dx:
  * bnp = [mean | rstd | gamma | beta | dgamma_now | dbeta_now] (6 x C floats) for the bf16
  * conv backward kernels that form dx while staging their operand (*_bf16_bn below). */

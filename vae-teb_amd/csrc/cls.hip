@@ -30,6 +30,7 @@
 
 #include "common.h"
 #include "conv.h"
+#include "dropout.h"
 
 namespace vt {
 
@@ -741,26 +742,6 @@ __global__ void k_add_act(const float* __restrict__ A, const float* __restrict__
     }
 }
 
-__device__ __forceinline__ uint32_t mix_hash(uint64_t seed, uint64_t idx) {
-    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (uint32_t)(z >> 32);
-}
-
-__device__ __forceinline__ uint32_t drop_threshold(float p) {
-    const double t = (double)p * 4294967296.0;
-    return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-}
-
-// Device-side seed offset (the seed_offset argument of the dropout / attention calls): added to every dropout seed, advanced
-// once per training step on the device (vt_dropout_seed_advance), so a captured step replayed
-// by the native executor draws new masks each replay (its host seeds are frozen at capture).
-__device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* __restrict__ soff) {
-    return soff ? seed + soff[0] : seed;
-}
-
 __global__ void k_seed_advance(uint64_t* off) {
     if (threadIdx.x == 0) off[0] += 0xD1B54A32D192ED03ull;
 }
@@ -1271,12 +1252,6 @@ int vt_add_act_fwd(const float* A, const float* Bm, int64_t n, int act, float* Y
     hipLaunchKernelGGL(k_add_act, dim3(ew_blocks(n)), dim3(256), 0, S(stream), A, Bm, n, act, Y);
     VT_LAUNCH_CHECK("vt_add_act_fwd");
     return VT_OK;
-}
-
-// the seed offset is read only when something is dropped (p > 0): a caller without one, or an
-// eval / p = 0 call, passes nothing the kernels would dereference
-static inline const uint64_t* seed_off(const void* off, float p) {
-    return p > 0.f ? reinterpret_cast<const uint64_t*>(off) : nullptr;
 }
 
 int vt_dropout_seed_advance(void* offset, void* stream) {

@@ -15,6 +15,7 @@
 
 #include "bnbwd.h"
 #include "common.h"
+#include "dropout.h"
 
 namespace vt {
 
@@ -647,12 +648,75 @@ __global__ __launch_bounds__(NT) void k_bn_apply4(const float* __restrict__ x, i
     }
 }
 
+// Dropout1d of the BatchNorm backward's incoming gradient (vt_batchnorm_bwd_dropout): the
+// kernels read dy through dmask, i.e. the value cls.hip's k_dropout would have written
+struct DropArg {
+    int L;
+    float p;
+    uint64_t seed;                // the effective seed (eff_seed applied in the kernel)
+    const uint64_t* soff;
+};
+__device__ __forceinline__ float dmask(const DropArg& d, uint64_t seed, uint32_t th, float sc, int64_t i, int C,
+                                       int ch, float g) {
+    const uint64_t m = d.L > 0 ? (uint64_t)((i / ((int64_t)d.L * C)) * C + ch) : (uint64_t)i;
+    return mix_hash(seed, m) >= th ? g * sc : 0.f;
+}
+
+// k_bn_apply4 followed by Dropout1d over (sample, channel) columns of L rows (L = 0: element-wise
+// dropout): each element the value cls.hip's k_dropout writes from the applied output (the same
+// hash of index b C + c, threshold and scale) — one pass over the activations instead of two
 template <int ACT>
+__global__ __launch_bounds__(NT) void k_bn_apply4d(const float* __restrict__ x, int64_t n, int C,
+                                                   const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   float* __restrict__ y, int L, float p, uint64_t seed,
+                                                   const uint64_t* __restrict__ soff) {
+    __shared__ float4 q4[BNV_C];   // (mean, rstd, gamma, beta) per channel
+    for (int c = threadIdx.x; c < C; c += NT) q4[c] = make_float4(mean[c], rstd[c], gamma[c], beta[c]);
+    __syncthreads();
+    seed = eff_seed(seed, soff);
+    const uint32_t th = drop_threshold(p);
+    const float sc = 1.f / (1.f - p);
+    const int64_t LC = (int64_t)L * C;
+    auto drop = [&](int64_t i, int ch, float v) {
+        const uint64_t m = L > 0 ? (uint64_t)((i / LC) * C + ch) : (uint64_t)i;
+        return mix_hash(seed, m) >= th ? v * sc : 0.f;
+    };
+    const int64_t base = (int64_t)blockIdx.x * (NT * 4 * BNV_V);
+    const int step = (NT * 4) % C;
+    int c = (int)((base + 4 * threadIdx.x) % C);
+#pragma unroll
+    for (int v = 0; v < BNV_V; ++v, c = wrapc(c + step, C)) {
+        const int64_t j = base + 4 * (threadIdx.x + NT * v);
+        if (j >= n) break;
+        int ce[4];
+        chan4(c, C, ce);
+        if (j + 4 <= n) {
+            const float4 xv = *(const float4*)(x + j);
+            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float4 q = q4[ce[e]];
+                o[e] = drop(j + e, ce[e], bn_fwd_val(xs[e], q.x, q.y, q.z, q.w, ACT));
+            }
+            *(float4*)(y + j) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (int e = 0; e < (int)(n - j); ++e) {
+                const float4 q = q4[ce[e]];
+                y[j + e] = drop(j + e, ce[e], bn_fwd_val(x[j + e], q.x, q.y, q.z, q.w, ACT));
+            }
+        }
+    }
+}
+
+template <int ACT, bool DROP = false>
 __global__ __launch_bounds__(NT) void k_bn_dx4(const float* __restrict__ dy, const float* __restrict__ x, int64_t n,
                                                int64_t M, int C, const float* __restrict__ mean,
                                                const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                const float* __restrict__ beta, const float* __restrict__ dgamma,
-                                               const float* __restrict__ dbeta, float* __restrict__ dx) {
+                                               const float* __restrict__ dbeta, float* __restrict__ dx,
+                                               DropArg dr = DropArg{}) {
     __shared__ float p[6][BNV_C];
     for (int c = threadIdx.x; c < C; c += NT) {
         p[0][c] = mean[c];
@@ -668,6 +732,10 @@ __global__ __launch_bounds__(NT) void k_bn_dx4(const float* __restrict__ dy, con
     const int step = (NT * 4) % C;
     int c = (int)((base + 4 * threadIdx.x) % C);
     auto one = [&](float xe, float dye, int cc) { return bn_bwd_val(dye, xe, &p[0][0], BNV_C, cc, ACT, inv); };
+    const uint64_t dseed = DROP ? eff_seed(dr.seed, dr.soff) : 0;
+    const uint32_t th = DROP ? drop_threshold(dr.p) : 0u;
+    const float dsc = DROP ? 1.f / (1.f - dr.p) : 1.f;
+    auto gm = [&](int64_t i, int cc, float g) { return DROP ? dmask(dr, dseed, th, dsc, i, C, cc, g) : g; };
 #pragma unroll
     for (int v = 0; v < BNV_V; ++v, c = wrapc(c + step, C)) {
         const int64_t j = base + 4 * (threadIdx.x + NT * v);
@@ -676,10 +744,11 @@ __global__ __launch_bounds__(NT) void k_bn_dx4(const float* __restrict__ dy, con
         chan4(c, C, ce);
         if (j + 4 <= n) {
             const float4 xv = *(const float4*)(x + j), gv = *(const float4*)(dy + j);
-            *(float4*)(dx + j) = make_float4(one(xv.x, gv.x, ce[0]), one(xv.y, gv.y, ce[1]), one(xv.z, gv.z, ce[2]),
-                                             one(xv.w, gv.w, ce[3]));
+            *(float4*)(dx + j) = make_float4(one(xv.x, gm(j, ce[0], gv.x), ce[0]), one(xv.y, gm(j + 1, ce[1], gv.y), ce[1]),
+                                             one(xv.z, gm(j + 2, ce[2], gv.z), ce[2]),
+                                             one(xv.w, gm(j + 3, ce[3], gv.w), ce[3]));
         } else {
-            for (int e = 0; e < (int)(n - j); ++e) dx[j + e] = one(x[j + e], dy[j + e], ce[e]);
+            for (int e = 0; e < (int)(n - j); ++e) dx[j + e] = one(x[j + e], gm(j + e, ce[e], dy[j + e]), ce[e]);
         }
     }
 }
@@ -688,12 +757,12 @@ __global__ __launch_bounds__(NT) void k_bn_dx4(const float* __restrict__ dy, con
 // r0 a multiple of 4: thread tid < T' reads the float4s at flat offsets
 // r0*C + 4 tid + 4T' k, 4T' a multiple of C, so its four channels never change;
 // the per-thread sums are combined in LDS in fixed order.
-template <int KIND, int ACT>
+template <int KIND, int ACT, bool DROP = false>
 __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x, const float* __restrict__ dy,
                                                      int64_t M, int C, int64_t rows_per_block, int Tp,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                     float* __restrict__ part, BnFin fin) {
+                                                     float* __restrict__ part, BnFin fin, DropArg dr = DropArg{}) {
     __shared__ float red0[4 * NT], red1[4 * NT];
     // partials: plain stores for a separate finaliser, agent-coherent for the in-kernel one
     const __amdgpu_buffer_rsrc_t pr = agent_rsrc(part, (int64_t)2 * C * gridDim.x * 4);
@@ -714,6 +783,10 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
     if (tid < Tp) {
         int ce[4];
         chan4((4 * tid) % C, C, ce);
+        const uint64_t dseed = DROP ? eff_seed(dr.seed, dr.soff) : 0;
+        const uint32_t th = DROP ? drop_threshold(dr.p) : 0u;
+        const float dsc = DROP ? 1.f / (1.f - dr.p) : 1.f;
+        auto gm = [&](int64_t i, int cc, float g) { return DROP ? dmask(dr, dseed, th, dsc, i, C, cc, g) : g; };
         float mu[4], rs[4], ga[4], be[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -769,6 +842,14 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
                     xv[u] = *(const float4*)(x + f + 4 * (int64_t)Tp * u);
                     gv[u] = KIND == 2 ? *(const float4*)(dy + f + 4 * (int64_t)Tp * u) : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
+                if constexpr (DROP) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int64_t i0 = f + 4 * (int64_t)Tp * u;
+                        gv[u] = make_float4(gm(i0, ce[0], gv[u].x), gm(i0 + 1, ce[1], gv[u].y),
+                                            gm(i0 + 2, ce[2], gv[u].z), gm(i0 + 3, ce[3], gv[u].w));
+                    }
+                }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     acc4(0, xv[u].x, gv[u].x);
@@ -783,12 +864,15 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
                 const float4 xv = *(const float4*)(x + f);
                 float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (KIND == 2) gv = *(const float4*)(dy + f);
+                if constexpr (DROP)
+                    gv = make_float4(gm(f, ce[0], gv.x), gm(f + 1, ce[1], gv.y), gm(f + 2, ce[2], gv.z),
+                                     gm(f + 3, ce[3], gv.w));
                 accx(0, xv.x, gv.x);
                 accx(1, xv.y, gv.y);
                 accx(2, xv.z, gv.z);
                 accx(3, xv.w, gv.w);
             } else {
-                for (int e = 0; e < (int)(end - f); ++e) accx(e, x[f + e], KIND == 2 ? dy[f + e] : 0.f);
+                for (int e = 0; e < (int)(end - f); ++e) accx(e, x[f + e], KIND == 2 ? gm(f + e, ce[e], dy[f + e]) : 0.f);
             }
         }
     }
@@ -859,29 +943,37 @@ static void bn_apply_vec(const float* x, int64_t M, int C, const float* mean, co
 
 static void bn_dx_vec(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
                       const float* gamma, const float* beta, int act, const float* dgamma, const float* dbeta,
-                      float* dx, hipStream_t st) {
+                      float* dx, hipStream_t st, const DropArg* dr = nullptr) {
     const int64_t n = M * C;
 #define VT_F(A)                                                                                                   \
-    hipLaunchKernelGGL(k_bn_dx4<A>, dim3(bnv_blocks(n)), dim3(NT), 0, st, dy, x, n, M, C, mean, rstd, gamma, beta, \
-                       dgamma, dbeta, dx)
+    if (dr)                                                                                                       \
+        hipLaunchKernelGGL((k_bn_dx4<A, true>), dim3(bnv_blocks(n)), dim3(NT), 0, st, dy, x, n, M, C, mean, rstd,  \
+                           gamma, beta, dgamma, dbeta, dx, *dr);                                                    \
+    else                                                                                                          \
+        hipLaunchKernelGGL((k_bn_dx4<A>), dim3(bnv_blocks(n)), dim3(NT), 0, st, dy, x, n, M, C, mean, rstd, gamma,  \
+                           beta, dgamma, dbeta, dx, DropArg{})
     VT_ACT_SWITCH(act, VT_F)
 #undef VT_F
 }
 
 static void col_partial_vec(int kind, const float* x, const float* dy, int64_t M, int C, int64_t rpb, int blocks,
                             const float* mean, const float* rstd, const float* gamma, const float* beta, int act,
-                            float* part, hipStream_t st, BnFin fin) {
+                            float* part, hipStream_t st, BnFin fin, const DropArg* dr = nullptr) {
     const int Tp = colp_threads(C);
     if (kind == 0) {
         hipLaunchKernelGGL((k_col_partial4<0, ACT_NONE>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean,
-                           rstd, gamma, beta, part, fin);
+                           rstd, gamma, beta, part, fin, DropArg{});
     } else if (kind == 1) {
         hipLaunchKernelGGL((k_col_partial4<1, ACT_NONE>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean,
-                           rstd, gamma, beta, part, fin);
+                           rstd, gamma, beta, part, fin, DropArg{});
     } else {
-#define VT_F(A)                                                                                                       \
-    hipLaunchKernelGGL((k_col_partial4<2, A>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean, rstd, gamma, \
-                       beta, part, fin)
+#define VT_F(A)                                                                                                      \
+    if (dr)                                                                                                          \
+        hipLaunchKernelGGL((k_col_partial4<2, A, true>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean,   \
+                           rstd, gamma, beta, part, fin, *dr);                                                         \
+    else                                                                                                             \
+        hipLaunchKernelGGL((k_col_partial4<2, A>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean, rstd,   \
+                           gamma, beta, part, fin, DropArg{})
         VT_ACT_SWITCH(act, VT_F)
 #undef VT_F
     }
@@ -898,14 +990,14 @@ static BnFin no_fin() {
 // ws), else the separate k_bn_finalize launch
 static void col_partial_fin(int kind, const float* x, const float* dy, int64_t M, int C, int64_t rpb, int blocks,
                             const float* mean, const float* rstd, const float* gamma, const float* beta, int act,
-                            float* ws, hipStream_t st, BnFin f) {
+                            float* ws, hipStream_t st, BnFin f, const DropArg* dr = nullptr) {
     if (C <= 128 && g_bn_fold) {
         const int ng = (blocks + BN_GB - 1) / BN_GB;
         f.gpart = reinterpret_cast<double*>(ws + (((int64_t)2 * C * blocks + 1) & ~(int64_t)1));
         f.slot0 = arrive_slots((unsigned)ng + 1);
-        col_partial_vec(kind, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f);
+        col_partial_vec(kind, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f, dr);
     } else {
-        col_partial_vec(kind, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, no_fin());
+        col_partial_vec(kind, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, no_fin(), dr);
         hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(NT), 0, st, ws, blocks, C, f);
     }
 }
@@ -1128,6 +1220,38 @@ int vt_batchnorm_fwd(const float* x, int64_t M, int C, const float* gamma, const
     return VT_OK;
 }
 
+int vt_batchnorm_fwd_dropout(const float* x, int64_t M, int C, const float* gamma, const float* beta, int act,
+                             float eps, float momentum, float* y, float* mean, float* rstd, float* run_mean,
+                             float* run_var, int L, float p, int64_t seed, const void* seed_offset, float* ws,
+                             int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0 && C <= 256 && L >= 0 && (L == 0 || M % L == 0) && p >= 0.f && p < 1.f,
+                 "vt_batchnorm_fwd_dropout: shape (C <= 256, M a multiple of L) / 0 <= p < 1");
+    int64_t rpb;
+    const int blocks = bn_blocks(M, ws_floats, C, &rpb);
+    VT_CHECK_ARG(blocks >= 1, "vt_batchnorm_fwd_dropout: workspace too small");
+    hipStream_t st = S(stream);
+    BnFin f0 = fin_of(0, M);
+    f0.mean = mean;
+    col_partial_fin(0, x, nullptr, M, C, rpb, blocks, nullptr, nullptr, nullptr, nullptr, 0, ws, st, f0);
+    BnFin f1 = fin_of(1, M);
+    f1.eps = eps;
+    f1.momentum = momentum;
+    f1.mean = mean;
+    f1.rstd = rstd;
+    f1.run_mean = run_mean;
+    f1.run_var = run_var;
+    col_partial_fin(1, x, nullptr, M, C, rpb, blocks, mean, nullptr, nullptr, nullptr, 0, ws, st, f1);
+    const int64_t n = M * C;
+    const uint64_t* so = seed_off(seed_offset, p);
+#define VT_F(A)                                                                                                  \
+    hipLaunchKernelGGL(k_bn_apply4d<A>, dim3(bnv_blocks(n)), dim3(NT), 0, st, x, n, C, mean, rstd, gamma, beta, y, \
+                       L, p, (uint64_t)seed, so)
+    VT_ACT_SWITCH(act, VT_F)
+#undef VT_F
+    VT_LAUNCH_CHECK("vt_batchnorm_fwd_dropout");
+    return VT_OK;
+}
+
 int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, int act, float* dx, float* dgamma, float* dbeta,
                      int accumulate_params, float* ws, int64_t ws_floats, void* stream) {
@@ -1147,6 +1271,33 @@ int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const fl
     hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
                        accumulate_params);
     VT_LAUNCH_CHECK("vt_batchnorm_bwd");
+    return VT_OK;
+}
+
+int vt_batchnorm_bwd_dropout(const float* dy, const float* x, int64_t M, int C, const float* mean, const float* rstd,
+                             const float* gamma, const float* beta, int act, int L, float p, int64_t seed,
+                             const void* seed_offset, float* dx, float* dgamma, float* dbeta, int accumulate_params,
+                             float* ws, int64_t ws_floats, void* stream) {
+    VT_CHECK_ARG(M > 0 && C > 0 && C <= 256 && L >= 0 && (L == 0 || M % L == 0) && p >= 0.f && p < 1.f,
+                 "vt_batchnorm_bwd_dropout: shape (C <= 256, M a multiple of L) / 0 <= p < 1");
+    if (p == 0.f)
+        return vt_batchnorm_bwd(dy, x, M, C, mean, rstd, gamma, beta, act, dx, dgamma, dbeta, accumulate_params, ws,
+                                ws_floats, stream);
+    int64_t rpb;
+    const int blocks = bn_blocks(M, ws_floats - 2 * C, C, &rpb);
+    VT_CHECK_ARG(blocks >= 1, "vt_batchnorm_bwd_dropout: workspace too small");
+    hipStream_t st = S(stream);
+    const DropArg dr{L, p, (uint64_t)seed, seed_off(seed_offset, p)};
+    float* dg_now = ws + (ws_floats - 2 * C);
+    float* db_now = dg_now + C;
+    BnFin f = fin_of(2, M);
+    f.dgamma = dg_now;
+    f.dbeta = db_now;
+    col_partial_fin(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f, &dr);
+    bn_dx_vec(dy, x, M, C, mean, rstd, gamma, beta, act, dg_now, db_now, dx, st, &dr);
+    hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
+                       accumulate_params);
+    VT_LAUNCH_CHECK("vt_batchnorm_bwd_dropout");
     return VT_OK;
 }
 

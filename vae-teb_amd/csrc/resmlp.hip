@@ -40,7 +40,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MAXL = VT_MLP_MAX_LAYERS;
 constexpr int KC = 32;          // reduction rows of W staged per step
 constexpr int FWD_THREADS = 256;  // 4 waves x 16 rows
-constexpr int DW_THREADS = 512;   // 8 waves over (n, k) tile pairs
 
 struct MlpLayer {
     int K, N, ln, act;

@@ -19,6 +19,7 @@ torch.manual_seed makes runs repeatable).
 """
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -40,6 +41,11 @@ def _seed():
     """(host seed, device seed offset or None) of one dropout / attention-dropout op; the op
     keeps the pair for its backward (the same masks)."""
     return int(torch.randint(0, 2 ** 62, (1,)).item()), _SEED_OFF
+
+
+# Dropout1d of the inception blocks fused into their BatchNorm apply / backward passes
+# (vt_batchnorm_{fwd,bwd}_dropout: the same values as the separate dropout launches); 0: separate
+BN_DROP_FUSE = int(os.environ.get("VAETEB_BN_DROP_FUSE", "1"))
 
 
 def _sarg(seed):
@@ -146,10 +152,15 @@ class _InceptionF(torch.autograd.Function):
         mean = torch.empty(C4, device=x.device)
         rstd = torch.empty(C4, device=x.device)
         bws = WS.get(_BN_WS, x.device, 5)
-        call("vt_batchnorm_fwd", ptr(cat), B * L, C4, ptr(g), ptr(b), ACT["relu"], eps, momentum, ptr(y), ptr(mean),
-             ptr(rstd), ptr(run_mean), ptr(run_var), ptr(bws), bws.numel(), st)
-        if p > 0:
-            call("vt_dropout_apply", ptr(y), y.numel(), C4, L, float(p), *_sarg(seed), ptr(y), st)
+        if p > 0 and BN_DROP_FUSE:   # BN + ReLU + Dropout1d in the apply pass (the separate calls' values)
+            call("vt_batchnorm_fwd_dropout", ptr(cat), B * L, C4, ptr(g), ptr(b), ACT["relu"], eps, momentum, ptr(y),
+                 ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), L, float(p), *_sarg(seed), ptr(bws), bws.numel(),
+                 st)
+        else:
+            call("vt_batchnorm_fwd", ptr(cat), B * L, C4, ptr(g), ptr(b), ACT["relu"], eps, momentum, ptr(y),
+                 ptr(mean), ptr(rstd), ptr(run_mean), ptr(run_var), ptr(bws), bws.numel(), st)
+            if p > 0:
+                call("vt_dropout_apply", ptr(y), y.numel(), C4, L, float(p), *_sarg(seed), ptr(y), st)
         ctx.save_for_backward(x, x0, mp, cat, mean, rstd)
         ctx.params = (wb1, ws, wm, wl, wb2, g, b)
         ctx.cfg = (p, seed, bf16)
@@ -165,15 +176,18 @@ class _InceptionF(torch.autograd.Function):
         C4 = 4 * f
         st = _st()
         gy = gy.contiguous()
-        if p > 0:
+        if p > 0 and not BN_DROP_FUSE:
             gd = torch.empty_like(gy)
             call("vt_dropout_apply", ptr(gy), gy.numel(), C4, L, float(p), *_sarg(seed), ptr(gd), st)
             gy = gd
         gcat = torch.empty_like(cat)
         pbn = _ParamGrads([g, b], [True, True])
         bws = WS.get(_BN_WS, x.device, 5)
-        call("vt_batchnorm_bwd", ptr(gy), ptr(cat), B * L, C4, ptr(mean), ptr(rstd), ptr(g), ptr(b), ACT["relu"],
-             ptr(gcat), ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(bws), bws.numel(), st)
+        # the Dropout1d mask applied as the BatchNorm backward reads gy (p = 0: plain backward)
+        pf = float(p) if BN_DROP_FUSE else 0.0
+        call("vt_batchnorm_bwd_dropout", ptr(gy), ptr(cat), B * L, C4, ptr(mean), ptr(rstd), ptr(g), ptr(b),
+             ACT["relu"], L, pf, *_sarg(seed), ptr(gcat), ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(bws),
+             bws.numel(), st)
         pw = _ParamGrads([wb1, ws, wm, wl, wb2], [True] * 5)
         gx0 = torch.empty_like(x0)
         # backward-data taps: one launch for the block's five flipped images (bf16)
