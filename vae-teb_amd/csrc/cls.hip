@@ -889,7 +889,9 @@ __global__ __launch_bounds__(64 * AFW, 4) void k_attn_fwd(const float* __restric
             if (kt < nkt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float e = expf(st[kt][r] * scale - m);
+                    // fused as written (fmaf): the contraction is not left to the compiler, whose
+                    // choice moved with the launch bounds (a separate product rounds once more)
+                    const float e = expf(fmaf(st[kt][r], scale, -m));
                     st[kt][r] = e;
                     l += e;
                 }
@@ -997,14 +999,14 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd(const float* __restrict__ q
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int ql = 4 * lc + r;
-                const float pr = expf(sc[r] * scale - lses[ql]);
+                const float pr = expf(fmaf(sc[r], scale, -lses[ql]));   // fused as written (as the forward)
                 float keep = 1.f;
                 if (p > 0.f) {
                     const uint64_t id = ((uint64_t)bh * S + q0 + ql) * S + 16 * kt + lr;
                     keep = mix_hash(seed, id) >= th ? dsc : 0.f;
                 }
                 pd[r] = pr * keep;                       // dropped probabilities (used by O)
-                ds[r] = pr * (dp[r] * keep - Dq[ql]);    // dS = P (dP - D)
+                ds[r] = pr * fmaf(dp[r], keep, -Dq[ql]);   // dS = P (dP - D)
             }
             // dV^T[dim][key] += dO^T[dim][q] Pd[q][key];  dK^T[dim][key] += Q^T[dim][q] dS[q][key]
 #pragma unroll
