@@ -785,7 +785,17 @@ __global__ __launch_bounds__(256) void k_time_mean(const float* __restrict__ X, 
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         const float* xb = X + (int64_t)b * L * C + c;
         float s = 0.f;
-        for (int t = 0; t < L; ++t) s += xb[(int64_t)t * C];
+        int t = 0;
+        // 16 rows' loads in flight, then added in row order (the same sum as the one-at-a-time
+        // loop, which waited out a load per row: 85 us per launch at L = 256)
+        for (; t + 16 <= L; t += 16) {
+            float v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = xb[(int64_t)(t + u) * C];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s += v[u];
+        }
+        for (; t < L; ++t) s += xb[(int64_t)t * C];
         Y[(int64_t)b * C + c] = s / (float)L;
     }
 }

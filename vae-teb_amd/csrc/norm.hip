@@ -449,11 +449,13 @@ __device__ __forceinline__ void bn_fin_channel(int c, int C, double s0, double s
     } else {
         f.dbeta[c] = f.accumulate ? f.dbeta[c] + (float)s0 : (float)s0;
         f.dgamma[c] = f.accumulate ? f.dgamma[c] + (float)s1 : (float)s1;
-        if (f.bnp) {   // vt_batchnorm_bwd_coef: the packed parameters and the parameter gradients
+        if (f.bnp) {   // vt_batchnorm_bwd_coef: the packed parameters
             f.bnp[c] = f.mean[c];
             f.bnp[C + c] = f.rstd[c];
             f.bnp[2 * C + c] = f.gamma[c];
             f.bnp[3 * C + c] = f.beta[c];
+        }
+        if (f.pg) {    // the parameter gradients (+)= the same float sums (no separate pass)
             f.pb[c] = f.pacc ? f.pb[c] + (float)s0 : (float)s0;
             f.pg[c] = f.pacc ? f.pg[c] + (float)s1 : (float)s1;
         }
@@ -1266,10 +1268,11 @@ int vt_batchnorm_bwd(const float* dy, const float* x, int64_t M, int C, const fl
     BnFin f = fin_of(2, M);
     f.dgamma = dg_now;
     f.dbeta = db_now;
+    f.pg = dgamma;   // the parameter gradients written by the same finalize (round 5: was a
+    f.pb = dbeta;    // k_reduce_parts launch over the one fresh sum per channel)
+    f.pacc = accumulate_params;
     col_partial_fin(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f);
     bn_dx_vec(dy, x, M, C, mean, rstd, gamma, beta, act, dg_now, db_now, dx, st);
-    hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
-                       accumulate_params);
     VT_LAUNCH_CHECK("vt_batchnorm_bwd");
     return VT_OK;
 }
@@ -1293,10 +1296,11 @@ int vt_batchnorm_bwd_dropout(const float* dy, const float* x, int64_t M, int C, 
     BnFin f = fin_of(2, M);
     f.dgamma = dg_now;
     f.dbeta = db_now;
+    f.pg = dgamma;
+    f.pb = dbeta;
+    f.pacc = accumulate_params;
     col_partial_fin(2, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f, &dr);
     bn_dx_vec(dy, x, M, C, mean, rstd, gamma, beta, act, dg_now, db_now, dx, st, &dr);
-    hipLaunchKernelGGL(k_reduce_parts, dim3(2 * C), dim3(NT), 0, st, dg_now, 1, 2 * C, dgamma, dbeta, C,
-                       accumulate_params);
     VT_LAUNCH_CHECK("vt_batchnorm_bwd_dropout");
     return VT_OK;
 }
