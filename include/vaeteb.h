@@ -672,6 +672,15 @@ int vt_maxpool3_bwd(const float* dY, const float* X, int B, int L, int C, float*
  * replaces: y + residual -> relu (ref/model/inception_time.py:165-167),
  *           y_seq + attn_out (:310)                                            */
 int vt_add_act_fwd(const float* A, const float* Bm, int64_t n, int act, float* Y, void* stream);
+/* FHRResidual's tail fused with its Dropout1d (ref/model/inception_time.py:152-170):
+ * vt_add_act_dropout_fwd: S_out = act(A + Bm) (saved), Y = Dropout1d(S_out) over L-row samples
+ *   of C channels (L = 0: element-wise) — the values of vt_add_act_fwd + vt_dropout_apply;
+ * vt_act_dropout_bwd: dX = Dropout1d(dY) act'(S) — the values of vt_dropout_apply +
+ *   vt_act_bwd.  act: 0 none, 1 ReLU.                                                      */
+int vt_add_act_dropout_fwd(const float* A, const float* Bm, int64_t n, int C, int act, int L, float p, int64_t seed,
+                           const void* seed_offset, float* S_out, float* Y, void* stream);
+int vt_act_dropout_bwd(const float* dY, const float* S_in, int64_t n, int C, int act, int L, float p, int64_t seed,
+                       const void* seed_offset, float* dX, void* stream);
 /* Dropout with a stateless counter hash: keep element i iff hash(seed, m(i)) >=
  * p * 2^32, kept values scaled by 1/(1-p); m(i) = i (nn.Dropout) or, with
  * L > 0 on (B, L, C) data, the (sample, channel) pair (nn.Dropout1d drops whole

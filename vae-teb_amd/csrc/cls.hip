@@ -742,6 +742,81 @@ __global__ void k_add_act(const float* __restrict__ A, const float* __restrict__
     }
 }
 
+// FHRResidual's tail in one pass each way (ref/model/inception_time.py:152-170): forward
+// s = act(a + b) (saved for the backward) and y = Dropout1d(s); backward dx = Dropout1d(dy) act'(s)
+// — each element the value of k_add_act + k_dropout / k_dropout + k_act_bwd (the same mask index,
+// hash, scale and products).  act: 0 none, 1 ReLU.  F4: four channels of one row per thread.
+template <bool F4>
+__global__ void k_add_act_drop(const float* __restrict__ A, const float* __restrict__ Bm, int64_t n, int C, int act,
+                               int L, float p, uint64_t seed, const uint64_t* __restrict__ soff,
+                               float* __restrict__ S, float* __restrict__ Y) {
+    seed = eff_seed(seed, soff);
+    const uint32_t th = drop_threshold(p);
+    const float sc = 1.f / (1.f - p);
+    const int64_t LC = (int64_t)L * C;
+    constexpr int V = F4 ? 4 : 1;
+    for (int64_t i0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * V; i0 < n;
+         i0 += (int64_t)gridDim.x * blockDim.x * V) {
+        const uint64_t m = L > 0 ? (uint64_t)((i0 / LC) * C + i0 % C) : (uint64_t)i0;
+        float a[V], b[V], sv[V], yv[V];
+        if constexpr (F4) {
+            const float4 a4 = *reinterpret_cast<const float4*>(A + i0), b4 = *reinterpret_cast<const float4*>(Bm + i0);
+            a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
+            b[0] = b4.x; b[1] = b4.y; b[2] = b4.z; b[3] = b4.w;
+        } else {
+            a[0] = A[i0];
+            b[0] = Bm[i0];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const float v = a[e] + b[e];
+            sv[e] = act == 1 ? fmaxf(v, 0.f) : v;
+            yv[e] = mix_hash(seed, m + e) >= th ? sv[e] * sc : 0.f;
+        }
+        if constexpr (F4) {
+            *reinterpret_cast<float4*>(S + i0) = make_float4(sv[0], sv[1], sv[2], sv[3]);
+            *reinterpret_cast<float4*>(Y + i0) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+        } else {
+            S[i0] = sv[0];
+            Y[i0] = yv[0];
+        }
+    }
+}
+
+template <bool F4>
+__global__ void k_act_drop_bwd(const float* __restrict__ dY, const float* __restrict__ S, int64_t n, int C, int act,
+                               int L, float p, uint64_t seed, const uint64_t* __restrict__ soff,
+                               float* __restrict__ dX) {
+    seed = eff_seed(seed, soff);
+    const uint32_t th = drop_threshold(p);
+    const float sc = 1.f / (1.f - p);
+    const int64_t LC = (int64_t)L * C;
+    constexpr int V = F4 ? 4 : 1;
+    for (int64_t i0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * V; i0 < n;
+         i0 += (int64_t)gridDim.x * blockDim.x * V) {
+        const uint64_t m = L > 0 ? (uint64_t)((i0 / LC) * C + i0 % C) : (uint64_t)i0;
+        float g[V], sv[V], o[V];
+        if constexpr (F4) {
+            const float4 g4 = *reinterpret_cast<const float4*>(dY + i0), s4 = *reinterpret_cast<const float4*>(S + i0);
+            g[0] = g4.x; g[1] = g4.y; g[2] = g4.z; g[3] = g4.w;
+            sv[0] = s4.x; sv[1] = s4.y; sv[2] = s4.z; sv[3] = s4.w;
+        } else {
+            g[0] = dY[i0];
+            sv[0] = S[i0];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const float gd = mix_hash(seed, m + e) >= th ? g[e] * sc : 0.f;
+            o[e] = gd * (act == 1 ? (sv[e] > 0.f ? 1.f : 0.f) : 1.f);
+        }
+        if constexpr (F4) {
+            *reinterpret_cast<float4*>(dX + i0) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+            dX[i0] = o[0];
+        }
+    }
+}
+
 __global__ void k_seed_advance(uint64_t* off) {
     if (threadIdx.x == 0) off[0] += 0xD1B54A32D192ED03ull;
 }
@@ -1256,6 +1331,42 @@ int vt_maxpool3_bwd(const float* dY, const float* X, int B, int L, int C, float*
                            accumulate);
     }
     VT_LAUNCH_CHECK("vt_maxpool3_bwd");
+    return VT_OK;
+}
+
+static bool f4_ok(int64_t n, int C, const void* a, const void* b, const void* c, const void* d) {
+    const uintptr_t o = reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+                        reinterpret_cast<uintptr_t>(c) | reinterpret_cast<uintptr_t>(d);
+    return C % 4 == 0 && n % 4 == 0 && (o & 15) == 0;
+}
+
+int vt_add_act_dropout_fwd(const float* A, const float* Bm, int64_t n, int C, int act, int L, float p, int64_t seed,
+                           const void* seed_offset, float* S_out, float* Y, void* stream) {
+    VT_CHECK_ARG(n > 0 && C > 0 && L >= 0 && (act == 0 || act == 1) && p >= 0.f && p < 1.f && n % C == 0,
+                 "vt_add_act_dropout_fwd: args (act none/relu, 0 <= p < 1, n a multiple of C)");
+    const uint64_t* so = seed_off(seed_offset, p);
+    if (f4_ok(n, C, A, Bm, S_out, Y))
+        hipLaunchKernelGGL(k_add_act_drop<true>, dim3(ew_blocks(n / 4)), dim3(256), 0, S(stream), A, Bm, n, C, act, L,
+                           p, (uint64_t)seed, so, S_out, Y);
+    else
+        hipLaunchKernelGGL(k_add_act_drop<false>, dim3(ew_blocks(n)), dim3(256), 0, S(stream), A, Bm, n, C, act, L, p,
+                           (uint64_t)seed, so, S_out, Y);
+    VT_LAUNCH_CHECK("vt_add_act_dropout_fwd");
+    return VT_OK;
+}
+
+int vt_act_dropout_bwd(const float* dY, const float* S_in, int64_t n, int C, int act, int L, float p, int64_t seed,
+                       const void* seed_offset, float* dX, void* stream) {
+    VT_CHECK_ARG(n > 0 && C > 0 && L >= 0 && (act == 0 || act == 1) && p >= 0.f && p < 1.f && n % C == 0,
+                 "vt_act_dropout_bwd: args (act none/relu, 0 <= p < 1, n a multiple of C)");
+    const uint64_t* so = seed_off(seed_offset, p);
+    if (f4_ok(n, C, dY, S_in, dX, dX))
+        hipLaunchKernelGGL(k_act_drop_bwd<true>, dim3(ew_blocks(n / 4)), dim3(256), 0, S(stream), dY, S_in, n, C, act,
+                           L, p, (uint64_t)seed, so, dX);
+    else
+        hipLaunchKernelGGL(k_act_drop_bwd<false>, dim3(ew_blocks(n)), dim3(256), 0, S(stream), dY, S_in, n, C, act, L,
+                           p, (uint64_t)seed, so, dX);
+    VT_LAUNCH_CHECK("vt_act_dropout_bwd");
     return VT_OK;
 }
 

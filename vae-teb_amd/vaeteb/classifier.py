@@ -43,8 +43,9 @@ def _seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item()), _SEED_OFF
 
 
-# Dropout1d of the inception blocks fused into their BatchNorm apply / backward passes
-# (vt_batchnorm_{fwd,bwd}_dropout: the same values as the separate dropout launches); 0: separate
+# Dropout1d fused into the producing / consuming pass: the inception blocks' BatchNorm apply and
+# backward (vt_batchnorm_{fwd,bwd}_dropout), the residual blocks' add + ReLU and its backward
+# (vt_add_act_dropout_fwd, vt_act_dropout_bwd) — the same values as separate launches; 0: separate
 BN_DROP_FUSE = int(os.environ.get("VAETEB_BN_DROP_FUSE", "1"))
 
 
@@ -237,11 +238,16 @@ class _ResidualF(torch.autograd.Function):
         call("vt_batchnorm_fwd", ptr(r), B * L, C4, ptr(g), ptr(b), ACT["none"], eps, momentum, ptr(rb), ptr(mean),
              ptr(rstd), ptr(run_mean), ptr(run_var), ptr(bws), bws.numel(), st)
         s = torch.empty_like(r)
-        call("vt_add_act_fwd", ptr(y), ptr(rb), s.numel(), ACT["relu"], ptr(s), st)
         out = s
-        if p > 0:
+        if p > 0 and BN_DROP_FUSE:   # s = relu(y + rb) saved, out = Dropout1d(s): one pass
             out = torch.empty_like(s)
-            call("vt_dropout_apply", ptr(s), s.numel(), C4, L, float(p), *_sarg(seed), ptr(out), st)
+            call("vt_add_act_dropout_fwd", ptr(y), ptr(rb), s.numel(), C4, ACT["relu"], L, float(p), *_sarg(seed),
+                 ptr(s), ptr(out), st)
+        else:
+            call("vt_add_act_fwd", ptr(y), ptr(rb), s.numel(), ACT["relu"], ptr(s), st)
+            if p > 0:
+                out = torch.empty_like(s)
+                call("vt_dropout_apply", ptr(s), s.numel(), C4, L, float(p), *_sarg(seed), ptr(out), st)
         ctx.save_for_backward(x, r, s, mean, rstd)
         ctx.params = (w, g, b)
         ctx.cfg = (p, seed, bf16)
@@ -257,11 +263,15 @@ class _ResidualF(torch.autograd.Function):
         st = _st()
         gout = gout.contiguous()
         gs = torch.empty_like(s)
-        src = gout
-        if p > 0:
-            call("vt_dropout_apply", ptr(gout), gout.numel(), C4, L, float(p), *_sarg(seed), ptr(gs), st)
-            src = gs
-        call("vt_act_bwd", ptr(src), ptr(s), s.numel(), ACT["relu"], ptr(gs), st)
+        if p > 0 and BN_DROP_FUSE:   # Dropout1d(gout) relu'(s) in one pass
+            call("vt_act_dropout_bwd", ptr(gout), ptr(s), s.numel(), C4, ACT["relu"], L, float(p), *_sarg(seed),
+                 ptr(gs), st)
+        else:
+            src = gout
+            if p > 0:
+                call("vt_dropout_apply", ptr(gout), gout.numel(), C4, L, float(p), *_sarg(seed), ptr(gs), st)
+                src = gs
+            call("vt_act_bwd", ptr(src), ptr(s), s.numel(), ACT["relu"], ptr(gs), st)
         gr = torch.empty_like(r)
         pbn = _ParamGrads([g, b], [True, True])
         bws = WS.get(_BN_WS, x.device, 5)
