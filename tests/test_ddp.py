@@ -44,8 +44,14 @@ def _worker(rank, world, port, bucket_mb, q, reduce_dtype=torch.float32):
         results.append((st.g.clone() / world, fired_before_finish, len(gb.buckets)))
     # every parameter / grad is a view of the flat buffers
     ok_views = all(p.data_ptr() >= st.p.data_ptr() and p.grad.data_ptr() >= st.g.data_ptr() for p in st.params)
-    q.put((rank, [r[0] for r in results], [r[1] for r in results], results[0][2], ok_views))
+    # numpy through the queue: a tensor would be shared by file descriptor, which fails when this
+    # process exits before the parent has received it (EOFError in the resource sharer)
+    q.put((rank, [r[0].numpy() for r in results], [r[1] for r in results], results[0][2], ok_views))
     dist.destroy_process_group()
+
+
+def _torch_out(o):
+    return (o[0], [torch.from_numpy(a) for a in o[1]], o[2], o[3], o[4])
 
 
 @pytest.mark.parametrize("bucket_mb", [0.01, 64.0])
@@ -57,11 +63,11 @@ def test_bucketed_allreduce_matches_full_batch_average(bucket_mb):
     procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=120) for _ in range(world)]
+    out = [_torch_out(q.get(timeout=120)) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    out.sort()
+    out.sort(key=lambda o: o[0])
     # reference: average of the per-rank gradients computed independently
     torch.manual_seed(0)
     ref_model = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64),
@@ -97,7 +103,7 @@ def test_bucketed_allreduce_bf16():
     procs = [ctx.Process(target=_worker, args=(r, world, port, 0.01, q, torch.bfloat16)) for r in range(world)]
     for p in procs:
         p.start()
-    out = sorted([q.get(timeout=120) for _ in range(world)], key=lambda o: o[0])
+    out = sorted([_torch_out(q.get(timeout=120)) for _ in range(world)], key=lambda o: o[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
