@@ -112,6 +112,48 @@ def profile_mfma(ROOT_=None):
     return None, None
 
 
+LSTM_KERNELS = {"recurrence": ("k_lstm16_fwd", "k_lstm16_bwd", "k_lstm_fwd", "k_lstm_bwd"),
+                "weight gradient": ("k_sk_dw16", "k_sk_sum", "k_lstm_dw")}
+
+
+def profile_lstm(ROOT_=None):
+    """SURVEY.md §8(d) / BASELINE.md §4: the encoders' LSTMs are latency-bound and reported
+    separately.  From the latest committed timed-step profile of this bench
+    (profiles/rNN/kernel_stats_timed.csv: kernel time per step of every LSTM kernel) and its
+    critical chain (critchain_timed.txt, tools/critchain.py: the LSTM recurrences' share of the
+    step's longest dependent chain of kernels).  Returns a dict or None."""
+    import csv
+    import glob
+    import re
+    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
+        ks, cc = os.path.join(d, "kernel_stats_timed.csv"), os.path.join(d, "critchain_timed.txt")
+        if not (os.path.exists(ks) and os.path.exists(cc)):
+            continue
+        fam = {f: 0.0 for f in LSTM_KERNELS}
+        per = {}
+        for r in csv.DictReader(open(ks)):
+            for f, pats in LSTM_KERNELS.items():
+                if any(p in r["Name"] for p in pats):
+                    fam[f] += float(r["PerStepNs"]) / 1e3
+                    short = re.sub(r"\(.*", "", r["Name"].replace("(anonymous namespace)::", "")).replace("void ", "")
+                    short = short.split("::")[-1]
+                    per[short] = round(per.get(short, 0.0) + float(r["PerStepNs"]) / 1e3, 1)
+        lines = open(cc).read().splitlines()
+        m = re.search(r"critical chain \d+ kernels, ([\d.]+) us busy of ([\d.]+) us", "\n".join(lines[:3]))
+        chain = [re.match(r"\s*([\d.]+) us\s+(.*)", l) for l in lines[2:]]
+        on_chain = sum(float(c.group(1)) for c in chain if c and "lstm" in c.group(2))
+        if not m or not any(fam.values()):
+            continue
+        busy = float(m.group(1))
+        return {"bound": "latency (sequential recurrence: S = 256 dependent steps x 4 layers x 2 encoders, fwd + bwd)",
+                "kernel_us_per_step": {f: round(v, 1) for f, v in fam.items()},
+                "per_kernel_us_per_step": per,
+                "critical_chain_us": round(on_chain, 1), "critical_chain_busy_us": busy,
+                "critical_chain_share": round(on_chain / busy, 4),
+                "source": os.path.relpath(ks, ROOT) + " + " + os.path.relpath(cc, ROOT)}
+    return None
+
+
 # SURVEY.md §8(d): algorithmic HBM bytes per sample of the whole step (c2, S = 256):
 # front-end raw read + analytic-signal write and read + feature write, VAE activations
 # (4,161,024 leaf activation elements per sample x 2 B x 4 passes, measured with hooks on
@@ -653,6 +695,9 @@ def main():
     hbm = pmc_kernels() if (J, Q, T, B) == (11, 4, 16, 256) and not c4 else None
     if hbm:
         out["hbm_kernels"] = hbm
+    lstm = profile_lstm() if (J, Q, T, B) == (11, 4, 16, 256) and not c4 and args.lstm == "16-mixed" else None
+    if lstm:
+        out["lstm"] = lstm
     mfma_steps = args.steps
     if graph:
         # the MFMA head GEMMs run inside the graph: time them with HIP events in

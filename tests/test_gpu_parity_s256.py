@@ -495,20 +495,32 @@ def test_production_geometry_end_to_end_vs_oracle():
 
 
 def test_bench_batch_fp32_step_vs_fp64_oracle():
-    """the bench's own batch.  One exact-fp32 c2 step at B = 256 — raw
-    windows -> FrontEnd(J=11 Q=4 T=16) -> SeqVaeTeb(S = 256) — against the fp64 oracle step
+    """the bench's own batch.  One exact-fp32 c2 step at B = 256 —
+    raw windows -> FrontEnd(J=11 Q=4 T=16) -> SeqVaeTeb(S = 256) — against the fp64 oracle step
     (oracle/model_ref.py, run on this box's host) on the same features: the 17 train-mode
-    BatchNorms then reduce over 65,536 (encoders) to 1,048,576 (last decoder block) rows with
-    the kernels' split partials, the MLPs / LSTMs run their full 256-sample grids, the heads
-    their 256-row GEMMs.  Losses within 1e-5; the pre-clip gradient norm equal to the fp64 norm
-    of the reduced gradients and as close to the oracle's as the oracle's own fp32 step's
-    whole-gradient error allows; the non-head gradients (the four 4096^2 head weights are
-    checked by norm) within 2x of the oracle fp32 step's median / p90 rel-L2 over the gradients
-    that step gets within 1e-3 of fp64, and each within 10x of it + 2e-5.  The front-end rows at B = 256 are those of B = 4 runs
-    bit for bit (test_gpu_frontend.py), and a B = 4 slice of them is held to the fp64 oracle
-    front-end here."""
+    BatchNorms then reduce over 65,536 (encoders) to 1,048,576 (last decoder block) rows with the
+    kernels' split partials, the MLPs / LSTMs run their full 256-sample grids, the heads their
+    256-row GEMMs.
+
+    At this batch an fp32 step is not a fixed distance from fp64: the oracle's own fp32 step run
+    from initial weights perturbed by one ulp lands anywhere in a spread as wide as the distance
+    itself (CPU measurement, tools/b256_ensemble.py: pre-clip norm gap +2.0e-5 for the plain fp32
+    run, -2.3e-5 .. -1.3e-4 for four one-ulp members; whole-gradient rel-L2 3.2e-4 .. 6.4e-4;
+    median per-gradient 5.5e-4 .. 1.1e-3).  So the bound is that ENSEMBLE, computed here: the
+    plain fp32 oracle step and ENS one-ulp perturbed fp32 oracle steps (golden_util.perturb_ulp_),
+    each compared with the fp64 step, and the HIP step held to 1.5x the ensemble's largest
+    distance for the pre-clip norm, the whole gradient and the median / p90 of the per-gradient
+    rel-L2, every single gradient within 10x its largest member distance + 2e-5.  Losses within
+    1e-5; the pre-clip norm equal to the fp64 norm of the gradients it reduced; the four head
+    gradients' norms as before.  The front-end rows at B = 256 are those of B = 4 runs bit for bit
+    (test_gpu_frontend.py), and a B = 4 slice of them is held to the fp64 oracle front-end here.
+    (Round 6 finding: the LSTM cell on the libm expf / tanhf / IEEE divide instead of the hardware
+    v_exp / v_rcp forms moved this step's norm gap from +3.6e-5 to -1.7e-4 — the same scatter as
+    the oracle's members, not a bias of the approximations)"""
     _need_gpu()
     import time
+    from golden_util import det_fill_, perturb_ulp_
+    from oracle import model_ref as M
     from vaeteb import synthetic
     from vaeteb.frontend import FrontEnd, FrontEndPlan, load_stats
     from vaeteb.train import Trainer
@@ -531,70 +543,64 @@ def test_bench_batch_fp32_step_vs_fp64_oracle():
     L = tr.step({"x": torch.from_numpy(x).cuda()}, eps=torch.from_numpy(eps).cuda())
     torch.cuda.synchronize()
     gn = float(L["grad_norm"])
+
+    def member(seed):   # the oracle's fp32 step from one-ulp perturbed initial weights
+        ref = perturb_ulp_(det_fill_(M.SeqVaeTebRef(S, *widths)), seed)
+        T = lambda a: torch.from_numpy(np.asarray(a)).float()
+        _, _, g, _ = M.train_step(ref, {"y_st": T(feats["fhr_st"]), "y_ph": T(feats["fhr_ph"]),
+                                        "x_ph": T(feats["fhr_up_ph"]), "y_raw": T(feats["fhr"])}, T(eps), 1e-5)
+        return g
+    ENS = 4
     t0 = time.time()
     _, L_o, g_o, _ = _oracle_step(feats, eps, widths)
     t1 = time.time()
     _, _, g_o32, _ = _oracle_step(feats, eps, widths, torch.float32)
-    print(f"oracle steps at B={B}: fp64 {t1 - t0:.1f} s, fp32 {time.time() - t1:.1f} s")
+    members = [g_o32] + [member(s) for s in range(1, ENS + 1)]
+    print(f"oracle steps at B={B}: fp64 {t1 - t0:.1f} s, {ENS + 1} fp32 {time.time() - t1:.1f} s")
     for k in LOSSES:
         exp = L_o[k].item()
         assert abs(L[k].item() - exp) <= 1e-5 * abs(exp) + 1e-7, (k, L[k].item(), exp)
     norm = lambda gs: torch.sqrt(sum((g.double() ** 2).sum() for g in gs)).item()
-    gn_o, gn_o32 = norm(g_o.values()), norm(g_o32.values())
+    gn_o = norm(g_o.values())
     params = dict(m.named_parameters())
     heads = {k for k, p in params.items() if p.numel() >= 1 << 20}
     assert len(heads) == 4, heads
-    # everything is printed first (the assertions follow): the norms (97 % of the squared gradient
-    # norm is in the heads) and every gradient's rel-L2 to the fp64 oracle beside the oracle's own
-    # fp32 distance
+    flat = lambda gs: torch.cat([g.detach().double().cpu().reshape(-1) for g in gs])
+    go = flat(g_o[k] for k in g_o)
+    names = [k for k in g_o if k not in heads and g_o[k].norm() > 0]
+
+    def dist(g):   # (norm gap, whole-gradient rel-L2, per-gradient rel-L2 of the non-head gradients)
+        return (abs(norm(g[k] for k in g_o) - gn_o) / gn_o, (flat(g[k] for k in g_o) - go).norm().item() / go.norm().item(),
+                np.array([rel(g[k], g_o[k]) for k in names]))
+    ours = dist({k: params[k].grad for k in g_o})
+    ens = [dist(g) for g in members]
+    # the well-conditioned gradients: those the plain fp32 oracle step gets within 1e-3 of fp64
+    good = ens[0][2] < 1e-3
+    assert good.sum() >= 300, good.sum()
     gn_d = norm(p.grad for p in params.values())
-    print(f"grad norm: ours {gn:.7f} (fp64 norm of our gradients {gn_d:.7f}), oracle fp64 {gn_o:.7f}, "
-          f"oracle fp32 {gn_o32:.7f}")
-    contrib = sorted(((params[k].grad.double().norm().item() ** 2 - g.double().norm().item() ** 2, k)
-                      for k, g in g_o.items()), key=lambda t: -abs(t[0]))[:8]
-    for dsq, k in contrib:
-        print(f"  |grad|^2 ours - oracle: {k}: {dsq:+.3e} (oracle fp32 "
-              f"{g_o32[k].double().norm().item() ** 2 - g_o[k].double().norm().item() ** 2:+.3e})")
+    print(f"grad norm: ours {gn:.7f} (fp64 norm of our gradients {gn_d:.7f}), oracle fp64 {gn_o:.7f}")
+    for tag, (ng, ev, per) in [("ours", ours)] + [(f"fp32 member {i}", e) for i, e in enumerate(ens)]:
+        print(f"  {tag}: norm gap {ng:.3e}, whole-gradient rel-L2 {ev:.3e}, over {good.sum()} well-conditioned "
+              f"non-head gradients median {np.median(per[good]):.3e} p90 {np.percentile(per[good], 90):.3e} "
+              f"max {per[good].max():.3e}")
     hn = {}
     for k in sorted(heads):
         hn[k] = (params[k].grad.double().norm().item(), g_o[k].double().norm().item(), g_o32[k].double().norm().item())
         print(f"{k}: |grad| ours {hn[k][0]:.7f}, oracle fp64 {hn[k][1]:.7f}, fp32 {hn[k][2]:.7f}; rel-L2 ours "
               f"{rel(params[k].grad, g_o[k]):.3e}, oracle fp32 {rel(g_o32[k], g_o[k]):.3e}")
-    table = sorted(((rel(params[k].grad, gr), rel(g_o32[k], gr), k) for k, gr in g_o.items()
-                    if k not in heads and gr.norm() > 0), reverse=True)
-    for e, e32, k in table[:15]:
-        print(f"  worst: {k}: ours {e:.3e}, oracle fp32 {e32:.3e}")
-    big = sorted(((g_o[k].double().norm().item(), k) for k in g_o), reverse=True)[:10]
-    for nrm, k in big:
-        print(f"  largest: {k}: |grad| {nrm:.5f}; rel-L2 ours {rel(params[k].grad, g_o[k]):.3e}, oracle fp32 "
-              f"{rel(g_o32[k], g_o[k]):.3e}")
-    errs = np.array([e for e, e32, k in table if e32 < 1e-3])
-    e32 = np.array([e32 for e, e32, k in table])
-    print(f"B=256 grads vs fp64 oracle over {len(errs)} well-conditioned non-head gradients: median "
-          f"{np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} max {errs.max():.3e}; the oracle's own fp32 "
-          f"step: median {np.median(e32):.3e} max {e32.max():.3e}")
-    # the pre-clip norm: the kernel's reduction equals the fp64 norm of the gradients it reduced,
-    # and those gradients, as one vector, are as close to the fp64 oracle's as the oracle's own
-    # fp32 step is (measured: ours 6.1803279 vs fp64 6.1801055, i.e. 3.6e-5 — the oracle's fp32
-    # norm landed 2.2e-6 away by cancellation, while its vector error is of the same size as ours)
-    flat = lambda gs: torch.cat([g.detach().double().cpu().reshape(-1) for g in gs])
-    go = flat(g_o[k] for k in g_o)
-    ev, ev32 = (flat(params[k].grad for k in g_o) - go).norm().item() / go.norm().item(), \
-        (flat(g_o32[k] for k in g_o) - go).norm().item() / go.norm().item()
-    print(f"whole-gradient rel-L2 to fp64: ours {ev:.3e}, oracle fp32 {ev32:.3e}")
+    env = np.max(np.stack([e[2] for e in ens]), 0)     # per gradient: the ensemble's largest distance
+    table = sorted(zip(ours[2], env, names), reverse=True)
+    for e, e32, k in table[:10]:
+        print(f"  worst: {k}: ours {e:.3e}, fp32 ensemble max {e32:.3e}")
+    env_ng, env_ev = max(e[0] for e in ens), max(e[1] for e in ens)
+    env_med = max(np.median(e[2][good]) for e in ens)
+    env_p90 = max(np.percentile(e[2][good], 90) for e in ens)
     assert abs(gn - gn_d) <= 1e-6 * gn_d, (gn, gn_d)
-    assert ev <= max(1e-5, 2 * ev32), (ev, ev32)
-    assert abs(gn - gn_o) <= max(1e-5, 2 * ev32) * gn_o, (gn, gn_o, gn_o32)
+    assert ours[0] <= 1.5 * env_ng + 1e-6, (ours[0], env_ng)
+    assert ours[1] <= 1.5 * env_ev, (ours[1], env_ev)
+    assert np.median(ours[2][good]) <= 1.5 * env_med, (np.median(ours[2][good]), env_med)
+    assert np.percentile(ours[2][good], 90) <= 1.5 * env_p90, (np.percentile(ours[2][good], 90), env_p90)
     for k, (a, e, e32_) in hn.items():
         assert abs(a - e) <= max(1e-5 * e, 2 * abs(e32_ - e)), (k, a, e, e32_)
-    # at B = 256 an fp32 step is itself ~6e-4 (median) from fp64 — 17 BatchNorms reducing over up
-    # to 1M rows, 256-step LSTMs (measured: the oracle's own fp32 median 6.2e-4, max 5.3e-3) — so
-    # the fixed J=6 bounds (median 2e-5) do not apply; the HIP step is held to the oracle's own
-    # fp32 error: median and p90 within 2x of it, and every gradient within 10x + 2e-5
-    e32w = np.array([e32 for e, e32, k in table if e32 < 1e-3])
-    assert len(errs) >= 300, len(errs)
-    assert np.median(errs) <= max(2e-5, 2 * np.median(e32w)), (np.median(errs), np.median(e32w))
-    assert np.percentile(errs, 90) <= max(5e-5, 2 * np.percentile(e32w, 90)), (np.percentile(errs, 90),
-                                                                                 np.percentile(e32w, 90))
     worst = max((e / (2e-5 + 10 * e32), k) for e, e32, k in table)
     assert worst[0] <= 1.0, worst

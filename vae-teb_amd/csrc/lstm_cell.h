@@ -31,6 +31,14 @@ __device__ __forceinline__ float ftanh(float x) {
     return ax < 0.3f ? small : big;
 }
 
+// The libm forms (OCML expf / tanhf, IEEE divide), as PyTorch's CPU LSTM evaluates them:
+// the exact-fp32 recurrences use them when lstm.hip is built with -DVT_LSTM_LIBM=1.  Measured
+// in round 6 (VERDICT r05 item 1 asked whether the hardware forms' last-bit error biases the
+// B = 256 gradient): they are not closer to the fp64 oracle — the gradient scatters with any
+// last-bit change as the oracle's own one-ulp perturbed fp32 runs do.
+__device__ __forceinline__ float sigm_ieee(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float tanh_ieee(float x) { return tanhf(x); }
+
 // The cell arithmetic of one step, shared by the plain and the fused kernels so
 // both give the same bits wherever they are inlined: contraction is spelled out
 // (fmaf) and otherwise off, so the compiler's choice cannot depend on context.
@@ -38,10 +46,11 @@ __device__ __forceinline__ float cell_fwd_c(float c, float gi, float gf, float g
 #pragma clang fp contract(off)
     return fmaf(gf, c, gi * gg);
 }
+template <bool IEEE = false>
 __device__ __forceinline__ void cell_bwd(float dh, float gi, float gf, float gg, float go, float c, float cp, float& dc,
                                          float& v0, float& v1, float& v2, float& v3) {
 #pragma clang fp contract(off)
-    const float tc = ftanh(c);
+    const float tc = IEEE ? tanh_ieee(c) : ftanh(c);
     const float d_o = dh * tc;
     dc = fmaf(dh * go, fmaf(-tc, tc, 1.f), dc);
     const float di = dc * gg, dgg = dc * gi, df = dc * cp;
