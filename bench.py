@@ -87,11 +87,12 @@ MFMA_CALLS = {
 MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 
 
-def profile_mfma(ROOT_=None):
+def profile_mfma(workload="c2"):
     """Decoder-head MFMA kernel time per step from the latest committed rocprofv3
-    kernel-stats summary of this bench (profiles/r*/kernel_stats_*.csv): the sum of
-    k_mfma_gemm + k_mfma_dw + k_mfma_reduce over the profiled steps (one k_adamw4 per
-    step).  Returns (ms per step, csv path) or (None, None)."""
+    kernel-stats summary of this bench and workload (profiles/r*/kernel_stats_timed.csv for
+    c2, kernel_stats_c4_timed.csv for c4): the sum of k_mfma_gemm + k_mfma_dw (+ the split
+    reduce k_mfma_reduce of rounds <= 5) over the profiled steps (one k_adamw4 per step).
+    Returns (ms per step, csv path) or (None, None)."""
     import csv
     import glob
     # latest round first (profiles/rNN); within a round, the file named in profiles/rNN/LATEST
@@ -101,8 +102,11 @@ def profile_mfma(ROOT_=None):
         latest = os.path.join(d, "LATEST")
         pinned = os.path.exists(latest) and open(latest).read().strip() == os.path.basename(f)
         return (os.path.basename(d), pinned, os.path.getmtime(f))
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_step*.csv")) +
-                   glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_timed.csv")), key=key)
+    if workload == "c4":
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_c4_timed.csv")), key=key)
+    else:
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_step*.csv")) +
+                       glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_timed.csv")), key=key)
     for f in reversed(files):
         rows = list(csv.DictReader(open(f)))
         steps = sum(int(r["Calls"]) for r in rows if "k_adamw4" in r["Name"])
@@ -167,13 +171,13 @@ def step_bytes_per_sample(plan, fe, n_params, batch):
     return front + ACT_ELEMS_PER_SAMPLE * 2 * 4 + 46 * n_params / batch
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, fname="pmc_traffic.json"):
     """HBM bytes per launch of the roofline kernel from the latest committed
-    rocprofv3 PMC measurement (profiles/r*/pmc_traffic.json, written by
-    tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes of this
-    same bench command), or None."""
+    rocprofv3 PMC measurement (profiles/r*/pmc_traffic.json — pmc_traffic_c5.json for the
+    c5 workload — written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE
+    passes of this same bench command), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", fname)))
     for f in reversed(files):
         d = json.load(open(f))
         if d.get("kernel") == kernel:
@@ -294,6 +298,8 @@ def run_c5(args, rank, world, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    _lib.call("vt_bucket_marker", 0, _lib.stream())   # timed-region markers (tools/step_stats.py)
+    torch.cuda.synchronize()
     timer.reset(True)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -302,6 +308,7 @@ def run_c5(args, rank, world, dev):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    _lib.call("vt_bucket_marker", 0, _lib.stream())
     timer.enabled = False
     if world > 1:
         t = torch.tensor([dt], device=dev)
@@ -310,6 +317,10 @@ def run_c5(args, rank, world, dev):
     k_ms, k_n = timer.mean_ms("vt_scat_mod_spec")
     k_bytes = timer.total_flops["vt_scat_mod_spec"] / max(k_n, 1)
     achieved = k_bytes / (k_ms * 1e-3) / 1e9
+    # PMC traffic of the same kernel from separate FETCH_SIZE / WRITE_SIZE passes of this command
+    # (profiles/rNN/pmc_traffic_c5.json): an average over the launches of the cascade's levels,
+    # quoted for the default geometry only
+    traffic, traffic_src = pmc_traffic("k_scat_mod_spec", "pmc_traffic_c5.json") if B == 64 else (None, None)
     out = {"metric": "scattering samples/sec, Scattering1D(J=8, Q=12) 16384-pt windows, batch 64/GPU",
            "value": round(args.steps * B * world / dt, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
@@ -319,7 +330,8 @@ def run_c5(args, rank, world, dev):
                       "seq_len": N, "parallelism": f"replicas{world}"},
            "roofline": {"bound": "hbm", "kernel": "vt_scat_mod_spec (k_scat_mod_spec)", "achieved": round(achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": None, "avg_launch_ms": round(k_ms, 4), "launches": k_n,
+                        "traffic": traffic, "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                        "traffic_source": traffic_src, "avg_launch_ms": round(k_ms, 4), "launches": k_n,
                         "algorithmic_bytes": round(k_bytes)},
            "checksum": float(S.double().abs().sum().item())}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -645,12 +657,15 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32" if (args.heads, args.conv, args.mlp, args.lstm) == ("fp32", "fp32", "fp32", "fp32") else
                  "bf16 MFMA (" + " + ".join(n for n, v in (("decoder heads", args.heads), ("conv blocks", args.conv),
-                                                         ("ResidualMLP linears", args.mlp)) if v == "bf16")
+                                                         ("ResidualMLP linears", args.mlp),
+                                                         ("classifier convolutions", args.conv if c4 else "")) if v == "bf16")
                  + (", LSTM recurrences f16 fwd / bf16 bwd" if args.lstm == "16-mixed" else "")
                  + "), fp32 accumulation; fp32 LayerNorm / BatchNorm / LSTM state / front-end / optimizer",
         "data": "synthetic",
         "config": {"workload": (f"c4: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTebClassifier("
-                                f"R={16 * S}, FHRInceptionTimeClassifier f32 d6 attention, dropout 0.2) end-to-end "
+                                f"R={16 * S}, FHRInceptionTimeClassifier d6 attention, "
+                                f"{'bf16-MFMA' if args.conv == 'bf16' else 'exact-fp32'} convolutions, fp32-MFMA "
+                                f"attention, dropout 0.2) end-to-end "
                                 f"train step, CE + 0.1 ELBO, batch {B}/GPU") if c4 else
                                (f"c2: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTeb(R={16 * S}) "
                                 f"train step, batch {B}/GPU"), "global_batch": B * world, "seq_len": N,
@@ -711,12 +726,13 @@ def main():
     mfma_ms = timer.total_ms(list(MFMA_CALLS))
     if mfma_ms > 0:
         # MFMA utilisation of the decoder heads from KERNEL time: the committed rocprofv3 summary of this
-        # bench (k_mfma_gemm + k_mfma_dw + k_mfma_reduce per step); the live HIP-event span around the
+        # bench and workload (k_mfma_gemm + k_mfma_dw per step); the live HIP-event span around the
         # C-ABI calls (which also covers the split-K reduces' launch gaps) is kept as call_span_ms
         flops_step = sum(timer.total_flops[n] for n in MFMA_CALLS) / mfma_steps
-        k_mfma_ms, k_src = profile_mfma() if (J, Q, T, B) == (11, 4, 16, 256) else (None, None)
+        k_mfma_ms, k_src = profile_mfma(args.workload) if (J, Q, T, B) == (11, 4, 16, 256) else (None, None)
         tf = flops_step / (k_mfma_ms * 1e-3) / 1e12 if k_mfma_ms else None
-        out["mfma"] = {"kernels": "k_mfma_gemm + k_mfma_dw + k_mfma_reduce (decoder heads, bf16)",
+        out["mfma"] = {"kernels": "k_mfma_gemm (split-K sums in its last-arriving workgroups) + k_mfma_dw "
+                                  "(decoder heads, bf16)",
                        "flop_per_step": flops_step, "kernel_ms_per_step": k_mfma_ms and round(k_mfma_ms, 4),
                        "source": k_src, "achieved": tf and round(tf, 1), "peak": MFMA_PEAK_TFLOPS,
                        "unit": "TFLOP/s", "frac": tf and round(tf / MFMA_PEAK_TFLOPS, 4),

@@ -716,9 +716,78 @@ def gen_classifier():
     save("seqvae_classifier_s16_b4.npz", **d)
 
 
+def gen_classifier_amp():
+    """Config 4's end-to-end step (seqvae_classifier_s16_b4.npz's batch and weights) at the
+    reference's own 16-bit training precision (VERDICT r05 item 8: the bench runs the classifier's
+    convolutions on bf16 MFMA): torch.autocast('cpu', bf16) literally, and Emu16 (the CUDA
+    autocast op split: Linear / Conv1d / LSTM operands and outputs rounded) in bf16 and in fp16
+    with GradScaler's 2^16 — logits, losses and every gradient's rel-L2 distance from the same
+    step in fp32: the spread the bench-precision HIP step is held to (tests/test_gpu_classifier.py)."""
+    import vae_teb_model as V
+    B, S = 4, 16
+    rng = np.random.Generator(np.random.PCG64(45))   # the batch of gen_classifier's seqvae fixture
+    y_st = rng.standard_normal((B, S, 43)).astype(np.float32)
+    y_ph = rng.standard_normal((B, S, 44)).astype(np.float32)
+    x_ph = rng.standard_normal((B, S, 130)).astype(np.float32)
+    y_raw = rng.standard_normal((B, 16 * S)).astype(np.float32)
+    eps = rng.standard_normal((B, S, 32)).astype(np.float32)
+    labels = np.array([1, 0, 0, 1], dtype=np.int64)
+    T = torch.from_numpy
+
+    def run(mode, scale16=65536.0):
+        m = V.SeqVaeTebClassifier(sequence_length=S, freeze_vae=False, classifier_dropout=0.0)
+        m.vae_model = build_ref_model(S)
+        _crop_conv_long_(m.classifier)
+        det_fill_(m.classifier)
+        m.train()
+        m.vae_model.reparameterize = lambda mu, lv: mu + T(eps) * torch.exp(0.5 * lv)
+        scale = 1.0
+        import contextlib
+        ctx = contextlib.nullcontext()
+        if mode == "cpu_bf16":
+            ctx = torch.autocast("cpu", dtype=torch.bfloat16)
+        elif mode in ("emu_bf16", "emu_fp16"):
+            emu = Emu16(torch.bfloat16 if mode == "emu_bf16" else torch.float16)
+            ctx, scale = emu, (scale16 if mode == "emu_fp16" else 1.0)
+            for mod in m.modules():
+                if isinstance(mod, torch.nn.LSTM):
+                    mod.forward = emu.lstm_forward(mod)
+        with ctx:
+            out = m.compute_loss(T(y_st), T(y_ph), T(x_ph), T(labels), y_raw=T(y_raw), compute_vae_loss=True,
+                                 vae_loss_weight=0.1)
+        (out["total_loss"].float() * scale).backward()
+        grads = [p.grad.detach().float() / scale for _, p in m.named_parameters()]
+        return out, grads, [k for k, _ in m.named_parameters()]
+
+    o32, g32, names = run("fp32")
+    d = dict(B=B, S=S, param_names=np.array(names), logits_fp32=o32["logits"].detach().float().numpy())
+    for k in ("classification_loss", "vae_loss", "total_loss"):
+        d[f"fp32_{k}"] = o32[k].item()
+    for mode in ("cpu_bf16", "emu_bf16", "emu_fp16"):
+        t = time.time()
+        o, g, _ = run(mode)
+        scale16 = 65536.0
+        while mode == "emu_fp16" and not all(torch.isfinite(x).all() for x in g) and scale16 > 1:
+            # GradScaler: a step with inf / NaN gradients is skipped and the scale halved; the
+            # fixture records the first scale whose backward stays finite
+            scale16 /= 2
+            o, g, _ = run(mode, scale16)
+        if mode == "emu_fp16":
+            d["emu_fp16_scale"] = scale16
+        for k in ("classification_loss", "vae_loss", "total_loss"):
+            d[f"{mode}_{k}"] = o[k].float().item()
+        lg = o["logits"].detach().float()
+        d[f"{mode}_logits_rel"] = ((lg - o32["logits"].detach()).norm() / o32["logits"].detach().norm()).item()
+        d[f"{mode}_grad_rel"] = np.array([((a - b).norm() / b.norm().clamp_min(1e-30)).item() for a, b in zip(g, g32)])
+        print(f"classifier amp {mode}: {time.time() - t:.1f}s total={d[f'{mode}_total_loss']:.6f} "
+              f"(fp32 {d['fp32_total_loss']:.6f}) logits rel {d[f'{mode}_logits_rel']:.2e} grad rel median "
+              f"{np.median(d[f'{mode}_grad_rel']):.2e}")
+    save("seqvae_classifier_s16_b4_amp.npz", **d)
+
+
 GENS = dict(kat=gen_kymatio_kat, filters=gen_filters, scattering=gen_scattering, frontend=gen_frontend,
             stats=gen_stats_and_norm, model=gen_model, amp=gen_amp, te=gen_te, tiny=gen_tiny,
-            classifier=gen_classifier, traj=gen_traj, traj_lowlr=gen_traj_lowlr, model_big=lambda: gen_model((256, 300)))
+            classifier=gen_classifier, classifier_amp=gen_classifier_amp, traj=gen_traj, traj_lowlr=gen_traj_lowlr, model_big=lambda: gen_model((256, 300)))
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()

@@ -22,7 +22,7 @@ from golden_util import det_fill_  # noqa: E402
 from vaeteb.model import SeqVaeTeb  # noqa: E402
 from vaeteb.train import Trainer  # noqa: E402
 
-S, B = 64, 8
+S, B = int(os.environ.get("LB_S", 64)), int(os.environ.get("LB_B", 8))
 g = torch.Generator().manual_seed(7)
 batch = {"fhr_st": torch.randn(B, S, 43, generator=g), "fhr_ph": torch.randn(B, S, 44, generator=g),
          "fhr_up_ph": torch.randn(B, S, 130, generator=g), "fhr": torch.randn(B, 16 * S, generator=g)}

@@ -12,8 +12,10 @@
 //     counted vmcnt + raw s_barrier (the M = 256 shape is load-latency bound);
 //     rows are 128 B, 16-B chunks XOR-swizzled on the SOURCE address so the
 //     ds_read_b128 fragment reads are bank-conflict free;
-//   * split-K with a fixed-order slab reduction (deterministic) so that
-//     tiles x splits ~ the 256 CUs.
+//   * split-K so that tiles x splits ~ the 256 CUs; the split partials are combined by the
+//     workgroup of the tile that arrives last (common.h last_arrival), in the fixed split order
+//     (((p0 + p1) + p2) + ...) + bias, then + C — the order of the separate reduce pass this
+//     replaced (k_mfma_reduce4, 8 launches / 68 us per step in round 5), so the same bits.
 // Operand images: the weight side is a bf16 shadow of the fp32 master weights
 // (W for the forward, W^T for the input gradient) refreshed by
 // vt_mfma_weight_shadow; the activation side (X, dY, X^T, dY^T) is converted by
@@ -43,11 +45,39 @@ __device__ __forceinline__ void glds16(const __bf16* src, char* lds) {
                                      (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-// grid (N/64, Mpad/256, splits); K = reduction length of ONE split (multiple of 64)
+VT_ARRIVE_POOL(g_arrive_gemm);
+
+// b128 agent-coherent (sc1) accesses of the split partials
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_agent4(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, CPOL_SC1);
+}
+__device__ __forceinline__ f32x4 ld_agent4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, CPOL_SC1));
+}
+
+// common.h last_arrival with its flag in the kernel's (by then unused) dynamic LDS: the
+// operand stages take all 160 KB, so a static __shared__ word would not fit beside them
+__device__ __forceinline__ bool last_arrival_in(unsigned* ctr, unsigned total, unsigned* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // every wave is past its last LDS read of the stages
+    if (threadIdx.x == 0) {
+        const unsigned old = atomicAdd(ctr, 1u);
+        const bool last = old == total - 1;
+        if (last) atomicExch(ctr, 0u);
+        *flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return *flag != 0u;
+}
+
+// grid (N/64, Mpad/256, splits); K = reduction length of ONE split (multiple of 64).  splits > 1:
+// part holds tiles x splits slabs of 512 x 32 floats (a thread's 32 accumulators as 8 float4,
+// wave-contiguous), slot0 the tiles' arrival counters
 __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, int64_t lda,
                                                   const __bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                   float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
-                                                  int accumulate, float* __restrict__ part) {
+                                                  int accumulate, float* __restrict__ part, unsigned slot0) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sa = smem;                     // NA stages of A
     char* sb = smem + NA * A_BYTES;      // NB stages of B
@@ -125,76 +155,39 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the re-read DMAs before the block exits
 
+    if (part) {
+        // this split's partial, then the tile's last arrival sums the splits in index order
+        const int splits = gridDim.z, z = blockIdx.z;
+        const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+        const int64_t slab = (int64_t)QT * 32 * 4;                    // bytes per (tile, split)
+        const __amdgpu_buffer_rsrc_t pr = agent_rsrc(part + (int64_t)tile * splits * QT * 32, splits * slab);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) st_agent4(pr, (unsigned)(z * slab + (g * QT + tid) * 16), acc[g >> 2][g & 3]);
+        if (!last_arrival_in(&g_arrive_gemm[slot0 + tile], (unsigned)splits, (unsigned*)smem)) return;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            f32x4 s = z == 0 ? acc[g >> 2][g & 3] : ld_agent4(pr, (unsigned)((g * QT + tid) * 16));
+            for (int p = 1; p < splits; ++p)
+                s += p == z ? acc[g >> 2][g & 3] : ld_agent4(pr, (unsigned)(p * slab + (g * QT + tid) * 16));
+            acc[g >> 2][g & 3] = s;
+        }
+    }
     // C/D layout of 16x16x32: col = lane & 15, row = 4 * (lane >> 4) + r
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int col = n0 + 16 * j + lr;
-            const float bcol = (!part && bias) ? bias[col] : 0.f;
+            const float bcol = bias ? bias[col] : 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = m0 + 32 * w + 16 * i + 4 * lc + r;
                 if (row >= M) continue;
-                const float v = acc[i][j][r];
-                if (part) {
-                    part[((int64_t)blockIdx.z * M + row) * N + col] = v;
-                } else {
-                    float o = v + bcol;
-                    if (accumulate) o += C[(int64_t)row * ldc + col];
-                    C[(int64_t)row * ldc + col] = o;
-                }
+                float o = acc[i][j][r] + bcol;
+                if (accumulate) o = C[(int64_t)row * ldc + col] + o;
+                C[(int64_t)row * ldc + col] = o;
             }
         }
-}
-
-// fixed-order sum of the split slabs (+ bias, + C when accumulating)
-// one output per thread (any alignment)
-__global__ void k_mfma_reduce(const float* __restrict__ part, int splits, int64_t MN, int N, const float* bias,
-                              float* __restrict__ C, int accumulate) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= MN) return;
-    float s = 0.f;
-    for (int p = 0; p < splits; ++p) s += part[p * MN + i];
-    if (bias) s += bias[i % N];
-    C[i] = accumulate ? C[i] + s : s;
-}
-
-// Four consecutive outputs per thread (N a multiple of 64, ldc == N, C and bias 16-B aligned), every split's float4 in
-// flight before the first add; the same sum order as one element at a time:
-// (((0 + p_0) + p_1) + ...) + bias, then + C.
-template <int SPL>
-__global__ __launch_bounds__(256) void k_mfma_reduce4(const float* __restrict__ part, int splits, int64_t MN, int N,
-                                                      const float* bias, float* __restrict__ C, int accumulate) {
-    const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-    if (i >= MN) return;
-    const int ns = SPL ? SPL : splits;
-    float4 v[SPL ? SPL : 1];
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (SPL > 0) {
-#pragma unroll
-        for (int p = 0; p < SPL; ++p) v[p] = *(const float4*)(part + p * MN + i);
-#pragma unroll
-        for (int p = 0; p < SPL; ++p) {
-            s.x += v[p].x; s.y += v[p].y; s.z += v[p].z; s.w += v[p].w;
-        }
-    } else {
-        for (int p = 0; p < ns; ++p) {
-            const float4 q = *(const float4*)(part + p * MN + i);
-            s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
-        }
-    }
-    const int col = (int)(i % N);
-    if (bias) {
-        const float4 b = *(const float4*)(bias + col);
-        s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
-    }
-    float4* c = (float4*)(C + i);
-    if (accumulate) {
-        const float4 o = *c;
-        s.x = o.x + s.x; s.y = o.y + s.y; s.z = o.z + s.z; s.w = o.w + s.w;
-    }
-    *c = s;
 }
 
 // out[m][k] = bf16(X[m][k]) for m < M, k < K; zero in the padding (Mpad x Kpad)
@@ -371,7 +364,7 @@ static MfmaPlan plan(int64_t M, int N, int64_t K) {
     p.Kpad = up_to(K, QK);
     p.a_floats = up_to(p.Mpad * p.Kpad / 2, 64);
     p.splits = mfma_splits((p.Mpad / QM) * (N / QN), p.Kpad / QK);
-    p.part_floats = p.splits > 1 ? (int64_t)p.splits * M * N : 0;
+    p.part_floats = p.splits > 1 ? (int64_t)p.splits * p.Mpad * N : 0;   // tiles x splits x 512 x 32
     return p;
 }
 
@@ -388,21 +381,9 @@ static int run(const char* who, const __bf16* A, const __bf16* B, int64_t ldb, i
     }
     const int kper = (int)(p.Kpad / p.splits);
     dim3 grid(N / QN, (unsigned)(p.Mpad / QM), p.splits);
+    const unsigned tiles = grid.x * grid.y;
     hipLaunchKernelGGL(k_mfma_gemm, grid, dim3(QT), GEMM_LDS, st, A, p.Kpad, B, ldb, (int)M, N, kper, C, (int64_t)N,
-                       bias, accumulate, p.splits > 1 ? part : nullptr);
-    if (p.splits > 1) {
-        const int64_t MN = M * N;
-        const dim3 g((unsigned)((MN / 4 + 255) / 256));
-        if ((reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(bias)) & 15)
-            hipLaunchKernelGGL(k_mfma_reduce, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, part, p.splits, MN,
-                               N, bias, C, accumulate);
-        else if (p.splits == 4)
-            hipLaunchKernelGGL(k_mfma_reduce4<4>, g, dim3(256), 0, st, part, p.splits, MN, N, bias, C, accumulate);
-        else if (p.splits == 2)
-            hipLaunchKernelGGL(k_mfma_reduce4<2>, g, dim3(256), 0, st, part, p.splits, MN, N, bias, C, accumulate);
-        else
-            hipLaunchKernelGGL(k_mfma_reduce4<0>, g, dim3(256), 0, st, part, p.splits, MN, N, bias, C, accumulate);
-    }
+                       bias, accumulate, p.splits > 1 ? part : nullptr, p.splits > 1 ? arrive_slots(tiles) : 0u);
     VT_LAUNCH_CHECK(who);
     return VT_OK;
 }
