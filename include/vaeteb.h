@@ -43,6 +43,17 @@ int vt_stream_fork(void* from, void* to);
 int vt_stream_mark(void* stream, int* slot);
 int vt_stream_wait_mark(void* stream, int slot);
 int vt_abi_version(void);
+/* Zero every last-arriving-workgroup counter pool of the library (the in-kernel finalisers of
+ * the split sums, BatchNorm column sums and head GEMMs, csrc/common.h last_arrival), stream
+ * ordered.  A finished kernel leaves its counters at 0; after a failed or aborted launch a
+ * counter may not be, and the next kernel using it would elect the wrong last workgroup —
+ * call this (with nothing else in flight) to recover.  No reference counterpart (library
+ * hygiene).                                                                                 */
+int vt_arrive_reset(void* stream);
+/* Diagnostic: the hipGraph capture state of `stream` as text (status, capture id, node counts
+ * by type, the stream's current dependency nodes, kernel nodes with an empty grid) into buf[len]
+ * (tools/capture_probe.py).  No reference counterpart.                                        */
+int vt_capture_info(void* stream, char* buf, int len);
 
 /* ------------------------------------------------------------------ front-end
  * Twiddle tables `tw`: float2[n], tw[k] = exp(-2*pi*i*k/n) computed in fp64 on

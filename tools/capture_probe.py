@@ -17,6 +17,8 @@ first crash, as the GPU-box rules require).
     model_lstm       ... the LSTM weight-gradient branch only (side stream 2)
     model_head_norec ... the head branch with Tensor.record_stream disabled
     model_head_join  ... the head branch joined back to the main stream right after its kernel
+    model_head_info  ... model_head with the capture state dumped (VAETEB_CAPTURE_TRACE)
+    model_lstm_info  ... model_lstm with the capture state dumped (the branch that captures fine)
     unjoined_refork  s1 forked, kernel, NOT joined, forked again, kernel, joined (the head
                      branch's shape: side stream 1 is forked again by the encoders' backward)
 """
@@ -32,9 +34,14 @@ if variant.startswith("model_"):
     # (the production setting, dropped under capture); model_lstm: the LSTM weight gradients on
     # side stream 2 only
     os.environ["VAETEB_LSTM_GRAD_SIDE_STREAM"] = "0" if variant.startswith("model_head") else "2"
-    os.environ["VAETEB_HEAD_GRAD_SIDE_STREAM"] = "0" if variant == "model_lstm" else "1"
+    os.environ["VAETEB_HEAD_GRAD_SIDE_STREAM"] = "0" if variant.startswith("model_lstm") else "1"
     if variant == "model_head_join":
         os.environ["VAETEB_HEAD_GRAD_JOIN"] = "1"
+    if variant in ("model_head_info", "model_lstm_info"):
+        # round 6: the capture state (hipStreamGetCaptureInfo_v2, node types,
+        # dependency sets) of the side stream right after the head branch and of every stream
+        # before the capture ends, printed to stderr (vaeteb._lib.capture_info)
+        os.environ["VAETEB_CAPTURE_TRACE"] = "1"
 
 import torch  # noqa: E402
 

@@ -4,6 +4,8 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <utility>
+#include <vector>
 
 #include "common.h"
 
@@ -17,17 +19,40 @@ void set_error(const char* fmt, ...) {
     va_end(ap);
 }
 
-unsigned arrive_slots(unsigned n) {
-    static std::atomic<unsigned> next{0};
+unsigned arrive_slots(unsigned n, hipStream_t st) {
+    static std::atomic<unsigned> next[2];
+    constexpr unsigned HALF = ARRIVE_POOL / 2;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const int cap = (st && hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) ? 1 : 0;
     for (;;) {
-        const unsigned b = next.fetch_add(n) % ARRIVE_POOL;
-        if (b + n <= ARRIVE_POOL) return b;
+        const unsigned b = next[cap].fetch_add(n) % HALF;
+        if (b + n <= HALF) return b + cap * HALF;
     }
+}
+
+static std::vector<std::pair<const void*, size_t>>& arrive_pools() {
+    static std::vector<std::pair<const void*, size_t>> v;
+    return v;
+}
+int register_arrive_pool(const void* sym, size_t bytes) {
+    arrive_pools().emplace_back(sym, bytes);
+    return (int)arrive_pools().size();
 }
 }  // namespace vt
 
 extern "C" {
 const char* vt_last_error(void) { return vt::g_err; }
+
+int vt_arrive_reset(void* stream) {
+    for (const auto& [sym, bytes] : vt::arrive_pools()) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, sym) != hipSuccess || hipMemsetAsync(p, 0, bytes, vt::S(stream)) != hipSuccess) {
+            vt::set_error("vt_arrive_reset: cannot clear a counter pool");
+            return VT_ERR_HIP;
+        }
+    }
+    return VT_OK;
+}
 int vt_abi_version(void) { return 1; }
 }
 
@@ -142,4 +167,67 @@ extern "C" int vt_stream_fork(void* from, void* to) {
     int slot;
     const int rc = vt_stream_mark(from, &slot);
     return rc != VT_OK ? rc : vt_stream_wait_mark(to, slot);
+}
+
+// ------------------------------------------------------------ capture inspection
+// Diagnostic (tools/capture_probe.py model_head_info): the capture state of
+// `stream` — status, capture id, the captured graph's node count by type, the stream's current
+// dependency set (the nodes its next captured operation would depend on: type, and for kernel
+// nodes the grid / block / dynamic LDS), and every kernel node of the graph with an empty grid or
+// block — written as text into buf.  Reads the graph under capture, never modifies it.
+extern "C" int vt_capture_info(void* stream, char* buf, int len) {
+    if (!buf || len <= 0) return VT_ERR_ARG;
+    int o = 0;
+    auto put = [&](const char* fmt, auto... a) {
+        if (o < len) o += snprintf(buf + o, (size_t)(len - o), fmt, a...);
+    };
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    const hipError_t e = hipStreamGetCaptureInfo_v2((hipStream_t)stream, &st, &id, &g, &deps, &nd);
+    put("stream %p: %s status %d capture %llu", stream, hipGetErrorString(e), (int)st, id);
+    if (e != hipSuccess || st != hipStreamCaptureStatusActive || !g) return VT_OK;
+    auto kern = [&](hipGraphNode_t n) {
+        hipKernelNodeParams p{};
+        if (hipGraphKernelNodeGetParams(n, &p) == hipSuccess)
+            put(" kernel fn %p grid %ux%ux%u block %ux%ux%u lds %u", p.func, p.gridDim.x, p.gridDim.y, p.gridDim.z,
+                p.blockDim.x, p.blockDim.y, p.blockDim.z, p.sharedMemBytes);
+    };
+    size_t nn = 0;
+    (void)hipGraphGetNodes(g, nullptr, &nn);
+    std::vector<hipGraphNode_t> nodes(nn);
+    if (nn) (void)hipGraphGetNodes(g, nodes.data(), &nn);
+    int count[32] = {0}, empty_kernels = 0;
+    for (size_t i = 0; i < nn; ++i) {
+        hipGraphNodeType t = hipGraphNodeTypeEmpty;
+        (void)hipGraphNodeGetType(nodes[i], &t);
+        count[(int)t & 31]++;
+        if (t == hipGraphNodeTypeKernel) {
+            hipKernelNodeParams p{};
+            if (hipGraphKernelNodeGetParams(nodes[i], &p) == hipSuccess &&
+                (p.gridDim.x * p.gridDim.y * p.gridDim.z == 0 || p.blockDim.x * p.blockDim.y * p.blockDim.z == 0)) {
+                ++empty_kernels;
+                put("\n  EMPTY-GRID node %zu:", i);
+                kern(nodes[i]);
+            }
+        }
+    }
+    put("\n  graph %p: %zu nodes; by type:", (void*)g, nn);
+    for (int t = 0; t < 32; ++t)
+        if (count[t]) put(" [%d]=%d", t, count[t]);
+    put(" (0 kernel, 1 memcpy, 2 memset, 3 host, 4 graph, 5 empty, 6 wait-event, 7 event-record); empty grids %d",
+        empty_kernels);
+    put("\n  dependencies of the next captured op: %zu", nd);
+    for (size_t i = 0; i < nd; ++i) {
+        hipGraphNodeType t = hipGraphNodeTypeEmpty;
+        (void)hipGraphNodeGetType(deps[i], &t);
+        size_t ndep = 0, nchild = 0;
+        (void)hipGraphNodeGetDependencies(deps[i], nullptr, &ndep);
+        (void)hipGraphNodeGetDependentNodes(deps[i], nullptr, &nchild);
+        put("\n   dep %zu: node %p type %d (%zu deps, %zu dependents)", i, (void*)deps[i], (int)t, ndep, nchild);
+        if (t == hipGraphNodeTypeKernel) kern(deps[i]);
+    }
+    return VT_OK;
 }

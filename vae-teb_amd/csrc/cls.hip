@@ -1277,7 +1277,11 @@ int vt_zconv16_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int
     VT_CHECK_ARG(ws_floats >= G * n, "vt_zconv16_bwd_weight: workspace too small");
     hipStream_t st = S(stream);
     hipLaunchKernelGGL(k_zconv16_dw, dim3(G), dim3(D16T), 0, st, dY, ldy, X, ldx, B, L, Cin, Cout, K, pad_left, ws);
-    sum_splits_launch(ws, G, n, dW, accumulate, st, K, Cout, Cin);   // slab order [k][o][i] -> dW [o][i][k]
+    const int rc = sum_splits_launch(ws, G, n, dW, accumulate, st, K, Cout, Cin);   // slab order [k][o][i] -> dW [o][i][k]
+    if (rc) {
+        set_error("vt_zconv16_bwd_weight: %d weight-gradient slabs exceed the split sum's limit", G);
+        return rc;
+    }
     VT_LAUNCH_CHECK("vt_zconv16_bwd_weight");
     return VT_OK;
 }
@@ -1299,7 +1303,11 @@ int vt_zconv_bwd_weight(const float* dY, int ldy, const float* X, int ldx, int B
     VT_CHECK_ARG(ws_floats >= G * n, "vt_zconv_bwd_weight: workspace too small");
     hipStream_t st = S(stream);
     hipLaunchKernelGGL(k_zconv_dw, dim3(G), dim3(DT), 0, st, dY, ldy, X, ldx, B, L, Cin, Cout, K, pad_left, ws);
-    sum_splits_launch(ws, G, n, dW, accumulate, st);
+    const int rc = sum_splits_launch(ws, G, n, dW, accumulate, st);
+    if (rc) {
+        set_error("vt_zconv_bwd_weight: %d weight-gradient slabs exceed the split sum's limit", G);
+        return rc;
+    }
     VT_LAUNCH_CHECK("vt_zconv_bwd_weight");
     return VT_OK;
 }

@@ -33,8 +33,15 @@ const void* bucket_marker_kernel();
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// n consecutive arrival counters of a VT_ARRIVE_POOL (round-robin; n <= ARRIVE_POOL / 4)
-unsigned arrive_slots(unsigned n);
+// n consecutive arrival counters of a VT_ARRIVE_POOL (round-robin; n <= ARRIVE_POOL / 8).  Launches
+// enqueued on a capturing stream draw from the upper half of the pool, all others from the lower
+// half: counters baked into a captured step are never handed to an eager launch, however many
+// eager launches wrap their half, so an eager kernel on another stream cannot share a counter with
+// a replay running beside it.  (Two captures share the upper half: their graphs are replayed one
+// at a time.)
+unsigned arrive_slots(unsigned n, hipStream_t st);
+// host shadow of a VT_ARRIVE_POOL, registered at load time for vt_arrive_reset
+int register_arrive_pool(const void* sym, size_t bytes);
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -57,9 +64,17 @@ __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2
 // pool of zero-initialised device words (VT_ARRIVE_POOL); the last arrival resets its counter,
 // so a counter is zero again whenever its kernel has finished (graph replays reuse the same
 // slots).  Host side: arrive_slots() hands out disjoint runs round-robin, so kernels that may
-// run concurrently on different streams never share one.
+// run concurrently on different streams never share one; vt_arrive_reset zeroes every pool
+// after a failed launch.
+// INVARIANT: every cross-workgroup partial a finaliser reads is written with st_agent and read
+// with ld_agent (sc1: past the XCD's L2).  There is no release / acquire fence, so a plain load
+// or store of a partial (another XCD's L2 may hold a stale line) would silently break the
+// reduction: k_sum_splits_grp, bn_fold_finalize / k_col_partial4 and k_mfma_gemm keep to it.
 constexpr unsigned ARRIVE_POOL = 1u << 16;
-#define VT_ARRIVE_POOL(name) static __device__ unsigned name[::vt::ARRIVE_POOL]
+#define VT_ARRIVE_POOL(name)                                 \
+    static __device__ unsigned name[::vt::ARRIVE_POOL];      \
+    [[maybe_unused]] static const int name##_registered =    \
+        ::vt::register_arrive_pool((const void*)&name, sizeof(unsigned) * ::vt::ARRIVE_POOL)
 
 // agent-coherent (sc1) buffer accesses of a partial-result array: a descriptor over the array
 // (uniform base) and per-lane byte offsets

@@ -551,7 +551,7 @@ int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int 
     float* p = const_cast<float*>(part);
     const unsigned bx = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_sum_splits_grp, dim3(bx, (unsigned)((splits + SG_GRP - 1) / SG_GRP)), dim3(256), 0, st, p,
-                       splits, n, out, accumulate, arrive_slots(bx), pm);
+                       splits, n, out, accumulate, arrive_slots(bx, st), pm);
     return VT_OK;
 }
 
@@ -654,7 +654,10 @@ int vt_conv1d_direct_bwd_weight(const float* dY, const float* X, int B, int L_in
     VT_CONV_DW(7, 1) VT_CONV_DW(7, 3) VT_CONV_DW(8, 1) VT_CONV_DW(8, 2) VT_CONV_DW(9, 1) VT_CONV_DW(9, 2)
     VT_CONV_DW(10, 1) VT_CONV_DW(10, 2) VT_CONV_DW(11, 1) VT_CONV_DW(11, 2)
 #undef VT_CONV_DW
-    sum_splits_launch(ws, (int)splits, nout, dW, accumulate, st);
+    if (const int rc = sum_splits_launch(ws, (int)splits, nout, dW, accumulate, st)) {
+        set_error("vt_conv1d_direct_bwd_weight: %d weight-gradient slabs exceed the split sum's limit", (int)splits);
+        return rc;
+    }
     VT_LAUNCH_CHECK("vt_conv1d_direct_bwd_weight");
     return VT_OK;
 }

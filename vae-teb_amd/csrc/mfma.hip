@@ -383,7 +383,7 @@ static int run(const char* who, const __bf16* A, const __bf16* B, int64_t ldb, i
     dim3 grid(N / QN, (unsigned)(p.Mpad / QM), p.splits);
     const unsigned tiles = grid.x * grid.y;
     hipLaunchKernelGGL(k_mfma_gemm, grid, dim3(QT), GEMM_LDS, st, A, p.Kpad, B, ldb, (int)M, N, kper, C, (int64_t)N,
-                       bias, accumulate, p.splits > 1 ? part : nullptr, p.splits > 1 ? arrive_slots(tiles) : 0u);
+                       bias, accumulate, p.splits > 1 ? part : nullptr, p.splits > 1 ? arrive_slots(tiles, st) : 0u);
     VT_LAUNCH_CHECK(who);
     return VT_OK;
 }

@@ -996,7 +996,7 @@ static void col_partial_fin(int kind, const float* x, const float* dy, int64_t M
     if (C <= 128 && g_bn_fold) {
         const int ng = (blocks + BN_GB - 1) / BN_GB;
         f.gpart = reinterpret_cast<double*>(ws + (((int64_t)2 * C * blocks + 1) & ~(int64_t)1));
-        f.slot0 = arrive_slots((unsigned)ng + 1);
+        f.slot0 = arrive_slots((unsigned)ng + 1, st);
         col_partial_vec(kind, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, f, dr);
     } else {
         col_partial_vec(kind, x, dy, M, C, rpb, blocks, mean, rstd, gamma, beta, act, ws, st, no_fin(), dr);

@@ -130,6 +130,16 @@ def wait_for(waiter, src=None):
             raise RuntimeError(f"vt_stream_fork: {lib().last_error()}")
 
 
+def capture_info(src=None):
+    """Diagnostic: the hipGraph capture state of stream `src` (default: the current stream) as
+    text — vt_capture_info (tools/capture_probe.py)."""
+    import ctypes
+    buf = ctypes.create_string_buffer(1 << 16)
+    s = stream() if src is None else (src if isinstance(src, int) else src.cuda_stream)
+    call("vt_capture_info", s, buf, len(buf))
+    return buf.value.decode()
+
+
 def mark(src=None):
     """A pooled event recorded on `src` (default: the current stream); see wait_mark."""
     import ctypes

@@ -325,6 +325,8 @@ def fit(module, train_loader, max_epochs=1, gradient_clip_val=0.5, val_loader=No
             # Lightning validates in eval mode: BatchNorm uses (and does not update)
             # its running statistics
             module.eval()
+            if buckets is not None and bsync is not None:
+                bsync()   # DDP broadcasts buffers before an eval forward too: rank 0's statistics
             for i, batch in enumerate(val_loader):
                 with torch.no_grad():
                     module.validation_step(mv(batch), i)

@@ -78,6 +78,8 @@ def train_base_model_pytorch(trainer, train_loader, validation_loader, epochs, c
             L = trainer.step(mv(batch))
             tr_sum += torch.stack([L[k].detach().to(torch.float64).reshape(()) for k in KEYS])
         model.eval()
+        if getattr(trainer, "buffer_sync", None) is not None:
+            trainer.buffer_sync()   # DDP broadcast_buffers applies to the eval forward too (rank 0's stats)
         va_sum = torch.zeros(len(KEYS), dtype=torch.float64, device=dev)
         with torch.no_grad():
             for batch in validation_loader:

@@ -366,7 +366,11 @@ class ConvStack(nn.Sequential):
         blocks = list(self)
         if not (CONV_FOLD and len(blocks) > 1 and x.is_cuda and
                 all(isinstance(b, ConvBlock) and b.training and b.bf16 and not b.sync_bn for b in blocks) and
-                not any(b.tanh for b in blocks[:-1])):   # the staging applies the inner blocks' ReLU
+                not any(b.tanh for b in blocks[:-1]) and   # the staging applies the inner blocks' ReLU
+                # a folded block's backward needs its input's gradient (the fused bf16 path): every
+                # inner output must require grad, else the unfolded stack runs (checked here, before
+                # the forward updates the running statistics, not as an error in the backward)
+                torch.is_grad_enabled() and all(b.conv.weight.requires_grad for b in blocks[:-1])):
             return super().forward(x)
         xin = None
         for i, blk in enumerate(blocks):

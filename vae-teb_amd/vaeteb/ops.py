@@ -36,6 +36,7 @@ class _Workspace:
 
 
 WS = _Workspace()
+CAPTURE_TRACE = os.environ.get("VAETEB_CAPTURE_TRACE", "0") == "1"   # diagnostic: capture state dumps
 WS_LINEAR = 1 << 25  # 128 MiB of split-K partials (a 4096x4097 head gradient fits unsplit)
 
 
@@ -304,6 +305,10 @@ class LinearF(torch.autograd.Function):
                          ptr(ws_s), ws_s.numel(), _st())
                 gy2.record_stream(side)
                 x2.record_stream(side)
+                if CAPTURE_TRACE and torch.cuda.is_current_stream_capturing():   # diagnostic (capture_probe.py)
+                    import sys
+                    print(f"[capture] head branch enqueued on side stream:\n{_lib.capture_info(side)}\n"
+                          f"[capture] the decoder's stream:\n{_lib.capture_info()}", file=sys.stderr, flush=True)
                 if HEAD_GRAD_JOIN:   # diagnostic (tools/capture_probe.py model_head_join)
                     _lib.wait_for(_lib.stream(), side)
             else:

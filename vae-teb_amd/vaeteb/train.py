@@ -175,8 +175,11 @@ class BufferBroadcast:
     """DistributedDataParallel's `broadcast_buffers=True` — the default of the reference's DDP
     wrap (ref/model/graph_model.py:644) and of Lightning's DDPStrategy (:470-471): before every
     training forward, rank `src`'s floating buffers (BatchNorm running mean / variance) overwrite
-    every other rank's, so ranks never drift apart and checkpoints / eval-mode validation see
-    rank 0's statistics on every rank.  One collective per step: the buffers are rebound as views
+    every other rank's, so ranks never drift apart.  DDP broadcasts before an eval forward as well:
+    the epoch driver (loop.train_base_model_pytorch) and lightning.fit call it before their
+    validation passes, so eval-mode validation sees rank 0's statistics on every rank; after the
+    last training step each rank holds its own step's update until the next call (a checkpoint is
+    written by rank 0, whose statistics these are).  One collective per call: the buffers are rebound as views
     of one flat tensor (state_dict keys and values unchanged; rebound again if a buffer is
     replaced, e.g. by .to() or load_state_dict(assign=True)).  The step counters
     (num_batches_tracked) advance identically on every rank and are not sent."""
@@ -632,6 +635,13 @@ class Trainer:
                     self._update()
                 if CAPTURE_JOIN:
                     _join_side_streams()
+                if os.environ.get("VAETEB_CAPTURE_TRACE", "0") == "1":   # diagnostic (capture_probe.py)
+                    import sys
+                    from . import ops
+                    from ._lib import capture_info
+                    for st in [torch.cuda.current_stream(), *ops.SIDE_STREAMS]:
+                        print(f"[capture] before end, {'capture' if st == torch.cuda.current_stream() else 'side'} "
+                              f"stream:\n{capture_info(st)}", file=sys.stderr, flush=True)
         finally:
             if self.buckets is not None:
                 self.buckets.mark_capture = False
