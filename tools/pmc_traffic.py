@@ -30,7 +30,7 @@ def per_instance(path, pats, counter):
     return acc
 
 
-def roofline_kernel(d, kernel, out):
+def roofline_kernel(d, kernel, out, command=None):
     f = per_instance(os.path.join(d, "fetch_counter_collection.csv"), [kernel], "FETCH_SIZE")
     w = per_instance(os.path.join(d, "write_counter_collection.csv"), [kernel], "WRITE_SIZE")
     fv = [x for v in f.values() for x in v]
@@ -40,8 +40,8 @@ def roofline_kernel(d, kernel, out):
            "WRITE_SIZE_kib_raw": sum(wv) / len(wv), "fetch_bytes": fetch_b, "write_bytes": write_b,
            "traffic_bytes_per_launch": fetch_b + write_b,
            "correction": "FETCH_SIZE x2 (gfx950 half-counts wide reads), KiB -> bytes",
-           "command": "rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-trace -- python3 bench.py --steps 2 "
-                      "--warmup 1 --no-cpu-baseline (tools/gpu_prof.sh)"}
+           "command": command or "rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-trace -- python3 bench.py --steps 2 "
+                                 "--warmup 1 --no-cpu-baseline (tools/gpu_prof.sh)"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
@@ -78,8 +78,9 @@ if __name__ == "__main__":
     ap.add_argument("--kernels", nargs="*")
     ap.add_argument("--durations")
     ap.add_argument("--out")
+    ap.add_argument("--command", help="the profiled command, recorded in the roofline-kernel JSON")
     a = ap.parse_args()
     if a.kernels:
         kernels(a.dir, a.kernels, a.durations, a.out)
     else:
-        roofline_kernel(a.dir, a.kernel, a.out_json)
+        roofline_kernel(a.dir, a.kernel, a.out_json, a.command)
