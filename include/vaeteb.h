@@ -615,6 +615,27 @@ int vt_lstm16_pair_bwd(const float* dh_out, const float* gates1, const float* c1
                        const float* w_ih1, const float* gates0, const float* c0, const float* w_hh0,
                        const float* w_ih0, int In0, int B, int seq, int hidden, float* dgates1, float* dgates0,
                        float* dx, void* stream);
+/* All four layers of nn.LSTM(num_layers=4) in ONE launch (round 6): the two layer pairs of
+ * vt_lstm16_pair_fwd run concurrently, pair 1 (layers 2, 3) consuming layer 1's h chunk by
+ * chunk as pair 0 publishes it (a per-chunk flag; agent-coherent stores / loads) — S + 4
+ * chunks of steps instead of 2 (S + 1 chunk).  params: the 16 pointers [w_ih, w_hh, b_ih,
+ * b_hh] of layers 0..3; outs: the 12 pointers [h, c, gates] of layers 0..3.  Outputs are
+ * exactly two vt_lstm16_pair_fwd calls', bit for bit (which it runs instead when the
+ * workgroups per pair are not a multiple of 8, or VAETEB_L16_CHAIN=0).
+ * replaces: nn.LSTM(in, 64, 4 layers) under torch.amp.autocast (vae_teb_model.py:474-480,
+ *           :647-653)                                                                   */
+int vt_lstm16_quad_fwd(const float* x, int In, const float* const* params, int B, int seq, int hidden,
+                       float* const* outs, void* stream);
+/* Its backward in one launch: layers 3, 2 (dh_out at layer 3's outputs) publish layer 2's dX —
+ * the gradient at layer 1's outputs, written to dmid [B, S, hidden] — chunk by chunk to layers
+ * 1, 0 running concurrently.  w: [w_ih, w_hh] x 4 layers; gc: [gates, c] x 4 layers (the
+ * forward's); dg: the 4 layers' dgates [B, S, 4 hidden]; dx: layer 0's input gradient [B, S,
+ * In0] (may be null).  Exactly two vt_lstm16_pair_bwd calls', bit for bit.                */
+int vt_lstm16_quad_bwd(const float* dh_out, const float* const* w, const float* const* gc, int In0, int B, int seq,
+                       int hidden, float* const* dg, float* dmid, float* dx, void* stream);
+/* Timeouts of the chained launches' bounded waits since the last reset (0 unless a producer
+ * workgroup could not run; host-synchronous diagnostic).                                  */
+int vt_lstm16_chain_errors(int* count, int reset);
 /* All of a layer's parameter gradients in one pass over dgates [B*S, 4H]:
  * dw_ih (+)= dgates^T x, dw_hh (+)= dgates^T h_{t-1}, db_ih and db_hh (may be
  * null) (+)= column sums of dgates.  In + hidden + 1 <= 144; ws: at least

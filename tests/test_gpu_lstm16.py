@@ -274,6 +274,8 @@ def test_lstm16_pair_bitwise_per_layer(ops, monkeypatch, In, B, S, nl):
     gy = torch.randn(B, S, 64, device="cuda")
     outs, names = [], []
     real_call = ops.call
+    monkeypatch.setattr(ops, "LSTM_CHAIN_FWD", 0)   # the pair launches themselves (chained: the test below)
+    monkeypatch.setattr(ops, "LSTM_CHAIN_BWD", 0)
     for pair in (0, 1):
         monkeypatch.setattr(ops, "LSTM_PAIR", pair)
         called = []
@@ -289,3 +291,44 @@ def test_lstm16_pair_bitwise_per_layer(ops, monkeypatch, In, B, S, nl):
     assert names[1].count("vt_lstm16_pair_fwd") == nl // 2 and names[1].count("vt_lstm16_pair_bwd") == nl // 2
     for k, (a, b) in enumerate(zip(*outs)):
         assert torch.equal(a, b), (k, (a != b).sum().item(), (a - b).abs().max().item())
+
+
+@pytest.mark.parametrize("In,B,S", [(20, 256, 256), (32, 256, 256), (20, 256, 300), (32, 64, 17), (20, 6, 40)])
+def test_lstm16_quad_chained_bitwise_pairs(ops, monkeypatch, In, B, S):
+    """vt_lstm16_quad_fwd / _bwd (round 6: the encoder's four layers in one launch each way, pair
+    (2, 3) consuming layer 1's h — and in the backward layers (1, 0) consuming layer 2's dX — chunk
+    by chunk through per-chunk flags) == the two pair launches bit for bit: output, dx and every
+    parameter gradient; at the bench geometry (B = 256: 128 workgroups per pair, chained), S = 300,
+    S not a multiple of the chunk, and B = 6 (3 workgroups per pair: not a multiple of 8, so the
+    library runs the pairs one after the other).  Repeated twice in the process (the flags are left
+    zero for the next launch), and no bounded wait timed out."""
+    import ctypes
+    from vaeteb import _lib
+    torch.manual_seed(5 + In + S + B)
+    ref = torch.nn.LSTM(In, 64, 4, batch_first=True)
+    params = [p.detach().cuda() for p in ref.parameters()]
+    x = torch.randn(B, S, In, device="cuda")
+    gy = torch.randn(B, S, 64, device="cuda")
+    cnt = ctypes.c_int()
+    _lib.call("vt_lstm16_chain_errors", ctypes.byref(cnt), 1)
+    outs, names = [], []
+    real_call = ops.call
+    for chain in (0, 1, 1):
+        monkeypatch.setattr(ops, "LSTM_CHAIN_FWD", chain)
+        monkeypatch.setattr(ops, "LSTM_CHAIN_BWD", chain)
+        called = []
+        monkeypatch.setattr(ops, "call", lambda name, *a: (called.append(name), real_call(name, *a))[1])
+        pd = [p.clone().requires_grad_() for p in params]
+        xd = x.clone().requires_grad_()
+        y = ops.lstm(xd, pd, half=True)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        outs.append([y.detach(), xd.grad] + [p.grad for p in pd])
+        names.append(called)
+    assert names[0].count("vt_lstm16_pair_fwd") == 2 and "vt_lstm16_quad_fwd" not in names[0]
+    assert names[1].count("vt_lstm16_quad_fwd") == 1 and names[1].count("vt_lstm16_quad_bwd") == 1
+    _lib.call("vt_lstm16_chain_errors", ctypes.byref(cnt), 1)
+    assert cnt.value == 0, cnt.value
+    for run in (1, 2):
+        for k, (a, b) in enumerate(zip(outs[0], outs[run])):
+            assert torch.equal(a, b), (run, k, (a != b).sum().item(), (a - b).abs().max().item())

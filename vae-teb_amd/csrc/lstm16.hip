@@ -38,6 +38,12 @@ static constexpr int H = 64;
 static constexpr int G4 = 4 * H;
 static constexpr int TC = 16;   // steps per chunk
 
+// flags of the chained launches (k_lstm16_fwd4 / _bwd4): T x nch words per launch from a pool
+// (arrive_slots: launches on different streams never share them), and the bounded waits'
+// timeout counter (vt_lstm16_chain_errors)
+VT_ARRIVE_POOL(g_chain_flags);
+static __device__ unsigned g_chain_err[1];
+
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -248,17 +254,43 @@ __host__ __device__ constexpr int64_t fwd2_stage_bytes(int ns, int S) {
     return (int64_t)ns * ((S + TC - 1) / TC) * TC * HX * 2;
 }
 
-template <int NS, int KX, int ROLE>
+// Chained layer pairs (round 6): the four layers of an encoder in ONE
+// launch, pair 0 (layers 0, 1) in workgroups [0, T) and pair 1 (layers 2, 3) in [T, 2T), tile b's
+// consumer at b + T.  Pair 0's upper layer publishes each finished 16-step chunk of its h —
+// agent-coherent (sc1) stores, a wait for them, then a per-(tile, chunk) flag — and pair 1's lower
+// layer stages that chunk into its input image when the flag is up (sc1 loads), instead of waiting
+// for the whole first launch: 4 layers in S + 4 chunks of steps instead of 2 (S + 1 chunk).  A
+// consumer only waits on a workgroup of LOWER index (in-order dispatch: resident or finished,
+// and with T a multiple of 8 on the same XCD), producers never wait: no deadlock whatever the
+// occupancy; the waits are bounded anyway (a timeout counts an error, vt_lstm16_chain_errors).
+// CH: 0 an independent pair, 1 producer, 2 consumer.
+constexpr unsigned CHAIN_SPIN_MAX = 1u << 23;   // ~0.5 s of polling, then give up (counted)
+
+__device__ __forceinline__ void chain_wait(unsigned* flag, unsigned* err) {
+    unsigned n = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++n > CHAIN_SPIN_MAX) {
+            if ((threadIdx.x & 63) == 0) atomicAdd(err, 1u);
+            break;
+        }
+    }
+}
+
+template <int NS, int KX, int ROLE, int CH = 0>
 __device__ __forceinline__ void fwd2_role(int In, const float* __restrict__ wih, const float* __restrict__ bih,
                                           const float* __restrict__ whh, const float* __restrict__ bhh, int B, int S,
                                           float* __restrict__ out_h, float* __restrict__ out_c,
-                                          float* __restrict__ gates, _Float16 (*hs)[NS][HS], const _Float16* ximg,
-                                          _Float16 (*himg)[NS][TC][HX]) {
+                                          float* __restrict__ gates, _Float16 (*hs)[NS][HS], _Float16* ximg,
+                                          _Float16 (*himg)[NS][TC][HX], int tile = 0, unsigned* flags = nullptr,
+                                          unsigned* err = nullptr, const float* __restrict__ xin = nullptr) {
     const int j = threadIdx.x & (G4 - 1), lane = j & 63, w = j >> 6, ln = lane & 15, lg = lane >> 4;
     const int u = 16 * w + ln;
     const int sl = lg & (NS - 1), sa = (ln >> 2) & (NS - 1);
     const bool wr = NS == 4 || lg < NS;
-    const int b0 = blockIdx.x * NS;
+    const int b0 = (CH ? tile : (int)blockIdx.x) * NS;
+    // producer's upper layer: h through the coherence point (the consumer may sit on another XCD)
+    const __amdgpu_buffer_rsrc_t hrs = agent_rsrc(out_h, (int64_t)B * S * H * 4);
     const int64_t ob = (int64_t)(b0 + sl < B ? b0 + sl : B - 1) * S;
     f16x8 bh[4][2];
     f16x8 bx[4][KX];
@@ -291,6 +323,30 @@ __device__ __forceinline__ void fwd2_role(int In, const float* __restrict__ wih,
         const int ch = ROLE == 0 ? k : k - 1;   // this role's chunk in period k
         const bool act = ch >= 0 && ch < nch;   // block-uniform per role
         const int n = act ? (S - TC * ch < TC ? S - TC * ch : TC) : 0;
+        if constexpr (CH == 2) {
+            // consumer: this chunk of the producer's h (its input), f16 as the staging of the
+            // independent pair converts it, once its flag is up
+            if (ROLE == 0 && act) {
+                unsigned* fl = flags + tile * nch + ch;
+                chain_wait(fl, err);
+                typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+                const __amdgpu_buffer_rsrc_t xr = agent_rsrc(xin, (int64_t)B * S * In * 4);
+                const int i4 = In >> 2, per = TC * i4;
+                for (int q = j; q < NS * per; q += G4) {
+                    const int s_ = q / per, rem = q - s_ * per, tt = rem / i4, k4 = rem - tt * i4, t = TC * ch + tt;
+                    const int bs = b0 + s_ < B ? b0 + s_ : B - 1;
+                    if (t < S) {
+                        const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                            xr, (int)((((int64_t)bs * S + t) * In + 4 * k4) * 4), 0, CPOL_SC1));
+                        *reinterpret_cast<f16x4*>(ximg + ((int64_t)s_ * nch * TC + t) * HX + 4 * k4) =
+                            f16x4{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();   // the chunk's input image complete (both roles: one barrier more per period)
+            if (ROLE == 0 && act && j == 0) atomicExch(flags + tile * nch + ch, 0u);   // every wave saw it
+        }
         if (act) {
             // the chunk's input projection from its 16-bit image: A rows (sample sa, step
             // 4 m + (ln & 3)), k = 32 ks + 8 lg + e (zero columns past In)
@@ -338,11 +394,21 @@ __device__ __forceinline__ void fwd2_role(int In, const float* __restrict__ wih,
                 }
                 if (wr) {
                     *reinterpret_cast<float4*>(gates + ((ob + t) * H + u) * 4) = make_float4(gi, gf, gg, go);
-                    out_h[(ob + t) * H + u] = hn;
+                    if (CH == 1 && ROLE == 1)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hn), hrs,
+                                                              (int)(((ob + t) * H + u) * 4), 0, CPOL_SC1);
+                    else
+                        out_h[(ob + t) * H + u] = hn;
                     out_c[(ob + t) * H + u] = c;
                 }
             }
             lds_barrier();
+        }
+        if constexpr (CH == 1) {
+            // producer: the chunk's h stores have reached the coherence point, then its flag
+            if (ROLE == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();
+            if (ROLE == 1 && act && j == 0) atomicAdd(flags + tile * nch + ch, 1u);
         }
     }
 }
@@ -405,6 +471,90 @@ __global__ __launch_bounds__(2 * G4) void k_lstm16_fwd2(const float* __restrict_
         fwd2_role<NS, KXA, 0>(In, wihA, bihA, whhA, bhhA, B, S, hA, cA, gA, hsA, ximg, himg);
     else
         fwd2_role<NS, 2, 1>(H, wihB, bihB, whhB, bhhB, B, S, hB, cB, gB, hsB, ximg, himg);
+}
+
+// the four layers' parameters [w_ih, w_hh, b_ih, b_hh] x 4 (the Python flat list's order) and
+// outputs [h, c, gates] x 4 of a chained launch
+struct Quad {
+    const float* p[16];
+    float* o[12];
+};
+
+// zero the recurrence images and the staged input image, then (stage) the tile's whole input
+// x [B, S, In] in f16 (k_lstm16_fwd2's prologue)
+template <int NS>
+__device__ __forceinline__ void fwd2_prologue(const float* __restrict__ x, int In, int B, int S, int b0, bool stage,
+                                              _Float16 (*hsA)[NS][HS], _Float16 (*hsB)[NS][HS], _Float16* ximg) {
+    const int nch = (S + TC - 1) / TC, rows = NS * nch * TC;
+    for (int i = threadIdx.x; i < 2 * NS * HS; i += 2 * G4) {
+        (&hsA[0][0][0])[i] = (_Float16)0.f;
+        (&hsB[0][0][0])[i] = (_Float16)0.f;
+    }
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    for (int i = threadIdx.x; i < rows * HX / 4; i += 2 * G4)
+        reinterpret_cast<f16x4*>(ximg)[i] = f16x4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+    lds_barrier();
+    if (stage) {
+        const int i4 = In >> 2;
+        const int per = S * i4, total = NS * per;
+        constexpr int U = 8;
+        for (int q0 = threadIdx.x; q0 < total; q0 += U * 2 * G4) {
+            float4 v[U];
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const int q = q0 + r * 2 * G4;
+                const int s = q / per, rem = q - s * per, t = rem / i4, k4 = rem - t * i4;
+                const int bs = b0 + s < B ? b0 + s : B - 1;
+                v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (q < total) v[r] = *reinterpret_cast<const float4*>(x + ((int64_t)bs * S + t) * In + 4 * k4);
+            }
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const int q = q0 + r * 2 * G4;
+                const int s = q / per, rem = q - s * per, t = rem / i4, k4 = rem - t * i4;
+                if (q < total)
+                    *reinterpret_cast<f16x4*>(ximg + ((int64_t)s * nch * TC + t) * HX + 4 * k4) =
+                        f16x4{(_Float16)v[r].x, (_Float16)v[r].y, (_Float16)v[r].z, (_Float16)v[r].w};
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+}
+
+// four layers in one launch (see fwd2_role): workgroups [0, T) run layers 0, 1 of tile b (the
+// producer: the staged input x [B, S, In], In <= 32 KXA), [T, 2T) layers 2, 3 of tile b - T (the
+// consumer: its input, layer 1's h, staged chunk by chunk as published).  slot0: T x nch zeroed
+// words of g_chain_flags (left zero by the consumers).  Same arithmetic
+// per role as two k_lstm16_fwd2 launches: the same bits.
+template <int NS, int KXA>
+__global__ __launch_bounds__(2 * G4) void k_lstm16_fwd4(const float* __restrict__ x, int In, Quad q, int B, int S,
+                                                        int T, unsigned slot0) {
+    unsigned* flags = g_chain_flags + slot0;
+    unsigned* err = g_chain_err;
+    __shared__ __attribute__((aligned(16))) _Float16 hsA[2][NS][HS];
+    __shared__ __attribute__((aligned(16))) _Float16 hsB[2][NS][HS];
+    __shared__ __attribute__((aligned(16))) _Float16 himg[2][NS][TC][HX];
+    extern __shared__ __attribute__((aligned(16))) _Float16 ximg[];
+    const bool cons = (int)blockIdx.x >= T;
+    const int tile = cons ? (int)blockIdx.x - T : (int)blockIdx.x;
+    fwd2_prologue<NS>(x, In, B, S, tile * NS, !cons, hsA, hsB, ximg);
+    const bool A = threadIdx.x < G4;
+    if (!cons) {
+        if (A)
+            fwd2_role<NS, KXA, 0, 1>(In, q.p[0], q.p[2], q.p[1], q.p[3], B, S, q.o[0], q.o[1], q.o[2], hsA, ximg,
+                                     himg, tile, flags, err);
+        else
+            fwd2_role<NS, 2, 1, 1>(H, q.p[4], q.p[6], q.p[5], q.p[7], B, S, q.o[3], q.o[4], q.o[5], hsB, ximg, himg,
+                                   tile, flags, err);
+    } else {
+        if (A)
+            fwd2_role<NS, 2, 0, 2>(H, q.p[8], q.p[10], q.p[9], q.p[11], B, S, q.o[6], q.o[7], q.o[8], hsA, ximg,
+                                   himg, tile, flags, err, q.o[3]);
+        else
+            fwd2_role<NS, 2, 1, 2>(H, q.p[12], q.p[14], q.p[13], q.p[15], B, S, q.o[9], q.o[10], q.o[11], hsB, ximg,
+                                   himg, tile, flags, err);
+    }
 }
 
 static constexpr int DS = G4 + 8;   // bf16 row stride of the dg image (528 B)
@@ -587,19 +737,25 @@ __global__ __launch_bounds__(G4) void k_lstm16_bwd(const float* __restrict__ dh_
 // to L through an LDS image (fp32, [NS][TC][H]) instead of HBM; L reads it one step at a
 // time.  Per role the arithmetic is k_lstm16_bwd's instruction for instruction, so dgates of
 // both layers and L's dX are bit-identical to two vt_lstm16_layer_bwd calls.
-template <int NS, int NTX, int ROLE>
+// CH (chained backward, k_lstm16_bwd4): 1 = the upper pair (layers 3, 2), whose lower role publishes
+// its dX chunk by chunk (sc1 stores, a wait, the chunk's flag); 2 = the lower pair (layers 1, 0),
+// whose upper role reads dh_out (= that dX) with sc1 loads, each chunk after its flag is up.
+template <int NS, int NTX, int ROLE, int CH = 0>
 __device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, const float* __restrict__ gates,
                                           const float* __restrict__ cst, const float* __restrict__ whh,
                                           const float* __restrict__ wih, int In, int B, int S,
                                           float* __restrict__ dgates, float* __restrict__ dx,
                                           __bf16 (*dgs)[TC][NS][DS], float (*dximg)[NS][TC][H],
-                                          __bf16 (*wT)[DS]) {
+                                          __bf16 (*wT)[DS], int tile = 0, unsigned* flags = nullptr,
+                                          unsigned* err = nullptr) {
     const int j = threadIdx.x & (G4 - 1), lane = j & 63, w = j >> 6, ln = lane & 15, lg = lane >> 4;
     const int u = 16 * w + ln;
     const int sl = lg & (NS - 1), sa = (ln >> 2) & (NS - 1);
     const bool wr = NS == 4 || lg < NS;
     constexpr int RPS = 16 / NS, MT = TC * NS / 16;
-    const int b0 = blockIdx.x * NS;
+    const int b0 = (CH ? tile : (int)blockIdx.x) * NS;
+    const int nchk = (S + TC - 1) / TC;
+    const __amdgpu_buffer_rsrc_t drs = agent_rsrc(CH == 2 ? dh_out : dx, (int64_t)B * S * (CH == 2 ? H : In) * 4);
     const int64_t ob = (int64_t)(b0 + sl < B ? b0 + sl : B - 1) * S;
     bf16x8 bw[8];
 #pragma unroll
@@ -628,7 +784,11 @@ __device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, cons
             t = t < S ? t : S - 1;
             t = t > 0 ? t : 0;
             g[k] = *reinterpret_cast<const float4*>(gates + ((ob + t) * H + u) * 4);
-            if (ROLE == 0) d[k] = dh_out[(ob + t) * H + u];
+            if (ROLE == 0 && CH == 2)
+                d[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     drs, (int)(((ob + t) * H + u) * 4), 0, CPOL_SC1));
+            else if (ROLE == 0)
+                d[k] = dh_out[(ob + t) * H + u];
             c[k + 1] = cst[(ob + t) * H + u];
         }
         // c_{tb-1} (c_{-1} = 0 is applied at the use: a select here would wait for the load)
@@ -638,6 +798,7 @@ __device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, cons
     f32x4 ax[MT];
     const int tl0 = ((S - 1) / TC) * TC;
     const int nch = tl0 / TC + 1;
+    if (CH == 2 && ROLE == 0) chain_wait(flags + tile * nchk + (nch - 1), err);   // the last chunk's dh
     load_half(tl0 + 8, gA, cA, dA);
     float dc = 0.f;
     int cur = 0;
@@ -649,8 +810,14 @@ __device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, cons
 #pragma unroll
         for (int i = TC - 1; i >= 0; --i) {
             // unconditional (indices clamped; an idle period's values are never used)
+            // the consumer leaves the chunk's flag zero for the next launch once every wave has
+            // passed its wait (at i == 7 of the previous period, or before the loop: a barrier since)
+            if (CH == 2 && ROLE == 0 && i == 14 && act && j == 0) atomicExch(flags + tile * nchk + t0 / TC, 0u);
             if (i == 15) load_half(t0, gB, cB, dB);
-            if (i == 7) load_half(t0 - 8, gA, cA, dA);
+            if (i == 7) {
+                if (CH == 2 && ROLE == 0 && act && t0 >= TC) chain_wait(flags + tile * nchk + t0 / TC - 1, err);
+                load_half(t0 - 8, gA, cA, dA);
+            }
             if (i < n) {
                 const int t = t0 + i, k8 = i & 7;
                 const float4 gq = i >= 8 ? gA[k8] : gB[k8];
@@ -703,12 +870,24 @@ __device__ __forceinline__ void bwd2_role(const float* __restrict__ dh_out, cons
                         dximg[xb][sr][tt][col] = ax[m][r];
                     } else if (col < In) {
                         const int64_t b = b0 + sr < B ? b0 + sr : B - 1;
-                        if (t < S) dx[(b * S + t) * In + col] = ax[m][r];
+                        if (t < S) {
+                            if (CH == 1) {
+                                // (a bit_cast of the vector element itself stored element 0 for every r:
+                                // clang / ROCm 7.2, seen in the ISA — the value goes through a scalar first)
+                                const float v = ax[m][r];
+                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), drs,
+                                                                      (int)(((b * S + t) * In + col) * 4), 0, CPOL_SC1);
+                            }
+                            else
+                                dx[(b * S + t) * In + col] = ax[m][r];
+                        }
                     }
                 }
         }
         cur ^= 1;   // (both images start zero: L's first chunk may start on either)
+        if (CH == 1 && ROLE == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the chunk's dX landed
         lds_barrier();
+        if (CH == 1 && ROLE == 1 && act && j == 0) atomicAdd(flags + tile * nchk + t0 / TC, 1u);
     }
 }
 
@@ -737,6 +916,53 @@ __global__ __launch_bounds__(2 * G4) void k_lstm16_bwd2(const float* __restrict_
         bwd2_role<NS, 4, 0>(dh_out, gatesU, cU, whhU, wihU, H, B, S, dgU, nullptr, dgsU, dximg, wTU);
     else
         bwd2_role<NS, NTXL, 1>(nullptr, gatesL, cL, whhL, wihL, InL, B, S, dgL, dx, dgsL, dximg, wTL);
+}
+
+// four layers' backward in one launch: workgroups [0, T) run layers 3, 2 of tile b (the producer:
+// layer 2's dX, the gradient at layer 1's outputs, published chunk by chunk into dmid [B, S, H]),
+// [T, 2T) layers 1, 0 of tile b - T (the consumer, reading dmid as each chunk's flag comes up).
+// p: [w_ih, w_hh] x 4 layers; gc: [gates, c] x 4 layers; dg[4]: dgates of each layer; dx: layer
+// 0's input gradient (may be null).  Per role the arithmetic of two k_lstm16_bwd2 launches.
+struct QuadB {
+    const float* w_ih[4];
+    const float* w_hh[4];
+    const float* gates[4];
+    const float* c[4];
+    float* dg[4];
+};
+template <int NS, int NTXL>
+__global__ __launch_bounds__(2 * G4) void k_lstm16_bwd4(const float* __restrict__ dh_out, QuadB q, int In0, int B,
+                                                        int S, int T, float* __restrict__ dmid, float* __restrict__ dx,
+                                                        unsigned slot0) {
+    unsigned* flags = g_chain_flags + slot0;
+    unsigned* err = g_chain_err;
+    __shared__ __attribute__((aligned(16))) __bf16 dgsU[2][TC][NS][DS];
+    __shared__ __attribute__((aligned(16))) __bf16 dgsL[2][TC][NS][DS];
+    __shared__ __attribute__((aligned(16))) float dximg[2][NS][TC][H];
+    __shared__ __attribute__((aligned(16))) __bf16 wTU[H][DS];
+    __shared__ __attribute__((aligned(16))) __bf16 wTL[H][DS];
+    for (int i = threadIdx.x; i < 2 * TC * NS * DS; i += 2 * G4) {
+        (&dgsU[0][0][0][0])[i] = (__bf16)0.f;
+        (&dgsL[0][0][0][0])[i] = (__bf16)0.f;
+    }
+    lds_barrier();
+    const bool cons = (int)blockIdx.x >= T;
+    const int tile = cons ? (int)blockIdx.x - T : (int)blockIdx.x;
+    if (!cons) {
+        if (threadIdx.x < G4)
+            bwd2_role<NS, 4, 0, 1>(dh_out, q.gates[3], q.c[3], q.w_hh[3], q.w_ih[3], H, B, S, q.dg[3], nullptr, dgsU,
+                                   dximg, wTU, tile, flags, err);
+        else
+            bwd2_role<NS, 4, 1, 1>(nullptr, q.gates[2], q.c[2], q.w_hh[2], q.w_ih[2], H, B, S, q.dg[2], dmid, dgsL,
+                                   dximg, wTL, tile, flags, err);
+    } else {
+        if (threadIdx.x < G4)
+            bwd2_role<NS, 4, 0, 2>(dmid, q.gates[1], q.c[1], q.w_hh[1], q.w_ih[1], H, B, S, q.dg[1], nullptr, dgsU,
+                                   dximg, wTU, tile, flags, err);
+        else
+            bwd2_role<NS, NTXL, 1, 2>(nullptr, q.gates[0], q.c[0], q.w_hh[0], q.w_ih[0], In0, B, S, q.dg[0], dx, dgsL,
+                                      dximg, wTL, tile, flags, err);
+    }
 }
 
 }  // namespace l16
@@ -870,6 +1096,105 @@ int vt_lstm16_pair_bwd(const float* dh_out, const float* gates1, const float* c1
         hipLaunchKernelGGL((k_lstm16_bwd2<2, 4>), grid, dim3(2 * G4), 0, st, dh_out, gates1, c1, w_hh1, w_ih1, gates0,
                            c0, w_hh0, w_ih0, In0, B, seq, dgates1, dgates0, dx);
     VT_LAUNCH_CHECK("vt_lstm16_pair_bwd");
+    return VT_OK;
+}
+
+// the chained launches need T (workgroups per pair) a multiple of 8 — tile b's producer and
+// consumer then sit on the same XCD of the round-robin workgroup placement — and flags within the
+// pool; otherwise (or VAETEB_L16_CHAIN=0) the two pair launches run one after the other (the same
+// kernels' arithmetic: the same bits either way)
+static bool l16_chain_ok(int T, int seq) {
+    static const bool on = !getenv("VAETEB_L16_CHAIN") || atoi(getenv("VAETEB_L16_CHAIN")) != 0;
+    return on && T % 8 == 0 && (int64_t)T * ((seq + TC - 1) / TC) <= (int64_t)vt::ARRIVE_POOL / 8;
+}
+
+int vt_lstm16_quad_fwd(const float* x, int In, const float* const* params, int B, int seq, int hidden,
+                       float* const* outs, void* stream) {
+    VT_CHECK_ARG(hidden == H, "vt_lstm16_quad_fwd: hidden size %d (kernel built for %d)", hidden, H);
+    VT_CHECK_ARG(B > 0 && seq > 0 && In > 0 && In <= 64 && In % 4 == 0,
+                 "vt_lstm16_quad_fwd: shape (input size %d: a multiple of 4, at most 64)", In);
+    VT_CHECK_ARG(x && params && outs, "vt_lstm16_quad_fwd: null pointer");
+    Quad q;
+    for (int i = 0; i < 16; ++i) {
+        VT_CHECK_ARG(params[i], "vt_lstm16_quad_fwd: null parameter %d", i);
+        q.p[i] = params[i];
+    }
+    for (int i = 0; i < 12; ++i) {
+        VT_CHECK_ARG(outs[i], "vt_lstm16_quad_fwd: null output %d", i);
+        q.o[i] = outs[i];
+    }
+    const int ns = l16_pair_ns(), T = (B + ns - 1) / ns;
+    const int64_t lds = fwd2_stage_bytes(ns, seq);
+    VT_CHECK_ARG(lds <= L16_PAIR_STAGE_MAX, "vt_lstm16_quad_fwd: sequence length %d too long for the staged input", seq);
+    if (!l16_chain_ok(T, seq)) {
+        int rc = vt_lstm16_pair_fwd(x, In, q.p[0], q.p[2], q.p[1], q.p[3], q.p[4], q.p[6], q.p[5], q.p[7], B, seq, H,
+                                    q.o[0], q.o[1], q.o[2], q.o[3], q.o[4], q.o[5], stream);
+        if (rc) return rc;
+        return vt_lstm16_pair_fwd(q.o[3], H, q.p[8], q.p[10], q.p[9], q.p[11], q.p[12], q.p[14], q.p[13], q.p[15], B,
+                                  seq, H, q.o[6], q.o[7], q.o[8], q.o[9], q.o[10], q.o[11], stream);
+    }
+    hipStream_t st = vt::S(stream);
+    const unsigned slot0 = vt::arrive_slots((unsigned)(T * ((seq + TC - 1) / TC)), st);
+    const dim3 grid(2 * T);
+#define VT_L16F4(NS_, KX_) \
+    hipLaunchKernelGGL((k_lstm16_fwd4<NS_, KX_>), grid, dim3(2 * G4), lds, st, x, In, q, B, seq, T, slot0)
+    if (ns == 4) {
+        if (In <= 32) VT_L16F4(4, 1);
+        else VT_L16F4(4, 2);
+    } else {
+        if (In <= 32) VT_L16F4(2, 1);
+        else VT_L16F4(2, 2);
+    }
+#undef VT_L16F4
+    VT_LAUNCH_CHECK("vt_lstm16_quad_fwd");
+    return VT_OK;
+}
+
+int vt_lstm16_quad_bwd(const float* dh_out, const float* const* w, const float* const* gc, int In0, int B, int seq,
+                       int hidden, float* const* dg, float* dmid, float* dx, void* stream) {
+    VT_CHECK_ARG(hidden == H, "vt_lstm16_quad_bwd: hidden size %d (kernel built for %d)", hidden, H);
+    VT_CHECK_ARG(B > 0 && seq > 0 && In0 > 0 && In0 <= 64, "vt_lstm16_quad_bwd: shape (input size %d, at most 64)",
+                 In0);
+    VT_CHECK_ARG(dh_out && w && gc && dg && dmid, "vt_lstm16_quad_bwd: null pointer");
+    QuadB q;
+    for (int l = 0; l < 4; ++l) {
+        q.w_ih[l] = w[2 * l];
+        q.w_hh[l] = w[2 * l + 1];
+        q.gates[l] = gc[2 * l];
+        q.c[l] = gc[2 * l + 1];
+        q.dg[l] = dg[l];
+        VT_CHECK_ARG(q.w_hh[l] && q.gates[l] && q.c[l] && q.dg[l] && (q.w_ih[l] || (l == 0 && !dx)),
+                     "vt_lstm16_quad_bwd: null pointer (layer %d)", l);
+    }
+    const int T = (B + 1) / 2;
+    if (!l16_chain_ok(T, seq)) {
+        int rc = vt_lstm16_pair_bwd(dh_out, q.gates[3], q.c[3], q.w_hh[3], q.w_ih[3], q.gates[2], q.c[2], q.w_hh[2],
+                                    q.w_ih[2], H, B, seq, H, q.dg[3], q.dg[2], dmid, stream);
+        if (rc) return rc;
+        return vt_lstm16_pair_bwd(dmid, q.gates[1], q.c[1], q.w_hh[1], q.w_ih[1], q.gates[0], q.c[0], q.w_hh[0],
+                                  q.w_ih[0], In0, B, seq, H, q.dg[1], q.dg[0], dx, stream);
+    }
+    hipStream_t st = vt::S(stream);
+    const unsigned slot0 = vt::arrive_slots((unsigned)(T * ((seq + TC - 1) / TC)), st);
+    if (In0 <= 32)
+        hipLaunchKernelGGL((k_lstm16_bwd4<2, 2>), dim3(2 * T), dim3(2 * G4), 0, st, dh_out, q, In0, B, seq, T, dmid,
+                           dx, slot0);
+    else
+        hipLaunchKernelGGL((k_lstm16_bwd4<2, 4>), dim3(2 * T), dim3(2 * G4), 0, st, dh_out, q, In0, B, seq, T, dmid,
+                           dx, slot0);
+    VT_LAUNCH_CHECK("vt_lstm16_quad_bwd");
+    return VT_OK;
+}
+
+int vt_lstm16_chain_errors(int* count, int reset) {
+    VT_CHECK_ARG(count, "vt_lstm16_chain_errors: null pointer");
+    unsigned v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_chain_err), sizeof(v)) != hipSuccess) return VT_ERR_HIP;
+    *count = (int)v;
+    if (reset) {
+        v = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_chain_err), &v, sizeof(v)) != hipSuccess) return VT_ERR_HIP;
+    }
     return VT_OK;
 }
 

@@ -7,6 +7,7 @@ so no transposes are needed between the MLP, conv and LSTM stages (the
 reference transposes to (B, C, L) for torch's conv1d at
 ref/model/vae_teb_model.py:539,545,693,917).
 """
+import ctypes
 import os
 
 import torch
@@ -101,6 +102,10 @@ LSTM_GRAD_DEFER = int(os.environ.get("VAETEB_LSTM_GRAD_DEFER", "1"))
 # behind the lower in the same workgroup, bit-identical to the per-layer kernels)
 LSTM_PAIR = int(os.environ.get("VAETEB_L16_PAIR", "1"))
 _L16_PAIR_NS = 4 if os.environ.get("VAETEB_L16_PAIR_NS") == "4" else 2
+# 4-layer 16-bit LSTMs as ONE launch each way (vt_lstm16_quad_fwd / _bwd: the two layer pairs
+# concurrent, chained chunk by chunk through per-chunk flags; bit-identical to the pair launches)
+LSTM_CHAIN_FWD = int(os.environ.get("VAETEB_L16_CHAIN_FWD", "1"))
+LSTM_CHAIN_BWD = int(os.environ.get("VAETEB_L16_CHAIN_BWD", "1"))
 
 
 def _l16_pair_fits(S):
@@ -878,6 +883,20 @@ class LSTMF(torch.autograd.Function):
             c = torch.empty_like(h)
             gates = torch.empty((B, S, 4 * H), device=x.device)
             h16 = half and In <= 64 and In % 4 == 0
+            if h16 and LSTM_PAIR and LSTM_CHAIN_FWD and l == 0 and nl == 4 and H == 64 and _l16_pair_fits(S):
+                # all four layers in one launch: pair (2, 3) consumes layer 1's h chunk by chunk
+                hs = [h] + [torch.empty_like(h) for _ in range(3)]
+                cs = [c] + [torch.empty_like(h) for _ in range(3)]
+                gs = [gates] + [torch.empty_like(gates) for _ in range(3)]
+                pv = (ctypes.c_void_p * 16)(*[ptr(t) for t in params])
+                ov = (ctypes.c_void_p * 12)(*[ptr(t) for i in range(4) for t in (hs[i], cs[i], gs[i])])
+                call("vt_lstm16_quad_fwd", ptr(inp), In, ctypes.addressof(pv), B, S, H, ctypes.addressof(ov), _st())
+                saved += [inp, hs[0], cs[0], gs[0], hs[0], hs[1], cs[1], gs[1],
+                          hs[1], hs[2], cs[2], gs[2], hs[2], hs[3], cs[3], gs[3]]
+                pairs += [0, 2]
+                inp = hs[3]
+                l = 4
+                continue
             if h16 and LSTM_PAIR and l + 1 < nl and H <= 64 and _l16_pair_fits(S):
                 # layers l and l + 1 in one launch (the upper one chunk behind the lower)
                 w_ih1, w_hh1, b_ih1, b_hh1 = params[4 * l + 4: 4 * l + 8]
@@ -992,6 +1011,24 @@ class LSTMF(torch.autograd.Function):
             grads[4 * l: 4 * l + 4] = [gw_ih, gw_hh, *pb.result()]
 
         l = nl - 1
+        if LSTM_CHAIN_BWD and ctx.pairs == [0, 2] and nl == 4:
+            # the four layers' backward in one launch: layer 2's dX (dmid, the gradient at layer
+            # 1's outputs) handed to layers 1, 0 chunk by chunk (vt_lstm16_quad_bwd)
+            In0 = saved[0].shape[-1]
+            dgs = [torch.empty((B, S, 4 * H), device=gy.device) for _ in range(4)]
+            dmid = torch.empty((B, S, H), device=gy.device)
+            need_dx = ctx.needs_input_grad[0]
+            gin = torch.empty((B, S, In0), device=gy.device) if need_dx else None
+            wv = (ctypes.c_void_p * 8)(*[ptr(params[4 * k + i]) for k in range(4) for i in (0, 1)])
+            gv = (ctypes.c_void_p * 8)(*[ptr(saved[4 * k + i]) for k in range(4) for i in (3, 2)])
+            dv = (ctypes.c_void_p * 4)(*[ptr(t) for t in dgs])
+            call("vt_lstm16_quad_bwd", ptr(dh), ctypes.addressof(wv), ctypes.addressof(gv), In0, B, S, H,
+                 ctypes.addressof(dv), ptr(dmid), ptr(gin) if need_dx else None, _st())
+            for k in (3, 2, 1, 0):
+                wgrad(k, dgs[k], True)
+            if need_dx:
+                dh = gx = gin
+            l = -1
         while l >= 0:
             if l - 1 in ctx.pairs:
                 # layers l (upper) and l - 1 (lower) in one launch: the upper layer's dX goes
