@@ -405,17 +405,26 @@ def main():
                          "memory-bound clip + AdamW of the current step")
     ap.add_argument("--serial-encoders", action="store_true",
                     help="run the source / target encoders on one stream (default: two HIP streams)")
-    ap.add_argument("--heads", choices=["bf16", "fp32"], default="bf16",
+    ap.add_argument("--precision", choices=["bf16", "fp16"], default="bf16",
+                    help="16-bit operand format of the heads / conv blocks / ResidualMLP linears left at their "
+                         "default: bf16 (MI355X default, no loss scale) or fp16 (the reference's own autocast width, "
+                         "ref/model/graph_model.py:510,709-726, trained with the device-side dynamic loss scale)")
+    ap.add_argument("--heads", choices=["bf16", "fp16", "fp32"], default="bf16",
                     help="decoder R x R head GEMMs: bf16 MFMA (the reference trains in fp16 autocast; bf16 is the documented deviation, DESIGN.md §5) or fp32")
-    ap.add_argument("--conv", choices=["bf16", "fp32"], default="bf16",
+    ap.add_argument("--conv", choices=["bf16", "fp16", "fp32"], default="bf16",
                     help="conv blocks: bf16 MFMA with fp32 accumulation / BatchNorm (bf16 for the reference's fp16 autocast) or exact fp32")
-    ap.add_argument("--mlp", choices=["bf16", "fp32"], default="bf16",
+    ap.add_argument("--mlp", choices=["bf16", "fp16", "fp32"], default="bf16",
                     help="ResidualMLP stacks: Linear layers on bf16 MFMA with fp32 accumulation, LayerNorm fp32 "
                          "(bf16 for the reference's fp16 autocast) or exact fp32")
     ap.add_argument("--lstm", choices=["16-mixed", "fp32"], default="16-mixed",
                     help="encoder LSTMs: 16-bit MFMA recurrences over 4-sample tiles (f16 forward / bf16 backward "
                          "operands, fp32 state: the reference's own 16-mixed LSTM width) or exact fp32")
     args = ap.parse_args()
+    for k in ("heads", "conv", "mlp"):
+        if getattr(args, k) == "bf16":
+            setattr(args, k, args.precision)
+    assert not (args.workload == "c4" and "fp16" in (args.heads, args.conv, args.mlp)), \
+        "fp16 operands: c2 only (the classifier's convolutions have bf16 / fp32 kernels)"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without torchrun: N fresh rank processes (before this
         # process touches the GPU), rank 0's JSON line relayed, the first failure's exit code
@@ -656,11 +665,13 @@ def main():
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32" if (args.heads, args.conv, args.mlp, args.lstm) == ("fp32", "fp32", "fp32", "fp32") else
-                 "bf16 MFMA (" + " + ".join(n for n, v in (("decoder heads", args.heads), ("conv blocks", args.conv),
-                                                         ("ResidualMLP linears", args.mlp),
-                                                         ("classifier convolutions", args.conv if c4 else "")) if v == "bf16")
+                 f"{args.precision} MFMA (" + " + ".join(
+                     n for n, v in (("decoder heads", args.heads), ("conv blocks", args.conv),
+                                    ("ResidualMLP linears", args.mlp),
+                                    ("classifier convolutions", args.conv if c4 else "")) if v in ("bf16", "fp16"))
                  + (", LSTM recurrences f16 fwd / bf16 bwd" if args.lstm == "16-mixed" else "")
-                 + "), fp32 accumulation; fp32 LayerNorm / BatchNorm / LSTM state / front-end / optimizer",
+                 + "), fp32 accumulation; fp32 LayerNorm / BatchNorm / LSTM state / front-end / optimizer"
+                 + ("; dynamic loss scale (GradScaler semantics, device-side)" if trainer.loss_scale else ""),
         "data": "synthetic",
         "config": {"workload": (f"c4: front-end J={J} Q={Q} T={T} (N=4096, S={S}) + SeqVaeTebClassifier("
                                 f"R={16 * S}, FHRInceptionTimeClassifier d6 attention, "
@@ -671,6 +682,7 @@ def main():
                                 f"train step, batch {B}/GPU"), "global_batch": B * world, "seq_len": N,
                    "parallelism": f"dp{world}"},
         "elbo": elbo,
+        **({"loss_scale": trainer.scaler_state()} if trainer.loss_scale else {}),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "mode": (f"step captured once, replayed by the native "
                  f"{len(caps[0].side) + 1 - bool(caps[0].markers)}-stream executor (vt_stepgraph); "

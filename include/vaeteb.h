@@ -54,6 +54,17 @@ int vt_arrive_reset(void* stream);
  * by type, the stream's current dependency nodes, kernel nodes with an empty grid) into buf[len]
  * (tools/capture_probe.py).  No reference counterpart.                                        */
 int vt_capture_info(void* stream, char* buf, int len);
+/* The 16-bit MFMA operand format of the decoder heads (vt_mfma_*), the bf16 conv blocks
+ * (vt_conv1d_*_bf16*, vt_conv1d_*16*, vt_batchnorm_bwd_x16) and the bf16 ResidualMLP stacks
+ * (vt_resmlp_bf16_*), and of the weight shadows they read (vt_mfma_weight_shadow,
+ * vt_conv1d_bf16_shadow*, vt_adamw_step_dev_shadow): 0 = bf16 (default), 1 = fp16, the
+ * reference's autocast width (ref/model/graph_model.py:510 precision="16-mixed",
+ * :709-711 torch.amp.autocast('cuda')), trained with the dynamic loss scale below.  Read at
+ * launch time by every such entry point (library-wide: set it before a forward / capture;
+ * a captured step keeps the format it was captured with; shadow buffers written in one format
+ * must not be read in the other).  Returns the previous format.                            */
+int vt_set_h16_format(int fp16);
+int vt_get_h16_format(void);
 
 /* ------------------------------------------------------------------ front-end
  * Twiddle tables `tw`: float2[n], tw[k] = exp(-2*pi*i*k/n) computed in fp64 on
@@ -204,6 +215,17 @@ int vt_grad_norm_workspace_floats(void);
  * (max_norm <= 0: no clipping).  replaces: clip_grad_norm_ ref/model/graph_model.py:724 */
 int vt_grad_norm_clip(const float* g, int64_t n, float pre_scale, float max_norm, float* out2, float* ws,
                       void* stream);
+/* The same over a buffer that holds scale * gradients (the backward ran on loss * scale:
+ * the fp16 operand format, vt_set_h16_format), with the dynamic loss scale on the device,
+ * scaler = float[4] {scale, growth tracker, found_inf, skipped-step count}: found_inf = the
+ * squared norm is not finite; out3[0] = pre_scale * ||g|| / scale (inf if found), out3[1] =
+ * pre_scale * clip_coef / scale (0 if found), out3[2] = found_inf; then scale *= backoff_factor
+ * and tracker = 0 if found, else tracker + 1 == growth_interval -> scale *= growth_factor.
+ * replaces: torch.amp.GradScaler('cuda') scale / unscale_ / update around clip_grad_norm_
+ *           (ref/model/graph_model.py:670, 718-726), GradScaler defaults 2.0 / 0.5 / 2000   */
+int vt_grad_norm_clip_scaled(const float* g, int64_t n, float pre_scale, float max_norm, float* out3, float* ws,
+                             float* scaler, float growth_factor, float backoff_factor, int growth_interval,
+                             void* stream);
 /* torch.optim.AdamW (decoupled decay) with g <- g*gscale[0] (nullable).
  * replaces: torch.optim.AdamW configured at ref/model/graph_model.py:654-660,
  *           ref/model/pytorch_lightning_modules.py:540-546                       */
@@ -227,6 +249,18 @@ int vt_adamw_step_dev_shadow(float* p, const float* g, float* m, float* v, int64
                              float beta2, float eps, float weight_decay, int* step, float* coef, const float* gscale,
                              int n_tiled, const int64_t* tiled_off, const int* tiled_N, const int* tiled_K,
                              const int64_t* tiled_w16, const int64_t* tiled_w16t, void* stream);
+/* vt_adamw_step_dev / vt_adamw_step_dev_shadow skipped on the device when skip[0] != 0 (the
+ * found_inf of vt_grad_norm_clip_scaled, out3 + 2): no parameter, moment, shadow or step-counter
+ * change, as GradScaler.step skips optimizer.step (ref/model/graph_model.py:725).  The shadows
+ * are written in the current 16-bit format (vt_set_h16_format).                           */
+int vt_adamw_step_dev_skip(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                           float beta2, float eps, float weight_decay, int* step, float* coef, const float* gscale,
+                           const float* skip, void* stream);
+int vt_adamw_step_dev_shadow_skip(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                                  float beta2, float eps, float weight_decay, int* step, float* coef,
+                                  const float* gscale, int n_tiled, const int64_t* tiled_off, const int* tiled_N,
+                                  const int* tiled_K, const int64_t* tiled_w16, const int64_t* tiled_w16t,
+                                  const float* skip, void* stream);
 /* Tuning switch: 1 (default) = the float4 AdamW kernel when p, g, m, v are all
  * 16-byte aligned, 0 = the scalar kernel.  Same per-element expression: the
  * two give the same bits (tested).  Env override: VAETEB_ADAMW_SCALAR=1.         */

@@ -42,4 +42,8 @@ for M, C in SHAPES:
         us = e0.elapsed_time(e1) / 20 * 1e3
         res.append(f"{us:7.1f} us {nbytes / us / 1e3:6.0f} GB/s")
     ck = int(d16.view(torch.int16).to(torch.int64).sum().item())
-    print(f"M {M:8d} C {C:3d}: coef {res[0]} | x16 {res[1]} | rows checksum {ck}", flush=True)
+    dg.zero_()
+    db.zero_()
+    coef()
+    cc = hash(tuple(torch.cat([dg, db, bnp]).view(torch.int32).tolist()))
+    print(f"M {M:8d} C {C:3d}: coef {res[0]} | x16 {res[1]} | rows checksum {ck} | coef bits {cc}", flush=True)

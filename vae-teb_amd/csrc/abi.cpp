@@ -38,6 +38,9 @@ int register_arrive_pool(const void* sym, size_t bytes) {
     arrive_pools().emplace_back(sym, bytes);
     return (int)arrive_pools().size();
 }
+
+static std::atomic<int> g_h16{0};   // 16-bit MFMA operand format (h16.h): 0 bf16, 1 fp16
+int h16_format() { return g_h16.load(std::memory_order_relaxed); }
 }  // namespace vt
 
 extern "C" {
@@ -54,6 +57,8 @@ int vt_arrive_reset(void* stream) {
     return VT_OK;
 }
 int vt_abi_version(void) { return 1; }
+int vt_set_h16_format(int fp16) { return vt::g_h16.exchange(fp16 ? 1 : 0); }
+int vt_get_h16_format(void) { return vt::h16_format(); }
 }
 
 // ------------------------------------------------------------ stream forks

@@ -179,7 +179,7 @@ int sum_splits_launch(const float* part, int splits, int64_t n, float* out, int 
                       int pK = 0, int pCo = 0, int pCi = 0);
 // conv_fwd16.hip: the flat-staged bf16 forward (returns its position tile, or VT_ERR_ARG);
 // ibn (nullable): x is the previous block's pre-BN output, its BatchNorm + act applied in staging
-int cfw16_launch(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,
+int cfw16_launch(const float* x, const Geo& g, const void* w16, float* y, int Lo, float* stats, hipStream_t st,
                  const BnIn* ibn = nullptr);
 // conv_bf16.hip: the reflect mirror rows of a direct-dX backward-data conv added back (k_conv_fold_edges)
 void fold_edges_launch(float* dx, const float* edge, int B, int L, int pad, int C, hipStream_t st);

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include "conv.h"
+#include "h16.h"
 
 namespace vt {
 
@@ -29,9 +30,6 @@ namespace vt {
 int g_conv_kern = 11;
 
 namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int CB = 32;   // input channels per staged chunk (= one MFMA k-step)
 constexpr int RS = 40;   // bf16 row stride of window and tap rows
@@ -53,10 +51,11 @@ struct FoldOut {
     float* edge;   // nullable: the edge rows are dropped (causal padding)
 };
 
-__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
-    bf16x8 r;
+template <typename H>
+__device__ __forceinline__ hv8<H> pack8(const float (&v)[8]) {
+    hv8<H> r;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+    for (int j = 0; j < 8; ++j) r[j] = (H)v[j];
     return r;
 }
 
@@ -66,11 +65,11 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
 // the BatchNorm-backward parameters of its one channel sit in registers.  U rows per
 // round, all their loads issued before the first use.  Same values and the same bf16
 // roundings as the octet staging below (bit-identical results).
-template <int K, int WIN, bool BNB, bool IBN = false>
-__device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const float* __restrict__ xb,
+template <typename H, int K, int WIN, bool BNB, bool IBN = false>
+__device__ __forceinline__ void stage_window_cl(H* __restrict__ xs, const float* __restrict__ xb,
                                                 const float* __restrict__ x2b, const Geo& g, int t0, int TP, int Lo,
                                                 int c0, const float* __restrict__ bp, int act, float invM,
-                                                __bf16* __restrict__ dbf, int b, bool write_dbf,
+                                                H* __restrict__ dbf, int b, bool write_dbf,
                                                 const float* ip = nullptr, int ics = 0, int iact = 0) {
     constexpr int NR = (WIN + 7) / 8, U = K <= 3 ? 3 : 6;
     const int tid = threadIdx.x, cl = tid & 31, rg = tid >> 5;
@@ -129,12 +128,12 @@ __device__ __forceinline__ void stage_window_cl(__bf16* __restrict__ xs, const f
                     v = g.up ? up_lerp(a[u], q[u], l1[u]) : a[u];
                 }
             }
-            xs[r * RS + cl] = (__bf16)v;
+            xs[r * RS + cl] = (H)v;
             if constexpr (BNB) {
                 // the bf16 side output: the row's channels and its zero channel padding up to cpad
                 const int t = t0 + r - g.pad;
                 if (write_dbf && rok[u] && c < cpad && t >= t0 && t < t0 + TP)
-                    dbf[((int64_t)b * g.L_in + t) * cpad + c] = (__bf16)v;
+                    dbf[((int64_t)b * g.L_in + t) * cpad + c] = (H)v;
             }
         }
     }
@@ -156,18 +155,19 @@ int g_conv_cl = 1;
 // for their own rows t0 .. t0 + TP - 1 (each row once) — the weight gradient's operand.
 // IBN (not with BNB): x is the previous block's pre-BN conv output, its BatchNorm + activation
 // (bi, staged into LDS at byte ipo) applied to the source samples while the window is staged.
-template <int K, int NT, bool BNB = false, bool CL = true, bool IBN = false>
-__global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, Geo g, const __bf16* __restrict__ w16,
+template <int K, int NT, bool BNB = false, bool CL = true, bool IBN = false, typename H = __bf16>
+__global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, Geo g, const H* __restrict__ w16,
                                                    int cin32, float* __restrict__ y, int Lo,
                                                    float* __restrict__ stats, const float* __restrict__ x2,
                                                    const float* __restrict__ bnp, int act, float invM,
-                                                   __bf16* __restrict__ dbf, FoldOut fo, BnIn bi, int ipo) {
+                                                   H* __restrict__ dbf, FoldOut fo, BnIn bi, int ipo) {
     static_assert(!(BNB && IBN), "k_conv_bf16: BNB and IBN exclusive");
     using C = BCfg<K, NT>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
-    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
-    __bf16* xs = lb;           // [WIN][RS]
-    __bf16* ws = lb + C::XB;   // [K][TC][RS]
+    extern __shared__ __attribute__((aligned(16))) char lb_raw[];
+    H* const lb = reinterpret_cast<H*>(lb_raw);
+    H* xs = lb;           // [WIN][RS]
+    H* ws = lb + C::XB;   // [K][TC][RS]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
     const int t0 = blockIdx.x * TP, co0 = blockIdx.y * TC, b = blockIdx.z;
     const float* xb = x + (int64_t)b * g.L_in * g.Cin;
@@ -192,28 +192,28 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
             // taps (K x TC rows x 4 octets, 16 B each from the shadow): loads first, stores
             // after the window
             constexpr int NWI = (K * TC * 4 + 255) / 256;
-            bf16x8 wt[NWI];
+            hv8<H> wt[NWI];
 #pragma unroll
             for (int it = 0; it < NWI; ++it) {
                 const int i = tid + 256 * it;
                 const int ic = i < K * TC * 4 ? i : K * TC * 4 - 1;
                 const int oct = ic & 3, r = ic >> 2, k = r / TC, co = r - k * TC;
                 const int coc = co0 + co < g.Cout ? co0 + co : g.Cout - 1;
-                wt[it] = *(const bf16x8*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
+                wt[it] = *(const hv8<H>*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
             }
-            stage_window_cl<K, WIN, BNB, IBN>(xs, xb, x2b, g, t0, TP, Lo, c0, bp, act, invM, dbf, b,
+            stage_window_cl<H, K, WIN, BNB, IBN>(xs, xb, x2b, g, t0, TP, Lo, c0, bp, act, invM, dbf, b,
                                               BNB && dbf && blockIdx.y == 0, ip, cin32, bi.act);
 #pragma unroll
             for (int it = 0; it < NWI; ++it) {
                 const int i = tid + 256 * it;
                 if (i >= K * TC * 4) continue;
                 const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
-                bf16x8 val = wt[it];
+                hv8<H> val = wt[it];
                 if (co0 + co >= g.Cout) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
+                    for (int j = 0; j < 8; ++j) val[j] = (H)0.f;
                 }
-                *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = val;
+                *(hv8<H>*)(ws + (k * TC + co) * RS + 8 * oct) = val;
             }
         } else if constexpr (K <= 3) {
             // small K (few taps, little MFMA work per staged row): the per-element staging
@@ -235,39 +235,39 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
                     }
                     if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
                         const int cpad = (g.Cin + 7) & ~7;
-                        *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v);
+                        *(hv8<H>*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8<H>(v);
                     }
                 } else {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
                         v[j] = (ok && cb + j < g.Cin) ? src_val<IBN>(xb, g, tp, cb + j, ip, cin32, bi.act) : 0.f;
                 }
-                *(bf16x8*)(xs + row * RS + 8 * oct) = pack8(v);
+                *(hv8<H>*)(xs + row * RS + 8 * oct) = pack8<H>(v);
             }
             for (int i = tid; i < K * TC * 4; i += 256) {
                 const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
-                bf16x8 val;
+                hv8<H> val;
                 if (co0 + co < g.Cout) {
-                    val = *(const bf16x8*)(w16 + ((int64_t)(co0 + co) * K + k) * cin32 + c0 + 8 * oct);
+                    val = *(const hv8<H>*)(w16 + ((int64_t)(co0 + co) * K + k) * cin32 + c0 + 8 * oct);
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
+                    for (int j = 0; j < 8; ++j) val[j] = (H)0.f;
                 }
-                *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = val;
+                *(hv8<H>*)(ws + (k * TC + co) * RS + 8 * oct) = val;
             }
         } else {
             // window: WIN rows x 4 octets of 8 channels, fp32 -> bf16, and the chunk's taps
             // (K x TC rows x 4 octets, 16 B each from the shadow): every load of the thread
             // issued before the first store (clamped addresses, masked values)
             constexpr int NI = (WIN * 4 + 255) / 256, NWI = (K * TC * 4 + 255) / 256;
-            bf16x8 wt[NWI];
+            hv8<H> wt[NWI];
     #pragma unroll
             for (int it = 0; it < NWI; ++it) {
                 const int i = tid + 256 * it;
                 const int ic = i < K * TC * 4 ? i : K * TC * 4 - 1;
                 const int oct = ic & 3, r = ic >> 2, k = r / TC, co = r - k * TC;
                 const int coc = co0 + co < g.Cout ? co0 + co : g.Cout - 1;
-                wt[it] = *(const bf16x8*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
+                wt[it] = *(const hv8<H>*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
             }
             // window items in rounds of NB (all loads of a round in flight together)
             constexpr int NB = BNB ? (NI < 2 ? NI : 2) : (NI < 3 ? NI : 3);
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
                     }
                     if (dbf && blockIdx.y == 0 && in && t >= t0 && t < t0 + TP && cb < g.Cin) {
                         const int cpad = (g.Cin + 7) & ~7;   // cb < Cin and cb % 8 == 0: the octet fits the padded row
-                        *(bf16x8*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8(v[it]);
+                        *(hv8<H>*)(dbf + ((int64_t)b * g.L_in + t) * cpad + cb) = pack8<H>(v[it]);
                     }
                 } else {
                     src_vec<8, IBN>(xb, g, tp, cb, ok, v[it], ip, cin32, bi.act);
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
     #pragma unroll
             for (int it = 0; it < NB; ++it) {
                 const int i = tid + 256 * (r0 + it);
-                if (r0 + it < NI && i < WIN * 4) *(bf16x8*)(xs + (i >> 2) * RS + 8 * (i & 3)) = pack8(v[it]);
+                if (r0 + it < NI && i < WIN * 4) *(hv8<H>*)(xs + (i >> 2) * RS + 8 * (i & 3)) = pack8<H>(v[it]);
             }
             }
     #pragma unroll
@@ -315,29 +315,29 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
                 const int i = tid + 256 * it;
                 if (i >= K * TC * 4) continue;
                 const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
-                bf16x8 val = wt[it];
+                hv8<H> val = wt[it];
                 if (co0 + co >= g.Cout) {
     #pragma unroll
-                    for (int j = 0; j < 8; ++j) val[j] = (__bf16)0.f;
+                    for (int j = 0; j < 8; ++j) val[j] = (H)0.f;
                 }
-                *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = val;
+                *(hv8<H>*)(ws + (k * TC + co) * RS + 8 * oct) = val;
             }
         }
         __syncthreads();
-        const __bf16* xq = xs + (PM * 16 * wv + lr) * RS + 8 * lc;
-        const __bf16* wq = ws + lr * RS + 8 * lc;
+        const H* xq = xs + (PM * 16 * wv + lr) * RS + 8 * lc;
+        const H* wq = ws + lr * RS + 8 * lc;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            bf16x8 af[PM], bf[NT];
+            hv8<H> af[PM], bf[NT];
 #pragma unroll
-            for (int m = 0; m < PM; ++m) af[m] = *(const bf16x8*)(xq + (16 * m + k) * RS);
+            for (int m = 0; m < PM; ++m) af[m] = *(const hv8<H>*)(xq + (16 * m + k) * RS);
 #pragma unroll
-            for (int n = 0; n < NT; ++n) bf[n] = *(const bf16x8*)(wq + (k * TC + 16 * n) * RS);
+            for (int n = 0; n < NT; ++n) bf[n] = *(const hv8<H>*)(wq + (k * TC + 16 * n) * RS);
 #pragma unroll
             for (int m = 0; m < PM; ++m)
 #pragma unroll
                 for (int n = 0; n < NT; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bf[n], acc[m][n], 0, 0, 0);
+                    acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
         }
         __syncthreads();
     }
@@ -414,21 +414,22 @@ __global__ __launch_bounds__(256) void k_conv_bf16(const float* __restrict__ x, 
 
 // bf16 shadows of W [Cout][Cin][K]: w16 [Cout][K][cin32] (forward) and
 // w16t [Cin][K][cout32] = W[co][ci][K-1-k] (backward-data), zero-padded.
+template <typename H>
 __global__ void k_conv_shadow(const float* __restrict__ W, int Cout, int Cin, int K, int cin32, int cout32,
-                              __bf16* __restrict__ w16, __bf16* __restrict__ w16t) {
+                              H* __restrict__ w16, H* __restrict__ w16t) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n1 = (int64_t)Cout * K * cin32;
     if (i < n1) {
         const int ci = (int)(i % cin32);
         const int64_t r = i / cin32;
         const int k = (int)(r % K), co = (int)(r / K);
-        w16[i] = (__bf16)(ci < Cin ? W[((int64_t)co * Cin + ci) * K + k] : 0.f);
+        w16[i] = (H)(ci < Cin ? W[((int64_t)co * Cin + ci) * K + k] : 0.f);
     } else if (i < n1 + (int64_t)Cin * K * cout32) {
         const int64_t j = i - n1;
         const int co = (int)(j % cout32);
         const int64_t r = j / cout32;
         const int k = (int)(r % K), ci = (int)(r / K);
-        w16t[j] = (__bf16)(co < Cout ? W[((int64_t)co * Cin + ci) * K + (K - 1 - k)] : 0.f);
+        w16t[j] = (H)(co < Cout ? W[((int64_t)co * Cin + ci) * K + (K - 1 - k)] : 0.f);
     }
 }
 
@@ -440,10 +441,11 @@ struct ConvShadowBatch {
     int n;
     const float* W[CSB_MAX];
     int Cout[CSB_MAX], Cin[CSB_MAX], K[CSB_MAX];
-    __bf16* w16[CSB_MAX];
-    __bf16* w16t[CSB_MAX];
+    void* w16[CSB_MAX];
+    void* w16t[CSB_MAX];
     int prefix[CSB_MAX + 1];   // workgroups
 };
+template <typename H>
 __global__ __launch_bounds__(256) void k_conv_shadow_batch(ConvShadowBatch cb) {
     int h = 0;
     while (h + 1 < cb.n && (int)blockIdx.x >= cb.prefix[h + 1]) ++h;
@@ -456,13 +458,13 @@ __global__ __launch_bounds__(256) void k_conv_shadow_batch(ConvShadowBatch cb) {
         const int ci = (int)(i % cin32);
         const int64_t r = i / cin32;
         const int k = (int)(r % K), co = (int)(r / K);
-        cb.w16[h][i] = (__bf16)(ci < Cin ? W[((int64_t)co * Cin + ci) * K + k] : 0.f);
+        reinterpret_cast<H*>(cb.w16[h])[i] = (H)(ci < Cin ? W[((int64_t)co * Cin + ci) * K + k] : 0.f);
     } else if (i < n1 + (int64_t)Cin * K * cout32) {
         const int64_t j = i - n1;
         const int co = (int)(j % cout32);
         const int64_t r = j / cout32;
         const int k = (int)(r % K), ci = (int)(r / K);
-        cb.w16t[h][j] = (__bf16)(co < Cout ? W[((int64_t)co * Cin + ci) * K + (K - 1 - k)] : 0.f);
+        reinterpret_cast<H*>(cb.w16t[h])[j] = (H)(co < Cout ? W[((int64_t)co * Cin + ci) * K + (K - 1 - k)] : 0.f);
     }
 }
 
@@ -473,13 +475,35 @@ struct BnB {
     const float* bnp;
     int act;
     float invM;
-    __bf16* dbf;   // nullable: bf16 copy of the BN input gradient (the weight gradient's operand)
+    void* dbf;     // nullable: bf16 copy of the BN input gradient (the weight gradient's operand)
 };
 
 template <int K, int NT>
-int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
+int bf_nt(const float* x, const Geo& g, const void* w16v, int cin32, float* y, int Lo, float* stats,
           hipStream_t st, const BnB* bn, FoldOut fo, const BnIn* ibn) {
     using C = BCfg<K, NT>;
+    if (x && h16_format()) {
+        // fp16 operands (h16.h): the default kernel set only — the plain forward / backward-data
+        // conv; the fused-BN backward staging and the conv-stack fold are bf16-only A/B paths
+        if (bn || ibn) {
+            set_error("conv bf16: the fused BatchNorm staging / conv-stack fold paths have no fp16 form");
+            return VT_ERR_ARG;
+        }
+        if ((g_conv_kern & 1) && (K <= 5 || (g_conv_kern & 4)) && fo.pad < 0 && ((uintptr_t)x & 15) == 0) {
+            const int tp = cfw16_launch(x, g, w16v, y, Lo, stats, st, nullptr);
+            if (tp > 0) return tp;
+        }
+        dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
+        const _Float16* w16 = (const _Float16*)w16v;
+        if (g_conv_cl == 2)
+            hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true, false, _Float16>), grid, dim3(256), C::LDS_BYTES, st, x,
+                               g, w16, cin32, y, Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, BnIn{}, 0);
+        else
+            hipLaunchKernelGGL((k_conv_bf16<K, NT, false, false, false, _Float16>), grid, dim3(256), C::LDS_BYTES, st,
+                               x, g, w16, cin32, y, Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, BnIn{}, 0);
+        return C::TP;
+    }
+    const __bf16* w16 = (const __bf16*)w16v;
     // flat-staged forward where it measured faster than k_conv_bf16 (isolated, decoder
     // geometry: K 5 / 3 layers 60 -> 52, 102 -> 60 us; K >= 7 slower: 30 -> 43 us at K 11)
     if (x && !bn && (g_conv_kern & 1) && (K <= 5 || (g_conv_kern & 4)) && fo.pad < 0 && ((uintptr_t)x & 15) == 0) {
@@ -491,28 +515,28 @@ int bf_nt(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, 
     const BnIn bi = ibn ? *ibn : BnIn{};
     const int ipo = C::LDS_BYTES, ilds = C::LDS_BYTES + 16 * cin32;   // IBN: [4][cin32] parameters
     if (x && bn && cl)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT, true, true>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
-                           cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo, bi, 0);
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, true, true, false, __bf16>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g, w16,
+                           cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, (__bf16*)bn->dbf, fo, bi, 0);
     else if (x && bn)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT, true, false>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g,
-                           w16, cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, bn->dbf, fo, bi, 0);
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, true, false, false, __bf16>), grid, dim3(256), C::LDS_BYTES + 24 * g.Cin, st, x, g,
+                           w16, cin32, y, Lo, stats, bn->x2, bn->bnp, bn->act, bn->invM, (__bf16*)bn->dbf, fo, bi, 0);
     else if (x && cl && ibn)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true, true>), grid, dim3(256), ilds, st, x, g, w16, cin32, y,
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true, true, __bf16>), grid, dim3(256), ilds, st, x, g, w16, cin32, y,
                            Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, bi, ipo);
     else if (x && cl)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, true, false, __bf16>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
                            Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, bi, 0);
     else if (x && ibn)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, false, true>), grid, dim3(256), ilds, st, x, g, w16, cin32, y,
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, false, true, __bf16>), grid, dim3(256), ilds, st, x, g, w16, cin32, y,
                            Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, bi, ipo);
     else if (x)
-        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, false>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
+        hipLaunchKernelGGL((k_conv_bf16<K, NT, false, false, false, __bf16>), grid, dim3(256), C::LDS_BYTES, st, x, g, w16, cin32, y,
                            Lo, stats, nullptr, nullptr, 0, 0.f, nullptr, fo, bi, 0);
     return C::TP;
 }
 
 template <int K>
-int bf_k(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats, hipStream_t st,
+int bf_k(const float* x, const Geo& g, const void* w16, int cin32, float* y, int Lo, float* stats, hipStream_t st,
          const BnB* bn, FoldOut fo, const BnIn* ibn) {
     switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
         case 1: return bf_nt<K, 1>(x, g, w16, cin32, y, Lo, stats, st, bn, fo, ibn);
@@ -525,7 +549,7 @@ int bf_k(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, i
 }
 
 // x == nullptr: no launch, only the position tile of this geometry
-int bf_launch(const float* x, const Geo& g, const __bf16* w16, int cin32, float* y, int Lo, float* stats,
+int bf_launch(const float* x, const Geo& g, const void* w16, int cin32, float* y, int Lo, float* stats,
               hipStream_t st, const BnB* bn = nullptr, FoldOut fo = FoldOut{-1, 0, nullptr},
               const BnIn* ibn = nullptr) {
     switch (g.K) {
@@ -593,8 +617,8 @@ int vt_conv1d_bf16_shadow(const float* W, int Cout, int Cin, int K, void* w16, v
     VT_CHECK_ARG(Cout > 0 && Cin > 0 && K > 0 && K <= KMAXB, "vt_conv1d_bf16_shadow: shape");
     const int cin32 = cdiv(Cin, 32) * 32, cout32 = cdiv(Cout, 32) * 32;
     const int64_t n = (int64_t)Cout * K * cin32 + (int64_t)Cin * K * cout32;
-    hipLaunchKernelGGL(k_conv_shadow, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(stream), W, Cout, Cin, K,
-                       cin32, cout32, (__bf16*)w16, (__bf16*)w16t);
+    VT_H16(hipLaunchKernelGGL(k_conv_shadow<H>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(stream), W, Cout,
+                              Cin, K, cin32, cout32, (H*)w16, (H*)w16t));
     VT_LAUNCH_CHECK("vt_conv1d_bf16_shadow");
     return VT_OK;
 }
@@ -613,12 +637,12 @@ int vt_conv1d_bf16_shadow_batch(int n, const int64_t* W, const int* Cout, const 
         cb.Cout[h] = Cout[h];
         cb.Cin[h] = Cin[h];
         cb.K[h] = K[h];
-        cb.w16[h] = reinterpret_cast<__bf16*>(w16[h]);
-        cb.w16t[h] = reinterpret_cast<__bf16*>(w16t[h]);
+        cb.w16[h] = reinterpret_cast<void*>(w16[h]);
+        cb.w16t[h] = reinterpret_cast<void*>(w16t[h]);
         const int64_t e = (int64_t)Cout[h] * K[h] * (cdiv(Cin[h], 32) * 32) + (int64_t)Cin[h] * K[h] * (cdiv(Cout[h], 32) * 32);
         cb.prefix[h + 1] = cb.prefix[h] + (int)((e + 255) / 256);
     }
-    hipLaunchKernelGGL(k_conv_shadow_batch, dim3((unsigned)cb.prefix[n]), dim3(256), 0, S(stream), cb);
+    VT_H16(hipLaunchKernelGGL(k_conv_shadow_batch<H>, dim3((unsigned)cb.prefix[n]), dim3(256), 0, S(stream), cb));
     VT_LAUNCH_CHECK("vt_conv1d_bf16_shadow_batch");
     return VT_OK;
 }
@@ -634,7 +658,7 @@ static int bn_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16
     const int TP = bf_launch(nullptr, g, nullptr, cin32, nullptr, g.L_out, nullptr, nullptr);
     const int tps = cdiv(g.L_out, TP);
     VT_CHECK_ARG(ws && ws_floats >= (int64_t)B * tps * 2 * Cout, "%s: workspace too small", who);
-    bf_launch(X, g, (const __bf16*)w16, cin32, conv_out, g.L_out, ws, st, nullptr, FoldOut{-1, 0, nullptr}, ibn);
+    if (bf_launch(X, g, w16, cin32, conv_out, g.L_out, ws, st, nullptr, FoldOut{-1, 0, nullptr}, ibn) < 0) return VT_ERR_ARG;
     bn_stats_finalize_launch(ws, tps, B, TP, g.L_out, Cout, eps, momentum, mean, rstd, run_mean, run_var, st);
     if (Y) bn_apply_launch(conv_out, (int64_t)B * g.L_out, Cout, mean, rstd, gamma, beta, act, Y, st);
     VT_LAUNCH_CHECK(who);
@@ -666,7 +690,7 @@ int vt_conv1d_fwd_bf16(const float* X, int B, int L_in, int Cin, const void* w16
     VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB && (mode == 0 || mode == 1),
                  "vt_conv1d_fwd_bf16: shape (K <= %d)", KMAXB);
     Geo g = geo(B, L_in, Cin, Cout, K, mode, up);
-    bf_launch(X, g, (const __bf16*)w16, cdiv(Cin, 32) * 32, Y, g.L_out, nullptr, S(stream));
+    if (bf_launch(X, g, w16, cdiv(Cin, 32) * 32, Y, g.L_out, nullptr, S(stream)) < 0) return VT_ERR_ARG;
     VT_LAUNCH_CHECK("vt_conv1d_fwd_bf16");
     return VT_OK;
 }
@@ -677,7 +701,7 @@ static int bwd_gpad(const float* dY, int B, int L_in, int Cin, const void* w16t,
     VT_CHECK_ARG(B > 0 && L_in > 0 && Cin > 0 && Cout > 0 && K > 0 && K <= KMAXB, "%s: shape", who);
     Geo f = geo(B, L_in, Cin, Cout, K, mode, up);
     Geo g = geo(B, f.L_out, Cout, Cin, K, 0, 0);  // input dY (L_out x Cout), causal pad K-1
-    bf_launch(dY, g, (const __bf16*)w16t, cdiv(Cout, 32) * 32, gpad, f.L_out + K - 1, nullptr, st, bn, fo);
+    if (bf_launch(dY, g, w16t, cdiv(Cout, 32) * 32, gpad, f.L_out + K - 1, nullptr, st, bn, fo) < 0) return VT_ERR_ARG;
     VT_LAUNCH_CHECK(who);
     return VT_OK;
 }
@@ -691,7 +715,7 @@ int vt_conv1d_bwd_gpad_bf16_bn(const float* dY, const float* Xc, const float* bn
                                int L_in, int Cin, const void* w16t, int Cout, int K, int mode, int up, float* gpad,
                                void* dxbn16, void* stream) {
     VT_CHECK_ARG(Xc && bnp && act >= 0 && act <= 3 && M > 0, "vt_conv1d_bwd_gpad_bf16_bn: BatchNorm arguments");
-    const BnB bn{Xc, bnp, act, 1.f / (float)M, (__bf16*)dxbn16};
+    const BnB bn{Xc, bnp, act, 1.f / (float)M, dxbn16};
     return bwd_gpad(dY, B, L_in, Cin, w16t, Cout, K, mode, up, gpad, S(stream), &bn, "vt_conv1d_bwd_gpad_bf16_bn");
 }
 
@@ -702,7 +726,7 @@ int vt_conv1d_bwd_dx_bf16_bn(const float* dY, const float* Xc, const float* bnp,
     const Geo f = geo(B, L_in, Cin, Cout, K, mode, up);
     VT_CHECK_ARG(!up && (mode == 0 || f.L_up > f.pad) && (mode == 0 || f.pad == 0 || edge),
                  "vt_conv1d_bwd_dx_bf16_bn: geometry (no upsample, reflect needs L > pad and an edge buffer)");
-    const BnB bn{Xc, bnp, act, 1.f / (float)M, (__bf16*)dxbn16};
+    const BnB bn{Xc, bnp, act, 1.f / (float)M, dxbn16};
     const FoldOut fo{f.pad, L_in, mode == 0 ? nullptr : edge};
     const int rc = bwd_gpad(dY, B, L_in, Cin, w16t, Cout, K, mode, up, dX, S(stream), &bn,
                             "vt_conv1d_bwd_dx_bf16_bn", fo);

@@ -28,25 +28,25 @@
 #include <stdlib.h>
 
 #include "conv.h"
+#include "h16.h"
 
 namespace vt {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int RS = 40;   // bf16 row stride of the staged window / tap rows (as conv_bf16.hip)
-constexpr int XRB = 64;  // rows per k_bn_bwd_x16 workgroup
+// rows per k_bn_bwd_x16 block: 64, or 256 (VAETEB_BNX16_ROWS; every element's value is computed
+// the same way for any block height: the same bits)
 
 // ------------------------------------------------------------------ 1. BN backward -> bf16
-template <int ACT>
+template <typename H, int ACT, int XRB = 64>
 __global__ __launch_bounds__(256) void k_bn_bwd_x16(const float* __restrict__ dy, const float* __restrict__ x2,
                                                     const float* __restrict__ bnp, int64_t M, int C, int c32,
-                                                    float invM, __bf16* __restrict__ d16) {
+                                                    float invM, H* __restrict__ d16) {
     extern __shared__ __attribute__((aligned(16))) float xl[];
     float* prm = xl;                                                // [C][8]: mean rstd gamma beta dgamma dbeta
-    __bf16* img = reinterpret_cast<__bf16*>(xl + 8 * ((C + 3) & ~3));   // [XRB][c32]
+    H* img = reinterpret_cast<H*>(xl + 8 * ((C + 3) & ~3));   // [XRB][c32]
     const int tid = threadIdx.x;
     for (int i = tid; i < 6 * C; i += 256) {
         const int k = i / C, c = i - k * C;
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_x16(const float* __restrict__ dy
                     const float4 p0 = *reinterpret_cast<const float4*>(prm + 8 * c);
                     const float2 p1 = *reinterpret_cast<const float2*>(prm + 8 * c + 4);
                     const float v = bn_bwd_val_r(va[j], vq[j], p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, ACT, invM);
-                    img[r * c32 + c] = (__bf16)v;
+                    img[r * c32 + c] = (H)v;
                 }
                 if (++c == C) {
                     c = 0;
@@ -93,11 +93,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_x16(const float* __restrict__ dy
         const int segs = c32 / 8;
         for (int i = tid; i < nr * segs; i += 256) {
             const int r = i / segs, s = i - r * segs;
-            bf16x8 v = *reinterpret_cast<const bf16x8*>(img + r * c32 + 8 * s);
+            hv8<H> v = *reinterpret_cast<const hv8<H>*>(img + r * c32 + 8 * s);
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                if (8 * s + j >= C) v[j] = (__bf16)0.f;
-            *reinterpret_cast<bf16x8*>(d16 + (r0 + r) * c32 + 8 * s) = v;
+                if (8 * s + j >= C) v[j] = (H)0.f;
+            *reinterpret_cast<hv8<H>*>(d16 + (r0 + r) * c32 + 8 * s) = v;
         }
         __syncthreads();
     }
@@ -136,8 +136,8 @@ struct DCfg {
     }
 };
 
-template <int K, int NT>
-__device__ __forceinline__ void load_taps(bf16x8* wt, const __bf16* __restrict__ w16t, int co0,
+template <typename H, int K, int NT>
+__device__ __forceinline__ void load_taps(hv8<H>* wt, const H* __restrict__ w16t, int co0,
                                           int Co, int c32, int c0) {
     using C = DCfg<K, NT>;
     const int tid = threadIdx.x;
@@ -147,12 +147,12 @@ __device__ __forceinline__ void load_taps(bf16x8* wt, const __bf16* __restrict__
         const int ic = i < K * C::TC * 4 ? i : K * C::TC * 4 - 1;
         const int oct = ic & 3, r = ic >> 2, k = r / C::TC, co = r - k * C::TC;
         const int coc = co0 + co < Co ? co0 + co : Co - 1;
-        wt[it] = *(const bf16x8*)(w16t + ((int64_t)coc * K + k) * c32 + c0 + 8 * oct);
+        wt[it] = *(const hv8<H>*)(w16t + ((int64_t)coc * K + k) * c32 + c0 + 8 * oct);
     }
 }
 
-template <int K, int NT>
-__device__ __forceinline__ void store_taps(const bf16x8* wt, __bf16* __restrict__ ws, int co0,
+template <typename H, int K, int NT>
+__device__ __forceinline__ void store_taps(const hv8<H>* wt, H* __restrict__ ws, int co0,
                                            int Co) {
     using C = DCfg<K, NT>;
     const int tid = threadIdx.x;
@@ -161,12 +161,12 @@ __device__ __forceinline__ void store_taps(const bf16x8* wt, __bf16* __restrict_
         const int i = tid + 256 * it;
         if (i >= K * C::TC * 4) continue;
         const int oct = i & 3, r = i >> 2, k = r / C::TC, co = r - k * C::TC;
-        bf16x8 v = wt[it];
+        hv8<H> v = wt[it];
         if (co0 + co >= Co) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+            for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
         }
-        *(bf16x8*)(ws + (k * C::TC + co) * RS + 8 * oct) = v;
+        *(hv8<H>*)(ws + (k * C::TC + co) * RS + 8 * oct) = v;
     }
 }
 
@@ -181,15 +181,16 @@ __device__ __forceinline__ float fold_gup(const float* __restrict__ gp, int gs, 
     return v;
 }
 
-template <int K, int NT, bool UPF, int PMX = 0>
-__global__ __launch_bounds__(256) void k_cbd16(const __bf16* __restrict__ d16, BdGeo g,
-                                               const __bf16* __restrict__ w16t, float* __restrict__ dx) {
+template <typename H, int K, int NT, bool UPF, int PMX = 0>
+__global__ __launch_bounds__(256) void k_cbd16(const H* __restrict__ d16, BdGeo g,
+                                               const H* __restrict__ w16t, float* __restrict__ dx) {
     using C = DCfg<K, NT, PMX>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
-    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
+    extern __shared__ __attribute__((aligned(16))) char lb_raw[];
+    H* const lb = reinterpret_cast<H*>(lb_raw);
     const int nch = g.nch, c32 = 32 * nch;
-    __bf16* xs = lb;                     // [nch][WIN][RS]
-    __bf16* ws = lb + nch * WIN * RS;    // [K][TC][RS]
+    H* xs = lb;                     // [nch][WIN][RS]
+    H* ws = lb + nch * WIN * RS;    // [K][TC][RS]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
     const int co0 = blockIdx.y * TC, b = blockIdx.z;
     int p0, s0 = 0, s1 = 0;
@@ -200,27 +201,27 @@ __global__ __launch_bounds__(256) void k_cbd16(const __bf16* __restrict__ d16, B
     } else {
         p0 = g.p_first + blockIdx.x * TP;   // causal: only the rows the crop keeps (p_first = pad)
     }
-    bf16x8 wt[C::NWI];
-    load_taps<K, NT>(wt, w16t, co0, g.Co, c32, 0);   // in flight during the window staging
+    hv8<H> wt[C::NWI];
+    load_taps<H, K, NT>(wt, w16t, co0, g.Co, c32, 0);   // in flight during the window staging
     // the operand window: d16 rows p0 - (K - 1) .. p0 - (K - 1) + WIN - 1 of sample b, all chunks
     // (one contiguous run of rows in HBM), 16-byte items, zero outside [0, Lf)
     {
         const int segs = 4 * nch;
-        const __bf16* db = d16 + (int64_t)b * g.Lf * c32;
+        const H* db = d16 + (int64_t)b * g.Lf * c32;
         const int rbase = p0 - (K - 1);
         constexpr int U = 8;
         for (int i0 = tid; i0 < WIN * segs; i0 += 256 * U) {
-            bf16x8 v[U];
+            hv8<H> v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int i = i0 + 256 * u;
                 const int r = i / segs, s = i - r * segs;
                 const int dr = rbase + r;
                 const bool ok = i < WIN * segs && dr >= 0 && dr < g.Lf;
-                v[u] = *(const bf16x8*)(db + (int64_t)(ok ? dr : 0) * c32 + (ok ? 8 * s : 0));
+                v[u] = *(const hv8<H>*)(db + (int64_t)(ok ? dr : 0) * c32 + (ok ? 8 * s : 0));
                 if (!ok) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[u][j] = (__bf16)0.f;
+                    for (int j = 0; j < 8; ++j) v[u][j] = (H)0.f;
                 }
             }
 #pragma unroll
@@ -228,11 +229,11 @@ __global__ __launch_bounds__(256) void k_cbd16(const __bf16* __restrict__ d16, B
                 const int i = i0 + 256 * u;
                 if (i >= WIN * segs) continue;
                 const int r = i / segs, s = i - r * segs;
-                *(bf16x8*)(xs + ((s >> 2) * WIN + r) * RS + 8 * (s & 3)) = v[u];
+                *(hv8<H>*)(xs + ((s >> 2) * WIN + r) * RS + 8 * (s & 3)) = v[u];
             }
         }
     }
-    store_taps<K, NT>(wt, ws, co0, g.Co);
+    store_taps<H, K, NT>(wt, ws, co0, g.Co);
     __syncthreads();
     f32x4 acc[PM][NT];
 #pragma unroll
@@ -241,25 +242,25 @@ __global__ __launch_bounds__(256) void k_cbd16(const __bf16* __restrict__ d16, B
         for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int ch = 0; ch < nch; ++ch) {
         const bool more = ch + 1 < nch;
-        if (more) load_taps<K, NT>(wt, w16t, co0, g.Co, c32, 32 * (ch + 1));   // in flight during the MFMAs
-        const __bf16* xq = xs + (ch * WIN + PM * 16 * wv + lr) * RS + 8 * lc;
-        const __bf16* wq = ws + lr * RS + 8 * lc;
+        if (more) load_taps<H, K, NT>(wt, w16t, co0, g.Co, c32, 32 * (ch + 1));   // in flight during the MFMAs
+        const H* xq = xs + (ch * WIN + PM * 16 * wv + lr) * RS + 8 * lc;
+        const H* wq = ws + lr * RS + 8 * lc;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            bf16x8 af[PM], bf[NT];
+            hv8<H> af[PM], bf[NT];
 #pragma unroll
-            for (int m = 0; m < PM; ++m) af[m] = *(const bf16x8*)(xq + (16 * m + k) * RS);
+            for (int m = 0; m < PM; ++m) af[m] = *(const hv8<H>*)(xq + (16 * m + k) * RS);
 #pragma unroll
-            for (int n = 0; n < NT; ++n) bf[n] = *(const bf16x8*)(wq + (k * TC + 16 * n) * RS);
+            for (int n = 0; n < NT; ++n) bf[n] = *(const hv8<H>*)(wq + (k * TC + 16 * n) * RS);
 #pragma unroll
             for (int m = 0; m < PM; ++m)
 #pragma unroll
                 for (int n = 0; n < NT; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bf[n], acc[m][n], 0, 0, 0);
+                    acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
         }
         __syncthreads();
         if (more) {
-            store_taps<K, NT>(wt, ws, co0, g.Co);
+            store_taps<H, K, NT>(wt, ws, co0, g.Co);
             __syncthreads();
         }
     }
@@ -334,39 +335,39 @@ static int ups_rows(int L, int pad, int TP) {
     return -1;
 }
 
-template <int K, int NT>
-int cbd_nt(const __bf16* d16, BdGeo g, int B, const __bf16* w16t, float* dx, bool upf, hipStream_t st) {
+template <typename H, int K, int NT>
+int cbd_nt(const H* d16, BdGeo g, int B, const H* w16t, float* dx, bool upf, hipStream_t st) {
     using C = DCfg<K, NT>;
     const int lds = C::lds_bytes(g.nch, upf);
     if (upf) {
         g.TS = ups_rows(g.L, g.pad, C::TP);
         if (g.TS < 1) return VT_ERR_ARG;
         dim3 grid(cdiv(g.L, g.TS), cdiv(g.Co, C::TC), B);
-        hipLaunchKernelGGL((k_cbd16<K, NT, true>), grid, dim3(256), lds, st, d16, g, w16t, dx);
+        hipLaunchKernelGGL((k_cbd16<H, K, NT, true>), grid, dim3(256), lds, st, d16, g, w16t, dx);
     } else if (NT <= 2 && g.p_end - g.p_first <= 256) {
         // short rows (the encoders' L = 256): 128-position tiles, two per sample, every wave
         // busy (a 512-position tile left half of its waves without rows).  Each output's sum
         // over chunks and taps is one lane's, in the same order: the same bits
         using C2 = DCfg<K, NT, 2>;
         dim3 grid(cdiv(g.p_end - g.p_first, C2::TP), cdiv(g.Co, C2::TC), B);
-        hipLaunchKernelGGL((k_cbd16<K, NT, false, 2>), grid, dim3(256), C2::lds_bytes(g.nch, false), st, d16, g, w16t,
+        hipLaunchKernelGGL((k_cbd16<H, K, NT, false, 2>), grid, dim3(256), C2::lds_bytes(g.nch, false), st, d16, g, w16t,
                            dx);
     } else {
         dim3 grid(cdiv(g.p_end - g.p_first, C::TP), cdiv(g.Co, C::TC), B);
-        hipLaunchKernelGGL((k_cbd16<K, NT, false>), grid, dim3(256), lds, st, d16, g, w16t, dx);
+        hipLaunchKernelGGL((k_cbd16<H, K, NT, false>), grid, dim3(256), lds, st, d16, g, w16t, dx);
     }
     return VT_OK;
 }
 
-template <int K>
-int cbd_k(const __bf16* d16, const BdGeo& g, int B, const __bf16* w16t, float* dx, bool upf, hipStream_t st) {
+template <typename H, int K>
+int cbd_k(const H* d16, const BdGeo& g, int B, const H* w16t, float* dx, bool upf, hipStream_t st) {
     switch (cdiv(g.Co, 16) < 6 ? cdiv(g.Co, 16) : 6) {
-        case 1: return cbd_nt<K, 1>(d16, g, B, w16t, dx, upf, st);
-        case 2: return cbd_nt<K, 2>(d16, g, B, w16t, dx, upf, st);
-        case 3: return cbd_nt<K, 3>(d16, g, B, w16t, dx, upf, st);
-        case 4: return cbd_nt<K, 4>(d16, g, B, w16t, dx, upf, st);
-        case 5: return cbd_nt<K, 5>(d16, g, B, w16t, dx, upf, st);
-        default: return cbd_nt<K, 6>(d16, g, B, w16t, dx, upf, st);
+        case 1: return cbd_nt<H, K, 1>(d16, g, B, w16t, dx, upf, st);
+        case 2: return cbd_nt<H, K, 2>(d16, g, B, w16t, dx, upf, st);
+        case 3: return cbd_nt<H, K, 3>(d16, g, B, w16t, dx, upf, st);
+        case 4: return cbd_nt<H, K, 4>(d16, g, B, w16t, dx, upf, st);
+        case 5: return cbd_nt<H, K, 5>(d16, g, B, w16t, dx, upf, st);
+        default: return cbd_nt<H, K, 6>(d16, g, B, w16t, dx, upf, st);
     }
 }
 
@@ -384,22 +385,34 @@ int vt_batchnorm_bwd_x16(const float* dY, const float* Xc, const float* bnp, int
     VT_CHECK_ARG(dY && Xc && bnp && d16 && M > 0 && C > 0 && C <= 1024 && act >= 0 && act <= 3,
                  "vt_batchnorm_bwd_x16: arguments");
     const int c32 = cdiv(C, 32) * 32;
-    const size_t lds = (size_t)8 * ((C + 3) & ~3) * 4 + (size_t)XRB * c32 * 2;
+    static const int xrb = getenv("VAETEB_BNX16_ROWS") && atoi(getenv("VAETEB_BNX16_ROWS")) == 256 ? 256 : 64;
+    const size_t lds = (size_t)8 * ((C + 3) & ~3) * 4 + (size_t)xrb * c32 * 2;
     VT_CHECK_ARG(lds <= 160 * 1024, "vt_batchnorm_bwd_x16: C too large");
     // at most 8 workgroups per CU of 64-row blocks, each walking several blocks: the per-workgroup
     // parameter staging (6 C loads + a barrier) is paid once per workgroup, not per block
     // (the same element computation: the same bits)
-    const int64_t blocks = (M + XRB - 1) / XRB;
+    const int64_t blocks = (M + xrb - 1) / xrb;
     static const int cap = getenv("VAETEB_BNX16_GRID") ? atoi(getenv("VAETEB_BNX16_GRID")) : 2048;
     const dim3 grid((unsigned)(blocks < cap ? blocks : cap));
     const float invM = 1.f / (float)M;
     hipStream_t st = S(stream);
-    switch (act) {
-        case 0: hipLaunchKernelGGL(k_bn_bwd_x16<0>, grid, dim3(256), lds, st, dY, Xc, bnp, M, C, c32, invM, (__bf16*)d16); break;
-        case 1: hipLaunchKernelGGL(k_bn_bwd_x16<1>, grid, dim3(256), lds, st, dY, Xc, bnp, M, C, c32, invM, (__bf16*)d16); break;
-        case 2: hipLaunchKernelGGL(k_bn_bwd_x16<2>, grid, dim3(256), lds, st, dY, Xc, bnp, M, C, c32, invM, (__bf16*)d16); break;
-        default: hipLaunchKernelGGL(k_bn_bwd_x16<3>, grid, dim3(256), lds, st, dY, Xc, bnp, M, C, c32, invM, (__bf16*)d16); break;
-    }
+#define VT_BNX(A, R) hipLaunchKernelGGL((k_bn_bwd_x16<H, A, R>), grid, dim3(256), lds, st, dY, Xc, bnp, M, C, c32, invM, (H*)d16)
+    VT_H16(if (xrb == 256) {
+        switch (act) {
+            case 0: VT_BNX(0, 256); break;
+            case 1: VT_BNX(1, 256); break;
+            case 2: VT_BNX(2, 256); break;
+            default: VT_BNX(3, 256); break;
+        }
+    } else {
+        switch (act) {
+            case 0: VT_BNX(0, 64); break;
+            case 1: VT_BNX(1, 64); break;
+            case 2: VT_BNX(2, 64); break;
+            default: VT_BNX(3, 64); break;
+        }
+    });
+#undef VT_BNX
     VT_LAUNCH_CHECK("vt_batchnorm_bwd_x16");
     return VT_OK;
 }
@@ -428,21 +441,20 @@ int vt_conv1d_bwd_dx16(const void* d16, int B, int L_in, int Cin, const void* w1
     g.p_end = mode == 0 ? f.pad + L_in : g.Lp;
     hipStream_t st = S(stream);
     int rc = VT_ERR_ARG;
-    const __bf16* a = (const __bf16*)d16;
-    const __bf16* w = (const __bf16*)w16t;
-    switch (K) {
-        case 1: rc = cbd_k<1>(a, g, B, w, dX, up, st); break;
-        case 2: rc = cbd_k<2>(a, g, B, w, dX, up, st); break;
-        case 3: rc = cbd_k<3>(a, g, B, w, dX, up, st); break;
-        case 4: rc = cbd_k<4>(a, g, B, w, dX, up, st); break;
-        case 5: rc = cbd_k<5>(a, g, B, w, dX, up, st); break;
-        case 6: rc = cbd_k<6>(a, g, B, w, dX, up, st); break;
-        case 7: rc = cbd_k<7>(a, g, B, w, dX, up, st); break;
-        case 8: rc = cbd_k<8>(a, g, B, w, dX, up, st); break;
-        case 9: rc = cbd_k<9>(a, g, B, w, dX, up, st); break;
-        case 10: rc = cbd_k<10>(a, g, B, w, dX, up, st); break;
-        default: rc = cbd_k<11>(a, g, B, w, dX, up, st); break;
-    }
+    VT_H16(const H* a = (const H*)d16; const H* w = (const H*)w16t;
+           switch (K) {
+               case 1: rc = cbd_k<H, 1>(a, g, B, w, dX, up, st); break;
+               case 2: rc = cbd_k<H, 2>(a, g, B, w, dX, up, st); break;
+               case 3: rc = cbd_k<H, 3>(a, g, B, w, dX, up, st); break;
+               case 4: rc = cbd_k<H, 4>(a, g, B, w, dX, up, st); break;
+               case 5: rc = cbd_k<H, 5>(a, g, B, w, dX, up, st); break;
+               case 6: rc = cbd_k<H, 6>(a, g, B, w, dX, up, st); break;
+               case 7: rc = cbd_k<H, 7>(a, g, B, w, dX, up, st); break;
+               case 8: rc = cbd_k<H, 8>(a, g, B, w, dX, up, st); break;
+               case 9: rc = cbd_k<H, 9>(a, g, B, w, dX, up, st); break;
+               case 10: rc = cbd_k<H, 10>(a, g, B, w, dX, up, st); break;
+               default: rc = cbd_k<H, 11>(a, g, B, w, dX, up, st); break;
+           });
     VT_CHECK_ARG(rc == VT_OK, "vt_conv1d_bwd_dx16: tile too small for the upsample fold");
     VT_LAUNCH_CHECK("vt_conv1d_bwd_dx16");
     if (!up && mode == 1 && f.pad > 0) {

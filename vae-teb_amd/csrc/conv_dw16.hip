@@ -6,6 +6,7 @@
 #include <stdlib.h>
 
 #include "conv.h"
+#include "h16.h"
 
 namespace vt {
 
@@ -13,8 +14,6 @@ extern int g_conv_kern;   // conv_bf16.hip (vt_conv_bf16_set_kernels)
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int KMAXB = 11;
 
 // ------------------------------------------------------------ weight grad
@@ -33,11 +32,12 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 constexpr int DWR = 64;  // rows per staged chunk (2 MFMA k-steps)
 constexpr int KMAXB_DW = 11;
 
-__device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int row0, int col0, int stride) {
+template <typename H>
+__device__ __forceinline__ hv8<H> tr_frag(const H* img, int row0, int col0, int stride) {
     // lane 4q+p of each 16-lane group addresses row (row0 + q), columns col0 + 4p .. +3; two reads
     // (rows +0..3 and +4..7 of the lane group's 8-row block)
     const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const __bf16* a0 = img + (row0 + 8 * g + q) * stride + col0 + 4 * p;
+    const H* a0 = img + (row0 + 8 * g + q) * stride + col0 + 4 * p;
     const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
     const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (__attribute__((address_space(3))) v4i16*)(a0 + 4 * stride));
@@ -45,27 +45,28 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int row0, int col0,
     // miscompiled (each lane's element 0 replicated by v_perm_b32)
     typedef short v8i16 __attribute__((ext_vector_type(8)));
     const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(hv8<H>, r);
 }
 
 // DYB: dY given in bf16 (dyb16, row stride dys = ceil8(Cout)), e.g. the BN input
 // gradient written by the fused backward-data kernel (k_conv_bf16 BNB + dbf).
 // IBN: x is the previous block's pre-BN conv output, its BatchNorm + activation (bi) applied
 // while the window is staged (parameters in LDS at byte ipo, channel stride ceil16(Cin))
-template <int K, int PPW, bool DYB = false, int NWV = 4, bool IBN = false>
+template <int K, int PPW, bool DYB = false, int NWV = 4, bool IBN = false, typename H = __bf16>
 __global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restrict__ dy, const float* __restrict__ x, Geo g,
                                                       int64_t rows_per_split, int NTc, int npairs, int dstride,
                                                       int xstride, float* __restrict__ part,
-                                                      const __bf16* __restrict__ dyb16, int dys, BnIn bi, int ipo) {
-    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
+                                                      const H* __restrict__ dyb16, int dys, BnIn bi, int ipo) {
+    extern __shared__ __attribute__((aligned(16))) char lb_raw[];
+    H* const lb = reinterpret_cast<H*>(lb_raw);
     float* ip = reinterpret_cast<float*>(reinterpret_cast<char*>(lb) + ipo);
     const int ics = (g.Cin + 15) / 16 * 16;
     if constexpr (IBN) {
         stage_bn_in(bi, g.Cin, ip, ics);
         __syncthreads();
     }
-    __bf16* ds = lb;                          // [DWR][dstride]   dY rows
-    __bf16* xs = lb + DWR * dstride;          // [DWR + K - 1 (+pad)][xstride] input window
+    H* ds = lb;                          // [DWR][dstride]   dY rows
+    H* xs = lb + DWR * dstride;          // [DWR + K - 1 (+pad)][xstride] input window
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
     int mt[PPW], nt[PPW];
     bool act[PPW];
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restri
         constexpr int UR = K <= 3 ? 1 : (IBN ? 2 : 4);   // small K, input BN: registers (occupancy) first
         const int nd = DWR * (cout16 / 4), nx = (DWR + K - 1) * (cin16 / 4);
         if constexpr (DYB) {
-            const __bf16* db16 = dyb16 + ((int64_t)b * g.L_out + t0) * dys;
+            const H* db16 = dyb16 + ((int64_t)b * g.L_out + t0) * dys;
             typedef short v4s __attribute__((ext_vector_type(4)));
             for (int i0 = tid; i0 < nd; i0 += 64 * NWV * UR) {
                 v4s v[UR];
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restri
                     const int t = i / (cout16 / 4), c = 4 * (i - t * (cout16 / 4));
                     if (i < nd)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) ds[t * dstride + c + j] = (__bf16)v[u][j];
+                        for (int j = 0; j < 4; ++j) ds[t * dstride + c + j] = (H)v[u][j];
                 }
             }
         }
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restri
                 const int t = i / (cin16 / 4), c = 4 * (i - t * (cin16 / 4));
                 if (i < nx)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) xs[t * xstride + c + j] = (__bf16)v[u][j];
+                    for (int j = 0; j < 4; ++j) xs[t * xstride + c + j] = (H)v[u][j];
             }
         }
         __syncthreads();
@@ -168,11 +169,11 @@ __global__ __launch_bounds__(64 * NWV) void k_conv_dw_bf16(const float* __restri
 #pragma unroll
             for (int j = 0; j < PPW; ++j) {
                 // no early-out on inactive pairs: the transposed read needs all 64 lanes (EXEC all ones)
-                const bf16x8 a = tr_frag(ds, 32 * s, 16 * mt[j], dstride);
+                const hv8<H> a = tr_frag<H>(ds, 32 * s, 16 * mt[j], dstride);
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    const bf16x8 bb = tr_frag(xs, 32 * s + k, 16 * nt[j], xstride);
-                    acc[j][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[j][k], 0, 0, 0);
+                    const hv8<H> bb = tr_frag<H>(xs, 32 * s + k, 16 * nt[j], xstride);
+                    acc[j][k] = mfma16(a, bb, acc[j][k]);
                 }
             }
         }
@@ -211,17 +212,18 @@ constexpr int CDW_UF_WIDE = 12;   // ... for the 256-row chunks
 // CR: rows per chunk — 64 (DWR), or 256 for the narrow layers (dY <= 32 channels: four times
 // the MFMA work per staged chunk, the same k-step order, so the same bits)
 // IBN: as k_conv_dw_bf16 (the previous block's BatchNorm + act applied as the window is formed)
-template <int K, int PPW, int NWV, int CR = DWR, bool IBN = false>
-__global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ dyb16, int dys,
+template <int K, int PPW, int NWV, int CR = DWR, bool IBN = false, typename H = __bf16>
+__global__ __launch_bounds__(64 * NWV) void k_cdw16(const H* __restrict__ dyb16, int dys,
                                                    const float* __restrict__ x, Geo g, int64_t rows_per_split,
                                                    int NTc, int npairs, int dstride, int xstride,
                                                    float* __restrict__ part, int64_t total, BnIn bi, int ipo) {
     constexpr int NT = 64 * NWV;
     constexpr int UD = CR == DWR ? CDW_UD * 256 / NT : CR * 4 / NT;   // CR 256: dY rows of <= 4 segments
     constexpr int UF = CR == DWR ? CDW_UF * 256 / NT : CDW_UF_WIDE * 256 / NT;
-    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
-    __bf16* ds = lb;                          // [CR][dstride]   dY rows
-    __bf16* xs = lb + CR * dstride;           // [CR + K - 1 (+pad)][xstride] input window
+    extern __shared__ __attribute__((aligned(16))) char lb_raw[];
+    H* const lb = reinterpret_cast<H*>(lb_raw);
+    H* ds = lb;                          // [CR][dstride]   dY rows
+    H* xs = lb + CR * dstride;           // [CR + K - 1 (+pad)][xstride] input window
     float* F = reinterpret_cast<float*>(lb + CR * dstride + (CR + KMAXB_DW + 8) * xstride);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int mt[PPW], nt[PPW];
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
     if constexpr (IBN) stage_bn_in(bi, g.Cin, ip, cin16);   // read after the first chunk's barrier
     // one chunk's operands into registers: dY segments and the F rows (float4 from the
     // boundary at or below the source run)
-    bf16x8 dv[UD];
+    hv8<H> dv[UD];
     float4 fv[UF];
     struct Chunk {
         int b, t0, n, lo, hi, off, nv;
@@ -257,16 +259,16 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
         c.t0 = (int)(r - (int64_t)c.b * g.L_out);
         c.n = g.L_out - c.t0 < CR ? g.L_out - c.t0 : CR;
         if (r + c.n > r1) c.n = (int)(r1 - r);
-        const __bf16* db = dyb16 + ((int64_t)c.b * g.L_out + c.t0) * dys;
+        const H* db = dyb16 + ((int64_t)c.b * g.L_out + c.t0) * dys;
 #pragma unroll
         for (int u = 0; u < UD; ++u) {
             const int i = tid + NT * u;
             const int t = i / dsegs, sg = i - t * dsegs;
             const bool ok = i < CR * dsegs && t < c.n && 8 * sg < dys;
-            dv[u] = *(const bf16x8*)(db + (int64_t)(ok ? t : 0) * dys + (ok ? 8 * sg : 0));
+            dv[u] = *(const hv8<H>*)(db + (int64_t)(ok ? t : 0) * dys + (ok ? 8 * sg : 0));
             if (!ok) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) dv[u][j] = (__bf16)0.f;
+                for (int j = 0; j < 8; ++j) dv[u][j] = (H)0.f;
             }
         }
         src_span(g, c.t0, c.n + K - 1, c.lo, c.hi);
@@ -299,7 +301,7 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
             const int i = tid + NT * u;
             if (i < CR * dsegs) {
                 const int t = i / dsegs, sg = i - t * dsegs;
-                *(bf16x8*)(ds + t * dstride + 8 * sg) = dv[u];
+                *(hv8<H>*)(ds + t * dstride + 8 * sg) = dv[u];
             }
         }
 #pragma unroll
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
                 const bool in = t < cur.n + K - 1 && src_row(g, tp, i0, i1, l1);
                 const float* p0 = F + cur.off + (in ? i0 - cur.lo : 0) * g.Cin;
                 const float* p1 = F + cur.off + (in ? i1 - cur.lo : 0) * g.Cin;
-                bf16x8 v;
+                hv8<H> v;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
@@ -328,9 +330,9 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
                         a = bn_relu_at(ip, cin16, cb + j, a);
                         q = g.up ? bn_relu_at(ip, cin16, cb + j, q) : 0.f;
                     }
-                    v[j] = (__bf16)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
+                    v[j] = (H)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
                 }
-                *(bf16x8*)(xs + t * xstride + cb) = v;
+                *(hv8<H>*)(xs + t * xstride + cb) = v;
             }
         }
         __syncthreads();
@@ -342,11 +344,11 @@ __global__ __launch_bounds__(64 * NWV) void k_cdw16(const __bf16* __restrict__ d
             if (!act[0]) break;  // wave-uniform: a wave without pairs only stages
 #pragma unroll
             for (int j = 0; j < PPW; ++j) {
-                const bf16x8 a = tr_frag(ds, 32 * s, 16 * mt[j], dstride);
+                const hv8<H> a = tr_frag<H>(ds, 32 * s, 16 * mt[j], dstride);
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    const bf16x8 bb = tr_frag(xs, 32 * s + k, 16 * nt[j], xstride);
-                    acc[j][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[j][k], 0, 0, 0);
+                    const hv8<H> bb = tr_frag<H>(xs, 32 * s + k, 16 * nt[j], xstride);
+                    acc[j][k] = mfma16(a, bb, acc[j][k]);
                 }
             }
         }
@@ -380,7 +382,7 @@ using namespace vt;
 extern "C" {
 
 static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin, int Cout, int K, int mode, int up,
-                      float* dW, int accumulate, float* ws, int64_t ws_floats, hipStream_t st, const __bf16* dy16,
+                      float* dW, int accumulate, float* ws, int64_t ws_floats, hipStream_t st, const void* dy16,
                       int dys = 0, const BnIn* ibn = nullptr) {
     VT_CHECK_ARG(B > 0 && L_in > 0 && K > 0 && K <= KMAXB && Cin > 0 && Cout > 0 && Cin <= 128 && Cout <= 128,
                  "vt_conv1d_bwd_weight_bf16: shape (K <= %d, channels <= 128)", KMAXB);
@@ -435,35 +437,40 @@ static int bwd_weight(const float* dY, const float* X, int B, int L_in, int Cin,
     const BnIn bi = ibn ? *ibn : BnIn{};
     const int ib = ibn ? 16 * (16 * cdiv(Cin, 16)) : 0;
     const int ipo_w = ((int)lds_wide + 15) & ~15, ipo_f = ((int)lds_flat + 15) & ~15, ipo_d = ((int)lds + 15) & ~15;
-#define VT_DWB_ONE(IB)                                                                                          \
+#define VT_DWB_ONE(IB, HT)                                                                                      \
     if (wide && nwv == 8)                                                                                       \
-        hipLaunchKernelGGL((k_cdw16<KK, PP, 8, 256, IB>), grid, dim3(512), ipo_w + ib, st, dy16, dys, X, g, rps,  \
-                           NTc, npairs, dstride, xstride, ws, total_x, bi, ipo_w);                             \
+        hipLaunchKernelGGL((k_cdw16<KK, PP, 8, 256, IB, HT>), grid, dim3(512), ipo_w + ib, st, (const HT*)dy16,   \
+                           dys, X, g, rps, NTc, npairs, dstride, xstride, ws, total_x, bi, ipo_w);             \
     else if (wide)                                                                                              \
-        hipLaunchKernelGGL((k_cdw16<KK, PP, 4, 256, IB>), grid, dim3(256), ipo_w + ib, st, dy16, dys, X, g, rps,  \
-                           NTc, npairs, dstride, xstride, ws, total_x, bi, ipo_w);                             \
+        hipLaunchKernelGGL((k_cdw16<KK, PP, 4, 256, IB, HT>), grid, dim3(256), ipo_w + ib, st, (const HT*)dy16,   \
+                           dys, X, g, rps, NTc, npairs, dstride, xstride, ws, total_x, bi, ipo_w);             \
     else if (flat && nwv == 8)                                                                                  \
-        hipLaunchKernelGGL((k_cdw16<KK, PP, 8, DWR, IB>), grid, dim3(512), ipo_f + ib, st, dy16, dys, X, g, rps,  \
-                           NTc, npairs, dstride, xstride, ws, total_x, bi, ipo_f);                             \
+        hipLaunchKernelGGL((k_cdw16<KK, PP, 8, DWR, IB, HT>), grid, dim3(512), ipo_f + ib, st, (const HT*)dy16,   \
+                           dys, X, g, rps, NTc, npairs, dstride, xstride, ws, total_x, bi, ipo_f);             \
     else if (flat)                                                                                              \
-        hipLaunchKernelGGL((k_cdw16<KK, PP, 4, DWR, IB>), grid, dim3(256), ipo_f + ib, st, dy16, dys, X, g, rps,  \
-                           NTc, npairs, dstride, xstride, ws, total_x, bi, ipo_f);                             \
+        hipLaunchKernelGGL((k_cdw16<KK, PP, 4, DWR, IB, HT>), grid, dim3(256), ipo_f + ib, st, (const HT*)dy16,   \
+                           dys, X, g, rps, NTc, npairs, dstride, xstride, ws, total_x, bi, ipo_f);             \
     else if (dy16 && nwv == 8)                                                                                  \
-        hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true, 8, IB>), grid, dim3(512), ipo_d + ib, st, dY, X, g, rps, \
-                           NTc, npairs, dstride, xstride, ws, dy16, dys, bi, ipo_d);                           \
+        hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true, 8, IB, HT>), grid, dim3(512), ipo_d + ib, st, dY, X, g,  \
+                           rps, NTc, npairs, dstride, xstride, ws, (const HT*)dy16, dys, bi, ipo_d);           \
     else if (dy16)                                                                                              \
-        hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true, 4, IB>), grid, dim3(256), ipo_d + ib, st, dY, X, g, rps, \
-                           NTc, npairs, dstride, xstride, ws, dy16, dys, bi, ipo_d);                           \
+        hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, true, 4, IB, HT>), grid, dim3(256), ipo_d + ib, st, dY, X, g,  \
+                           rps, NTc, npairs, dstride, xstride, ws, (const HT*)dy16, dys, bi, ipo_d);           \
     else if (!IB)                                                                                               \
-        hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, false, 4, false>), grid, dim3(256), ipo_d, st, dY, X, g, rps,   \
-                           NTc, npairs, dstride, xstride, ws, nullptr, 0, bi, ipo_d);
+        hipLaunchKernelGGL((k_conv_dw_bf16<KK, PP, false, 4, false, HT>), grid, dim3(256), ipo_d, st, dY, X, g,   \
+                           rps, NTc, npairs, dstride, xstride, ws, (const HT*)nullptr, 0, bi, ipo_d);
+    // fp16 operands (h16.h): the default kernel set; the conv-stack fold (ibn) is bf16-only
+    const bool f16 = h16_format() != 0;
+    VT_CHECK_ARG(!(f16 && ibn), "vt_conv1d_bwd_weight_bf16_in: the conv-stack fold has no fp16 form");
 #define VT_DWB(KK_, PP_)                    \
     if (K == KK_ && ppw == PP_) {           \
         constexpr int KK = KK_, PP = PP_;   \
-        if (ibn) {                          \
-            VT_DWB_ONE(true)                \
+        if (f16) {                          \
+            VT_DWB_ONE(false, _Float16)     \
+        } else if (ibn) {                   \
+            VT_DWB_ONE(true, __bf16)        \
         } else {                            \
-            VT_DWB_ONE(false)               \
+            VT_DWB_ONE(false, __bf16)       \
         }                                   \
     }
 #define VT_DWB6(KK) VT_DWB(KK, 1) VT_DWB(KK, 2) VT_DWB(KK, 3) VT_DWB(KK, 4) VT_DWB(KK, 5) VT_DWB(KK, 6)
@@ -493,8 +500,7 @@ int vt_conv1d_bwd_weight_bf16_dy16(const void* dY16, const float* X, int B, int 
                                    int mode, int up, float* dW, int accumulate, float* ws, int64_t ws_floats,
                                    void* stream) {
     VT_CHECK_ARG(dY16 != nullptr, "vt_conv1d_bwd_weight_bf16_dy16: null dY16");
-    return bwd_weight(nullptr, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream),
-                      (const __bf16*)dY16);
+    return bwd_weight(nullptr, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream), dY16);
 }
 
 int vt_conv1d_bwd_weight_bf16_dy16s(const void* dY16, int dys, const float* X, int B, int L_in, int Cin, int Cout,
@@ -503,7 +509,7 @@ int vt_conv1d_bwd_weight_bf16_dy16s(const void* dY16, int dys, const float* X, i
     VT_CHECK_ARG(dY16 != nullptr && dys >= ((Cout + 7) & ~7) && dys % 8 == 0,
                  "vt_conv1d_bwd_weight_bf16_dy16s: null dY16 or row stride %d (a multiple of 8 >= ceil8(Cout))", dys);
     return bwd_weight(nullptr, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream),
-                      (const __bf16*)dY16, dys);
+                      dY16, dys);
 }
 
 // the weight gradient of a block whose input is the previous block's pre-BN conv output X
@@ -520,7 +526,7 @@ int vt_conv1d_bwd_weight_bf16_in(const float* dY, const void* dY16, int dys, con
     (void)dY;
     const BnIn bi{in_mean, in_rstd, in_gamma, in_beta, in_act};
     return bwd_weight(dY, X, B, L_in, Cin, Cout, K, mode, up, dW, accumulate, ws, ws_floats, S(stream),
-                      (const __bf16*)dY16, dY16 ? dys : 0, &bi);
+                      dY16, dY16 ? dys : 0, &bi);
 }
 
 }  // extern "C"

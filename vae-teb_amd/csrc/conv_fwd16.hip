@@ -16,13 +16,12 @@
 // taps prefetched into registers during the current chunk's MFMAs (F's LDS is reused
 // for the taps).
 #include "conv.h"
+#include "h16.h"
 
 namespace vt {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int RS = 40;   // bf16 row stride of window / tap rows (as conv_bf16.hip)
 
@@ -36,21 +35,22 @@ struct FCfg {
 
 // IBN: x is the previous block's pre-BN conv output; its BatchNorm + activation (bi, staged
 // into LDS at byte ipo) are applied to the source samples as the window is formed
-template <int K, int NT, bool IBN = false>
+template <int K, int NT, bool IBN = false, typename H = __bf16>
 __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo g, int nch,
-                                               const __bf16* __restrict__ w16, float* __restrict__ y, int Lo,
+                                               const H* __restrict__ w16, float* __restrict__ y, int Lo,
                                                float* __restrict__ stats, int64_t total, BnIn bi, int ipo) {
     using C = FCfg<K, NT>;
     constexpr int PM = C::PM, TC = C::TC, TP = C::TP, WIN = C::WIN;
-    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
+    extern __shared__ __attribute__((aligned(16))) char lb_raw[];
+    H* const lb = reinterpret_cast<H*>(lb_raw);
     const int cin32 = 32 * nch;
-    __bf16* xs = lb;                                              // [nch][WIN][RS]
+    H* xs = lb;                                              // [nch][WIN][RS]
     char* rest = reinterpret_cast<char*>(lb + nch * WIN * RS);   // F (fp32 source rows), then the taps
     float* F = reinterpret_cast<float*>(rest);
-    __bf16* ws = reinterpret_cast<__bf16*>(rest);
+    H* ws = reinterpret_cast<H*>(rest);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lc = lane >> 4;
     const int t0 = blockIdx.x * TP, co0 = blockIdx.y * TC, b = blockIdx.z;
-    bf16x8 wt[C::NWI];
+    hv8<H> wt[C::NWI];
     auto load_taps = [&](int c0) {
 #pragma unroll
         for (int it = 0; it < C::NWI; ++it) {
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
             const int ic = i < K * TC * 4 ? i : K * TC * 4 - 1;
             const int oct = ic & 3, r = ic >> 2, k = r / TC, co = r - k * TC;
             const int coc = co0 + co < g.Cout ? co0 + co : g.Cout - 1;
-            wt[it] = *(const bf16x8*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
+            wt[it] = *(const hv8<H>*)(w16 + ((int64_t)coc * K + k) * cin32 + c0 + 8 * oct);
         }
     };
     load_taps(0);   // in flight during the window staging
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
             const bool in = tp < Lo + K - 1 && src_row(g, tp, i0, i1, l1);
             const float* p0 = F + off + (in ? i0 - lo : 0) * g.Cin;
             const float* p1 = F + off + (in ? i1 - lo : 0) * g.Cin;
-            bf16x8 v;
+            hv8<H> v;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int c = cb + j < g.Cin ? cb + j : g.Cin - 1;
@@ -120,9 +120,9 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
                     q = g.up ? bn_relu_at(ip, cin32, cb + j, q) : 0.f;
                 }
                 // conv.h src_vec's values
-                v[j] = (__bf16)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
+                v[j] = (H)((in && cb + j < g.Cin) ? (g.up ? up_lerp(a, q, l1) : a) : 0.f);
             }
-            *(bf16x8*)(xs + ((s >> 2) * WIN + r) * RS + 8 * (s & 3)) = v;
+            *(hv8<H>*)(xs + ((s >> 2) * WIN + r) * RS + 8 * (s & 3)) = v;
         }
     }
     __syncthreads();   // F is dead: the taps take its place
@@ -132,12 +132,12 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
             const int i = tid + 256 * it;
             if (i >= K * TC * 4) continue;
             const int oct = i & 3, r = i >> 2, k = r / TC, co = r - k * TC;
-            bf16x8 v = wt[it];
+            hv8<H> v = wt[it];
             if (co0 + co >= g.Cout) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+                for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
             }
-            *(bf16x8*)(ws + (k * TC + co) * RS + 8 * oct) = v;
+            *(hv8<H>*)(ws + (k * TC + co) * RS + 8 * oct) = v;
         }
     };
     store_taps();
@@ -150,20 +150,20 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
     for (int ch = 0; ch < nch; ++ch) {
         const bool more = ch + 1 < nch;
         if (more) load_taps(32 * (ch + 1));
-        const __bf16* xq = xs + (ch * WIN + PM * 16 * wv + lr) * RS + 8 * lc;
-        const __bf16* wq = ws + lr * RS + 8 * lc;
+        const H* xq = xs + (ch * WIN + PM * 16 * wv + lr) * RS + 8 * lc;
+        const H* wq = ws + lr * RS + 8 * lc;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            bf16x8 af[PM], bf[NT];
+            hv8<H> af[PM], bf[NT];
 #pragma unroll
-            for (int m = 0; m < PM; ++m) af[m] = *(const bf16x8*)(xq + (16 * m + k) * RS);
+            for (int m = 0; m < PM; ++m) af[m] = *(const hv8<H>*)(xq + (16 * m + k) * RS);
 #pragma unroll
-            for (int n = 0; n < NT; ++n) bf[n] = *(const bf16x8*)(wq + (k * TC + 16 * n) * RS);
+            for (int n = 0; n < NT; ++n) bf[n] = *(const hv8<H>*)(wq + (k * TC + 16 * n) * RS);
 #pragma unroll
             for (int m = 0; m < PM; ++m)
 #pragma unroll
                 for (int n = 0; n < NT; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bf[n], acc[m][n], 0, 0, 0);
+                    acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
         }
         __syncthreads();
         if (more) {
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void k_cfw16(const float* __restrict__ x, Geo 
 
 // source rows a window of WIN padded positions can read: WIN + 2 (x2 upsample: half, + 2)
 template <int K, int NT>
-int cfw_nt(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,
+int cfw_nt(const float* x, const Geo& g, const void* w16, float* y, int Lo, float* stats, hipStream_t st,
            const BnIn* ibn) {
     using C = FCfg<K, NT>;
     const int nch = cdiv(g.Cin, 32);
@@ -252,16 +252,21 @@ int cfw_nt(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, fl
     dim3 grid(cdiv(Lo, C::TP), cdiv(g.Cout, C::TC), g.B);
     const int64_t total = (int64_t)g.B * g.L_in * g.Cin;
     const BnIn bi = ibn ? *ibn : BnIn{};
-    if (ibn)
-        hipLaunchKernelGGL((k_cfw16<K, NT, true>), grid, dim3(256), lds, st, x, g, nch, w16, y, Lo, stats, total, bi,
-                           ipo);
+    if (h16_format()) {   // fp16 operands (h16.h); the conv-stack fold (ibn) is bf16-only
+        if (ibn) return VT_ERR_ARG;
+        hipLaunchKernelGGL((k_cfw16<K, NT, false, _Float16>), grid, dim3(256), lds, st, x, g, nch,
+                           (const _Float16*)w16, y, Lo, stats, total, bi, ipo);
+    } else if (ibn)
+        hipLaunchKernelGGL((k_cfw16<K, NT, true, __bf16>), grid, dim3(256), lds, st, x, g, nch, (const __bf16*)w16, y, Lo, stats,
+                           total, bi, ipo);
     else
-        hipLaunchKernelGGL((k_cfw16<K, NT>), grid, dim3(256), lds, st, x, g, nch, w16, y, Lo, stats, total, bi, ipo);
+        hipLaunchKernelGGL((k_cfw16<K, NT, false, __bf16>), grid, dim3(256), lds, st, x, g, nch, (const __bf16*)w16, y, Lo, stats,
+                           total, bi, ipo);
     return C::TP;
 }
 
 template <int K>
-int cfw_k(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,
+int cfw_k(const float* x, const Geo& g, const void* w16, float* y, int Lo, float* stats, hipStream_t st,
           const BnIn* ibn) {
     switch (cdiv(g.Cout, 16) < 6 ? cdiv(g.Cout, 16) : 6) {
         case 1: return cfw_nt<K, 1>(x, g, w16, y, Lo, stats, st, ibn);
@@ -278,7 +283,7 @@ int cfw_k(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, flo
 // the flat-staged forward for geometry g (conv_bf16.hip dispatches here when enabled):
 // returns the position tile (> 0, the statistics' tile height), or VT_ERR_ARG when the
 // window's source rows do not fit in LDS (the caller uses k_conv_bf16)
-int cfw16_launch(const float* x, const Geo& g, const __bf16* w16, float* y, int Lo, float* stats, hipStream_t st,
+int cfw16_launch(const float* x, const Geo& g, const void* w16, float* y, int Lo, float* stats, hipStream_t st,
                  const BnIn* ibn) {
     switch (g.K) {
         case 1: return cfw_k<1>(x, g, w16, y, Lo, stats, st, ibn);

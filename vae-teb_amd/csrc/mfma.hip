@@ -20,12 +20,9 @@
 // (W for the forward, W^T for the input gradient) refreshed by
 // vt_mfma_weight_shadow; the activation side (X, dY, X^T, dY^T) is converted by
 // small prep kernels into zero-padded images, so the main loop has no predicates.
-#include "common.h"
+#include "h16.h"
 
 namespace vt {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int QM = 256, QN = 64, QK = 64, QT = 512;
 constexpr int ROWB = QK * 2;                      // 128 B per operand row in LDS
@@ -40,7 +37,7 @@ constexpr int GEMM_LDS = NA * A_BYTES + NB * B_BYTES;   // 160 KB
 // 16-B chunk position of chunk c in LDS row r (involution)
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
-__device__ __forceinline__ void glds16(const __bf16* src, char* lds) {
+__device__ __forceinline__ void glds16(const void* src, char* lds) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
@@ -74,8 +71,9 @@ __device__ __forceinline__ bool last_arrival_in(unsigned* ctr, unsigned total, u
 // grid (N/64, Mpad/256, splits); K = reduction length of ONE split (multiple of 64).  splits > 1:
 // part holds tiles x splits slabs of 512 x 32 floats (a thread's 32 accumulators as 8 float4,
 // wave-contiguous), slot0 the tiles' arrival counters
-__global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, int64_t lda,
-                                                  const __bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
+template <typename H>
+__global__ __launch_bounds__(QT) void k_mfma_gemm(const H* __restrict__ A, int64_t lda,
+                                                  const H* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                   float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
                                                   int accumulate, float* __restrict__ part, unsigned slot0) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -117,22 +115,22 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // k 0..31, 32..63: chunks 4h + lc
             const int c = 4 * h + lc;
-            bf16x8 af[2], bfr[4];
+            hv8<H> af[2], bfr[4];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int r = 32 * w + 16 * i + lr;
-                af[i] = *(const bf16x8*)(ta + r * ROWB + 16 * swz(r, c));
+                af[i] = *(const hv8<H>*)(ta + r * ROWB + 16 * swz(r, c));
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int r = 16 * j + lr;
-                bfr[j] = *(const bf16x8*)(tb + r * ROWB + 16 * swz(r, c));
+                bfr[j] = *(const hv8<H>*)(tb + r * ROWB + 16 * swz(r, c));
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
         }
     };
 
@@ -190,20 +188,22 @@ __global__ __launch_bounds__(QT) void k_mfma_gemm(const __bf16* __restrict__ A, 
         }
 }
 
-// out[m][k] = bf16(X[m][k]) for m < M, k < K; zero in the padding (Mpad x Kpad)
-__global__ void k_bf16_rows(const float* __restrict__ X, int64_t M, int K, __bf16* __restrict__ out, int64_t Mpad,
+// out[m][k] = H(X[m][k]) for m < M, k < K; zero in the padding (Mpad x Kpad)
+template <typename H>
+__global__ void k_bf16_rows(const float* __restrict__ X, int64_t M, int K, H* __restrict__ out, int64_t Mpad,
                             int Kpad) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = Mpad * Kpad;
     if (i >= total) return;
     const int64_t m = i / Kpad;
     const int k = (int)(i - m * Kpad);
-    out[i] = (m < M && k < K) ? (__bf16)X[m * K + k] : (__bf16)0.f;
+    out[i] = (m < M && k < K) ? (H)X[m * K + k] : (H)0.f;
 }
 
-// out[c][r] = bf16(X[r][c]) (X is R x Cn row-major); zero padded to Cpad x Rpad
+// out[c][r] = H(X[r][c]) (X is R x Cn row-major); zero padded to Cpad x Rpad
+template <typename H>
 __global__ __launch_bounds__(256) void k_bf16_transpose(const float* __restrict__ X, int64_t R, int Cn,
-                                                        __bf16* __restrict__ out, int64_t Cpad, int64_t Rpad) {
+                                                        H* __restrict__ out, int64_t Cpad, int64_t Rpad) {
     __shared__ float tile[64][65];
     const int64_t r0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -214,23 +214,24 @@ __global__ __launch_bounds__(256) void k_bf16_transpose(const float* __restrict_
     __syncthreads();
     for (int i = ty; i < 64; i += 4) {
         const int64_t c = c0 + i, r = r0 + tx;
-        if (c < Cpad && r < Rpad) out[c * Rpad + r] = (__bf16)tile[tx][i];
+        if (c < Cpad && r < Rpad) out[c * Rpad + r] = (H)tile[tx][i];
     }
 }
 
-// W fp32 [N][K] -> W16 = bf16(W) [N][K] and W16t = bf16(W)^T [K][N]  (N, K multiples of 64)
+// W fp32 [N][K] -> W16 = H(W) [N][K] and W16t = H(W)^T [K][N]  (N, K multiples of 64)
+template <typename H>
 __global__ __launch_bounds__(256) void k_bf16_shadow(const float* __restrict__ W, int N, int K,
-                                                     __bf16* __restrict__ W16, __bf16* __restrict__ W16t) {
+                                                     H* __restrict__ W16, H* __restrict__ W16t) {
     __shared__ float tile[64][65];
     const int64_t n0 = (int64_t)blockIdx.y * 64, k0 = (int64_t)blockIdx.x * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int i = ty; i < 64; i += 4) {
         const float v = W[(n0 + i) * K + k0 + tx];
         tile[i][tx] = v;
-        W16[(n0 + i) * K + k0 + tx] = (__bf16)v;
+        W16[(n0 + i) * K + k0 + tx] = (H)v;
     }
     __syncthreads();
-    for (int i = ty; i < 64; i += 4) W16t[(k0 + i) * N + n0 + tx] = (__bf16)tile[tx][i];
+    for (int i = ty; i < 64; i += 4) W16t[(k0 + i) * N + n0 + tx] = (H)tile[tx][i];
 }
 
 // ------------------------------------------------------------ weight gradient
@@ -253,20 +254,22 @@ __device__ __forceinline__ int dw_pos(int r, int c) { return r * DWS + (r >> 3) 
 
 // 16 x 32 fragment (16 columns col0.., 32 rows row0..) of a [r][col] image, r the reduction:
 // lane 4q + p of 16-lane group g reads rows row0 + 8g + q (+4), columns col0 + 4p .. +3
-__device__ __forceinline__ bf16x8 dw_frag(const __bf16* img, int row0, int col0) {
+template <typename H>
+__device__ __forceinline__ hv8<H> dw_frag(const H* img, int row0, int col0) {
     const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const __bf16* a0 = img + dw_pos(row0 + 8 * g + q, col0 + 4 * p);
-    const __bf16* a1 = img + dw_pos(row0 + 8 * g + q + 4, col0 + 4 * p);
+    const H* a0 = img + dw_pos(row0 + 8 * g + q, col0 + 4 * p);
+    const H* a1 = img + dw_pos(row0 + 8 * g + q + 4, col0 + 4 * p);
     const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
     const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a1);
     const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(hv8<H>, r);
 }
 
+template <typename H>
 __global__ __launch_bounds__(256) void k_mfma_dw(const float* __restrict__ dY, int64_t R, int N,
                                                  const float* __restrict__ X, int K, float* __restrict__ dW,
                                                  int accumulate) {
-    __shared__ __attribute__((aligned(16))) __bf16 img[2][DWIMG];  // [0] dY chunk, [1] X chunk
+    __shared__ __attribute__((aligned(16))) H img[2][DWIMG];  // [0] dY chunk, [1] X chunk
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
     const int n0 = blockIdx.y * DWT, k0 = blockIdx.x * DWT;
     // staging: chunk rows r0 .. r0 + 63, 32 float4 per row per operand; thread -> (row, quad) pairs
@@ -286,9 +289,8 @@ __global__ __launch_bounds__(256) void k_mfma_dw(const float* __restrict__ dY, i
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int e = tid + 256 * i, row = e >> 5, q4 = e & 31;
-                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-                const bf16x4 v = {(__bf16)pf[o][i].x, (__bf16)pf[o][i].y, (__bf16)pf[o][i].z, (__bf16)pf[o][i].w};
-                *(bf16x4*)(img[o] + dw_pos(row, 4 * q4)) = v;
+                const hv4<H> v = {(H)pf[o][i].x, (H)pf[o][i].y, (H)pf[o][i].z, (H)pf[o][i].w};
+                *(hv4<H>*)(img[o] + dw_pos(row, 4 * q4)) = v;
             }
     };
     f32x4 acc[4][4];
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(256) void k_mfma_dw(const float* __restrict__ dY, i
         if (r0 + DWC < R) load(r0 + DWC);
 #pragma unroll
         for (int s = 0; s < DWC / 32; ++s) {
-            bf16x8 a[4], b[4];
+            hv8<H> a[4], b[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) a[i] = dw_frag(img[0], 32 * s, 64 * wm + 16 * i);
 #pragma unroll
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(256) void k_mfma_dw(const float* __restrict__ dY, i
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
         }
         __syncthreads();
     }
@@ -368,11 +370,12 @@ static MfmaPlan plan(int64_t M, int N, int64_t K) {
     return p;
 }
 
-static int run(const char* who, const __bf16* A, const __bf16* B, int64_t ldb, int64_t M, int N, const MfmaPlan& p,
+template <typename H>
+static int run(const char* who, const H* A, const H* B, int64_t ldb, int64_t M, int N, const MfmaPlan& p,
                float* C, const float* bias, int accumulate, float* part, hipStream_t st) {
     static bool attr = false;
     if (!attr) {   // 160 KB of dynamic LDS (above the 64 KB default cap)
-        if (hipFuncSetAttribute((const void*)k_mfma_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, GEMM_LDS) !=
+        if (hipFuncSetAttribute((const void*)k_mfma_gemm<H>, hipFuncAttributeMaxDynamicSharedMemorySize, GEMM_LDS) !=
             hipSuccess) {
             set_error("%s: cannot allow %d B of LDS for k_mfma_gemm", who, GEMM_LDS);
             return VT_ERR_HIP;
@@ -382,7 +385,7 @@ static int run(const char* who, const __bf16* A, const __bf16* B, int64_t ldb, i
     const int kper = (int)(p.Kpad / p.splits);
     dim3 grid(N / QN, (unsigned)(p.Mpad / QM), p.splits);
     const unsigned tiles = grid.x * grid.y;
-    hipLaunchKernelGGL(k_mfma_gemm, grid, dim3(QT), GEMM_LDS, st, A, p.Kpad, B, ldb, (int)M, N, kper, C, (int64_t)N,
+    hipLaunchKernelGGL(k_mfma_gemm<H>, grid, dim3(QT), GEMM_LDS, st, A, p.Kpad, B, ldb, (int)M, N, kper, C, (int64_t)N,
                        bias, accumulate, p.splits > 1 ? part : nullptr, p.splits > 1 ? arrive_slots(tiles, st) : 0u);
     VT_LAUNCH_CHECK(who);
     return VT_OK;
@@ -409,8 +412,8 @@ int vt_mfma_workspace_floats(int64_t R, int K, int N, int64_t* floats) {
 
 int vt_mfma_weight_shadow(const float* W, int N, int K, void* W16, void* W16t, void* stream) {
     VT_CHECK_ARG(vt_mfma_supported(K, N) && W && W16 && W16t, "vt_mfma_weight_shadow: K and N must be multiples of 64");
-    hipLaunchKernelGGL(k_bf16_shadow, dim3(K / 64, N / 64), dim3(256), 0, S(stream), W, N, K, (__bf16*)W16,
-                       (__bf16*)W16t);
+    VT_H16(hipLaunchKernelGGL(k_bf16_shadow<H>, dim3(K / 64, N / 64), dim3(256), 0, S(stream), W, N, K, (H*)W16,
+                              (H*)W16t));
     VT_LAUNCH_CHECK("vt_mfma_weight_shadow");
     return VT_OK;
 }
@@ -421,11 +424,14 @@ int vt_mfma_linear_fwd(const float* X, int64_t R, int K, const void* W16, int N,
     VT_CHECK_ARG(R > 0 && vt_mfma_supported(K, N), "vt_mfma_linear_fwd: K and N must be positive multiples of 64");
     MfmaPlan p = plan(R, N, K);
     VT_CHECK_ARG(p.a_floats + p.part_floats <= ws_floats, "vt_mfma_linear_fwd: workspace too small");
-    __bf16* A = (__bf16*)ws;
     const int64_t tot = p.Mpad * p.Kpad;
-    hipLaunchKernelGGL(k_bf16_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, S(stream), X, R, K, A, p.Mpad,
-                       (int)p.Kpad);
-    return run("vt_mfma_linear_fwd", A, (const __bf16*)W16, K, R, N, p, Y, bias, 0, ws + p.a_floats, S(stream));
+    int rc = VT_OK;
+    VT_H16(H* A = (H*)ws;
+           hipLaunchKernelGGL(k_bf16_rows<H>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, S(stream), X, R, K, A,
+                              p.Mpad, (int)p.Kpad);
+           rc = run("vt_mfma_linear_fwd", (const H*)A, (const H*)W16, K, R, N, p, Y, bias, 0, ws + p.a_floats,
+                    S(stream)));
+    return rc;
 }
 
 // dX[R,K] (+)= dY[R,N] W[N,K]      (W16t = bf16 shadow of W^T, [K][N])
@@ -434,12 +440,14 @@ int vt_mfma_linear_bwd_data(const float* dY, int64_t R, int N, const void* W16t,
     VT_CHECK_ARG(R > 0 && vt_mfma_supported(N, K), "vt_mfma_linear_bwd_data: K and N must be positive multiples of 64");
     MfmaPlan p = plan(R, K, N);  // C = dX (M=R, cols=K), reduction over N
     VT_CHECK_ARG(p.a_floats + p.part_floats <= ws_floats, "vt_mfma_linear_bwd_data: workspace too small");
-    __bf16* A = (__bf16*)ws;
     const int64_t tot = p.Mpad * p.Kpad;
-    hipLaunchKernelGGL(k_bf16_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, S(stream), dY, R, N, A,
-                       p.Mpad, (int)p.Kpad);
-    return run("vt_mfma_linear_bwd_data", A, (const __bf16*)W16t, N, R, K, p, dX, nullptr, accumulate,
-               ws + p.a_floats, S(stream));
+    int rc = VT_OK;
+    VT_H16(H* A = (H*)ws;
+           hipLaunchKernelGGL(k_bf16_rows<H>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, S(stream), dY, R, N, A,
+                              p.Mpad, (int)p.Kpad);
+           rc = run("vt_mfma_linear_bwd_data", (const H*)A, (const H*)W16t, N, R, K, p, dX, nullptr, accumulate,
+                    ws + p.a_floats, S(stream)));
+    return rc;
 }
 
 // dW[N,K] (+)= dY[R,N]^T X[R,K];  db (+)= column sums of dY (if db != NULL)
@@ -448,22 +456,24 @@ int vt_mfma_linear_bwd_weight(const float* dY, int64_t R, int N, const float* X,
     VT_CHECK_ARG(R > 0 && vt_mfma_supported(K, N), "vt_mfma_linear_bwd_weight: K and N must be positive multiples of 64");
     if (N % DWT == 0 && K % DWT == 0) {
         // direct: fp32 operands staged and transposed in LDS, no split (k_mfma_dw)
-        hipLaunchKernelGGL(k_mfma_dw, dim3(K / DWT, N / DWT), dim3(256), 0, S(stream), dY, R, N, X, K, dW,
-                           accumulate);
+        VT_H16(hipLaunchKernelGGL(k_mfma_dw<H>, dim3(K / DWT, N / DWT), dim3(256), 0, S(stream), dY, R, N, X, K, dW,
+                                  accumulate));
         VT_LAUNCH_CHECK("vt_mfma_linear_bwd_weight");
         return db ? vt_colsum(dY, R, N, db, accumulate, ws, ws_floats, stream) : VT_OK;
     }
     MfmaPlan p = plan(N, K, R);  // C = dW (M=N, cols=K), reduction over R
     const int64_t b_floats = up_to((int64_t)K * p.Kpad / 2, 64);
     VT_CHECK_ARG(p.a_floats + b_floats + p.part_floats + N <= ws_floats, "vt_mfma_linear_bwd_weight: workspace too small");
-    __bf16* A = (__bf16*)ws;                   // dY^T  [Npad][Rpad]
-    __bf16* Bt = (__bf16*)(ws + p.a_floats);   // X^T   [K][Rpad]
     float* part = ws + p.a_floats + b_floats;
-    hipLaunchKernelGGL(k_bf16_transpose, dim3((unsigned)(p.Kpad / 64), (unsigned)(p.Mpad / 64)), dim3(256), 0,
-                       S(stream), dY, R, N, A, p.Mpad, p.Kpad);
-    hipLaunchKernelGGL(k_bf16_transpose, dim3((unsigned)(p.Kpad / 64), (unsigned)(K / 64)), dim3(256), 0, S(stream), X,
-                       R, K, Bt, (int64_t)K, p.Kpad);
-    int rc = run("vt_mfma_linear_bwd_weight", A, Bt, p.Kpad, N, K, p, dW, nullptr, accumulate, part, S(stream));
+    int rc = VT_OK;
+    VT_H16(H* A = (H*)ws;                   // dY^T  [Npad][Rpad]
+           H* Bt = (H*)(ws + p.a_floats);   // X^T   [K][Rpad]
+           hipLaunchKernelGGL(k_bf16_transpose<H>, dim3((unsigned)(p.Kpad / 64), (unsigned)(p.Mpad / 64)), dim3(256), 0,
+                              S(stream), dY, R, N, A, p.Mpad, p.Kpad);
+           hipLaunchKernelGGL(k_bf16_transpose<H>, dim3((unsigned)(p.Kpad / 64), (unsigned)(K / 64)), dim3(256), 0,
+                              S(stream), X, R, K, Bt, (int64_t)K, p.Kpad);
+           rc = run("vt_mfma_linear_bwd_weight", (const H*)A, (const H*)Bt, p.Kpad, N, K, p, dW, nullptr, accumulate,
+                    part, S(stream)));
     if (rc || !db) return rc;
     return vt_colsum(dY, R, N, db, accumulate, part, ws_floats - p.a_floats - b_floats, stream);
 }

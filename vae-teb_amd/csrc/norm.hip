@@ -759,7 +759,7 @@ __global__ __launch_bounds__(NT) void k_bn_dx4(const float* __restrict__ dy, con
 // r0 a multiple of 4: thread tid < T' reads the float4s at flat offsets
 // r0*C + 4 tid + 4T' k, 4T' a multiple of C, so its four channels never change;
 // the per-thread sums are combined in LDS in fixed order.
-template <int KIND, int ACT, bool DROP = false>
+template <int KIND, int ACT, bool DROP = false, int U = 4>
 __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x, const float* __restrict__ dy,
                                                      int64_t M, int C, int64_t rows_per_block, int Tp,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -835,25 +835,26 @@ __global__ __launch_bounds__(NT) void k_col_partial4(const float* __restrict__ x
             if constexpr (PIN) acc4(e, v, g);
             else acc(e, v, g);
         };
+        // U float4 of each stream in flight per thread (the same f sequence for any U: the same sums)
         int64_t f = r0 * C + 4 * tid;
         if constexpr (PIN) {
-            for (; f + 12 * (int64_t)Tp + 4 <= end; f += 16 * (int64_t)Tp) {
-                float4 xv[4], gv[4];
+            for (; f + 4 * (U - 1) * (int64_t)Tp + 4 <= end; f += 4 * U * (int64_t)Tp) {
+                float4 xv[U], gv[U];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < U; ++u) {
                     xv[u] = *(const float4*)(x + f + 4 * (int64_t)Tp * u);
                     gv[u] = KIND == 2 ? *(const float4*)(dy + f + 4 * (int64_t)Tp * u) : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
                 if constexpr (DROP) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
+                    for (int u = 0; u < U; ++u) {
                         const int64_t i0 = f + 4 * (int64_t)Tp * u;
                         gv[u] = make_float4(gm(i0, ce[0], gv[u].x), gm(i0 + 1, ce[1], gv[u].y),
                                             gm(i0 + 2, ce[2], gv[u].z), gm(i0 + 3, ce[3], gv[u].w));
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < U; ++u) {
                     acc4(0, xv[u].x, gv[u].x);
                     acc4(1, xv[u].y, gv[u].y);
                     acc4(2, xv[u].z, gv[u].z);
@@ -958,10 +959,21 @@ static void bn_dx_vec(const float* dy, const float* x, int64_t M, int C, const f
 #undef VT_F
 }
 
+// float4 of each stream in flight per thread of k_col_partial4 (VAETEB_COLP_U: 4 or 8; same bits)
+static int g_colp_u = getenv("VAETEB_COLP_U") ? atoi(getenv("VAETEB_COLP_U")) : 4;
+
 static void col_partial_vec(int kind, const float* x, const float* dy, int64_t M, int C, int64_t rpb, int blocks,
                             const float* mean, const float* rstd, const float* gamma, const float* beta, int act,
                             float* part, hipStream_t st, BnFin fin, const DropArg* dr = nullptr) {
     const int Tp = colp_threads(C);
+    if (kind == 2 && !dr && g_colp_u == 8) {
+#define VT_F(A)                                                                                                    \
+        hipLaunchKernelGGL((k_col_partial4<2, A, false, 8>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp,   \
+                           mean, rstd, gamma, beta, part, fin, DropArg{})
+        VT_ACT_SWITCH(act, VT_F)
+#undef VT_F
+        return;
+    }
     if (kind == 0) {
         hipLaunchKernelGGL((k_col_partial4<0, ACT_NONE>), dim3(blocks), dim3(NT), 0, st, x, dy, M, C, rpb, Tp, mean,
                            rstd, gamma, beta, part, fin, DropArg{});

@@ -8,10 +8,13 @@
 //                       gradient_clip_val=0.5, ref/model/graph_model.py:511)
 //   AdamW            : torch.optim.AdamW single-tensor update order, with the
 //                      hyper-parameters of ref/model/graph_model.py:654-660.
+//   dynamic loss scale (fp16 operands, round 6): torch.amp.GradScaler's unscale_ + inf check
+//                      + step skip + update (ref/model/graph_model.py:670,718-726), on device
+//                      state, no host sync (vt_grad_norm_clip_scaled, vt_adamw_step_dev*_skip).
 #include <math.h>
 #include <stdlib.h>
 
-#include "common.h"
+#include "h16.h"
 
 namespace vt {
 
@@ -71,6 +74,61 @@ __global__ void k_norm_finalize(const double* __restrict__ partial, int count, f
     }
 }
 
+// GradScaler over the flat gradient buffer, which holds scale * (the gradients): the backward
+// ran on loss * scale.  sc = {scale, growth tracker, found_inf of this step, skipped steps}.
+//   found_inf = the squared norm is not finite (an inf / NaN anywhere in the buffer: its sum of
+//               squares is then inf / NaN — GradScaler's _amp_foreach_non_finite_check_and_unscale_);
+//   out[0]   = the pre-clip norm of the UNSCALED gradients, pre_scale * ||g|| / scale (inf if found);
+//   out[1]   = the factor AdamW applies to the raw buffer: pre_scale * clip_coef / scale (0 if found);
+//   out[2]   = found_inf (AdamW and its step counter skip the step: GradScaler.step);
+// then the scale update of GradScaler.update (torch's _amp_update_scale_): found -> scale *=
+// backoff, tracker = 0; else tracker + 1 == interval -> scale *= growth, tracker = 0.  The norm
+// and coefficient use the OLD scale (the one the backward ran with).
+__global__ void k_norm_finalize_scaled(const double* __restrict__ partial, int count, float pre_scale, float max_norm,
+                                       float* __restrict__ out, float* __restrict__ sc, float growth, float backoff,
+                                       int interval) {
+    __shared__ double red[256];
+    double a = 0.0;
+    for (int i = threadIdx.x; i < count; i += blockDim.x) a += partial[i];
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float scale = sc[0];
+        const float inv = (float)(1.0 / (double)scale);   // GradScaler: scale.double().reciprocal().float()
+        const bool found = !isfinite(red[0]);
+        if (found) {
+            out[0] = INFINITY;
+            out[1] = 0.f;
+            out[2] = 1.f;
+            sc[0] = scale * backoff;
+            sc[1] = 0.f;
+            sc[3] += 1.f;
+        } else {
+            const float norm = (float)sqrt(red[0]) * inv * pre_scale;
+            float coef = 1.0f;
+            if (max_norm > 0.f) {
+                coef = max_norm / (norm + 1e-6f);
+                coef = coef > 1.0f ? 1.0f : coef;
+            }
+            out[0] = norm;
+            out[1] = pre_scale * inv * coef;
+            out[2] = 0.f;
+            const float t = sc[1] + 1.f;
+            if (t >= (float)interval) {
+                sc[0] = scale * growth;
+                sc[1] = 0.f;
+            } else {
+                sc[1] = t;
+            }
+        }
+        sc[2] = out[2];
+    }
+}
+
 // One element of the torch.optim.AdamW single-tensor update, shared by the
 // scalar and the float4 kernels.  Contraction is off (every multiply and add
 // rounded, as torch's separate lerp_ / mul_ / addcmul_ / addcdiv_ ops), so the
@@ -114,7 +172,9 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw(float* __restrict__ p, co
                                                        float lr, float beta1, float beta2, float eps, float wd,
                                                        float step_size, float bc2_sqrt,
                                                        const float* __restrict__ gscale,
-                                                       const float* __restrict__ coef) {
+                                                       const float* __restrict__ coef,
+                                                       const float* __restrict__ skip) {
+    if (skip && skip[0] != 0.f) return;   // GradScaler.step: an overflowing step is skipped
     const AdamwK k = adamw_consts(lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         adamw_elem(k, p[i], g[i], m[i], v[i]);
@@ -147,7 +207,9 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw4(float* __restrict__ p, c
                                                         float lr, float beta1, float beta2, float eps, float wd,
                                                         float step_size, float bc2_sqrt,
                                                         const float* __restrict__ gscale,
-                                                        const float* __restrict__ coef, AdamwSkip sk) {
+                                                        const float* __restrict__ coef, AdamwSkip sk,
+                                                        const float* __restrict__ skip) {
+    if (skip && skip[0] != 0.f) return;
     const AdamwK k = adamw_consts(lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
     float4* p4 = reinterpret_cast<float4*>(p);
     const float4* g4 = reinterpret_cast<const float4*>(g);
@@ -207,8 +269,9 @@ __global__ __launch_bounds__(OPT_THREADS) void k_adamw4(float* __restrict__ p, c
 }
 
 // AdamW over 2-D weights W [N][K] (N, K multiples of 64; each 64-float aligned in the flat
-// buffers) as 64 x 64 tiles, writing the bf16 shadows the MFMA GEMMs read — W16 [N][K] and the
-// transposed W16t [K][N] (round to nearest even, as k_bf16_shadow) — from the updated values:
+// buffers) as 64 x 64 tiles, writing the 16-bit shadows the MFMA GEMMs read (H: bf16 or fp16,
+// h16.h) — W16 [N][K] and the transposed W16t [K][N] (round to nearest even, as k_bf16_shadow)
+// — from the updated values:
 // the forward then needs no shadow pass.  The same element function as the flat kernels (the
 // same bits); gradient reads and fp32 write-backs non-temporal, the shadows cached (read by the
 // next forward).  Up to 4 weights per launch, workgroup b -> (weight, tile) by prefix sums.
@@ -217,14 +280,17 @@ struct TileHeads {
     int64_t off[4];
     int N[4], K[4];
     int prefix[5];
-    __bf16* w16[4];
-    __bf16* w16t[4];
+    void* w16[4];
+    void* w16t[4];
 };
+template <typename H>
 __global__ __launch_bounds__(256) void k_adamw_tile16(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v, float lr,
                                                       float beta1, float beta2, float eps, float wd, float step_size,
                                                       float bc2_sqrt, const float* __restrict__ gscale,
-                                                      const float* __restrict__ coef, TileHeads th) {
+                                                      const float* __restrict__ coef, TileHeads th,
+                                                      const float* __restrict__ skip) {
+    if (skip && skip[0] != 0.f) return;
     __shared__ float tile[64][65];
     const AdamwK k = adamw_consts(lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
     int h = 0;
@@ -243,7 +309,8 @@ __global__ __launch_bounds__(256) void k_adamw_tile16(float* __restrict__ p, con
         ma[j] = *reinterpret_cast<const float4*>(m + e);
         va[j] = *reinterpret_cast<const float4*>(v + e);
     }
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    H* const w16 = reinterpret_cast<H*>(th.w16[h]);
+    H* const w16t = reinterpret_cast<H*>(th.w16t[h]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         adamw_elem(k, pa[j].x, ga[j].x, ma[j].x, va[j].x);
@@ -255,8 +322,8 @@ __global__ __launch_bounds__(256) void k_adamw_tile16(float* __restrict__ p, con
         __builtin_nontemporal_store(f32x4n{pa[j].x, pa[j].y, pa[j].z, pa[j].w}, reinterpret_cast<f32x4n*>(p + e));
         __builtin_nontemporal_store(f32x4n{ma[j].x, ma[j].y, ma[j].z, ma[j].w}, reinterpret_cast<f32x4n*>(m + e));
         __builtin_nontemporal_store(f32x4n{va[j].x, va[j].y, va[j].z, va[j].w}, reinterpret_cast<f32x4n*>(v + e));
-        *reinterpret_cast<bf16x4*>(th.w16[h] + (n0 + r) * K + k0 + 4 * tx) =
-            bf16x4{(__bf16)pa[j].x, (__bf16)pa[j].y, (__bf16)pa[j].z, (__bf16)pa[j].w};
+        *reinterpret_cast<hv4<H>*>(w16 + (n0 + r) * K + k0 + 4 * tx) =
+            hv4<H>{(H)pa[j].x, (H)pa[j].y, (H)pa[j].z, (H)pa[j].w};
         tile[r][4 * tx] = pa[j].x;
         tile[r][4 * tx + 1] = pa[j].y;
         tile[r][4 * tx + 2] = pa[j].z;
@@ -267,16 +334,17 @@ __global__ __launch_bounds__(256) void k_adamw_tile16(float* __restrict__ p, con
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int i = ty + 16 * j;
-        *reinterpret_cast<bf16x4*>(th.w16t[h] + (k0 + i) * N + n0 + 4 * tx) =
-            bf16x4{(__bf16)tile[4 * tx][i], (__bf16)tile[4 * tx + 1][i], (__bf16)tile[4 * tx + 2][i],
-                   (__bf16)tile[4 * tx + 3][i]};
+        *reinterpret_cast<hv4<H>*>(w16t + (k0 + i) * N + n0 + 4 * tx) =
+            hv4<H>{(H)tile[4 * tx][i], (H)tile[4 * tx + 1][i], (H)tile[4 * tx + 2][i], (H)tile[4 * tx + 3][i]};
     }
 }
 
 static inline bool aligned16(const void* a) { return ((uintptr_t)a & 15u) == 0; }
 
-// step += 1; coef = {lr / (1 - b1^step), sqrt(1 - b2^step)} in fp64 (as the host path)
-__global__ void k_adamw_coef(int* step, float lr, float beta1, float beta2, float* coef) {
+// step += 1; coef = {lr / (1 - b1^step), sqrt(1 - b2^step)} in fp64 (as the host path); a skipped
+// step (GradScaler) leaves the step counter as it is, as torch's optimizer.step never ran
+__global__ void k_adamw_coef(int* step, float lr, float beta1, float beta2, float* coef, const float* skip) {
+    if (skip && skip[0] != 0.f) return;
     const int s = step[0] + 1;
     step[0] = s;
     const double bc1 = 1.0 - pow((double)beta1, (double)s);
@@ -307,7 +375,7 @@ static int g_adamw_vec = -1;  // -1: from VAETEB_ADAMW_SCALAR (unset: vector ker
 
 static void adamw_launch(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                          float eps, float wd, float step_size, float bc2_sqrt, const float* gscale, const float* coef,
-                         hipStream_t st, const AdamwSkip* skip = nullptr) {
+                         hipStream_t st, const AdamwSkip* skip = nullptr, const float* skipf = nullptr) {
     AdamwSkip sk{};
     if (skip) sk = *skip;
     int64_t skipped4 = 0;
@@ -326,7 +394,7 @@ static void adamw_launch(float* p, const float* g, float* m, float* v, int64_t n
         const dim3 grid(grid_for((n / 4 - skipped4 + 1) / (U == 4 ? 4 : 2), cap > 0 ? cap : 2048));
 #define VT_ADAMW4(UU, NN)                                                                                          \
     hipLaunchKernelGGL((k_adamw4<UU, NN>), grid, dim3(OPT_THREADS), 0, st, p, g, m, v, n, lr, beta1, beta2, eps, wd, \
-                       step_size, bc2_sqrt, gscale, coef, sk)
+                       step_size, bc2_sqrt, gscale, coef, sk, skipf)
         if (U == 4) {
             if (nt) VT_ADAMW4(4, true); else VT_ADAMW4(4, false);
         } else {
@@ -335,7 +403,7 @@ static void adamw_launch(float* p, const float* g, float* m, float* v, int64_t n
 #undef VT_ADAMW4
     } else {
         hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 8192)), dim3(OPT_THREADS), 0, st, p, g, m, v, n, lr, beta1,
-                           beta2, eps, wd, step_size, bc2_sqrt, gscale, coef);
+                           beta2, eps, wd, step_size, bc2_sqrt, gscale, coef, skipf);
     }
 }
 
@@ -358,30 +426,53 @@ int vt_grad_norm_clip(const float* g, int64_t n, float pre_scale, float max_norm
     return VT_OK;
 }
 
+int vt_grad_norm_clip_scaled(const float* g, int64_t n, float pre_scale, float max_norm, float* out3, float* ws,
+                             float* scaler, float growth_factor, float backoff_factor, int growth_interval,
+                             void* stream) {
+    VT_CHECK_ARG(n > 0 && out3 && scaler && growth_interval > 0 && growth_factor >= 1.f && backoff_factor > 0.f &&
+                     backoff_factor <= 1.f,
+                 "vt_grad_norm_clip_scaled: args");
+    const int blocks = grid_for(n / 4 + 1, NORM_BLOCKS);
+    double* wd = reinterpret_cast<double*>(ws);
+    hipLaunchKernelGGL(k_sumsq, dim3(blocks), dim3(OPT_THREADS), 0, S(stream), g, n, wd);
+    hipLaunchKernelGGL(k_norm_finalize_scaled, dim3(1), dim3(256), 0, S(stream), wd, blocks, pre_scale, max_norm, out3,
+                       scaler, growth_factor, backoff_factor, growth_interval);
+    VT_LAUNCH_CHECK("vt_grad_norm_clip_scaled");
+    return VT_OK;
+}
+
 int vt_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                   float eps, float weight_decay, int step, const float* gscale, void* stream) {
     VT_CHECK_ARG(n > 0 && step >= 1, "vt_adamw_step: n=%lld step=%d", (long long)n, step);
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
     adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, (float)((double)lr / bc1), (float)sqrt(bc2),
-                 gscale, nullptr, S(stream));
+                 gscale, nullptr, S(stream), nullptr, nullptr);
     VT_LAUNCH_CHECK("vt_adamw_step");
+    return VT_OK;
+}
+
+int vt_adamw_step_dev_skip(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                           float beta2, float eps, float weight_decay, int* step, float* coef, const float* gscale,
+                           const float* skip, void* stream) {
+    VT_CHECK_ARG(n > 0 && step && coef, "vt_adamw_step_dev: args");
+    hipLaunchKernelGGL(k_adamw_coef, dim3(1), dim3(1), 0, S(stream), step, lr, beta1, beta2, coef, skip);
+    adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, S(stream), nullptr, skip);
+    VT_LAUNCH_CHECK("vt_adamw_step_dev");
     return VT_OK;
 }
 
 int vt_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                       float eps, float weight_decay, int* step, float* coef, const float* gscale, void* stream) {
-    VT_CHECK_ARG(n > 0 && step && coef, "vt_adamw_step_dev: args");
-    hipLaunchKernelGGL(k_adamw_coef, dim3(1), dim3(1), 0, S(stream), step, lr, beta1, beta2, coef);
-    adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, S(stream));
-    VT_LAUNCH_CHECK("vt_adamw_step_dev");
-    return VT_OK;
+    return vt_adamw_step_dev_skip(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, coef, gscale, nullptr,
+                                  stream);
 }
 
-int vt_adamw_step_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
-                             float beta2, float eps, float weight_decay, int* step, float* coef, const float* gscale,
-                             int n_tiled, const int64_t* tiled_off, const int* tiled_N, const int* tiled_K,
-                             const int64_t* tiled_w16, const int64_t* tiled_w16t, void* stream) {
+int vt_adamw_step_dev_shadow_skip(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                                  float beta2, float eps, float weight_decay, int* step, float* coef,
+                                  const float* gscale, int n_tiled, const int64_t* tiled_off, const int* tiled_N,
+                                  const int* tiled_K, const int64_t* tiled_w16, const int64_t* tiled_w16t,
+                                  const float* skip, void* stream) {
     VT_CHECK_ARG(n > 0 && step && coef && n_tiled >= 0 && n_tiled <= 4, "vt_adamw_step_dev_shadow: args (<= 4 tiled)");
     VT_CHECK_ARG(aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v),
                  "vt_adamw_step_dev_shadow: buffers must be 16-byte aligned");
@@ -404,18 +495,26 @@ int vt_adamw_step_dev_shadow(float* p, const float* g, float* m, float* v, int64
         th.N[h] = N;
         th.K[h] = K;
         th.prefix[h + 1] = th.prefix[h] + (N / 64) * (K / 64);
-        th.w16[h] = reinterpret_cast<__bf16*>(tiled_w16[h]);
-        th.w16t[h] = reinterpret_cast<__bf16*>(tiled_w16t[h]);
+        th.w16[h] = reinterpret_cast<void*>(tiled_w16[h]);
+        th.w16t[h] = reinterpret_cast<void*>(tiled_w16t[h]);
     }
     sk.n = n_tiled;
     hipStream_t st = S(stream);
-    hipLaunchKernelGGL(k_adamw_coef, dim3(1), dim3(1), 0, st, step, lr, beta1, beta2, coef);
+    hipLaunchKernelGGL(k_adamw_coef, dim3(1), dim3(1), 0, st, step, lr, beta1, beta2, coef, skip);
     if (n_tiled > 0)
-        hipLaunchKernelGGL(k_adamw_tile16, dim3((unsigned)th.prefix[n_tiled]), dim3(256), 0, st, p, g, m, v, lr, beta1,
-                           beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, th);
-    adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, st, &sk);
+        VT_H16(hipLaunchKernelGGL(k_adamw_tile16<H>, dim3((unsigned)th.prefix[n_tiled]), dim3(256), 0, st, p, g, m, v, lr,
+                                  beta1, beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, th, skip));
+    adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, 0.f, 1.f, gscale, coef, st, &sk, skip);
     VT_LAUNCH_CHECK("vt_adamw_step_dev_shadow");
     return VT_OK;
+}
+
+int vt_adamw_step_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                             float beta2, float eps, float weight_decay, int* step, float* coef, const float* gscale,
+                             int n_tiled, const int64_t* tiled_off, const int* tiled_N, const int* tiled_K,
+                             const int64_t* tiled_w16, const int64_t* tiled_w16t, void* stream) {
+    return vt_adamw_step_dev_shadow_skip(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, coef, gscale, n_tiled,
+                                         tiled_off, tiled_N, tiled_K, tiled_w16, tiled_w16t, nullptr, stream);
 }
 
 int vt_adamw_set_vector(int on) {

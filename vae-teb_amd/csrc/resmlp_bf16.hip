@@ -34,13 +34,11 @@
 
 #include <stdlib.h>
 
-#include "common.h"
+#include "h16.h"
 
 namespace vt {
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int MAXL = VT_MLP_MAX_LAYERS;
 constexpr int MAXG = MAXL + 1;   // layers + skip projection
@@ -129,10 +127,6 @@ __device__ __forceinline__ int kperm(int p) {
     return 16 * (j >> 2) + 4 * g + (j & 3);
 }
 
-__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
 // act over a whole tile (one uniform switch, not one per element)
 template <int NT>
 __device__ __forceinline__ void act_tile(f32x4 (&z)[NT], int act) {
@@ -185,24 +179,24 @@ __device__ __forceinline__ void actd_tile(f32x4 (&z)[NT], int act) {
 }
 
 // B fragments of a transposed activation tile (k-step s = features 32s..32s+31)
-template <int NT>
-__device__ __forceinline__ void frags(const f32x4 (&a)[NT], bf16x8 (&b)[(NT + 1) / 2]) {
+template <int NT, typename H>
+__device__ __forceinline__ void frags(const f32x4 (&a)[NT], hv8<H> (&b)[(NT + 1) / 2]) {
 #pragma unroll
     for (int s = 0; s < (NT + 1) / 2; ++s) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            b[s][j] = (__bf16)a[2 * s][j];
-            b[s][4 + j] = (2 * s + 1 < NT) ? (__bf16)a[2 * s + 1][j] : (__bf16)0.f;
+            b[s][j] = (H)a[2 * s][j];
+            b[s][4 + j] = (2 * s + 1 < NT) ? (H)a[2 * s + 1][j] : (H)0.f;
         }
     }
 }
 
 // acc[t] = sum_s (image rows 16t..16t+15) x b[s];  nt output tiles, ks k-steps (runtime, <= template bounds)
-template <int NT, int KS>
-__device__ __forceinline__ void tile_gemm(const __bf16* img, int stride, int nt, int ks, const bf16x8 (&b)[KS],
+template <int NT, int KS, typename H>
+__device__ __forceinline__ void tile_gemm(const H* img, int stride, int nt, int ks, const hv8<H> (&b)[KS],
                                           f32x4 (&acc)[NT]) {
     const int lane = threadIdx.x & 63;
-    const __bf16* p = img + (lane & 15) * stride + 8 * (lane >> 4);
+    const H* p = img + (lane & 15) * stride + 8 * (lane >> 4);
     const int step = 16 * stride;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -210,7 +204,7 @@ __device__ __forceinline__ void tile_gemm(const __bf16* img, int stride, int nt,
         if (t < nt) {
 #pragma unroll
             for (int s = 0; s < KS; ++s)
-                if (s < ks) c = mfma(*(const bf16x8*)(p + 32 * s), b[s], c);
+                if (s < ks) c = mfma16(*(const hv8<H>*)(p + 32 * s), b[s], c);
         }
         acc[t] = c;
         p += step;
@@ -377,19 +371,20 @@ __device__ __forceinline__ void ln_fwd(f32x4 (&z)[NT], int C, const float* gl, c
 // backward workgroups then copy them to LDS with LDS-DMA (global_load_lds, no
 // VGPR round trip), instead of every workgroup re-gathering and converting the
 // fp32 weights (18 us of a 92 us backward workgroup, tools/mlpb_phases.py).
+template <typename H>
 __global__ __launch_bounds__(256) void k_mlpb_prep(const BDesc* __restrict__ dp) {
     const BDesc& d = *dp;
     const int seg = blockIdx.y, e = blockIdx.x * 256 + threadIdx.x;
-    __bf16* fimg = reinterpret_cast<__bf16*>(d.gimg);
+    H* fimg = reinterpret_cast<H*>(d.gimg);
     float* fprm = reinterpret_cast<float*>(d.gimg + d.fimg);
-    __bf16* bimg = reinterpret_cast<__bf16*>(d.gimg + d.gbo);
+    H* bimg = reinterpret_cast<H*>(d.gimg + d.gbo);
     float* bprm = reinterpret_cast<float*>(d.gimg + d.gpo);
     if (seg < d.nG) {                                  // forward image of GEMM seg: [pad16 N][fs]
         const BG& G = d.G[seg];
         if (e >= p16(G.N) * G.fs) return;
         const int n = e / G.fs, q = e - n * G.fs;
         const int k = (q & ~31) + kperm(q & 31);
-        fimg[G.fo + e] = (__bf16)((n < G.N && q < p32(G.K) && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f);
+        fimg[G.fo + e] = (H)((n < G.N && q < p32(G.K) && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f);
     } else if (seg == d.nG) {                          // forward params
         const int d0p = p16(d.d0);
         if (e < d.pin) {
@@ -409,7 +404,7 @@ __global__ __launch_bounds__(256) void k_mlpb_prep(const BDesc* __restrict__ dp)
         if (e >= p16(G.K) * G.bs) return;
         const int k = e / G.bs, q = e - k * G.bs;
         const int n = (q & ~31) + kperm(q & 31);
-        bimg[G.gbw + e] = (__bf16)((q < p32(G.N) && n < G.N && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f);
+        bimg[G.gbw + e] = (H)((q < p32(G.N) && n < G.N && k < G.K) ? G.W[(int64_t)n * G.K + k] : 0.f);
     } else {                                           // backward LN params (+ the input LN)
         if (e >= d.bprm) return;
         if (e >= d.bpin) {
@@ -446,13 +441,14 @@ __device__ __forceinline__ void lds_copy_wait() {
 // (the optimizer rewrites them each step); loads in batches of SB per thread,
 // all in flight before the first conversion
 
-__device__ void stage_fwd(const BDesc& d, __bf16* img, float* prm) {
+template <typename H>
+__device__ void stage_fwd(const BDesc& d, H* img, float* prm) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int g = 0; g < d.nG; ++g) {
         const BG& G = d.G[g];
         const int Np = p16(G.N), Kp = p32(G.K);
         const float* __restrict__ W = G.W;
-        __bf16* dst = img + G.fo;
+        H* dst = img + G.fo;
         // wave w: rows n = w, w + 8, ... (two per pass); lane: columns p = lane + 64 j
         for (int n0 = wv; n0 < Np; n0 += 2 * NW) {
             float v[2][3];
@@ -469,7 +465,7 @@ __device__ void stage_fwd(const BDesc& d, __bf16* img, float* prm) {
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
                     const int n = n0 + NW * r, p = lane + 64 * j;
-                    if (n < Np && p < Kp) dst[n * G.fs + p] = (__bf16)v[r][j];
+                    if (n < Np && p < Kp) dst[n * G.fs + p] = (H)v[r][j];
                 }
         }
         const bool lnl = g < d.L && d.l[g].ln;
@@ -487,7 +483,7 @@ __device__ void stage_fwd(const BDesc& d, __bf16* img, float* prm) {
 }
 
 // ID: identity skip (out += x0); otherwise skip 0 / 2 (projection of x0 at the end)
-template <int NT, bool ID>
+template <int NT, bool ID, typename H>
 __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp, const float* __restrict__ X, int64_t R,
                                                     float* __restrict__ out, float* __restrict__ xh,
                                                     float* __restrict__ rs, int64_t Rp) {
@@ -495,13 +491,13 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
                             // by layer is copied to scratch)
     constexpr int KS = (NT + 1) / 2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const __bf16* img = reinterpret_cast<const __bf16*>(smem);
+    const H* img = reinterpret_cast<const H*>(smem);
     float* prm = reinterpret_cast<float*>(smem + d.fimg);
     if (d.gimg) {
         lds_copy(smem, d.gimg, d.fbytes);
         lds_copy_wait();
     } else {
-        stage_fwd(d, reinterpret_cast<__bf16*>(smem), prm);
+        stage_fwd<H>(d, reinterpret_cast<H*>(smem), prm);
         __syncthreads();
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4, lr = lane & 15;
@@ -519,19 +515,19 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
 #pragma unroll
             for (int t = 0; t < NT; ++t) x0[t] = a[t];
         }
-        bf16x8 bx[KS], b[KS];
-        frags<NT>(a, bx);
+        hv8<H> bx[KS], b[KS];
+        frags<NT, H>(a, bx);
 #pragma unroll
         for (int s = 0; s < KS; ++s) b[s] = bx[s];
         for (int l = 0; l < L; ++l) {
             const int K = d.G[l].K, N = d.G[l].N, fo = d.G[l].fo, fs = d.G[l].fs, po = d.G[l].po;
-            tile_gemm<NT, KS>(img + fo, fs, (N + 15) >> 4, (K + 31) >> 5, b, a);
+            tile_gemm<NT, KS, H>(img + fo, fs, (N + 15) >> 4, (K + 31) >> 5, b, a);
 #pragma unroll
             for (int t = 0; t < NT; ++t) a[t] += *(const f32x4*)(prm + po + 16 * t + 4 * g4);   // bias (0 past N)
             if (d.l[l].ln)
                 ln_fwd<NT>(a, N, prm + po + p16(N), prm + po + 2 * p16(N), d.l[l].act, d.eps,
                            xh16 + (int64_t)d.l[l].xo * Rp, rs + (int64_t)d.l[l].ri * Rp, Rp, row, rok);
-            if (l < L - 1) frags<NT>(a, b);
+            if (l < L - 1) frags<NT, H>(a, b);
         }
         if constexpr (ID) {
 #pragma unroll
@@ -539,7 +535,7 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
         } else if (d.skip == 2) {
             const BG& G = d.G[L];
             f32x4 sk[NT];
-            tile_gemm<NT, KS>(img + G.fo, G.fs, (G.N + 15) >> 4, (G.K + 31) >> 5, bx, sk);
+            tile_gemm<NT, KS, H>(img + G.fo, G.fs, (G.N + 15) >> 4, (G.K + 31) >> 5, bx, sk);
 #pragma unroll
             for (int t = 0; t < NT; ++t) a[t] += sk[t] + *(const f32x4*)(prm + G.po + 16 * t + 4 * g4);
         }
@@ -550,7 +546,8 @@ __global__ __launch_bounds__(BT, 1) void k_mlpb_fwd(const BDesc* __restrict__ dp
 // ----------------------------------------------------------------- backward
 // W^T image of GEMM G: img[k][32s + 8g + j] = W[32s + kperm(8g + j)][k]
 // (column p = n-position of the permuted image per wave, lanes over k: coalesced W rows)
-__device__ void stage_wt(const BG& G, __bf16* img) {
+template <typename H>
+__device__ void stage_wt(const BG& G, H* img) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int Kp = p16(G.K), Np = p32(G.N);
     const float* __restrict__ W = G.W;
@@ -569,7 +566,7 @@ __device__ void stage_wt(const BG& G, __bf16* img) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 const int p = p0 + NW * r, k = lane + 64 * j;
-                if (p < Np && k < Kp) img[G.bw + k * G.bs + p] = (__bf16)v[r][j];
+                if (p < Np && k < Kp) img[G.bw + k * G.bs + p] = (H)v[r][j];
             }
     }
 }
@@ -659,16 +656,16 @@ __device__ __forceinline__ void ln_bwd(f32x4 (&dh)[NT], const f32x4 (&xv)[NT], f
 }
 
 // transposed tile -> bf16 image rows [f][col0 + r] (row stride S) for the tiles covering C
-template <int NT, int S>
-__device__ __forceinline__ void put_img(__bf16* im, const f32x4 (&a)[NT], int C, int col0) {
+template <int NT, int S, typename H>
+__device__ __forceinline__ void put_img(H* im, const f32x4 (&a)[NT], int C, int col0) {
     const int lane = threadIdx.x & 63, g4 = lane >> 4, lr = lane & 15;
     const int nt = (C + 15) >> 4;
-    __bf16* p = im + 4 * g4 * S + col0 + lr;
+    H* p = im + 4 * g4 * S + col0 + lr;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         if (t >= nt) continue;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) p[(16 * t + i) * S] = (__bf16)a[t][i];
+        for (int i = 0; i < 4; ++i) p[(16 * t + i) * S] = (H)a[t][i];
     }
 }
 
@@ -734,8 +731,8 @@ __device__ __forceinline__ void flush_cols(float* red, const float (&la)[NT], co
 // dW partial of one GEMM over images of ROWS rows (row stride S) -> dst[n * K1 + k]
 // (k < K): wave (wn = w >> 2, wk = w & 3) owns output tiles tn = wn + 2a,
 // tk = wk + 4c, one tn at a time (TKS accumulators live)
-template <int TNS, int TKS, int ROWS, int S>
-__device__ __forceinline__ void dw_img(const __bf16* zi, const __bf16* hi, int N, int K, float* __restrict__ dst) {
+template <int TNS, int TKS, int ROWS, int S, typename H>
+__device__ __forceinline__ void dw_img(const H* zi, const H* hi, int N, int K, float* __restrict__ dst) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wn = wv >> 2, wk = wv & 3;
     const int g4 = lane >> 4, lr = lane & 15, K1 = K + 1;
     const int ntn = (N + 15) >> 4, ntk = (K + 15) >> 4;
@@ -748,11 +745,11 @@ __device__ __forceinline__ void dw_img(const __bf16* zi, const __bf16* hi, int N
         for (int c = 0; c < TKS; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
         for (int s = 0; s < ROWS / 32; ++s) {
-            const bf16x8 af = *(const bf16x8*)(zi + 16 * tn * S + off + 32 * s);
+            const hv8<H> af = *(const hv8<H>*)(zi + 16 * tn * S + off + 32 * s);
 #pragma unroll
             for (int c = 0; c < TKS; ++c) {
                 const int tk = wk + 4 * c;
-                if (tk < ntk) acc[c] = mfma(af, *(const bf16x8*)(hi + 16 * tk * S + off + 32 * s), acc[c]);
+                if (tk < ntk) acc[c] = mfma16(af, *(const hv8<H>*)(hi + 16 * tk * S + off + 32 * s), acc[c]);
             }
         }
 #pragma unroll
@@ -779,7 +776,7 @@ __device__ __forceinline__ void dw_img(const __bf16* zi, const __bf16* hi, int N
     do {                                                                                     \
         if (stamps && threadIdx.x == 0) stamps[(int64_t)blockIdx.x * 256 + (k)] = wall_clock64(); \
     } while (0)
-template <int NT, int TPW, int OCC = 1>
+template <int NT, int TPW, int OCC = 1, typename H = __bf16>
 __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restrict__ dp, const float* __restrict__ dout,
                                                     const float* __restrict__ xh, const float* __restrict__ rs,
                                                     int64_t R, int64_t Rp, float* __restrict__ dx,
@@ -791,9 +788,9 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
     constexpr int ROWS = IMR * TPW;            // rows per workgroup (one image)
     constexpr int IS = ROWS + 16;              // image row stride: == 16 mod 32 -> conflict-free fragments
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __bf16* wimg = reinterpret_cast<__bf16*>(smem);
-    __bf16* zimg = wimg + d.bwimg;
-    __bf16* himg = zimg + d.bzrows * IS;
+    H* wimg = reinterpret_cast<H*>(smem);
+    H* zimg = wimg + d.bwimg;
+    H* himg = zimg + d.bzrows * IS;
     float* prm = reinterpret_cast<float*>(himg + d.bhrows * IS);   // [LN params per LN layer][input LN]
     float* red = prm + d.bprm;                                     // [NW][48 NT]
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4;
@@ -808,7 +805,7 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
         lds_copy_wait();
     } else {
     if (d.bres)
-        for (int g = 0; g < d.nG; ++g) stage_wt(d.G[g], wimg);
+        for (int g = 0; g < d.nG; ++g) stage_wt<H>(d.G[g], wimg);
     // gamma / beta of every LayerNorm (+ the input LN), staged once; layer l's at prm + l.bpo
     for (int l = 0; l <= L; ++l) {
         const bool inl = l == L;
@@ -874,12 +871,12 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
             if (d.gimg)
                 lds_copy(reinterpret_cast<char*>(wimg), d.gimg + d.gbo + 2 * G.gbw, 2 * ((p16(K) * G.bs + 7) & ~7));
             else
-                stage_wt(G, wimg);
+                stage_wt<H>(G, wimg);
         }
         float la[NT], lb[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
-        bf16x8 b[TPW][KS];
+        hv8<H> b[TPW][KS];
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             const int64_t row = rbase + IMR * u;
@@ -899,9 +896,9 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
             if (step == 1 && u == 0) MB_STAMP(240);   // diagnostic sub-phases of step 1, first tile
             colsum<NT>(dz, N, lb);            // the bias gradient: fp32 sum of dZ (not of its bf16 image)
             if (step == 1 && u == 0) MB_STAMP(241);
-            put_img<NT, IS>(zimg, dz, N, 128 * u + 16 * wv);
+            put_img<NT, IS, H>(zimg, dz, N, 128 * u + 16 * wv);
             if (step == 1 && u == 0) MB_STAMP(242);
-            frags<NT>(dz, b[u]);
+            frags<NT, H>(dz, b[u]);
             if (step == 1 && u == 0) MB_STAMP(243);
         }
         MB_STAMP(3 + 6 * step);
@@ -926,7 +923,7 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
 #pragma unroll
                 for (int t = 0; t < NT; ++t) hv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            put_img<NT, IS>(himg, hv, K, 128 * u + 16 * wv);
+            put_img<NT, IS, H>(himg, hv, K, 128 * u + 16 * wv);
 #pragma unroll
             for (int t = 0; t < NT; ++t) xc[u][t] = xn[u][t];   // the next step's LN input
             rsc[u] = rsn[u];
@@ -939,7 +936,7 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             f32x4 nh[NT];
-            tile_gemm<NT, KS>(wimg + G.bw, bs, (K + 15) >> 4, (N + 31) >> 5, b[u], nh);
+            tile_gemm<NT, KS, H>(wimg + G.bw, bs, (K + 15) >> 4, (N + 31) >> 5, b[u], nh);
             if (skp) {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) dh[u][t] += nh[t];
@@ -949,7 +946,7 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
             }
         }
         // dW over the block's rows -> this workgroup's partial (db: column K, from the column sums)
-        dw_img<TNS, TKS, ROWS, IS>(zimg, himg, N, K, pb + G.wo);
+        dw_img<TNS, TKS, ROWS, IS, H>(zimg, himg, N, K, pb + G.wo);
         MB_STAMP(6 + 6 * step);
         flush_cols<NT>(red, la, lb, N, ln, ln ? pb + d.l[l].lpo : nullptr, pb + G.wo + K, K + 1);
         MB_STAMP(7 + 6 * step);
@@ -999,17 +996,17 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
 // grouping: other rounding, same precision).
 // (the second launch bound is waves per SIMD: two 512-thread workgroups per CU for the narrow
 // stacks with 128-row blocks, whose W^T images fit 80 KB; one otherwise)
-template <int NT, int TPW>
+template <int NT, int TPW, typename H = __bf16>
 __global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx(const BDesc* __restrict__ dp, const float* __restrict__ dout,
                                                      const float* __restrict__ xh, const float* __restrict__ rs,
                                                      int64_t R, int64_t Rp, float* __restrict__ dx,
-                                                     float* __restrict__ part, __bf16* __restrict__ dz16) {
+                                                     float* __restrict__ part, H* __restrict__ dz16) {
     const BDesc& d = *dp;
     constexpr int KS = (NT + 1) / 2;
     constexpr int ROWS = IMR * TPW;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // every W^T image at its global-image offset G.gbw, then the LN parameters
-    __bf16* wimg = reinterpret_cast<__bf16*>(smem);
+    H* wimg = reinterpret_cast<H*>(smem);
     float* prm = reinterpret_cast<float*>(smem + (d.gpo - d.gbo));   // [LN params per LN layer][input LN]
     float* red = prm + d.bprm;                                         // [2][NW][48 NT]: flushes double-buffered
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4;
@@ -1051,7 +1048,7 @@ __global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx
 #pragma unroll
         for (int t = 0; t < NT; ++t) la[t] = lb[t] = 0.f;
         const int ntz = (N + 15) >> 4;
-        __bf16* zrow = dz16 + G.zo;
+        H* zrow = dz16 + G.zo;
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             const int64_t row = rbase + IMR * u;
@@ -1074,17 +1071,17 @@ __global__ __launch_bounds__(BT, (NT <= 4 && TPW == 1) ? 4 : 2) void k_mlpb_bwdx
             load_sv<NT>(xc[u], xH, CH, Rp, row, row < R);
             colsum<NT>(dz, N, lb);
             // dZ row (bf16, 0 past N and for rows past R) for the weight-gradient kernel
-            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-            __bf16* zp = zrow + row * G.zs + 4 * g4;
+            
+            H* zp = zrow + row * G.zs + 4 * g4;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
                 if (t < ntz)
-                    *(bf16x4*)(zp + 16 * t) = bf16x4{(__bf16)dz[t][0], (__bf16)dz[t][1], (__bf16)dz[t][2],
-                                                      (__bf16)dz[t][3]};
-            bf16x8 b[KS];
-            frags<NT>(dz, b);
+                    *(hv4<H>*)(zp + 16 * t) = hv4<H>{(H)dz[t][0], (H)dz[t][1], (H)dz[t][2],
+                                                      (H)dz[t][3]};
+            hv8<H> b[KS];
+            frags<NT, H>(dz, b);
             f32x4 nh[NT];
-            tile_gemm<NT, KS>(wimg + G.gbw, bs, (K + 15) >> 4, (N + 31) >> 5, b, nh);
+            tile_gemm<NT, KS, H>(wimg + G.gbw, bs, (K + 15) >> 4, (N + 31) >> 5, b, nh);
             if (skp) {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) dh[u][t] += nh[t];
@@ -1128,27 +1125,28 @@ __device__ __forceinline__ int dz_pos(int r, int c) { return r * DZS + (r >> 3) 
 
 // 16 columns col0.. x 32 rows row0.. of a [r][col] image as an MFMA operand (rows = the
 // contraction): lane 4q + p of 16-lane group g reads rows row0 + 8g + q (+4), columns col0 + 4p ..
-__device__ __forceinline__ bf16x8 dz_frag(const __bf16* img, int row0, int col0) {
+template <typename H>
+__device__ __forceinline__ hv8<H> dz_frag(const H* img, int row0, int col0) {
     typedef short v4i16 __attribute__((ext_vector_type(4)));
     typedef short v8i16 __attribute__((ext_vector_type(8)));
     const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const __bf16* a0 = img + dz_pos(row0 + 8 * g + q, col0 + 4 * p);
-    const __bf16* a1 = img + dz_pos(row0 + 8 * g + q + 4, col0 + 4 * p);
+    const H* a0 = img + dz_pos(row0 + 8 * g + q, col0 + 4 * p);
+    const H* a1 = img + dz_pos(row0 + 8 * g + q + 4, col0 + 4 * p);
     const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
     const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a1);
     const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(hv8<H>, r);
 }
 
 // grid (row chunks, GEMMs), 256 threads; MT >= output tiles per wave (4 waves share the
 // ceil(N/16) x ceil(K/16) tiles round-robin).  part: [chunk][dP], this GEMM's N x K at G.dwo.
-template <int MT>
-__global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, const __bf16* __restrict__ dz16,
+template <int MT, typename H = __bf16>
+__global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, const H* __restrict__ dz16,
                                                  const float* __restrict__ xh, int64_t R, int64_t Rp, int chunk_rows,
                                                  float* __restrict__ part) {
     const BDesc& d = *dp;
-    __shared__ __attribute__((aligned(16))) __bf16 zimg[DZIMG];
-    __shared__ __attribute__((aligned(16))) __bf16 himg[DZIMG];
+    __shared__ __attribute__((aligned(16))) H zimg[DZIMG];
+    __shared__ __attribute__((aligned(16))) H himg[DZIMG];
     const int gi = blockIdx.y;
     const BG& G = d.G[gi];
     const int N = G.N, K = G.K;
@@ -1159,7 +1157,7 @@ __global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, c
     const int actH = hsrc >= 0 ? d.l[hsrc].act : 0;
     const int kp = p16(K);                // saved-xhat row stride (floats)
     const _Float16* xH = xh_region(xh, hsrc >= 0 ? d.l[hsrc].xo : 0, Rp);
-    const __bf16* zsrc = dz16 + G.zo;
+    const H* zsrc = dz16 + G.zo;
     const int zs = G.zs;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lc = lane >> 4;
     const int ntn = (N + 15) >> 4, ntk = (K + 15) >> 4, ntiles = ntn * ntk;
@@ -1169,7 +1167,7 @@ __global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, c
     const int64_t Rz = (R + DWROWS - 1) / DWROWS * DWROWS;   // rows past it are all 0: skipped
     const int64_t r0 = (int64_t)blockIdx.x * chunk_rows;
     const int64_t r1 = r0 + chunk_rows < Rz ? r0 + chunk_rows : Rz;
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    
     for (int64_t rb = r0; rb < r1; rb += DWROWS) {
         // dZ rows: 16-B pieces (8 bf16), zs / 8 per row; rows past R are 0 (k_mlpb_bwdx writes
         // the rows of its blocks only, not up to the padded Rp)
@@ -1193,7 +1191,7 @@ __global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, c
                 const int k = 4 * q + i;
                 h[i] = (row < R && k < K) ? bact(fmaf(h[i], gam[k], bet[k]), actH) : 0.f;
             }
-            *(bf16x4*)(himg + dz_pos(r, 4 * q)) = bf16x4{(__bf16)h[0], (__bf16)h[1], (__bf16)h[2], (__bf16)h[3]};
+            *(hv4<H>*)(himg + dz_pos(r, 4 * q)) = hv4<H>{(H)h[0], (H)h[1], (H)h[2], (H)h[3]};
         }
         __syncthreads();
 #pragma unroll
@@ -1203,7 +1201,7 @@ __global__ __launch_bounds__(256) void k_mlpb_dw(const BDesc* __restrict__ dp, c
                 const int tile = w + 4 * j;
                 if (tile < ntiles) {
                     const int tn = tile / ntk, tk = tile - tn * ntk;
-                    acc[j] = mfma(dz_frag(zimg, 32 * s, 16 * tn), dz_frag(himg, 32 * s, 16 * tk), acc[j]);
+                    acc[j] = mfma16(dz_frag<H>(zimg, 32 * s, 16 * tn), dz_frag<H>(himg, 32 * s, 16 * tk), acc[j]);
                 }
             }
         }
@@ -1619,15 +1617,15 @@ int vt_resmlp_bf16_fwd(int n_layers, const int* dims, const int* layer_ln, const
     const BPlan& p = *pp;
     VT_CHECK_ARG(x && out && xhat && rstd, "vt_resmlp_bf16_fwd: null buffer");
     // the weight images of this step (read again by the backward of this forward)
-    hipLaunchKernelGGL(k_mlpb_prep, dim3((unsigned)p.prep_x, (unsigned)p.prep_y), dim3(256), 0, st, ddev);
+    VT_H16(hipLaunchKernelGGL(k_mlpb_prep<H>, dim3((unsigned)p.prep_x, (unsigned)p.prep_y), dim3(256), 0, st, ddev));
     const dim3 grid((unsigned)n_fwd_blocks(rows));
     const bool id = skip == 1;
     switch (p.nt * 2 + (id ? 1 : 0)) {
 #define VT_MBF(NTV, IDV)                                                                                   \
     case NTV * 2 + IDV:                                                                                    \
-        set_lds(k_mlpb_fwd<NTV, IDV>, p.d.fbytes);                                                        \
-        hipLaunchKernelGGL((k_mlpb_fwd<NTV, IDV>), grid, dim3(BT), p.d.fbytes, st, ddev, x, rows, out, xhat, rstd, \
-                           p.Rp);                                                                          \
+        VT_H16(set_lds(k_mlpb_fwd<NTV, IDV, H>, p.d.fbytes);                                              \
+               hipLaunchKernelGGL((k_mlpb_fwd<NTV, IDV, H>), grid, dim3(BT), p.d.fbytes, st, ddev, x, rows, out, \
+                                  xhat, rstd, p.Rp));                                                       \
         break;
         VT_MBF(2, 0) VT_MBF(2, 1) VT_MBF(4, 0) VT_MBF(4, 1) VT_MBF(6, 0) VT_MBF(6, 1) VT_MBF(9, 0)
         default: VT_MBF(9, 1)
@@ -1669,9 +1667,9 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
     const dim3 grid((unsigned)p.nblk);
 #define VT_MBB(NTV, TPWV, OCCV)                                                                                  \
     if (p.nt == NTV && p.tpw == TPWV && p.occ == OCCV) {                                                           \
-        set_lds(k_mlpb_bwd<NTV, TPWV, OCCV>, p.d.bbytes);                                                          \
-        hipLaunchKernelGGL((k_mlpb_bwd<NTV, TPWV, OCCV>), grid, dim3(BT), p.d.bbytes, st, ddev, dout, xhat, rstd, rows, \
-                           p.Rp, dx, ws, g_mlpb_stamps);                                                           \
+        VT_H16(set_lds(k_mlpb_bwd<NTV, TPWV, OCCV, H>, p.d.bbytes);                                                \
+               hipLaunchKernelGGL((k_mlpb_bwd<NTV, TPWV, OCCV, H>), grid, dim3(BT), p.d.bbytes, st, ddev, dout, xhat,  \
+                                  rstd, rows, p.Rp, dx, ws, g_mlpb_stamps));                                         \
     }
     VT_MBB(2, 2, 1) VT_MBB(4, 2, 1) VT_MBB(2, 1, 1) VT_MBB(4, 1, 1) VT_MBB(6, 1, 1) VT_MBB(9, 1, 1)
     VT_MBB(2, 1, 2) VT_MBB(4, 1, 2)
@@ -1717,6 +1715,7 @@ int vt_resmlp_bf16_bwd_data(int n_layers, const int* dims, const int* layer_ln, 
     if (rc) return rc;
     const BPlan& p = *pp;
     VT_CHECK_ARG(p.d.xbytes > 0, "vt_resmlp_bf16_bwd_data: the W^T images do not fit in LDS (use vt_resmlp_bf16_bwd)");
+    VT_CHECK_ARG(!h16_format(), "vt_resmlp_bf16_bwd_data: the split backward has no fp16 form (use vt_resmlp_bf16_bwd)");
     VT_CHECK_ARG(dout && xhat && rstd && dx && grads && dz16, "vt_resmlp_bf16_bwd_data: null buffer");
     VT_CHECK_ARG(ws && ws_floats >= p.xnblk * p.d.xP, "vt_resmlp_bf16_bwd_data: workspace %lld floats < %lld",
                  (long long)ws_floats, (long long)(p.xnblk * p.d.xP));
@@ -1739,8 +1738,8 @@ int vt_resmlp_bf16_bwd_data(int n_layers, const int* dims, const int* layer_ln, 
     __bf16* z = reinterpret_cast<__bf16*>(dz16);
 #define VT_MBX(NTV, TPWV)                                                                                       \
     if (p.nt == NTV && p.xtpw == TPWV) {                                                                          \
-        set_lds(k_mlpb_bwdx<NTV, TPWV>, p.d.xbytes);                                                              \
-        hipLaunchKernelGGL((k_mlpb_bwdx<NTV, TPWV>), grid, dim3(BT), p.d.xbytes, st, ddev, dout, xhat, rstd, rows, \
+        set_lds(k_mlpb_bwdx<NTV, TPWV, __bf16>, p.d.xbytes);                                                              \
+        hipLaunchKernelGGL((k_mlpb_bwdx<NTV, TPWV, __bf16>), grid, dim3(BT), p.d.xbytes, st, ddev, dout, xhat, rstd, rows, \
                            p.Rp, dx, ws, z);                                                                      \
     }
     VT_MBX(2, 1) VT_MBX(2, 2) VT_MBX(4, 1) VT_MBX(4, 2) VT_MBX(6, 1) VT_MBX(9, 1)
@@ -1762,6 +1761,7 @@ int vt_resmlp_bf16_bwd_weight(int n_layers, const int* dims, const int* layer_ln
     if (rc) return rc;
     const BPlan& p = *pp;
     VT_CHECK_ARG(p.d.xbytes > 0, "vt_resmlp_bf16_bwd_weight: no split plan for this stack");
+    VT_CHECK_ARG(!h16_format(), "vt_resmlp_bf16_bwd_weight: the split backward has no fp16 form");
     VT_CHECK_ARG(xhat && dz16 && grads, "vt_resmlp_bf16_bwd_weight: null buffer");
     VT_CHECK_ARG(ws && ws_floats >= (int64_t)p.dw_chunks * p.d.dP,
                  "vt_resmlp_bf16_bwd_weight: workspace %lld floats < %lld", (long long)ws_floats,
@@ -1779,10 +1779,10 @@ int vt_resmlp_bf16_bwd_weight(int n_layers, const int* dims, const int* layer_ln
     const dim3 grid((unsigned)p.dw_chunks, (unsigned)p.d.nG);
     const __bf16* z = reinterpret_cast<const __bf16*>(dz16);
     switch (p.mt) {
-        case 1: hipLaunchKernelGGL(k_mlpb_dw<1>, grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
-        case 4: hipLaunchKernelGGL(k_mlpb_dw<4>, grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
-        case 9: hipLaunchKernelGGL(k_mlpb_dw<9>, grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
-        default: hipLaunchKernelGGL(k_mlpb_dw<21>, grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
+        case 1: hipLaunchKernelGGL((k_mlpb_dw<1, __bf16>), grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
+        case 4: hipLaunchKernelGGL((k_mlpb_dw<4, __bf16>), grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
+        case 9: hipLaunchKernelGGL((k_mlpb_dw<9, __bf16>), grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
+        default: hipLaunchKernelGGL((k_mlpb_dw<21, __bf16>), grid, dim3(256), 0, st, ddev, z, xhat, rows, p.Rp, p.dw_rows, ws); break;
     }
     sum_launch(sa, emax, ws, p.dw_chunks, accumulate, st);
     VT_LAUNCH_CHECK("vt_resmlp_bf16_bwd_weight");

@@ -130,6 +130,23 @@ def wait_for(waiter, src=None):
             raise RuntimeError(f"vt_stream_fork: {lib().last_error()}")
 
 
+_H16 = [None]
+
+
+def set_h16(fp16):
+    """The library's 16-bit MFMA operand format (vt_set_h16_format): False bf16 (default), True fp16
+    (the reference's autocast width, trained with a dynamic loss scale: vaeteb.train.Trainer)."""
+    v = 1 if fp16 else 0
+    if _H16[0] != v:
+        lib().fns["vt_set_h16_format"](v)
+        _H16[0] = v
+
+
+def h16():
+    """The current 16-bit operand format: 'fp16' or 'bf16'."""
+    return "fp16" if lib().fns["vt_get_h16_format"]() else "bf16"
+
+
 def capture_info(src=None):
     """Diagnostic: the hipGraph capture state of stream `src` (default: the current stream) as
     text — vt_capture_info (tools/capture_probe.py)."""

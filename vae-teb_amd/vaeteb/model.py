@@ -365,7 +365,7 @@ class ConvStack(nn.Sequential):
     def forward(self, x):
         blocks = list(self)
         if not (CONV_FOLD and len(blocks) > 1 and x.is_cuda and
-                all(isinstance(b, ConvBlock) and b.training and b.bf16 and not b.sync_bn for b in blocks) and
+                all(isinstance(b, ConvBlock) and b.training and b.bf16 == "bf16" and not b.sync_bn for b in blocks) and
                 not any(b.tanh for b in blocks[:-1]) and   # the staging applies the inner blocks' ReLU
                 # a folded block's backward needs its input's gradient (the fused bf16 path): every
                 # inner output must require grad, else the unfolded stack runs (checked here, before
@@ -513,6 +513,9 @@ class ConditionalEncoder(nn.Module):
         return mu, lv
 
 
+PRECISIONS = ("fp32", "bf16", "fp16")
+
+
 class Decoder(nn.Module):
     """ref/model/vae_teb_model.py:823-929 with the head width R = 16*S."""
 
@@ -531,17 +534,17 @@ class Decoder(nn.Module):
         self.set_head_precision(head_precision)
 
     def set_head_precision(self, precision):
-        """"fp32": every GEMM on the fp32 kernels (parity mode); "bf16": the
-        R x R head GEMMs on bf16 MFMA with fp32 accumulation (the reference
-        trains in fp16 autocast, ref/model/graph_model.py:510,710; bf16 here is the
-        documented deviation)."""
-        if precision not in ("fp32", "bf16"):
-            raise ValueError(f"head_precision must be 'fp32' or 'bf16', got {precision!r}")
+        """"fp32": every GEMM on the fp32 kernels (parity mode); "bf16" / "fp16": the
+        R x R head GEMMs on 16-bit MFMA with fp32 accumulation — "fp16" is the reference's
+        own autocast width (ref/model/graph_model.py:510,710; trained with the dynamic loss
+        scale), "bf16" the MI355X default (no loss scale)."""
+        if precision not in PRECISIONS:
+            raise ValueError(f"head_precision must be one of {PRECISIONS}, got {precision!r}")
         self.head_precision = precision
         for head in (self.output_mu, self.output_logvar):
             for m in head.modules():
                 if isinstance(m, Linear):
-                    m.mfma = precision == "bf16"
+                    m.mfma = ops.h16_flag(precision != "fp32" and precision)
 
     def forward(self, z):
         lin = self.linear(z)                       # (B, S, 87)
@@ -589,29 +592,53 @@ class SeqVaeTeb(nn.Module):
                 m.half = precision == "16-mixed"
 
     def set_mlp_precision(self, precision):
-        """"fp32": the ResidualMLP stacks on exact-fp32 MFMA (parity mode); "bf16":
-        their Linear layers on bf16 MFMA with fp32 accumulation, LayerNorm and
-        reductions fp32 — the reference trains in fp16 autocast (bf16 here: DESIGN.md §5)
-        (ref/model/graph_model.py:510, :709-711)."""
-        if precision not in ("fp32", "bf16"):
-            raise ValueError(f"mlp_precision must be 'fp32' or 'bf16', got {precision!r}")
+        """"fp32": the ResidualMLP stacks on exact-fp32 MFMA (parity mode); "bf16" / "fp16":
+        their Linear layers on 16-bit MFMA with fp32 accumulation, LayerNorm and reductions
+        fp32 — the reference trains in fp16 autocast (ref/model/graph_model.py:510, :709-711);
+        "fp16" is that width (with the trainer's loss scale), "bf16" the default."""
+        if precision not in PRECISIONS:
+            raise ValueError(f"mlp_precision must be one of {PRECISIONS}, got {precision!r}")
         self.mlp_precision = precision
         for m in self.modules():
             if isinstance(m, ResidualMLP):
-                m.bf16 = precision == "bf16"
+                m.bf16 = ops.h16_flag(precision != "fp32" and precision)
+        self._check_h16()
 
     def set_conv_precision(self, precision):
-        """"fp32": exact-fp32 MFMA convs (parity mode); "bf16": bf16-MFMA convs with
-        fp32 accumulation and fp32 BatchNorm — the reference trains in fp16 (bf16 here: DESIGN.md §5) under
-        autocast (ref/model/graph_model.py:510, :709-711)."""
-        if precision not in ("fp32", "bf16"):
-            raise ValueError(f"conv_precision must be 'fp32' or 'bf16', got {precision!r}")
+        """"fp32": exact-fp32 MFMA convs (parity mode); "bf16" / "fp16": 16-bit-MFMA convs
+        with fp32 accumulation and fp32 BatchNorm — the reference trains in fp16 autocast
+        (ref/model/graph_model.py:510, :709-711); "fp16" is that width, "bf16" the default."""
+        if precision not in PRECISIONS:
+            raise ValueError(f"conv_precision must be one of {PRECISIONS}, got {precision!r}")
         self.conv_precision = precision
         for m in self.modules():
             if isinstance(m, ConvBlock):
-                m.bf16 = precision == "bf16"
+                m.bf16 = ops.h16_flag(precision != "fp32" and precision)
+        self._check_h16()
+
+    def set_head_precision(self, precision):
+        """The decoder heads' precision (Decoder.set_head_precision), kept to one 16-bit format."""
+        self.decoder.set_head_precision(precision)
+        self._check_h16()
+
+    def _check_h16(self):
+        """One 16-bit operand format per model (the library's format is selected per op, but the
+        optimizer writes every shadow of a step in one format): bf16 and fp16 do not mix."""
+        fams = {p for p in (self.decoder.head_precision, getattr(self, "conv_precision", "fp32"),
+                            getattr(self, "mlp_precision", "fp32")) if p != "fp32"}
+        if len(fams) > 1:
+            raise ValueError(f"head / conv / MLP precisions mix bf16 and fp16: {sorted(fams)}")
+        self.h16_format = fams.pop() if fams else None
+
+    @property
+    def loss_scaling(self):
+        """True when the model trains 16-bit fp16 operands: the trainer then runs GradScaler's
+        dynamic loss scale (ref/model/graph_model.py:670, 718-726)."""
+        return getattr(self, "h16_format", None) == "fp16"
 
     def forward(self, y_st, y_ph, x_ph, eps=None):
+        if getattr(self, "h16_format", None) and x_ph.is_cuda:
+            _lib.set_h16(self.h16_format == "fp16")   # the prepass shadows below are written in it
         prev = dict(_PAR)
         _PAR["on"], _PAR["next"] = bool(self.concurrent_encoders and x_ph.is_cuda), 1
         # conv weight gradients of this step's backward go to side stream GRAD_SIDE (off the

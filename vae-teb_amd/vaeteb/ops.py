@@ -51,6 +51,28 @@ def _check(*ts):
             raise TypeError(f"expected a CUDA float32 tensor, got {t.dtype} on {t.device}")
 
 
+# ------------------------------------------------------- 16-bit operand format
+# A module's 16-bit flag (Linear.mfma, ResidualMLP.bf16, ConvBlock.bf16): False (fp32 kernels),
+# "bf16" (or True) or "fp16" — the operand type of the library's 16-bit MFMA kernels (csrc/h16.h).
+# Every op that launches them selects the format first, in its forward and in its backward, so
+# models of either format can share a process; fp16 is the reference's autocast width and is
+# trained with the dynamic loss scale of vaeteb.train.Trainer (GradScaler).
+def h16_flag(flag):
+    """Normalise a 16-bit flag: False, "bf16" or "fp16"."""
+    if not flag:
+        return False
+    return "fp16" if flag == "fp16" else "bf16"
+
+
+def _h16(flag):
+    if flag:
+        _lib.set_h16(flag == "fp16")
+
+
+def _shadow_dtype():
+    return torch.float16 if _lib._H16[0] == 1 else torch.bfloat16
+
+
 # ----------------------------------------------------------- gradient sink
 # Parameters whose .grad is a persistent view of the trainer's flat gradient
 # buffer (vaeteb.train.FlatState sets p._vt_sink) receive their gradient
@@ -189,15 +211,18 @@ def _take_prepared(key):
 
 
 def _weight_shadow(w, prepass=False):
-    """bf16 images of an fp32 master weight W [N, K]: (W16 [N, K], W16t [K, N]),
-    rewritten from W on every forward (the optimizer updates W in place)."""
+    """16-bit images of an fp32 master weight W [N, K] in the current format (bf16 / fp16):
+    (W16 [N, K], W16t [K, N]), rewritten from W on every forward unless the optimizer step wrote
+    them with the weights (_fresh) or the prepass did (_take_prepared)."""
     N, K = w.shape
     key = (w.data_ptr(), N, K)
     sh = _SHADOW.get(key)
-    if sh is None:
-        sh = (torch.empty((N, K), dtype=torch.bfloat16, device=w.device),
-              torch.empty((K, N), dtype=torch.bfloat16, device=w.device))
+    dt = _shadow_dtype()
+    if sh is None or sh[0].dtype != dt:
+        sh = (torch.empty((N, K), dtype=dt, device=w.device),
+              torch.empty((K, N), dtype=dt, device=w.device))
         _SHADOW[key] = sh
+        _FRESH.pop(key, None)
     if prepass or not (_take_prepared(key) or _fresh(key, w)):
         call("vt_mfma_weight_shadow", ptr(w), N, K, ptr(sh[0]), ptr(sh[1]), _st())
     return sh
@@ -238,9 +263,10 @@ class LinearF(torch.autograd.Function):
         x2 = x.reshape(-1, K).contiguous()
         R = x2.shape[0]
         y = torch.empty((R, N), device=x.device)
-        mfma = bool(mfma) and mfma_ok(K, N)
+        mfma = h16_flag(mfma) if mfma_ok(K, N) else False
         w16t = None
         if mfma:
+            _h16(mfma)
             w16, w16t = _weight_shadow(w)
             ws = WS.get(WS_LINEAR, x.device, 1)
             call("vt_mfma_linear_fwd", ptr(x2), R, K, ptr(w16), N, ptr(b), ptr(y), ptr(ws), ws.numel(), _st())
@@ -256,6 +282,7 @@ class LinearF(torch.autograd.Function):
     def backward(ctx, gy):
         x2, w16t = ctx.saved_tensors
         w, b = ctx.w, ctx.b
+        _h16(ctx.mfma)
         N, K = w.shape
         R = x2.shape[0]
         gy2 = gy.reshape(R, N).contiguous()
@@ -292,7 +319,8 @@ class LinearF(torch.autograd.Function):
                 # only: with bucketed all-reduce hooks the heads' bucket must be ready early)
                 cs = torch.cuda.current_stream()
 
-                def run(gy2=gy2, x2=x2, pg=pg, cs=cs, R=R, N=N, K=K, pre=pre):
+                def run(gy2=gy2, x2=x2, pg=pg, cs=cs, R=R, N=N, K=K, pre=pre, fmt=ctx.mfma):
+                    _h16(fmt)
                     with torch.cuda.stream(cs):
                         ws_d = WS.get(WS_LINEAR, gy2.device, 1)
                         call(pre + "linear_bwd_weight", ptr(gy2), R, N, ptr(x2), K, ptr(pg.out[0]), ptr(pg.out[1]),
@@ -458,7 +486,8 @@ class ResMLPF(torch.autograd.Function):
         d0, DL = spec.dims_l[0], spec.dims_l[-1]
         x2 = x.reshape(-1, d0).contiguous()
         R = x2.shape[0]
-        n_xh, n_rs, _ = spec.sizes(R, bf16)
+        n_xh, n_rs, _ = spec.sizes(R, bool(bf16))
+        _h16(bf16)
         out = torch.empty((R, DL), device=x.device)
         xh = torch.empty(n_xh, device=x.device)
         rs = torch.empty(n_rs, device=x.device)
@@ -473,6 +502,7 @@ class ResMLPF(torch.autograd.Function):
     def backward(ctx, gout):
         xh, rs = ctx.saved_tensors
         spec, params, R, bf16 = ctx.spec, ctx.params, ctx.R, ctx.bf16
+        _h16(bf16)
         d0, DL = spec.dims_l[0], spec.dims_l[-1]
         g2 = gout.reshape(R, DL).contiguous()
         present = [i for i, p in enumerate(params) if p is not None]
@@ -483,7 +513,7 @@ class ResMLPF(torch.autograd.Function):
             grads[i] = gt
         dx = torch.empty((R, d0), device=xh.device)
         pp = spec.param_ptrs if spec.param_ptrs is not None else spec.pointers(params)
-        split = bf16 and MLPB_SPLIT and spec.split_sizes(R)[3]
+        split = bf16 == "bf16" and MLPB_SPLIT and spec.split_sizes(R)[3]   # (no fp16 form of the split)
         if split:
             # the data-gradient chain here; the weight gradients from the saved dZ rows on the
             # weight-gradient side stream when they are written in place (off the critical chain)
@@ -507,7 +537,7 @@ class ResMLPF(torch.autograd.Function):
                 call("vt_resmlp_bf16_bwd_weight", spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp,
                      ptr(xh), ptr(dz16), R, gp, pg.acc, ptr(wsw), wsw.numel(), _st())
         else:
-            ws_floats = spec.sizes(R, bf16)[2]
+            ws_floats = spec.sizes(R, bool(bf16))[2]
             ws = WS.get(ws_floats, xh.device, 5)
             call("vt_resmlp_bf16_bwd" if bf16 else "vt_resmlp_bwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip,
                  spec.eps, pp, ptr(g2), ptr(xh), ptr(rs), R, ptr(dx), spec.grad_pointers(grads), pg.acc, ptr(ws),
@@ -520,7 +550,7 @@ class ResMLPF(torch.autograd.Function):
 
 
 def resmlp(x, spec, params, bf16=False):
-    return ResMLPF.apply(x, spec, bool(bf16), *params)
+    return ResMLPF.apply(x, spec, h16_flag(bf16), *params)
 
 
 # -------------------------------------------------------- LayerNorm + act
@@ -562,17 +592,19 @@ _CONV_SHADOW = {}
 
 
 def _conv_shadow(w, prepass=False):
-    """bf16 shadows of a conv weight W [Cout][Cin][K] (vt_conv1d_bf16_shadow):
-    w16 [Cout][K][ceil32(Cin)] and the transposed / flipped w16t
-    [Cin][K][ceil32(Cout)], rewritten from W on every forward."""
+    """16-bit shadows (the current format) of a conv weight W [Cout][Cin][K]
+    (vt_conv1d_bf16_shadow): w16 [Cout][K][ceil32(Cin)] and the transposed / flipped w16t
+    [Cin][K][ceil32(Cout)], rewritten from W on every forward (unless fresh / prepared)."""
     Cout, Cin, K = w.shape
     key = (w.data_ptr(), Cout, Cin, K)
     sh = _CONV_SHADOW.get(key)
-    if sh is None:
+    dt = _shadow_dtype()
+    if sh is None or sh[0].dtype != dt:
         up32 = lambda n: (n + 31) // 32 * 32
-        sh = (torch.empty(Cout * K * up32(Cin), dtype=torch.bfloat16, device=w.device),
-              torch.empty(Cin * K * up32(Cout), dtype=torch.bfloat16, device=w.device))
+        sh = (torch.empty(Cout * K * up32(Cin), dtype=dt, device=w.device),
+              torch.empty(Cin * K * up32(Cout), dtype=dt, device=w.device))
         _CONV_SHADOW[key] = sh
+        _FRESH.pop(key, None)
     if prepass or not (_take_prepared(key) or _fresh(key, w)):
         call("vt_conv1d_bf16_shadow", ptr(w), Cout, Cin, K, ptr(sh[0]), ptr(sh[1]), _st())
     return sh
@@ -603,8 +635,9 @@ class ConvBNActF(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, g, b, run_mean, run_var, mode, up, act, momentum, eps, bf16=False, xin=None, vout=False):
         _check(x, w, g, b)
-        if (xin is not None or vout) and not bf16:
-            raise ValueError("the conv-stack BatchNorm fold needs the bf16 conv kernels")
+        if (xin is not None or vout) and bf16 != "bf16":
+            raise ValueError("the conv-stack BatchNorm fold needs the bf16 conv kernels (no fp32 / fp16 form)")
+        _h16(bf16)
         B, L, Cin = x.shape
         Cout, _, K = w.shape
         x = x.contiguous()
@@ -645,6 +678,7 @@ class ConvBNActF(torch.autograd.Function):
             gy = torch.zeros_like(conv)
         w, g, b = ctx.params
         mode, up, act, bf16 = ctx.cfg
+        _h16(bf16)
         # the input is the previous block's pre-BN output: its BatchNorm + act in the weight
         # gradient's staging (the backward-data output below is dL/d(that block's y), as always)
         inb = (*(ptr(t) for t in xin), ctx.in_act) if xin else None
@@ -668,7 +702,7 @@ class ConvBNActF(torch.autograd.Function):
             call("vt_batchnorm_bwd_coef", ptr(gy), ptr(conv), M, Cout, ptr(mean), ptr(rstd), ptr(g), ptr(b),
                  ACT[act], ptr(pbn.out[0]), ptr(pbn.out[1]), pbn.acc, ptr(bnp), ptr(ws), ws.numel(), _st())
             c32 = (Cout + 31) // 32 * 32
-            dxbn = torch.empty(M * c32, dtype=torch.bfloat16, device=x.device)
+            dxbn = torch.empty(M * c32, dtype=_shadow_dtype(), device=x.device)
             call("vt_batchnorm_bwd_x16", ptr(gy), ptr(conv), ptr(bnp), ACT[act], M, Cout, ptr(dxbn), _st())
             srcs = (dxbn,)
             dw_args = lambda wsx: (ptr(dxbn), c32, ptr(x), B, L, Cin, Cout, K, mode, up, ptr(pw.out[0]), pw.acc,
@@ -769,6 +803,7 @@ class SyncConvBNActF(torch.autograd.Function):
         Lo = _lib.lib().fns["vt_conv1d_out_len"](L, K, mode, up)
         conv = torch.empty((B, Lo, Cout), device=x.device)
         if bf16:
+            _h16(bf16)
             w16, w16t = _conv_shadow(w)
             call("vt_conv1d_fwd_bf16", ptr(x), B, L, Cin, ptr(w16), Cout, K, mode, up, ptr(conv), _st())
         else:
@@ -798,6 +833,7 @@ class SyncConvBNActF(torch.autograd.Function):
         x, conv, mean, rstd, w16t = ctx.saved_tensors
         w, g, b = ctx.params
         mode, up, act, bf16, group = ctx.cfg
+        _h16(bf16)
         B, L, Cin = x.shape
         Cout, _, K = w.shape
         Lo = conv.shape[1]
@@ -836,8 +872,8 @@ class SyncConvBNActF(torch.autograd.Function):
 
 def sync_conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momentum=0.9, eps=1e-5, bf16=False,
                      group=None):
-    return SyncConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps, bool(bf16),
-                                group)
+    return SyncConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps,
+                                h16_flag(bf16), group)
 
 
 def conv_bn_eval(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", eps=1e-5, bf16=False):
@@ -852,6 +888,7 @@ def conv_bn_eval(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", eps=
     Lo = _lib.lib().fns["vt_conv1d_out_len"](L, K, mode, up)
     conv = torch.empty((B, Lo, Cout), device=x.device)
     if bf16:
+        _h16(h16_flag(bf16))
         w16, _ = _conv_shadow(w)
         call("vt_conv1d_fwd_bf16", ptr(x), B, L, Cin, ptr(w16), Cout, K, mode, up, ptr(conv), _st())
     else:
@@ -1182,7 +1219,7 @@ def conv_bn_act(x, w, g, b, run_mean, run_var, mode, up=False, act="relu", momen
                 xin=None, vout=False):
     """xin / vout: the conv-stack BatchNorm fold (ConvBNActF); vout returns (pre-BN output, its
     BatchNorm as the next block's xin)."""
-    out = ConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps, bool(bf16), xin,
+    out = ConvBNActF.apply(x, w, g, b, run_mean, run_var, int(mode), int(up), act, momentum, eps, h16_flag(bf16), xin,
                            bool(vout))
     if not vout:
         return out

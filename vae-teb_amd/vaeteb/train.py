@@ -381,14 +381,21 @@ class Trainer:
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=1e-4, max_norm=1.0, beta_kld=1e-5,
                  frontend=None, world_size=1, group=None, bucket_mb=64.0, vae_loss_weight=0.1,
-                 reduce_dtype=torch.float32, ddp=None, broadcast_buffers=True):
+                 reduce_dtype=torch.float32, ddp=None, broadcast_buffers=True, loss_scale=None, init_scale=2.0 ** 16,
+                 growth_factor=2.0, backoff_factor=0.5, growth_interval=2000):
         """ddp: the bucketed gradient all-reduce (GradBuckets) on (True) / off (False);
         default on exactly when world_size > 1.  ddp=True with one rank (an initialised
         single-rank process group) runs the data-parallel step's whole machinery — buckets,
         the world > 1 stream budget, the segmented native replay — at N = 1 (bench.py
         --ddp-probe).  broadcast_buffers (DDP's flag, default True as in the reference):
         with several ranks, rank 0's BatchNorm running statistics are broadcast before every
-        step (BufferBroadcast)."""
+        step (BufferBroadcast).
+        loss_scale: torch.amp.GradScaler('cuda') around the step (ref/model/graph_model.py:670,
+        718-726) — the backward runs on loss * scale, the clip sees the unscaled norm, a step
+        whose gradients overflow (inf / NaN) is skipped and the scale backs off, growth_interval
+        clean steps double it; all on device state (self.scaler = {scale, growth tracker,
+        found_inf, skipped steps}), no host sync.  Default: on exactly when the model trains
+        fp16 operands (SeqVaeTeb.loss_scaling); bf16 keeps fp32's range and needs none."""
         self.model = model
         self.vae_loss_weight = vae_loss_weight
         self.frontend = frontend
@@ -398,7 +405,11 @@ class Trainer:
         self.world = world_size
         self.steps = 0
         dev = self.state.p.device
-        self.norm_out = torch.zeros(2, device=dev)
+        vae = getattr(model, "vae_model", model)
+        self.loss_scale = bool(getattr(vae, "loss_scaling", False)) if loss_scale is None else bool(loss_scale)
+        self.scaler_cfg = (float(growth_factor), float(backoff_factor), int(growth_interval))
+        self.scaler = torch.tensor([float(init_scale), 0.0, 0.0, 0.0], device=dev) if self.loss_scale else None
+        self.norm_out = torch.zeros(4, device=dev)   # pre-clip norm, AdamW gradient factor, found_inf
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)   # AdamW step counter (device side)
         self.adam_coef = torch.zeros(2, device=dev)
         self.graph = None
@@ -483,12 +494,14 @@ class Trainer:
         if self.buffer_sync is not None and not (self.state.p.is_cuda and torch.cuda.is_current_stream_capturing()):
             self.buffer_sync()   # DDP broadcast_buffers (under capture: CapturedStep.replay issues it)
         losses = self.loss(batch, eps)
+        # GradScaler.scale: the backward seeds carry the scale (device scalar, no sync)
+        root = losses["total_loss"] * self.scaler[0] if self.loss_scale else losses["total_loss"]
         if BWD_SAME_THREAD:
             # the backward on this thread instead of autograd's device worker thread
             with torch.autograd.set_multithreading_enabled(False):
-                losses["total_loss"].backward()
+                root.backward()
         else:
-            losses["total_loss"].backward()
+            root.backward()
         if torch.cuda.is_available():
             # gradients written in place on side streams (no AccumulateGrad, so
             # autograd does not join those streams for us)
@@ -510,7 +523,8 @@ class Trainer:
         shadows appear."""
         import ctypes
         from . import ops
-        sig = (len(ops._SHADOW), len(ops._CONV_SHADOW))
+        sig = (len(ops._SHADOW), len(ops._CONV_SHADOW), _lib._H16[0],
+               tuple(v[0].data_ptr() for v in list(ops._SHADOW.values())[:8]))
         if getattr(self, "_splan_sig", None) == sig:
             return self._splan
         heads, convs = [], []
@@ -545,8 +559,21 @@ class Trainer:
         self.steps += 1
         st = _lib.stream()
         s = self.state
-        _lib.call("vt_grad_norm_clip", s.g.data_ptr(), s.numel, 1.0 / self.world, float(self.max_norm),
-                  self.norm_out.data_ptr(), self.norm_ws.data_ptr(), st)
+        vae = getattr(self.model, "vae_model", self.model)
+        fmt = getattr(vae, "h16_format", None)
+        if fmt and s.p.is_cuda:
+            _lib.set_h16(fmt == "fp16")     # the shadows below are written in the model's format
+        skip = None
+        if self.loss_scale:
+            # GradScaler: unscale + inf check + clip coefficient + scale update in one finalise;
+            # an overflowing step is skipped on the device (skip = found_inf)
+            g, b, n = self.scaler_cfg
+            _lib.call("vt_grad_norm_clip_scaled", s.g.data_ptr(), s.numel, 1.0 / self.world, float(self.max_norm),
+                      self.norm_out.data_ptr(), self.norm_ws.data_ptr(), self.scaler.data_ptr(), g, b, n, st)
+            skip = self.norm_out.data_ptr() + 8
+        else:
+            _lib.call("vt_grad_norm_clip", s.g.data_ptr(), s.numel, 1.0 / self.world, float(self.max_norm),
+                      self.norm_out.data_ptr(), self.norm_ws.data_ptr(), st)
         if adam_stream is not None:
             _lib.wait_for(adam_stream, st)
             st = adam_stream.cuda_stream
@@ -554,20 +581,29 @@ class Trainer:
         plan = self._shadow_plan() if (SHADOW_UPDATE and s.p.is_cuda) else None
         ops._FRESH.clear()
         if plan is None:
-            _lib.call("vt_adamw_step_dev", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(), s.numel,
-                      float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
-                      self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4, st)
+            _lib.call("vt_adamw_step_dev_skip", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(),
+                      s.numel, float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps),
+                      float(self.wd), self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4,
+                      skip, st)
             return
         n_heads, n_convs, _, a, keys = plan
-        _lib.call("vt_adamw_step_dev_shadow", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(),
+        _lib.call("vt_adamw_step_dev_shadow_skip", s.p.data_ptr(), s.g.data_ptr(), s.m.data_ptr(), s.v.data_ptr(),
                   s.numel, float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps),
                   float(self.wd), self.step_dev.data_ptr(), self.adam_coef.data_ptr(), self.norm_out.data_ptr() + 4,
-                  n_heads, a["h_off"], a["h_N"], a["h_K"], a["h_w16"], a["h_w16t"], st)
+                  n_heads, a["h_off"], a["h_N"], a["h_K"], a["h_w16"], a["h_w16t"], skip, st)
         if n_convs:
             _lib.call("vt_conv1d_bf16_shadow_batch", n_convs, a["c_w"], a["c_co"], a["c_ci"], a["c_k"], a["c_w16"],
                       a["c_w16t"], st)
         for key, w in keys:
             ops.mark_fresh(key, w)           # the next forward uses these shadows as they are
+
+    def scaler_state(self):
+        """The dynamic loss scale (host copy, syncs): {scale, growth_tracker, found_inf (last step),
+        skipped_steps} — GradScaler.get_scale() / _growth_tracker; None without loss scaling."""
+        if not self.loss_scale:
+            return None
+        v = self.scaler.tolist()
+        return {"scale": v[0], "growth_tracker": int(v[1]), "found_inf": bool(v[2]), "skipped_steps": int(v[3])}
 
     # ------------------------------------------------------------ hipGraph
     def capture(self, batch, eps=None, warmup=2, pre_capture=None, native=False, n_streams=4, update=True):
