@@ -339,6 +339,21 @@ int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const
                        const float* const* params, const float* dout, const float* xhat, const float* rstd,
                        int64_t rows, float* dx, float* const* grads, int accumulate, float* ws, int64_t ws_floats,
                        void* stream);
+/* The forward's weight images (the 16-bit W / W^T images and staged LayerNorm parameters every
+ * launch of a stack copies into LDS, rebuilt from the fp32 master weights each step) for SEVERAL
+ * stacks in one launch (round 6): vt_resmlp_bf16_plan returns a stack's plan handle (its
+ * arguments as vt_resmlp_bf16_fwd; cached, valid for the library's lifetime),
+ * vt_resmlp_bf16_prep_batch builds the images of up to 32 plans in the current 16-bit format,
+ * and vt_resmlp_bf16_fwd_prepped is vt_resmlp_bf16_fwd without its own image pass (the caller
+ * prepared that plan's images after the weights last changed, same stream order).  The same
+ * images and results as vt_resmlp_bf16_fwd.  replaces: the per-Linear weight casts of autocast
+ * (ref/model/graph_model.py:709-711), once per step for the whole model.                      */
+int vt_resmlp_bf16_plan(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                        const float* const* params, int64_t rows, int64_t* handle, void* stream);
+int vt_resmlp_bf16_prep_batch(int n, const int64_t* handles, void* stream);
+int vt_resmlp_bf16_fwd_prepped(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                               float eps, const float* const* params, const float* x, int64_t rows, float* out,
+                               float* xhat, float* rstd, void* stream);
 /* The same backward split in two (round 5), so the weight gradients leave the data-gradient
  * chain (ref/model/vae_teb_model.py:336-403 backward, the reference's autograd of Linear /
  * LayerNorm under fp16 autocast):

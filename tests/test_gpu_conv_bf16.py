@@ -11,6 +11,8 @@ replicate decoder blocks with and without the x2 upsample):
     operands: rel-L2 <= 1e-5 (accumulation order only);
   * vs fp32: rel-L2 <= 1e-2 (bf16 has an 8-bit mantissa: ~3e-3 expected);
   * model: a full SeqVaeTeb step with bf16 convs stays within 1e-2 of fp32.
+The exact / rounded-model / weight-gradient cases also run with the fp16 operand format
+(round 6, csrc/h16.h: the same kernels instantiated for _Float16, the model rounding to fp16).
 """
 import pytest
 import torch
@@ -35,11 +37,21 @@ def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
 
+FMTS = ["bf16", "fp16"]
+DT = {"bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+def _fmt(L, fmt):
+    L.set_h16(fmt == "fp16")
+    return lambda t: t.to(DT[fmt]).float()
+
+
 def _shadow(L, w):
     Cout, Cin, K = w.shape
     up = lambda n: (n + 31) // 32 * 32
-    w16 = torch.empty(Cout * K * up(Cin), dtype=torch.bfloat16, device="cuda")
-    w16t = torch.empty(Cin * K * up(Cout), dtype=torch.bfloat16, device="cuda")
+    dt = torch.float16 if L.h16() == "fp16" else torch.bfloat16
+    w16 = torch.empty(Cout * K * up(Cin), dtype=dt, device="cuda")
+    w16t = torch.empty(Cin * K * up(Cout), dtype=dt, device="cuda")
     L.call("vt_conv1d_bf16_shadow", L.ptr(w), Cout, Cin, K, L.ptr(w16), L.ptr(w16t), L.stream())
     return w16, w16t
 
@@ -64,8 +76,10 @@ def _ints(shape, seed, lo=-3, hi=4):
     return torch.randint(lo, hi, shape, generator=g).float().cuda()
 
 
+@pytest.mark.parametrize("fmt", FMTS)
 @pytest.mark.parametrize("geo", GEOS)
-def test_conv_bf16_exact_integer(L, geo):
+def test_conv_bf16_exact_integer(L, geo, fmt):
+    _fmt(L, fmt)
     B, Lin, Cin, Cout, K, mode, up = geo
     Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
     # even integers keep the x2 upsample's 1/4, 3/4 weights exact in bf16
@@ -77,8 +91,10 @@ def test_conv_bf16_exact_integer(L, geo):
     assert torch.equal(g16, g32)
 
 
+@pytest.mark.parametrize("fmt", FMTS)
 @pytest.mark.parametrize("geo", GEOS)
-def test_conv_bf16_random(L, geo):
+def test_conv_bf16_random(L, geo, fmt):
+    rb = _fmt(L, fmt)
     B, Lin, Cin, Cout, K, mode, up = geo
     Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
     torch.manual_seed(sum(geo))
@@ -89,7 +105,6 @@ def test_conv_bf16_random(L, geo):
     assert _rel(y16, y32) < 1e-2 and _rel(g16, g32) < 1e-2
     # the bf16 model: fp32 kernels on bf16-rounded operands (the forward rounds
     # the upsampled / padded window values, so round x before a non-upsampling conv only)
-    rb = lambda t: t.bfloat16().float()
     if not up:
         y32b, _, _, _ = _run(L, rb(x), rb(w), mode, up, rb(dy))
         assert _rel(y16, y32b) < 1e-5
@@ -105,10 +120,12 @@ def _dw(L, fn, dy, x, mode, up, Cout, K):
     return dw
 
 
+@pytest.mark.parametrize("fmt", FMTS)
 @pytest.mark.parametrize("geo", GEOS)
-def test_conv_bf16_weight_grad(L, geo):
+def test_conv_bf16_weight_grad(L, geo, fmt):
     """dW on bf16 MFMA (transposed LDS reads): exact on small integers, bf16
     model 1e-5, vs fp32 1e-2."""
+    rb = _fmt(L, fmt)
     B, Lin, Cin, Cout, K, mode, up = geo
     Lo = L.lib().fns["vt_conv1d_out_len"](Lin, K, mode, up)
     x, dy = _ints((B, Lin, Cin), 4) * 4, _ints((B, Lo, Cout), 5)
@@ -119,7 +136,6 @@ def test_conv_bf16_weight_grad(L, geo):
     d16 = _dw(L, "vt_conv1d_bwd_weight_bf16", dy, x, mode, up, Cout, K)
     assert _rel(d16, _dw(L, "vt_conv1d_direct_bwd_weight", dy, x, mode, up, Cout, K)) < 1e-2
     if not up:
-        rb = lambda t: t.bfloat16().float()
         assert _rel(d16, _dw(L, "vt_conv1d_direct_bwd_weight", rb(dy), rb(x), mode, up, Cout, K)) < 1e-5
 
 

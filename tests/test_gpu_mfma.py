@@ -163,7 +163,7 @@ def test_model_bf16_heads_close_to_fp32(golden):
     out = {}
     for prec in ("fp32", "bf16"):
         m = det_fill_(SeqVaeTeb(sequence_length=16, head_precision=prec)).cuda()
-        assert all(l.mfma == (prec == "bf16") for l in m.decoder.output_mu.modules() if hasattr(l, "mfma"))
+        assert all(bool(l.mfma) == (prec == "bf16") for l in m.decoder.output_mu.modules() if hasattr(l, "mfma"))
         ins = [torch.from_numpy(g[k]).cuda() for k in ("y_st", "y_ph", "x_ph", "eps", "y_raw")]
         fo = m(*ins[:3], eps=ins[3])
         loss = m.compute_loss(fo, ins[0], ins[1], ins[4], beta=float(g["beta"]))["total_loss"]

@@ -388,6 +388,34 @@ def gen_amp():
     save("model_s256_b2_amp.npz", **d)
 
 
+def gen_amp_fp16_ens():
+    """The reference's fp16 spread at S = 256 / B = 2 as an ENSEMBLE (round 6: the fp16 step test,
+    tests/test_gpu_fp16.py): the Emu16 fp16 + GradScaler step of gen_amp run from initial weights
+    perturbed by one ulp (golden_util.perturb_ulp_, seeds 1-3) — each member's losses, forward
+    outputs and gradients compared with the UNPERTURBED fp32 step, as the trajectory ensembles
+    are (one 16-bit run is one sample of a spread whose scalar losses can land near fp32 by
+    chance)."""
+    from golden_util import perturb_ulp_
+    S, B = 256, 2
+    inputs = _amp_inputs(S, B)
+    fw32, l32, g32, _ = run_ref_step(build_ref_model(S), *inputs[:4], inputs[4], 1e-5)
+    names = list(g32.keys())
+    d = dict(S=S, B=B, param_names=np.array(names), seeds=np.array([1, 2, 3]))
+    for seed in (1, 2, 3):
+        t = time.time()
+        fw, losses, grads = run_ref_step_amp(perturb_ulp_(build_ref_model(S), seed), inputs, 1e-5, "emu_fp16")
+        tag = f"emu_fp16_p{seed}"
+        for k in ("mse_loss", "nll_loss", "kld_loss", "total_loss"):
+            d[f"{tag}_loss_{k}"] = losses[k].item()
+        for k, v in fw.items():
+            d[f"{tag}_fwrel_{k}"] = ((v - fw32[k]).norm() / fw32[k].norm()).item()
+        d[f"{tag}_grad_rel"] = np.array([((grads[k] - g32[k]).norm() / g32[k].norm().clamp_min(1e-30)).item()
+                                         for k in names])
+        print(f"fp16 ens {seed}: {time.time() - t:.1f}s kld {losses['kld_loss'].item():.6f} "
+              f"(fp32 {l32['kld_loss'].item():.6f})", flush=True)
+    save("model_s256_b2_fp16ens.npz", **d)
+
+
 TRAJ_STEPS = 20
 
 
@@ -734,11 +762,14 @@ def gen_classifier_amp():
     labels = np.array([1, 0, 0, 1], dtype=np.int64)
     T = torch.from_numpy
 
-    def run(mode, scale16=65536.0):
+    def run(mode, scale16=65536.0, perturb=None):
         m = V.SeqVaeTebClassifier(sequence_length=S, freeze_vae=False, classifier_dropout=0.0)
         m.vae_model = build_ref_model(S)
         _crop_conv_long_(m.classifier)
         det_fill_(m.classifier)
+        if perturb is not None:   # a one-ulp perturbed member of the 16-bit ensemble
+            from golden_util import perturb_ulp_
+            perturb_ulp_(m, perturb)
         m.train()
         m.vae_model.reparameterize = lambda mu, lv: mu + T(eps) * torch.exp(0.5 * lv)
         scale = 1.0
@@ -763,9 +794,16 @@ def gen_classifier_amp():
     d = dict(B=B, S=S, param_names=np.array(names), logits_fp32=o32["logits"].detach().float().numpy())
     for k in ("classification_loss", "vae_loss", "total_loss"):
         d[f"fp32_{k}"] = o32[k].item()
-    for mode in ("cpu_bf16", "emu_bf16", "emu_fp16"):
+    # the 16-bit modes, then bf16 members from one-ulp perturbed weights (round 6: a chaotic scalar
+    # gradient — the last decoder block's BatchNorm over 1024 rows — moves by 10-40 % between
+    # 16-bit runs, so three single runs under-sample the spread; the deviations stay measured
+    # from the UNPERTURBED fp32 step, as the trajectory ensembles)
+    for mode in ("cpu_bf16", "emu_bf16", "emu_fp16", "emu_bf16_p1", "emu_bf16_p2", "emu_bf16_p3"):
         t = time.time()
-        o, g, _ = run(mode)
+        base, pseed = (mode[:-3], int(mode[-1])) if "_p" in mode else (mode, None)
+        o, g, _ = run(base, perturb=pseed)
+        mode_ = mode
+        mode = base
         scale16 = 65536.0
         while mode == "emu_fp16" and not all(torch.isfinite(x).all() for x in g) and scale16 > 1:
             # GradScaler: a step with inf / NaN gradients is skipped and the scale halved; the
@@ -774,6 +812,7 @@ def gen_classifier_amp():
             o, g, _ = run(mode, scale16)
         if mode == "emu_fp16":
             d["emu_fp16_scale"] = scale16
+        mode = mode_
         for k in ("classification_loss", "vae_loss", "total_loss"):
             d[f"{mode}_{k}"] = o[k].float().item()
         lg = o["logits"].detach().float()
@@ -786,7 +825,7 @@ def gen_classifier_amp():
 
 
 GENS = dict(kat=gen_kymatio_kat, filters=gen_filters, scattering=gen_scattering, frontend=gen_frontend,
-            stats=gen_stats_and_norm, model=gen_model, amp=gen_amp, te=gen_te, tiny=gen_tiny,
+            stats=gen_stats_and_norm, model=gen_model, amp=gen_amp, amp_fp16_ens=gen_amp_fp16_ens, te=gen_te, tiny=gen_tiny,
             classifier=gen_classifier, classifier_amp=gen_classifier_amp, traj=gen_traj, traj_lowlr=gen_traj_lowlr, model_big=lambda: gen_model((256, 300)))
 
 if __name__ == "__main__":

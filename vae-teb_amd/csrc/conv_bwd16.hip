@@ -36,8 +36,8 @@ namespace {
 
 
 constexpr int RS = 40;   // bf16 row stride of the staged window / tap rows (as conv_bf16.hip)
-// rows per k_bn_bwd_x16 block: 64, or 256 (VAETEB_BNX16_ROWS; every element's value is computed
-// the same way for any block height: the same bits)
+// rows per k_bn_bwd_x16 block (XRB): 64, or 256 for C <= 4 (vt_batchnorm_bwd_x16; every element's
+// value is computed the same way for any block height: the same bits)
 
 // ------------------------------------------------------------------ 1. BN backward -> bf16
 template <typename H, int ACT, int XRB = 64>
@@ -385,7 +385,11 @@ int vt_batchnorm_bwd_x16(const float* dY, const float* Xc, const float* bnp, int
     VT_CHECK_ARG(dY && Xc && bnp && d16 && M > 0 && C > 0 && C <= 1024 && act >= 0 && act <= 3,
                  "vt_batchnorm_bwd_x16: arguments");
     const int c32 = cdiv(C, 32) * 32;
-    static const int xrb = getenv("VAETEB_BNX16_ROWS") && atoi(getenv("VAETEB_BNX16_ROWS")) == 256 ? 256 : 64;
+    // rows per block: 256 for the narrowest layers (C <= 4: one 64-row block is only 1 KB per
+    // stream; measured C = 1, M = 1 M: 19.9 -> 15.1 us), 64 otherwise (C = 32: 5.4 vs 9.4 us);
+    // VAETEB_BNX16_ROWS = 64 / 256 forces one (tools/bn_micro.py; the same bits either way)
+    static const int xrb_env = getenv("VAETEB_BNX16_ROWS") ? atoi(getenv("VAETEB_BNX16_ROWS")) : 0;
+    const int xrb = xrb_env == 256 || xrb_env == 64 ? xrb_env : (C <= 4 ? 256 : 64);
     const size_t lds = (size_t)8 * ((C + 3) & ~3) * 4 + (size_t)xrb * c32 * 2;
     VT_CHECK_ARG(lds <= 160 * 1024, "vt_batchnorm_bwd_x16: C too large");
     // at most 8 workgroups per CU of 64-row blocks, each walking several blocks: the per-workgroup

@@ -28,6 +28,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -372,9 +373,7 @@ __device__ __forceinline__ void ln_fwd(f32x4 (&z)[NT], int C, const float* gl, c
 // VGPR round trip), instead of every workgroup re-gathering and converting the
 // fp32 weights (18 us of a 92 us backward workgroup, tools/mlpb_phases.py).
 template <typename H>
-__global__ __launch_bounds__(256) void k_mlpb_prep(const BDesc* __restrict__ dp) {
-    const BDesc& d = *dp;
-    const int seg = blockIdx.y, e = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void mlpb_prep_seg(const BDesc& d, int seg, int e) {
     H* fimg = reinterpret_cast<H*>(d.gimg);
     float* fprm = reinterpret_cast<float*>(d.gimg + d.fimg);
     H* bimg = reinterpret_cast<H*>(d.gimg + d.gbo);
@@ -418,6 +417,32 @@ __global__ __launch_bounds__(256) void k_mlpb_prep(const BDesc* __restrict__ dp)
         const int Np = p16(d.G[l].N), c = e - d.l[l].bpo, w = c >= Np, f = c - w * Np;
         bprm[e] = f < d.G[l].N ? (w == 0 ? d.l[l].g : d.l[l].be)[f] : 0.f;
     }
+}
+
+template <typename H>
+__global__ __launch_bounds__(256) void k_mlpb_prep(const BDesc* __restrict__ dp) {
+    mlpb_prep_seg<H>(*dp, blockIdx.y, blockIdx.x * 256 + threadIdx.x);
+}
+
+// Every stack of a model in ONE launch (round 6, VERDICT r05 item 5: the 14 k_mlpb_prep launches of
+// a step were each ~6.7 us of latency on the forward's chain): blockIdx.y walks the stacks' segment
+// ranges (prefix y0), each block then does k_mlpb_prep's work for its (stack, segment) — the same
+// element mapping, the same images.
+constexpr int PREP_BATCH = 32;
+struct PrepBatch {
+    int n;
+    const BDesc* d[PREP_BATCH];
+    int y0[PREP_BATCH + 1];
+    int x[PREP_BATCH];
+};
+template <typename H>
+__device__ __forceinline__ void mlpb_prep_seg(const BDesc& d, int seg, int e);
+template <typename H>
+__global__ __launch_bounds__(256) void k_mlpb_prep_batch(PrepBatch pb) {
+    int s = 0;
+    while (s + 1 < pb.n && (int)blockIdx.y >= pb.y0[s + 1]) ++s;
+    if ((int)blockIdx.x >= pb.x[s]) return;
+    mlpb_prep_seg<H>(*pb.d[s], (int)blockIdx.y - pb.y0[s], blockIdx.x * 256 + threadIdx.x);
 }
 
 // bytes [0, nbytes) of global src -> LDS dst (16-B aligned, nbytes a multiple of 16)
@@ -1605,19 +1630,59 @@ int vt_resmlp_bf16_sizes(int n_layers, const int* dims, const int* layer_ln, con
     return VT_OK;
 }
 
-int vt_resmlp_bf16_fwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
-                       const float* const* params, const float* x, int64_t rows, float* out, float* xhat, float* rstd,
-                       void* stream) {
-    hipStream_t st = S(stream);
+int vt_resmlp_bf16_plan(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                        const float* const* params, int64_t rows, int64_t* handle, void* stream) {
     const BPlan* pp;
     const BDesc* ddev;
-    const int rc = get_plan(pp, ddev, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, st,
-                            "vt_resmlp_bf16_fwd");
+    const int rc = get_plan(pp, ddev, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, S(stream),
+                            "vt_resmlp_bf16_plan");
+    if (rc) return rc;
+    VT_CHECK_ARG(handle, "vt_resmlp_bf16_plan: null handle");
+    // a stable copy per cached plan (the plan cache's vectors may move their entries); the image
+    // buffer it points at is the plan's own
+    static std::unordered_map<const BPlan*, std::unique_ptr<BPlan>> handles;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& h = handles[pp];
+    if (!h) h.reset(new BPlan(*pp));
+    *handle = reinterpret_cast<int64_t>(h.get());
+    return VT_OK;
+}
+
+int vt_resmlp_bf16_prep_batch(int n, const int64_t* handles, void* stream) {
+    VT_CHECK_ARG(n >= 1 && n <= PREP_BATCH && handles, "vt_resmlp_bf16_prep_batch: 1..%d plans", PREP_BATCH);
+    PrepBatch pb{};
+    pb.n = n;
+    int xmax = 0;
+    for (int i = 0; i < n; ++i) {
+        const BPlan* p = reinterpret_cast<const BPlan*>(handles[i]);
+        VT_CHECK_ARG(p && p->d.gimg, "vt_resmlp_bf16_prep_batch: plan %d", i);
+        pb.d[i] = device_desc(p->d, S(stream));
+        VT_CHECK_ARG(pb.d[i], "vt_resmlp_bf16_prep_batch: descriptor upload failed");
+        pb.y0[i + 1] = pb.y0[i] + p->prep_y;
+        pb.x[i] = p->prep_x;
+        xmax = p->prep_x > xmax ? p->prep_x : xmax;
+    }
+    VT_H16(hipLaunchKernelGGL(k_mlpb_prep_batch<H>, dim3((unsigned)xmax, (unsigned)pb.y0[n]), dim3(256), 0, S(stream),
+                              pb));
+    VT_LAUNCH_CHECK("vt_resmlp_bf16_prep_batch");
+    return VT_OK;
+}
+
+static int resmlp_fwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                      const float* const* params, const float* x, int64_t rows, float* out, float* xhat, float* rstd,
+                      hipStream_t st, bool prep, const char* who) {
+    const BPlan* pp;
+    const BDesc* ddev;
+    const int rc = get_plan(pp, ddev, n_layers, dims, layer_ln, layer_act, skip, eps, params, rows, st, who);
     if (rc) return rc;
     const BPlan& p = *pp;
-    VT_CHECK_ARG(x && out && xhat && rstd, "vt_resmlp_bf16_fwd: null buffer");
-    // the weight images of this step (read again by the backward of this forward)
-    VT_H16(hipLaunchKernelGGL(k_mlpb_prep<H>, dim3((unsigned)p.prep_x, (unsigned)p.prep_y), dim3(256), 0, st, ddev));
+    VT_CHECK_ARG(x && out && xhat && rstd, "%s: null buffer", who);
+    // the weight images of this step (read again by the backward of this forward); prepared already
+    // (vt_resmlp_bf16_prep_batch, in the current format) when prep is false
+    if (prep)
+        VT_H16(hipLaunchKernelGGL(k_mlpb_prep<H>, dim3((unsigned)p.prep_x, (unsigned)p.prep_y), dim3(256), 0, st,
+                                  ddev));
     const dim3 grid((unsigned)n_fwd_blocks(rows));
     const bool id = skip == 1;
     switch (p.nt * 2 + (id ? 1 : 0)) {
@@ -1631,8 +1696,22 @@ int vt_resmlp_bf16_fwd(int n_layers, const int* dims, const int* layer_ln, const
         default: VT_MBF(9, 1)
 #undef VT_MBF
     }
-    VT_LAUNCH_CHECK("vt_resmlp_bf16_fwd");
+    VT_LAUNCH_CHECK(who);
     return VT_OK;
+}
+
+int vt_resmlp_bf16_fwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,
+                       const float* const* params, const float* x, int64_t rows, float* out, float* xhat, float* rstd,
+                       void* stream) {
+    return resmlp_fwd(n_layers, dims, layer_ln, layer_act, skip, eps, params, x, rows, out, xhat, rstd, S(stream), true,
+                      "vt_resmlp_bf16_fwd");
+}
+
+int vt_resmlp_bf16_fwd_prepped(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip,
+                               float eps, const float* const* params, const float* x, int64_t rows, float* out,
+                               float* xhat, float* rstd, void* stream) {
+    return resmlp_fwd(n_layers, dims, layer_ln, layer_act, skip, eps, params, x, rows, out, xhat, rstd, S(stream),
+                      false, "vt_resmlp_bf16_fwd_prepped");
 }
 
 int vt_resmlp_bf16_bwd(int n_layers, const int* dims, const int* layer_ln, const int* layer_act, int skip, float eps,

@@ -667,12 +667,26 @@ class SeqVaeTeb(nn.Module):
             ops._PREPARED.clear()   # no stale shadow events outlive the forward they were made for
             if self.training:
                 self._count_bn()
+        if ops.MLP_PREP_BATCH and x_ph.is_cuda:
+            self._mlp_prep(y_st.shape[0] * y_st.shape[1])
         try:
             return self._forward(y_st, y_ph, x_ph, eps)
         finally:
             _PAR.update(prev)
             for bn in getattr(self, "_bn_list", ()):
                 bn._vt_batched = False   # counted by this forward's prepass only
+
+    def _mlp_prep(self, rows):
+        """The 16-bit weight images of every fused 16-bit ResidualMLP stack of this model (all run on
+        the B*S rows) in one launch at the start of the forward (ops.mlp_prep_batch): each stack's
+        forward then skips its own image pass.  Same images, same bits."""
+        key = (self.mlp_precision, rows)
+        if getattr(self, "_mlp_prep_key", None) != key:   # the module walk once per setting
+            self._mlp_prep_key = key
+            self._mlp_prep_mods = [m for m in self.modules() if isinstance(m, ResidualMLP) and m.bf16 and m.fused]
+        stacks = [fs for fs in (m._fused_spec() for m in self._mlp_prep_mods) if fs is not None]
+        ops._MLP_PREPPED.clear()   # images of an earlier forward that never ran are stale
+        ops.mlp_prep_batch(stacks, rows)
 
     def _bn_counters(self):
         """The num_batches_tracked buffers of every BatchNorm as views of one int64

@@ -461,6 +461,40 @@ class MlpSpec:
         import ctypes
         return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
 
+    def plan_handle(self, rows, params):
+        """The library's cached plan of this stack at `rows` rows (vt_resmlp_bf16_plan), for the
+        batched image pass; keyed by the parameter addresses (a moved parameter is a new plan)."""
+        pp = self.param_ptrs if self.param_ptrs is not None else self.pointers(params)
+        key = (rows, tuple(pp))
+        h = getattr(self, "_handles", {}).get(key)
+        if h is None:
+            import ctypes
+            hv = ctypes.c_int64()
+            call("vt_resmlp_bf16_plan", self.L, self.dims, self.ln, self.act, self.skip, self.eps, pp, rows,
+                 ctypes.byref(hv), _st())
+            self.__dict__.setdefault("_handles", {})[key] = h = hv.value
+        return h
+
+
+# plans whose 16-bit weight images the model's batched pass (mlp_prep_batch) prepared for the coming
+# forward: each such forward skips its own image pass once (vt_resmlp_bf16_fwd_prepped)
+_MLP_PREPPED = set()
+MLP_PREP_BATCH = int(os.environ.get("VAETEB_MLP_PREP_BATCH", "1"))
+
+
+def mlp_prep_batch(stacks, rows):
+    """One launch building the 16-bit weight images of every (spec, params) stack at `rows` rows
+    (vt_resmlp_bf16_prep_batch) in the current format — the per-stack image passes of the step's
+    16-bit ResidualMLP forwards (14 launches of ~7 us each on the forward chain) become one."""
+    if not stacks:
+        return
+    import ctypes
+    hs = [spec.plan_handle(rows, params) for spec, params in stacks]
+    for i in range(0, len(hs), 32):
+        chunk = hs[i:i + 32]
+        call("vt_resmlp_bf16_prep_batch", len(chunk), (ctypes.c_int64 * len(chunk))(*chunk), _st())
+    _MLP_PREPPED.update(hs)
+
     def grad_pointers(self, ts):
         """Pointer array of the gradient destinations, reused while they stay put
         (the trainer's in-place gradient sinks)."""
@@ -492,8 +526,16 @@ class ResMLPF(torch.autograd.Function):
         xh = torch.empty(n_xh, device=x.device)
         rs = torch.empty(n_rs, device=x.device)
         pp = spec.param_ptrs if spec.param_ptrs is not None else spec.pointers(params)
-        call("vt_resmlp_bf16_fwd" if bf16 else "vt_resmlp_fwd", spec.L, spec.dims, spec.ln, spec.act, spec.skip,
-             spec.eps, pp, ptr(x2), R, ptr(out), ptr(xh), ptr(rs), _st())
+        fn = "vt_resmlp_fwd"
+        if bf16:
+            fn = "vt_resmlp_bf16_fwd"
+            if _MLP_PREPPED:
+                h = spec.plan_handle(R, params)
+                if h in _MLP_PREPPED:          # images prepared by this step's batched pass
+                    _MLP_PREPPED.discard(h)
+                    fn = "vt_resmlp_bf16_fwd_prepped"
+        call(fn, spec.L, spec.dims, spec.ln, spec.act, spec.skip, spec.eps, pp, ptr(x2), R, ptr(out), ptr(xh),
+             ptr(rs), _st())
         ctx.save_for_backward(xh, rs)
         ctx.spec, ctx.params, ctx.shape, ctx.R, ctx.bf16 = spec, params, x.shape, R, bf16
         return out.reshape(*x.shape[:-1], DL)
