@@ -117,6 +117,8 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
  * default: measured faster in the step); returns the previous grid (same bits either way) */
 int vt_fe_set_pairs_persist(int grid);
 int vt_fe_set_pairs_direct(int on);
+/* half-image pair kernel (default 1; 0: the full-image form); returns the previous setting */
+int vt_fe_set_pairs_half(int on);
 /* Storage form of the analytic slots on the 8192-point geometry (n_pad 8192,
  * pad_left + N <= 8192), shared by vt_fe_wavelet (writes) and vt_fe_pairs (reads):
  * 1 = polar {arg(a) / 2 pi, |a|} (the pair product becomes |a_i| |a_j|

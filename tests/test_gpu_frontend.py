@@ -290,6 +290,7 @@ def test_pairs_persistent_kernel_bitwise(fe11, B):
     fns = _lib.lib().fns
     x = torch.from_numpy(synthetic.batch(5150, B, 4096)).cuda()
     prev = fns["vt_fe_set_pairs_persist"](0)
+    prev_half = fns["vt_fe_set_pairs_half"](0)     # the full-image kernel the persistent form mirrors
     try:
         ref = fe11.raw(x)["pairs"].clone()
         fns["vt_fe_set_pairs_persist"](-1)
@@ -298,5 +299,45 @@ def test_pairs_persistent_kernel_bitwise(fe11, B):
         got_small = fe11.raw(x)["pairs"].clone()
     finally:
         fns["vt_fe_set_pairs_persist"](prev)
+        fns["vt_fe_set_pairs_half"](prev_half)
     torch.cuda.synchronize()
     assert torch.equal(got, ref) and torch.equal(got_small, ref)
+
+
+@pytest.mark.parametrize("B", [4, 8])
+def test_pairs_full_image_kernel_vs_oracle(fe11, B):
+    """The full-image pair kernel (k_fe_pairs8k, vt_fe_set_pairs_half(0), the default of rounds
+    2-5) held to the fp64 oracle as the default half-image kernel is in
+    test_pairs_random_inputs_vs_oracle; the two forms agree to fp32 rounding (other DFT-16
+    factorisation and summation order: 1e-5 of the batch's largest coefficient, not bitwise)."""
+    from vaeteb import _lib, synthetic
+    fns = _lib.lib().fns
+    x = synthetic.batch(903, B, 4096)
+    xt = torch.from_numpy(x).cuda()
+    half = fe11.raw(xt)["pairs"].clone()
+    prev = fns["vt_fe_set_pairs_half"](0)
+    try:
+        full = fe11.raw(xt)["pairs"].clone()
+    finally:
+        fns["vt_fe_set_pairs_half"](prev)
+    torch.cuda.synchronize()
+    diff = (half - full).abs().max().item()
+    assert diff <= 1e-5 * full.abs().max().item(), diff
+    p = fe11.plan
+    o64 = F.PhaseFrontEnd(11, 4, 16, 4096, dtype=np.float64)
+    o32 = F.PhaseFrontEnd(11, 4, 16, 4096)
+    a64 = o64.analytic(x[:, [0, 1]])
+    nph = fe11.C_ph
+    out_all = full.cpu().numpy()
+    for sel, cross in ((p.phase_mask, False), (p.cross_mask, True)):
+        r32 = torch_engine(o32.forward, x, compute_phase=not cross, compute_cross_phase=cross, pair_subset=sel)
+        r64 = o64.forward(x, compute_phase=not cross, compute_cross_phase=cross, pair_subset=sel)
+        k = "cross_phase_corr" if cross else "phase_corr"
+        out = out_all[:, nph:] if cross else out_all[:, :nph]
+        ii, jj = o64.i_idx[sel], o64.j_idx[sel]
+        aj = a64[:, 1] if cross else a64[:, 0]
+        scale = np.sqrt((o64._lowpass(np.abs(a64[:, 0][:, ii]) * np.abs(aj[:, jj]) + 0j, 256) ** 2).sum(-1))
+        err = np.sqrt(((out - r64[k]) ** 2).sum(-1)) / scale
+        ref_err = np.sqrt(((r32[k] - r64[k]) ** 2).sum(-1)) / scale
+        assert err.max() <= 2 * ref_err.max() + 1e-5, (k, err.max(), ref_err.max())
+        assert np.median(err) <= 2 * np.median(ref_err) + 1e-6, (k, np.median(err), np.median(ref_err))

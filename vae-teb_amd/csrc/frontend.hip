@@ -605,6 +605,182 @@ __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     }
 }
 
+// ------------------------------------------- pairs, half-image form (round 6)
+// The same pruned 8192-point transform through HALF the LDS image, so that three 8-wave
+// workgroups share a CU (6 waves per SIMD instead of 4: k_fe_pairs8k is issue / latency
+// bound at two workgroups per CU, 0.46 of its wave cycles in issue stalls).
+//   pass 1  the radix-16 over n2 begins with its radix-2 step: s[n] = v[n] + v[n + 8]
+//           feeds the even blocks k2 = 2m, d[n] = (v[n] - v[n + 8]) W_16^n the odd ones
+//           (a DFT-8 each).  Passes 2 and 3 never mix blocks, so the 8 blocks of one
+//           parity run through ONE 8-block image (34 KB, which first holds the staged
+//           product) while the other parity's d[] waits in registers.
+//   pass 2  each radix-16 job (block, n1a) split over two waves by output parity (the
+//           same radix-2 step, then a DFT-8); the pair reads before a barrier, writes after.
+//   pass 3  each (block, k'b) row summed by four lanes, 8 terms each, both outputs
+//           k'a = 0, 1 at once, the partials combined by DPP.
+// Another DFT-16 factorisation and summation order than k_fe_pairs8k (other rounding);
+// held to the same fp64 oracle (kymatio_phase_scattering.py:211-218, :233-273, :275-360).
+static constexpr int PRH_IMG = 8 * 528;                           // one parity's 8 blocks, 33-padded
+static constexpr int PRH_BUF = PRH_IMG > 4096 ? PRH_IMG : 4096;  // ... aliasing the staged product
+static constexpr int PRH_LDS = (PRH_BUF + PR_ZP) * (int)sizeof(float2);
+
+__device__ __forceinline__ c2 w16c(int n) { return w32(2 * n); }  // W_16^n (n a compile-time constant)
+
+// quad butterflies by DPP: lane l receives lane l ^ 1 / l ^ 2 of its quad
+__device__ __forceinline__ float qx1(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float qx2(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+}
+
+// reflect-padded source index of column n1 = t, row n2 (training geometry: one reflection)
+__device__ __forceinline__ int prh_src(int t, int n2) {
+    const int i = t + 512 * n2 - 2048;
+    return n2 < 4 ? -i : (n2 < 12 ? i : 2 * 4096 - 2 - i);
+}
+
+// blocks k2 = 2m + H (m < 8) from y (pass 1's DFT-8 input of that parity) to their 512 outputs
+// X[k2 + 16 k'b + 256 k'a] (k'a < 2) in Z (conj(X phi), as k_fe_pairs8k); w[m] = W_8192^{t k2}
+// (w[0] unused for H = 0).  Enters with img free, leaves with pass 3's reads of img possibly
+// still in flight in other waves (the caller's barrier).
+template <int H>
+__device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], const c2 (&w)[8],
+                                           const float2* __restrict__ tab, float ph) {
+    const int t = threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    pdft8(y);
+    img[pr_pos(t)] = F2(H == 0 ? y[0] : pmul(y[0], w[0]));
+#pragma unroll
+    for (int m = 1; m < 8; ++m) img[528 * m + pr_pos(t)] = F2(pmul(y[m], w[m]));
+    // pass 2: wave wv -> output parity p2 = wv & 1 of blocks 2 (wv >> 1) + (lane >> 5), n1a = lane & 31
+    const int p2 = wv & 1, n1a = lane & 31;
+    float2* base = img + 528 * (2 * (wv >> 1) + (lane >> 5)) + n1a;
+    c2 tw[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int kb = 2 * q + p2;
+        if (kb > 0) tw[q] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
+    }
+    __syncthreads();
+    c2 x[8];
+    if (p2 == 0) {
+#pragma unroll
+        for (int n = 0; n < 8; ++n) x[n] = C2(base[33 * n]) + C2(base[33 * (n + 8)]);
+    } else {
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const c2 e = C2(base[33 * n]) - C2(base[33 * (n + 8)]);
+            x[n] = n == 0 ? e : (n == 4 ? mul_mi(e) : pmul(e, w16c(n)));
+        }
+    }
+    __syncthreads();   // the other parity's wave has read the column too: write in place
+    pdft8(x);
+    if (p2 == 0) {
+        base[0] = F2(x[0]);
+#pragma unroll
+        for (int q = 1; q < 8; ++q) base[33 * 2 * q] = F2(pmul(x[q], tw[q]));
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) base[33 * (2 * q + 1)] = F2(pmul(x[q], tw[q]));
+    }
+    __syncthreads();
+    // pass 3: row (block m = wv, k'b = (t >> 2) & 15), quarter q3 = t & 3 (n1a = 8 q3 + j)
+    {
+        const int q3 = t & 3, kb3 = (t >> 2) & 15;
+        const float2* row = img + 528 * wv + 33 * kb3 + 8 * q3;
+        c2 e0 = C2(row[0]), e1 = e0;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            const c2 v = C2(row[j]);
+            e0 += v;
+            e1 = pmac(e1, v, w32(j));                // W_32^j
+        }
+        // W_32^{8 q3} = (-i)^q3
+        float rx = (q3 & 1) ? e1.y : e1.x, ry = (q3 & 1) ? -e1.x : e1.y;
+        const float sg = (q3 & 2) ? -1.f : 1.f;
+        rx *= sg;
+        ry *= sg;
+        float a0 = e0.x + qx1(e0.x), a1 = e0.y + qx1(e0.y), b0 = rx + qx1(rx), b1 = ry + qx1(ry);
+        a0 += qx2(a0);
+        a1 += qx2(a1);
+        b0 += qx2(b0);
+        b1 += qx2(b1);
+        if (q3 < 2) {
+            const int k3 = (2 * wv + H) + 16 * kb3 + 256 * q3;
+            const float xr = q3 ? b0 : a0, xi = q3 ? b1 : a1;
+            Z[z512_pos(k3)] = make_float2(xr * ph, -xi * ph);
+        }
+    }
+}
+
+template <bool POLAR>
+__global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_fe_pairs8k_h(
+    const float2* __restrict__ analytic, int n_slots, int n_pairs, int B, const int* __restrict__ slot_i,
+    const int* __restrict__ slot_j, const float* __restrict__ power, const float2* __restrict__ tab,
+    const float* __restrict__ phi0, int start, int S, float* __restrict__ out) {
+    constexpr int N = 4096;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2* img = sm;              // the staged product (4096), then one parity's blocks (PRH_IMG)
+    float2* Z = sm + PRH_BUF;      // PR_ZP
+    const int t = threadIdx.x;
+    const int item = xcd_item(blockIdx.x, n_pairs * B);
+    const int pair = item % n_pairs;
+    const int64_t b = item / n_pairs;
+    const float2* ai = analytic + (b * n_slots + slot_i[pair]) * (int64_t)N;
+    const float2* aj = analytic + (b * n_slots + slot_j[pair]) * (int64_t)N;
+    const float pw = power[pair];
+    // phi at this lane's pass-3 outputs k3 = (2 wv + H) + 16 k'b + 256 k'a, one per parity H
+    const int k3e = 2 * (t >> 6) + 16 * ((t >> 2) & 15) + 256 * (t & 1);
+    const float phe = phi0[k3e], pho = phi0[k3e + 1];
+    // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283)
+    {
+        float2 xa[8], xb[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            xa[k] = ai[t + PR_T * k];
+            xb[k] = aj[t + PR_T * k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) img[t + PR_T * k] = pair_prod<POLAR>(xa[k], xb[k], pw);
+    }
+    __syncthreads();
+    // 1: column n1 = t of the reflect-padded product, radix-2 step over n2
+    c2 s[8], d[8], w[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+        const c2 va = C2(img[prh_src(t, n)]), vb = C2(img[prh_src(t, n + 8)]);
+        s[n] = va + vb;
+        d[n] = va - vb;
+    }
+#pragma unroll
+    for (int n = 1; n < 8; ++n) d[n] = n == 4 ? mul_mi(d[n]) : pmul(d[n], w16c(n));
+#pragma unroll
+    for (int m = 1; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m - 1) + t]);   // W_8192^{t 2m}
+    __syncthreads();   // the product is consumed: the image overwrites it
+    prh_parity<0>(img, Z, s, w, tab, phe);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m) + t]);       // W_8192^{t (2m + 1)}
+    __syncthreads();   // the even blocks' pass 3 has read the image
+    prh_parity<1>(img, Z, d, w, tab, pho);
+    c2 w5[7], wb5[7];
+    if (t < 64) fft512_twiddles(tab, w5, wb5);
+    __syncthreads();
+    // 4: inverse FFT of length 512 by wave 0, keep the real part of [start, start + S)
+    if (t < 64) {
+        c2 r[8];
+        wave_fft512(Z, w5, wb5, r);
+        float* o = out + (b * n_pairs + pair) * (int64_t)S;
+        const float inv = 1.0f / (float)PR_NB;
+        const int k0 = (t >> 3) + 8 * (t & 7);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int m = k0 + 64 * j - start;
+            if (m >= 0 && m < S) o[m] = r[j].x * inv;
+        }
+    }
+}
+
 // ------------------------------------------- wavelets, 8192-point register FFT
 // Inverse FFT of xhat * psi for the training geometry (n_pad = 8192) as the
 // forward 16 x 16 x 32 decomposition of the pair kernel on conj(input)
@@ -1091,6 +1267,23 @@ int vt_fe_set_pairs_persist(int grid) {
     return prev;
 }
 
+// half-image pair kernel (k_fe_pairs8k_h, three workgroups per CU) on the training geometry:
+// VAETEB_PAIRS_HALF=0 selects the full-image k_fe_pairs8k (the form of rounds 2-5)
+static int g_pairs_half = -1;
+static int pairs_half() {
+    if (g_pairs_half < 0) {
+        const char* e = getenv("VAETEB_PAIRS_HALF");
+        g_pairs_half = !(e != nullptr && e[0] == '0');
+    }
+    return g_pairs_half;
+}
+
+int vt_fe_set_pairs_half(int on) {
+    const int prev = pairs_half();
+    g_pairs_half = on ? 1 : 0;
+    return prev;
+}
+
 int vt_fe_set_pairs_direct(int on) {
     const int prev = pairs_direct();
     g_pairs_direct = on ? 1 : 0;
@@ -1136,6 +1329,13 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
                                (PR_IMG + PR_ZP) * sizeof(float2),
                                S(stream), (const float2*)analytic, n_slots, n_pairs, (int)B, slot_i, slot_j, power, tab,
                                phi0, start, S_out, out);
+            VT_LAUNCH_CHECK("vt_fe_pairs");
+            return VT_OK;
+        }
+        if (geo && !direct && g_pairs_stamps == nullptr && pairs_half()) {
+            hipLaunchKernelGGL(pol ? k_fe_pairs8k_h<true> : k_fe_pairs8k_h<false>, dim3((unsigned)total), dim3(PR_T),
+                               PRH_LDS, S(stream), (const float2*)analytic, n_slots, n_pairs, (int)B, slot_i, slot_j,
+                               power, tab, phi0, start, S_out, out);
             VT_LAUNCH_CHECK("vt_fe_pairs");
             return VT_OK;
         }

@@ -475,6 +475,16 @@ class MlpSpec:
             self.__dict__.setdefault("_handles", {})[key] = h = hv.value
         return h
 
+    def grad_pointers(self, ts):
+        """Pointer array of the gradient destinations, reused while they stay put
+        (the trainer's in-place gradient sinks)."""
+        key = tuple(0 if t is None else t.data_ptr() for t in ts)
+        if key != self._grad_key:
+            import ctypes
+            self._grad_key = key
+            self._grad_ptrs = (ctypes.c_void_p * len(ts))(*[k or None for k in key])
+        return self._grad_ptrs
+
 
 # plans whose 16-bit weight images the model's batched pass (mlp_prep_batch) prepared for the coming
 # forward: each such forward skips its own image pass once (vt_resmlp_bf16_fwd_prepped)
@@ -494,16 +504,6 @@ def mlp_prep_batch(stacks, rows):
         chunk = hs[i:i + 32]
         call("vt_resmlp_bf16_prep_batch", len(chunk), (ctypes.c_int64 * len(chunk))(*chunk), _st())
     _MLP_PREPPED.update(hs)
-
-    def grad_pointers(self, ts):
-        """Pointer array of the gradient destinations, reused while they stay put
-        (the trainer's in-place gradient sinks)."""
-        key = tuple(0 if t is None else t.data_ptr() for t in ts)
-        if key != self._grad_key:
-            import ctypes
-            self._grad_key = key
-            self._grad_ptrs = (ctypes.c_void_p * len(ts))(*[k or None for k in key])
-        return self._grad_ptrs
 
 
 class ResMLPF(torch.autograd.Function):
