@@ -354,6 +354,44 @@ def _oracle_step(feats, eps, widths, dtype=torch.float64, S=256):
     return fw, L, grads, ref.state_dict()
 
 
+def _relu_kinks(feats, eps, widths, factor=10.0, S=256):
+    """ReLU inputs of the oracle's training forward on these features that sit within `factor` x
+    the fp32-vs-fp64 distance of the kink: |x64| <= factor |x32 - x64| (x32 != x64).  At such a unit
+    the derivative's 0 / 1 is decided by fp32 rounding — the fp32 oracle and any other fp32 step
+    (ours) may take different sides — and one flipped unit moves its layer's weight gradient by
+    ~1 / (B S) of its norm.  Returns (count, smallest |x64| / |x32 - x64|)."""
+    import torch.nn.functional as Fn
+    from golden_util import det_fill_
+    from oracle import model_ref as M
+    rec = {}
+    orig = Fn.relu
+    for dt in (torch.float64, torch.float32):
+        rec[dt] = []
+
+        def relu(x, inplace=False, _r=rec[dt]):
+            _r.append(x.detach().double().clone())
+            return orig(x, inplace=inplace)
+        ref = det_fill_(M.SeqVaeTebRef(S, *widths)).to(dt)
+        ref.train()
+        T = lambda a: torch.from_numpy(np.asarray(a)).to(dt)
+        Fn.relu = relu
+        try:
+            with torch.no_grad():
+                ref(T(feats["fhr_st"]), T(feats["fhr_ph"]), T(feats["fhr_up_ph"]), T(eps))
+        finally:
+            Fn.relu = orig
+    n, worst = 0, float("inf")
+    for a, b in zip(rec[torch.float64], rec[torch.float32]):
+        d = (b - a).abs()
+        m = d > 0
+        if not m.any():
+            continue
+        ratio = a.abs()[m] / d[m]
+        n += int((ratio <= factor).sum())
+        worst = min(worst, ratio.min().item())
+    return n, worst
+
+
 def test_j6_config2_step_end_to_end_vs_oracle():
     """BASELINE config 2's literal variant: raw windows -> FrontEnd(J=6, Q=1, T=16) ->
     SeqVaeTeb(widths 8 / 13 / 7) train step, vs the oracle on the same windows."""
@@ -390,12 +428,33 @@ def test_j6_config2_step_end_to_end_vs_oracle():
     L = tr.step({"x": torch.from_numpy(x).cuda()}, eps=torch.from_numpy(eps).cuda())
     torch.cuda.synchronize()
     fw_o, L_o, g_o, sd_o = _oracle_step(feats, eps, widths)
-    _, _, g_o32, sd_o32 = _oracle_step(feats, eps, widths, torch.float32)   # the oracle's own fp32 error
+    # the oracle's own fp32 reproducibility: the plain fp32 step and ENS steps from one-ulp perturbed
+    # initial weights (golden_util.perturb_ulp_, as the bench-batch test).  Round 6 finding
+    # (tools/j6_step_diag.py): at this window one ReLU unit of the target encoder's mu_layer sits
+    # within fp32 rounding of its kink — the fp32 steps that flip it (our step on the half-image pair
+    # kernel's features; the oracle's member 3; our own one-ulp members) move mu_layer's weight
+    # gradients by up to 1.1e-2 while the fp64 step moves by 3e-6 for the same feature change, and
+    # our flipped step equals that oracle member gradient for gradient.  So each gradient is held to
+    # the ensemble's largest distance, as at B = 256, not to the one plain fp32 run.
+    from golden_util import det_fill_, perturb_ulp_
+    from oracle import model_ref as M
+
+    def member(seed):
+        ref = det_fill_(M.SeqVaeTebRef(256, *widths))
+        if seed:
+            perturb_ulp_(ref, seed)
+        Tf = lambda a: torch.from_numpy(np.asarray(a)).float()
+        _, _, g, _ = M.train_step(ref, {"y_st": Tf(feats["fhr_st"]), "y_ph": Tf(feats["fhr_ph"]),
+                                        "x_ph": Tf(feats["fhr_up_ph"]), "y_raw": Tf(feats["fhr"])}, Tf(eps), 1e-5)
+        return g, ref.state_dict()
+    ENS = 4
+    members = [member(s) for s in range(ENS + 1)]          # seed 0: the plain fp32 oracle step
+    g_o32, sd_o32 = members[0]
     # precondition: the oracle is well-conditioned at these features (a 1e-6 relative
     # perturbation, below fp32 rounding, moves its fp64 gradients by far less than the bounds)
     prng = np.random.default_rng(4244)
-    _, _, g_p, _ = _oracle_step({k: v * (1 + 1e-6 * prng.standard_normal(v.shape)) for k, v in feats.items()},
-                                eps, widths)
+    _, _, g_p, sd_p = _oracle_step({k: v * (1 + 1e-6 * prng.standard_normal(v.shape)) for k, v in feats.items()},
+                                   eps, widths)
     sens = np.median([rel(g_p[k], gr) for k, gr in g_o.items() if gr.norm() > 0])
     assert sens <= 5e-5, f"oracle ill-conditioned at this window (perturbed median rel {sens:.2e})"
     assert L["mse_loss"].item() == 0.0       # 8 + 13 != 87: the reference's MSE branch is off
@@ -403,36 +462,43 @@ def test_j6_config2_step_end_to_end_vs_oracle():
         exp = L_o[k].item()
         assert abs(L[k].item() - exp) <= 1e-5 * abs(exp) + 1e-7, (k, L[k].item(), exp)
     params = dict(m.named_parameters())
+    env = {k: max(rel(g[k], gr) for g, _ in members) for k, gr in g_o.items() if gr.norm() > 0}
     worst, ratios = [], []
     for k, gr in g_o.items():
         if gr.norm() == 0:      # decoder.linear: no MSE term, no gradient
-            worst.append((params[k].grad.abs().max().item() * 1e30, k))
+            worst.append((params[k].grad.abs().max().item() * 1e30, k, 0.0, 0.0, 0.0))
             continue
-        e_ours, e_ref = rel(params[k].grad, gr), rel(g_o32[k], gr)
-        ratios.append(e_ours / max(e_ref, 1e-12))
-        worst.append((e_ours / (2e-5 + 10 * e_ref), k))
-    # fixed bounds from the errors measured here (round 4: median 6.8e-6, p90 1.0e-5 over the
-    # gradients the oracle's own fp32 run gets within 1e-3 of fp64): the per-parameter bound
-    # above is relative to the oracle's fp32 error, which is large for the chaotic ones, so
-    # these aggregates are what a regression of the HIP gradients would fail
-    errs = np.array([rel(params[k].grad, gr) for k, gr in g_o.items()
-                     if gr.norm() > 0 and rel(g_o32[k], gr) < 1e-3])
-    print(f"J6 grads vs fp64 oracle: median ours/oracle-fp32 error ratio {np.median(ratios):.2f}, "
+        e_ours = rel(params[k].grad, gr)
+        ratios.append(e_ours / max(env[k], 1e-12))
+        # + the gradient's own conditioning at these features: how far the fp64 oracle's gradient
+        # moves for the 1e-6 feature perturbation above (a fp32 front-end's rounding is that size)
+        e_pert = rel(g_p[k], gr)
+        worst.append((e_ours / (2e-5 + 10 * env[k] + 2 * e_pert), k, e_ours, env[k], e_pert))
+    # fixed bounds from the errors measured here (round 4: median 6.8e-6, p90 1.0e-5) over the
+    # gradients every ensemble member gets within 1e-3 of fp64: the per-parameter bound above is
+    # relative to the ensemble, which is large for the chaotic ones, so these aggregates are what a
+    # regression of the HIP gradients would fail
+    errs = np.array([rel(params[k].grad, g_o[k]) for k in env if env[k] < 1e-3])
+    print(f"J6 grads vs fp64 oracle: median ours/ensemble error ratio {np.median(ratios):.2f}, "
           f"worst {max(worst)}; ours rel-L2 over {len(errs)} well-conditioned gradients: median "
           f"{np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} max {errs.max():.3e}")
     assert len(errs) >= 100 and np.median(errs) <= 2e-5 and np.percentile(errs, 90) <= 5e-5, errs
     assert np.median(ratios) <= 2.0, np.median(ratios)
     worst = max(worst)
     assert worst[0] <= 1.0, worst
-    # after clip + AdamW: within 10x the oracle's own fp32-vs-fp64 distance (+1e-6), as the
+    # after clip + AdamW: within 10x the ensemble's largest fp32-vs-fp64 distance (+1e-6), as the
     # gradients (AdamW carries a gradient's error into the step: the conditional encoder's
-    # logvar-head LayerNorm weight measured 4.8x).  With the MSE
-    # term off, decoder.linear's biases feed only BatchNorm-normalised channels: their exact
-    # gradient is 0 and an fp32 step gives rounding noise, which AdamW scales to lr-sized
-    # steps — the reference's fp32 step does the same, so only that bound is meaningful there
+    # logvar-head LayerNorm weight measured 4.8x), + twice the parameter's own conditioning (the
+    # 1e-6 feature perturbation of the fp64 step: a bias whose gradient entries sit near AdamW's eps
+    # moves by ~lr).  With the MSE term off, decoder.linear's biases feed only BatchNorm-normalised
+    # channels: their exact gradient is 0 and an fp32 step gives rounding noise, which AdamW scales
+    # to lr-sized steps — the reference's fp32 step does the same, so only that bound is
+    # meaningful there
     sd = m.state_dict()
-    worst = max((rel(sd[k], v) / (1e-6 + 10 * rel(sd_o32[k], v)), k) for k, v in sd_o.items()
+    worst = max((rel(sd[k], v) / (1e-6 + 10 * max(rel(sm[k], v) for _, sm in members) + 2 * rel(sd_p[k], v)), k,
+                 rel(sd[k], v), rel(sd_o32[k], v), rel(sd_p[k], v)) for k, v in sd_o.items()
                 if v.dtype == torch.float64 and v.norm() > 0)
+    print(f"J6 parameters after clip + AdamW: worst {worst}")
     assert worst[0] <= 1.0, worst
 
     # end to end: the oracle step on its own fp64 features; the spread the reference's own

@@ -644,11 +644,21 @@ __device__ __forceinline__ int prh_src(int t, int n2) {
 // X[k2 + 16 k'b + 256 k'a] (k'a < 2) in Z (conj(X phi), as k_fe_pairs8k); w[m] = W_8192^{t k2}
 // (w[0] unused for H = 0).  Enters with img free, leaves with pass 3's reads of img possibly
 // still in flight in other waves (the caller's barrier).
-template <int H>
+// P3: pass-3 form (1: one lane per row on waves 0-1, the default; 0: four lanes per row)
+template <int H, int OCC, int P3>
 __device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], const c2 (&w)[8],
-                                           const float2* __restrict__ tab, float ph) {
+                                           const float2* __restrict__ tab, const float* __restrict__ phi0) {
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    // phi at this lane's pass-3 outputs (loaded ahead, consumed after two barriers)
+    float ph, ph1 = 0.f;
+    if constexpr (P3 == 1) {
+        const int k3 = (2 * (t >> 4) + H) + 16 * (t & 15);
+        ph = t < 128 ? phi0[k3] : 0.f;
+        ph1 = t < 128 ? phi0[k3 + 256] : 0.f;
+    } else {
+        ph = phi0[(2 * (t >> 6) + H) + 16 * ((t >> 2) & 15) + 256 * (t & 1)];
+    }
     pdft8(y);
     img[pr_pos(t)] = F2(H == 0 ? y[0] : pmul(y[0], w[0]));
 #pragma unroll
@@ -657,12 +667,16 @@ __device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], c
     const int p2 = wv & 1, n1a = lane & 31;
     float2* base = img + 528 * (2 * (wv >> 1) + (lane >> 5)) + n1a;
     c2 tw[8];
+    auto load_tw = [&]() {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int kb = 2 * q + p2;
-        if (kb > 0) tw[q] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
-    }
+        for (int q = 0; q < 8; ++q) {
+            const int kb = 2 * q + p2;
+            if (kb > 0) tw[q] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
+        }
+    };
+    if constexpr (OCC == 6) load_tw();   // in flight across the barrier (at 8 waves / SIMD: after it, registers)
     __syncthreads();
+    if constexpr (OCC != 6) load_tw();
     c2 x[8];
     if (p2 == 0) {
 #pragma unroll
@@ -685,8 +699,28 @@ __device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], c
         for (int q = 0; q < 8; ++q) base[33 * (2 * q + 1)] = F2(pmul(x[q], tw[q]));
     }
     __syncthreads();
-    // pass 3: row (block m = wv, k'b = (t >> 2) & 15), quarter q3 = t & 3 (n1a = 8 q3 + j)
-    {
+    if constexpr (P3 == 1) {
+        // pass 3: one lane per row (block m = t >> 4, k'b = t & 15), waves 0-1 only (the kernel is
+        // issue bound: idle waves cost nothing, a row's work split over lanes costs the combine).
+        // The two outputs of the 32-point DFT over n1a by two radix-2 folds:
+        //   X0 = sum_n x_n,  X1 = sum_{n<8} ((x_n - x_{n+16}) - i (x_{n+8} - x_{n+24})) W_32^n
+        if (t < 128) {
+            const int m3 = t >> 4, kb3 = t & 15;
+            const float2* row = img + 528 * m3 + 33 * kb3;
+            c2 x0 = c2{0.f, 0.f}, x1 = c2{0.f, 0.f};
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const c2 a = C2(row[n]), b = C2(row[n + 8]), c = C2(row[n + 16]), e = C2(row[n + 24]);
+                x0 += (a + c) + (b + e);
+                const c2 f = add_mi(a - c, b - e);
+                x1 = n == 0 ? f : pmac(x1, f, w32(n));
+            }
+            const int k3 = (2 * m3 + H) + 16 * kb3;
+            Z[z512_pos(k3)] = make_float2(x0.x * ph, -x0.y * ph);
+            Z[z512_pos(k3 + 256)] = make_float2(x1.x * ph1, -x1.y * ph1);
+        }
+    } else {
+        // pass 3: row (block m = wv, k'b = (t >> 2) & 15), quarter q3 = t & 3 (n1a = 8 q3 + j)
         const int q3 = t & 3, kb3 = (t >> 2) & 15;
         const float2* row = img + 528 * wv + 33 * kb3 + 8 * q3;
         c2 e0 = C2(row[0]), e1 = e0;
@@ -714,8 +748,9 @@ __device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], c
     }
 }
 
-template <bool POLAR>
-__global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_fe_pairs8k_h(
+// OCC: waves per SIMD the registers are fitted to (6: three workgroups per CU, 80 VGPRs; 8: four, 64)
+template <bool POLAR, int OCC, int P3 = 1>
+__global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void k_fe_pairs8k_h(
     const float2* __restrict__ analytic, int n_slots, int n_pairs, int B, const int* __restrict__ slot_i,
     const int* __restrict__ slot_j, const float* __restrict__ power, const float2* __restrict__ tab,
     const float* __restrict__ phi0, int start, int S, float* __restrict__ out) {
@@ -730,19 +765,18 @@ __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(6, 6))) vo
     const float2* ai = analytic + (b * n_slots + slot_i[pair]) * (int64_t)N;
     const float2* aj = analytic + (b * n_slots + slot_j[pair]) * (int64_t)N;
     const float pw = power[pair];
-    // phi at this lane's pass-3 outputs k3 = (2 wv + H) + 16 k'b + 256 k'a, one per parity H
-    const int k3e = 2 * (t >> 6) + 16 * ((t >> 2) & 15) + 256 * (t & 1);
-    const float phe = phi0[k3e], pho = phi0[k3e + 1];
     // 0: accelerated product c[u], u < N (kymatio_phase_scattering.py:211-218, :282-283)
-    {
-        float2 xa[8], xb[8];
+    constexpr int LB = OCC == 6 ? 8 : 4;   // loads in flight per batch
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            xa[k] = ai[t + PR_T * k];
-            xb[k] = aj[t + PR_T * k];
+    for (int k0 = 0; k0 < 8; k0 += LB) {
+        float2 xa[LB], xb[LB];
+#pragma unroll
+        for (int k = 0; k < LB; ++k) {
+            xa[k] = ai[t + PR_T * (k0 + k)];
+            xb[k] = aj[t + PR_T * (k0 + k)];
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) img[t + PR_T * k] = pair_prod<POLAR>(xa[k], xb[k], pw);
+        for (int k = 0; k < LB; ++k) img[t + PR_T * (k0 + k)] = pair_prod<POLAR>(xa[k], xb[k], pw);
     }
     __syncthreads();
     // 1: column n1 = t of the reflect-padded product, radix-2 step over n2
@@ -758,11 +792,17 @@ __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(6, 6))) vo
 #pragma unroll
     for (int m = 1; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m - 1) + t]);   // W_8192^{t 2m}
     __syncthreads();   // the product is consumed: the image overwrites it
-    prh_parity<0>(img, Z, s, w, tab, phe);
+    prh_parity<0, OCC, P3>(img, Z, s, w, tab, phi0);
+    if constexpr (OCC == 6) {
 #pragma unroll
-    for (int m = 0; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m) + t]);       // W_8192^{t (2m + 1)}
+        for (int m = 0; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m) + t]);   // W_8192^{t (2m + 1)}
+    }
     __syncthreads();   // the even blocks' pass 3 has read the image
-    prh_parity<1>(img, Z, d, w, tab, pho);
+    if constexpr (OCC != 6) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m) + t]);
+    }
+    prh_parity<1, OCC, P3>(img, Z, d, w, tab, phi0);
     c2 w5[7], wb5[7];
     if (t < 64) fft512_twiddles(tab, w5, wb5);
     __syncthreads();
@@ -1273,14 +1313,14 @@ static int g_pairs_half = -1;
 static int pairs_half() {
     if (g_pairs_half < 0) {
         const char* e = getenv("VAETEB_PAIRS_HALF");
-        g_pairs_half = !(e != nullptr && e[0] == '0');
+        g_pairs_half = e != nullptr ? atoi(e) : 1;
     }
     return g_pairs_half;
 }
 
 int vt_fe_set_pairs_half(int on) {
     const int prev = pairs_half();
-    g_pairs_half = on ? 1 : 0;
+    g_pairs_half = on < 0 ? 0 : on;   // 2: the 64-VGPR form (four workgroups per CU)
     return prev;
 }
 
@@ -1333,7 +1373,12 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
             return VT_OK;
         }
         if (geo && !direct && g_pairs_stamps == nullptr && pairs_half()) {
-            hipLaunchKernelGGL(pol ? k_fe_pairs8k_h<true> : k_fe_pairs8k_h<false>, dim3((unsigned)total), dim3(PR_T),
+            const int hf = pairs_half();   // 1: 3 workgroups / CU; 2: 4; 3: 3 with the four-lane pass 3
+            hipLaunchKernelGGL(pol ? (hf == 2 ? k_fe_pairs8k_h<true, 8> : hf == 3 ? k_fe_pairs8k_h<true, 6, 0>
+                                                                      : k_fe_pairs8k_h<true, 6>)
+                                   : (hf == 2 ? k_fe_pairs8k_h<false, 8> : hf == 3 ? k_fe_pairs8k_h<false, 6, 0>
+                                                                       : k_fe_pairs8k_h<false, 6>),
+                               dim3((unsigned)total), dim3(PR_T),
                                PRH_LDS, S(stream), (const float2*)analytic, n_slots, n_pairs, (int)B, slot_i, slot_j,
                                power, tab, phi0, start, S_out, out);
             VT_LAUNCH_CHECK("vt_fe_pairs");
