@@ -475,10 +475,11 @@ def test_j6_config2_step_end_to_end_vs_oracle():
         e_pert = rel(g_p[k], gr)
         worst.append((e_ours / (2e-5 + 10 * env[k] + 2 * e_pert), k, e_ours, env[k], e_pert))
     # fixed bounds from the errors measured here (round 4: median 6.8e-6, p90 1.0e-5) over the
-    # gradients every ensemble member gets within 1e-3 of fp64: the per-parameter bound above is
-    # relative to the ensemble, which is large for the chaotic ones, so these aggregates are what a
-    # regression of the HIP gradients would fail
-    errs = np.array([rel(params[k].grad, g_o[k]) for k in env if env[k] < 1e-3])
+    # gradients every ensemble member gets within 1e-4 of fp64 (a clean fp32 gradient lands ~1e-5
+    # away; a member that flips the kink unit moves the gradients upstream of it by 1e-4 .. 1e-2):
+    # the per-parameter bound above is relative to the ensemble, which is large for the chaotic
+    # ones, so these aggregates are what a regression of the HIP gradients would fail
+    errs = np.array([rel(params[k].grad, g_o[k]) for k in env if env[k] < 1e-4])
     print(f"J6 grads vs fp64 oracle: median ours/ensemble error ratio {np.median(ratios):.2f}, "
           f"worst {max(worst)}; ours rel-L2 over {len(errs)} well-conditioned gradients: median "
           f"{np.median(errs):.3e} p90 {np.percentile(errs, 90):.3e} max {errs.max():.3e}")

@@ -644,7 +644,9 @@ __device__ __forceinline__ int prh_src(int t, int n2) {
 // X[k2 + 16 k'b + 256 k'a] (k'a < 2) in Z (conj(X phi), as k_fe_pairs8k); w[m] = W_8192^{t k2}
 // (w[0] unused for H = 0).  Enters with img free, leaves with pass 3's reads of img possibly
 // still in flight in other waves (the caller's barrier).
-// P3: pass-3 form (1: one lane per row on waves 0-1, the default; 0: four lanes per row)
+// P3: pass-3 form (1: one lane per row on waves 0-1, the default; 0: four lanes per row).  Measured
+// and dropped: pass 2 as one thread per radix-16 job on waves 0-3 (no pair split, no middle barrier,
+// fewer VALU): 0.78 vs 0.67 ms per launch in the step — four waves cannot hide its 16 LDS reads.
 template <int H, int OCC, int P3>
 __device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], const c2 (&w)[8],
                                            const float2* __restrict__ tab, const float* __restrict__ phi0) {
@@ -663,40 +665,42 @@ __device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], c
     img[pr_pos(t)] = F2(H == 0 ? y[0] : pmul(y[0], w[0]));
 #pragma unroll
     for (int m = 1; m < 8; ++m) img[528 * m + pr_pos(t)] = F2(pmul(y[m], w[m]));
-    // pass 2: wave wv -> output parity p2 = wv & 1 of blocks 2 (wv >> 1) + (lane >> 5), n1a = lane & 31
-    const int p2 = wv & 1, n1a = lane & 31;
-    float2* base = img + 528 * (2 * (wv >> 1) + (lane >> 5)) + n1a;
-    c2 tw[8];
-    auto load_tw = [&]() {
+    {
+        // pass 2: wave wv -> output parity p2 = wv & 1 of blocks 2 (wv >> 1) + (lane >> 5), n1a = lane & 31
+        const int p2 = wv & 1, n1a = lane & 31;
+        float2* base = img + 528 * (2 * (wv >> 1) + (lane >> 5)) + n1a;
+        c2 tw[8];
+        auto load_tw = [&]() {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int kb = 2 * q + p2;
-            if (kb > 0) tw[q] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
+            for (int q = 0; q < 8; ++q) {
+                const int kb = 2 * q + p2;
+                if (kb > 0) tw[q] = C2(tab[TW8K_T2 + 32 * (kb - 1) + n1a]);
+            }
+        };
+        if constexpr (OCC == 6) load_tw();   // in flight across the barrier (at 8 waves / SIMD: after it, registers)
+        __syncthreads();
+        if constexpr (OCC != 6) load_tw();
+        c2 x[8];
+        if (p2 == 0) {
+#pragma unroll
+            for (int n = 0; n < 8; ++n) x[n] = C2(base[33 * n]) + C2(base[33 * (n + 8)]);
+        } else {
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const c2 e = C2(base[33 * n]) - C2(base[33 * (n + 8)]);
+                x[n] = n == 0 ? e : (n == 4 ? mul_mi(e) : pmul(e, w16c(n)));
+            }
         }
-    };
-    if constexpr (OCC == 6) load_tw();   // in flight across the barrier (at 8 waves / SIMD: after it, registers)
-    __syncthreads();
-    if constexpr (OCC != 6) load_tw();
-    c2 x[8];
-    if (p2 == 0) {
+        __syncthreads();   // the other parity's wave has read the column too: write in place
+        pdft8(x);
+        if (p2 == 0) {
+            base[0] = F2(x[0]);
 #pragma unroll
-        for (int n = 0; n < 8; ++n) x[n] = C2(base[33 * n]) + C2(base[33 * (n + 8)]);
-    } else {
+            for (int q = 1; q < 8; ++q) base[33 * 2 * q] = F2(pmul(x[q], tw[q]));
+        } else {
 #pragma unroll
-        for (int n = 0; n < 8; ++n) {
-            const c2 e = C2(base[33 * n]) - C2(base[33 * (n + 8)]);
-            x[n] = n == 0 ? e : (n == 4 ? mul_mi(e) : pmul(e, w16c(n)));
+            for (int q = 0; q < 8; ++q) base[33 * (2 * q + 1)] = F2(pmul(x[q], tw[q]));
         }
-    }
-    __syncthreads();   // the other parity's wave has read the column too: write in place
-    pdft8(x);
-    if (p2 == 0) {
-        base[0] = F2(x[0]);
-#pragma unroll
-        for (int q = 1; q < 8; ++q) base[33 * 2 * q] = F2(pmul(x[q], tw[q]));
-    } else {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) base[33 * (2 * q + 1)] = F2(pmul(x[q], tw[q]));
     }
     __syncthreads();
     if constexpr (P3 == 1) {
@@ -1373,11 +1377,14 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
             return VT_OK;
         }
         if (geo && !direct && g_pairs_stamps == nullptr && pairs_half()) {
-            const int hf = pairs_half();   // 1: 3 workgroups / CU; 2: 4; 3: 3 with the four-lane pass 3
-            hipLaunchKernelGGL(pol ? (hf == 2 ? k_fe_pairs8k_h<true, 8> : hf == 3 ? k_fe_pairs8k_h<true, 6, 0>
-                                                                      : k_fe_pairs8k_h<true, 6>)
-                                   : (hf == 2 ? k_fe_pairs8k_h<false, 8> : hf == 3 ? k_fe_pairs8k_h<false, 6, 0>
-                                                                       : k_fe_pairs8k_h<false, 6>),
+            // 1: 3 workgroups / CU; 2: 4 (64 VGPRs, spills: slower); 3: 3 with the four-lane pass 3
+            const int hf = pairs_half();
+            hipLaunchKernelGGL(pol ? (hf == 2   ? k_fe_pairs8k_h<true, 8>
+                                      : hf == 3 ? k_fe_pairs8k_h<true, 6, 0>
+                                                : k_fe_pairs8k_h<true, 6>)
+                                   : (hf == 2   ? k_fe_pairs8k_h<false, 8>
+                                      : hf == 3 ? k_fe_pairs8k_h<false, 6, 0>
+                                                : k_fe_pairs8k_h<false, 6>),
                                dim3((unsigned)total), dim3(PR_T),
                                PRH_LDS, S(stream), (const float2*)analytic, n_slots, n_pairs, (int)B, slot_i, slot_j,
                                power, tab, phi0, start, S_out, out);
