@@ -640,15 +640,16 @@ __device__ __forceinline__ int prh_src(int t, int n2) {
     return n2 < 4 ? -i : (n2 < 12 ? i : 2 * 4096 - 2 - i);
 }
 
-// blocks k2 = 2m + H (m < 8) from y (pass 1's DFT-8 input of that parity) to their 512 outputs
-// X[k2 + 16 k'b + 256 k'a] (k'a < 2) in Z (conj(X phi), as k_fe_pairs8k); w[m] = W_8192^{t k2}
-// (w[0] unused for H = 0).  Enters with img free, leaves with pass 3's reads of img possibly
-// still in flight in other waves (the caller's barrier).
+// blocks k2 = 2m + H (m < 8) from y (pass 1's output of that parity: the DFT-8 and the twiddles
+// W_8192^{t k2} already applied in registers, ahead of the barrier that frees the image) to their
+// 512 outputs X[k2 + 16 k'b + 256 k'a] (k'a < 2) in Z (conj(X phi), as k_fe_pairs8k).  Enters
+// with img free, leaves with pass 3's reads of img possibly still in flight in waves 0-1 (the
+// caller's barrier).
 // P3: pass-3 form (1: one lane per row on waves 0-1, the default; 0: four lanes per row).  Measured
 // and dropped: pass 2 as one thread per radix-16 job on waves 0-3 (no pair split, no middle barrier,
 // fewer VALU): 0.78 vs 0.67 ms per launch in the step — four waves cannot hide its 16 LDS reads.
 template <int H, int OCC, int P3>
-__device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], const c2 (&w)[8],
+__device__ __forceinline__ void prh_parity(float2* img, float2* Z, const c2 (&y)[8],
                                            const float2* __restrict__ tab, const float* __restrict__ phi0) {
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -661,10 +662,8 @@ __device__ __forceinline__ void prh_parity(float2* img, float2* Z, c2 (&y)[8], c
     } else {
         ph = phi0[(2 * (t >> 6) + H) + 16 * ((t >> 2) & 15) + 256 * (t & 1)];
     }
-    pdft8(y);
-    img[pr_pos(t)] = F2(H == 0 ? y[0] : pmul(y[0], w[0]));
 #pragma unroll
-    for (int m = 1; m < 8; ++m) img[528 * m + pr_pos(t)] = F2(pmul(y[m], w[m]));
+    for (int m = 0; m < 8; ++m) img[528 * m + pr_pos(t)] = F2(y[m]);
     {
         // pass 2: wave wv -> output parity p2 = wv & 1 of blocks 2 (wv >> 1) + (lane >> 5), n1a = lane & 31
         const int p2 = wv & 1, n1a = lane & 31;
@@ -793,20 +792,22 @@ __global__ __launch_bounds__(PR_T) __attribute__((amdgpu_waves_per_eu(OCC, OCC))
     }
 #pragma unroll
     for (int n = 1; n < 8; ++n) d[n] = n == 4 ? mul_mi(d[n]) : pmul(d[n], w16c(n));
+    // pass 1 of the even blocks in registers while other waves may still read the product
 #pragma unroll
     for (int m = 1; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m - 1) + t]);   // W_8192^{t 2m}
+    pdft8(s);
+#pragma unroll
+    for (int m = 1; m < 8; ++m) s[m] = pmul(s[m], w[m]);
     __syncthreads();   // the product is consumed: the image overwrites it
-    prh_parity<0, OCC, P3>(img, Z, s, w, tab, phi0);
-    if constexpr (OCC == 6) {
+    prh_parity<0, OCC, P3>(img, Z, s, tab, phi0);
+    // pass 1 of the odd blocks in registers: waves 2-7 run it while waves 0-1 finish pass 3
 #pragma unroll
-        for (int m = 0; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m) + t]);   // W_8192^{t (2m + 1)}
-    }
+    for (int m = 0; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m) + t]);       // W_8192^{t (2m + 1)}
+    pdft8(d);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) d[m] = pmul(d[m], w[m]);
     __syncthreads();   // the even blocks' pass 3 has read the image
-    if constexpr (OCC != 6) {
-#pragma unroll
-        for (int m = 0; m < 8; ++m) w[m] = C2(tab[TW8K_T1 + 512 * (2 * m) + t]);
-    }
-    prh_parity<1, OCC, P3>(img, Z, d, w, tab, phi0);
+    prh_parity<1, OCC, P3>(img, Z, d, tab, phi0);
     c2 w5[7], wb5[7];
     if (t < 64) fft512_twiddles(tab, w5, wb5);
     __syncthreads();
