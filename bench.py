@@ -699,7 +699,7 @@ def main():
                                "double-buffered features)" if args.overlap_update else
                                "eager, next batch's front-end overlapped with the whole step" if args.prefetch
                                else "eager"),
-        "roofline": {"bound": "hbm", "kernel": "vt_fe_pairs (k_fe_pairs8k)", "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": "vt_fe_pairs (k_fe_pairs8k_h)", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src, "avg_launch_ms": round(k_ms, 4), "launches": k_n,

@@ -118,8 +118,9 @@ int vt_fe_pairs(const void* analytic, int64_t B, int n_slots, int N, int n_pad, 
 int vt_fe_set_pairs_persist(int grid);
 int vt_fe_set_pairs_direct(int on);
 /* pair kernel form on the training geometry: 1 = half-image k_fe_pairs8k_h at three workgroups per CU
- * (default), 2 = the same at four (64 VGPRs), 0 = the full-image k_fe_pairs8k of rounds 2-5;
- * initial value from VAETEB_PAIRS_HALF; returns the previous setting */
+ * (default), 2 = the same at four (64 VGPRs), 3 = three per CU with the four-lane pass 3, 0 = the
+ * full-image k_fe_pairs8k of rounds 2-5; initial value from VAETEB_PAIRS_HALF; returns the previous
+ * setting */
 int vt_fe_set_pairs_half(int on);
 /* Storage form of the analytic slots on the 8192-point geometry (n_pad 8192,
  * pad_left + N <= 8192), shared by vt_fe_wavelet (writes) and vt_fe_pairs (reads):
