@@ -1264,7 +1264,7 @@ struct SumArgs {
 
 __global__ __launch_bounds__(256) void k_mlpb_sum(SumArgs sa, const float* __restrict__ part, int nblk, int accumulate) {
     // 64 outputs per workgroup; wave w sums partials w, w + 4, w + 8, ... in sequence
-    // (coalesced 256-byte rows, 16 loads in flight), then (w0 + w1) + (w2 + w3)
+    // (coalesced 256-byte rows, up to 64 loads in flight), then (w0 + w1) + (w2 + w3)
     __shared__ float red[4][64];
     const SumSeg& sg = sa.s[blockIdx.y];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1276,6 +1276,15 @@ __global__ __launch_bounds__(256) void k_mlpb_sum(SumArgs sa, const float* __res
     if (i < E) {
         const float* q = src + i;
         int b = w;
+        // 64 loads in flight while 64 partials remain for this wave (one batch at 256 blocks), then
+        // 16, then one at a time: the same sequence of b, so the same sums as 16 at a time
+        for (; b + 4 * 63 < nblk; b += 256) {
+            float v[64];
+#pragma unroll
+            for (int m = 0; m < 64; ++m) v[m] = q[(int64_t)(b + 4 * m) * P];
+#pragma unroll
+            for (int m = 0; m < 64; ++m) a += v[m];
+        }
         for (; b + 60 < nblk; b += 64) {
             float v[16];
 #pragma unroll
