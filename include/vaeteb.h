@@ -148,6 +148,11 @@ int vt_fe_normalize(const float* in, int64_t B, int C, int in_C, int S, const in
 int vt_fe_normalize_window(const float* in, int64_t B, int C, int in_C, int in_S, int s0, int S_len,
                            const int* kind, const float* mean, const float* stdv, float log_eps, float* out,
                            int out_C, int out_off, void* stream);
+/* dst[r][dst_col0 + c] = src[r][src_col0 + c] for c < ncols, r < rows (row strides ld_src / ld_dst
+ * floats): the encoders' last-axis concatenation and its backward split (ref/model/vae_teb_model.py
+ * torch.cat([a, b], dim=-1) before cross_modal_fusion / the conditional encoder's MLP).            */
+int vt_copy_cols(const float* src, int64_t rows, int ld_src, int src_col0, int ncols, float* dst, int ld_dst,
+                 int dst_col0, void* stream);
 /* fhr / up: (x-mean)/(std+1e-8)  (hdf5_dataset.py:78-80)                                */
 int vt_normalize_raw(const float* x, int64_t rows, int64_t row_stride, int N, float mean, float stdv, float* out,
                      void* stream);

@@ -488,7 +488,7 @@ class TargetEncoder(nn.Module):
         a, b = fork(lambda: self.scatter_fused_norm(self.conv_scattering(self.mlp_scattering(y_st))),
                     lambda: self.phase_fused_norm(self.conv_phase(self.mlp_phase(y_ph))))
         yield
-        h = self.cross_modal_fusion(torch.cat([a, b], dim=-1))
+        h = self.cross_modal_fusion(ops.cat_last([a, b]))
         yield
         h = self.lstm(h)
         yield
@@ -508,7 +508,7 @@ class ConditionalEncoder(nn.Module):
         self.fc_logvar = ResidualMLP(hd[4], hd[5:], final_activation=False, use_skip_connection=False)
 
     def forward(self, h_x, h_y):
-        h = self.mlp(torch.cat([h_x, h_y], dim=-1))
+        h = self.mlp(ops.cat_last([h_x, h_y]))
         mu, lv = fork(lambda: self.fc_mu(h), lambda: self.fc_logvar(h))
         return mu, lv
 
