@@ -153,6 +153,11 @@ int vt_fe_normalize_window(const float* in, int64_t B, int C, int in_C, int in_S
  * torch.cat([a, b], dim=-1) before cross_modal_fusion / the conditional encoder's MLP).            */
 int vt_copy_cols(const float* src, int64_t rows, int ld_src, int src_col0, int ncols, float* dst, int ld_dst,
                  int dst_col0, void* stream);
+/* torch.clamp(x, lo, hi)'s backward in one pass: gx = (lo <= x <= hi) ? g : 0 (the target encoder's logvar
+ * clamp, ref/model/vae_teb_model.py:568).                                                   */
+int vt_clamp_bwd(const float* g, const float* x, int64_t n, float lo, float hi, float* gx, void* stream);
+/* zero the ranges [starts[r], ends[r]) of base (1 <= n <= 16) in one launch                    */
+int vt_zero_ranges(float* base, int n, const int64_t* starts, const int64_t* ends, void* stream);
 /* fhr / up: (x-mean)/(std+1e-8)  (hdf5_dataset.py:78-80)                                */
 int vt_normalize_raw(const float* x, int64_t rows, int64_t row_stride, int N, float mean, float stdv, float* out,
                      void* stream);

@@ -1,3 +1,5 @@
+// Glue kernels of the step that were ATen launches on the critical chain.
+//
 // Column-range copies of row-major fp32 matrices: the concatenation along the last axis in the
 // encoders (ref/model/vae_teb_model.py: torch.cat([a, b], dim=-1) before cross_modal_fusion and the
 // conditional encoder's MLP) and its backward split.  ATen's strided copy of a column slice into a
@@ -27,6 +29,31 @@ __global__ __launch_bounds__(256) void k_copy_cols(const float* __restrict__ src
     }
 }
 
+// torch.clamp's backward (autograd: where((x >= lo) & (x <= hi), g, 0), four ATen launches): one pass
+__global__ __launch_bounds__(256) void k_clamp_bwd(const float* __restrict__ g, const float* __restrict__ x, int64_t n,
+                                                   float lo, float hi, float* __restrict__ gx) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        gx[i] = (v >= lo && v <= hi) ? g[i] : 0.f;
+    }
+}
+
+// zero up to ZR_MAX ranges [a, b) of one buffer in one launch (the gradient buffer's non-first-writer
+// ranges at the step start: one Fill launch each before)
+constexpr int ZR_MAX = 16;
+struct ZeroRanges {
+    int n;
+    int64_t a[ZR_MAX], len[ZR_MAX];
+};
+__global__ __launch_bounds__(256) void k_zero_ranges(float* __restrict__ base, ZeroRanges zr, int64_t total) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t j = i;
+        int r = 0;
+        while (r + 1 < zr.n && j >= zr.len[r]) j -= zr.len[r++];
+        base[zr.a[r] + j] = 0.f;
+    }
+}
+
 }  // namespace
 }  // namespace vt
 
@@ -48,5 +75,31 @@ extern "C" int vt_copy_cols(const float* src, int64_t rows, int ld_src, int src_
         hipLaunchKernelGGL(k_copy_cols<1>, dim3(grid), dim3(256), 0, S(stream), src, rows, ld_src, src_col0, ncols, dst,
                            ld_dst, dst_col0);
     VT_LAUNCH_CHECK("vt_copy_cols");
+    return VT_OK;
+}
+
+extern "C" int vt_clamp_bwd(const float* g, const float* x, int64_t n, float lo, float hi, float* gx, void* stream) {
+    VT_CHECK_ARG(g && x && gx && n > 0, "vt_clamp_bwd: shape");
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_clamp_bwd, dim3(grid), dim3(256), 0, S(stream), g, x, n, lo, hi, gx);
+    VT_LAUNCH_CHECK("vt_clamp_bwd");
+    return VT_OK;
+}
+
+extern "C" int vt_zero_ranges(float* base, int n, const int64_t* starts, const int64_t* ends, void* stream) {
+    VT_CHECK_ARG(base && n >= 1 && n <= ZR_MAX && starts && ends, "vt_zero_ranges: 1 <= n <= %d ranges", ZR_MAX);
+    ZeroRanges zr{};
+    zr.n = n;
+    int64_t total = 0;
+    for (int r = 0; r < n; ++r) {
+        VT_CHECK_ARG(ends[r] >= starts[r] && starts[r] >= 0, "vt_zero_ranges: range %d", r);
+        zr.a[r] = starts[r];
+        zr.len[r] = ends[r] - starts[r];
+        total += zr.len[r];
+    }
+    if (total == 0) return VT_OK;
+    const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_zero_ranges, dim3(grid), dim3(256), 0, S(stream), base, zr, total);
+    VT_LAUNCH_CHECK("vt_zero_ranges");
     return VT_OK;
 }

@@ -494,7 +494,7 @@ class TargetEncoder(nn.Module):
         yield
         h = self.pre_output(self.lstm_norm(h))
         yield
-        return self.mu_layer(h), torch.clamp(self.logvar_layer(h), -10, 10)
+        return self.mu_layer(h), ops.clamp(self.logvar_layer(h), -10, 10)
 
 
 class ConditionalEncoder(nn.Module):

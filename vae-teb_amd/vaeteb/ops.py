@@ -1282,6 +1282,33 @@ class CatLastF(torch.autograd.Function):
         return tuple(outs)
 
 
+class ClampF(torch.autograd.Function):
+    """torch.clamp(x, lo, hi) with its backward in one pass (vt_clamp_bwd: (lo <= x <= hi) ? g : 0,
+    autograd's where((x >= lo) & (x <= hi), g, 0) — four ATen launches on the critical chain); the
+    forward is ATen's clamp (NaN propagating as the reference's)."""
+
+    @staticmethod
+    def forward(ctx, x, lo, hi):
+        ctx.save_for_backward(x)
+        ctx.lo, ctx.hi = float(lo), float(hi)
+        return torch.clamp(x, lo, hi)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        g = g.contiguous()
+        gx = torch.empty_like(x)
+        call("vt_clamp_bwd", ptr(g), ptr(x), x.numel(), ctx.lo, ctx.hi, ptr(gx), _st())
+        return gx, None, None
+
+
+def clamp(x, lo, hi):
+    """The encoders' logvar clamp: ClampF on a contiguous fp32 device tensor, torch.clamp otherwise."""
+    if x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.numel() > 0 and x.requires_grad:
+        return ClampF.apply(x, lo, hi)
+    return torch.clamp(x, lo, hi)
+
+
 def cat_last(xs):
     """The last-axis concatenation of the encoders: CatLastF for fp32 device tensors of equal leading
     shape, torch.cat otherwise."""
