@@ -17,24 +17,31 @@ namespace {
 template <int V>
 __global__ __launch_bounds__(256) void k_copy_cols(const float* __restrict__ src, int64_t rows, int ld_src, int sc0,
                                                    int ncols, float* __restrict__ dst, int ld_dst, int dc0) {
-    const int per_row = ncols / V;
-    const int64_t n = rows * per_row;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = i / per_row;
+    const unsigned per_row = (unsigned)(ncols / V);
+    const unsigned n = (unsigned)(rows * per_row);   // < 2^31 (checked on the host): 32-bit index math
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const unsigned r = i / per_row;
         const int c = (int)(i - r * per_row) * V;
-        const float* s = src + r * ld_src + sc0 + c;
-        float* d = dst + r * ld_dst + dc0 + c;
+        const float* s = src + (int64_t)r * ld_src + sc0 + c;
+        float* d = dst + (int64_t)r * ld_dst + dc0 + c;
         if constexpr (V == 4) *(float4*)d = *(const float4*)s;
         else *d = *s;
     }
 }
 
 // torch.clamp's backward (autograd: where((x >= lo) & (x <= hi), g, 0), four ATen launches): one pass
+// (V = 4: float4 pieces, n a multiple of 4 and the pointers 16-B aligned)
+template <int V>
 __global__ __launch_bounds__(256) void k_clamp_bwd(const float* __restrict__ g, const float* __restrict__ x, int64_t n,
                                                    float lo, float hi, float* __restrict__ gx) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float v = x[i];
-        gx[i] = (v >= lo && v <= hi) ? g[i] : 0.f;
+    auto one = [&](float v, float gv) { return (v >= lo && v <= hi) ? gv : 0.f; };
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / V; i += (int64_t)gridDim.x * blockDim.x) {
+        if constexpr (V == 4) {
+            const float4 v = ((const float4*)x)[i], gv = ((const float4*)g)[i];
+            ((float4*)gx)[i] = make_float4(one(v.x, gv.x), one(v.y, gv.y), one(v.z, gv.z), one(v.w, gv.w));
+        } else {
+            gx[i] = one(x[i], g[i]);
+        }
     }
 }
 
@@ -67,6 +74,7 @@ extern "C" int vt_copy_cols(const float* src, int64_t rows, int ld_src, int src_
     const bool v4 = ncols % 4 == 0 && src_col0 % 4 == 0 && dst_col0 % 4 == 0 && ld_src % 4 == 0 && ld_dst % 4 == 0 &&
                     ((uintptr_t)src & 15u) == 0 && ((uintptr_t)dst & 15u) == 0;
     const int64_t n = rows * (v4 ? ncols / 4 : ncols);
+    VT_CHECK_ARG(n < (1ll << 31), "vt_copy_cols: %lld pieces (at most 2^31 - 1)", (long long)n);
     const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     if (v4)
         hipLaunchKernelGGL(k_copy_cols<4>, dim3(grid), dim3(256), 0, S(stream), src, rows, ld_src, src_col0, ncols, dst,
@@ -80,8 +88,13 @@ extern "C" int vt_copy_cols(const float* src, int64_t rows, int ld_src, int src_
 
 extern "C" int vt_clamp_bwd(const float* g, const float* x, int64_t n, float lo, float hi, float* gx, void* stream) {
     VT_CHECK_ARG(g && x && gx && n > 0, "vt_clamp_bwd: shape");
-    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_clamp_bwd, dim3(grid), dim3(256), 0, S(stream), g, x, n, lo, hi, gx);
+    const bool v4 = n % 4 == 0 && (((uintptr_t)g | (uintptr_t)x | (uintptr_t)gx) & 15u) == 0;
+    const int64_t pieces = v4 ? n / 4 : n;
+    const unsigned grid = (unsigned)std::min<int64_t>((pieces + 255) / 256, 8192);
+    if (v4)
+        hipLaunchKernelGGL(k_clamp_bwd<4>, dim3(grid), dim3(256), 0, S(stream), g, x, n, lo, hi, gx);
+    else
+        hipLaunchKernelGGL(k_clamp_bwd<1>, dim3(grid), dim3(256), 0, S(stream), g, x, n, lo, hi, gx);
     VT_LAUNCH_CHECK("vt_clamp_bwd");
     return VT_OK;
 }
