@@ -535,7 +535,7 @@ def main():
             if args.native and fe_in_graph:
                 # this step's windows into the graph's static input, its noise, the replay
                 # (front-end + model step)
-                torch.randn(caps[0].static_eps.shape, out=caps[0].static_eps)
+                caps[0].static_eps.normal_()   # in place: no temporary + copy (randn(out=) made one)
                 if args.overlap_adam:
                     _lib.wait_for(torch.cuda.current_stream(), adam_side)
                     return caps[0].replay({"x": pool[i % 2]}, adam_stream=adam_side)
@@ -544,7 +544,7 @@ def main():
                 # the step's own front-end first, on the same stream (as the eager step), then
                 # this step's noise (drawn outside the graph) and the replay
                 fe(pool[i % 2], out=caps[0].static_in)
-                torch.randn(caps[0].static_eps.shape, out=caps[0].static_eps)
+                caps[0].static_eps.normal_()   # in place: no temporary + copy (randn(out=) made one)
                 if args.overlap_adam:
                     # the previous step's AdamW (side stream) ran beside this front-end: join it
                     _lib.wait_for(torch.cuda.current_stream(), adam_side)
@@ -555,7 +555,7 @@ def main():
                 step.first = False
             main.wait_event(ready[slot])
             if args.native:                         # this step's noise, drawn outside the graph
-                torch.randn(caps[slot].static_eps.shape, out=caps[slot].static_eps)
+                caps[slot].static_eps.normal_()
             out = caps[slot].replay()
             done[slot].record(main)
             if not last:
