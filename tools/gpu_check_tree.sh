@@ -1,7 +1,7 @@
 #!/bin/bash
-# the encoders' concatenation on vt_copy_cols: the GPU suite, two bench lines (ELBO must be the
-# previous tree's bit for bit), a kernel trace of the bench
-out=$GRAFT_REPO_ROOT/gpurun_out/${1:-cat}
+# A tree check: the GPU suite, two bench lines (compare their ELBO with an earlier tree's for
+# bit-identity), a kernel trace of the bench.  Usage: tools/gpu_check_tree.sh OUTDIR
+out=$GRAFT_REPO_ROOT/gpurun_out/${1:-check}
 cd $GRAFT_REPO_ROOT && mkdir -p $out || exit 1
 ( while sleep 45; do date >> $out/heartbeat; done ) & hb=$!
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 400 --timeout-method thread > $out/pytest_gpu.log 2>&1; rc=$?
