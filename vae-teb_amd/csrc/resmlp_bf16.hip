@@ -715,10 +715,14 @@ __device__ __forceinline__ void colsum(const f32x4 (&z)[NT], int C, float (&lb)[
 }
 
 // workgroup partials of the column sums, fixed-order sum over the waves:
-// LayerNorm gamma | beta (la, if ln) -> dln[0 .. 2C); bias (lb, if db) -> db[f * dbs]
+// LayerNorm gamma | beta (la, if ln) -> dln[0 .. 2C); bias (lb, if db) -> db[f * dbs].
+// flush_cols = flush_write (each wave's column sums into red), a barrier, flush_sum (the fixed-order
+// sum over the waves into the partial); k_mlpb_bwd runs flush_sum of a layer step after the NEXT
+// step's opening barrier instead of behind a barrier of its own (the same sums, one barrier less
+// per layer step; red is next written after that step's image barrier)
 template <int NT>
-__device__ __forceinline__ void flush_cols(float* red, const float (&la)[NT], const float (&lb)[NT], int C, bool ln,
-                                           float* __restrict__ dln, float* __restrict__ db, int dbs) {
+__device__ __forceinline__ void flush_write(float* red, const float (&la)[NT], const float (&lb)[NT], int C, bool ln,
+                                            bool db) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4, lr = lane & 15;
     const int nt = (C + 15) >> 4;
     float* rw = red + wv * (48 * NT);
@@ -733,7 +737,11 @@ __device__ __forceinline__ void flush_cols(float* red, const float (&la)[NT], co
         for (int t = 0; t < NT; ++t)
             if (t < nt) rw[32 * NT + t * 16 + 4 * g4 + (lr >> 2)] = lb[t];
     }
-    __syncthreads();
+}
+template <int NT>
+__device__ __forceinline__ void flush_sum(const float* red, int C, bool ln, float* __restrict__ dln,
+                                          float* __restrict__ db, int dbs) {
+    const int nt = (C + 15) >> 4;
     if (ln) {
         for (int idx = threadIdx.x; idx < nt * 32; idx += BT) {
             const int t = idx >> 5, which = (idx >> 4) & 1, f = 16 * t + (idx & 15);
@@ -751,6 +759,13 @@ __device__ __forceinline__ void flush_cols(float* red, const float (&la)[NT], co
             db[(int64_t)f * dbs] = s;
         }
     }
+}
+template <int NT>
+__device__ __forceinline__ void flush_cols(float* red, const float (&la)[NT], const float (&lb)[NT], int C, bool ln,
+                                           float* __restrict__ dln, float* __restrict__ db, int dbs) {
+    flush_write<NT>(red, la, lb, C, ln, db != nullptr);
+    __syncthreads();
+    flush_sum<NT>(red, C, ln, dln, db, dbs);
 }
 
 // dW partial of one GEMM over images of ROWS rows (row stride S) -> dst[n * K1 + k]
@@ -862,6 +877,10 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
     }
 
     const int nsteps = L + (d.skip == 2 ? 1 : 0);
+    // the previous layer step's column-sum flush, summed after this step's opening barrier
+    int fC = 0, fdbs = 0;
+    bool fln = false, fpend = false;
+    float *fdln = nullptr, *fdb = nullptr;
     for (int step = 0; step < nsteps; ++step) {
         const bool skp = step == L;
         const int l = skp ? -1 : L - 1 - step;
@@ -891,6 +910,7 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
             }
         }
         __syncthreads();                      // previous step done with the W^T / dZ / H images and red
+        if (fpend) flush_sum<NT>(red, fC, fln, fdln, fdb, fdbs);   // before this step's image barrier
         MB_STAMP(2 + 6 * step);
         if (!d.bres) {
             if (d.gimg)
@@ -973,8 +993,13 @@ __global__ __launch_bounds__(BT, 2 * OCC) void k_mlpb_bwd(const BDesc* __restric
         // dW over the block's rows -> this workgroup's partial (db: column K, from the column sums)
         dw_img<TNS, TKS, ROWS, IS, H>(zimg, himg, N, K, pb + G.wo);
         MB_STAMP(6 + 6 * step);
-        flush_cols<NT>(red, la, lb, N, ln, ln ? pb + d.l[l].lpo : nullptr, pb + G.wo + K, K + 1);
+        flush_write<NT>(red, la, lb, N, ln, true);
+        fC = N, fln = ln, fdln = ln ? pb + d.l[l].lpo : nullptr, fdb = pb + G.wo + K, fdbs = K + 1, fpend = true;
         MB_STAMP(7 + 6 * step);
+    }
+    if (fpend) {
+        __syncthreads();
+        flush_sum<NT>(red, fC, fln, fdln, fdb, fdbs);   // red is next written after the final barrier below
     }
     // identity skip: d x0 += dout
     if (d.skip == 1) {
